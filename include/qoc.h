@@ -1,0 +1,101 @@
+/*
+ * qoc.h — C ABI of the MI355X-native GRAPE propagation/gradient engine (libqoc_mi355x.so).
+ *
+ * Drop-in boundary for the piecewise-constant Schrödinger hot path of
+ * olof3/QuantumOptimalControl.jl.  Every entry point names the reference
+ * interface it replaces (file:line in the reference repository).
+ *
+ * Conventions (identical to Julia's memory layout, so a ccall shim passes
+ * arrays without conversion):
+ *   - complex matrices are column-major, interleaved (re, im) double pairs
+ *     (Julia Matrix{ComplexF64});
+ *   - controls u are column-major nu x Nt Float64 per seed (Julia Matrix{Float64}),
+ *     seeds contiguous: u[b*nu*Nt + k*nu + j] == u_b[j,k];
+ *   - dJdu uses the same layout as u;
+ *   - every entry point returns QOC_OK (0) or a negative error code; the
+ *     message is available from qoc_last_error(ctx) (ctx may be NULL);
+ *   - one caller thread per context (the reference is called from Ipopt's
+ *     single callback thread, examples/ipopt_callbacks_exp.jl:11-31).
+ * Host-side inputs are always fp64; a QOC_FP32 context converts them once.
+ */
+#ifndef QOC_MI355X_H
+#define QOC_MI355X_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QOC_OK 0
+#define QOC_ERR_ARG (-1)        /* bad argument / dimension mismatch  (src/gradient_computations.jl:84-87) */
+#define QOC_ERR_HIP (-2)        /* HIP runtime failure */
+#define QOC_ERR_STALE (-3)      /* u differs from the last propagate  (src/gradient_computations.jl:37-39) */
+#define QOC_ERR_STATE (-4)      /* call order violated (e.g. sensitivity before propagate) */
+#define QOC_ERR_UNSUPPORTED (-5)/* size outside the compiled kernel envelope */
+
+#define QOC_FP64 0
+#define QOC_FP32 1
+
+#define QOC_COST_TRACE 0     /* J = 1-|tr(X'x)|^2/n^2            (src/penalty_fcns.jl:15-24) */
+#define QOC_COST_ZCAL 1      /* z-calibrated, 4 columns           (src/penalty_fcns.jl:27-42, src/fidelities.jl:48-137) */
+#define QOC_COST_EXTERNAL 2  /* caller supplies lambda_final      (any Julia closure dJfinal_dx) */
+
+typedef struct qoc_ctx qoc_ctx;
+
+/* Workspace for B seeds sharing (A0, A_j, x0, target).
+ * Replaces setup_grape_cache (src/gradient_computations.jl:79-96): x, λ (B x (Nt+1) x N x m),
+ * propagators Uk_vec (B x Nt x N x N), dJdu and the u copy live in HBM. */
+int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, int precision);
+void qoc_destroy(qoc_ctx* ctx);
+const char* qoc_last_error(const qoc_ctx* ctx);
+void* qoc_stream(qoc_ctx* ctx);                 /* hipStream_t the engine launches on */
+int qoc_synchronize(qoc_ctx* ctx);
+
+/* Δt-prescaled generators A0Δt and A_jΔt (src/utils.jl:86-91), N x N each. */
+int qoc_set_generators(qoc_ctx* ctx, const double* A0, const double* const* Aj);
+/* x0 (N x m) shared by all seeds (per_seed = 0) or B x N x m (per_seed = 1) — propagate :14. */
+int qoc_set_x0(qoc_ctx* ctx, const double* x0, int per_seed);
+/* Terminal cost: kind QOC_COST_TRACE (X_target N x m, normalisation n),
+ * QOC_COST_ZCAL (m must be 4), QOC_COST_EXTERNAL (X_target may be NULL). */
+int qoc_set_cost(qoc_ctx* ctx, int kind, const double* X_target, double n);
+/* Guard-state penalty L = mu sum |x[P,C]|^2 (src/penalty_fcns.jl:1-11); 0-based indices; mu = 0 disables. */
+int qoc_set_state_penalty(qoc_ctx* ctx, const int* P, int np, const int* C, int nc, double mu);
+
+/* propagate (src/gradient_computations.jl:2-32) for all B seeds, host pointers.
+ * u: B x nu x Nt (see layout above).  J_out (B, may be NULL) receives the objective
+ * of examples/ipopt_callbacks_exp.jl:18, Jfinal(x[end]) + sum(L, x)
+ * (for QOC_COST_EXTERNAL only the penalty part). */
+int qoc_propagate(qoc_ctx* ctx, const double* u, double* J_out);
+/* grape_sensitivity (src/gradient_computations.jl:35-77), host pointers.
+ * Returns QOC_ERR_STALE unless u is bitwise the u of the last propagate.
+ * lambda_final (B x N x m) is required for QOC_COST_EXTERNAL and ignored otherwise. */
+int qoc_grape_sensitivity(qoc_ctx* ctx, const double* u, int dUkdp_order,
+                          const double* lambda_final, double* dJdu_out);
+
+/* Device-pointer variants (inputs already resident in HBM, asynchronous on qoc_stream). */
+int qoc_propagate_dev(qoc_ctx* ctx, const double* d_u, double* d_J);
+int qoc_grape_sensitivity_dev(qoc_ctx* ctx, const double* d_u, int dUkdp_order, double* d_dJdu);
+/* One GRAPE gradient eval = f + f_grad of examples/ipopt_callbacks_exp.jl:11-31 (no spline map). */
+int qoc_eval_dev(qoc_ctx* ctx, const double* d_u, int dUkdp_order, double* d_J, double* d_dJdu);
+
+/* Lazy readback of cache fields (test/test_gradient_computation.jl:84,86 read cache.x / cache.λ). */
+int qoc_get_states(qoc_ctx* ctx, int seed, int k, double* x_out);       /* k in [0,Nt], -1 = final */
+int qoc_get_costates(qoc_ctx* ctx, int seed, int k, double* lam_out);
+int qoc_get_propagator(qoc_ctx* ctx, int seed, int k, double* U_out);   /* Uk_vec[k+1], k in [0,Nt) */
+/* Histogram of selected (Padé degree, squarings) since the last reset:
+ * hist[di*64 + s], di = index of degree in {3,5,7,9,13}.  Used for the FLOP accounting. */
+int qoc_pade_histogram(qoc_ctx* ctx, long long* hist, int reset);
+
+/* Standalone ops on the same kernels. */
+/* exponential!(A, ExpMethodHigham2005()) for `count` independent N x N matrices
+ * (src/gradient_computations.jl:24, third-party ExponentialUtilities). */
+int qoc_expm_batched(int device, int N, int count, int precision, const double* A, double* X,
+                     int* degree_out, int* squarings_out);
+/* expm_jacobian! (src/gradient_computations.jl:177-213): dFdp_j for F = exp(dt(A0 + sum p_j A_j)),
+ * truncated Taylor order 1..4; dFdp_out is nu x (N x N). */
+int qoc_expm_jacobian(int device, int N, int nu, const double* A0, const double* const* Aj,
+                      const double* p, int order, double dt, double* dFdp_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QOC_MI355X_H */

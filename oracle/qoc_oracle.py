@@ -1,0 +1,442 @@
+"""CPU restatement (numpy, fp64) of the reference's PWC GRAPE hot path.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the
+*checker*.  The product path (``quantumoptimalcontrol.jl_amd/qoc_amd``) never
+imports it and fails loudly when its HIP library is missing.
+
+Every function cites the reference file:line it restates (paths relative to
+olof3/QuantumOptimalControl.jl).  The reference is Julia and cannot run in this
+image (no ``julia``); parity of this restatement is pinned by the reference's
+own known-answer values and tolerance contracts:
+
+* ``test/test_fidelities.jl:53-118``   — phase-calibrated fidelity known answers
+* ``test/test_expm_jacobian.jl:13-35`` — Taylor expm-Jacobian FD thresholds
+* ``test/test_penalty_fcns.jl:7-40``   — cost gradients (Wirtinger convention)
+* ``examples/cavity_qubit.jl:80-81``   — cavity forward known answer 0.999979
+* ``scipy.linalg.expm`` agreement for the third-party ``exponential!``
+  (ExponentialUtilities ``ExpMethodHigham2005``, version unpinned in
+  ``Project.toml:9``: restated below from its published algorithm).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+# ---------------------------------------------------------------------------
+# Padé coefficients (b_0 .. b_d) of ExpMethodHigham2005 / LinearAlgebra.exp!
+# (third-party, called at src/gradient_computations.jl:24).
+# ---------------------------------------------------------------------------
+PADE = {
+    3: [120.0, 60.0, 12.0, 1.0],
+    5: [30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0],
+    7: [17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0],
+    9: [17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0,
+        2162160.0, 110880.0, 3960.0, 90.0, 1.0],
+    13: [64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
+         1187353796428800.0, 129060195264000.0, 10559470521600.0,
+         670442572800.0, 33522128640.0, 1323241920.0, 40840800.0, 960960.0,
+         16380.0, 182.0, 1.0],
+}
+
+# Degree-minimal complex GEMM count per degree (SURVEY.md §8d accounting).
+GEMMS_PER_DEGREE = {3: 2, 5: 3, 7: 4, 9: 5, 13: 6}
+
+
+def pade_degree(nA: float) -> tuple[int, int]:
+    """Degree / squaring selection of ExpMethodHigham2005 from ||A||_1.
+
+    Thresholds 2.1 / 0.95 / 0.25 / 0.015 and theta_13 = 5.4 as in
+    LinearAlgebra.exp! (mirrored by ExponentialUtilities).
+    """
+    if nA <= 2.1:
+        if nA > 0.95:
+            return 9, 0
+        if nA > 0.25:
+            return 7, 0
+        if nA > 0.015:
+            return 5, 0
+        return 3, 0
+    s = math.log2(nA / 5.4)
+    si = int(math.ceil(s)) if s > 0 else 0
+    return 13, si
+
+
+def expm_higham2005(A: np.ndarray) -> tuple[np.ndarray, int, int]:
+    """U = exp(A) by scaling-and-squaring Padé; returns (U, degree, squarings).
+
+    Restates ``ExponentialUtilities.exponential!(A, ExpMethodHigham2005(), cache)``
+    (src/gradient_computations.jl:24).  Balancing (``gebal!('B')``) is omitted:
+    for the skew-Hermitian generators of this path (A = -i H dt) the row and
+    column norms are equal, so gebal's scaling is the identity and only a
+    permutation (value-neutral) could remain.
+    """
+    A = np.array(A, dtype=np.complex128, copy=True)
+    n = A.shape[0]
+    eye = np.eye(n, dtype=np.complex128)
+    nA = float(np.abs(A).sum(axis=0).max()) if n else 0.0
+    d, s = pade_degree(nA)
+    C = PADE[d]
+    if d < 13:
+        A2 = A @ A
+        P = eye.copy()
+        U = C[1] * P
+        V = C[0] * P
+        for k in range(1, len(C) // 2):
+            P = P @ A2
+            U = U + C[2 * k + 1] * P
+            V = V + C[2 * k] * P
+        U = A @ U
+    else:
+        if s > 0:
+            A = A / float(2 ** s)
+        A2 = A @ A
+        A4 = A2 @ A2
+        A6 = A2 @ A4
+        U = A @ (A6 @ (C[13] * A6 + C[11] * A4 + C[9] * A2)
+                 + C[7] * A6 + C[5] * A4 + C[3] * A2 + C[1] * eye)
+        V = (A6 @ (C[12] * A6 + C[10] * A4 + C[8] * A2)
+             + C[6] * A6 + C[4] * A4 + C[2] * A2 + C[0] * eye)
+    X = np.linalg.solve(V - U, V + U)  # LAPACK gesv (LU, partial pivoting)
+    for _ in range(s):
+        X = X @ X
+    return X, d, s
+
+
+# ---------------------------------------------------------------------------
+# Generators (src/utils.jl:86-91)
+# ---------------------------------------------------------------------------
+def setup_bilinear_matrices(H0, Tc, dt=1.0):
+    """A0 = -i H0 dt, A1 = -i (Tc+Tc') dt, A2 = -i (i (Tc-Tc')) dt (src/utils.jl:86-91)."""
+    H0 = np.asarray(H0, dtype=np.complex128)
+    Tc = np.asarray(Tc, dtype=np.complex128)
+    A0 = -1j * H0 * dt
+    A1 = -1j * (Tc + Tc.conj().T) * dt
+    A2 = -1j * (1j * (Tc - Tc.conj().T)) * dt
+    return A0, A1, A2
+
+
+# ---------------------------------------------------------------------------
+# GRAPE cache + forward propagation (src/gradient_computations.jl:2-32,79-96)
+# ---------------------------------------------------------------------------
+@dataclass
+class GrapeCache:
+    x: list = field(default_factory=list)      # Nt+1 states, N x m
+    lam: list = field(default_factory=list)    # Nt+1 co-states
+    dJdu: np.ndarray | None = None             # nu x Nt
+    Uk: list = field(default_factory=list)     # Nt propagators
+    u: np.ndarray | None = None                # u used by the last propagate
+    degrees: list = field(default_factory=list)
+
+
+def setup_grape_cache(A0, x0, u_shape) -> GrapeCache:
+    """Workspace; errors on a dimension mismatch (src/gradient_computations.jl:79-96)."""
+    x0 = np.asarray(x0)
+    if x0.ndim == 1:
+        x0 = x0[:, None]
+    if x0.shape[0] != np.asarray(A0).shape[0]:
+        raise ValueError("Error when creating cache, A0 and x0 have incompatiable dimensions")
+    nu, Nt = u_shape
+    return GrapeCache(x=[None] * (Nt + 1), lam=[None] * (Nt + 1),
+                      dJdu=np.zeros((nu, Nt)), Uk=[None] * Nt,
+                      u=np.zeros((nu, Nt)), degrees=[None] * Nt)
+
+
+def propagate(A0, A, u, x0, cache: GrapeCache | None = None) -> list:
+    """x_{k+1} = exp(A0 + sum_j u[j,k] A_j) x_k (src/gradient_computations.jl:2-32)."""
+    u = np.asarray(u, dtype=np.float64)
+    x0 = np.asarray(x0, dtype=np.complex128)
+    if x0.ndim == 1:
+        x0 = x0[:, None]
+    Nt = u.shape[1]
+    if cache is None:
+        cache = setup_grape_cache(A0, x0, u.shape)
+    cache.u = u.copy()                                   # :12
+    cache.x[0] = x0.copy()                               # :14
+    for k in range(Nt):                                  # :17-25
+        Ak = np.array(A0, dtype=np.complex128, copy=True)
+        for j in range(len(A)):
+            Ak = Ak + u[j, k] * A[j]
+        cache.Uk[k], d, s = expm_higham2005(Ak)
+        cache.degrees[k] = (d, s)
+    for k in range(Nt):                                  # :27-29
+        cache.x[k + 1] = cache.Uk[k] @ cache.x[k]
+    return cache.x
+
+
+def expm_jacobian(A0, A, p, order=2, dt=1.0) -> list:
+    """Truncated-Taylor derivative of exp(dt(A0+sum p_j A_j)) w.r.t. p_j.
+
+    Restates ``expm_jacobian!`` (src/gradient_computations.jl:177-213) term by
+    term: order 1 dt*A_j (:179-182), order 2 dt^2/2 (A_j X + X A_j) (:194-197),
+    order 3 dt^3/6 (A_j X^2 + X A_j X + X^2 A_j) (:199-202), order 4
+    dt^4/24 (A_j X^3 + X A_j X^2 + X^2 A_j X + X^3 A_j) (:204-210).
+    """
+    out = [dt * np.asarray(Aj, dtype=np.complex128) for Aj in A]
+    if order <= 1:
+        return out
+    X = np.array(A0, dtype=np.complex128, copy=True)
+    for j in range(len(A)):
+        X = X + p[j] * A[j]
+    for j in range(len(A)):
+        AjX = A[j] @ X
+        XAj = X @ A[j]
+        if order >= 2:
+            out[j] = out[j] + (dt ** 2 / 2) * (AjX + XAj)
+        if order >= 3:
+            out[j] = out[j] + (dt ** 3 / 6) * (AjX @ X + XAj @ X + X @ XAj)
+        if order >= 4:
+            X2 = X @ X
+            out[j] = out[j] + (dt ** 4 / 24) * (AjX @ X2 + XAj @ X2 + X2 @ AjX + X2 @ XAj)
+    return out
+
+
+def compute_u_sensitivity(xk, lam_kp1, dU) -> float:
+    """sum_l Re(lam[:,l]' dU x[:,l]) (src/gradient_computations.jl:217-223)."""
+    return float(np.real(np.sum(np.conj(lam_kp1) * (dU @ xk))))
+
+
+def grape_sensitivity(A0, A, dJfinal_dx, u, x0, cache: GrapeCache, dUkdp_order=3,
+                      dL_dx=None) -> np.ndarray:
+    """Co-state sweep + Taylor-Jacobian contraction (src/gradient_computations.jl:35-77)."""
+    u = np.asarray(u, dtype=np.float64)
+    if cache.u is None or u.shape != cache.u.shape or not np.array_equal(u, cache.u):
+        raise ValueError("Cache data from other control signal u")       # :37-39
+    Nt = u.shape[1]
+    x, lam = cache.x, cache.lam
+    assert len(x) == len(lam) == Nt + 1                                   # :44
+    lam[Nt] = np.asarray(dJfinal_dx(x[Nt]), dtype=np.complex128)         # :46
+    if dL_dx is not None:
+        lam[Nt] = lam[Nt] + dL_dx(x[Nt])                                  # :47-49
+    for k in range(Nt - 1, -1, -1):                                       # :52-58
+        lam[k] = cache.Uk[k].conj().T @ lam[k + 1]
+        if dL_dx is not None:
+            lam[k] = lam[k] + dL_dx(x[k])
+    for k in range(Nt - 1, -1, -1):                                       # :65-74
+        dU = expm_jacobian(A0, A, u[:, k], order=dUkdp_order)
+        for j in range(len(A)):
+            cache.dJdu[j, k] = compute_u_sensitivity(x[k], lam[k + 1], dU[j])
+    return cache.dJdu
+
+
+# ---------------------------------------------------------------------------
+# Costs (src/penalty_fcns.jl)
+# ---------------------------------------------------------------------------
+def setup_state_penalty(inds_penalty, inds_css, mu):
+    """L = mu sum |x[P,C]|^2, dL/dx = 2 mu x[P,C] (src/penalty_fcns.jl:1-11); 0-based indices."""
+    P = np.asarray(inds_penalty, dtype=np.int64)
+    C = np.asarray(inds_css, dtype=np.int64)
+
+    def L(x):
+        return float(mu * np.sum(np.abs(x[np.ix_(P, C)]) ** 2))
+
+    def dL_dx(x):
+        g = np.zeros_like(np.asarray(x, dtype=np.complex128))
+        g[np.ix_(P, C)] = 2 * mu * x[np.ix_(P, C)]
+        return g
+    return L, dL_dx
+
+
+def setup_infidelity(x_target, n=None):
+    """J = 1 - |tr(X'x)|^2/n^2, dJ/dx = -(2 Omega/n^2) X (src/penalty_fcns.jl:15-24)."""
+    X = np.asarray(x_target, dtype=np.complex128)
+    if X.ndim == 1:
+        X = X[:, None]
+    n = X.shape[1] if n is None else n
+
+    def J(x):
+        return float(1 - abs(np.trace(X.conj().T @ x)) ** 2 / n ** 2)
+
+    def dJ_dx(x):
+        om = np.trace(X.conj().T @ x)
+        return (-2 * om / n ** 2) * X
+    return J, dJ_dx
+
+
+def setup_infidelity_zcalibrated(x_target):
+    """Z-calibrated two-qubit infidelity (src/penalty_fcns.jl:27-42); needs 4 columns."""
+    X = np.asarray(x_target, dtype=np.complex128)
+    if X.shape[1] != 4:
+        raise ValueError("Only works for two-qubit gates, x_target must have four columns")
+
+    def J(x):
+        m = np.diag(X.conj().T @ x)
+        return float(1 - abs_sum_phase_calibrated(m) ** 2 / 16)
+
+    def dJ_dx(x):
+        m = np.diag(X.conj().T @ x)
+        F, grad_F = abs_sum_phase_calibrated_rrule(m)
+        return (-2 * F / 16) * (X * grad_F[None, :])
+    return J, dJ_dx
+
+
+# ---------------------------------------------------------------------------
+# Phase-calibrated fidelities (src/fidelities.jl)
+# ---------------------------------------------------------------------------
+def _angle(z):
+    return math.atan2(z.imag, z.real)
+
+
+def _cis(t):
+    return complex(math.cos(t), math.sin(t))
+
+
+def golden_section_search(f, lo, hi, tol):
+    """src/fidelities.jl:105-137 (returns (min value, minimiser))."""
+    if lo > hi:
+        raise ValueError(f"x_lower must be less than x_upper ({lo}, {hi})")
+    gr = 0.5 * (3.0 - math.sqrt(5.0))
+    xm = lo + gr * (hi - lo)
+    fm = f(xm)
+    while hi - lo >= tol:
+        if hi - xm > xm - lo:
+            xn = xm + gr * (hi - xm)
+            fn = f(xn)
+            if fn < fm:
+                lo, xm, fm = xm, xn, fn
+            else:
+                hi = xn
+        else:
+            xn = xm - gr * (xm - lo)
+            fn = f(xn)
+            if fn < fm:
+                hi, xm, fm = xm, xn, fn
+            else:
+                lo = xn
+    return fm, xm
+
+
+def _mod2pi(x):
+    return x % (2 * math.pi)
+
+
+def optimal_calibration(m, theta_tol=1e-9):
+    """src/fidelities.jl:81-101: best local-Z phase by golden section."""
+    m = [complex(v) for v in m]
+    a1 = abs(m[0]) ** 2 + abs(m[1]) ** 2
+    b1 = 2 * abs(m[0]) * abs(m[1])
+    a2 = abs(m[2]) ** 2 + abs(m[3]) ** 2
+    b2 = 2 * abs(m[2]) * abs(m[3])
+    p1 = _mod2pi(_angle(m[0]) - _angle(m[1]))
+    p2 = _mod2pi(_angle(m[2]) - _angle(m[3]))
+    if abs(p2 - p1) <= math.pi:
+        pmean, D, alpha = (p1 + p2) / 2, abs(p2 - p1) / 2, (1 if p1 < p2 else -1)
+    else:
+        pmean, D, alpha = (2 * math.pi + p1 + p2) / 2, math.pi - abs(p2 - p1) / 2, (-1 if p1 < p2 else 1)
+
+    def J(dl):
+        return math.sqrt(a1 + b1 * math.cos(dl + D)) + math.sqrt(a2 + b2 * math.cos(dl - D))
+    mJ, dopt = golden_section_search(lambda dl: -J(dl), -D, D, theta_tol)
+    th1 = pmean + alpha * dopt
+    th2 = _angle(m[0] + m[1] * _cis(th1)) - _angle(m[2] + m[3] * _cis(th1))
+    return -mJ, [th1, th2]
+
+
+def basic_calibration(m):
+    """src/fidelities.jl:65-69."""
+    t0 = _angle(m[0])
+    th = [-(_angle(m[1]) - t0), -(_angle(m[2]) - t0)]
+    return abs(m[0] + m[1] * _cis(th[0]) + m[2] * _cis(th[1]) + m[3] * _cis(th[0] + th[1])), th
+
+
+def grid_calibration(m):
+    """src/fidelities.jl:72-79 (100-point grid on [0, 2pi])."""
+    best, tb = -math.inf, 0.0
+    for t in np.linspace(0, 2 * math.pi, 100):
+        v = abs(m[0] + m[1] * _cis(t)) + abs(m[2] + m[3] * _cis(t))
+        if v > best:
+            best, tb = v, float(t)
+    return best, tb
+
+
+def abs_sum_phase_calibrated(m, calibration="optimal"):
+    """src/fidelities.jl:11-40 (all calibration variants)."""
+    m = [complex(v) for v in m]
+    if calibration == "lms_phase":
+        t1 = -_angle(m[0].conjugate() * m[1] + m[2].conjugate() * m[3])
+        return abs(m[0] + m[1] * _cis(t1)) + abs(m[2] + m[3] * _cis(t1))
+    if calibration == "lms_phase2":
+        x1, x2 = math.sqrt(abs(m[0] * m[1])), math.sqrt(abs(m[2] * m[3]))
+        eps = np.finfo(np.float64).eps
+        if x1 < eps or x2 < eps:
+            return abs(m[0]) + abs(m[1]) + abs(m[2]) + abs(m[3])
+        t1 = -_angle(m[0].conjugate() * m[1] / x1 + m[2].conjugate() * m[3] / x2)
+        return abs(m[0] + m[1] * _cis(t1)) + abs(m[2] + m[3] * _cis(t1))
+    if calibration == "lms_phase3":
+        x1, x2 = abs(m[0]) + abs(m[1]), abs(m[2]) + abs(m[3])
+        t1 = -_angle(m[0].conjugate() * m[1] / x1 + m[2].conjugate() * m[3] / x2)
+        return abs(m[0] + m[1] * _cis(t1)) + abs(m[2] + m[3] * _cis(t1))
+    if calibration == "optimal":
+        return optimal_calibration(m)[0]
+    if calibration == "basic":
+        return basic_calibration(m)[0]
+    if calibration == "none":
+        return abs(sum(m))
+    if calibration == "grid":
+        return grid_calibration(m)[0]
+    return None  # unmatched symbol returns `nothing` in the reference
+
+
+def abs_sum_phase_calibrated_rrule(m):
+    """ChainRulesCore.rrule (src/fidelities.jl:48-56): value F and dF/dm (Wirtinger)."""
+    m = [complex(v) for v in m]
+    F, th = optimal_calibration(m)
+    v1 = m[0] + _cis(th[0]) * m[1]
+    v2 = m[2] + _cis(th[0]) * m[3]
+    g = np.array([v1 / abs(v1), v1 / abs(v1) * _cis(-th[0]),
+                  v2 / abs(v2), v2 / abs(v2) * _cis(-th[0])], dtype=np.complex128)
+    return F, g
+
+
+def abs_sum_phase_calibrated_grad(m, th1):
+    """Gradient of F^2 (src/fidelities.jl:42-46)."""
+    m = [complex(v) for v in m]
+    v1 = m[0] + _cis(th1) * m[1]
+    v2 = m[2] + _cis(th1) * m[3]
+    return 2 * (abs(v1) + abs(v2)) * np.array(
+        [v1 / abs(v1), v1 / abs(v1) * _cis(-th1), v2 / abs(v2), v2 / abs(v2) * _cis(-th1)])
+
+
+def infidelity(U_target, Uf, calibration="lms_phase"):
+    """src/fidelities.jl:1-7 (4x4 only)."""
+    U_target = np.asarray(U_target)
+    if U_target.shape != (4, 4):
+        raise ValueError("Not supported yet")
+    return 1 - abs_sum_phase_calibrated(np.diag(U_target.conj().T @ Uf), calibration) / 4
+
+
+# ---------------------------------------------------------------------------
+# Batched convenience used by the parity tests and bench cpu_baseline
+# ---------------------------------------------------------------------------
+def grape_eval(A0, A, u, x0, x_target, n=None, order=3, penalty=None):
+    """One GRAPE gradient eval = propagate + J + grape_sensitivity.
+
+    Mirrors the Ipopt callbacks f / f_grad (examples/ipopt_callbacks_exp.jl:11-31)
+    without the spline map.  ``penalty`` = (P, C, mu) enables the state penalty.
+    Returns (J, dJdu, cache).
+    """
+    Jf, dJf = setup_infidelity(x_target, n)
+    L = dL = None
+    if penalty is not None:
+        L, dL = setup_state_penalty(*penalty)
+    cache = setup_grape_cache(A0, x0, np.shape(u))
+    x = propagate(A0, A, u, x0, cache)
+    J = Jf(x[-1]) + (sum(L(xk) for xk in x) if L is not None else 0.0)
+    dJdu = grape_sensitivity(A0, A, dJf, cache.u, x0, cache, dUkdp_order=order, dL_dx=dL)
+    return J, dJdu.copy(), cache
+
+
+def eval_flops(N, m, nu, degrees, order=3):
+    """Reference-equivalent algorithmic FLOPs of one eval (SURVEY.md §8d formula).
+
+    F_slice = 8N^3 (G(d)+s) + (40/3) N^3 + 8N^2 m   (forward)
+            + 8N^2 m + 8N^3 * G_jac * nu + 8N^2 m nu   (backward), G_jac = 5 at order 3.
+    """
+    gj = {1: 0, 2: 2, 3: 5, 4: 9}[order]
+    f = 0.0
+    for d, s in degrees:
+        f += 8 * N ** 3 * (GEMMS_PER_DEGREE[d] + s) + (40.0 / 3.0) * N ** 3 + 8 * N ** 2 * m
+        f += 8 * N ** 2 * m + 8 * N ** 3 * gj * nu + 8 * N ** 2 * m * nu
+    return f

@@ -1,0 +1,383 @@
+// qoc_chain.hpp — serial-in-k propagator chains, fused costs, and the per-slice gradient.
+//
+//   k_chain_fwd : x_{k+1} = U_k x_k              (src/gradient_computations.jl:27-29)
+//                 + terminal cost J / dJ/dx coefficients (src/penalty_fcns.jl:15-42,
+//                   src/fidelities.jl:48-56,81-137) + state penalty L (src/penalty_fcns.jl:1-11)
+//   k_chain_bwd : λ_k = U_k^† λ_{k+1} + dL/dx(x_k) (src/gradient_computations.jl:46-58)
+//   k_grad      : dJdu[j,k] = Σ_l Re(λ_{k+1,l}^† dU_j x_{k,l}) with the truncated Taylor
+//                 dU_j of expm_jacobian! (src/gradient_computations.jl:65-74,177-223),
+//                 contracted through matrix-vector products instead of forming dU_j:
+//                   λ^† X^b A_j X^a x = <(X^†)^b λ, A_j X^a x>,  coefficient 1/(a+b+1)!.
+//
+// One workgroup per seed for the chains (the time axis is a serial recurrence);
+// U_k is staged through double-buffered LDS with the next slice prefetched into
+// registers while the current matvec runs.
+#pragma once
+#include "qoc_common.hpp"
+
+namespace qoc {
+
+constexpr int CHAIN_THREADS = 256;
+constexpr int CHAIN_PREF = 16;  // max U elements per thread prefetched (N*N <= 4096)
+
+enum { COST_TRACE = 0, COST_ZCAL = 1, COST_EXTERNAL = 2 };
+
+// ----- golden-section phase calibration (src/fidelities.jl:81-137), one lane -----
+__device__ inline double mod2pi(double x) {
+  const double tp = 2.0 * M_PI;
+  double r = fmod(x, tp);
+  if (r < 0) r += tp;
+  return r;
+}
+
+__device__ inline void optimal_calibration(const cx<double> m[4], double tol, double* F, double* th1) {
+  auto ab = [](cx<double> z) { return sqrt(z.r * z.r + z.i * z.i); };
+  auto ang = [](cx<double> z) { return atan2(z.i, z.r); };
+  const double a1 = ab(m[0]) * ab(m[0]) + ab(m[1]) * ab(m[1]);
+  const double b1 = 2 * ab(m[0]) * ab(m[1]);
+  const double a2 = ab(m[2]) * ab(m[2]) + ab(m[3]) * ab(m[3]);
+  const double b2 = 2 * ab(m[2]) * ab(m[3]);
+  const double p1 = mod2pi(ang(m[0]) - ang(m[1]));
+  const double p2 = mod2pi(ang(m[2]) - ang(m[3]));
+  double pm, D, al;
+  if (fabs(p2 - p1) <= M_PI) {
+    pm = (p1 + p2) / 2;
+    D = fabs(p2 - p1) / 2;
+    al = p1 < p2 ? 1 : -1;
+  } else {
+    pm = (2 * M_PI + p1 + p2) / 2;
+    D = M_PI - fabs(p2 - p1) / 2;
+    al = p1 < p2 ? -1 : 1;
+  }
+  auto f = [&](double dl) { return -(sqrt(a1 + b1 * cos(dl + D)) + sqrt(a2 + b2 * cos(dl - D))); };
+  double lo = -D, hi = D;
+  const double gr = 0.5 * (3.0 - sqrt(5.0));
+  double xm = lo + gr * (hi - lo), fm = f(xm);
+  while (hi - lo >= tol) {
+    if (hi - xm > xm - lo) {
+      const double xn = xm + gr * (hi - xm), fn = f(xn);
+      if (fn < fm) {
+        lo = xm;
+        xm = xn;
+        fm = fn;
+      } else {
+        hi = xn;
+      }
+    } else {
+      const double xn = xm - gr * (xm - lo), fn = f(xn);
+      if (fn < fm) {
+        hi = xm;
+        xm = xn;
+        fm = fn;
+      } else {
+        lo = xn;
+      }
+    }
+  }
+  *F = -fm;
+  *th1 = pm + al * xm;
+}
+
+// Cooperative copy of an N x N column-major complex matrix into LDS with leading dimension N+1.
+template <typename T>
+__device__ __forceinline__ void prefetch_u(const cx<T>* __restrict__ src, int NN, cx<T> (&pre)[CHAIN_PREF]) {
+#pragma unroll
+  for (int r = 0; r < CHAIN_PREF; ++r) {
+    const int e = threadIdx.x + CHAIN_THREADS * r;
+    if (e < NN) pre[r] = src[e];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void commit_u(cx<T>* __restrict__ dst, int N, const cx<T> (&pre)[CHAIN_PREF]) {
+  const int NN = N * N;
+#pragma unroll
+  for (int r = 0; r < CHAIN_PREF; ++r) {
+    const int e = threadIdx.x + CHAIN_THREADS * r;
+    if (e < NN) {
+      const int i = e % N, j = e / N;
+      dst[i + (N + 1) * j] = pre[r];
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
+    int N, int m, int Nt, const cx<T>* __restrict__ U, const cx<T>* __restrict__ x0, int x0_per_seed,
+    cx<T>* __restrict__ X, const cx<T>* __restrict__ Xt, int cost_kind, double n_norm,
+    const unsigned char* __restrict__ pmask, double mu, double* __restrict__ Jout, cx<double>* __restrict__ coef) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int NN = N * N, Nm = N * m, LDU = N * (N + 1);
+  cx<T>* ub = reinterpret_cast<cx<T>*>(smem);  // 2 x N(N+1)
+  cx<T>* xb = ub + 2 * LDU;                     // N*m
+  double* red = reinterpret_cast<double*>(xb + Nm);
+  const cx<T>* Ub = U + (size_t)b * Nt * NN;
+  cx<T>* Xb = X + (size_t)b * (Nt + 1) * Nm;
+  const cx<T>* x0b = x0 + (x0_per_seed ? (size_t)b * Nm : 0);
+  double pen = 0.0;
+  for (int o = tid; o < Nm; o += CHAIN_THREADS) {
+    const cx<T> v = x0b[o];
+    xb[o] = v;
+    Xb[o] = v;
+    if (pmask && pmask[o]) pen += (double)v.r * v.r + (double)v.i * v.i;
+  }
+  cx<T> pre[CHAIN_PREF];
+  prefetch_u(Ub, NN, pre);
+  commit_u(ub, N, pre);
+  __syncthreads();
+  for (int k = 0; k < Nt; ++k) {
+    const cx<T>* cur = ub + (k & 1) * LDU;
+    if (k + 1 < Nt) prefetch_u(Ub + (size_t)(k + 1) * NN, NN, pre);
+    cx<T> y[4];
+    int cnt = 0;
+    for (int o = tid; o < Nm; o += CHAIN_THREADS, ++cnt) {
+      const int i = o % N, c = o / N;
+      cx<T> acc = {0, 0};
+      const cx<T>* xc = xb + N * c;
+      for (int j = 0; j < N; ++j) acc = cfma(acc, cur[i + (N + 1) * j], xc[j]);
+      if (cnt < 4) y[cnt] = acc;
+    }
+    __syncthreads();
+    cnt = 0;
+    cx<T>* Xk = Xb + (size_t)(k + 1) * Nm;
+    for (int o = tid; o < Nm; o += CHAIN_THREADS, ++cnt) {
+      const cx<T> v = y[cnt];
+      xb[o] = v;
+      Xk[o] = v;
+      if (pmask && pmask[o]) pen += (double)v.r * v.r + (double)v.i * v.i;
+    }
+    if (k + 1 < Nt) commit_u(ub + ((k + 1) & 1) * LDU, N, pre);
+    __syncthreads();
+  }
+  // ---- costs on x_N ----
+  const double psum = block_sum(pen, red) * mu;
+  if (cost_kind == COST_TRACE) {
+    double orr = 0, oii = 0;
+    for (int o = tid; o < Nm; o += CHAIN_THREADS) {
+      const cx<T> t = Xt[o], v = xb[o];
+      orr += (double)t.r * v.r + (double)t.i * v.i;
+      oii += (double)t.r * v.i - (double)t.i * v.r;
+    }
+    orr = block_sum(orr, red);
+    oii = block_sum(oii, red);
+    if (tid == 0) {
+      const double n2 = n_norm * n_norm;
+      Jout[b] = 1.0 - (orr * orr + oii * oii) / n2 + psum;
+      for (int c = 0; c < m; ++c) coef[(size_t)b * m + c] = cx<double>{-2.0 * orr / n2, -2.0 * oii / n2};
+    }
+  } else if (cost_kind == COST_ZCAL) {
+    cx<double> mm[4];
+    for (int c = 0; c < 4; ++c) {
+      double orr = 0, oii = 0;
+      for (int i = tid; i < N; i += CHAIN_THREADS) {
+        const cx<T> t = Xt[i + N * c], v = xb[i + N * c];
+        orr += (double)t.r * v.r + (double)t.i * v.i;
+        oii += (double)t.r * v.i - (double)t.i * v.r;
+      }
+      mm[c].r = block_sum(orr, red);
+      mm[c].i = block_sum(oii, red);
+    }
+    if (tid == 0) {
+      double F, th;
+      optimal_calibration(mm, 1e-9, &F, &th);
+      Jout[b] = 1.0 - F * F / 16.0 + psum;
+      const cx<double> e = {cos(th), sin(th)}, em = {cos(th), -sin(th)};
+      const cx<double> v1 = {mm[0].r + e.r * mm[1].r - e.i * mm[1].i, mm[0].i + e.r * mm[1].i + e.i * mm[1].r};
+      const cx<double> v2 = {mm[2].r + e.r * mm[3].r - e.i * mm[3].i, mm[2].i + e.r * mm[3].i + e.i * mm[3].r};
+      const double a1 = sqrt(v1.r * v1.r + v1.i * v1.i), a2 = sqrt(v2.r * v2.r + v2.i * v2.i);
+      const cx<double> g[4] = {{v1.r / a1, v1.i / a1},
+                               {(v1.r * em.r - v1.i * em.i) / a1, (v1.r * em.i + v1.i * em.r) / a1},
+                               {v2.r / a2, v2.i / a2},
+                               {(v2.r * em.r - v2.i * em.i) / a2, (v2.r * em.i + v2.i * em.r) / a2}};
+      const double s = -2.0 * F / 16.0;
+      for (int c = 0; c < 4; ++c) coef[(size_t)b * m + c] = cx<double>{s * g[c].r, s * g[c].i};
+    }
+  } else {
+    if (tid == 0) {
+      Jout[b] = psum;
+      for (int c = 0; c < m; ++c) coef[(size_t)b * m + c] = cx<double>{0, 0};
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
+    int N, int m, int Nt, const cx<T>* __restrict__ U, const cx<T>* __restrict__ X, cx<T>* __restrict__ Lam,
+    const cx<T>* __restrict__ Xt, int cost_kind, const cx<double>* __restrict__ coef,
+    const unsigned char* __restrict__ pmask, double mu) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int NN = N * N, Nm = N * m, LDU = N * (N + 1);
+  cx<T>* ub = reinterpret_cast<cx<T>*>(smem);
+  cx<T>* lb = ub + 2 * LDU;
+  const cx<T>* Ub = U + (size_t)b * Nt * NN;
+  const cx<T>* Xb = X + (size_t)b * (Nt + 1) * Nm;
+  cx<T>* Lb = Lam + (size_t)b * (Nt + 1) * Nm;
+  const T tmu = (T)(2.0 * mu);
+  // λ_{Nt+1} = dJfinal/dx(x_N) (+ dL/dx(x_N))
+  for (int o = tid; o < Nm; o += CHAIN_THREADS) {
+    cx<T> v;
+    if (cost_kind == COST_EXTERNAL) {
+      v = Lb[(size_t)Nt * Nm + o];
+    } else {
+      const cx<double> cf = coef[(size_t)b * m + o / N];
+      const cx<T> t = Xt[o];
+      v.r = (T)(cf.r * t.r - cf.i * t.i);
+      v.i = (T)(cf.r * t.i + cf.i * t.r);
+    }
+    if (pmask && pmask[o]) {
+      const cx<T> xv = Xb[(size_t)Nt * Nm + o];
+      v.r += tmu * xv.r;
+      v.i += tmu * xv.i;
+    }
+    lb[o] = v;
+    Lb[(size_t)Nt * Nm + o] = v;
+  }
+  cx<T> pre[CHAIN_PREF];
+  prefetch_u(Ub + (size_t)(Nt - 1) * NN, NN, pre);
+  commit_u(ub + ((Nt - 1) & 1) * LDU, N, pre);
+  __syncthreads();
+  for (int k = Nt - 1; k >= 0; --k) {
+    const cx<T>* cur = ub + (k & 1) * LDU;
+    if (k > 0) prefetch_u(Ub + (size_t)(k - 1) * NN, NN, pre);
+    cx<T> y[4];
+    int cnt = 0;
+    for (int o = tid; o < Nm; o += CHAIN_THREADS, ++cnt) {
+      const int i = o % N, c = o / N;
+      cx<T> acc = {0, 0};
+      const cx<T>* lc = lb + N * c;
+      const cx<T>* ucol = cur + (N + 1) * i;  // column i of U_k
+      for (int j = 0; j < N; ++j) acc = cfmaconj(acc, ucol[j], lc[j]);
+      if (pmask && pmask[o]) {
+        const cx<T> xv = Xb[(size_t)k * Nm + o];
+        acc.r += tmu * xv.r;
+        acc.i += tmu * xv.i;
+      }
+      if (cnt < 4) y[cnt] = acc;
+    }
+    __syncthreads();
+    cnt = 0;
+    cx<T>* Lk = Lb + (size_t)k * Nm;
+    for (int o = tid; o < Nm; o += CHAIN_THREADS, ++cnt) {
+      lb[o] = y[cnt];
+      Lk[o] = y[cnt];
+    }
+    if (k > 0) commit_u(ub + ((k - 1) & 1) * LDU, N, pre);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Per-slice gradient.  unit = (b, k) = blockIdx.x.
+// ---------------------------------------------------------------------------
+constexpr int GRAD_THREADS = 256;
+
+template <typename T>
+__global__ __launch_bounds__(GRAD_THREADS) void k_grad(int N, int m, int nu, int Nt, int order,
+                                                       const cx<T>* __restrict__ Agen, const double* __restrict__ u,
+                                                       const cx<T>* __restrict__ X, const cx<T>* __restrict__ Lam,
+                                                       double* __restrict__ dJdu) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int unit = blockIdx.x, b = unit / Nt, k = unit - b * Nt, tid = threadIdx.x;
+  const int NN = N * N, Nm = N * m, LD = N + 1;
+  cx<T>* Xk = reinterpret_cast<cx<T>*>(smem);  // N x (N+1)
+  cx<T>* P = Xk + N * LD;                       // order x Nm
+  cx<T>* Q = P + order * Nm;                    // order x Nm
+  double* red = reinterpret_cast<double*>(Q + order * Nm);
+  for (int e = tid; e < NN; e += GRAD_THREADS) {
+    cx<T> a = Agen[e];
+    for (int j = 0; j < nu; ++j) {
+      const T uj = (T)u[(size_t)unit * nu + j];
+      const cx<T> g = Agen[(size_t)(j + 1) * NN + e];
+      a.r += uj * g.r;
+      a.i += uj * g.i;
+    }
+    Xk[(e % N) + LD * (e / N)] = a;
+  }
+  const cx<T>* xk = X + ((size_t)b * (Nt + 1) + k) * Nm;
+  const cx<T>* lk = Lam + ((size_t)b * (Nt + 1) + k + 1) * Nm;
+  for (int o = tid; o < Nm; o += GRAD_THREADS) {
+    P[o] = xk[o];
+    Q[o] = lk[o];
+  }
+  __syncthreads();
+  for (int a = 1; a < order; ++a) {
+    const cx<T>* Pp = P + (a - 1) * Nm;
+    const cx<T>* Qp = Q + (a - 1) * Nm;
+    for (int o = tid; o < Nm; o += GRAD_THREADS) {
+      const int i = o % N, c = o / N;
+      cx<T> pa = {0, 0}, qa = {0, 0};
+      for (int l = 0; l < N; ++l) {
+        pa = cfma(pa, Xk[i + LD * l], Pp[l + N * c]);
+        qa = cfmaconj(qa, Xk[l + LD * i], Qp[l + N * c]);
+      }
+      P[a * Nm + o] = pa;
+      Q[a * Nm + o] = qa;
+    }
+    __syncthreads();
+  }
+  const double fact[5] = {1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0, 1.0 / 120.0};
+  for (int j = 0; j < nu; ++j) {
+    const cx<T>* Aj = Agen + (size_t)(j + 1) * NN;
+    double acc = 0.0;
+    for (int o = tid; o < Nm; o += GRAD_THREADS) {
+      const int i = o % N, c = o / N;
+      for (int a = 0; a < order; ++a) {
+        cx<T> r = {0, 0};
+        const cx<T>* Pa = P + a * Nm + N * c;
+        for (int l = 0; l < N; ++l) r = cfma(r, Aj[i + N * l], Pa[l]);
+        for (int bb = 0; a + bb < order; ++bb) {
+          const cx<T> qv = Q[bb * Nm + o];
+          acc += fact[a + bb] * ((double)qv.r * r.r + (double)qv.i * r.i);
+        }
+      }
+    }
+    const double s = block_sum(acc, red);
+    if (tid == 0) dJdu[(size_t)b * nu * Nt + (size_t)k * nu + j] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Small helpers used by the host API.
+// ---------------------------------------------------------------------------
+__global__ void k_compare_u(const double* __restrict__ a, const double* __restrict__ b, size_t n, int* flag) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    // bitwise comparison (the reference's `u != cache.u` is elementwise ==; NaN never occurs here)
+    if (__double_as_longlong(a[e]) != __double_as_longlong(b[e])) atomicOr(flag, 1);
+  }
+}
+
+template <typename T>
+__global__ void k_cvt_in(const cx<double>* __restrict__ src, cx<T>* __restrict__ dst, size_t n) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    dst[e] = cx<T>{(T)src[e].r, (T)src[e].i};
+}
+template <typename T>
+__global__ void k_cvt_out(const cx<T>* __restrict__ src, cx<double>* __restrict__ dst, size_t n) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    dst[e] = cx<double>{(double)src[e].r, (double)src[e].i};
+}
+
+// C = alpha * A * B + beta * C  (naive, N x N complex fp64; standalone expm_jacobian only)
+__global__ void k_cgemm_naive(int N, const cx<double>* A, const cx<double>* B, cx<double>* C, double alpha,
+                              double beta) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * N) return;
+  const int i = e % N, j = e / N;
+  cx<double> s = {0, 0};
+  for (int l = 0; l < N; ++l) s = cfma(s, A[i + N * l], B[l + N * j]);
+  C[e] = cx<double>{alpha * s.r + beta * C[e].r, alpha * s.i + beta * C[e].i};
+}
+// Y = sum_t w_t X_t
+__global__ void k_axpby(int n, cx<double>* Y, double a, const cx<double>* A, double b, const cx<double>* B) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  cx<double> r = {a * A[e].r, a * A[e].i};
+  if (B) {
+    r.r += b * B[e].r;
+    r.i += b * B[e].i;
+  }
+  Y[e] = r;
+}
+
+}  // namespace qoc

@@ -1,0 +1,89 @@
+"""ctypes binding of libqoc_mi355x.so (the C ABI in include/qoc.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950).  There is
+no CPU fallback: if the library is missing or cannot be loaded every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libqoc_mi355x.so")
+
+QOC_OK = 0
+QOC_ERR_ARG = -1
+QOC_ERR_HIP = -2
+QOC_ERR_STALE = -3
+QOC_ERR_STATE = -4
+QOC_ERR_UNSUPPORTED = -5
+QOC_FP64 = 0
+QOC_FP32 = 1
+QOC_COST_TRACE = 0
+QOC_COST_ZCAL = 1
+QOC_COST_EXTERNAL = 2
+
+# Every symbol include/qoc.h declares, with (restype, argtypes).
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+_vp = C.c_void_p
+SIGNATURES = {
+    "qoc_create": (C.c_int, [C.POINTER(_vp), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "qoc_destroy": (None, [_vp]),
+    "qoc_last_error": (C.c_char_p, [_vp]),
+    "qoc_stream": (_vp, [_vp]),
+    "qoc_synchronize": (C.c_int, [_vp]),
+    "qoc_set_generators": (C.c_int, [_vp, _dp, C.POINTER(_dp)]),
+    "qoc_set_x0": (C.c_int, [_vp, _dp, C.c_int]),
+    "qoc_set_cost": (C.c_int, [_vp, C.c_int, _dp, C.c_double]),
+    "qoc_set_state_penalty": (C.c_int, [_vp, _ip, C.c_int, _ip, C.c_int, C.c_double]),
+    "qoc_propagate": (C.c_int, [_vp, _dp, _dp]),
+    "qoc_grape_sensitivity": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp]),
+    "qoc_propagate_dev": (C.c_int, [_vp, _vp, _vp]),
+    "qoc_grape_sensitivity_dev": (C.c_int, [_vp, _vp, C.c_int, _vp]),
+    "qoc_eval_dev": (C.c_int, [_vp, _vp, C.c_int, _vp, _vp]),
+    "qoc_get_states": (C.c_int, [_vp, C.c_int, C.c_int, _dp]),
+    "qoc_get_costates": (C.c_int, [_vp, C.c_int, C.c_int, _dp]),
+    "qoc_get_propagator": (C.c_int, [_vp, C.c_int, C.c_int, _dp]),
+    "qoc_pade_histogram": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
+    "qoc_expm_batched": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _ip]),
+    "qoc_expm_jacobian": (C.c_int, [C.c_int, C.c_int, C.c_int, _dp, C.POINTER(_dp), _dp, C.c_int, C.c_double, _dp]),
+}
+
+
+class QOCError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[qoc {code}] {msg}")
+        self.code = code
+
+
+class StaleCacheError(QOCError, ValueError):
+    """Raised like the reference's ``error("Cache data from other control signal u")``."""
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load the HIP library (raises if it was not built — there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise QOCError(QOC_ERR_STATE, f"{LIB_PATH} not built; run __graft_entry__.build()")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, ctx=None) -> None:
+    if rc == QOC_OK:
+        return
+    msg = load().qoc_last_error(ctx).decode(errors="replace")
+    if rc == QOC_ERR_STALE:
+        raise StaleCacheError(rc, msg)
+    raise QOCError(rc, msg)

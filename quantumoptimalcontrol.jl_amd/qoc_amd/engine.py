@@ -1,0 +1,234 @@
+"""Batched GRAPE engine on one MI355X (thin owner of a ``qoc_ctx``).
+
+All heavy state (per-slice propagators U_k, states x_k, co-states λ_k) stays in HBM;
+numpy arrays cross the boundary only for inputs and results, in Julia's memory layout
+(column-major, interleaved complex).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+_dp = C.POINTER(C.c_double)
+
+
+def _cm_complex(a: np.ndarray) -> np.ndarray:
+    """Column-major interleaved complex128 copy (Julia ComplexF64 layout) as a flat array."""
+    a = np.asarray(a, dtype=np.complex128)
+    return np.ascontiguousarray(a.reshape(a.shape[0], -1).T).ravel()
+
+
+def _from_cm(flat: np.ndarray, rows: int, cols: int) -> np.ndarray:
+    return flat.reshape(cols, rows).T.copy()
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_dp)
+
+
+def _u_layout(u: np.ndarray, B: int, nu: int, Nt: int) -> np.ndarray:
+    """(B, nu, Nt) or (nu, Nt) float64 -> contiguous B x (nu x Nt column-major)."""
+    u = np.asarray(u, dtype=np.float64)
+    if u.ndim == 2:
+        u = u[None]
+    if u.shape != (B, nu, Nt):
+        raise ValueError(f"u has shape {u.shape}, expected {(B, nu, Nt)}")
+    return np.ascontiguousarray(np.transpose(u, (0, 2, 1)))
+
+
+class GrapeEngine:
+    """B seeds sharing (A0, A_j, x0, target) on ``device`` (precision 'fp64' | 'fp32')."""
+
+    def __init__(self, A0, A, x0, Nt: int, B: int = 1, precision: str = "fp64", device: int = 0):
+        lib = L.load()
+        A0 = np.asarray(A0, dtype=np.complex128)
+        x0 = np.asarray(x0, dtype=np.complex128)
+        if x0.ndim == 1:
+            x0 = x0[:, None]
+        self.N = A0.shape[0]
+        if x0.shape[0] != self.N:
+            raise ValueError("Error when creating cache, A0 and x0 have incompatiable dimensions")
+        self.m = x0.shape[1]
+        self.nu = len(A)
+        self.Nt = int(Nt)
+        self.B = int(B)
+        self.precision = precision
+        self.device = device
+        prec = {"fp64": L.QOC_FP64, "fp32": L.QOC_FP32}[precision]
+        h = C.c_void_p()
+        L.check(lib.qoc_create(C.byref(h), device, self.N, self.m, self.nu, self.Nt, self.B, prec))
+        self._h = h
+        self._lib = lib
+        self._gen_key = None
+        self.set_generators(A0, A)
+        self.set_x0(x0)
+        self.cost_kind = None
+
+    # ---- lifetime ----------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.qoc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        L.check(rc, self._h)
+
+    # ---- configuration -----------------------------------------------------------
+    def set_generators(self, A0, A):
+        A0 = np.asarray(A0, dtype=np.complex128)
+        key = (A0.tobytes(), tuple(np.asarray(a, dtype=np.complex128).tobytes() for a in A))
+        if key == self._gen_key:
+            return
+        if len(A) != self.nu:
+            raise ValueError(f"expected {self.nu} control generators, got {len(A)}")
+        a0 = _cm_complex(A0).view(np.float64)
+        aj = [_cm_complex(a).view(np.float64) for a in A]
+        arr = (_dp * self.nu)(*[_ptr(a) for a in aj])
+        self._chk(self._lib.qoc_set_generators(self._h, _ptr(a0), arr))
+        self._gen_key = key
+
+    def set_x0(self, x0, per_seed: bool = False):
+        x0 = np.asarray(x0, dtype=np.complex128)
+        if per_seed:
+            flat = np.concatenate([_cm_complex(x) for x in x0]).view(np.float64)
+        else:
+            if x0.ndim == 1:
+                x0 = x0[:, None]
+            flat = _cm_complex(x0).view(np.float64)
+        self._chk(self._lib.qoc_set_x0(self._h, _ptr(flat), int(per_seed)))
+        self.x0 = x0
+
+    def set_cost_trace(self, x_target, n=None):
+        xt = np.asarray(x_target, dtype=np.complex128)
+        if xt.ndim == 1:
+            xt = xt[:, None]
+        n = xt.shape[1] if n is None else n
+        flat = _cm_complex(xt).view(np.float64)
+        self._chk(self._lib.qoc_set_cost(self._h, L.QOC_COST_TRACE, _ptr(flat), float(n)))
+        self.cost_kind = "trace"
+
+    def set_cost_zcalibrated(self, x_target):
+        flat = _cm_complex(x_target).view(np.float64)
+        self._chk(self._lib.qoc_set_cost(self._h, L.QOC_COST_ZCAL, _ptr(flat), 4.0))
+        self.cost_kind = "zcal"
+
+    def set_cost_external(self):
+        self._chk(self._lib.qoc_set_cost(self._h, L.QOC_COST_EXTERNAL, None, 1.0))
+        self.cost_kind = "external"
+
+    def set_state_penalty(self, inds_penalty, inds_css, mu):
+        P = np.ascontiguousarray(inds_penalty, dtype=np.int32)
+        Cc = np.ascontiguousarray(inds_css, dtype=np.int32)
+        ip = C.POINTER(C.c_int)
+        self._chk(self._lib.qoc_set_state_penalty(self._h, P.ctypes.data_as(ip), len(P), Cc.ctypes.data_as(ip),
+                                                  len(Cc), float(mu)))
+
+    # ---- hot path (host arrays) ---------------------------------------------------
+    def propagate(self, u) -> np.ndarray:
+        """Forward pass for all seeds; returns J (B,) = Jfinal(x_N) + sum_k L(x_k)."""
+        ub = _u_layout(u, self.B, self.nu, self.Nt)
+        J = np.zeros(self.B)
+        self._chk(self._lib.qoc_propagate(self._h, _ptr(ub), _ptr(J)))
+        return J
+
+    def grape_sensitivity(self, u, order: int = 3, lambda_final=None) -> np.ndarray:
+        """dJdu (B, nu, Nt); raises StaleCacheError unless u is the last propagated u."""
+        ub = _u_layout(u, self.B, self.nu, self.Nt)
+        lam = None
+        if lambda_final is not None:
+            lf = np.asarray(lambda_final, dtype=np.complex128)
+            if lf.ndim == 2:
+                lf = lf[None]
+            lam = np.concatenate([_cm_complex(x) for x in lf]).view(np.float64)
+        out = np.zeros((self.B, self.Nt, self.nu))
+        self._chk(self._lib.qoc_grape_sensitivity(self._h, _ptr(ub), int(order),
+                                                  _ptr(lam) if lam is not None else None, _ptr(out)))
+        return np.transpose(out, (0, 2, 1)).copy()
+
+    # ---- hot path (device pointers, e.g. torch tensors on cuda) ---------------------
+    def eval_device(self, d_u: int, order: int, d_J: int, d_dJdu: int):
+        """f + f_grad on device-resident buffers (B x Nt x nu doubles in, B / B x Nt x nu out)."""
+        self._chk(self._lib.qoc_eval_dev(self._h, C.c_void_p(d_u), int(order), C.c_void_p(d_J),
+                                         C.c_void_p(d_dJdu)))
+
+    def propagate_device(self, d_u: int, d_J: int):
+        self._chk(self._lib.qoc_propagate_dev(self._h, C.c_void_p(d_u), C.c_void_p(d_J)))
+
+    def grape_sensitivity_device(self, d_u: int, order: int, d_dJdu: int):
+        self._chk(self._lib.qoc_grape_sensitivity_dev(self._h, C.c_void_p(d_u), int(order), C.c_void_p(d_dJdu)))
+
+    def stream(self) -> int:
+        return self._lib.qoc_stream(self._h)
+
+    def synchronize(self):
+        self._chk(self._lib.qoc_synchronize(self._h))
+
+    # ---- readback -------------------------------------------------------------------
+    def state(self, k: int, seed: int = 0) -> np.ndarray:
+        buf = np.zeros(2 * self.N * self.m)
+        self._chk(self._lib.qoc_get_states(self._h, seed, k, _ptr(buf)))
+        return _from_cm(buf.view(np.complex128), self.N, self.m)
+
+    def costate(self, k: int, seed: int = 0) -> np.ndarray:
+        buf = np.zeros(2 * self.N * self.m)
+        self._chk(self._lib.qoc_get_costates(self._h, seed, k, _ptr(buf)))
+        return _from_cm(buf.view(np.complex128), self.N, self.m)
+
+    def propagator(self, k: int, seed: int = 0) -> np.ndarray:
+        buf = np.zeros(2 * self.N * self.N)
+        self._chk(self._lib.qoc_get_propagator(self._h, seed, k, _ptr(buf)))
+        return _from_cm(buf.view(np.complex128), self.N, self.N)
+
+    def pade_histogram(self, reset: bool = False) -> dict:
+        h = np.zeros(5 * 64, dtype=np.int64)
+        self._chk(self._lib.qoc_pade_histogram(self._h, h.ctypes.data_as(C.POINTER(C.c_longlong)), int(reset)))
+        out = {}
+        for di, d in enumerate((3, 5, 7, 9, 13)):
+            for s in range(64):
+                if h[di * 64 + s]:
+                    out[(d, s)] = int(h[di * 64 + s])
+        return out
+
+
+def expm(A, precision: str = "fp64", device: int = 0, return_degrees: bool = False):
+    """Batched exponential!(A, ExpMethodHigham2005()) on the GPU; A is (N,N) or (count,N,N)."""
+    lib = L.load()
+    A = np.asarray(A, dtype=np.complex128)
+    single = A.ndim == 2
+    if single:
+        A = A[None]
+    cnt, N, _ = A.shape
+    flat = np.concatenate([_cm_complex(a) for a in A]).view(np.float64)
+    out = np.zeros_like(flat)
+    deg = np.zeros(cnt, dtype=np.int32)
+    sq = np.zeros(cnt, dtype=np.int32)
+    ip = C.POINTER(C.c_int)
+    L.check(lib.qoc_expm_batched(device, N, cnt, {"fp64": L.QOC_FP64, "fp32": L.QOC_FP32}[precision],
+                                 _ptr(flat), _ptr(out), deg.ctypes.data_as(ip), sq.ctypes.data_as(ip)))
+    X = np.stack([_from_cm(x, N, N) for x in out.view(np.complex128).reshape(cnt, N * N)])
+    X = X[0] if single else X
+    return (X, deg, sq) if return_degrees else X
+
+
+def expm_jacobian(A0, A, p, order=2, dt=1.0, device: int = 0) -> list:
+    """expm_jacobian! (src/gradient_computations.jl:177-213) on the GPU; returns nu N x N matrices."""
+    lib = L.load()
+    A0 = np.asarray(A0, dtype=np.complex128)
+    N = A0.shape[0]
+    nu = len(A)
+    a0 = _cm_complex(A0).view(np.float64)
+    aj = [_cm_complex(a).view(np.float64) for a in A]
+    arr = (_dp * nu)(*[_ptr(a) for a in aj])
+    pp = np.ascontiguousarray(p, dtype=np.float64)
+    out = np.zeros(2 * N * N * nu)
+    L.check(lib.qoc_expm_jacobian(device, N, nu, _ptr(a0), arr, _ptr(pp), int(order), float(dt), _ptr(out)))
+    return [_from_cm(x, N, N) for x in out.view(np.complex128).reshape(nu, N * N)]
