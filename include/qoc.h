@@ -85,6 +85,12 @@ int qoc_get_propagator(qoc_ctx* ctx, int seed, int k, double* U_out);   /* Uk_ve
  * hist[di*64 + s], di = index of degree in {3,5,7,9,13}.  Used for the FLOP accounting. */
 int qoc_pade_histogram(qoc_ctx* ctx, long long* hist, int reset);
 
+/* Live per-kernel timing: when enabled, hipEvents are recorded on qoc_stream around each hot-path
+ * kernel (phase 0 k_expm, 1 k_chain_fwd, 2 k_chain_bwd, 3 k_grad).  qoc_phase_times synchronises the
+ * stream and returns the accumulated milliseconds and launch counts per phase. */
+int qoc_set_profiling(qoc_ctx* ctx, int enable);
+int qoc_phase_times(qoc_ctx* ctx, double* ms_out /*[4]*/, long long* launches_out /*[4]*/, int reset);
+
 /* Standalone ops on the same kernels. */
 /* exponential!(A, ExpMethodHigham2005()) for `count` independent N x N matrices
  * (src/gradient_computations.jl:24, third-party ExponentialUtilities). */

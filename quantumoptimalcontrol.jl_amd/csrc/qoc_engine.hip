@@ -50,6 +50,16 @@ struct qoc_ctx {
   double* d_stage = nullptr;             // host->device staging (fp64 complex), max(B*N*m, (nu+1)*N*N)*2
   size_t stage_elems = 0;
   std::vector<double> h_u;
+  // live per-kernel timing (hipEvents recorded on `stream` around each hot-path launch)
+  bool profiling = false;
+  struct Mark {
+    int phase;
+    hipEvent_t a, b;
+  };
+  std::vector<Mark> marks;
+  std::vector<hipEvent_t> event_pool;
+  double phase_ms[4] = {0, 0, 0, 0};
+  long long phase_n[4] = {0, 0, 0, 0};
   bool have_gen = false, have_x0 = false, have_cost = false, have_prop = false;
   std::string err;
 };
@@ -159,17 +169,44 @@ size_t grad_lds(const qoc_ctx* c, int order) {
   return (size_t)(c->N * (c->N + 1) + 2 * order * c->N * c->m) * c->esz + 64 * sizeof(double);
 }
 
+hipEvent_t take_event(qoc_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// RAII-less bracket: mark_begin returns the index of the pending mark, mark_end records its stop event.
+int mark_begin(qoc_ctx* c, int phase) {
+  if (!c->profiling) return -1;
+  qoc_ctx::Mark m{phase, take_event(c), take_event(c)};
+  (void)hipEventRecord(m.a, c->stream);
+  c->marks.push_back(m);
+  return (int)c->marks.size() - 1;
+}
+void mark_end(qoc_ctx* c, int idx) {
+  if (idx >= 0) (void)hipEventRecord(c->marks[idx].b, c->stream);
+}
+
 template <typename T>
 int run_forward(qoc_ctx* c) {
+  int mk = mark_begin(c, 0);
   hipError_t e = launch_expm(c->prec, c->stream, c->N, c->nu, c->B * c->Nt, c->d_A, c->d_u, nullptr, c->d_U,
                              c->d_hist, nullptr, nullptr);
+  mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm launch: %s", hipGetErrorString(e));
   const size_t lds = chain_lds(c);
   HIPCHK(c, hipFuncSetAttribute((const void*)k_chain_fwd<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  mk = mark_begin(c, 1);
   hipLaunchKernelGGL((k_chain_fwd<T>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
                      (const cx<T>*)c->d_U, (const cx<T>*)c->d_x0, c->x0_per_seed, (cx<T>*)c->d_X,
                      (const cx<T>*)c->d_Xt, c->cost_kind, c->cost_n, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu,
                      c->d_J, c->d_coef);
+  mark_end(c, mk);
   HIPCHK(c, hipGetLastError());
   return QOC_OK;
 }
@@ -178,14 +215,18 @@ template <typename T>
 int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
   size_t lds = chain_lds(c);
   HIPCHK(c, hipFuncSetAttribute((const void*)k_chain_bwd<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int mk = mark_begin(c, 2);
   hipLaunchKernelGGL((k_chain_bwd<T>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
                      (const cx<T>*)c->d_U, (const cx<T>*)c->d_X, (cx<T>*)c->d_L, (const cx<T>*)c->d_Xt, c->cost_kind,
                      (const cx<double>*)c->d_coef, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu);
+  mark_end(c, mk);
   HIPCHK(c, hipGetLastError());
   lds = grad_lds(c, order);
   HIPCHK(c, hipFuncSetAttribute((const void*)k_grad<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  mk = mark_begin(c, 3);
   hipLaunchKernelGGL((k_grad<T>), dim3(c->B * c->Nt), dim3(GRAD_THREADS), lds, c->stream, c->N, c->m, c->nu, c->Nt,
                      order, (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, d_dJdu);
+  mark_end(c, mk);
   HIPCHK(c, hipGetLastError());
   return QOC_OK;
 }
@@ -272,6 +313,11 @@ void qoc_destroy(qoc_ctx* c) {
                   c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage};
   for (void* p : ptrs)
     if (p) hipFree(p);
+  for (auto& m : c->marks) {
+    hipEventDestroy(m.a);
+    hipEventDestroy(m.b);
+  }
+  for (auto e : c->event_pool) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -473,6 +519,35 @@ int qoc_get_propagator(qoc_ctx* c, int seed, int k, double* U_out) {
   HIPCHK(c, hipSetDevice(c->dev));
   const size_t NN = (size_t)c->N * c->N;
   return download(c, (char*)c->d_U + ((size_t)seed * c->Nt + k) * NN * c->esz, U_out, NN);
+}
+
+int qoc_set_profiling(qoc_ctx* c, int enable) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  c->profiling = enable != 0;
+  return QOC_OK;
+}
+
+int qoc_phase_times(qoc_ctx* c, double* ms_out, long long* launches_out, int reset) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (auto& m : c->marks) {
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, m.a, m.b));
+    c->phase_ms[m.phase] += ms;
+    c->phase_n[m.phase] += 1;
+    c->event_pool.push_back(m.a);
+    c->event_pool.push_back(m.b);
+  }
+  c->marks.clear();
+  for (int p = 0; p < 4; ++p) {
+    if (ms_out) ms_out[p] = c->phase_ms[p];
+    if (launches_out) launches_out[p] = c->phase_n[p];
+    if (reset) {
+      c->phase_ms[p] = 0;
+      c->phase_n[p] = 0;
+    }
+  }
+  return QOC_OK;
 }
 
 int qoc_pade_histogram(qoc_ctx* c, long long* hist, int reset) {

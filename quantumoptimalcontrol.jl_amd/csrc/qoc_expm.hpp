@@ -3,19 +3,40 @@
 // Replaces ExponentialUtilities.exponential!(Ak, ExpMethodHigham2005(), cache)
 // called per time slice at src/gradient_computations.jl:17-25 (A_k formation :18-22).
 //
-// One workgroup (4 waves) per (seed, slice) unit.  Everything stays in LDS:
-//   * A_k = A0 + sum_j u[j,k] A_j is formed in LDS (planar re/im, column-major, ld = N),
-//   * ||A_k||_1 selects the Padé degree / squarings exactly as Higham (2005),
-//   * the Padé GEMMs run on v_mfma_f64_16x16x4_f64 (fp64) / v_mfma_f32_16x16x4_f32 (fp32),
-//     each wave owning a fixed set of 16x16 output tiles, complex = 4 real MFMAs,
-//   * (V-U) X = (V+U) is solved by a register-resident LU with partial pivoting
-//     (lane = row, wave = column mod 4, one workgroup barrier per pivot step with
-//     look-ahead pivot search) followed by a wave-local back substitution,
-//   * squarings reuse the GEMM, and U_k is written once to HBM (interleaved, column-major).
+// One workgroup (4 waves) per (seed, slice) unit, everything LDS-resident in THREE
+// N x N planar (re | im, column-major, ld = N) buffers so that two workgroups share a CU
+// at N = 40 in fp64:
+//   * A_k = A0 + sum_j u[j,k] A_j is formed in LDS; ||A_k||_1 selects the Padé degree /
+//     squarings exactly as Higham (2005) / LinearAlgebra.exp!;
+//   * the Padé GEMMs run on v_mfma_f64_16x16x4_f64 (fp64) or v_mfma_f32_16x16x4_f32
+//     (fp32): each wave owns fixed 16x16 output tiles, complex = 4 real MFMAs, operand
+//     fragments for k-step k+1 are fetched while k-step k is in the matrix pipe;
+//   * (V-U) X = (V+U) is solved by a blocked LU with partial pivoting (LAPACK gesv's
+//     |re|+|im| rule): 16-column panels are factored register-resident (lane = row,
+//     one barrier per pivot, DPP argmax, look-ahead), the trailing rank-16 updates and the
+//     blocked back substitution run on MFMA;
+//   * squarings reuse the GEMM; U_k is written once to HBM (interleaved, column-major).
 #pragma once
 #include "qoc_common.hpp"
 
 namespace qoc {
+
+// Diagnostic phase stamps (built only with -DQOC_PROBE by tools/; never in the product library).
+#ifdef QOC_PROBE
+__device__ unsigned long long g_probe[64];
+#define QOC_STAMP(i)                                                            \
+  do {                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+    unsigned long long t_;                                                      \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+    if (blockIdx.x == 7 && threadIdx.x == 0) g_probe[i] = t_;                   \
+  } while (0)
+#else
+#define QOC_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
 
 __constant__ double kPade3[4] = {120.0, 60.0, 12.0, 1.0};
 __constant__ double kPade5[6] = {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0};
@@ -31,12 +52,22 @@ __device__ __forceinline__ int degree_index(int d) {
   return d == 3 ? 0 : d == 5 ? 1 : d == 7 ? 2 : d == 9 ? 3 : 4;
 }
 
+// Wave-wide max of an unsigned key (DPP row shifts + row broadcasts), result uniform.
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 template <typename T, int NT>
 struct Expm {
-  static constexpr int NW = 4;                       // waves per workgroup
-  static constexpr int NMAX = 16 * NT;               // largest N for this instantiation
-  static constexpr int MT = (NT * NT + NW - 1) / NW; // output tiles per wave
-  static constexpr int NCW = (2 * NMAX + NW - 1) / NW;  // LU columns ([Q|P]) per wave
+  static constexpr int NW = 4;                        // waves per workgroup
+  static constexpr int NMAX = 16 * NT;                // largest N for this instantiation
+  static constexpr int MT = NT == 3 ? 3 : (NT * NT + NW - 1) / NW;  // Padé output tiles per wave
   using M = MF<T>;
   using v4 = typename M::v4;
 
@@ -45,58 +76,86 @@ struct Expm {
   };
 
   static __host__ __device__ size_t lds_bytes(int N) {
-    size_t b = (size_t)5 * 2 * N * N * sizeof(T);
+    size_t b = (size_t)3 * 2 * N * N * sizeof(T);
     b = (b + 15) & ~(size_t)15;
-    b += 2 * NMAX * sizeof(cx<T>);  // LU multipliers (double buffered)
-    b += (NMAX + 4) * sizeof(int);  // pivot rows
-    b += 8 * sizeof(double);        // reductions
+    b += (size_t)6 * N * sizeof(cx<T>);  // Gauss-Jordan pivot row / column broadcast (double buffered)
+    b += (2 * NMAX + 8) * sizeof(int);    // pivot rows + row positions
+    b += 16 * sizeof(double);             // reductions
     return (b + 15) & ~(size_t)15;
   }
 
-  // ---- tile geometry -------------------------------------------------------
-  static __device__ __forceinline__ bool owns(int q, int wave) { return wave + q * NW < NT * NT; }
-  static __device__ __forceinline__ int trow(int q, int wave, int lane, int i) {
-    const int t = wave + q * NW;
-    return (t / NT) * 16 + M::drow(lane, i);
+  // ---- tile geometry (Padé GEMMs) -------------------------------------------
+  // NT = 3: wave w < 3 owns the whole tile row w (A fragments shared by its 3 tiles), wave 3
+  // has no tile (the critical path is 3 tiles per wave either way).  NT <= 2: one tile per wave.
+  static constexpr bool ROWMAP = NT == 3;
+  static __device__ __forceinline__ bool owns(int q, int wave) {
+    return ROWMAP ? (wave < NT) : (wave + q * NW < NT * NT);
   }
-  static __device__ __forceinline__ int tcol(int q, int wave, int lane) {
-    const int t = wave + q * NW;
-    return (t % NT) * 16 + (lane & 15);
+  static __device__ __forceinline__ int tile_i(int q, int wave) { return ROWMAP ? wave : (wave + q * NW) / NT; }
+  static __device__ __forceinline__ int tile_j(int q, int wave) { return ROWMAP ? q : (wave + q * NW) % NT; }
+  static __device__ __forceinline__ int trow(int q, int wave, int lane, int i) {
+    return tile_i(q, wave) * 16 + M::drow(lane, i);
+  }
+  static __device__ __forceinline__ int tcol(int q, int wave, int lane) { return tile_j(q, wave) * 16 + (lane & 15); }
+
+  struct Frag {
+    T ar[MT], ai[MT], br[MT], bi[MT];
+  };
+
+  // Operand fragments of k-step kk (A rows and B columns of this wave's tiles; zero-padded).
+  static __device__ __forceinline__ void load_frag(int N, int kk, const T* __restrict__ Ar,
+                                                   const T* __restrict__ Ai, const T* __restrict__ Br,
+                                                   const T* __restrict__ Bi, Frag& f, int wave, int lane) {
+    const int li = lane & 15, k = min(kk + (lane >> 4), N - 1);
+    const bool kok = kk + (lane >> 4) < N;
+#pragma unroll
+    for (int q = 0; q < MT; ++q) {
+      const int row = min(tile_i(q, wave) * 16 + li, N - 1), col = min(tile_j(q, wave) * 16 + li, N - 1);
+      const bool aok = kok && tile_i(q, wave) * 16 + li < N, bok = kok && tile_j(q, wave) * 16 + li < N;
+      if (!ROWMAP || q == 0) {
+        const T xr = Ar[row + N * k], xi = Ai[row + N * k];
+        f.ar[q] = aok ? xr : T(0);
+        f.ai[q] = aok ? xi : T(0);
+      } else {
+        f.ar[q] = f.ar[0];
+        f.ai[q] = f.ai[0];
+      }
+      const T yr = Br[k + N * col], yi = Bi[k + N * col];
+      f.br[q] = bok ? yr : T(0);
+      f.bi[q] = bok ? yi : T(0);
+    }
   }
 
-  // ---- C = A * B (complex, operands planar in LDS, result in D-layout registers) ----
+  // C = A * B (complex, operands planar in LDS, result in D-layout registers).  The loads of
+  // k-step k+1 are issued before the MFMAs of k-step k (branch-free, clamped addresses).
   static __device__ __forceinline__ void gemm(int N, const T* __restrict__ Ar, const T* __restrict__ Ai,
-                                              const T* __restrict__ Br, const T* __restrict__ Bi,
-                                              Tiles& C, int wave, int lane) {
+                                              const T* __restrict__ Br, const T* __restrict__ Bi, Tiles& C,
+                                              int wave, int lane) {
 #pragma unroll
     for (int q = 0; q < MT; ++q) {
       C.r[q] = v4{0, 0, 0, 0};
       C.i[q] = v4{0, 0, 0, 0};
     }
-    const int li = lane & 15, kq = lane >> 4;
+    if (!owns(0, wave)) return;
+    Frag cur, nxt;
+    load_frag(N, 0, Ar, Ai, Br, Bi, cur, wave, lane);
     for (int kk = 0; kk < N; kk += 4) {
-      const int k = kk + kq;
-      const bool kok = k < N;
+      load_frag(N, kk + 4, Ar, Ai, Br, Bi, nxt, wave, lane);  // harmless clamped reads past the end
 #pragma unroll
       for (int q = 0; q < MT; ++q) {
-        if (owns(q, wave)) {
-          const int t = wave + q * NW;
-          const int row = (t / NT) * 16 + li, col = (t % NT) * 16 + li;
-          T ar = 0, ai = 0, br = 0, bi = 0;
-          if (kok && row < N) {
-            ar = Ar[row + N * k];
-            ai = Ai[row + N * k];
-          }
-          if (kok && col < N) {
-            br = Br[k + N * col];
-            bi = Bi[k + N * col];
-          }
-          C.r[q] = M::mma(ar, br, C.r[q]);
-          C.i[q] = M::mma(ar, bi, C.i[q]);
-          C.r[q] = M::mma(-ai, bi, C.r[q]);
-          C.i[q] = M::mma(ai, br, C.i[q]);
+        if (ROWMAP || owns(q, wave)) {
+          C.r[q] = M::mma(cur.ar[q], cur.br[q], C.r[q]);
+          C.i[q] = M::mma(cur.ar[q], cur.bi[q], C.i[q]);
         }
       }
+#pragma unroll
+      for (int q = 0; q < MT; ++q) {
+        if (ROWMAP || owns(q, wave)) {
+          C.r[q] = M::mma(-cur.ai[q], cur.bi[q], C.r[q]);
+          C.i[q] = M::mma(cur.ai[q], cur.br[q], C.i[q]);
+        }
+      }
+      cur = nxt;
     }
   }
 
@@ -117,7 +176,7 @@ struct Expm {
     }
   }
 
-  // dst = a*X + b*I   (X in registers)
+  // dst = a*X + b*I
   static __device__ __forceinline__ void axpi(Tiles& dst, T a, const Tiles& X, T b, int wave, int lane) {
 #pragma unroll
     for (int q = 0; q < MT; ++q) {
@@ -145,149 +204,427 @@ struct Expm {
       }
     }
   }
-  // dst += a*Y (Y planar in LDS, read at D-layout positions)
-  static __device__ __forceinline__ void axpy_lds(int N, Tiles& dst, T a, const T* Yr, const T* Yi, int wave,
-                                                  int lane) {
+
+  // ---- A_k = A0 + sum_j u_j A_j, scaled by 2^-s, into planar LDS ----------------
+  static __device__ __forceinline__ void form_A(int N, int nu, int unit, const cx<T>* __restrict__ Agen,
+                                                const double* __restrict__ u, const cx<T>* __restrict__ Ain,
+                                                T* Ar, T* Ai, T scale, int tid) {
+    const int NN = N * N;
+    constexpr int PER = (NMAX * NMAX + 255) / 256;
+    cx<T> a[PER];
+    if (Agen) {
 #pragma unroll
-    for (int q = 0; q < MT; ++q) {
-      if (owns(q, wave)) {
-        const int col = tcol(q, wave, lane);
+      for (int r = 0; r < PER; ++r) {
+        const int e = tid + 256 * r;
+        if (e < NN) a[r] = Agen[e];
+      }
+      for (int j = 0; j < nu; ++j) {
+        const T uj = (T)u[(size_t)unit * nu + j];
+        const cx<T>* G = Agen + (size_t)(j + 1) * NN;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = trow(q, wave, lane, i);
-          if (row < N && col < N) {
-            dst.r[q][i] += a * Yr[row + N * col];
-            dst.i[q][i] += a * Yi[row + N * col];
+        for (int r = 0; r < PER; ++r) {
+          const int e = tid + 256 * r;
+          if (e < NN) {
+            const cx<T> g = G[e];
+            a[r].r += uj * g.r;
+            a[r].i += uj * g.i;
           }
         }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < PER; ++r) {
+        const int e = tid + 256 * r;
+        if (e < NN) a[r] = Ain[(size_t)unit * NN + e];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      const int e = tid + 256 * r;
+      if (e < NN) {
+        Ar[e] = a[r].r * scale;
+        Ai[e] = a[r].i * scale;
       }
     }
   }
 
-  // ---- LU solve of Q X = P (Q, P planar in LDS); X written planar to (Xr, Xi) ----
-  // Partial pivoting with LAPACK's izamax rule (|re|+|im|, first maximum), like gesv.
-  static __device__ void pivot_search(int N, cx<T> v, bool pivoted, int p, cx<T>* lbuf, int* rplist, int lane) {
-    double a = (lane < N && !pivoted) ? (double)(fabs(v.r) + fabs(v.i)) : -1.0;
-    int idx = lane;
+  // ---- Gauss-Jordan without interchanges (fast path) -----------------------------
+  // Used when Q is strictly column diagonally dominant: partial pivoting (gesv) then performs
+  // no row interchanges and elimination without pivoting is backward stable (growth <= 2), so
+  // the result equals the pivoted solve to rounding.  [Q | P] is register-tiled in 2D:
+  // thread (rg = tid & 7, cg = tid >> 3) owns rows rg + 8a and columns cg + 32b, so each step
+  // needs only RA + CB broadcast values (pivot row + multiplier column, double-buffered in LDS)
+  // and one workgroup barrier.
+  static constexpr int RA = (NMAX + 7) / 8;
+  static constexpr int CB = (2 * NMAX + 31) / 32;
+
+  static __device__ __forceinline__ bool col_dominant(int N, const T* Qr, const T* Qi, int tid) {
+    bool ok = true;
+    const int c = tid >> 2, part = tid & 3;
+    double off = 0.0, dg = 0.0;
+    if (c < N)
+      for (int i = part; i < N; i += 4) {
+        const double xr = Qr[i + N * c], xi = Qi[i + N * c];
+        const double a = sqrt(xr * xr + xi * xi);
+        if (i == c)
+          dg = a;
+        else
+          off += a;
+      }
+    off += __shfl_xor(off, 1);
+    off += __shfl_xor(off, 2);
+    dg += __shfl_xor(dg, 1);
+    dg += __shfl_xor(dg, 2);
+    if (c < N) ok = dg > off;
+    return __syncthreads_and(ok) != 0;
+  }
+
+  static __device__ __forceinline__ void gj_solve(int N, const T* Qr, const T* Qi, const T* Pr, const T* Pi, T* Xr,
+                                                  T* Xi, cx<T>* scratch, int tid) {
+    const int rg = tid & 7, cg = tid >> 3;
+    cx<T> m[RA][CB];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double oa = __shfl_xor(a, off);
-      const int oi = __shfl_xor(idx, off);
-      if (oa > a || (oa == a && oi < idx)) {
-        a = oa;
-        idx = oi;
+    for (int a = 0; a < RA; ++a)
+#pragma unroll
+      for (int b = 0; b < CB; ++b) {
+        const int r = rg + 8 * a, c = cg + 32 * b;
+        m[a][b] = cx<T>{0, 0};
+        if (r < N && c < 2 * N) {
+          const T* cr = c < N ? Qr + N * c : Pr + N * (c - N);
+          const T* ci = c < N ? Qi + N * c : Pi + N * (c - N);
+          m[a][b] = cx<T>{cr[r], ci[r]};
+        }
+      }
+    cx<T>* rowb = scratch;       // 2 x 2N
+    cx<T>* colb = rowb + 4 * N;  // 2 x N
+    if (rg == 0)
+#pragma unroll
+      for (int b = 0; b < CB; ++b) {
+        const int c = cg + 32 * b;
+        if (c < 2 * N) rowb[c] = m[0][b];
+      }
+    if (cg == 0)
+#pragma unroll
+      for (int a = 0; a < RA; ++a) {
+        const int r = rg + 8 * a;
+        if (r < N) colb[r] = m[a][0];
+      }
+    cx<T> dinv[RA];  // 1 / pivot of each owned row (the row is never normalised in place)
+#pragma unroll
+    for (int a = 0; a < RA; ++a) dinv[a] = cx<T>{0, 0};
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int p = 0; p < N; ++p) {
+      __syncthreads();
+      const cx<T>* rb = rowb + (p & 1) * 2 * N;
+      const cx<T>* cb = colb + (p & 1) * N;
+      // all broadcast reads first (clamped indices, no branches) -> one LDS round trip
+      const cx<T> pv = rb[p];
+      cx<T> cv[RA], rv[CB];
+#pragma unroll
+      for (int a = 0; a < RA; ++a) cv[a] = cb[min(rg + 8 * a, N - 1)];
+#pragma unroll
+      for (int b = 0; b < CB; ++b) rv[b] = rb[min(cg + 32 * b, 2 * N - 1)];
+      const cx<T> inv = cinv(pv);
+      cx<T> l[RA];
+#pragma unroll
+      for (int a = 0; a < RA; ++a) {
+        const int r = rg + 8 * a;
+        const bool act = r < N && r != p;
+        const cx<T> t = cmul(cv[a], inv);
+        l[a].r = act ? t.r : T(0);
+        l[a].i = act ? t.i : T(0);
+        if (r == p) dinv[a] = inv;
+      }
+#pragma unroll
+      for (int b = 0; b < CB; ++b) {
+        // column groups of this wave are cg in [8 wv, 8 wv + 8): skip columns that are all done
+        if (8 * wv + 7 + 32 * b > p) {
+          const int c = cg + 32 * b;
+          const bool act = c < 2 * N && c > p;
+          const T ur = act ? rv[b].r : T(0), ui = act ? rv[b].i : T(0);
+#pragma unroll
+          for (int a = 0; a < RA; ++a) {
+            m[a][b].r -= l[a].r * ur - l[a].i * ui;
+            m[a][b].i -= l[a].r * ui + l[a].i * ur;
+          }
+        }
+      }
+      const int pn = p + 1;
+      if (pn < N) {
+        cx<T>* rbn = rowb + (pn & 1) * 2 * N;
+        cx<T>* cbn = colb + (pn & 1) * N;
+        if (rg == (pn & 7)) {
+          const int an = pn >> 3;
+#pragma unroll
+          for (int a = 0; a < RA; ++a)
+            if (a == an)
+#pragma unroll
+              for (int b = 0; b < CB; ++b) {
+                const int c = cg + 32 * b;
+                if (c < 2 * N) rbn[c] = m[a][b];
+              }
+        }
+        if (cg == (pn & 31)) {
+          const int bn = pn >> 5;
+#pragma unroll
+          for (int b = 0; b < CB; ++b)
+            if (b == bn)
+#pragma unroll
+              for (int a = 0; a < RA; ++a) {
+                const int r = rg + 8 * a;
+                if (r < N) cbn[r] = m[a][b];
+              }
+        }
       }
     }
-    const int r = __builtin_amdgcn_readfirstlane(idx);
+#pragma unroll
+    for (int a = 0; a < RA; ++a)
+#pragma unroll
+      for (int b = 0; b < CB; ++b) {
+        const int r = rg + 8 * a, c = cg + 32 * b;
+        if (r < N && c >= N && c < 2 * N) {
+          const cx<T> x = cmul(m[a][b], dinv[a]);
+          Xr[r + N * (c - N)] = x.r;
+          Xi[r + N * (c - N)] = x.i;
+        }
+      }
+    __syncthreads();
+  }
+
+  // ---- LU with partial pivoting -----------------------------------------------
+  // Row r of the combined matrix [Q | P] stays in place (physical row); rplist[p] is the
+  // pivot row chosen at step p and pos[r] the step at which row r was chosen.
+  static __device__ __forceinline__ T* colr(int N, T* Qr, T* Pr, int c) { return c < N ? Qr + N * c : Pr + N * (c - N); }
+
+  // Owner wave of column p: pick the pivot among rows not yet chosen and publish multipliers.
+  static __device__ __forceinline__ void pivot_search(int N, cx<T> v, bool piv, int p, int c0, cx<T>* Lp,
+                                                      int* rplist, int* pos, int lane) {
+    const float a = (float)(fabs(v.r) + fabs(v.i));
+    const unsigned key = (lane < N && !piv) ? __float_as_uint(a) + 1u : 0u;
+    const unsigned mx = wave_max_u32(key);
+    const unsigned long long hit = __ballot(key == mx);
+    const int r = (int)__builtin_ctzll(hit);
     cx<T> d;
     d.r = bcast(v.r, r);
     d.i = bcast(v.i, r);
     const cx<T> inv = cinv(d);
     cx<T> l = {0, 0};
-    if (lane < N && !pivoted && lane != r) l = cmul(v, inv);
-    if (lane < NMAX) lbuf[(p & 1) * NMAX + lane] = l;
-    if (lane == 0) rplist[p] = r;
+    if (lane < N && !piv && lane != r) l = cmul(v, inv);
+    if (lane < N) Lp[(p - c0) * N + lane] = l;
+    if (lane == 0) {
+      rplist[p] = r;
+      pos[r] = p;
+    }
   }
 
-  static __device__ void lu_solve(int N, T* Qr, T* Qi, const T* Pr, const T* Pi, T* Xr, T* Xi, cx<T>* lbuf,
-                                  int* rplist, int wave, int lane) {
-    T mr[NCW], mi[NCW];
+  static __device__ __forceinline__ void lu_solve(int N, T* Qr, T* Qi, T* Pr, T* Pi, T* Xr, T* Xi, int* rplist,
+                                                  int* pos, int wave, int lane, int tid) {
+    cx<T>* Lp = reinterpret_cast<cx<T>*>(Xr);  // panel multipliers (w x N), X buffer unused until back-subst
+    for (int r = tid; r < N; r += 256) pos[r] = 1 << 30;
+    __syncthreads();
+    for (int c0 = 0; c0 < N; c0 += 16) {
+      const int c1 = min(N, c0 + 16), w = c1 - c0;
+      // ---------------- panel factorization (register resident) ----------------
+      T mr[4], mi[4];
 #pragma unroll
-    for (int q = 0; q < NCW; ++q) {
-      const int c = wave + NW * q;
-      T vr = 0, vi = 0;
-      if (lane < N) {
-        if (c < N) {
-          vr = Qr[lane + N * c];
-          vi = Qi[lane + N * c];
-        } else if (c < 2 * N) {
-          vr = Pr[lane + N * (c - N)];
-          vi = Pi[lane + N * (c - N)];
+      for (int q = 0; q < 4; ++q) {
+        const int c = c0 + wave + NW * q;
+        mr[q] = mi[q] = T(0);
+        if (c < c1 && lane < N) {
+          mr[q] = Qr[lane + N * c];
+          mi[q] = Qi[lane + N * c];
         }
       }
-      mr[q] = vr;
-      mi[q] = vi;
-    }
-    bool pivoted = false;
-    int mypos = 1 << 30;
-    if (wave == 0) pivot_search(N, cx<T>{mr[0], mi[0]}, false, 0, lbuf, rplist, lane);
-
-    for (int p = 0; p < N; ++p) {
-      __syncthreads();
-      const int r = __builtin_amdgcn_readfirstlane(rplist[p]);
-      cx<T> l = {0, 0};
-      if (lane < NMAX) l = lbuf[(p & 1) * NMAX + lane];
-      if (lane == r) {
-        pivoted = true;
-        mypos = p;
-      }
-      const int pn = p + 1;
-      const bool look = (pn < N) && (wave == (pn & 3));
-      const int qn = pn >> 2;
-      if (look) {
-        cx<T> v = {0, 0};
+      bool piv = lane < N ? (pos[lane] < c0) : true;
+      QOC_STAMP(10 + (c0 >> 4) * 4);
+      if (wave == 0) pivot_search(N, cx<T>{mr[0], mi[0]}, piv, c0, c0, Lp, rplist, pos, lane);
+      for (int p = c0; p < c1; ++p) {
+        __syncthreads();
+        const int r = __builtin_amdgcn_readfirstlane(rplist[p]);
+        cx<T> l = {0, 0};
+        if (lane < N) l = Lp[(p - c0) * N + lane];
+        if (lane == r) piv = true;
+        const int pn = p + 1;
+        const bool look = (pn < c1) && (wave == ((pn - c0) & 3));
+        const int qn = (pn - c0) >> 2;
+        if (look) {
 #pragma unroll
-        for (int q = 0; q < NCW; ++q) {
-          if (q == qn) {
+          for (int q = 0; q < 4; ++q) {
+            if (q == qn) {
+              const T pr = bcast(mr[q], r), pi = bcast(mi[q], r);
+              mr[q] -= l.r * pr - l.i * pi;
+              mi[q] -= l.r * pi + l.i * pr;
+              pivot_search(N, cx<T>{mr[q], mi[q]}, piv, pn, c0, Lp, rplist, pos, lane);
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = c0 + wave + NW * q;
+          if (c > p && c < c1 && !(look && q == qn)) {
             const T pr = bcast(mr[q], r), pi = bcast(mi[q], r);
             mr[q] -= l.r * pr - l.i * pi;
             mi[q] -= l.r * pi + l.i * pr;
-            v.r = mr[q];
-            v.i = mi[q];
-          }
-        }
-        pivot_search(N, v, pivoted, pn, lbuf, rplist, lane);
-      }
-#pragma unroll
-      for (int q = 0; q < NCW; ++q) {
-        const int c = wave + NW * q;
-        if (c > p && c < 2 * N && !(look && q == qn)) {
-          const T pr = bcast(mr[q], r), pi = bcast(mi[q], r);
-          mr[q] -= l.r * pr - l.i * pi;
-          mi[q] -= l.r * pi + l.i * pr;
-        }
-      }
-    }
-    // Upper factor to LDS (overwrites Q) for the back substitution.
-#pragma unroll
-    for (int q = 0; q < NCW; ++q) {
-      const int c = wave + NW * q;
-      if (c < N && lane < N) {
-        Qr[lane + N * c] = mr[q];
-        Qi[lane + N * c] = mi[q];
-      }
-    }
-    __syncthreads();
-    // Wave-local back substitution on this wave's right-hand-side columns.
-    for (int p = N - 1; p >= 0; --p) {
-      const int r = __builtin_amdgcn_readfirstlane(rplist[p]);
-      cx<T> d = {Qr[r + N * p], Qi[r + N * p]};
-      const cx<T> inv = cinv(d);
-      cx<T> uc = {0, 0};
-      if (lane < N) uc = cx<T>{Qr[lane + N * p], Qi[lane + N * p]};
-      const bool upd = mypos < p;
-#pragma unroll
-      for (int q = 0; q < NCW; ++q) {
-        const int c = wave + NW * q;
-        if (c >= N && c < 2 * N) {
-          cx<T> xv = {bcast(mr[q], r), bcast(mi[q], r)};
-          xv = cmul(xv, inv);
-          if (lane == r) {
-            mr[q] = xv.r;
-            mi[q] = xv.i;
-          } else if (upd) {
-            mr[q] -= uc.r * xv.r - uc.i * xv.i;
-            mi[q] -= uc.r * xv.i + uc.i * xv.r;
           }
         }
       }
-    }
 #pragma unroll
-    for (int q = 0; q < NCW; ++q) {
-      const int c = wave + NW * q;
-      if (c >= N && c < 2 * N && lane < N) {
-        Xr[mypos + N * (c - N)] = mr[q];
-        Xi[mypos + N * (c - N)] = mi[q];
+      for (int q = 0; q < 4; ++q) {
+        const int c = c0 + wave + NW * q;
+        if (c < c1 && lane < N) {
+          Qr[lane + N * c] = mr[q];
+          Qi[lane + N * c] = mi[q];
+        }
+      }
+      __syncthreads();
+      QOC_STAMP(11 + (c0 >> 4) * 4);
+      // ---------------- U12 = L11^-1 A12 for this panel's pivot rows ----------------
+      const int ntr = 2 * N - c1;
+      for (int jj = tid; jj < ntr; jj += 256) {
+        T* cr = colr(N, Qr, Pr, c1 + jj);
+        T* ci = colr(N, Qi, Pi, c1 + jj);
+        cx<T> uu[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          if (t < w) {
+            const int rt = rplist[c0 + t];
+            cx<T> acc = {cr[rt], ci[rt]};
+#pragma unroll
+            for (int s = 0; s < t; ++s) {
+              const cx<T> lv = Lp[s * N + rt];
+              acc.r -= lv.r * uu[s].r - lv.i * uu[s].i;
+              acc.i -= lv.r * uu[s].i + lv.i * uu[s].r;
+            }
+            uu[t] = acc;
+            cr[rt] = acc.r;
+            ci[rt] = acc.i;
+          }
+        }
+      }
+      __syncthreads();
+      QOC_STAMP(12 + (c0 >> 4) * 4);
+      // ---------------- trailing rank-w update on MFMA ----------------
+      if (ntr > 0) {
+        const int nct = (ntr + 15) >> 4;
+        for (int t = wave; t < NT * nct; t += NW) {
+          const int ti = t % NT, tc = t / NT;
+          const int rowA = ti * 16 + (lane & 15);
+          const bool rowok = rowA < N && pos[rowA] >= c1;
+          const int colB = c1 + tc * 16 + (lane & 15);
+          const bool colok = colB < 2 * N;
+          const T* bcr = colr(N, Qr, Pr, colok ? colB : 0);
+          const T* bci = colr(N, Qi, Pi, colok ? colB : 0);
+          v4 accr, acci;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = ti * 16 + M::drow(lane, i);
+            accr[i] = (row < N && colok) ? bcr[row] : T(0);
+            acci[i] = (row < N && colok) ? bci[row] : T(0);
+          }
+          for (int kk = 0; kk < w; kk += 4) {
+            const int s = kk + (lane >> 4);
+            T ar = 0, ai = 0, br = 0, bi = 0;
+            if (s < w) {
+              if (rowok) {
+                const cx<T> lv = Lp[s * N + rowA];
+                ar = -lv.r;
+                ai = -lv.i;
+              }
+              if (colok) {
+                const int rs = rplist[c0 + s];
+                br = bcr[rs];
+                bi = bci[rs];
+              }
+            }
+            accr = M::mma(ar, br, accr);
+            acci = M::mma(ar, bi, acci);
+            accr = M::mma(-ai, bi, accr);
+            acci = M::mma(ai, br, acci);
+          }
+          T* ocr = colr(N, Qr, Pr, colok ? colB : 0);
+          T* oci = colr(N, Qi, Pi, colok ? colB : 0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = ti * 16 + M::drow(lane, i);
+            if (row < N && colok && pos[row] >= c1) {
+              ocr[row] = accr[i];
+              oci[row] = acci[i];
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+    QOC_STAMP(30);
+    // ---------------- blocked back substitution: X = U^-1 Y ----------------
+    for (int kb = (N - 1) >> 4; kb >= 0; --kb) {
+      const int c0 = kb * 16, c1 = min(N, c0 + 16), w = c1 - c0;
+      for (int j = tid; j < N; j += 256) {
+        cx<T> x[16];
+#pragma unroll
+        for (int t = 15; t >= 0; --t) {
+          if (t < w) {
+            const int rt = rplist[c0 + t];
+            cx<T> acc = {Pr[rt + N * j], Pi[rt + N * j]};
+#pragma unroll
+            for (int s = t + 1; s < 16; ++s) {
+              if (s < w) {
+                const cx<T> uv = {Qr[rt + N * (c0 + s)], Qi[rt + N * (c0 + s)]};
+                acc.r -= uv.r * x[s].r - uv.i * x[s].i;
+                acc.i -= uv.r * x[s].i + uv.i * x[s].r;
+              }
+            }
+            const cx<T> dg = {Qr[rt + N * (c0 + t)], Qi[rt + N * (c0 + t)]};
+            x[t] = cmul(acc, cinv(dg));
+            Xr[(c0 + t) + N * j] = x[t].r;
+            Xi[(c0 + t) + N * j] = x[t].i;
+          }
+        }
+      }
+      __syncthreads();
+      if (c0 > 0) {
+        const int nrt = (c0 + 15) >> 4;
+        for (int t = wave; t < nrt * NT; t += NW) {
+          const int ti = t % nrt, tj = t / nrt;
+          const int qA = ti * 16 + (lane & 15);
+          const int rA = qA < c0 ? rplist[qA] : 0;
+          const int col = tj * 16 + (lane & 15);
+          v4 accr, acci;
+          int rowD[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int qD = ti * 16 + M::drow(lane, i);
+            rowD[i] = qD < c0 ? rplist[qD] : -1;
+            accr[i] = (rowD[i] >= 0 && col < N) ? Pr[rowD[i] + N * col] : T(0);
+            acci[i] = (rowD[i] >= 0 && col < N) ? Pi[rowD[i] + N * col] : T(0);
+          }
+          for (int kk = 0; kk < w; kk += 4) {
+            const int s = kk + (lane >> 4);
+            T ar = 0, ai = 0, br = 0, bi = 0;
+            if (s < w) {
+              if (qA < c0) {
+                ar = -Qr[rA + N * (c0 + s)];
+                ai = -Qi[rA + N * (c0 + s)];
+              }
+              if (col < N) {
+                br = Xr[(c0 + s) + N * col];
+                bi = Xi[(c0 + s) + N * col];
+              }
+            }
+            accr = M::mma(ar, br, accr);
+            acci = M::mma(ar, bi, acci);
+            accr = M::mma(-ai, bi, accr);
+            acci = M::mma(ai, br, acci);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (rowD[i] >= 0 && col < N) {
+              Pr[rowD[i] + N * col] = accr[i];
+              Pi[rowD[i] + N * col] = acci[i];
+            }
+          }
+        }
+        __syncthreads();
       }
     }
   }
@@ -297,60 +634,49 @@ struct Expm {
 // The kernel.  unit = blockIdx.x.  Either generators (Agen, u) or explicit matrices (Ain).
 // ---------------------------------------------------------------------------
 template <typename T, int NT>
-__global__ __launch_bounds__(256) void k_expm(int N, int nu, int nunits, const cx<T>* __restrict__ Agen,
-                                              const double* __restrict__ u, const cx<T>* __restrict__ Ain,
-                                              cx<T>* __restrict__ Uout, unsigned long long* __restrict__ hist,
-                                              int* __restrict__ deg_out, int* __restrict__ sq_out) {
+__global__ __launch_bounds__(256, 2) void k_expm(int N, int nu, int nunits, const cx<T>* __restrict__ Agen,
+                                                 const double* __restrict__ u, const cx<T>* __restrict__ Ain,
+                                                 cx<T>* __restrict__ Uout, unsigned long long* __restrict__ hist,
+                                                 int* __restrict__ deg_out, int* __restrict__ sq_out) {
   using E = Expm<T, NT>;
   using Tiles = typename E::Tiles;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int unit = blockIdx.x;
   if (unit >= nunits) return;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int NN = N * N;
+  QOC_STAMP(0);
   T* buf = reinterpret_cast<T*>(smem);
   auto re = [&](int b) { return buf + (size_t)b * 2 * NN; };
   auto im = [&](int b) { return buf + (size_t)b * 2 * NN + NN; };
-  size_t off = ((size_t)5 * 2 * NN * sizeof(T) + 15) & ~(size_t)15;
-  cx<T>* lbuf = reinterpret_cast<cx<T>*>(smem + off);
-  off += 2 * E::NMAX * sizeof(cx<T>);
+  size_t off = ((size_t)3 * 2 * NN * sizeof(T) + 15) & ~(size_t)15;
+  cx<T>* gjs = reinterpret_cast<cx<T>*>(smem + off);
+  off += (size_t)6 * N * sizeof(cx<T>);
   int* rplist = reinterpret_cast<int*>(smem + off);
-  off += (E::NMAX + 4) * sizeof(int);
+  int* pos = rplist + E::NMAX + 4;
+  off += (2 * E::NMAX + 8) * sizeof(int);
   double* red = reinterpret_cast<double*>(smem + ((off + 7) & ~(size_t)7));
 
-  // ---- A_k = A0 + sum_j u[j,k] A_j  (src/gradient_computations.jl:18-22) ----
-  T* Ar = re(0);
-  T* Ai = im(0);
-  for (int e = tid; e < NN; e += 256) {
-    cx<T> a;
-    if (Agen) {
-      a = Agen[e];
-      for (int j = 0; j < nu; ++j) {
-        const T uj = (T)u[(size_t)unit * nu + j];
-        const cx<T> g = Agen[(size_t)(j + 1) * NN + e];
-        a.r += uj * g.r;
-        a.i += uj * g.i;
-      }
-    } else {
-      a = Ain[(size_t)unit * NN + e];
-    }
-    Ar[e] = a.r;
-    Ai[e] = a.i;
-  }
+  // ---- A_k (src/gradient_computations.jl:18-22) and ||A_k||_1 ----
+  E::form_A(N, nu, unit, Agen, u, Ain, re(0), im(0), T(1), tid);
   __syncthreads();
-  // ---- ||A||_1 (max column sum of |a_ij|) ----
-  if (wave == 0) {
+  {
+    // 4 threads per column, then a max over columns.
+    const int c = tid >> 2, part = tid & 3;
     double s = 0.0;
-    if (lane < N)
-      for (int i = 0; i < N; ++i) {
-        const double xr = Ar[i + N * lane], xi = Ai[i + N * lane];
+    if (c < N)
+      for (int i = part; i < N; i += 4) {
+        const double xr = re(0)[i + N * c], xi = im(0)[i + N * c];
         s += sqrt(xr * xr + xi * xi);
       }
-    for (int o = 32; o > 0; o >>= 1) s = fmax(s, __shfl_xor(s, o));
-    if (lane == 0) red[0] = s;
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    for (int o = 4; o < 64; o <<= 1) s = fmax(s, __shfl_xor(s, o));
+    if (lane == 0) red[wave] = s;
   }
   __syncthreads();
-  const double nA = red[0];
+  const double nA = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
   int d, sq = 0;
   if (nA <= 2.1) {
     d = nA > 0.95 ? 9 : nA > 0.25 ? 7 : nA > 0.015 ? 5 : 3;
@@ -364,116 +690,126 @@ __global__ __launch_bounds__(256) void k_expm(int N, int nu, int nunits, const c
     if (deg_out) deg_out[unit] = d;
     if (sq_out) sq_out[unit] = sq;
   }
+  QOC_STAMP(1);
+  const T scale = (T)ldexp(1.0, -sq);
   if (sq > 0) {
-    const T sc = (T)ldexp(1.0, -sq);
     for (int e = tid; e < NN; e += 256) {
-      Ar[e] *= sc;
-      Ai[e] *= sc;
+      re(0)[e] *= scale;
+      im(0)[e] *= scale;
     }
     __syncthreads();
   }
 
   Tiles D, V, Up;
-  int qb, pb;  // LDS buffers holding Q = V-U and P = V+U
   if (d < 13) {
     const double* C = d == 3 ? kPade3 : d == 5 ? kPade5 : d == 7 ? kPade7 : kPade9;
-    E::gemm(N, Ar, Ai, Ar, Ai, D, wave, lane);  // A2
+    QOC_STAMP(20);
+    E::gemm(N, re(0), im(0), re(0), im(0), D, wave, lane);  // A2
+    QOC_STAMP(21);
     E::axpi(V, (T)C[2], D, (T)C[0], wave, lane);
     E::axpi(Up, (T)C[3], D, (T)C[1], wave, lane);
     if (d >= 5) {
-      E::store(N, re(1), im(1), D, wave, lane);
+      E::store(N, re(1), im(1), D, wave, lane);  // A2 -> B1
       __syncthreads();
       E::gemm(N, re(1), im(1), re(1), im(1), D, wave, lane);  // A4
       E::axpy(V, (T)C[4], D, wave);
       E::axpy(Up, (T)C[5], D, wave);
       if (d >= 7) {
-        E::store(N, re(2), im(2), D, wave, lane);
+        E::store(N, re(2), im(2), D, wave, lane);  // A4 -> B2
         __syncthreads();
         E::gemm(N, re(2), im(2), re(1), im(1), D, wave, lane);  // A6 = A4 A2
         E::axpy(V, (T)C[6], D, wave);
         E::axpy(Up, (T)C[7], D, wave);
         if (d >= 9) {
-          E::store(N, re(3), im(3), D, wave, lane);
           __syncthreads();
-          E::gemm(N, re(3), im(3), re(1), im(1), D, wave, lane);  // A8 = A6 A2
+          E::store(N, re(2), im(2), D, wave, lane);  // A6 -> B2
+          __syncthreads();
+          E::gemm(N, re(2), im(2), re(1), im(1), D, wave, lane);  // A8 = A6 A2
           E::axpy(V, (T)C[8], D, wave);
           E::axpy(Up, (T)C[9], D, wave);
         }
       }
+      __syncthreads();
     }
-    E::store(N, re(4), im(4), Up, wave, lane);
+    E::store(N, re(1), im(1), Up, wave, lane);  // U' -> B1
     __syncthreads();
-    E::gemm(N, Ar, Ai, re(4), im(4), D, wave, lane);  // U = A * Up
-    qb = 1;
-    pb = 2;
+    E::gemm(N, re(0), im(0), re(1), im(1), D, wave, lane);  // U = A U'
   } else {
     const double* C = kPade13;
-    E::gemm(N, Ar, Ai, Ar, Ai, D, wave, lane);  // A2
+    E::gemm(N, re(0), im(0), re(0), im(0), D, wave, lane);  // A2
     E::store(N, re(1), im(1), D, wave, lane);
     __syncthreads();
     E::gemm(N, re(1), im(1), re(1), im(1), D, wave, lane);  // A4
     E::store(N, re(2), im(2), D, wave, lane);
     __syncthreads();
-    E::gemm(N, re(2), im(2), re(1), im(1), D, wave, lane);  // A6
-    E::store(N, re(3), im(3), D, wave, lane);
+    E::gemm(N, re(2), im(2), re(1), im(1), D, wave, lane);  // A6 (registers)
     __syncthreads();
-    // T2 = b12 A6 + b10 A4 + b8 A2 -> buf4
-    for (int e = tid; e < NN; e += 256) {
-      re(4)[e] = (T)C[12] * re(3)[e] + (T)C[10] * re(2)[e] + (T)C[8] * re(1)[e];
-      im(4)[e] = (T)C[12] * im(3)[e] + (T)C[10] * im(2)[e] + (T)C[8] * im(1)[e];
+    // element-wise combinations at this wave's own tile positions (in place, no hazards)
+#pragma unroll
+    for (int q = 0; q < E::MT; ++q) {
+      if (E::owns(q, wave)) {
+        const int col = E::tcol(q, wave, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = E::trow(q, wave, lane, i);
+          const T dlt = row == col ? T(1) : T(0);
+          if (row < N && col < N) {
+            const int e = row + N * col;
+            const T a2r = re(1)[e], a2i = im(1)[e], a4r = re(2)[e], a4i = im(2)[e];
+            const T a6r = D.r[q][i], a6i = D.i[q][i];
+            re(1)[e] = (T)C[13] * a6r + (T)C[11] * a4r + (T)C[9] * a2r;  // T1 -> B1
+            im(1)[e] = (T)C[13] * a6i + (T)C[11] * a4i + (T)C[9] * a2i;
+            re(2)[e] = (T)C[12] * a6r + (T)C[10] * a4r + (T)C[8] * a2r;  // T2 -> B2
+            im(2)[e] = (T)C[12] * a6i + (T)C[10] * a4i + (T)C[8] * a2i;
+            V.r[q][i] = (T)C[6] * a6r + (T)C[4] * a4r + (T)C[2] * a2r + (T)C[0] * dlt;
+            V.i[q][i] = (T)C[6] * a6i + (T)C[4] * a4i + (T)C[2] * a2i;
+            Up.r[q][i] = (T)C[7] * a6r + (T)C[5] * a4r + (T)C[3] * a2r + (T)C[1] * dlt;
+            Up.i[q][i] = (T)C[7] * a6i + (T)C[5] * a4i + (T)C[3] * a2i;
+          }
+        }
+      }
     }
+    E::store(N, re(0), im(0), D, wave, lane);  // A6 -> B0 (A is re-formed below)
     __syncthreads();
-    E::gemm(N, re(3), im(3), re(4), im(4), V, wave, lane);  // A6 T2
-    E::axpy_lds(N, V, (T)C[6], re(3), im(3), wave, lane);
-    E::axpy_lds(N, V, (T)C[4], re(2), im(2), wave, lane);
-    E::axpy_lds(N, V, (T)C[2], re(1), im(1), wave, lane);
-    {
-      Tiles Z;
-      E::axpi(Z, (T)0, V, (T)C[0], wave, lane);  // Z = b0 I (V*0 + b0 I)
-      E::axpy(V, (T)1, Z, wave);
-    }
+    E::gemm(N, re(0), im(0), re(2), im(2), D, wave, lane);  // A6 T2
+    E::axpy(V, (T)1, D, wave);
+    E::gemm(N, re(0), im(0), re(1), im(1), D, wave, lane);  // A6 T1
+    E::axpy(Up, (T)1, D, wave);
     __syncthreads();
-    // T1 = b13 A6 + b11 A4 + b9 A2 -> buf4
-    for (int e = tid; e < NN; e += 256) {
-      re(4)[e] = (T)C[13] * re(3)[e] + (T)C[11] * re(2)[e] + (T)C[9] * re(1)[e];
-      im(4)[e] = (T)C[13] * im(3)[e] + (T)C[11] * im(2)[e] + (T)C[9] * im(1)[e];
-    }
+    E::store(N, re(1), im(1), Up, wave, lane);                       // U' -> B1
+    E::form_A(N, nu, unit, Agen, u, Ain, re(0), im(0), scale, tid);  // A -> B0 again
     __syncthreads();
-    E::gemm(N, re(3), im(3), re(4), im(4), Up, wave, lane);  // A6 T1
-    E::axpy_lds(N, Up, (T)C[7], re(3), im(3), wave, lane);
-    E::axpy_lds(N, Up, (T)C[5], re(2), im(2), wave, lane);
-    E::axpy_lds(N, Up, (T)C[3], re(1), im(1), wave, lane);
-    {
-      Tiles Z;
-      E::axpi(Z, (T)0, Up, (T)C[1], wave, lane);
-      E::axpy(Up, (T)1, Z, wave);
-    }
-    __syncthreads();
-    E::store(N, re(1), im(1), Up, wave, lane);
-    __syncthreads();
-    E::gemm(N, Ar, Ai, re(1), im(1), D, wave, lane);  // U = A * Up
-    qb = 2;
-    pb = 3;
+    E::gemm(N, re(0), im(0), re(1), im(1), D, wave, lane);  // U = A U'
   }
-  // Q = V - U, P = V + U (D-layout, own tiles), to LDS.
+  QOC_STAMP(2);
+  // Q = V - U -> B2 (free), then P = V + U -> B0 once every wave is done reading B0/B1.
   {
-    Tiles Q = V, P = V;
+    Tiles Q = V;
     E::axpy(Q, (T)-1, D, wave);
-    E::axpy(P, (T)1, D, wave);
-    E::store(N, re(qb), im(qb), Q, wave, lane);
-    E::store(N, re(pb), im(pb), P, wave, lane);
+    E::store(N, re(2), im(2), Q, wave, lane);
+    E::axpy(V, (T)1, D, wave);
   }
   __syncthreads();
-  E::lu_solve(N, re(qb), im(qb), re(pb), im(pb), Ar, Ai, lbuf, rplist, wave, lane);
+  E::store(N, re(0), im(0), V, wave, lane);
   __syncthreads();
+  QOC_STAMP(3);
+  if (E::col_dominant(N, re(2), im(2), tid)) {
+    E::gj_solve(N, re(2), im(2), re(0), im(0), re(1), im(1), gjs, tid);
+  } else {
+    E::lu_solve(N, re(2), im(2), re(0), im(0), re(1), im(1), rplist, pos, wave, lane, tid);
+  }
+  QOC_STAMP(5);
+  // X in B1; squarings
   for (int s = 0; s < sq; ++s) {
-    E::gemm(N, Ar, Ai, Ar, Ai, D, wave, lane);
+    E::gemm(N, re(1), im(1), re(1), im(1), D, wave, lane);
     __syncthreads();
-    E::store(N, Ar, Ai, D, wave, lane);
+    E::store(N, re(1), im(1), D, wave, lane);
     __syncthreads();
   }
+  QOC_STAMP(6);
   cx<T>* out = Uout + (size_t)unit * NN;
-  for (int e = tid; e < NN; e += 256) out[e] = cx<T>{Ar[e], Ai[e]};
+  for (int e = tid; e < NN; e += 256) out[e] = cx<T>{re(1)[e], im(1)[e]};
+  QOC_STAMP(7);
 }
 
 }  // namespace qoc

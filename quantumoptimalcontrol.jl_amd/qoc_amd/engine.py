@@ -188,6 +188,19 @@ class GrapeEngine:
         self._chk(self._lib.qoc_get_propagator(self._h, seed, k, _ptr(buf)))
         return _from_cm(buf.view(np.complex128), self.N, self.N)
 
+    PHASES = ("k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad")
+
+    def set_profiling(self, enable: bool = True):
+        self._chk(self._lib.qoc_set_profiling(self._h, int(enable)))
+
+    def phase_times(self, reset: bool = False) -> dict:
+        """{kernel: (total_ms, launches)} from hipEvents recorded on the engine stream."""
+        ms = np.zeros(4)
+        n = np.zeros(4, dtype=np.int64)
+        self._chk(self._lib.qoc_phase_times(self._h, _ptr(ms), n.ctypes.data_as(C.POINTER(C.c_longlong)),
+                                            int(reset)))
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.PHASES)}
+
     def pade_histogram(self, reset: bool = False) -> dict:
         h = np.zeros(5 * 64, dtype=np.int64)
         self._chk(self._lib.qoc_pade_histogram(self._h, h.ctypes.data_as(C.POINTER(C.c_longlong)), int(reset)))

@@ -1,0 +1,35 @@
+"""Multi-GPU epilogue: seeds are sharded contiguously over ranks (one process per GPU); the
+only exchange on the path is an all-gather of each rank's best (J, global seed id)
+(SURVEY.md §8e).  On ROCm ``torch.distributed``'s "nccl" backend is RCCL over xGMI; the same
+code runs on "gloo" for the CPU tests.
+"""
+from __future__ import annotations
+
+
+def shard(B_total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous block of seeds [start, stop) owned by `rank`."""
+    base, rem = divmod(B_total, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def gather_best(J_local, seed_offset: int, out=None):
+    """All-gather (min J, its global seed) over the default process group.
+
+    J_local: 1-D torch tensor of this rank's objectives (any device the backend supports).
+    Returns (J_best, seed_best) as Python numbers; `out` (2*world doubles) may be preallocated.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    jm, idx = torch.min(J_local, 0)
+    mine = torch.stack([jm.to(torch.float64), (idx + seed_offset).to(torch.float64)])
+    if world == 1:
+        return float(mine[0]), int(mine[1])
+    if out is None:
+        out = torch.empty(2 * world, dtype=torch.float64, device=J_local.device)
+    dist.all_gather_into_tensor(out, mine)
+    allv = out.view(world, 2)
+    r = int(torch.argmin(allv[:, 0]))
+    return float(allv[r, 0]), int(allv[r, 1])

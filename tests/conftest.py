@@ -19,3 +19,9 @@ def built_lib():
     g.build_lib()
     from qoc_amd import _lib
     return _lib.load()
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    import pathlib
+    return pathlib.Path(ROOT) / "tests" / "golden"

@@ -1,0 +1,98 @@
+"""CPU tests of the boundary and host logic (no GPU compute calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from qoc_amd import systems as S
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    txt = open(os.path.join(ROOT, "include", "qoc.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(qoc_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_builds_loads_and_exports_every_declared_symbol(built_lib):
+    syms = _declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(built_lib, s), f"{s} declared in include/qoc.h but not exported"
+    from qoc_amd import _lib
+    assert set(_lib.SIGNATURES) == set(syms)
+
+
+def test_last_error_without_context(built_lib):
+    msg = built_lib.qoc_last_error(None)
+    assert isinstance(msg, bytes)
+
+
+def test_create_rejects_bad_dimensions_before_touching_the_gpu(built_lib):
+    h = ctypes.c_void_p()
+    rc = built_lib.qoc_create(ctypes.byref(h), 0, 0, 1, 1, 1, 1, 0)
+    assert rc == -1 and not h.value
+    assert b"invalid dimensions" in built_lib.qoc_last_error(None)
+    rc = built_lib.qoc_create(ctypes.byref(h), 0, 200, 1, 1, 1, 1, 0)
+    assert rc == -5  # outside the LDS-resident kernel envelope
+
+
+def test_engine_dimension_mismatch_message(built_lib):
+    from qoc_amd import GrapeEngine
+    with pytest.raises(ValueError, match="incompatiable dimensions"):
+        GrapeEngine(np.eye(4), [np.eye(4)], np.ones((3, 1)), 10)
+
+
+def test_layout_helpers_are_julia_layout():
+    from qoc_amd.engine import _cm_complex, _from_cm, _u_layout
+    a = np.arange(6).reshape(2, 3) + 1j * np.arange(6).reshape(2, 3)
+    flat = _cm_complex(a)
+    assert np.array_equal(flat, a.ravel(order="F"))
+    assert np.array_equal(_from_cm(flat, 2, 3), a)
+    u = np.arange(2 * 2 * 5, dtype=float).reshape(2, 2, 5)  # B, nu, Nt
+    ub = _u_layout(u, 2, 2, 5)
+    assert ub.ravel()[1 * 10 + 3 * 2 + 1] == u[1, 1, 3]  # u[b*nu*Nt + k*nu + j]
+
+
+def test_quantum_basis_and_operators():
+    qb = S.QuantumBasis([3, 3])
+    assert qb("00") == 0 and qb("01") == 1 and qb("10") == 3 and qb("22") == 8
+    a = S.annihilation_op(4)
+    assert np.allclose(np.diag(a.T @ a), np.arange(4)) and np.allclose(a @ a.T - a.T @ a, np.diag([1, 1, 1, -3]))
+    a1, a2 = S.annihilation_ops(2, 3)
+    assert np.allclose(a1 @ a2, a2 @ a1)
+    assert np.allclose(S.qubit_hamiltonian(1, 0, 5), np.diag(np.arange(5)))
+    assert np.allclose(S.qubit_hamiltonian(0, 1, 5), np.diag([(k - 1) * k / 2 for k in range(5)]))
+
+
+def test_bilinear_matrices_are_skew_hermitian():
+    H0, Tc, _ = S.cavity_model(5)
+    for A in S.setup_bilinear_matrices(H0, Tc, 0.3):
+        assert np.allclose(A, -A.conj().T)
+
+
+def test_spline_matrix():
+    Bs = S.spline_matrix(10.0, 100, 10)
+    assert Bs.shape == (100, 10) and (Bs >= 0).all()
+    # interior cubic B-splines on a uniform grid: each has the same integral
+    assert np.allclose(Bs.sum(0), Bs.sum(0)[0], rtol=1e-2)
+
+
+def test_configs_match_baseline_shapes():
+    for name, (N, m, nu, Nt, B) in {"zz_batch": (9, 4, 2, 500, 512), "cavity": (40, 2, 2, 1000, 256),
+                                    "tunable_bus": (27, 1, 1, 2000, 512)}.items():
+        mk, mu, Bd = S.CONFIGS[name]
+        p = mk()
+        assert (p.N, p.m, p.nu, p.Nt, Bd) == (N, m, nu, Nt, B)
+        assert mu(2).shape == (2, nu, Nt)
+
+
+def test_gate_unitaries():
+    for g in ("CNOT", "iSwap", "CZ"):
+        U = S.gate_unitary(g)
+        assert np.allclose(U @ U.T, np.eye(4))
+    with pytest.raises(ValueError):
+        S.gate_unitary("T")

@@ -1,0 +1,79 @@
+// Diagnostic microbenchmark for k_expm: phase stamps (s_memtime) + wall time per configuration.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -DQOC_PROBE -o tools/expm_probe tools/expm_probe.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <cmath>
+#include "../quantumoptimalcontrol.jl_amd/csrc/qoc_expm.hpp"
+using namespace qoc;
+
+template <int NT>
+void run(int N, double scale, int units) {
+  using E = Expm<double, NT>;
+  std::vector<cx<double>> A((size_t)units * N * N);
+  srand(1);
+  for (int u = 0; u < units; ++u) {
+    // random skew-Hermitian with ||A||_1 ~ scale
+    std::vector<cx<double>> H((size_t)N * N);
+    for (int j = 0; j < N; ++j)
+      for (int i = 0; i <= j; ++i) {
+        double re = rand() / (double)RAND_MAX - 0.5, im = (i == j) ? 0 : rand() / (double)RAND_MAX - 0.5;
+        H[i + N * j] = {re, im};
+        H[j + N * i] = {re, -im};
+      }
+    double nrm = 0;
+    for (int j = 0; j < N; ++j) {
+      double s = 0;
+      for (int i = 0; i < N; ++i) s += std::hypot(H[i + N * j].r, H[i + N * j].i);
+      nrm = std::max(nrm, s);
+    }
+    for (int e = 0; e < N * N; ++e) A[(size_t)u * N * N + e] = {H[e].i * scale / nrm, -H[e].r * scale / nrm};
+  }
+  cx<double>*dA, *dX;
+  (void)hipMalloc(&dA, A.size() * 16);
+  (void)hipMalloc(&dX, A.size() * 16);
+  (void)hipMemcpy(dA, A.data(), A.size() * 16, hipMemcpyHostToDevice);
+  size_t lds = E::lds_bytes(N);
+  (void)hipFuncSetAttribute((const void*)k_expm<double, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  for (int it = 0; it < 3; ++it) {
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL((k_expm<double, NT>), dim3(units), dim3(256), lds, 0, N, 0, units, nullptr, nullptr, dA, dX,
+                       nullptr, nullptr, nullptr);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+  }
+  float ms;
+  (void)hipEventElapsedTime(&ms, a, b);
+  unsigned long long st[64];
+  (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_probe), sizeof(st));
+  printf("N=%d scale=%.3g units=%d lds=%zu  wall %.3f ms  (%.3f us/unit/CU-slot)\n", N, scale, units, lds, ms,
+         ms * 1e3 / units * 256);
+  const char* names[] = {"form+norm", "pade gemms", "Q/P store", "LU solve", "squarings", "store"};
+  int idx[] = {0, 1, 2, 3, 5, 6, 7};
+  for (int i = 0; i < 6; ++i) printf("   %-12s %8llu cycles(memtime)\n", names[i], st[idx[i + 1]] - st[idx[i]]);
+  for (int pn = 0; pn < 3; ++pn)
+    if (st[10 + 4 * pn])
+      printf("   panel %d: factor %llu  U12 %llu  trailing %llu\n", pn, st[11 + 4 * pn] - st[10 + 4 * pn],
+             st[12 + 4 * pn] - st[11 + 4 * pn], (pn < 2 && st[14 + 4 * pn] ? st[14 + 4 * pn] : st[30]) - st[12 + 4 * pn]);
+  printf("   backsub %llu   first GEMM (wave0) %llu\n", st[5] - st[30], st[21] - st[20]);
+  (void)hipMemset(0, 0, 0);
+  {
+    unsigned long long z[64] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_probe), z, sizeof(z));
+  }
+  (void)hipFree(dA);
+  (void)hipFree(dX);
+}
+
+int main(int argc, char** argv) {
+  run<1>(9, 0.1, 256 * 64);
+  run<2>(27, 30.0, 256 * 64);
+  run<3>(40, 0.5, 256 * 64);
+  run<3>(40, 0.5, 256);  // one workgroup per CU: uncontended phase costs
+  run<3>(40, 4.0, 256 * 16);
+  return 0;
+}
