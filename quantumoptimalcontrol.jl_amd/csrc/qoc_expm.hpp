@@ -391,6 +391,170 @@ struct Expm {
     __syncthreads();
   }
 
+  // ---- block Gauss-Jordan on MFMA (fast path for NT >= 2) ---------------------------
+  // [Q | P] lives in MFMA accumulator tiles (D layout) for the whole solve.  Pivots are taken in
+  // blocks of 4 (no interchanges: Q column diagonally dominant).  Per block: the owners publish
+  // the 4 panel columns and the 4 pivot rows to LDS, every thread solves D W = R for its own
+  // column(s) (W = the new pivot rows), and the rank-4 update M -= Panel' W is a single K = 4
+  // MFMA step per tile.  Two barriers per block instead of one per pivot with VALU updates.
+  static constexpr int NTC = (2 * NMAX + 15) / 16;           // column tiles of [Q | P]
+  static constexpr int MG = (NT * NTC + NW - 1) / NW;         // GJ tiles per wave
+
+  static __device__ __forceinline__ void gj_mfma(int N, const T* Qr, const T* Qi, const T* Pr, const T* Pi, T* Xr,
+                                                 T* Xi, cx<T>* scr, int wave, int lane, int tid) {
+    const int ntc = (2 * N + 15) >> 4, ntile = NT * ntc;
+    v4 ar[MG], ai[MG];
+#pragma unroll
+    for (int q = 0; q < MG; ++q) {
+      const int t = wave + NW * q;
+      const int ti = t % NT, tj = t / NT, col = tj * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = ti * 16 + M::drow(lane, i);
+        T vr = 0, vi = 0;
+        if (t < ntile && row < N && col < 2 * N) {
+          vr = col < N ? Qr[row + N * col] : Pr[row + N * (col - N)];
+          vi = col < N ? Qi[row + N * col] : Pi[row + N * (col - N)];
+        }
+        ar[q][i] = vr;
+        ai[q][i] = vi;
+      }
+    }
+    __syncthreads();  // Q / P buffers are dead from here on: scratch may overlap them
+    cx<T>* Pn = scr;          // N x 4 panel (column-major)
+    cx<T>* W = scr + 4 * N;   // 4 x 2N pivot rows -> D^-1 R
+    const int N2 = 2 * N;
+    for (int p0 = 0; p0 < N; p0 += 4) {
+      const int w = min(4, N - p0);
+      if (p0 == 20) QOC_STAMP(40);
+      // 1. publish panel columns [p0, p0+w) and pivot rows [p0, p0+w): only the tile column /
+      //    tile row that holds them (wave-uniform tests), one register per pivot-row tile.
+      const int tb = p0 >> 4;
+#pragma unroll
+      for (int q = 0; q < MG; ++q) {
+        const int t = wave + NW * q;
+        if (t < ntile) {
+          const int ti = t % NT, tj = t / NT, col = tj * 16 + (lane & 15);
+          if (tj == tb && col >= p0 && col < p0 + w) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int row = ti * 16 + M::drow(lane, i);
+              if (row < N) Pn[(col - p0) * N + row] = cx<T>{ar[q][i], ai[q][i]};
+            }
+          }
+          if (ti == tb && col < N2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int row = ti * 16 + M::drow(lane, i);
+              if (row >= p0 && row < p0 + w) W[(row - p0) * N2 + col] = cx<T>{ar[q][i], ai[q][i]};
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (p0 == 20) QOC_STAMP(41);
+      // 2. W = D^-1 R for the live columns (each thread its own columns; D read by broadcast)
+      for (int c = p0 + w + tid; c < N2; c += 256) {
+        cx<T> d[4][4], r[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          r[a] = a < w ? W[a * N2 + c] : cx<T>{0, 0};
+#pragma unroll
+          for (int b = 0; b < 4; ++b) d[a][b] = (a < w && b < w) ? Pn[b * N + p0 + a] : cx<T>{a == b ? T(1) : T(0), 0};
+        }
+        // forward elimination without interchanges, then back substitution (w <= 4)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const cx<T> inv = cinv(d[k][k]);
+#pragma unroll
+          for (int a = k + 1; a < 4; ++a) {
+            const cx<T> l = cmul(d[a][k], inv);
+#pragma unroll
+            for (int b = k + 1; b < 4; ++b) {
+              d[a][b].r -= l.r * d[k][b].r - l.i * d[k][b].i;
+              d[a][b].i -= l.r * d[k][b].i + l.i * d[k][b].r;
+            }
+            r[a].r -= l.r * r[k].r - l.i * r[k].i;
+            r[a].i -= l.r * r[k].i + l.i * r[k].r;
+          }
+          d[k][k] = inv;  // keep the reciprocal for the back substitution
+        }
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+          cx<T> acc = r[k];
+#pragma unroll
+          for (int b = k + 1; b < 4; ++b) {
+            acc.r -= d[k][b].r * r[b].r - d[k][b].i * r[b].i;
+            acc.i -= d[k][b].r * r[b].i + d[k][b].i * r[b].r;
+          }
+          r[k] = cmul(acc, d[k][k]);
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+          if (a < w) W[a * N2 + c] = r[a];
+      }
+      __syncthreads();
+      if (p0 == 20) QOC_STAMP(42);
+      // 3. rank-w update on MFMA; pivot rows become W
+      const int s = lane >> 4;
+#pragma unroll
+      for (int q = 0; q < MG; ++q) {
+        const int t = wave + NW * q;
+        if (t < ntile) {
+          const int ti = t % NT, tj = t / NT;
+          if (tj * 16 + 15 >= p0 + w) {
+            const int rowA = ti * 16 + (lane & 15), colB = tj * 16 + (lane & 15);
+            T xr = 0, xi = 0, yr = 0, yi = 0;
+            if (s < w && rowA < N && (rowA < p0 || rowA >= p0 + w)) {
+              const cx<T> v = Pn[s * N + rowA];
+              xr = -v.r;
+              xi = -v.i;
+            }
+            if (s < w && colB >= p0 + w && colB < N2) {
+              const cx<T> v = W[s * N2 + colB];
+              yr = v.r;
+              yi = v.i;
+            }
+            ar[q] = M::mma(xr, yr, ar[q]);
+            ai[q] = M::mma(xr, yi, ai[q]);
+            ar[q] = M::mma(-xi, yi, ar[q]);
+            ai[q] = M::mma(xi, yr, ai[q]);
+            if (ti == tb) {
+              const int col = tj * 16 + (lane & 15);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int row = ti * 16 + M::drow(lane, i);
+                if (row >= p0 && row < p0 + w && col >= p0 + w && col < N2) {
+                  const cx<T> v = W[(row - p0) * N2 + col];
+                  ar[q][i] = v.r;
+                  ai[q][i] = v.i;
+                }
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (p0 == 20) QOC_STAMP(43);
+    }
+#pragma unroll
+    for (int q = 0; q < MG; ++q) {
+      const int t = wave + NW * q;
+      if (t < ntile) {
+        const int ti = t % NT, tj = t / NT, col = tj * 16 + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = ti * 16 + M::drow(lane, i);
+          if (row < N && col >= N && col < N2) {
+            Xr[row + N * (col - N)] = ar[q][i];
+            Xi[row + N * (col - N)] = ai[q][i];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
   // ---- LU with partial pivoting -----------------------------------------------
   // Row r of the combined matrix [Q | P] stays in place (physical row); rplist[p] is the
   // pivot row chosen at step p and pos[r] the step at which row r was chosen.
@@ -794,7 +958,10 @@ __global__ __launch_bounds__(256, 2) void k_expm(int N, int nu, int nunits, cons
   __syncthreads();
   QOC_STAMP(3);
   if (E::col_dominant(N, re(2), im(2), tid)) {
-    E::gj_solve(N, re(2), im(2), re(0), im(0), re(1), im(1), gjs, tid);
+    if (NT >= 2)  // scratch (12 N complex) inside the dead Q buffer B2
+      E::gj_mfma(N, re(2), im(2), re(0), im(0), re(1), im(1), reinterpret_cast<cx<T>*>(re(2)), wave, lane, tid);
+    else
+      E::gj_solve(N, re(2), im(2), re(0), im(0), re(1), im(1), gjs, tid);
   } else {
     E::lu_solve(N, re(2), im(2), re(0), im(0), re(1), im(1), rplist, pos, wave, lane, tid);
   }

@@ -59,7 +59,8 @@ void run(int N, double scale, int units) {
     if (st[10 + 4 * pn])
       printf("   panel %d: factor %llu  U12 %llu  trailing %llu\n", pn, st[11 + 4 * pn] - st[10 + 4 * pn],
              st[12 + 4 * pn] - st[11 + 4 * pn], (pn < 2 && st[14 + 4 * pn] ? st[14 + 4 * pn] : st[30]) - st[12 + 4 * pn]);
-  printf("   backsub %llu   first GEMM (wave0) %llu\n", st[5] - st[30], st[21] - st[20]);
+  printf("   first GEMM (wave0) %llu   GJ block p0=20: publish %llu  W %llu  mfma %llu\n", st[21] - st[20],
+         st[41] - st[40], st[42] - st[41], st[43] - st[42]);
   (void)hipMemset(0, 0, 0);
   {
     unsigned long long z[64] = {0};
