@@ -14,11 +14,17 @@
 // registers while the current matvec runs.
 #pragma once
 #include "qoc_common.hpp"
+#include "qoc_expm.hpp"  // QOC_STAMP (diagnostic builds only)
 
 namespace qoc {
 
 constexpr int CHAIN_THREADS = 256;
-constexpr int CHAIN_PREF = 16;  // max U elements per thread prefetched (N*N <= 4096)
+// U elements prefetched per thread: N*N <= 256*PREF (fp32 N <= 64; fp64 N <= 45, which covers the
+// fp64 k_expm envelope N <= 44).  Larger fp64 arrays were not promoted to registers (scratch).
+template <typename T>
+struct ChainPref {
+  static constexpr int value = sizeof(T) == 8 ? 8 : 16;
+};
 
 enum { COST_TRACE = 0, COST_ZCAL = 1, COST_EXTERNAL = 2 };
 
@@ -78,26 +84,72 @@ __device__ inline void optimal_calibration(const cx<double> m[4], double tol, do
   *th1 = pm + al * xm;
 }
 
-// Cooperative copy of an N x N column-major complex matrix into LDS with leading dimension N+1.
+// Cooperative copy of an N x N column-major complex matrix into LDS with leading dimension N+1,
+// staged through registers (separate re/im scalars, unconditional clamped loads: a conditionally
+// written array of 16-byte structs was demoted to scratch by the compiler).
 template <typename T>
-__device__ __forceinline__ void prefetch_u(const cx<T>* __restrict__ src, int NN, cx<T> (&pre)[CHAIN_PREF]) {
+struct UPref {
+  T r[ChainPref<T>::value], i[ChainPref<T>::value];
+};
+template <typename T>
+__device__ __forceinline__ void prefetch_u(const cx<T>* __restrict__ src, int NN, UPref<T>& pre) {
 #pragma unroll
-  for (int r = 0; r < CHAIN_PREF; ++r) {
-    const int e = threadIdx.x + CHAIN_THREADS * r;
-    if (e < NN) pre[r] = src[e];
+  for (int r = 0; r < ChainPref<T>::value; ++r) {
+    const int e = min((int)threadIdx.x + CHAIN_THREADS * r, NN - 1);
+    const cx<T> v = src[e];
+    pre.r[r] = v.r;
+    pre.i[r] = v.i;
   }
 }
 template <typename T>
-__device__ __forceinline__ void commit_u(cx<T>* __restrict__ dst, int N, const cx<T> (&pre)[CHAIN_PREF]) {
+__device__ __forceinline__ void commit_u(cx<T>* __restrict__ dst, int N, const UPref<T>& pre) {
   const int NN = N * N;
 #pragma unroll
-  for (int r = 0; r < CHAIN_PREF; ++r) {
+  for (int r = 0; r < ChainPref<T>::value; ++r) {
     const int e = threadIdx.x + CHAIN_THREADS * r;
     if (e < NN) {
-      const int i = e % N, j = e / N;
-      dst[i + (N + 1) * j] = pre[r];
+      const int j = e / N, i = e - j * N;
+      dst[i + (N + 1) * j] = cx<T>{pre.r[r], pre.i[r]};
     }
   }
+}
+
+// Lanes cooperating on one output of the matvec: largest power of two S with S * Nm <= 256
+// (adjacent lanes of one wave, reduced with shuffles).
+__device__ __forceinline__ int chain_split(int Nm) {
+  int S = 1;
+  while (S < 8 && 2 * S * Nm <= CHAIN_THREADS) S <<= 1;
+  return S;
+}
+
+// y[i,c] = sum_j M(i,j) v[j,c] for this thread's (output, part); CONJT selects M = U^H.
+template <typename T, bool CONJT>
+__device__ __forceinline__ cx<T> chain_dot(const cx<T>* __restrict__ Um, const cx<T>* __restrict__ v, int N, int i,
+                                           int part, int S) {
+  cx<T> a0 = {0, 0}, a1 = {0, 0}, a2 = {0, 0}, a3 = {0, 0};
+  const int LD = N + 1;
+  int j = part;
+  for (; j + 3 * S < N; j += 4 * S) {
+    if (CONJT) {
+      a0 = cfmaconj(a0, Um[j + LD * i], v[j]);
+      a1 = cfmaconj(a1, Um[j + S + LD * i], v[j + S]);
+      a2 = cfmaconj(a2, Um[j + 2 * S + LD * i], v[j + 2 * S]);
+      a3 = cfmaconj(a3, Um[j + 3 * S + LD * i], v[j + 3 * S]);
+    } else {
+      a0 = cfma(a0, Um[i + LD * j], v[j]);
+      a1 = cfma(a1, Um[i + LD * (j + S)], v[j + S]);
+      a2 = cfma(a2, Um[i + LD * (j + 2 * S)], v[j + 2 * S]);
+      a3 = cfma(a3, Um[i + LD * (j + 3 * S)], v[j + 3 * S]);
+    }
+  }
+  for (; j < N; j += S) a0 = CONJT ? cfmaconj(a0, Um[j + LD * i], v[j]) : cfma(a0, Um[i + LD * j], v[j]);
+  a0.r += a1.r + a2.r + a3.r;
+  a0.i += a1.i + a2.i + a3.i;
+  for (int off = 1; off < S; off <<= 1) {
+    a0.r += __shfl_xor(a0.r, off);
+    a0.i += __shfl_xor(a0.i, off);
+  }
+  return a0;
 }
 
 template <typename T>
@@ -109,11 +161,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
   const int b = blockIdx.x, tid = threadIdx.x;
   const int NN = N * N, Nm = N * m, LDU = N * (N + 1);
   cx<T>* ub = reinterpret_cast<cx<T>*>(smem);  // 2 x N(N+1)
-  cx<T>* xb = ub + 2 * LDU;                     // N*m
-  double* red = reinterpret_cast<double*>(xb + Nm);
+  cx<T>* xb = ub + 2 * LDU;                     // 2 x N*m
+  double* red = reinterpret_cast<double*>(xb + 2 * Nm);
   const cx<T>* Ub = U + (size_t)b * Nt * NN;
   cx<T>* Xb = X + (size_t)b * (Nt + 1) * Nm;
   const cx<T>* x0b = x0 + (x0_per_seed ? (size_t)b * Nm : 0);
+  const int S = chain_split(Nm), part = tid % S, o0 = tid / S, ostride = CHAIN_THREADS / S;
   double pen = 0.0;
   for (int o = tid; o < Nm; o += CHAIN_THREADS) {
     const cx<T> v = x0b[o];
@@ -121,40 +174,52 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
     Xb[o] = v;
     if (pmask && pmask[o]) pen += (double)v.r * v.r + (double)v.i * v.i;
   }
-  cx<T> pre[CHAIN_PREF];
-  prefetch_u(Ub, NN, pre);
-  commit_u(ub, N, pre);
+  // U_k is double-buffered in LDS; the HBM loads run two slices ahead in registers (preA/preB).
+  UPref<T> preA, preB;
+  prefetch_u(Ub, NN, preA);
+  commit_u(ub, N, preA);
+  if (Nt > 1) prefetch_u(Ub + NN, NN, preA);
+  if (Nt > 2) prefetch_u(Ub + 2 * (size_t)NN, NN, preB);
   __syncthreads();
-  for (int k = 0; k < Nt; ++k) {
-    const cx<T>* cur = ub + (k & 1) * LDU;
-    if (k + 1 < Nt) prefetch_u(Ub + (size_t)(k + 1) * NN, NN, pre);
-    cx<T> y[4];
-    int cnt = 0;
-    for (int o = tid; o < Nm; o += CHAIN_THREADS, ++cnt) {
-      const int i = o % N, c = o / N;
-      cx<T> acc = {0, 0};
-      const cx<T>* xc = xb + N * c;
-      for (int j = 0; j < N; ++j) acc = cfma(acc, cur[i + (N + 1) * j], xc[j]);
-      if (cnt < 4) y[cnt] = acc;
-    }
-    __syncthreads();
-    cnt = 0;
-    cx<T>* Xk = Xb + (size_t)(k + 1) * Nm;
-    for (int o = tid; o < Nm; o += CHAIN_THREADS, ++cnt) {
-      const cx<T> v = y[cnt];
-      xb[o] = v;
-      Xk[o] = v;
-      if (pmask && pmask[o]) pen += (double)v.r * v.r + (double)v.i * v.i;
-    }
-    if (k + 1 < Nt) commit_u(ub + ((k + 1) & 1) * LDU, N, pre);
-    __syncthreads();
+#define QOC_FWD_STEP(KK, PNEXT)                                                    \
+  do {                                                                             \
+    const int k_ = (KK);                                                           \
+    if (k_ == 500) QOC_STAMP(50);                                                  \
+    const cx<T>* cur = ub + (k_ & 1) * LDU;                                        \
+    const cx<T>* xc = xb + (k_ & 1) * Nm;                                          \
+    cx<T>* xn = xb + ((k_ + 1) & 1) * Nm;                                          \
+    cx<T>* Xk = Xb + (size_t)(k_ + 1) * Nm;                                        \
+    for (int o = o0; o < Nm; o += ostride) {                                       \
+      const int i = o % N, c = o / N;                                              \
+      const cx<T> y = chain_dot<T, false>(cur, xc + N * c, N, i, part, S);         \
+      if (part == 0) {                                                             \
+        xn[o] = y;                                                                 \
+        Xk[o] = y;                                                                 \
+        if (pmask && pmask[o]) pen += (double)y.r * y.r + (double)y.i * y.i;       \
+      }                                                                            \
+    }                                                                              \
+    if (k_ == 500) QOC_STAMP(51);                                                  \
+    if (k_ + 1 < Nt) commit_u(ub + ((k_ + 1) & 1) * LDU, N, PNEXT);                \
+    if (k_ == 500) QOC_STAMP(52);                                                  \
+    if (k_ + 3 < Nt) prefetch_u(Ub + (size_t)(k_ + 3) * NN, NN, PNEXT);            \
+    if (k_ == 500) QOC_STAMP(53);                                                  \
+    lds_barrier();                                                                 \
+    if (k_ == 500) QOC_STAMP(54);                                                  \
+  } while (0)
+  int k = 0;
+  for (; k + 1 < Nt; k += 2) {
+    QOC_FWD_STEP(k, preA);
+    QOC_FWD_STEP(k + 1, preB);
   }
+  if (k < Nt) QOC_FWD_STEP(k, preA);
+#undef QOC_FWD_STEP
+  const cx<T>* xN = xb + (Nt & 1) * Nm;
   // ---- costs on x_N ----
   const double psum = block_sum(pen, red) * mu;
   if (cost_kind == COST_TRACE) {
     double orr = 0, oii = 0;
     for (int o = tid; o < Nm; o += CHAIN_THREADS) {
-      const cx<T> t = Xt[o], v = xb[o];
+      const cx<T> t = Xt[o], v = xN[o];
       orr += (double)t.r * v.r + (double)t.i * v.i;
       oii += (double)t.r * v.i - (double)t.i * v.r;
     }
@@ -170,7 +235,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
     for (int c = 0; c < 4; ++c) {
       double orr = 0, oii = 0;
       for (int i = tid; i < N; i += CHAIN_THREADS) {
-        const cx<T> t = Xt[i + N * c], v = xb[i + N * c];
+        const cx<T> t = Xt[i + N * c], v = xN[i + N * c];
         orr += (double)t.r * v.r + (double)t.i * v.i;
         oii += (double)t.r * v.i - (double)t.i * v.r;
       }
@@ -189,8 +254,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
                                {(v1.r * em.r - v1.i * em.i) / a1, (v1.r * em.i + v1.i * em.r) / a1},
                                {v2.r / a2, v2.i / a2},
                                {(v2.r * em.r - v2.i * em.i) / a2, (v2.r * em.i + v2.i * em.r) / a2}};
-      const double s = -2.0 * F / 16.0;
-      for (int c = 0; c < 4; ++c) coef[(size_t)b * m + c] = cx<double>{s * g[c].r, s * g[c].i};
+      const double sc = -2.0 * F / 16.0;
+      for (int c = 0; c < 4; ++c) coef[(size_t)b * m + c] = cx<double>{sc * g[c].r, sc * g[c].i};
     }
   } else {
     if (tid == 0) {
@@ -209,12 +274,14 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
   const int b = blockIdx.x, tid = threadIdx.x;
   const int NN = N * N, Nm = N * m, LDU = N * (N + 1);
   cx<T>* ub = reinterpret_cast<cx<T>*>(smem);
-  cx<T>* lb = ub + 2 * LDU;
+  cx<T>* lb = ub + 2 * LDU;  // 2 x N*m
   const cx<T>* Ub = U + (size_t)b * Nt * NN;
   const cx<T>* Xb = X + (size_t)b * (Nt + 1) * Nm;
   cx<T>* Lb = Lam + (size_t)b * (Nt + 1) * Nm;
   const T tmu = (T)(2.0 * mu);
-  // λ_{Nt+1} = dJfinal/dx(x_N) (+ dL/dx(x_N))
+  const int S = chain_split(Nm), part = tid % S, o0 = tid / S, ostride = CHAIN_THREADS / S;
+  // λ_{Nt+1} = dJfinal/dx(x_N) (+ dL/dx(x_N)), stored in buffer (Nt & 1)
+  cx<T>* l0 = lb + (Nt & 1) * Nm;
   for (int o = tid; o < Nm; o += CHAIN_THREADS) {
     cx<T> v;
     if (cost_kind == COST_EXTERNAL) {
@@ -230,41 +297,46 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
       v.r += tmu * xv.r;
       v.i += tmu * xv.i;
     }
-    lb[o] = v;
+    l0[o] = v;
     Lb[(size_t)Nt * Nm + o] = v;
   }
-  cx<T> pre[CHAIN_PREF];
-  prefetch_u(Ub + (size_t)(Nt - 1) * NN, NN, pre);
-  commit_u(ub + ((Nt - 1) & 1) * LDU, N, pre);
+  UPref<T> preA, preB;
+  prefetch_u(Ub + (size_t)(Nt - 1) * NN, NN, preA);
+  commit_u(ub + ((Nt - 1) & 1) * LDU, N, preA);
+  if (Nt > 1) prefetch_u(Ub + (size_t)(Nt - 2) * NN, NN, preA);
+  if (Nt > 2) prefetch_u(Ub + (size_t)(Nt - 3) * NN, NN, preB);
   __syncthreads();
-  for (int k = Nt - 1; k >= 0; --k) {
-    const cx<T>* cur = ub + (k & 1) * LDU;
-    if (k > 0) prefetch_u(Ub + (size_t)(k - 1) * NN, NN, pre);
-    cx<T> y[4];
-    int cnt = 0;
-    for (int o = tid; o < Nm; o += CHAIN_THREADS, ++cnt) {
-      const int i = o % N, c = o / N;
-      cx<T> acc = {0, 0};
-      const cx<T>* lc = lb + N * c;
-      const cx<T>* ucol = cur + (N + 1) * i;  // column i of U_k
-      for (int j = 0; j < N; ++j) acc = cfmaconj(acc, ucol[j], lc[j]);
-      if (pmask && pmask[o]) {
-        const cx<T> xv = Xb[(size_t)k * Nm + o];
-        acc.r += tmu * xv.r;
-        acc.i += tmu * xv.i;
-      }
-      if (cnt < 4) y[cnt] = acc;
-    }
-    __syncthreads();
-    cnt = 0;
-    cx<T>* Lk = Lb + (size_t)k * Nm;
-    for (int o = tid; o < Nm; o += CHAIN_THREADS, ++cnt) {
-      lb[o] = y[cnt];
-      Lk[o] = y[cnt];
-    }
-    if (k > 0) commit_u(ub + ((k - 1) & 1) * LDU, N, pre);
-    __syncthreads();
+#define QOC_BWD_STEP(KK, PNEXT)                                                    \
+  do {                                                                             \
+    const int k_ = (KK);                                                           \
+    const cx<T>* cur = ub + (k_ & 1) * LDU;                                        \
+    const cx<T>* lc = lb + ((k_ + 1) & 1) * Nm;                                    \
+    cx<T>* ln = lb + (k_ & 1) * Nm;                                                \
+    cx<T>* Lk = Lb + (size_t)k_ * Nm;                                              \
+    for (int o = o0; o < Nm; o += ostride) {                                       \
+      const int i = o % N, c = o / N;                                              \
+      cx<T> y = chain_dot<T, true>(cur, lc + N * c, N, i, part, S);                \
+      if (part == 0) {                                                             \
+        if (pmask && pmask[o]) {                                                   \
+          const cx<T> xv = Xb[(size_t)k_ * Nm + o];                                \
+          y.r += tmu * xv.r;                                                       \
+          y.i += tmu * xv.i;                                                       \
+        }                                                                          \
+        ln[o] = y;                                                                 \
+        Lk[o] = y;                                                                 \
+      }                                                                            \
+    }                                                                              \
+    if (k_ > 0) commit_u(ub + ((k_ - 1) & 1) * LDU, N, PNEXT);                     \
+    if (k_ >= 3) prefetch_u(Ub + (size_t)(k_ - 3) * NN, NN, PNEXT);                \
+    lds_barrier();                                                                 \
+  } while (0)
+  int k = Nt - 1;
+  for (; k >= 1; k -= 2) {
+    QOC_BWD_STEP(k, preA);
+    QOC_BWD_STEP(k - 1, preB);
   }
+  if (k == 0) QOC_BWD_STEP(0, preA);
+#undef QOC_BWD_STEP
 }
 
 // ---------------------------------------------------------------------------

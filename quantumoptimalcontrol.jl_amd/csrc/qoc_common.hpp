@@ -71,6 +71,15 @@ __device__ __forceinline__ double bcast(double v, int l) {
 }
 __device__ __forceinline__ int bcast(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations, not for its
+// outstanding global loads/stores (a __syncthreads() fence would drain vmcnt every step and
+// serialise the HBM prefetch of the next propagators behind the barrier).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Block-wide sum of a double over blockDim.x threads (<= 1024); result valid in all threads.
 __device__ __forceinline__ double block_sum(double v, double* scratch) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);

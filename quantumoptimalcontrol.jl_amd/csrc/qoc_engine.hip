@@ -163,7 +163,7 @@ int download(qoc_ctx* ctx, const void* dev, double* host, size_t nelem) {
 }
 
 size_t chain_lds(const qoc_ctx* c) {
-  return (size_t)(2 * c->N * (c->N + 1) + c->N * c->m) * c->esz + 64 * sizeof(double);
+  return (size_t)(2 * c->N * (c->N + 1) + 2 * c->N * c->m) * c->esz + 64 * sizeof(double);
 }
 size_t grad_lds(const qoc_ctx* c, int order) {
   return (size_t)(c->N * (c->N + 1) + 2 * order * c->N * c->m) * c->esz + 64 * sizeof(double);
@@ -257,7 +257,8 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   if (N < 1 || m < 1 || nu < 1 || Nt < 1 || B < 1)
     return fail(nullptr, QOC_ERR_ARG, "invalid dimensions N=%d m=%d nu=%d Nt=%d B=%d", N, m, nu, Nt, B);
   if (precision != QOC_FP64 && precision != QOC_FP32) return fail(nullptr, QOC_ERR_ARG, "invalid precision");
-  if (!expm_supported(N, precision) || N > kChainMaxN || N * m > 4 * CHAIN_THREADS)
+  if (!expm_supported(N, precision) || N > kChainMaxN || N * N > CHAIN_THREADS * (precision == QOC_FP64 ? 8 : 16) ||
+      N * m > 4 * CHAIN_THREADS)
     return fail(nullptr, QOC_ERR_UNSUPPORTED, "N=%d m=%d outside the LDS-resident kernel envelope", N, m);
   qoc_ctx* c = new qoc_ctx();
   c->dev = device;
