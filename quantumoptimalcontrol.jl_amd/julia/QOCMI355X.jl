@@ -1,0 +1,153 @@
+# QOCMI355X.jl — ccall shim that routes QuantumOptimalControl.jl's PWC GRAPE hot path to
+# libqoc_mi355x.so (C ABI: include/qoc.h).  Nothing else in the reference changes: the Ipopt
+# callbacks (examples/ipopt_callbacks_exp.jl) keep calling `QuantumOptimalControl.propagate`
+# and `grape_sensitivity`; only the `setup_grape_cache` line constructs an `MI355XCache`.
+#
+#   cache = QOCMI355X.setup_grape_cache(A0Δt, complex(x0), (2, segment_count))
+#   x     = QuantumOptimalControl.propagate(A0Δt, [A1Δt, A2Δt], u, x0, cache)      # method below
+#   dJdu  = QuantumOptimalControl.grape_sensitivity(A0Δt, [A1Δt, A2Δt], dJfinal_dx, cache.u, x0, cache;
+#                                                   dUkdp_order=3, dL_dx=dL_dx)
+#
+# Memory layout needs no conversion: Matrix{ComplexF64} is column-major interleaved (re, im),
+# exactly the ABI's layout; u / dJdu are Matrix{Float64} (nu x Nt).
+module QOCMI355X
+
+import QuantumOptimalControl
+const QOC = QuantumOptimalControl
+
+const libqoc = get(ENV, "QOC_MI355X_LIB", joinpath(@__DIR__, "..", "qoc_amd", "libqoc_mi355x.so"))
+
+const QOC_FP64 = Cint(0)
+const QOC_COST_TRACE = Cint(0)
+const QOC_COST_EXTERNAL = Cint(2)
+const QOC_ERR_STALE = Cint(-3)
+
+qoc_error(ctx) = unsafe_string(ccall((:qoc_last_error, libqoc), Cstring, (Ptr{Cvoid},), ctx))
+
+function check(rc, ctx)
+    rc == 0 && return nothing
+    # the reference raises error(...) at src/gradient_computations.jl:37-39 and :84-87
+    error(qoc_error(ctx))
+end
+
+mutable struct MI355XCache
+    ctx::Ptr{Cvoid}
+    N::Int
+    m::Int
+    nu::Int
+    Nt::Int
+    u::Matrix{Float64}
+    dJdu::Matrix{Float64}
+    gen::UInt64        # hash of the generators last uploaded
+    x0::UInt64
+    function MI355XCache(ctx, N, m, nu, Nt)
+        c = new(ctx, N, m, nu, Nt, zeros(nu, Nt), zeros(nu, Nt), 0, 0)
+        finalizer(c) do c
+            c.ctx != C_NULL && ccall((:qoc_destroy, libqoc), Cvoid, (Ptr{Cvoid},), c.ctx)
+            c.ctx = C_NULL
+        end
+        return c
+    end
+end
+
+"""
+    setup_grape_cache(A0, x0, u_size; device=0)
+
+GPU-resident replacement of `QuantumOptimalControl.setup_grape_cache`
+(src/gradient_computations.jl:79-96).  Errors on a dimension mismatch like the reference.
+"""
+function setup_grape_cache(A0, x0, u_size; device::Integer=0)
+    size(x0, 1) == size(A0, 1) || error("Error when creating cache, A0 and x0 have incompatiable dimensions")
+    nu, Nt = u_size
+    ref = Ref{Ptr{Cvoid}}(C_NULL)
+    rc = ccall((:qoc_create, libqoc), Cint,
+               (Ref{Ptr{Cvoid}}, Cint, Cint, Cint, Cint, Cint, Cint, Cint),
+               ref, device, size(A0, 1), size(x0, 2), nu, Nt, 1, QOC_FP64)
+    check(rc, C_NULL)
+    c = MI355XCache(ref[], size(A0, 1), size(x0, 2), nu, Nt)
+    check(ccall((:qoc_set_cost, libqoc), Cint, (Ptr{Cvoid}, Cint, Ptr{ComplexF64}, Cdouble),
+                c.ctx, QOC_COST_EXTERNAL, C_NULL, 1.0), c.ctx)
+    return c
+end
+
+function upload!(c::MI355XCache, A0, A, x0)
+    h = hash((A0, A))
+    if h != c.gen
+        A0c = Matrix{ComplexF64}(A0)
+        Ac = [Matrix{ComplexF64}(a) for a in A]
+        ptrs = [pointer(a) for a in Ac]
+        GC.@preserve A0c Ac ptrs begin
+            check(ccall((:qoc_set_generators, libqoc), Cint, (Ptr{Cvoid}, Ptr{ComplexF64}, Ptr{Ptr{ComplexF64}}),
+                        c.ctx, A0c, ptrs), c.ctx)
+        end
+        c.gen = h
+    end
+    hx = hash(x0)
+    if hx != c.x0
+        x0c = Matrix{ComplexF64}(reshape(x0, size(x0, 1), :))
+        GC.@preserve x0c check(ccall((:qoc_set_x0, libqoc), Cint, (Ptr{Cvoid}, Ptr{ComplexF64}, Cint),
+                                     c.ctx, x0c, 0), c.ctx)
+        c.x0 = hx
+    end
+end
+
+"""States of the last propagate, fetched lazily (the reference returns cache.x, Nt+1 matrices)."""
+struct LazyStates <: AbstractVector{Matrix{ComplexF64}}
+    c::MI355XCache
+end
+Base.size(s::LazyStates) = (s.c.Nt + 1,)
+function Base.getindex(s::LazyStates, k::Int)
+    out = Matrix{ComplexF64}(undef, s.c.N, s.c.m)
+    check(ccall((:qoc_get_states, libqoc), Cint, (Ptr{Cvoid}, Cint, Cint, Ptr{ComplexF64}),
+                s.c.ctx, 0, k - 1, out), s.c.ctx)
+    return out
+end
+
+function Base.getproperty(c::MI355XCache, s::Symbol)
+    s === :x && return LazyStates(c)
+    return getfield(c, s)
+end
+
+# propagate (src/gradient_computations.jl:2-32) on the GPU
+function QOC.propagate(A0, A::Vector{<:AbstractMatrix}, u, x0, cache::MI355XCache)
+    upload!(cache, A0, A, x0)
+    cache.u .= u                              # :12, kept for the stale-u check
+    J = Ref{Cdouble}(0.0)
+    check(ccall((:qoc_propagate, libqoc), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ref{Cdouble}),
+                cache.ctx, cache.u, J), cache.ctx)
+    return cache.x
+end
+
+# grape_sensitivity (src/gradient_computations.jl:35-77) on the GPU; the closure dJfinal_dx is
+# evaluated here at x[end] and handed over as λ_{Nt+1} (QOC_COST_EXTERNAL).
+function QOC.grape_sensitivity(A0, A::Vector{<:AbstractMatrix}, dJfinal_dx, u, x0, cache::MI355XCache;
+                               dUkdp_order=3, dL_dx=nothing)
+    dL_dx === nothing || dL_dx isa PenaltyGrad ||
+        error("dL_dx must come from QOCMI355X.setup_state_penalty (evaluated on the GPU)")
+    if dL_dx isa PenaltyGrad
+        P = Cint.(dL_dx.P .- 1); C = Cint.(dL_dx.C .- 1)
+        check(ccall((:qoc_set_state_penalty, libqoc), Cint,
+                    (Ptr{Cvoid}, Ptr{Cint}, Cint, Ptr{Cint}, Cint, Cdouble),
+                    cache.ctx, P, length(P), C, length(C), dL_dx.μ), cache.ctx)
+    end
+    λf = Matrix{ComplexF64}(dJfinal_dx(cache.x[end]))
+    rc = ccall((:qoc_grape_sensitivity, libqoc), Cint,
+               (Ptr{Cvoid}, Ptr{Float64}, Cint, Ptr{ComplexF64}, Ptr{Float64}),
+               cache.ctx, Matrix{Float64}(u), dUkdp_order, λf, cache.dJdu)
+    check(rc, cache.ctx)   # QOC_ERR_STALE -> "Cache data from other control signal u"
+    return cache.dJdu
+end
+
+"""Guard-state penalty whose gradient the GPU applies at every slice (src/penalty_fcns.jl:1-11)."""
+struct PenaltyGrad
+    P::Vector{Int}
+    C::Vector{Int}
+    μ::Float64
+end
+(g::PenaltyGrad)(x) = (d = zeros(eltype(x), size(x)); d[g.P, g.C] .= 2g.μ .* x[g.P, g.C]; d)
+function setup_state_penalty(inds_penalty, inds_css, μ)
+    L, _ = QOC.setup_state_penalty(inds_penalty, inds_css, μ)
+    return L, PenaltyGrad(collect(inds_penalty), collect(inds_css), Float64(μ))
+end
+
+end # module

@@ -97,3 +97,133 @@ def test_state_penalty(built_lib):
     qb = systems.QuantumBasis([3, 3])
     pen = (qb(["20", "21", "22"]), [0, 1, 2, 3], 0.37)
     _check(prob, systems.zz_controls(2, 40, 4.0, seed=9), penalty=pen)
+
+
+def test_zcalibrated_cost(built_lib):
+    """setup_infidelity_zcalibrated on the device (golden section in k_chain_fwd)."""
+    from qoc_amd import GrapeEngine, systems
+    prob = systems.zz_problem(40, tgate=4.0)
+    u = systems.zz_controls(3, 40, 4.0, seed=21)
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=3)
+    e.set_cost_zcalibrated(prob.x_target)
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    Jz, dJz = O.setup_infidelity_zcalibrated(prob.x_target)
+    for b in range(3):
+        cache = O.setup_grape_cache(prob.A0, prob.x0, u[b].shape)
+        x = O.propagate(prob.A0, prob.A, u[b], prob.x0, cache)
+        gr = O.grape_sensitivity(prob.A0, prob.A, dJz, cache.u, prob.x0, cache, dUkdp_order=3)
+        assert abs(J[b] - Jz(x[-1])) < 1e-11
+        assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) < 1e-8
+    e.close()
+
+
+def test_expm_jacobian_kernel_matches_oracle_and_fd_contract(built_lib):
+    from qoc_amd import expm_jacobian
+    rng = np.random.default_rng(0)
+    A0, A1, A2 = [0.05 * rng.standard_normal((3, 3)) for _ in range(3)]
+    u = np.array([1.0, 2.0])
+    for order in (1, 2, 3, 4):
+        for dt in (1.0, 0.25):
+            got = expm_jacobian(A0, [A1, A2], u, order, dt)
+            ref = O.expm_jacobian(A0, [A1, A2], u, order, dt)
+            for a, b in zip(got, ref):
+                assert np.abs(a - b).max() < 1e-15
+    from test_oracle import _fd_jac
+    for order, dt, thr in ((3, 1.0, 4e-4), (4, 1.0, 3e-5), (3, 0.25, 2e-6), (4, 0.25, 3e-8)):
+        got = expm_jacobian(A0, [A1, A2], u, order, dt)
+        err = np.linalg.norm(np.stack([x.ravel(order="F") for x in got], 1) - _fd_jac(A0, [A1, A2], u, dt))
+        assert err < thr
+
+
+def test_device_pointer_eval_matches_host_path(built_lib):
+    import torch
+    from qoc_amd import GrapeEngine, systems
+    prob = systems.cavity_problem(N_cavity=10, Nt=30)
+    u = systems.cavity_controls(4, 30, seed=3)
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=4)
+    e.set_cost_trace(prob.x_target, prob.n)
+    Jh = e.propagate(u)
+    gh = e.grape_sensitivity(u, 3)
+    ud = torch.from_numpy(np.ascontiguousarray(np.transpose(u, (0, 2, 1)))).cuda()
+    Jd = torch.empty(4, dtype=torch.float64, device="cuda")
+    gd = torch.empty(4, 30, 2, dtype=torch.float64, device="cuda")
+    e.eval_device(ud.data_ptr(), 3, Jd.data_ptr(), gd.data_ptr())
+    e.synchronize()
+    assert np.array_equal(Jd.cpu().numpy(), Jh)
+    assert np.array_equal(np.transpose(gd.cpu().numpy(), (0, 2, 1)), gh)
+    # stale check on the device path
+    e.propagate_device(ud.data_ptr(), Jd.data_ptr())
+    u2 = ud.clone()
+    u2[0, 0, 0] += 1e-3
+    from qoc_amd import StaleCacheError
+    with pytest.raises(StaleCacheError):
+        e.grape_sensitivity_device(u2.data_ptr(), 3, gd.data_ptr())
+    e.close()
+
+
+def test_reference_shaped_api(built_lib):
+    """propagate / grape_sensitivity mirror (closure dJfinal_dx evaluated on x[end], stale-u error)."""
+    import qoc_amd as Q
+    from qoc_amd import systems
+    prob = systems.zz_problem(30, tgate=3.0)
+    u = systems.zz_controls(1, 30, 3.0, seed=4)[0]
+    cache = Q.setup_grape_cache(prob.A0, prob.x0, u.shape)
+    x = Q.propagate(prob.A0, prob.A, u, prob.x0, cache)
+    assert len(x) == 31
+    Jf, dJf = Q.setup_infidelity(prob.x_target, 4)
+    user_closure = lambda xN: dJf(xN)  # noqa: E731  (untagged: goes through QOC_COST_EXTERNAL)
+    g = Q.grape_sensitivity(prob.A0, prob.A, user_closure, cache.u, prob.x0, cache, dUkdp_order=3)
+    Jr, gr, cr = O.grape_eval(prob.A0, prob.A, u, prob.x0, prob.x_target, 4, order=3)
+    assert abs(Jf(x[-1]) - Jr) < 1e-12
+    assert np.linalg.norm(g - gr) / np.linalg.norm(gr) < 1e-10
+    assert np.abs(x[7] - cr.x[7]).max() < 1e-13
+    assert np.abs(cache.lam[3] - cr.lam[3]).max() < 1e-12
+    with pytest.raises(Q.StaleCacheError, match="Cache data from other control signal u"):
+        Q.grape_sensitivity(prob.A0, prob.A, dJf, u * 1.01, prob.x0, cache)
+    L, dL = Q.setup_state_penalty([6, 7, 8], [0, 1, 2, 3], 0.3)
+    g2 = Q.grape_sensitivity(prob.A0, prob.A, dJf, cache.u, prob.x0, cache, dUkdp_order=3, dL_dx=dL)
+    Lo, dLo = O.setup_state_penalty([6, 7, 8], [0, 1, 2, 3], 0.3)
+    c2 = O.setup_grape_cache(prob.A0, prob.x0, u.shape)
+    O.propagate(prob.A0, prob.A, u, prob.x0, c2)
+    gr2 = O.grape_sensitivity(prob.A0, prob.A, O.setup_infidelity(prob.x_target, 4)[1], c2.u, prob.x0, c2,
+                              dUkdp_order=3, dL_dx=dLo)
+    assert np.linalg.norm(g2 - gr2) / np.linalg.norm(gr2) < 1e-10
+
+
+def test_fp32_small(built_lib):
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=10, Nt=40)
+    _check(prob, systems.cavity_controls(2, 40, seed=8), precision="fp32")
+
+
+def test_per_seed_x0(built_lib):
+    from qoc_amd import GrapeEngine, systems
+    prob = systems.zz_problem(20, tgate=2.0)
+    u = systems.zz_controls(2, 20, 2.0, seed=2)
+    rng = np.random.default_rng(5)
+    x0s = np.stack([np.linalg.qr(rng.standard_normal((9, 4)) + 1j * rng.standard_normal((9, 4)))[0] for _ in range(2)])
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2)
+    e.set_x0(x0s, per_seed=True)
+    e.set_cost_trace(prob.x_target, 4)
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    for b in range(2):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], x0s[b], prob.x_target, 4, order=3)
+        assert abs(J[b] - Jr) < 1e-12 and np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) < 1e-10
+    e.close()
+
+
+def test_non_dominant_q_uses_pivoted_lu(built_lib):
+    """Dense random generators with ||A||_1 ~ 4-5: Q = V-U is not diagonally dominant."""
+    from qoc_amd import expm, systems
+    rng = np.random.default_rng(9)
+    for N in (17, 33, 40):
+        A = []
+        for _ in range(3):
+            H = systems._gue(rng, N)
+            A.append(-1j * H * 4.5 / np.abs(H).sum(0).max())
+        X = expm(np.stack(A))
+        for a, x in zip(A, X):
+            Xr, d, s = O.expm_higham2005(a)
+            assert np.abs(x - Xr).max() < 1e-13

@@ -1,0 +1,87 @@
+"""Summarise a tools/profile.sh run into profiles/<tag>_<config>.md and profiles/traffic_<config>.json.
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are KB; on gfx950
+FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads, so it is doubled.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNELS = ("k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad")
+
+
+def short(name):
+    for k in KERNELS:
+        if k in name:
+            return k
+    return name.split("(")[0][:60]
+
+
+def stats(d):
+    f = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+    rows = []
+    if f:
+        for r in csv.DictReader(open(f[0])):
+            rows.append(r)
+    return rows, (f[0] if f else None)
+
+
+def pmc(d):
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    acc = defaultdict(lambda: defaultdict(list))
+    if not f:
+        return acc
+    for r in csv.DictReader(open(f[0])):
+        acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return acc
+
+
+def main(out_dir, cfg, tag, repo="."):
+    rows, src = stats(os.path.join(out_dir, "trace"))
+    fetch = pmc(os.path.join(out_dir, "pmc_fetch"))
+    write = pmc(os.path.join(out_dir, "pmc_write"))
+    sq = pmc(os.path.join(out_dir, "pmc_sq"))
+    lines = [f"# rocprofv3 summary — {tag}, config `{cfg}`", "",
+             f"Source: `{src}` (kernel-trace --stats of `bench.py --config {cfg} --steps 3 --warmup 1 --no-cpu`).", "",
+             "| kernel | calls | avg ms | total ms | % |", "|---|---|---|---|---|"]
+    for r in rows:
+        name = short(r.get("Name", r.get("KernelName", "")))
+        calls = r.get("Calls", "")
+        avg = float(r.get("AverageNs", 0)) / 1e6
+        tot = float(r.get("TotalDurationNs", 0)) / 1e6
+        pct = r.get("Percentage", "")
+        lines.append(f"| {name} | {calls} | {avg:.3f} | {tot:.2f} | {pct} |")
+    traffic = {}
+    lines += ["", "HBM traffic per launch from PMC (separate passes; FETCH_SIZE doubled per gfx950 rule):", "",
+              "| kernel | FETCH_SIZE KB (raw, mean) | WRITE_SIZE KB (mean) | HBM bytes/launch (corrected) |",
+              "|---|---|---|---|"]
+    for k in KERNELS:
+        fe = fetch.get(k, {}).get("FETCH_SIZE", [])
+        wr = write.get(k, {}).get("WRITE_SIZE", [])
+        if not fe and not wr:
+            continue
+        fm = sum(fe) / len(fe) if fe else 0.0
+        wm = sum(wr) / len(wr) if wr else 0.0
+        b = (2 * fm + wm) * 1024.0
+        traffic[k] = b
+        lines.append(f"| {k} | {fm:.0f} | {wm:.0f} | {b / 1e9:.3f} GB |")
+    if sq:
+        lines += ["", "| kernel | SQ_INSTS_VALU | SQ_INSTS_MFMA | SQ_INSTS_LDS | SQ_WAVES |", "|---|---|---|---|---|"]
+        for k in KERNELS:
+            c = sq.get(k)
+            if c:
+                m = {n: (sum(v) / len(v)) for n, v in c.items()}
+                lines.append(f"| {k} | {m.get('SQ_INSTS_VALU', 0):.3g} | {m.get('SQ_INSTS_MFMA', 0):.3g} | "
+                             f"{m.get('SQ_INSTS_LDS', 0):.3g} | {m.get('SQ_WAVES', 0):.3g} |")
+    os.makedirs(os.path.join(repo, "profiles"), exist_ok=True)
+    open(os.path.join(repo, "profiles", f"{tag}_{cfg}.md"), "w").write("\n".join(lines) + "\n")
+    if traffic:
+        json.dump(traffic, open(os.path.join(repo, "profiles", f"traffic_{cfg}.json"), "w"), indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3])
