@@ -91,6 +91,16 @@ int qoc_pade_histogram(qoc_ctx* ctx, long long* hist, int reset);
 int qoc_set_profiling(qoc_ctx* ctx, int enable);
 int qoc_phase_times(qoc_ctx* ctx, double* ms_out /*[4]*/, long long* launches_out /*[4]*/, int reset);
 
+/* Large-N path only: accumulated time, launch count and algorithmic FLOPs (8 M K Ncol per complex
+ * GEMM item) of the k_bgemm launches recorded while profiling was enabled. */
+int qoc_gemm_stats(qoc_ctx* ctx, double* ms, long long* launches, double* flops, int reset);
+
+/* Engine facts: info[0] = path (0 = LDS-resident kernels, 1 = large-N chunked GEMM pipeline),
+ * info[1] = slices per chunk (large-N), info[2] = Newton-Schulz iterations executed so far (large-N),
+ * info[3] = device bytes allocated by the context.  QOC_FORCE_LARGE_N=1 in the environment at
+ * qoc_create selects the large-N path for any size (testing). */
+int qoc_get_info(qoc_ctx* ctx, long long* info /*[4]*/);
+
 /* Standalone ops on the same kernels. */
 /* exponential!(A, ExpMethodHigham2005()) for `count` independent N x N matrices
  * (src/gradient_computations.jl:24, third-party ExponentialUtilities). */

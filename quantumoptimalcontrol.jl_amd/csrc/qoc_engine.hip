@@ -6,13 +6,17 @@
 // one HIP stream:  k_expm -> k_chain_fwd  |  k_chain_bwd -> k_grad.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "../../include/qoc.h"
+#include "qoc_bgemm.hpp"
 #include "qoc_chain.hpp"
 #include "qoc_expm.hpp"
 
@@ -60,6 +64,22 @@ struct qoc_ctx {
   std::vector<hipEvent_t> event_pool;
   double phase_ms[4] = {0, 0, 0, 0};
   long long phase_n[4] = {0, 0, 0, 0};
+  // large-N path: every k_bgemm launch bracketed while profiling (algorithmic FLOPs per launch)
+  struct GMark {
+    hipEvent_t a, b;
+    double flops;
+  };
+  std::vector<GMark> gmarks;
+  double gemm_ms = 0, gemm_flops = 0;
+  long long gemm_n = 0;
+  // large-N path (N beyond the LDS-resident kernels): chunked batched-GEMM pipeline
+  bool big = false;
+  int chunk = 0;                // slices per chunk
+  void* d_ws = nullptr;         // chunk workspace
+  double* d_red = nullptr;      // per-item reductions (chunk + 8 doubles)
+  long long big_hist[5 * 64] = {};
+  long long ns_iters = 0;       // Newton-Schulz iterations executed (all chunks)
+  size_t dev_bytes = 0;
   bool have_gen = false, have_x0 = false, have_cost = false, have_prop = false;
   std::string err;
 };
@@ -231,8 +251,364 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
   return QOC_OK;
 }
 
-int forward(qoc_ctx* c) { return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c); }
+// =============================================================================================
+// Large-N path: chunked batched-GEMM pipeline (N beyond the LDS-resident kernels).
+//   propagate : per chunk of slices  k_form_norm -> Padé products (6 GEMMs for d = 13, fused
+//               lincomb epilogues) -> Newton-Schulz solve of (V-U) X = (V+U) (all GEMM) ->
+//               squarings;  then the forward chain as Nt batched GEMMs over the seeds.
+//   sensitivity: backward chain as Nt batched U^H GEMMs; per chunk P_a = X^a x, Q_b = (X^H)^b λ,
+//               W_a = sum_b Q_b/(a+b+1)!, M' = W P^H (one GEMM, K = order*m), dJdu = Re<A_j, M'>.
+// =============================================================================================
+static const double hPade3[4] = {120.0, 60.0, 12.0, 1.0};
+static const double hPade5[6] = {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0};
+static const double hPade7[8] = {17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0};
+static const double hPade9[10] = {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0,
+                                  2162160.0, 110880.0, 3960.0, 90.0, 1.0};
+static const double hPade13[14] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
+                                   1187353796428800.0, 129060195264000.0, 10559470521600.0,
+                                   670442572800.0, 33522128640.0, 1323241920.0, 40840800.0,
+                                   960960.0, 16380.0, 182.0, 1.0};
+
+size_t big_ws_elems_per_item(int N, int m) {
+  const size_t NN = (size_t)N * N, Nm = (size_t)N * m;
+  return std::max(8 * NN, 2 * NN + 11 * Nm);
+}
+
+Opd mk_opd(const void* base, size_t elem_off, size_t esz, long long inner, int per = 0, long long outer = 0,
+           int u0 = 0) {
+  Opd o;
+  o.p = (const char*)base + elem_off * esz;
+  o.inner = inner;
+  o.per = per;
+  o.outer = outer;
+  o.u0 = u0;
+  return o;
+}
+
+GemmArgs gemm_args(int M, int K, int Ncol, int nitems) {
+  GemmArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.M = M;
+  g.K = K;
+  g.Ncol = Ncol;
+  g.nitems = nitems;
+  g.alpha1 = 1.0;
+  return g;
+}
+
+template <typename T>
+int big_gemm(qoc_ctx* c, int opa, int opb, GemmArgs g) {
+  g.tiles_m = (g.M + BG_BM - 1) / BG_BM;
+  g.tiles = g.tiles_m * ((g.Ncol + BG_BN - 1) / BG_BN);
+  const long long total = (long long)g.nitems * g.tiles;
+  if (total <= 0 || total >= (1LL << 31)) return fail(c, QOC_ERR_ARG, "GEMM grid out of range");
+  const dim3 grid((unsigned)total), blk(BG_THREADS);
+  qoc_ctx::GMark gm{nullptr, nullptr, 8.0 * g.M * (double)g.K * g.Ncol * g.nitems};
+  if (c->profiling) {
+    gm.a = take_event(c);
+    gm.b = take_event(c);
+    (void)hipEventRecord(gm.a, c->stream);
+  }
+  if (opa == 0 && opb == 0) hipLaunchKernelGGL((k_bgemm<T, 0, 0>), grid, blk, 0, c->stream, g);
+  else if (opa == 1 && opb == 0) hipLaunchKernelGGL((k_bgemm<T, 1, 0>), grid, blk, 0, c->stream, g);
+  else if (opa == 0 && opb == 1) hipLaunchKernelGGL((k_bgemm<T, 0, 1>), grid, blk, 0, c->stream, g);
+  else hipLaunchKernelGGL((k_bgemm<T, 1, 1>), grid, blk, 0, c->stream, g);
+  HIPCHK(c, hipGetLastError());
+  if (c->profiling) {
+    (void)hipEventRecord(gm.b, c->stream);
+    c->gmarks.push_back(gm);
+  }
+  return QOC_OK;
+}
+
+template <typename T>
+int big_lincomb(qoc_ctx* c, LinArgs a) {
+  const size_t total = (size_t)a.rows * a.cols * a.nitems;
+  const unsigned blocks = (unsigned)std::min<size_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL((k_lincomb<T>), dim3(blocks), dim3(256), 0, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  return QOC_OK;
+}
+
+// exp(A_k) for units [u0, u0+cnt) -> d_U.  Workspace buffers w(i), i < 8, of cnt x N x N.
+template <typename T>
+int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
+  const int N = c->N;
+  const size_t NN = (size_t)N * N, esz = c->esz;
+  auto w = [&](int i) { return mk_opd(c->d_ws, (size_t)i * c->chunk * NN, esz, (long long)NN); };
+  auto wp = [&](int i) { return (cx<T>*)((char*)c->d_ws + (size_t)i * c->chunk * NN * esz); };
+  const Opd dest = mk_opd(c->d_U, (size_t)u0 * NN, esz, (long long)NN);
+  int r;
+  // A_k and max ||A_k||_1 over the chunk
+  HIPCHK(c, hipMemsetAsync(c->d_red, 0, sizeof(double), c->stream));
+  hipLaunchKernelGGL((k_form_norm<T>), dim3(cnt), dim3(256), 0, c->stream, N, c->nu, u0, (const cx<T>*)c->d_A,
+                     (const double*)c->d_u, wp(0), (unsigned long long*)c->d_red);
+  HIPCHK(c, hipGetLastError());
+  double nA = 0.0;
+  HIPCHK(c, hipMemcpyAsync(&nA, c->d_red, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // Padé degree / squarings: the thresholds of k_expm (Higham 2005), one (d, s) per chunk chosen
+  // from the chunk's largest norm (any degree >= the per-slice choice meets the same bound).
+  int d, sq = 0;
+  if (nA <= 2.1) {
+    d = nA > 0.95 ? 9 : nA > 0.25 ? 7 : nA > 0.015 ? 5 : 3;
+  } else {
+    d = 13;
+    const double sl = std::log2(nA / 5.4);
+    sq = sl > 0 ? (int)std::ceil(sl) : 0;
+  }
+  const int di = d == 3 ? 0 : d == 5 ? 1 : d == 7 ? 2 : d == 9 ? 3 : 4;
+  c->big_hist[di * 64 + std::min(sq, 63)] += cnt;
+  const double* C = d == 3 ? hPade3 : d == 5 ? hPade5 : d == 7 ? hPade7 : d == 9 ? hPade9 : hPade13;
+  const double sc = std::ldexp(1.0, -sq);
+  GemmArgs g;
+  // buffers: 0 A, 1 A2, 2 A4, 3 A6, 4 T1/A8, 5 T2, 6 U', 7 V
+  g = gemm_args(N, N, N, cnt);
+  g.A = w(0); g.B = w(0); g.C1 = w(1); g.alpha1 = sc * sc;
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // A2
+  if (d == 13) {
+    g = gemm_args(N, N, N, cnt);
+    g.A = w(1); g.B = w(1); g.C1 = w(2);
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // A4
+    g.A = w(1); g.B = w(2); g.C1 = w(3);
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // A6 = A2 A4
+    LinArgs la;
+    std::memset(&la, 0, sizeof(la));
+    la.rows = N; la.cols = N; la.nitems = cnt; la.nt = 3;
+    la.Y[0] = w(3); la.Y[1] = w(2); la.Y[2] = w(1);
+    la.out = w(4); la.w[0] = C[13]; la.w[1] = C[11]; la.w[2] = C[9];
+    if ((r = big_lincomb<T>(c, la))) return r;  // T1
+    la.out = w(5); la.w[0] = C[12]; la.w[1] = C[10]; la.w[2] = C[8];
+    if ((r = big_lincomb<T>(c, la))) return r;  // T2
+    g = gemm_args(N, N, N, cnt);
+    g.A = w(3); g.B = w(4); g.C1 = w(6);
+    g.nY = 3; g.Y[0] = w(3); g.Y[1] = w(2); g.Y[2] = w(1);
+    g.w1[0] = C[7]; g.w1[1] = C[5]; g.w1[2] = C[3]; g.gamma1 = C[1];
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // U' = A6 T1 + c7 A6 + c5 A4 + c3 A2 + c1 I
+    g.B = w(5); g.C1 = w(7);
+    g.w1[0] = C[6]; g.w1[1] = C[4]; g.w1[2] = C[2]; g.gamma1 = C[0];
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // V
+  } else {
+    // powers A^{2k} = A^{2k-2} A2 (oracle: P = P @ A2), buffers 1.. ; U', V as lincombs
+    const int npow = d / 2;  // number of even powers beyond I: d=3:1, 5:2, 7:3, 9:4
+    for (int k = 2; k <= npow; ++k) {
+      g = gemm_args(N, N, N, cnt);
+      g.A = w(k - 1); g.B = w(1); g.C1 = w(k);
+      if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+    }
+    LinArgs la;
+    std::memset(&la, 0, sizeof(la));
+    la.rows = N; la.cols = N; la.nitems = cnt; la.nt = npow;
+    for (int k = 1; k <= npow; ++k) la.Y[k - 1] = w(k);
+    la.out = w(6); la.dI = C[1];
+    for (int k = 1; k <= npow; ++k) la.w[k - 1] = C[2 * k + 1];
+    if ((r = big_lincomb<T>(c, la))) return r;  // U'
+    la.out = w(7); la.dI = C[0];
+    for (int k = 1; k <= npow; ++k) la.w[k - 1] = C[2 * k];
+    if ((r = big_lincomb<T>(c, la))) return r;  // V
+  }
+  // U = (A/2^s) U';  P = V + U -> w1,  Q = V - U -> w2
+  g = gemm_args(N, N, N, cnt);
+  g.A = w(0); g.B = w(6); g.C1 = w(1); g.C2 = w(2);
+  g.alpha1 = sc; g.alpha2 = -sc;
+  g.nY = 1; g.Y[0] = w(7); g.w1[0] = 1.0; g.w2[0] = 1.0;
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  // Newton-Schulz for Q^{-1}:  Y0 = P / c0^2,  R = I - Q Y,  Y <- Y + Y R  (R_{k+1} = R_k^2).
+  // For A = -i H dt, P = conj-adjoint partner of Q and R0 = I - QP/c0^2 is tiny; ||R0||_F (computed
+  // in the GEMM epilogue) fixes the iteration count: smallest k with ||R0||^(2^k) <= tol.
+  const double c0sq = C[0] * C[0];
+  HIPCHK(c, hipMemsetAsync(c->d_red, 0, (size_t)cnt * sizeof(double), c->stream));
+  g = gemm_args(N, N, N, cnt);
+  g.A = w(2); g.B = w(1); g.C1 = w(3); g.alpha1 = -1.0 / c0sq; g.gamma1 = 1.0; g.sumsq = c->d_red;
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // R0 -> w3
+  std::vector<double> ss(cnt);
+  HIPCHK(c, hipMemcpyAsync(ss.data(), c->d_red, (size_t)cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  double e0 = 0.0;
+  for (double v : ss) e0 = std::max(e0, std::sqrt(v));
+  if (!(e0 < 0.9))
+    return fail(c, QOC_ERR_UNSUPPORTED,
+                "large-N solve: Newton-Schulz residual %.3g >= 0.9 (generators not skew-Hermitian?)", e0);
+  const double tol = c->prec == QOC_FP64 ? 1e-17 : 1e-8;
+  int iters = 1;
+  for (double e = e0 * e0; e > tol && iters < 8; e *= e) ++iters;
+  c->ns_iters += iters;
+  // Y1 = (P + P R0)/c0^2 -> w4
+  g = gemm_args(N, N, N, cnt);
+  g.A = w(1); g.B = w(3); g.C1 = w(4); g.alpha1 = 1.0 / c0sq;
+  g.nY = 1; g.Y[0] = w(1); g.w1[0] = 1.0 / c0sq;
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  int cur = 4;
+  for (int it = 1; it < iters; ++it) {
+    g = gemm_args(N, N, N, cnt);
+    g.A = w(2); g.B = w(cur); g.C1 = w(3); g.alpha1 = -1.0; g.gamma1 = 1.0;
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // R = I - Q Y
+    const int nxt = cur == 4 ? 5 : 4;
+    g = gemm_args(N, N, N, cnt);
+    g.A = w(cur); g.B = w(3); g.C1 = w(nxt);
+    g.nY = 1; g.Y[0] = w(cur); g.w1[0] = 1.0;
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // Y <- Y + Y R
+    cur = nxt;
+  }
+  // X = Y P, then s squarings; the last product lands in d_U
+  g = gemm_args(N, N, N, cnt);
+  g.A = w(cur); g.B = w(1); g.C1 = sq == 0 ? dest : w(6);
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  int xb = 6;
+  for (int q = 0; q < sq; ++q) {
+    const int nb = xb == 6 ? 7 : 6;
+    g = gemm_args(N, N, N, cnt);
+    g.A = w(xb); g.B = w(xb); g.C1 = q == sq - 1 ? dest : w(nb);
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+    xb = nb;
+  }
+  return QOC_OK;
+}
+
+template <typename T>
+int big_forward(qoc_ctx* c) {
+  const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
+  const size_t NN = (size_t)N * N, Nm = (size_t)N * m, esz = c->esz;
+  const long long units = (long long)B * Nt;
+  int r;
+  int mk = mark_begin(c, 0);
+  for (long long u0 = 0; u0 < units; u0 += c->chunk) {
+    const int cnt = (int)std::min<long long>(c->chunk, units - u0);
+    if ((r = big_expm_chunk<T>(c, u0, cnt))) return r;
+  }
+  mark_end(c, mk);
+  mk = mark_begin(c, 1);
+  // x_0 for every seed
+  LinArgs la;
+  std::memset(&la, 0, sizeof(la));
+  la.rows = N; la.cols = m; la.nitems = B; la.nt = 1; la.w[0] = 1.0;
+  la.Y[0] = mk_opd(c->d_x0, 0, esz, c->x0_per_seed ? (long long)Nm : 0);
+  la.out = mk_opd(c->d_X, 0, esz, (long long)(Nt + 1) * Nm);
+  if ((r = big_lincomb<T>(c, la))) return r;
+  // x_{k+1} = U_k x_k, batched over seeds
+  for (int k = 0; k < Nt; ++k) {
+    GemmArgs g = gemm_args(N, N, m, B);
+    g.A = mk_opd(c->d_U, (size_t)k * NN, esz, (long long)Nt * NN);
+    g.B = mk_opd(c->d_X, (size_t)k * Nm, esz, (long long)(Nt + 1) * Nm);
+    g.C1 = mk_opd(c->d_X, (size_t)(k + 1) * Nm, esz, (long long)(Nt + 1) * Nm);
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  }
+  // costs
+  const bool pen = c->mu != 0.0;
+  if (pen) {
+    hipLaunchKernelGGL((k_penalty_sum<T>), dim3(B), dim3(256), 0, c->stream, N, m, Nt, (const cx<T>*)c->d_X,
+                       c->d_pmask, c->mu, c->d_J);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (c->cost_kind == QOC_COST_TRACE) {
+    hipLaunchKernelGGL((k_trace_cost<T>), dim3(B), dim3(256), 0, c->stream, N, m, Nt, (const cx<T>*)c->d_X,
+                       (const cx<T>*)c->d_Xt, c->cost_n, pen ? 1 : 0, c->d_J, c->d_coef);
+    HIPCHK(c, hipGetLastError());
+  } else if (!pen) {
+    HIPCHK(c, hipMemsetAsync(c->d_J, 0, (size_t)B * sizeof(double), c->stream));
+  }
+  mark_end(c, mk);
+  return QOC_OK;
+}
+
+template <typename T>
+int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
+  const int N = c->N, m = c->m, Nt = c->Nt, B = c->B, nu = c->nu;
+  const size_t NN = (size_t)N * N, Nm = (size_t)N * m, esz = c->esz;
+  const bool pen = c->mu != 0.0;
+  const unsigned eb = (unsigned)std::min<size_t>((Nm * B + 255) / 256, 8192);
+  int r;
+  int mk = mark_begin(c, 2);
+  if (c->cost_kind == QOC_COST_TRACE) {
+    hipLaunchKernelGGL((k_lambda_final<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, (const cx<T>*)c->d_Xt,
+                       (const cx<double>*)c->d_coef, (cx<T>*)c->d_L);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (pen) {
+    hipLaunchKernelGGL((k_penalty_grad<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, Nt,
+                       (const cx<T>*)c->d_X, c->d_pmask, 2.0 * c->mu, (cx<T>*)c->d_L);
+    HIPCHK(c, hipGetLastError());
+  }
+  // λ_k = U_k^H λ_{k+1} (+ dL/dx(x_k))
+  for (int k = Nt - 1; k >= 0; --k) {
+    GemmArgs g = gemm_args(N, N, m, B);
+    g.A = mk_opd(c->d_U, (size_t)k * NN, esz, (long long)Nt * NN);
+    g.B = mk_opd(c->d_L, (size_t)(k + 1) * Nm, esz, (long long)(Nt + 1) * Nm);
+    g.C1 = mk_opd(c->d_L, (size_t)k * Nm, esz, (long long)(Nt + 1) * Nm);
+    if ((r = big_gemm<T>(c, 1, 0, g))) return r;
+    if (pen) {
+      hipLaunchKernelGGL((k_penalty_grad<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, k,
+                         (const cx<T>*)c->d_X, c->d_pmask, 2.0 * c->mu, (cx<T>*)c->d_L);
+      HIPCHK(c, hipGetLastError());
+    }
+  }
+  mark_end(c, mk);
+  mk = mark_begin(c, 3);
+  // gradient, per chunk of slice units
+  const long long units = (long long)B * Nt;
+  const int o = order;
+  const size_t C = (size_t)c->chunk;
+  const size_t offX = 0, offP = C * NN, offQ = offP + C * o * Nm, offW = offQ + C * (o > 1 ? o - 1 : 1) * Nm,
+               offM = offW + C * o * Nm;
+  static const double inv_fact[9] = {1.0, 1.0, 1.0 / 2, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720, 1.0 / 5040, 1.0 / 40320};
+  for (long long u0 = 0; u0 < units; u0 += c->chunk) {
+    const int cnt = (int)std::min<long long>(c->chunk, units - u0);
+    hipLaunchKernelGGL((k_form_norm<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)c->d_A,
+                       (const double*)c->d_u, (cx<T>*)((char*)c->d_ws + offX * esz), (unsigned long long*)nullptr);
+    HIPCHK(c, hipGetLastError());
+    const Opd Xk = mk_opd(c->d_ws, offX, esz, (long long)NN);
+    auto Pa = [&](int a) { return mk_opd(c->d_ws, offP + a * Nm, esz, (long long)(o * Nm)); };
+    auto Qb = [&](int b) {  // Q_0 = λ_{k+1} in place; Q_b (b >= 1) in the workspace
+      if (b == 0) return mk_opd(c->d_L, Nm, esz, (long long)Nm, Nt, (long long)(Nt + 1) * Nm, (int)u0);
+      return mk_opd(c->d_ws, offQ + (b - 1) * Nm, esz, (long long)((o - 1) * Nm));
+    };
+    auto Wa = [&](int a) { return mk_opd(c->d_ws, offW + a * Nm, esz, (long long)(o * Nm)); };
+    LinArgs la;
+    std::memset(&la, 0, sizeof(la));
+    la.rows = N; la.cols = m; la.nitems = cnt; la.nt = 1; la.w[0] = 1.0;
+    la.Y[0] = mk_opd(c->d_X, 0, esz, (long long)Nm, Nt, (long long)(Nt + 1) * Nm, (int)u0);
+    la.out = Pa(0);
+    if ((r = big_lincomb<T>(c, la))) return r;  // P_0 = x_k
+    for (int a = 1; a < o; ++a) {
+      GemmArgs g = gemm_args(N, N, m, cnt);
+      g.A = Xk; g.B = Pa(a - 1); g.C1 = Pa(a);
+      if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // P_a = X P_{a-1}
+    }
+    for (int b = 1; b < o; ++b) {
+      GemmArgs g = gemm_args(N, N, m, cnt);
+      g.A = Xk; g.B = Qb(b - 1); g.C1 = Qb(b);
+      if ((r = big_gemm<T>(c, 1, 0, g))) return r;  // Q_b = X^H Q_{b-1}
+    }
+    for (int a = 0; a < o; ++a) {
+      std::memset(&la, 0, sizeof(la));
+      la.rows = N; la.cols = m; la.nitems = cnt; la.nt = o - a;
+      for (int b = 0; b < o - a; ++b) {
+        la.Y[b] = Qb(b);
+        la.w[b] = inv_fact[a + b + 1];
+      }
+      la.out = Wa(a);
+      if ((r = big_lincomb<T>(c, la))) return r;  // W_a = sum_b Q_b/(a+b+1)!
+    }
+    GemmArgs g = gemm_args(N, o * m, N, cnt);
+    g.A = mk_opd(c->d_ws, offW, esz, (long long)(o * Nm));
+    g.B = mk_opd(c->d_ws, offP, esz, (long long)(o * Nm));
+    g.C1 = mk_opd(c->d_ws, offM, esz, (long long)NN);
+    if ((r = big_gemm<T>(c, 0, 1, g))) return r;  // M' = W P^H
+    hipLaunchKernelGGL((k_gen_contract<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)c->d_A,
+                       (const cx<T>*)((char*)c->d_ws + offM * esz), d_dJdu);
+    HIPCHK(c, hipGetLastError());
+  }
+  mark_end(c, mk);
+  return QOC_OK;
+}
+
+int forward(qoc_ctx* c) {
+  if (c->big) return c->prec == QOC_FP64 ? big_forward<double>(c) : big_forward<float>(c);
+  return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
+}
 int backward(qoc_ctx* c, int order, double* d_dJdu) {
+  if (c->big)
+    return c->prec == QOC_FP64 ? big_backward<double>(c, order, d_dJdu) : big_backward<float>(c, order, d_dJdu);
   return c->prec == QOC_FP64 ? run_backward<double>(c, order, d_dJdu) : run_backward<float>(c, order, d_dJdu);
 }
 
@@ -257,10 +633,14 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   if (N < 1 || m < 1 || nu < 1 || Nt < 1 || B < 1)
     return fail(nullptr, QOC_ERR_ARG, "invalid dimensions N=%d m=%d nu=%d Nt=%d B=%d", N, m, nu, Nt, B);
   if (precision != QOC_FP64 && precision != QOC_FP32) return fail(nullptr, QOC_ERR_ARG, "invalid precision");
-  if (!expm_supported(N, precision) || N > kChainMaxN || N * N > CHAIN_THREADS * (precision == QOC_FP64 ? 8 : 16) ||
-      N * m > 4 * CHAIN_THREADS)
-    return fail(nullptr, QOC_ERR_UNSUPPORTED, "N=%d m=%d outside the LDS-resident kernel envelope", N, m);
+  // LDS-resident kernels when the problem fits them, the chunked GEMM pipeline otherwise
+  const bool small = expm_supported(N, precision) && N <= kChainMaxN &&
+                     N * N <= CHAIN_THREADS * (precision == QOC_FP64 ? 8 : 16) && N * m <= 4 * CHAIN_THREADS;
+  const bool force_big = getenv("QOC_FORCE_LARGE_N") && atoi(getenv("QOC_FORCE_LARGE_N")) != 0;
+  if ((!small || force_big) && nu > 8)
+    return fail(nullptr, QOC_ERR_UNSUPPORTED, "large-N path supports nu <= 8 (got %d)", nu);
   qoc_ctx* c = new qoc_ctx();
+  c->big = !small || force_big;
   c->dev = device;
   c->N = N;
   c->m = m;
@@ -298,6 +678,24 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   };
   for (auto& a : allocs) {
     if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return bail(e, "hipMalloc");
+    c->dev_bytes += a.bytes;
+  }
+  if (c->big) {
+    // chunk of slices sized to a workspace of <= 8 GiB (and <= 1/8 of what is free)
+    size_t freeb = 0, totalb = 0;
+    (void)hipMemGetInfo(&freeb, &totalb);
+    const size_t per_item = big_ws_elems_per_item(N, m) * c->esz;
+    size_t budget = std::min<size_t>(8ull << 30, freeb / 8);
+    const long long units = (long long)B * Nt;
+    long long ch = std::max<long long>(1, (long long)(budget / per_item));
+    ch = std::min<long long>(ch, units);
+    ch = std::min<long long>(ch, 16384);
+    if (getenv("QOC_CHUNK")) ch = std::max(1, std::min<int>(atoi(getenv("QOC_CHUNK")), (int)std::min<long long>(units, 16384)));
+    c->chunk = (int)ch;
+    if ((e = hipMalloc(&c->d_ws, (size_t)ch * per_item)) != hipSuccess) return bail(e, "hipMalloc (workspace)");
+    if ((e = hipMalloc((void**)&c->d_red, ((size_t)ch + 8) * sizeof(double))) != hipSuccess)
+      return bail(e, "hipMalloc");
+    c->dev_bytes += (size_t)ch * per_item + ((size_t)ch + 8) * sizeof(double);
   }
   hipMemset(c->d_pmask, 0, Nm);
   hipMemset(c->d_hist, 0, 5 * 64 * sizeof(unsigned long long));
@@ -311,10 +709,14 @@ void qoc_destroy(qoc_ctx* c) {
   hipSetDevice(c->dev);
   if (c->stream) hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
-                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage};
+                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& m : c->marks) {
+    hipEventDestroy(m.a);
+    hipEventDestroy(m.b);
+  }
+  for (auto& m : c->gmarks) {
     hipEventDestroy(m.a);
     hipEventDestroy(m.b);
   }
@@ -366,6 +768,8 @@ int qoc_set_cost(qoc_ctx* c, int kind, const double* X_target, double n) {
     return fail(c, QOC_ERR_ARG, "unknown cost kind %d", kind);
   if (kind == QOC_COST_ZCAL && c->m != 4)
     return fail(c, QOC_ERR_ARG, "Only works for two-qubit gates, x_target must have four columns");
+  if (kind == QOC_COST_ZCAL && c->big)
+    return fail(c, QOC_ERR_UNSUPPORTED, "z-calibrated cost is not implemented on the large-N path");
   if (kind != QOC_COST_EXTERNAL && !X_target) return fail(c, QOC_ERR_ARG, "X_target is null");
   if (kind == QOC_COST_TRACE && !(n != 0.0)) return fail(c, QOC_ERR_ARG, "normalisation n must be nonzero");
   HIPCHK(c, hipSetDevice(c->dev));
@@ -540,6 +944,16 @@ int qoc_phase_times(qoc_ctx* c, double* ms_out, long long* launches_out, int res
     c->event_pool.push_back(m.b);
   }
   c->marks.clear();
+  for (auto& m : c->gmarks) {
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, m.a, m.b));
+    c->gemm_ms += ms;
+    c->gemm_n += 1;
+    c->gemm_flops += m.flops;
+    c->event_pool.push_back(m.a);
+    c->event_pool.push_back(m.b);
+  }
+  c->gmarks.clear();
   for (int p = 0; p < 4; ++p) {
     if (ms_out) ms_out[p] = c->phase_ms[p];
     if (launches_out) launches_out[p] = c->phase_n[p];
@@ -551,12 +965,38 @@ int qoc_phase_times(qoc_ctx* c, double* ms_out, long long* launches_out, int res
   return QOC_OK;
 }
 
+int qoc_gemm_stats(qoc_ctx* c, double* ms, long long* launches, double* flops, int reset) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  int r = qoc_phase_times(c, nullptr, nullptr, 0);  // drains pending marks
+  if (r) return r;
+  if (ms) *ms = c->gemm_ms;
+  if (launches) *launches = c->gemm_n;
+  if (flops) *flops = c->gemm_flops;
+  if (reset) {
+    c->gemm_ms = 0;
+    c->gemm_flops = 0;
+    c->gemm_n = 0;
+  }
+  return QOC_OK;
+}
+
+int qoc_get_info(qoc_ctx* c, long long* info) {
+  if (!c || !info) return fail(c, QOC_ERR_ARG, "null argument");
+  info[0] = c->big ? 1 : 0;
+  info[1] = c->chunk;
+  info[2] = c->ns_iters;
+  info[3] = (long long)c->dev_bytes;
+  return QOC_OK;
+}
+
 int qoc_pade_histogram(qoc_ctx* c, long long* hist, int reset) {
   if (!c || !hist) return fail(c, QOC_ERR_ARG, "null argument");
   HIPCHK(c, hipSetDevice(c->dev));
   HIPCHK(c, hipMemcpyAsync(hist, c->d_hist, 5 * 64 * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
   if (reset) HIPCHK(c, hipMemsetAsync(c->d_hist, 0, 5 * 64 * sizeof(long long), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int i = 0; i < 5 * 64; ++i) hist[i] += c->big_hist[i];
+  if (reset) std::memset(c->big_hist, 0, sizeof(c->big_hist));
   return QOC_OK;
 }
 

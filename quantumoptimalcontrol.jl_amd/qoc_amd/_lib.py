@@ -48,6 +48,8 @@ SIGNATURES = {
     "qoc_set_profiling": (C.c_int, [_vp, C.c_int]),
     "qoc_phase_times": (C.c_int, [_vp, _dp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_pade_histogram": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
+    "qoc_get_info": (C.c_int, [_vp, C.POINTER(C.c_longlong)]),
+    "qoc_gemm_stats": (C.c_int, [_vp, _dp, C.POINTER(C.c_longlong), _dp, C.c_int]),
     "qoc_expm_batched": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _ip]),
     "qoc_expm_jacobian": (C.c_int, [C.c_int, C.c_int, C.c_int, _dp, C.POINTER(_dp), _dp, C.c_int, C.c_double, _dp]),
 }

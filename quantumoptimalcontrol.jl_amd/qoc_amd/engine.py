@@ -201,6 +201,20 @@ class GrapeEngine:
                                             int(reset)))
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.PHASES)}
 
+    def info(self) -> dict:
+        """Which pipeline the context runs (qoc_get_info): 'lds' kernels or the 'large_n' GEMM path."""
+        v = np.zeros(4, dtype=np.int64)
+        self._chk(self._lib.qoc_get_info(self._h, v.ctypes.data_as(C.POINTER(C.c_longlong))))
+        return {"path": "large_n" if v[0] else "lds", "chunk": int(v[1]), "ns_iters": int(v[2]),
+                "device_bytes": int(v[3])}
+
+    def gemm_stats(self, reset: bool = False) -> dict:
+        """Large-N path: live HIP-event time / launches / algorithmic FLOPs of the k_bgemm launches."""
+        ms, fl = C.c_double(), C.c_double()
+        n = C.c_longlong()
+        self._chk(self._lib.qoc_gemm_stats(self._h, C.byref(ms), C.byref(n), C.byref(fl), int(reset)))
+        return {"ms": ms.value, "launches": n.value, "flops": fl.value}
+
     def pade_histogram(self, reset: bool = False) -> dict:
         h = np.zeros(5 * 64, dtype=np.int64)
         self._chk(self._lib.qoc_pade_histogram(self._h, h.ctypes.data_as(C.POINTER(C.c_longlong)), int(reset)))

@@ -36,8 +36,9 @@ def test_create_rejects_bad_dimensions_before_touching_the_gpu(built_lib):
     rc = built_lib.qoc_create(ctypes.byref(h), 0, 0, 1, 1, 1, 1, 0)
     assert rc == -1 and not h.value
     assert b"invalid dimensions" in built_lib.qoc_last_error(None)
-    rc = built_lib.qoc_create(ctypes.byref(h), 0, 200, 1, 1, 1, 1, 0)
-    assert rc == -5  # outside the LDS-resident kernel envelope
+    rc = built_lib.qoc_create(ctypes.byref(h), 0, 200, 1, 9, 1, 1, 0)
+    assert rc == -5  # beyond the LDS-resident kernels -> large-N path, which takes nu <= 8
+    assert b"nu <= 8" in built_lib.qoc_last_error(None)
 
 
 def test_engine_dimension_mismatch_message(built_lib):

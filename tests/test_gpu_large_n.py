@@ -1,0 +1,160 @@
+"""GPU parity of the large-N path (chunked batched-GEMM pipeline, Newton-Schulz Padé solve) vs the
+CPU oracle.  The path is selected automatically above the LDS-resident envelope (N > 48) and can be
+forced for any N with QOC_FORCE_LARGE_N=1, which lets the fp64 cases reuse the small physics
+configurations at the oracle's fp64 tolerances (|ΔJ| <= 1e-12, rel ||ΔdJdu|| <= 1e-10).
+fp32 (synthetic N = 256, config 5): |ΔJ| <= 1e-4, rel ||ΔdJdu|| <= 1e-3.
+"""
+import numpy as np
+import pytest
+
+import qoc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(prob, u, order=3, precision="fp64", penalty=None, x0=None):
+    from qoc_amd import GrapeEngine
+    B = u.shape[0]
+    e = GrapeEngine(prob.A0, prob.A, prob.x0 if x0 is None else x0, prob.Nt, B=B, precision=precision)
+    e.set_cost_trace(prob.x_target, prob.n)
+    if penalty is not None:
+        e.set_state_penalty(*penalty)
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, order)
+    info = e.info()
+    hist = e.pade_histogram()
+    e.close()
+    return J, g, info, hist
+
+
+def _compare(prob, u, J, g, order=3, tol=(1e-12, 1e-10), penalty=None, x0s=None):
+    for b in range(u.shape[0]):
+        x0 = prob.x0 if x0s is None else x0s[b]
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], x0, prob.x_target, prob.n, order=order, penalty=penalty)
+        assert abs(J[b] - Jr) <= tol[0], (b, J[b], Jr)
+        rel = np.linalg.norm(g[b] - gr) / max(np.linalg.norm(gr), 1e-300)
+        assert rel <= tol[1], (b, rel)
+
+
+def test_forced_large_n_cavity_fp64(built_lib, monkeypatch):
+    from qoc_amd import systems
+    monkeypatch.setenv("QOC_FORCE_LARGE_N", "1")
+    monkeypatch.setenv("QOC_CHUNK", "7")  # 90 slices -> 13 chunks, ragged last chunk
+    prob = systems.cavity_problem(N_cavity=6, Nt=30)
+    u = systems.cavity_controls(3, prob.Nt, seed=0)
+    J, g, info, hist = _run(prob, u)
+    assert info["path"] == "large_n" and info["chunk"] == 7 and info["ns_iters"] > 0
+    assert sum(hist.values()) == 3 * prob.Nt
+    _compare(prob, u, J, g)
+
+
+@pytest.mark.parametrize("order", [1, 2, 4])
+def test_forced_large_n_orders(built_lib, monkeypatch, order):
+    from qoc_amd import systems
+    monkeypatch.setenv("QOC_FORCE_LARGE_N", "1")
+    prob = systems.zz_problem(40)
+    u = systems.zz_controls(2, 40, 10.0, seed=1)
+    J, g, info, _ = _run(prob, u, order=order)
+    assert info["path"] == "large_n"
+    _compare(prob, u, J, g, order=order)
+
+
+def test_forced_large_n_penalty_and_per_seed_x0(built_lib, monkeypatch):
+    from qoc_amd import GrapeEngine, systems
+    monkeypatch.setenv("QOC_FORCE_LARGE_N", "1")
+    prob = systems.cavity_problem(N_cavity=6, Nt=20)
+    u = systems.cavity_controls(2, prob.Nt, seed=3)
+    pen = (list(range(prob.A0.shape[0] - 3, prob.A0.shape[0])), list(range(prob.x0.shape[1])), 0.7)
+    J, g, _, _ = _run(prob, u, penalty=pen)
+    _compare(prob, u, J, g, penalty=pen)
+    # per-seed x0
+    rng = np.random.default_rng(9)
+    x0s = []
+    for _ in range(2):
+        Z = rng.standard_normal(prob.x0.shape) + 1j * rng.standard_normal(prob.x0.shape)
+        x0s.append(np.linalg.qr(Z)[0])
+    x0s = np.stack(x0s)
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2)
+    assert e.info()["path"] == "large_n"
+    e.set_x0(x0s, per_seed=True)
+    e.set_cost_trace(prob.x_target, prob.n)
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    e.close()
+    _compare(prob, u, J, g, x0s=x0s)
+
+
+def _gue_problem(N, m, Nt, norm0, normj, nu=2, seed=0):
+    from qoc_amd import systems
+    rng = np.random.default_rng(seed)
+
+    def scaled(H, s):
+        return H * (s / np.abs(H).sum(axis=0).max())
+    A0 = -1j * scaled(systems._gue(rng, N), norm0)
+    A = [-1j * scaled(systems._gue(rng, N), normj) for _ in range(nu)]
+    x0 = np.eye(N, dtype=np.complex128)[:, :m]
+    Z = rng.standard_normal((N, m)) + 1j * rng.standard_normal((N, m))
+    Xt = np.linalg.qr(Z)[0]
+    return systems.Problem("gue", A0, A, x0, Xt, float(m), Nt, "fp64")
+
+
+def test_auto_large_n_ragged_fp64_with_squarings(built_lib, monkeypatch):
+    """N = 70 (not a multiple of the 64-wide GEMM tile), m = 3, norms that select d = 13 with
+    squarings in some chunks and lower degrees in others."""
+    monkeypatch.setenv("QOC_CHUNK", "3")
+    prob = _gue_problem(70, 3, 5, norm0=9.0, normj=2.0, seed=4)
+    rng = np.random.default_rng(5)
+    u = rng.uniform(-1, 1, size=(2, 2, prob.Nt))
+    u[1] *= 0.0  # seed 1: A_k = A0 only
+    J, g, info, hist = _run(prob, u)
+    assert info["path"] == "large_n"
+    assert any(s > 0 for (d, s) in hist), hist
+    _compare(prob, u, J, g)
+    # low-norm problem -> degrees < 13 on the same path
+    prob = _gue_problem(70, 3, 4, norm0=0.6, normj=0.1, seed=6)
+    u = rng.uniform(-1, 1, size=(2, 2, prob.Nt))
+    J, g, info, hist = _run(prob, u)
+    assert all(d < 13 for (d, s) in hist), hist
+    _compare(prob, u, J, g)
+
+
+def test_synthetic_n256_fp32(built_lib):
+    from qoc_amd import systems
+    prob = systems.synthetic_problem(256, Nt=3)
+    u = systems.synthetic_controls(2, 3, 2, seed=0)
+    J, g, info, hist = _run(prob, u, precision="fp32")
+    assert info["path"] == "large_n"
+    assert set(hist) == {(13, 0)}, hist
+    _compare(prob, u, J, g, tol=(1e-4, 1e-3))
+    # J ~ 1 for a Haar target, so also compare the propagated states themselves
+    from qoc_amd import GrapeEngine
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2, precision="fp32")
+    e.set_cost_trace(prob.x_target, prob.n)
+    e.propagate(u)
+    for b in range(2):
+        xr = O.propagate(prob.A0, prob.A, u[b], prob.x0)
+        for k in (1, prob.Nt):
+            x = e.state(k, seed=b)
+            assert np.linalg.norm(x - xr[k]) / np.linalg.norm(xr[k]) < 2e-5, (b, k)
+        U = e.propagator(0, seed=b)
+        Ur = O.expm_higham2005(prob.A0 + sum(u[b, j, 0] * prob.A[j] for j in range(2)))[0]
+        assert np.abs(U - Ur).max() < 2e-5
+    e.close()
+
+
+def test_synthetic_n256_fp64(built_lib):
+    from qoc_amd import systems
+    prob = systems.synthetic_problem(256, Nt=2)
+    u = systems.synthetic_controls(1, 2, 2, seed=1)
+    J, g, info, _ = _run(prob, u, precision="fp64")
+    _compare(prob, u, J, g, tol=(1e-11, 1e-9))
+
+
+def test_large_n_zcal_unsupported(built_lib, monkeypatch):
+    from qoc_amd import GrapeEngine, QOCError, systems
+    monkeypatch.setenv("QOC_FORCE_LARGE_N", "1")
+    prob = systems.zz_problem(10)
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=1)
+    with pytest.raises(QOCError):
+        e.set_cost_zcalibrated(prob.x_target)
+    e.close()
