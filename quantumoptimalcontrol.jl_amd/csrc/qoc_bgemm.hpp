@@ -33,149 +33,212 @@ __device__ __forceinline__ const cx<T>* opd_ptr(const Opd& o, int item) {
   return reinterpret_cast<const cx<T>*>(o.p) + off;
 }
 
-constexpr int BG_BM = 64, BG_BN = 64, BG_BK = 16, BG_THREADS = 256;
+constexpr int BG_BM = 64, BG_BN = 64, BG_THREADS = 256;
 
 // C1 = alpha1 * op(A) op(B) + sum_t w1[t] Y_t + gamma1 I
 // C2 = alpha2 * op(A) op(B) + sum_t w2[t] Y_t + gamma2 I          (optional)
+// C3 = alpha3 * op(A) op(B) + sum_t w3[t] Y_t + gamma3 I          (optional)
 // sumsq (optional): sumsq[item] += ||C1||_F^2 (Newton-Schulz residual bound, ||R||_2 <= ||R||_F).
 struct GemmArgs {
-  Opd A, B, C1, C2, Y[3];
+  Opd A, B, C1, C2, C3, Y[3];
   int nY;
   int M, K, Ncol;  // op(A): M x K, op(B): K x Ncol
   int nitems, tiles_m, tiles;
-  double alpha1, alpha2, gamma1, gamma2;
-  double w1[3], w2[3];
+  double alpha1, alpha2, alpha3, gamma1, gamma2, gamma3;
+  double w1[3], w2[3], w3[3];
   double* sumsq;
 };
 
-// LDS operand layouts: "k-major" [k][row] when the global operand is contiguous along rows,
-// "row-major" [row][k] when it is contiguous along k.  Padding spreads MFMA fragment reads over banks.
-template <bool KMAJOR>
-struct LdsLay;
+// Both operands are staged in LDS as [row or col][k] planes (re / im) with k contiguous.  K is
+// permuted inside each 16-deep sub-slab: at MFMA step t lane l multiplies k = 4 (l >> 4) + t, so a
+// lane's four k values are adjacent and one 16-byte LDS read (per 4 floats) fetches its fragment
+// for the sub-slab.  Rows are padded by 16 bytes: the 16 rows a lane group reads then fall on
+// distinct 16-byte bank slots.  A slab is KS sub-slabs (BK = 16 KS); NBUF = 2 double-buffers the
+// LDS image (one barrier per slab), NBUF = 1 uses one image and two barriers per slab but a smaller
+// LDS footprint (more workgroups per CU).
+template <typename T, int KS>
+struct BgLay {
+  static constexpr int BK = 16 * KS;
+  static constexpr int LDK = BK + 16 / (int)sizeof(T);  // row stride in elements
+  static constexpr int PLANE = BG_BM * LDK;
+};
+
+template <typename T>
+struct Vec4;
 template <>
-struct LdsLay<true> {
-  static constexpr int SIZE = BG_BK * (BG_BM + 4);
-  static __device__ __forceinline__ int at(int k, int r) { return k * (BG_BM + 4) + r; }
+struct Vec4<float> {
+  typedef float type __attribute__((ext_vector_type(4)));
 };
 template <>
-struct LdsLay<false> {
-  static constexpr int SIZE = BG_BM * (BG_BK + 1);
-  static __device__ __forceinline__ int at(int k, int r) { return r * (BG_BK + 1) + k; }
+struct Vec4<double> {
+  typedef double type __attribute__((ext_vector_type(4)));
 };
+
+// Stage one 64 x BK slab of an operand into registers; element (r, k) with r < R, k < K.
+// KCONT: memory contiguous along k (address k + ld * r), else along r (address r + ld * k).
+// Thread t owns one row/col r and, per sub-slab j, the four consecutive k of group kg.
+template <typename T, bool KCONT, bool CONJ, int KS>
+__device__ __forceinline__ void bg_load(const cx<T>* __restrict__ base, long long ld, int r0, int k0, int R, int K,
+                                        int tid, typename Vec4<T>::type (&re)[KS], typename Vec4<T>::type (&im)[KS]) {
+  const int r = KCONT ? (tid >> 2) : (tid & 63);
+  const int gr = r0 + r;
+#pragma unroll
+  for (int j = 0; j < KS; ++j) {
+    const int kg = (KCONT ? (tid & 3) : (tid >> 6)) + 4 * j;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int gk = k0 + 4 * kg + t;
+      const bool ok = gr < R && gk < K;
+      const long long off = KCONT ? (long long)(ok ? gk : 0) + ld * (ok ? gr : 0)
+                                  : (long long)(ok ? gr : 0) + ld * (ok ? gk : 0);
+      const cx<T> v = base[off];
+      re[j][t] = ok ? v.r : T(0);
+      im[j][t] = ok ? (CONJ ? -v.i : v.i) : T(0);
+    }
+  }
+}
+
+template <typename T, bool KCONT, int KS>
+__device__ __forceinline__ void bg_store(T* __restrict__ pre, T* __restrict__ pim, int tid,
+                                         const typename Vec4<T>::type (&re)[KS],
+                                         const typename Vec4<T>::type (&im)[KS]) {
+  using L = BgLay<T, KS>;
+  using V = typename Vec4<T>::type;
+  const int r = KCONT ? (tid >> 2) : (tid & 63);
+#pragma unroll
+  for (int j = 0; j < KS; ++j) {
+    const int kg = (KCONT ? (tid & 3) : (tid >> 6)) + 4 * j;
+    *reinterpret_cast<V*>(pre + r * L::LDK + 4 * kg) = re[j];
+    *reinterpret_cast<V*>(pim + r * L::LDK + 4 * kg) = im[j];
+  }
+}
 
 // OPA: 0 -> op(A) = A (stored M x K, contiguous along rows); 1 -> A^H (stored K x M, contiguous along k)
 // OPB: 0 -> op(B) = B (stored K x Ncol, contiguous along k); 1 -> B^H (stored Ncol x K, contiguous along cols)
-template <typename T, int OPA, int OPB>
+// M3: complex product with 3 real MFMAs (Gauss): P1 = ar br, P2 = ai bi, P3 = (ar+ai)(br+bi);
+// Re = P1 - P2, Im = P3 - P1 - P2.  25 % fewer MFMAs than the 4-product form; the imaginary part's
+// rounding error grows to ~2 eps |a||b| (cancellation in P3 - P1 - P2), well inside the fp32/fp64
+// parity tolerances.
+template <typename T, int OPA, int OPB, bool M3 = true, int KS = 1, int NBUF = 2>
 __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
   using MFT = MF<T>;
   using v4 = typename MFT::v4;
-  using LA = LdsLay<OPA == 0>;
-  using LB = LdsLay<OPB == 1>;
-  __shared__ T As[2][2][LA::SIZE];
-  __shared__ T Bs[2][2][LB::SIZE];
+  using V = typename Vec4<T>::type;
+  using L = BgLay<T, KS>;
+  // [buf][A re, A im, B re, B im][64][LDK]
+  __shared__ __attribute__((aligned(16))) T lds[NBUF * 4 * L::PLANE];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // XCD-aware order: consecutive workgroups are dispatched round-robin over the 8 XCDs; give each
   // XCD a contiguous range of (item, tile) so that one item's tiles share an L2.
-  const int L = blockIdx.x;
+  const int Lb = blockIdx.x;
   const int total = g.nitems * g.tiles;
-  const int lin = (total & 7) == 0 ? (L & 7) * (total >> 3) + (L >> 3) : L;
+  const int lin = (total & 7) == 0 ? (Lb & 7) * (total >> 3) + (Lb >> 3) : Lb;
   const int item = lin / g.tiles, tile = lin - item * g.tiles;
   const int tm = tile % g.tiles_m, tn = tile / g.tiles_m;
   const int row0 = tm * BG_BM, col0 = tn * BG_BN;
   const cx<T>* Ab = opd_ptr<T>(g.A, item);
   const cx<T>* Bb = opd_ptr<T>(g.B, item);
   const int M = g.M, K = g.K, NC = g.Ncol;
+  const long long ldA = OPA ? K : M, ldB = OPB ? NC : K;
 
-  cx<T> ra[4], rb[4];
-#define QOC_BG_LOAD(K0)                                                                      \
-  do {                                                                                       \
-    _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                          \
-      const int e = tid + BG_THREADS * r;                                                    \
-      const int ka = OPA ? (e & 15) : (e >> 6), ia = OPA ? (e >> 4) : (e & 63);              \
-      const int gr = row0 + ia, gk = (K0) + ka;                                              \
-      const bool oka = gr < M && gk < K;                                                     \
-      const size_t oa = OPA ? (size_t)(oka ? gk : 0) + (size_t)K * (oka ? gr : 0)            \
-                            : (size_t)(oka ? gr : 0) + (size_t)M * (oka ? gk : 0);           \
-      cx<T> va = Ab[oa];                                                                     \
-      if (OPA) va.i = -va.i;                                                                 \
-      ra[r] = oka ? va : cx<T>{0, 0};                                                        \
-      const int kb = OPB ? (e >> 6) : (e & 15), jb = OPB ? (e & 63) : (e >> 4);              \
-      const int gc = col0 + jb, gkb = (K0) + kb;                                             \
-      const bool okb = gc < NC && gkb < K;                                                   \
-      const size_t ob = OPB ? (size_t)(okb ? gc : 0) + (size_t)NC * (okb ? gkb : 0)          \
-                            : (size_t)(okb ? gkb : 0) + (size_t)K * (okb ? gc : 0);          \
-      cx<T> vb = Bb[ob];                                                                     \
-      if (OPB) vb.i = -vb.i;                                                                 \
-      rb[r] = okb ? vb : cx<T>{0, 0};                                                        \
-    }                                                                                        \
-  } while (0)
-#define QOC_BG_STORE(BUF)                                                                    \
-  do {                                                                                       \
-    _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                          \
-      const int e = tid + BG_THREADS * r;                                                    \
-      const int ka = OPA ? (e & 15) : (e >> 6), ia = OPA ? (e >> 4) : (e & 63);              \
-      As[BUF][0][LA::at(ka, ia)] = ra[r].r;                                                  \
-      As[BUF][1][LA::at(ka, ia)] = ra[r].i;                                                  \
-      const int kb = OPB ? (e >> 6) : (e & 15), jb = OPB ? (e & 63) : (e >> 4);              \
-      Bs[BUF][0][LB::at(kb, jb)] = rb[r].r;                                                  \
-      Bs[BUF][1][LB::at(kb, jb)] = rb[r].i;                                                  \
-    }                                                                                        \
-  } while (0)
-
-  v4 cr[2][2], ci[2][2];
+  V sar[KS], sai[KS], sbr[KS], sbi[KS];
+  v4 cr[2][2], ci[2][2], cs[2][2];
 #pragma unroll
   for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y) {
       cr[x][y] = v4{0, 0, 0, 0};
       ci[x][y] = v4{0, 0, 0, 0};
+      cs[x][y] = v4{0, 0, 0, 0};
     }
   const int wr = (wave & 1) * 32, wc = (wave >> 1) * 32;
   const int li = lane & 15, kq = lane >> 4;
-  const int nslab = (K + BG_BK - 1) / BG_BK;
-  QOC_BG_LOAD(0);
-  QOC_BG_STORE(0);
-  __syncthreads();
+  const int nslab = (K + L::BK - 1) / L::BK;
+  bg_load<T, OPA == 1, OPA == 1, KS>(Ab, ldA, row0, 0, M, K, tid, sar, sai);
+  bg_load<T, OPB == 0, OPB == 1, KS>(Bb, ldB, col0, 0, NC, K, tid, sbr, sbi);
+  if (NBUF == 2) {
+    bg_store<T, OPA == 1, KS>(lds + 0 * L::PLANE, lds + 1 * L::PLANE, tid, sar, sai);
+    bg_store<T, OPB == 0, KS>(lds + 2 * L::PLANE, lds + 3 * L::PLANE, tid, sbr, sbi);
+    __syncthreads();
+  }
   for (int s = 0; s < nslab; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nslab) QOC_BG_LOAD((s + 1) * BG_BK);
+    const T* cur = lds + (NBUF == 2 ? (s & 1) : 0) * 4 * L::PLANE;
+    if (NBUF == 1) {
+      if (s > 0) __syncthreads();  // previous slab's fragment reads are done
+      bg_store<T, OPA == 1, KS>(lds + 0 * L::PLANE, lds + 1 * L::PLANE, tid, sar, sai);
+      bg_store<T, OPB == 0, KS>(lds + 2 * L::PLANE, lds + 3 * L::PLANE, tid, sbr, sbi);
+      __syncthreads();
+    }
+    if (s + 1 < nslab) {
+      bg_load<T, OPA == 1, OPA == 1, KS>(Ab, ldA, row0, (s + 1) * L::BK, M, K, tid, sar, sai);
+      bg_load<T, OPB == 0, OPB == 1, KS>(Bb, ldB, col0, (s + 1) * L::BK, NC, K, tid, sbr, sbi);
+    }
 #pragma unroll
-    for (int kk = 0; kk < BG_BK; kk += 4) {
-      T ar[2], ai[2], br[2], bi[2];
+    for (int q = 0; q < KS; ++q) {
+      V ar[2], ai[2], br[2], bi[2];
 #pragma unroll
       for (int x = 0; x < 2; ++x) {
-        ar[x] = As[buf][0][LA::at(kk + kq, wr + 16 * x + li)];
-        ai[x] = As[buf][1][LA::at(kk + kq, wr + 16 * x + li)];
+        const int o = (wr + 16 * x + li) * L::LDK + 16 * q + 4 * kq;
+        ar[x] = *reinterpret_cast<const V*>(cur + 0 * L::PLANE + o);
+        ai[x] = *reinterpret_cast<const V*>(cur + 1 * L::PLANE + o);
       }
 #pragma unroll
       for (int y = 0; y < 2; ++y) {
-        br[y] = Bs[buf][0][LB::at(kk + kq, wc + 16 * y + li)];
-        bi[y] = Bs[buf][1][LB::at(kk + kq, wc + 16 * y + li)];
+        const int o = (wc + 16 * y + li) * L::LDK + 16 * q + 4 * kq;
+        br[y] = *reinterpret_cast<const V*>(cur + 2 * L::PLANE + o);
+        bi[y] = *reinterpret_cast<const V*>(cur + 3 * L::PLANE + o);
       }
+      if (M3) {
+        V as[2], bs[2];
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+        for (int x = 0; x < 2; ++x) as[x] = ar[x] + ai[x];
 #pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          cr[x][y] = MFT::mma(ar[x], br[y], cr[x][y]);
-          ci[x][y] = MFT::mma(ar[x], bi[y], ci[x][y]);
+        for (int y = 0; y < 2; ++y) bs[y] = br[y] + bi[y];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) {
+              cr[x][y] = MFT::mma(ar[x][t], br[y][t], cr[x][y]);
+              ci[x][y] = MFT::mma(ai[x][t], bi[y][t], ci[x][y]);
+              cs[x][y] = MFT::mma(as[x][t], bs[y][t], cs[x][y]);
+            }
         }
+      } else {
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+        for (int t = 0; t < 4; ++t) {
 #pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          cr[x][y] = MFT::mma(-ai[x], bi[y], cr[x][y]);
-          ci[x][y] = MFT::mma(ai[x], br[y], ci[x][y]);
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) {
+              cr[x][y] = MFT::mma(ar[x][t], br[y][t], cr[x][y]);
+              ci[x][y] = MFT::mma(ar[x][t], bi[y][t], ci[x][y]);
+            }
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) {
+              cr[x][y] = MFT::mma(-ai[x][t], bi[y][t], cr[x][y]);
+              ci[x][y] = MFT::mma(ai[x][t], br[y][t], ci[x][y]);
+            }
         }
+      }
     }
-    if (s + 1 < nslab) QOC_BG_STORE(buf ^ 1);
-    __syncthreads();
+    if (NBUF == 2) {
+      if (s + 1 < nslab) {
+        T* nxt = lds + ((s + 1) & 1) * 4 * L::PLANE;
+        bg_store<T, OPA == 1, KS>(nxt + 0 * L::PLANE, nxt + 1 * L::PLANE, tid, sar, sai);
+        bg_store<T, OPB == 0, KS>(nxt + 2 * L::PLANE, nxt + 3 * L::PLANE, tid, sbr, sbi);
+      }
+      __syncthreads();
+    }
   }
-#undef QOC_BG_LOAD
-#undef QOC_BG_STORE
 
   // ---- fused epilogue ----
   cx<T>* C1 = const_cast<cx<T>*>(opd_ptr<T>(g.C1, item));
   cx<T>* C2 = g.C2.p ? const_cast<cx<T>*>(opd_ptr<T>(g.C2, item)) : nullptr;
+  cx<T>* C3 = g.C3.p ? const_cast<cx<T>*>(opd_ptr<T>(g.C3, item)) : nullptr;
   const cx<T>* Y0 = g.nY > 0 ? opd_ptr<T>(g.Y[0], item) : nullptr;
   const cx<T>* Y1 = g.nY > 1 ? opd_ptr<T>(g.Y[1], item) : nullptr;
   const cx<T>* Y2 = g.nY > 2 ? opd_ptr<T>(g.Y[2], item) : nullptr;
@@ -190,18 +253,36 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
         const int row = row0 + wr + 16 * x + MFT::drow(lane, i);
         if (row < M && col < NC) {
           const size_t o = row + (size_t)M * col;
-          const double pr = cr[x][y][i], pi = ci[x][y][i];
+          double pr, pi;
+          if (M3) {
+            pr = (double)cr[x][y][i] - (double)ci[x][y][i];
+            pi = (double)cs[x][y][i] - (double)cr[x][y][i] - (double)ci[x][y][i];
+          } else {
+            pr = cr[x][y][i];
+            pi = ci[x][y][i];
+          }
           double r1 = g.alpha1 * pr, i1 = g.alpha1 * pi;
           double r2 = g.alpha2 * pr, i2 = g.alpha2 * pi;
-          if (Y0) { const cx<T> v = Y0[o]; r1 += g.w1[0] * v.r; i1 += g.w1[0] * v.i; r2 += g.w2[0] * v.r; i2 += g.w2[0] * v.i; }
-          if (Y1) { const cx<T> v = Y1[o]; r1 += g.w1[1] * v.r; i1 += g.w1[1] * v.i; r2 += g.w2[1] * v.r; i2 += g.w2[1] * v.i; }
-          if (Y2) { const cx<T> v = Y2[o]; r1 += g.w1[2] * v.r; i1 += g.w1[2] * v.i; r2 += g.w2[2] * v.r; i2 += g.w2[2] * v.i; }
+          double r3 = g.alpha3 * pr, i3 = g.alpha3 * pi;
+#define QOC_EPI_Y(YP, t)                                        \
+  if (YP) {                                                     \
+    const cx<T> v = YP[o];                                      \
+    r1 += g.w1[t] * v.r; i1 += g.w1[t] * v.i;                   \
+    r2 += g.w2[t] * v.r; i2 += g.w2[t] * v.i;                   \
+    r3 += g.w3[t] * v.r; i3 += g.w3[t] * v.i;                   \
+  }
+          QOC_EPI_Y(Y0, 0)
+          QOC_EPI_Y(Y1, 1)
+          QOC_EPI_Y(Y2, 2)
+#undef QOC_EPI_Y
           if (row == col) {
             r1 += g.gamma1;
             r2 += g.gamma2;
+            r3 += g.gamma3;
           }
           C1[o] = cx<T>{(T)r1, (T)i1};
           if (C2) C2[o] = cx<T>{(T)r2, (T)i2};
+          if (C3) C3[o] = cx<T>{(T)r3, (T)i3};
           mx += r1 * r1 + i1 * i1;
         }
       }
@@ -216,12 +297,13 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
 // Element-wise kernels
 // ---------------------------------------------------------------------------------------------
 
-// Out_item = sum_{t < nt} w_t Y_t,item + dI * I   (rows x cols per item, leading dimension rows).
+// Out_item = sum_{t < nt} w_t Y_t,item + dI * I   (rows x cols per item, leading dimension rows);
+// optionally a second output Out2 = sum_t w2_t Y_t + dI2 * I from the same reads.
 struct LinArgs {
-  Opd out, Y[4];
-  double w[4];
+  Opd out, out2, Y[4];
+  double w[4], w2[4];
   int nt, rows, cols, nitems;
-  double dI;
+  double dI, dI2;
 };
 
 template <typename T>
@@ -231,17 +313,24 @@ __global__ void k_lincomb(LinArgs a) {
   for (size_t gi = blockIdx.x * (size_t)blockDim.x + threadIdx.x; gi < total; gi += (size_t)gridDim.x * blockDim.x) {
     const int it = (int)(gi / per);
     const size_t e = gi - (size_t)it * per;
-    double r = 0, im = 0;
+    double r = 0, im = 0, r2 = 0, im2 = 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       if (t < a.nt) {
         const cx<T> v = opd_ptr<T>(a.Y[t], it)[e];
         r += a.w[t] * v.r;
         im += a.w[t] * v.i;
+        r2 += a.w2[t] * v.r;
+        im2 += a.w2[t] * v.i;
       }
     }
-    if (a.dI != 0.0 && (int)(e % a.rows) == (int)(e / a.rows)) r += a.dI;
+    const bool diag = (int)(e % a.rows) == (int)(e / a.rows);
+    if (diag) {
+      r += a.dI;
+      r2 += a.dI2;
+    }
     const_cast<cx<T>*>(opd_ptr<T>(a.out, it))[e] = cx<T>{(T)r, (T)im};
+    if (a.out2.p) const_cast<cx<T>*>(opd_ptr<T>(a.out2, it))[e] = cx<T>{(T)r2, (T)im2};
   }
 }
 

@@ -370,16 +370,12 @@ int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
     g = gemm_args(N, N, N, cnt);
     g.A = w(1); g.B = w(1); g.C1 = w(2);
     if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // A4
-    g.A = w(1); g.B = w(2); g.C1 = w(3);
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // A6 = A2 A4
-    LinArgs la;
-    std::memset(&la, 0, sizeof(la));
-    la.rows = N; la.cols = N; la.nitems = cnt; la.nt = 3;
-    la.Y[0] = w(3); la.Y[1] = w(2); la.Y[2] = w(1);
-    la.out = w(4); la.w[0] = C[13]; la.w[1] = C[11]; la.w[2] = C[9];
-    if ((r = big_lincomb<T>(c, la))) return r;  // T1
-    la.out = w(5); la.w[0] = C[12]; la.w[1] = C[10]; la.w[2] = C[8];
-    if ((r = big_lincomb<T>(c, la))) return r;  // T2
+    // A6 = A2 A4, with T1 = c13 A6 + c11 A4 + c9 A2 and T2 = c12 A6 + c10 A4 + c8 A2 from its epilogue
+    g.A = w(1); g.B = w(2); g.C1 = w(3); g.C2 = w(4); g.C3 = w(5);
+    g.nY = 2; g.Y[0] = w(2); g.Y[1] = w(1);
+    g.alpha2 = C[13]; g.w2[0] = C[11]; g.w2[1] = C[9];
+    g.alpha3 = C[12]; g.w3[0] = C[10]; g.w3[1] = C[8];
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
     g = gemm_args(N, N, N, cnt);
     g.A = w(3); g.B = w(4); g.C1 = w(6);
     g.nY = 3; g.Y[0] = w(3); g.Y[1] = w(2); g.Y[2] = w(1);
@@ -402,10 +398,9 @@ int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
     for (int k = 1; k <= npow; ++k) la.Y[k - 1] = w(k);
     la.out = w(6); la.dI = C[1];
     for (int k = 1; k <= npow; ++k) la.w[k - 1] = C[2 * k + 1];
-    if ((r = big_lincomb<T>(c, la))) return r;  // U'
-    la.out = w(7); la.dI = C[0];
-    for (int k = 1; k <= npow; ++k) la.w[k - 1] = C[2 * k];
-    if ((r = big_lincomb<T>(c, la))) return r;  // V
+    la.out2 = w(7); la.dI2 = C[0];
+    for (int k = 1; k <= npow; ++k) la.w2[k - 1] = C[2 * k];
+    if ((r = big_lincomb<T>(c, la))) return r;  // U', V in one pass
   }
   // U = (A/2^s) U';  P = V + U -> w1,  Q = V - U -> w2
   g = gemm_args(N, N, N, cnt);
@@ -429,7 +424,9 @@ int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
   if (!(e0 < 0.9))
     return fail(c, QOC_ERR_UNSUPPORTED,
                 "large-N solve: Newton-Schulz residual %.3g >= 0.9 (generators not skew-Hermitian?)", e0);
-  const double tol = c->prec == QOC_FP64 ? 1e-17 : 1e-8;
+  // stop once the residual bound is below the GEMMs' own rounding level (fp32 K=256 dot products
+  // carry ~1e-6 relative error; fp64 ~1e-15)
+  const double tol = c->prec == QOC_FP64 ? 1e-16 : 1e-7;
   int iters = 1;
   for (double e = e0 * e0; e > tol && iters < 8; e *= e) ++iters;
   c->ns_iters += iters;
@@ -563,31 +560,52 @@ int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
       return mk_opd(c->d_ws, offQ + (b - 1) * Nm, esz, (long long)((o - 1) * Nm));
     };
     auto Wa = [&](int a) { return mk_opd(c->d_ws, offW + a * Nm, esz, (long long)(o * Nm)); };
+    const Opd xk = mk_opd(c->d_X, 0, esz, (long long)Nm, Nt, (long long)(Nt + 1) * Nm, (int)u0);
     LinArgs la;
     std::memset(&la, 0, sizeof(la));
-    la.rows = N; la.cols = m; la.nitems = cnt; la.nt = 1; la.w[0] = 1.0;
-    la.Y[0] = mk_opd(c->d_X, 0, esz, (long long)Nm, Nt, (long long)(Nt + 1) * Nm, (int)u0);
-    la.out = Pa(0);
-    if ((r = big_lincomb<T>(c, la))) return r;  // P_0 = x_k
+    if (o == 1) {
+      la.rows = N; la.cols = m; la.nitems = cnt; la.nt = 1; la.w[0] = 1.0;
+      la.Y[0] = xk; la.out = Pa(0);
+      if ((r = big_lincomb<T>(c, la))) return r;  // P_0 = x_k
+    }
     for (int a = 1; a < o; ++a) {
       GemmArgs g = gemm_args(N, N, m, cnt);
-      g.A = Xk; g.B = Pa(a - 1); g.C1 = Pa(a);
+      g.A = Xk; g.B = a == 1 ? xk : Pa(a - 1); g.C1 = Pa(a);
+      if (a == 1) {  // P_0 = x_k copied into the stacked P from this GEMM's epilogue
+        g.C2 = Pa(0); g.alpha2 = 0.0; g.nY = 1; g.Y[0] = xk; g.w2[0] = 1.0;
+      }
       if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // P_a = X P_{a-1}
     }
+    if (o == 3) {
+      // Q_1 = X^H λ  (+ W_2 = λ/6 from the epilogue);  X^H Q_1 -> W_0 = λ + Q_1/2 + Q_2/6, W_1 = λ/2 + Q_1/6
+      GemmArgs g = gemm_args(N, N, m, cnt);
+      g.A = Xk; g.B = Qb(0); g.C1 = Qb(1);
+      g.C2 = Wa(2); g.alpha2 = 0.0; g.nY = 1; g.Y[0] = Qb(0); g.w2[0] = 1.0 / 6;
+      if ((r = big_gemm<T>(c, 1, 0, g))) return r;
+      g = gemm_args(N, N, m, cnt);
+      g.A = Xk; g.B = Qb(1);
+      g.nY = 2; g.Y[0] = Qb(0); g.Y[1] = Qb(1);
+      g.C1 = Wa(0); g.alpha1 = 1.0 / 6; g.w1[0] = 1.0; g.w1[1] = 0.5;
+      g.C2 = Wa(1); g.alpha2 = 0.0; g.w2[0] = 0.5; g.w2[1] = 1.0 / 6;
+      if ((r = big_gemm<T>(c, 1, 0, g))) return r;
+    } else {
     for (int b = 1; b < o; ++b) {
       GemmArgs g = gemm_args(N, N, m, cnt);
       g.A = Xk; g.B = Qb(b - 1); g.C1 = Qb(b);
       if ((r = big_gemm<T>(c, 1, 0, g))) return r;  // Q_b = X^H Q_{b-1}
     }
-    for (int a = 0; a < o; ++a) {
+    for (int a = 0; a < o; a += 2) {  // W_a = sum_b Q_b/(a+b+1)!, two W's per pass
       std::memset(&la, 0, sizeof(la));
       la.rows = N; la.cols = m; la.nitems = cnt; la.nt = o - a;
       for (int b = 0; b < o - a; ++b) {
         la.Y[b] = Qb(b);
         la.w[b] = inv_fact[a + b + 1];
+        la.w2[b] = b < o - a - 1 ? inv_fact[a + b + 2] : 0.0;
       }
       la.out = Wa(a);
-      if ((r = big_lincomb<T>(c, la))) return r;  // W_a = sum_b Q_b/(a+b+1)!
+      if (a + 1 < o) la.out2 = Wa(a + 1);
+      if ((r = big_lincomb<T>(c, la))) return r;
+    }
     }
     GemmArgs g = gemm_args(N, o * m, N, cnt);
     g.A = mk_opd(c->d_ws, offW, esz, (long long)(o * Nm));

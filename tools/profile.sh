@@ -9,7 +9,7 @@ TAG=${2:-r01}
 OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-STEPS=3
+STEPS=${STEPS:-3}
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run -f csv -- \
   python3 bench.py --config "$CFG" --steps $STEPS --warmup 1 --no-cpu > "$OUT/bench_trace.json" 2> "$OUT/trace.log"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run -f csv -- \
