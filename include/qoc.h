@@ -77,6 +77,19 @@ int qoc_grape_sensitivity_dev(qoc_ctx* ctx, const double* d_u, int dUkdp_order, 
 /* One GRAPE gradient eval = f + f_grad of examples/ipopt_callbacks_exp.jl:11-31 (no spline map). */
 int qoc_eval_dev(qoc_ctx* ctx, const double* d_u, int dUkdp_order, double* d_J, double* d_dJdu);
 
+/* Spline parameterisation of the controls, the optimisation variables of the Ipopt callbacks
+ * (examples/ipopt_callbacks_exp.jl:13-14, 28): u_b = transpose(Bs * c_b), dJdc_b = Bs' * transpose(dJdu_b).
+ * Bs is Nt x ns column-major (Julia Matrix); c_b is ns x nu column-major (reshape(c, nsplines, nu)),
+ * seeds contiguous (B x ns x nu). */
+int qoc_set_spline_basis(qoc_ctx* ctx, const double* Bs, int ns);
+/* f + f_grad of examples/ipopt_callbacks_exp.jl:11-31 in the coefficients, device pointers. */
+int qoc_eval_spline_dev(qoc_ctx* ctx, const double* d_c, int dUkdp_order, double* d_J, double* d_dJdc);
+/* Host-pointer variant (J_out: B, dJdc_out: B x ns x nu). */
+int qoc_eval_spline(qoc_ctx* ctx, const double* c, int dUkdp_order, double* J_out, double* dJdc_out);
+/* Constraints g = [norm(c), norm(diff(c, dims=1))] and their Jacobian (examples/ipopt_callbacks_exp.jl:33-51),
+ * device pointers: d_g (B x 2), d_gjac (B x 2 x nc, constraint-major = Ipopt's dense triplet order; may be NULL). */
+int qoc_spline_constraints_dev(qoc_ctx* ctx, const double* d_c, double* d_g, double* d_gjac);
+
 /* Lazy readback of cache fields (test/test_gradient_computation.jl:84,86 read cache.x / cache.λ). */
 int qoc_get_states(qoc_ctx* ctx, int seed, int k, double* x_out);       /* k in [0,Nt], -1 = final */
 int qoc_get_costates(qoc_ctx* ctx, int seed, int k, double* lam_out);

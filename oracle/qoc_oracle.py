@@ -440,3 +440,41 @@ def eval_flops(N, m, nu, degrees, order=3):
         f += 8 * N ** 3 * (GEMMS_PER_DEGREE[d] + s) + (40.0 / 3.0) * N ** 3 + 8 * N ** 2 * m
         f += 8 * N ** 2 * m + 8 * N ** 3 * gj * nu + 8 * N ** 2 * m * nu
     return f
+
+
+# ---------------------------------------------------------------------------
+# Spline map + constraint callbacks (examples/ipopt_callbacks_exp.jl:11-51)
+# ---------------------------------------------------------------------------
+def spline_eval(A0, A, Bs, c, x0, x_target, n=None, order=3, penalty=None):
+    """f(c) and f_grad(c) of setup_ipopt_callbacks.
+
+    c is the optimisation vector (ns*nu,), reshaped to ns x nu column-major (:13);
+    u = transpose(Bs*c) (:14); dJdc = Bs' * transpose(dJdu) (:28), returned flattened (:30).
+    """
+    Bs = np.asarray(Bs, dtype=np.float64)
+    ns = Bs.shape[1]
+    C = np.asarray(c, dtype=np.float64).reshape(ns, -1, order="F")
+    u = (Bs @ C).T
+    J, dJdu, _ = grape_eval(A0, A, u, x0, x_target, n, order=order, penalty=penalty)
+    dJdc = Bs.T @ dJdu.T
+    return J, dJdc.ravel(order="F")
+
+
+def spline_constraints(c, ns):
+    """g = [norm(c), norm(diff(c, dims=1))] and its dense Jacobian (2 x nc) (:33-51).
+
+    The reference takes the Jacobian with Zygote; at a zero norm this restatement returns a zero
+    row (the subgradient ChainRules' norm rule returns there).
+    """
+    c = np.asarray(c, dtype=np.float64)
+    C = c.reshape(ns, -1, order="F")
+    D = np.diff(C, axis=0)
+    g = np.array([np.linalg.norm(C), np.linalg.norm(D)])
+    J = np.zeros((2, c.size))
+    if g[0] > 0:
+        J[0] = c / g[0]
+    if g[1] > 0:
+        Dp = np.zeros((ns + 1, C.shape[1]))
+        Dp[1:ns] = D
+        J[1] = (Dp[:ns] - Dp[1:]).ravel(order="F") / g[1]
+    return g, J

@@ -19,6 +19,7 @@
 #include "qoc_bgemm.hpp"
 #include "qoc_chain.hpp"
 #include "qoc_expm.hpp"
+#include "qoc_spline.hpp"
 
 using namespace qoc;
 
@@ -80,6 +81,10 @@ struct qoc_ctx {
   long long big_hist[5 * 64] = {};
   long long ns_iters = 0;       // Newton-Schulz iterations executed (all chunks)
   size_t dev_bytes = 0;
+  // spline parameterisation (examples/ipopt_callbacks_exp.jl:13-14, 28)
+  double* d_Bs = nullptr;  // Nt x ns
+  int ns = 0;
+  double* d_cstage = nullptr;  // host-pointer variants: B x ns x nu coefficients / gradient
   bool have_gen = false, have_x0 = false, have_cost = false, have_prop = false;
   std::string err;
 };
@@ -727,7 +732,7 @@ void qoc_destroy(qoc_ctx* c) {
   hipSetDevice(c->dev);
   if (c->stream) hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
-                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red};
+                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& m : c->marks) {
@@ -995,6 +1000,69 @@ int qoc_gemm_stats(qoc_ctx* c, double* ms, long long* launches, double* flops, i
     c->gemm_flops = 0;
     c->gemm_n = 0;
   }
+  return QOC_OK;
+}
+
+int qoc_set_spline_basis(qoc_ctx* c, const double* Bs, int ns) {
+  if (!c || !Bs) return fail(c, QOC_ERR_ARG, "null argument");
+  if (ns < 1) return fail(c, QOC_ERR_ARG, "nsplines must be >= 1 (got %d)", ns);
+  HIPCHK(c, hipSetDevice(c->dev));
+  if (c->d_Bs) HIPCHK(c, hipFree(c->d_Bs));
+  if (c->d_cstage) HIPCHK(c, hipFree(c->d_cstage));
+  c->d_Bs = nullptr;
+  c->d_cstage = nullptr;
+  HIPCHK(c, hipMalloc((void**)&c->d_Bs, (size_t)c->Nt * ns * sizeof(double)));
+  HIPCHK(c, hipMalloc((void**)&c->d_cstage, (size_t)2 * c->B * ns * c->nu * sizeof(double)));
+  HIPCHK(c, hipMemcpy(c->d_Bs, Bs, (size_t)c->Nt * ns * sizeof(double), hipMemcpyHostToDevice));
+  c->ns = ns;
+  return QOC_OK;
+}
+
+int qoc_eval_spline_dev(qoc_ctx* c, const double* d_c, int order, double* d_J, double* d_dJdc) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  if (!c->ns) return fail(c, QOC_ERR_STATE, "spline basis not set (qoc_set_spline_basis)");
+  if (!d_c) return fail(c, QOC_ERR_ARG, "d_c is null");
+  HIPCHK(c, hipSetDevice(c->dev));
+  const long long nuT = (long long)c->B * c->Nt * c->nu;
+  const unsigned blocks = (unsigned)std::min<long long>((nuT + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_spline_u, dim3(blocks), dim3(256), 0, c->stream, c->B, c->Nt, c->ns, c->nu, c->d_Bs, d_c,
+                     c->d_u);
+  HIPCHK(c, hipGetLastError());
+  int r = qoc_eval_dev(c, c->d_u, order, d_J, c->d_dJdu);
+  if (r) return r;
+  if (d_dJdc) {
+    const long long outs = (long long)c->B * c->ns * c->nu;
+    const unsigned gb = (unsigned)std::min<long long>((outs * 64 + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_spline_grad, dim3(gb), dim3(256), 0, c->stream, c->B, c->Nt, c->ns, c->nu, c->d_Bs,
+                       c->d_dJdu, d_dJdc);
+    HIPCHK(c, hipGetLastError());
+  }
+  return QOC_OK;
+}
+
+int qoc_eval_spline(qoc_ctx* c, const double* coef, int order, double* J_out, double* dJdc_out) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  if (!c->ns) return fail(c, QOC_ERR_STATE, "spline basis not set (qoc_set_spline_basis)");
+  if (!coef) return fail(c, QOC_ERR_ARG, "c is null");
+  HIPCHK(c, hipSetDevice(c->dev));
+  const size_t nc = (size_t)c->B * c->ns * c->nu;
+  HIPCHK(c, hipMemcpyAsync(c->d_cstage, coef, nc * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  int r = qoc_eval_spline_dev(c, c->d_cstage, order, c->d_J, dJdc_out ? c->d_cstage + nc : nullptr);
+  if (r) return r;
+  if (J_out) HIPCHK(c, hipMemcpyAsync(J_out, c->d_J, c->B * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (dJdc_out)
+    HIPCHK(c, hipMemcpyAsync(dJdc_out, c->d_cstage + nc, nc * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return QOC_OK;
+}
+
+int qoc_spline_constraints_dev(qoc_ctx* c, const double* d_c, double* d_g, double* d_gjac) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  if (!c->ns) return fail(c, QOC_ERR_STATE, "spline basis not set (qoc_set_spline_basis)");
+  if (!d_c || !d_g) return fail(c, QOC_ERR_ARG, "null argument");
+  HIPCHK(c, hipSetDevice(c->dev));
+  hipLaunchKernelGGL(k_spline_constraints, dim3(c->B), dim3(256), 0, c->stream, c->ns, c->nu, d_c, d_g, d_gjac);
+  HIPCHK(c, hipGetLastError());
   return QOC_OK;
 }
 

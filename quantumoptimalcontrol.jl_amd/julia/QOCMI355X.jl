@@ -150,4 +150,66 @@ function setup_state_penalty(inds_penalty, inds_css, μ)
     return L, PenaltyGrad(collect(inds_penalty), collect(inds_css), Float64(μ))
 end
 
+"""
+    setup_ipopt_callbacks(A0Δt, A1Δt, A2Δt, x0, u_prototype, (Jfinal, dJfinal_dx), (L, dL_dx), B; x_target, n)
+
+GPU version of examples/ipopt_callbacks_exp.jl:1-54 for the trace infidelity: f / f_grad evaluate
+u = transpose(B*c), the propagation and the sensitivity in one `qoc_eval_spline` call (the spline map
+runs on the device); g / g_jac are the reference's norm constraints.  Returns the same tuple.
+"""
+function setup_ipopt_callbacks(A0Δt, A1Δt, A2Δt, x0, u_prototype, (Jfinal, dJfinal_dx), (L, dL_dx), B;
+                               x_target, n)
+    nu = size(u_prototype, 1)
+    ng = 2
+    nx = length(x0)
+    nsplines = size(B, 2)
+    nc = nu * nsplines
+    Nt = size(B, 1)
+    ref = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:qoc_create, libqoc), Cint, (Ref{Ptr{Cvoid}}, Cint, Cint, Cint, Cint, Cint, Cint, Cint),
+                ref, 0, size(A0Δt, 1), size(x0, 2), nu, Nt, 1, QOC_FP64), C_NULL)
+    cache = MI355XCache(ref[], size(A0Δt, 1), size(x0, 2), nu, Nt)
+    upload!(cache, A0Δt, [A1Δt, A2Δt], complex(x0))
+    Xt = Matrix{ComplexF64}(x_target)
+    check(ccall((:qoc_set_cost, libqoc), Cint, (Ptr{Cvoid}, Cint, Ptr{ComplexF64}, Cdouble),
+                cache.ctx, QOC_COST_TRACE, Xt, n), cache.ctx)
+    Bm = Matrix{Float64}(B)
+    check(ccall((:qoc_set_spline_basis, libqoc), Cint, (Ptr{Cvoid}, Ptr{Float64}, Cint),
+                cache.ctx, Bm, nsplines), cache.ctx)
+    c_prev = fill(NaN, nc)
+    J = Ref{Cdouble}(0.0)
+    dJdc = zeros(nc)
+    evaluate!(c) = check(ccall((:qoc_eval_spline, libqoc), Cint,
+                               (Ptr{Cvoid}, Ptr{Float64}, Cint, Ref{Cdouble}, Ptr{Float64}),
+                               cache.ctx, c, 3, J, dJdc), cache.ctx)
+    f = function (c::Vector{Float64})
+        c_prev .= c
+        evaluate!(c)
+        J[]
+    end
+    f_grad = function (c, f_grad_out)
+        c_prev == c || evaluate!(c)
+        f_grad_out .= dJdc
+    end
+    g_oop = function (c)
+        cm = reshape(c, nsplines, nu)
+        [sqrt(sum(abs2, cm)); sqrt(sum(abs2, diff(cm, dims=1)))]
+    end
+    g = (c, g_out) -> (g_out .= g_oop(c))
+    function g_jac(c, mode, rows, cols, g_jac_out)
+        if mode == :Structure
+            cols .= kron(ones(ng), 1:nc)
+            rows .= kron(1:ng, ones(nc))
+        else
+            cm = reshape(c, nsplines, nu)
+            g0, g1 = g_oop(c)
+            D = zeros(nsplines + 1, nu)
+            D[2:nsplines, :] .= diff(cm, dims=1)
+            j1 = (D[1:nsplines, :] .- D[2:end, :])[:]
+            g_jac_out .= [g0 > 0 ? c ./ g0 : zero(c); g1 > 0 ? j1 ./ g1 : zero(j1)]
+        end
+    end
+    f, g, f_grad, g_jac, nu, ng, nx, nc, cache
+end
+
 end # module

@@ -49,6 +49,10 @@ SIGNATURES = {
     "qoc_phase_times": (C.c_int, [_vp, _dp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_pade_histogram": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_get_info": (C.c_int, [_vp, C.POINTER(C.c_longlong)]),
+    "qoc_set_spline_basis": (C.c_int, [_vp, _dp, C.c_int]),
+    "qoc_eval_spline_dev": (C.c_int, [_vp, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "qoc_eval_spline": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp]),
+    "qoc_spline_constraints_dev": (C.c_int, [_vp, C.c_void_p, C.c_void_p, C.c_void_p]),
     "qoc_gemm_stats": (C.c_int, [_vp, _dp, C.POINTER(C.c_longlong), _dp, C.c_int]),
     "qoc_expm_batched": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _ip]),
     "qoc_expm_jacobian": (C.c_int, [C.c_int, C.c_int, C.c_int, _dp, C.POINTER(_dp), _dp, C.c_int, C.c_double, _dp]),

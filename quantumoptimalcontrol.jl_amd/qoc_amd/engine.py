@@ -166,6 +166,33 @@ class GrapeEngine:
     def grape_sensitivity_device(self, d_u: int, order: int, d_dJdu: int):
         self._chk(self._lib.qoc_grape_sensitivity_dev(self._h, C.c_void_p(d_u), int(order), C.c_void_p(d_dJdu)))
 
+    # ---- spline parameterisation (examples/ipopt_callbacks_exp.jl:13-14, 28, 33-51) --------
+    def set_spline_basis(self, Bs):
+        """Bs: Nt x ns basis matrix (u_b = transpose(Bs c_b))."""
+        Bs = np.asarray(Bs, dtype=np.float64)
+        if Bs.ndim != 2 or Bs.shape[0] != self.Nt:
+            raise ValueError(f"spline basis must be Nt x ns with Nt={self.Nt}, got {Bs.shape}")
+        self.ns = Bs.shape[1]
+        self._chk(self._lib.qoc_set_spline_basis(self._h, _ptr(np.asfortranarray(Bs).ravel(order="F")), self.ns))
+
+    def eval_spline(self, c, order: int = 3):
+        """c: (B, ns, nu) coefficients (Julia reshape(c, nsplines, nu) per seed) -> J (B,), dJdc (B, ns, nu)."""
+        c = np.asarray(c, dtype=np.float64).reshape(self.B, self.ns, self.nu)
+        cf = np.ascontiguousarray(np.transpose(c, (0, 2, 1)))  # column-major per seed
+        J = np.zeros(self.B)
+        g = np.zeros_like(cf)
+        self._chk(self._lib.qoc_eval_spline(self._h, _ptr(cf), int(order), _ptr(J), _ptr(g)))
+        return J, np.transpose(g, (0, 2, 1)).copy()
+
+    def eval_spline_device(self, d_c: int, order: int, d_J: int, d_dJdc: int):
+        """Device pointers: c and dJdc are B x nu x ns doubles (column-major ns x nu per seed)."""
+        self._chk(self._lib.qoc_eval_spline_dev(self._h, C.c_void_p(d_c), int(order), C.c_void_p(d_J),
+                                                C.c_void_p(d_dJdc)))
+
+    def spline_constraints_device(self, d_c: int, d_g: int, d_gjac: int = 0):
+        self._chk(self._lib.qoc_spline_constraints_dev(self._h, C.c_void_p(d_c), C.c_void_p(d_g),
+                                                       C.c_void_p(d_gjac) if d_gjac else None))
+
     def stream(self) -> int:
         return self._lib.qoc_stream(self._h)
 
