@@ -10,10 +10,12 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad")
+KERNELS = ("k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad", "k_bgemm", "k_form_norm", "k_lincomb", "k_gen_contract")
 
 
-def short(name):
+def short(name, variants=False):
+    if variants and "k_bgemm<" in name:
+        return "k_bgemm<" + name.split("k_bgemm<", 1)[1].split(">", 1)[0] + ">"
     for k in KERNELS:
         if k in name:
             return k
@@ -45,10 +47,10 @@ def main(out_dir, cfg, tag, repo="."):
     write = pmc(os.path.join(out_dir, "pmc_write"))
     sq = pmc(os.path.join(out_dir, "pmc_sq"))
     lines = [f"# rocprofv3 summary — {tag}, config `{cfg}`", "",
-             f"Source: `{src}` (kernel-trace --stats of `bench.py --config {cfg} --steps 3 --warmup 1 --no-cpu`).", "",
+             f"Source: `{src}` (kernel-trace --stats of `bench.py --config {cfg} --warmup 1 --no-cpu` (tools/profile*.sh)).", "",
              "| kernel | calls | avg ms | total ms | % |", "|---|---|---|---|---|"]
     for r in rows:
-        name = short(r.get("Name", r.get("KernelName", "")))
+        name = short(r.get("Name", r.get("KernelName", "")), variants=True)
         calls = r.get("Calls", "")
         avg = float(r.get("AverageNs", 0)) / 1e6
         tot = float(r.get("TotalDurationNs", 0)) / 1e6
@@ -69,13 +71,14 @@ def main(out_dir, cfg, tag, repo="."):
         traffic[k] = b
         lines.append(f"| {k} | {fm:.0f} | {wm:.0f} | {b / 1e9:.3f} GB |")
     if sq:
-        lines += ["", "| kernel | SQ_INSTS_VALU | SQ_INSTS_MFMA | SQ_INSTS_LDS | SQ_WAVES |", "|---|---|---|---|---|"]
+        names = sorted({n for c in sq.values() for n in c})
+        lines += ["", "SQ counters (mean per launch):", "", "| kernel | " + " | ".join(names) + " |",
+                  "|---|" + "---|" * len(names)]
         for k in KERNELS:
             c = sq.get(k)
             if c:
                 m = {n: (sum(v) / len(v)) for n, v in c.items()}
-                lines.append(f"| {k} | {m.get('SQ_INSTS_VALU', 0):.3g} | {m.get('SQ_INSTS_MFMA', 0):.3g} | "
-                             f"{m.get('SQ_INSTS_LDS', 0):.3g} | {m.get('SQ_WAVES', 0):.3g} |")
+                lines.append(f"| {k} | " + " | ".join(f"{m.get(n, 0):.3g}" for n in names) + " |")
     os.makedirs(os.path.join(repo, "profiles"), exist_ok=True)
     open(os.path.join(repo, "profiles", f"{tag}_{cfg}.md"), "w").write("\n".join(lines) + "\n")
     if traffic:
