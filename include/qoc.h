@@ -35,6 +35,11 @@ extern "C" {
 #define QOC_FP64 0
 #define QOC_FP32 1
 
+/* dUkdp_order: 1..4 = truncated Taylor series of expm_jacobian! (src/gradient_computations.jl:177-213,
+ * the reference's definition; 3 in the Ipopt path); QOC_DUKDP_EXACT = exact Fréchet derivative of the
+ * propagator (opt-in, SURVEY.md §8f item 2: one 2N x 2N block exponential per slice). */
+#define QOC_DUKDP_EXACT 0
+
 #define QOC_COST_TRACE 0     /* J = 1-|tr(X'x)|^2/n^2            (src/penalty_fcns.jl:15-24) */
 #define QOC_COST_ZCAL 1      /* z-calibrated, 4 columns           (src/penalty_fcns.jl:27-42, src/fidelities.jl:48-137) */
 #define QOC_COST_EXTERNAL 2  /* caller supplies lambda_final      (any Julia closure dJfinal_dx) */

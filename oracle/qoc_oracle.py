@@ -193,6 +193,23 @@ def expm_jacobian(A0, A, p, order=2, dt=1.0) -> list:
     return out
 
 
+def expm_frechet_block(A, E):
+    """(exp(A), L(A, E)) from the block exponential exp([[A, E], [0, A]]) = [[e^A, L], [0, e^A]].
+
+    The opt-in exact gradient mode (``dUkdp_order = "exact"``): the Fréchet
+    derivative replaces the truncated Taylor series of expm_jacobian! (src/gradient_computations.jl:
+    177-213).  The block exponential uses the same Higham-2005 Padé as the forward pass.
+    """
+    A = np.asarray(A, dtype=np.complex128)
+    n = A.shape[0]
+    M = np.zeros((2 * n, 2 * n), dtype=np.complex128)
+    M[:n, :n] = A
+    M[n:, n:] = A
+    M[:n, n:] = E
+    X, _, _ = expm_higham2005(M)
+    return X[:n, :n], X[:n, n:]
+
+
 def compute_u_sensitivity(xk, lam_kp1, dU) -> float:
     """sum_l Re(lam[:,l]' dU x[:,l]) (src/gradient_computations.jl:217-223)."""
     return float(np.real(np.sum(np.conj(lam_kp1) * (dU @ xk))))
@@ -215,7 +232,11 @@ def grape_sensitivity(A0, A, dJfinal_dx, u, x0, cache: GrapeCache, dUkdp_order=3
         if dL_dx is not None:
             lam[k] = lam[k] + dL_dx(x[k])
     for k in range(Nt - 1, -1, -1):                                       # :65-74
-        dU = expm_jacobian(A0, A, u[:, k], order=dUkdp_order)
+        if dUkdp_order == "exact":
+            Ak = np.asarray(A0, dtype=np.complex128) + sum(u[j, k] * np.asarray(A[j]) for j in range(len(A)))
+            dU = [expm_frechet_block(Ak, Aj)[1] for Aj in A]
+        else:
+            dU = expm_jacobian(A0, A, u[:, k], order=dUkdp_order)
         for j in range(len(A)):
             cache.dJdu[j, k] = compute_u_sensitivity(x[k], lam[k + 1], dU[j])
     return cache.dJdu

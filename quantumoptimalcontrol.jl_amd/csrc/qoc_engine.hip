@@ -19,6 +19,7 @@
 #include "qoc_bgemm.hpp"
 #include "qoc_chain.hpp"
 #include "qoc_expm.hpp"
+#include "qoc_frechet.hpp"
 #include "qoc_spline.hpp"
 
 using namespace qoc;
@@ -85,6 +86,9 @@ struct qoc_ctx {
   double* d_Bs = nullptr;  // Nt x ns
   int ns = 0;
   double* d_cstage = nullptr;  // host-pointer variants: B x ns x nu coefficients / gradient
+  // exact (Fréchet) gradient mode workspace, allocated on first use
+  void* d_fws = nullptr;
+  size_t fws_bytes = 0;
   bool have_gen = false, have_x0 = false, have_cost = false, have_prop = false;
   std::string err;
 };
@@ -218,6 +222,9 @@ void mark_end(qoc_ctx* c, int idx) {
 }
 
 template <typename T>
+int frechet_grad(qoc_ctx* c, double* d_dJdu);
+
+template <typename T>
 int run_forward(qoc_ctx* c) {
   int mk = mark_begin(c, 0);
   hipError_t e = launch_expm(c->prec, c->stream, c->N, c->nu, c->B * c->Nt, c->d_A, c->d_u, nullptr, c->d_U,
@@ -246,6 +253,12 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
                      (const cx<double>*)c->d_coef, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu);
   mark_end(c, mk);
   HIPCHK(c, hipGetLastError());
+  if (order == QOC_DUKDP_EXACT) {
+    mk = mark_begin(c, 3);
+    int r = frechet_grad<T>(c, d_dJdu);
+    mark_end(c, mk);
+    return r;
+  }
   lds = grad_lds(c, order);
   HIPCHK(c, hipFuncSetAttribute((const void*)k_grad<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   mk = mark_begin(c, 3);
@@ -336,22 +349,15 @@ int big_lincomb(qoc_ctx* c, LinArgs a) {
 }
 
 // exp(A_k) for units [u0, u0+cnt) -> d_U.  Workspace buffers w(i), i < 8, of cnt x N x N.
+// exp of cnt explicit n x n matrices (operand Asrc, chunk max 1-norm nA) -> dest, all GEMM:
+// Padé (Higham 2005 degree / squarings for nA) + Newton-Schulz solve + squarings.  Workspace:
+// 8 buffers of ws_items x n x n at ws; red >= cnt doubles.
 template <typename T>
-int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
-  const int N = c->N;
+int expm_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, double* red, const Opd& Asrc,
+                    const Opd& dest, double nA, bool count_hist) {
   const size_t NN = (size_t)N * N, esz = c->esz;
-  auto w = [&](int i) { return mk_opd(c->d_ws, (size_t)i * c->chunk * NN, esz, (long long)NN); };
-  auto wp = [&](int i) { return (cx<T>*)((char*)c->d_ws + (size_t)i * c->chunk * NN * esz); };
-  const Opd dest = mk_opd(c->d_U, (size_t)u0 * NN, esz, (long long)NN);
+  auto w = [&](int i) { return mk_opd(ws, (size_t)i * ws_items * NN, esz, (long long)NN); };
   int r;
-  // A_k and max ||A_k||_1 over the chunk
-  HIPCHK(c, hipMemsetAsync(c->d_red, 0, sizeof(double), c->stream));
-  hipLaunchKernelGGL((k_form_norm<T>), dim3(cnt), dim3(256), 0, c->stream, N, c->nu, u0, (const cx<T>*)c->d_A,
-                     (const double*)c->d_u, wp(0), (unsigned long long*)c->d_red);
-  HIPCHK(c, hipGetLastError());
-  double nA = 0.0;
-  HIPCHK(c, hipMemcpyAsync(&nA, c->d_red, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
   // Padé degree / squarings: the thresholds of k_expm (Higham 2005), one (d, s) per chunk chosen
   // from the chunk's largest norm (any degree >= the per-slice choice meets the same bound).
   int d, sq = 0;
@@ -363,13 +369,13 @@ int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
     sq = sl > 0 ? (int)std::ceil(sl) : 0;
   }
   const int di = d == 3 ? 0 : d == 5 ? 1 : d == 7 ? 2 : d == 9 ? 3 : 4;
-  c->big_hist[di * 64 + std::min(sq, 63)] += cnt;
+  if (count_hist) c->big_hist[di * 64 + std::min(sq, 63)] += cnt;
   const double* C = d == 3 ? hPade3 : d == 5 ? hPade5 : d == 7 ? hPade7 : d == 9 ? hPade9 : hPade13;
   const double sc = std::ldexp(1.0, -sq);
   GemmArgs g;
   // buffers: 0 A, 1 A2, 2 A4, 3 A6, 4 T1/A8, 5 T2, 6 U', 7 V
   g = gemm_args(N, N, N, cnt);
-  g.A = w(0); g.B = w(0); g.C1 = w(1); g.alpha1 = sc * sc;
+  g.A = Asrc; g.B = Asrc; g.C1 = w(1); g.alpha1 = sc * sc;
   if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // A2
   if (d == 13) {
     g = gemm_args(N, N, N, cnt);
@@ -409,7 +415,7 @@ int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
   }
   // U = (A/2^s) U';  P = V + U -> w1,  Q = V - U -> w2
   g = gemm_args(N, N, N, cnt);
-  g.A = w(0); g.B = w(6); g.C1 = w(1); g.C2 = w(2);
+  g.A = Asrc; g.B = w(6); g.C1 = w(1); g.C2 = w(2);
   g.alpha1 = sc; g.alpha2 = -sc;
   g.nY = 1; g.Y[0] = w(7); g.w1[0] = 1.0; g.w2[0] = 1.0;
   if ((r = big_gemm<T>(c, 0, 0, g))) return r;
@@ -417,12 +423,12 @@ int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
   // For A = -i H dt, P = conj-adjoint partner of Q and R0 = I - QP/c0^2 is tiny; ||R0||_F (computed
   // in the GEMM epilogue) fixes the iteration count: smallest k with ||R0||^(2^k) <= tol.
   const double c0sq = C[0] * C[0];
-  HIPCHK(c, hipMemsetAsync(c->d_red, 0, (size_t)cnt * sizeof(double), c->stream));
+  HIPCHK(c, hipMemsetAsync(red, 0, (size_t)cnt * sizeof(double), c->stream));
   g = gemm_args(N, N, N, cnt);
-  g.A = w(2); g.B = w(1); g.C1 = w(3); g.alpha1 = -1.0 / c0sq; g.gamma1 = 1.0; g.sumsq = c->d_red;
+  g.A = w(2); g.B = w(1); g.C1 = w(3); g.alpha1 = -1.0 / c0sq; g.gamma1 = 1.0; g.sumsq = red;
   if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // R0 -> w3
   std::vector<double> ss(cnt);
-  HIPCHK(c, hipMemcpyAsync(ss.data(), c->d_red, (size_t)cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(ss.data(), red, (size_t)cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   double e0 = 0.0;
   for (double v : ss) e0 = std::max(e0, std::sqrt(v));
@@ -465,6 +471,23 @@ int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
     xb = nb;
   }
   return QOC_OK;
+}
+
+// exp(A_k) for units [u0, u0+cnt) -> d_U (forms A_k from the generators, chunk max norm, then the GEMM expm)
+template <typename T>
+int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
+  const int N = c->N;
+  const size_t NN = (size_t)N * N, esz = c->esz;
+  cx<T>* a0 = (cx<T>*)c->d_ws;
+  HIPCHK(c, hipMemsetAsync(c->d_red, 0, sizeof(double), c->stream));
+  hipLaunchKernelGGL((k_form_norm<T>), dim3(cnt), dim3(256), 0, c->stream, N, c->nu, u0, (const cx<T>*)c->d_A,
+                     (const double*)c->d_u, a0, (unsigned long long*)c->d_red);
+  HIPCHK(c, hipGetLastError());
+  double nA = 0.0;
+  HIPCHK(c, hipMemcpyAsync(&nA, c->d_red, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return expm_gemm_chunk<T>(c, N, cnt, c->d_ws, (size_t)c->chunk, c->d_red, mk_opd(c->d_ws, 0, esz, (long long)NN),
+                            mk_opd(c->d_U, (size_t)u0 * NN, esz, (long long)NN), nA, true);
 }
 
 template <typename T>
@@ -546,6 +569,11 @@ int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
   }
   mark_end(c, mk);
   mk = mark_begin(c, 3);
+  if (order == QOC_DUKDP_EXACT) {
+    r = frechet_grad<T>(c, d_dJdu);
+    mark_end(c, mk);
+    return r;
+  }
   // gradient, per chunk of slice units
   const long long units = (long long)B * Nt;
   const int o = order;
@@ -622,6 +650,73 @@ int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
     HIPCHK(c, hipGetLastError());
   }
   mark_end(c, mk);
+  return QOC_OK;
+}
+
+// Exact gradient (QOC_DUKDP_EXACT): one Fréchet derivative per slice from the 2N x 2N block exponential
+// (qoc_frechet.hpp), k_expm when 2N fits the LDS-resident kernel, the GEMM pipeline otherwise.
+template <typename T>
+int frechet_grad(qoc_ctx* c, double* d_dJdu) {
+  const int N = c->N, n2 = 2 * N, nu = c->nu;
+  const size_t NN = (size_t)N * N, BB = (size_t)n2 * n2, esz = c->esz;
+  const long long units = (long long)c->B * c->Nt;
+  const bool small = expm_supported(n2, c->prec);
+  const size_t per_item = (small ? 2 : 10) * BB * esz + 3 * sizeof(double);
+  size_t freeb = 0, totalb = 0;
+  (void)hipMemGetInfo(&freeb, &totalb);
+  const size_t budget = std::min<size_t>(4ull << 30, std::max<size_t>(freeb / 8, per_item));
+  const int fch = (int)std::max<long long>(1, std::min<long long>({(long long)(budget / per_item), units, 16384LL}));
+  const size_t need = (size_t)fch * per_item + nu * NN * esz + 64 * sizeof(double);
+  if (c->fws_bytes < need) {
+    if (c->d_fws) HIPCHK(c, hipFree(c->d_fws));
+    c->d_fws = nullptr;
+    c->fws_bytes = 0;
+    HIPCHK(c, hipMalloc(&c->d_fws, need));
+    c->fws_bytes = need;
+  }
+  char* p = (char*)c->d_fws;
+  cx<T>* blocks = (cx<T>*)p;
+  p += (size_t)fch * BB * esz;
+  cx<T>* E = (cx<T>*)p;
+  p += (size_t)fch * BB * esz;
+  void* ws = nullptr;
+  if (!small) {
+    ws = p;
+    p += 8 * (size_t)fch * BB * esz;
+  }
+  cx<T>* At = (cx<T>*)p;
+  p += nu * NN * esz;
+  double* alpha = (double*)p;
+  p += (size_t)fch * sizeof(double);
+  double* red = (double*)p;  // fch + 8 doubles
+  hipLaunchKernelGGL((k_transpose_gens<T>), dim3(256), dim3(256), 0, c->stream, N, nu, (const cx<T>*)c->d_A, At);
+  HIPCHK(c, hipGetLastError());
+  int r;
+  for (long long u0 = 0; u0 < units; u0 += fch) {
+    const int cnt = (int)std::min<long long>(fch, units - u0);
+    hipLaunchKernelGGL((k_frechet_build<T>), dim3(cnt), dim3(256), 0, c->stream, N, c->m, nu, c->Nt, u0,
+                       (const cx<T>*)c->d_A, (const double*)c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L,
+                       blocks, alpha);
+    HIPCHK(c, hipGetLastError());
+    if (small) {
+      hipError_t e = launch_expm(c->prec, c->stream, n2, 0, cnt, nullptr, nullptr, blocks, E, nullptr, nullptr, nullptr);
+      if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm (Frechet block): %s", hipGetErrorString(e));
+    } else {
+      HIPCHK(c, hipMemsetAsync(red, 0, sizeof(double), c->stream));
+      hipLaunchKernelGGL((k_norm1_max<T>), dim3(cnt), dim3(256), 0, c->stream, n2, (const cx<T>*)blocks,
+                         (unsigned long long*)red);
+      HIPCHK(c, hipGetLastError());
+      double nA = 0.0;
+      HIPCHK(c, hipMemcpyAsync(&nA, red, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if ((r = expm_gemm_chunk<T>(c, n2, cnt, ws, (size_t)fch, red, mk_opd(blocks, 0, esz, (long long)BB),
+                                  mk_opd(E, 0, esz, (long long)BB), nA, false)))
+        return r;
+    }
+    hipLaunchKernelGGL((k_frechet_contract<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)At,
+                       (const cx<T>*)E, (const double*)alpha, d_dJdu);
+    HIPCHK(c, hipGetLastError());
+  }
   return QOC_OK;
 }
 
@@ -732,7 +827,7 @@ void qoc_destroy(qoc_ctx* c) {
   hipSetDevice(c->dev);
   if (c->stream) hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
-                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage};
+                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& m : c->marks) {
@@ -844,7 +939,7 @@ int qoc_grape_sensitivity_dev(qoc_ctx* c, const double* d_u, int order, double* 
   int r = check_ready(c);
   if (r) return r;
   if (!c->have_prop) return fail(c, QOC_ERR_STATE, "grape_sensitivity called before propagate");
-  if (order < 1 || order > 4) return fail(c, QOC_ERR_ARG, "dUkdp_order must be 1..4 (got %d)", order);
+  if (order < 0 || order > 4) return fail(c, QOC_ERR_ARG, "dUkdp_order must be 1..4 or QOC_DUKDP_EXACT (got %d)", order);
   if (c->cost_kind == QOC_COST_EXTERNAL)
     return fail(c, QOC_ERR_STATE, "QOC_COST_EXTERNAL needs qoc_grape_sensitivity (host lambda_final)");
   const size_t nu_t = (size_t)c->B * c->nu * c->Nt;
@@ -865,7 +960,7 @@ int qoc_eval_dev(qoc_ctx* c, const double* d_u, int order, double* d_J, double* 
     return fail(c, QOC_ERR_STATE, "qoc_eval_dev needs a device-side cost (TRACE or ZCAL)");
   int r = qoc_propagate_dev(c, d_u, d_J);
   if (r) return r;
-  if (order < 1 || order > 4) return fail(c, QOC_ERR_ARG, "dUkdp_order must be 1..4 (got %d)", order);
+  if (order < 0 || order > 4) return fail(c, QOC_ERR_ARG, "dUkdp_order must be 1..4 or QOC_DUKDP_EXACT (got %d)", order);
   return backward(c, order, d_dJdu ? d_dJdu : c->d_dJdu);
 }
 
@@ -888,7 +983,7 @@ int qoc_grape_sensitivity(qoc_ctx* c, const double* u, int order, const double* 
   int r = check_ready(c);
   if (r) return r;
   if (!c->have_prop) return fail(c, QOC_ERR_STATE, "grape_sensitivity called before propagate");
-  if (order < 1 || order > 4) return fail(c, QOC_ERR_ARG, "dUkdp_order must be 1..4 (got %d)", order);
+  if (order < 0 || order > 4) return fail(c, QOC_ERR_ARG, "dUkdp_order must be 1..4 or QOC_DUKDP_EXACT (got %d)", order);
   const size_t nu_t = (size_t)c->B * c->nu * c->Nt;
   if (!u) return fail(c, QOC_ERR_ARG, "u is null");
   if (c->h_u.size() == nu_t) {

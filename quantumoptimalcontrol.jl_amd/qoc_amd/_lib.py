@@ -19,6 +19,7 @@ QOC_ERR_STATE = -4
 QOC_ERR_UNSUPPORTED = -5
 QOC_FP64 = 0
 QOC_FP32 = 1
+QOC_DUKDP_EXACT = 0
 QOC_COST_TRACE = 0
 QOC_COST_ZCAL = 1
 QOC_COST_EXTERNAL = 2

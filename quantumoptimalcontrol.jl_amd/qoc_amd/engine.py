@@ -29,6 +29,15 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(_dp)
 
 
+def _order(order) -> int:
+    """dUkdp_order: 1..4 (Taylor, the reference's definition) or "exact" (Fréchet, QOC_DUKDP_EXACT = 0)."""
+    if isinstance(order, str):
+        if order != "exact":
+            raise ValueError(f"dUkdp_order must be 1..4 or 'exact' (got {order!r})")
+        return L.QOC_DUKDP_EXACT
+    return int(order)
+
+
 def _u_layout(u: np.ndarray, B: int, nu: int, Nt: int) -> np.ndarray:
     """(B, nu, Nt) or (nu, Nt) float64 -> contiguous B x (nu x Nt column-major)."""
     u = np.asarray(u, dtype=np.float64)
@@ -150,21 +159,21 @@ class GrapeEngine:
                 lf = lf[None]
             lam = np.concatenate([_cm_complex(x) for x in lf]).view(np.float64)
         out = np.zeros((self.B, self.Nt, self.nu))
-        self._chk(self._lib.qoc_grape_sensitivity(self._h, _ptr(ub), int(order),
+        self._chk(self._lib.qoc_grape_sensitivity(self._h, _ptr(ub), _order(order),
                                                   _ptr(lam) if lam is not None else None, _ptr(out)))
         return np.transpose(out, (0, 2, 1)).copy()
 
     # ---- hot path (device pointers, e.g. torch tensors on cuda) ---------------------
     def eval_device(self, d_u: int, order: int, d_J: int, d_dJdu: int):
         """f + f_grad on device-resident buffers (B x Nt x nu doubles in, B / B x Nt x nu out)."""
-        self._chk(self._lib.qoc_eval_dev(self._h, C.c_void_p(d_u), int(order), C.c_void_p(d_J),
+        self._chk(self._lib.qoc_eval_dev(self._h, C.c_void_p(d_u), _order(order), C.c_void_p(d_J),
                                          C.c_void_p(d_dJdu)))
 
     def propagate_device(self, d_u: int, d_J: int):
         self._chk(self._lib.qoc_propagate_dev(self._h, C.c_void_p(d_u), C.c_void_p(d_J)))
 
     def grape_sensitivity_device(self, d_u: int, order: int, d_dJdu: int):
-        self._chk(self._lib.qoc_grape_sensitivity_dev(self._h, C.c_void_p(d_u), int(order), C.c_void_p(d_dJdu)))
+        self._chk(self._lib.qoc_grape_sensitivity_dev(self._h, C.c_void_p(d_u), _order(order), C.c_void_p(d_dJdu)))
 
     # ---- spline parameterisation (examples/ipopt_callbacks_exp.jl:13-14, 28, 33-51) --------
     def set_spline_basis(self, Bs):
@@ -181,12 +190,12 @@ class GrapeEngine:
         cf = np.ascontiguousarray(np.transpose(c, (0, 2, 1)))  # column-major per seed
         J = np.zeros(self.B)
         g = np.zeros_like(cf)
-        self._chk(self._lib.qoc_eval_spline(self._h, _ptr(cf), int(order), _ptr(J), _ptr(g)))
+        self._chk(self._lib.qoc_eval_spline(self._h, _ptr(cf), _order(order), _ptr(J), _ptr(g)))
         return J, np.transpose(g, (0, 2, 1)).copy()
 
     def eval_spline_device(self, d_c: int, order: int, d_J: int, d_dJdc: int):
         """Device pointers: c and dJdc are B x nu x ns doubles (column-major ns x nu per seed)."""
-        self._chk(self._lib.qoc_eval_spline_dev(self._h, C.c_void_p(d_c), int(order), C.c_void_p(d_J),
+        self._chk(self._lib.qoc_eval_spline_dev(self._h, C.c_void_p(d_c), _order(order), C.c_void_p(d_J),
                                                 C.c_void_p(d_dJdc)))
 
     def spline_constraints_device(self, d_c: int, d_g: int, d_gjac: int = 0):

@@ -36,7 +36,7 @@ class SplineGrape:
     def __init__(self, engine, Bs, order: int = 3):
         import torch
         self.eng = engine
-        self.order = int(order)
+        self.order = order
         engine.set_spline_basis(Bs)
         self.ns, self.nu, self.B = engine.ns, engine.nu, engine.B
         self.nc = self.ns * self.nu

@@ -227,3 +227,40 @@ def test_non_dominant_q_uses_pivoted_lu(built_lib):
         for a, x in zip(A, X):
             Xr, d, s = O.expm_higham2005(a)
             assert np.abs(x - Xr).max() < 1e-13
+
+
+@pytest.mark.parametrize("which", ["zz", "tunable_bus_small"])
+def test_exact_frechet_gradient_matches_oracle(built_lib, which):
+    """QOC_DUKDP_EXACT: zz (2N = 18 -> k_expm block exponentials) and tunable bus (2N = 54 -> the GEMM
+    pipeline); oracle = per-control block exponentials (pinned to scipy expm_frechet and FD)."""
+    from qoc_amd import systems
+    if which == "zz":
+        prob = systems.zz_problem(20, tgate=2.0)
+        u = systems.zz_controls(2, 20, 2.0, seed=3)
+    else:
+        prob = systems.tunable_bus_problem(12, tgate=350.0 * 12 / 2000)
+        u = systems.tunable_bus_controls(2, 12, seed=1)
+    e = _engine(prob, u.shape[0])
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, "exact")
+    for b in range(u.shape[0]):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order="exact")
+        assert abs(J[b] - Jr) <= 1e-12
+        rel = np.linalg.norm(g[b] - gr) / np.linalg.norm(gr)
+        assert rel <= 1e-10, (b, rel)
+    e.close()
+
+
+def test_exact_gradient_large_n_path(built_lib, monkeypatch):
+    from qoc_amd import systems
+    monkeypatch.setenv("QOC_FORCE_LARGE_N", "1")
+    prob = systems.zz_problem(10, tgate=2.0)
+    u = systems.zz_controls(2, 10, 2.0, seed=4)
+    e = _engine(prob, 2)
+    assert e.info()["path"] == "large_n"
+    e.propagate(u)
+    g = e.grape_sensitivity(u, "exact")
+    for b in range(2):
+        _, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order="exact")
+        assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
+    e.close()

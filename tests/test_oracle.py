@@ -290,3 +290,39 @@ def test_c_restatement_matches_numpy():
         X, d, s = cpuref.expm(A)
         Xr, dr, sr = O.expm_higham2005(A)
         assert (d, s) == (dr, sr) and np.abs(X - Xr).max() < 1e-13 * (1 + s)
+
+
+# ---- exact (Fréchet) gradient mode, SURVEY.md §8f item 2 ------------------------------------
+def test_frechet_block_matches_scipy_expm_frechet():
+    from scipy.linalg import expm_frechet
+    rng = np.random.default_rng(11)
+    for n, sc in ((4, 0.1), (9, 1.0), (7, 6.0)):
+        H = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+        A = -1j * sc * (H + H.conj().T) / 2 / n
+        E = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+        X, L = O.expm_frechet_block(A, E)
+        Xs, Ls = expm_frechet(A, E)
+        assert np.abs(X - Xs).max() < 1e-13
+        assert np.abs(L - Ls).max() / np.abs(Ls).max() < 1e-12
+
+
+def test_exact_gradient_matches_finite_differences_and_adjoint_identity():
+    prob = S.zz_problem(12, tgate=3.0)
+    rng = np.random.default_rng(4)
+    u = rng.uniform(-1.5, 1.5, size=(2, prob.Nt))
+    J, g, cache = O.grape_eval(prob.A0, prob.A, u, prob.x0, prob.x_target, prob.n, order="exact")
+    eps = 1e-6
+    for (j, k) in ((0, 0), (1, 5), (0, 11)):
+        up, um = u.copy(), u.copy()
+        up[j, k] += eps
+        um[j, k] -= eps
+        fd = (O.grape_eval(prob.A0, prob.A, up, prob.x0, prob.x_target, prob.n)[0] -
+              O.grape_eval(prob.A0, prob.A, um, prob.x0, prob.x_target, prob.n)[0]) / (2 * eps)
+        assert abs(g[j, k] - fd) <= 1e-7 * max(1.0, abs(fd)), (j, k, g[j, k], fd)
+    # one Fréchet derivative per slice: Re tr(A_j L(A_k, x_k lam_{k+1}^H)) == Re<lam, L(A_k, A_j) x_k>
+    k = 4
+    Ak = prob.A0 + sum(u[j, k] * prob.A[j] for j in range(2))
+    Z = cache.x[k] @ cache.lam[k + 1].conj().T
+    _, Lz = O.expm_frechet_block(Ak, Z)
+    for j in range(2):
+        assert abs(np.real(np.trace(prob.A[j] @ Lz)) - g[j, k]) < 1e-12
