@@ -127,6 +127,51 @@ def spline_matrix(tgate: float, Nt: int, nsplines: int) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------
+# Column packing for parity-structured problems (src/utils.jl:96-109)
+# ---------------------------------------------------------------------------
+def compress_states(x, v):
+    """Pack the two disjoint (rows, cols) blocks of x into max(n1, n2) columns (src/utils.jl:96-102).
+
+    v = ((rows1, cols1), (rows2, cols2)) with 0-based index sequences.
+    """
+    (r1, c1), (r2, c2) = v
+    x = np.asarray(x)
+    n1, n2 = len(c1), len(c2)
+    out = np.zeros((x.shape[0], max(n1, n2)), dtype=x.dtype)
+    out[np.ix_(list(r1), range(n1))] = x[np.ix_(list(r1), list(c1))]
+    out[np.ix_(list(r2), range(n2))] = x[np.ix_(list(r2), list(c2))]
+    return out
+
+
+def decompress_states(xc, v):
+    """Inverse of compress_states (src/utils.jl:103-109)."""
+    (r1, c1), (r2, c2) = v
+    xc = np.asarray(xc)
+    n1, n2 = len(c1), len(c2)
+    out = np.zeros((xc.shape[0], n1 + n2), dtype=xc.dtype)
+    out[np.ix_(list(r1), list(c1))] = xc[np.ix_(list(r1), range(n1))]
+    out[np.ix_(list(r2), list(c2))] = xc[np.ix_(list(r2), range(n2))]
+    return out
+
+
+def compress_problem(prob, v):
+    """Problem with x0 / x_target packed by compress_states: m drops to max(n1, n2).
+
+    Valid when every generator maps span(rows1) and span(rows2) into themselves (block-diagonal in
+    the row partition), so U_k commutes with the packing and the chains, the trace cost (entries outside
+    the blocks are zero in x) and the gradient are unchanged.  Raises ValueError otherwise.
+    """
+    (r1, _), (r2, _) = v
+    r1, r2 = list(r1), list(r2)
+    for G in [prob.A0] + list(prob.A):
+        G = np.asarray(G)
+        if np.abs(G[np.ix_(r1, r2)]).max(initial=0.0) > 0 or np.abs(G[np.ix_(r2, r1)]).max(initial=0.0) > 0:
+            raise ValueError("generators couple the two row blocks; compress_states does not apply")
+    return Problem(prob.name + "_compressed", prob.A0, list(prob.A), compress_states(prob.x0, v),
+                   compress_states(prob.x_target, v), prob.n, prob.Nt, prob.precision)
+
+
+# ---------------------------------------------------------------------------
 # Problem container
 # ---------------------------------------------------------------------------
 @dataclass

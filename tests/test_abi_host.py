@@ -97,3 +97,30 @@ def test_gate_unitaries():
         assert np.allclose(U @ U.T, np.eye(4))
     with pytest.raises(ValueError):
         S.gate_unitary("T")
+
+
+def test_compress_states_reference_vectors():
+    """test/test_utils.jl:22-37 (1-based ranges shifted to 0-based)."""
+    from qoc_amd import systems as S
+    v = ((range(0, 27, 2), [0, 3]), (range(1, 26, 2), [1, 2]))
+    x0 = np.arange(1, 27 * 4 + 1).reshape(4, 27).T.copy()   # collect(reshape(1:27*4, 27, 4))
+    x0[np.ix_(range(0, 27, 2), [1, 2])] = 0
+    x0[np.ix_(range(1, 26, 2), [0, 3])] = 0
+    x1 = S.compress_states(x0, v)
+    assert x1.shape[1] == 2
+    assert np.array_equal(S.decompress_states(x1, v), x0)
+    v = ((range(0, 27, 2), [0, 3, 4]), (range(1, 26, 2), [1, 2]))
+    x0 = np.arange(1, 27 * 5 + 1).reshape(5, 27).T.copy()
+    x0[np.ix_(range(0, 27, 2), [1, 2])] = 0
+    x0[np.ix_(range(1, 26, 2), [0, 3, 4])] = 0
+    x1 = S.compress_states(x0, v)
+    assert x1.shape[1] == 3
+    assert np.array_equal(S.decompress_states(x1, v), x0)
+
+
+def test_compress_problem_rejects_coupling_generators():
+    from qoc_amd import systems as S
+    prob = S.zz_problem(10)
+    v = ((range(0, 9, 2), [0, 3]), (range(1, 9, 2), [1, 2]))
+    with pytest.raises(ValueError, match="couple"):
+        S.compress_problem(prob, v)

@@ -264,3 +264,46 @@ def test_exact_gradient_large_n_path(built_lib, monkeypatch):
         _, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order="exact")
         assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
     e.close()
+
+
+def test_compressed_states_give_identical_results(built_lib):
+    """compress_states (src/utils.jl:96-109): a parity-structured problem propagated with m = 2 packed
+    columns gives the same J, dJdu and (decompressed) states as the m = 4 original."""
+    from qoc_amd import GrapeEngine, systems
+    rng = np.random.default_rng(8)
+    N, Nt = 12, 15
+    r1, r2 = list(range(0, N, 2)), list(range(1, N, 2))
+
+    def block_gen(scale):
+        H = np.zeros((N, N), complex)
+        for r in (r1, r2):
+            G = rng.standard_normal((len(r), len(r))) + 1j * rng.standard_normal((len(r), len(r)))
+            H[np.ix_(r, r)] = (G + G.conj().T) / 2
+        return -1j * scale * H
+    A0, A = block_gen(0.2), [block_gen(0.05), block_gen(0.05)]
+    v = ((r1, [0, 3]), (r2, [1, 2]))
+
+    def structured(M):
+        M = M.copy()
+        M[np.ix_(r1, [1, 2])] = 0
+        M[np.ix_(r2, [0, 3])] = 0
+        return M
+    x0 = structured(np.eye(N, dtype=complex)[:, :4] + np.eye(N, dtype=complex)[:, 4:8])
+    Z = rng.standard_normal((N, 4)) + 1j * rng.standard_normal((N, 4))
+    xt = structured(Z)
+    full = systems.Problem("parity", A0, A, x0, xt, 4.0, Nt, "fp64")
+    comp = systems.compress_problem(full, v)
+    assert comp.x0.shape[1] == 2
+    u = rng.uniform(-1, 1, size=(2, 2, Nt))
+    res = []
+    for p in (full, comp):
+        e = GrapeEngine(p.A0, p.A, p.x0, Nt, B=2)
+        e.set_cost_trace(p.x_target, p.n)
+        J = e.propagate(u)
+        g = e.grape_sensitivity(u, 3)
+        res.append((J, g, e.state(Nt, seed=1)))
+        e.close()
+    (J0, g0, x0N), (J1, g1, x1N) = res
+    np.testing.assert_allclose(J1, J0, rtol=0, atol=1e-13)
+    np.testing.assert_allclose(g1, g0, rtol=1e-11, atol=1e-14)
+    np.testing.assert_allclose(systems.decompress_states(x1N, v), x0N, rtol=0, atol=1e-13)
