@@ -47,6 +47,15 @@ struct GemmArgs {
   double alpha1, alpha2, alpha3, gamma1, gamma2, gamma3;
   double w1[3], w2[3], w3[3];
   double* sumsq;
+  // MODE 1 (generator combine, LDS-resident-N gradient): op(B)(k, col) = Bsrc[k mod kb, col] * s(k / kb, col)
+  //   with s(0) = 1, s(j) = uc[(b Nt + t) nu + j - 1] for the slice (b, t) of column col (t < Nt, else 0);
+  //   Bsrc has leading dimension kb.  Columns map to slices as col = ((b sps) + t) m + i.
+  // MODE 2 (fused contraction): C is not stored; instead
+  //   dot[(b Nt + t) nu + row / kb] += Re(conj(Wd[row mod kb, col]) C[row, col])   (t < Nt).
+  const double* uc;
+  int kb, cm, sps, cNt, cnu;
+  double* dot;
+  Opd Wd;
 };
 
 // Both operands are staged in LDS as [row or col][k] planes (re / im) with k contiguous.  K is
@@ -119,7 +128,7 @@ __device__ __forceinline__ void bg_store(T* __restrict__ pre, T* __restrict__ pi
 // Re = P1 - P2, Im = P3 - P1 - P2.  25 % fewer MFMAs than the 4-product form; the imaginary part's
 // rounding error grows to ~2 eps |a||b| (cancellation in P3 - P1 - P2), well inside the fp32/fp64
 // parity tolerances.
-template <typename T, int OPA, int OPB, bool M3 = true, int KS = 1, int NBUF = 2>
+template <typename T, int OPA, int OPB, bool M3 = true, int KS = 1, int NBUF = 2, int MODE = 0>
 __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
   using MFT = MF<T>;
   using v4 = typename MFT::v4;
@@ -140,6 +149,45 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
   const cx<T>* Bb = opd_ptr<T>(g.B, item);
   const int M = g.M, K = g.K, NC = g.Ncol;
   const long long ldA = OPA ? K : M, ldB = OPB ? NC : K;
+  // MODE 1: the thread's B column (fixed across slabs) and its generator scales
+  double us[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) us[q] = q == 0 ? 1.0 : 0.0;
+  if (MODE == 1) {
+    const int gc = col0 + (tid >> 2);
+    if (gc < NC) {
+      const int sl = gc / g.cm, b = sl / g.sps, t = sl - b * g.sps;
+      if (t < g.cNt) {
+        const double* up = g.uc + ((size_t)b * g.cNt + t) * g.cnu;
+#pragma unroll
+        for (int q = 1; q < 9; ++q) us[q] = q <= g.cnu ? up[q - 1] : 0.0;
+      }
+    }
+  }
+  // MODE 1 B operand: like bg_load<KCONT = true> (op0, contiguous along k) with the generator-block
+  // scaling s(k / kb, col) (us[0] = 1); written inline so that us[] stays in registers.
+#define QOC_BG_LOADB(K0)                                                                  \
+  do {                                                                                    \
+    if (MODE == 1) {                                                                      \
+      const int gr_ = col0 + (tid >> 2);                                                  \
+      _Pragma("unroll") for (int j_ = 0; j_ < KS; ++j_) {                                 \
+        const int kg_ = (tid & 3) + 4 * j_;                                               \
+        _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_) {                                \
+          const int gk_ = (K0) + 4 * kg_ + t_;                                            \
+          const bool ok_ = gr_ < NC && gk_ < K;                                           \
+          const int blk_ = ok_ ? gk_ / g.kb : 0;                                          \
+          const int kr_ = ok_ ? gk_ - blk_ * g.kb : 0;                                    \
+          const cx<T> v_ = Bb[(long long)kr_ + (long long)g.kb * (ok_ ? gr_ : 0)];        \
+          double sc_ = us[0];                                                             \
+          _Pragma("unroll") for (int q_ = 1; q_ < 9; ++q_) sc_ = blk_ == q_ ? us[q_] : sc_; \
+          sbr[j_][t_] = ok_ ? (T)(sc_ * v_.r) : T(0);                                     \
+          sbi[j_][t_] = ok_ ? (T)(sc_ * v_.i) : T(0);                                     \
+        }                                                                                 \
+      }                                                                                   \
+    } else {                                                                              \
+      bg_load<T, OPB == 0, OPB == 1, KS>(Bb, ldB, col0, (K0), NC, K, tid, sbr, sbi);      \
+    }                                                                                     \
+  } while (0)
 
   V sar[KS], sai[KS], sbr[KS], sbi[KS];
   v4 cr[2][2], ci[2][2], cs[2][2];
@@ -155,7 +203,7 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
   const int li = lane & 15, kq = lane >> 4;
   const int nslab = (K + L::BK - 1) / L::BK;
   bg_load<T, OPA == 1, OPA == 1, KS>(Ab, ldA, row0, 0, M, K, tid, sar, sai);
-  bg_load<T, OPB == 0, OPB == 1, KS>(Bb, ldB, col0, 0, NC, K, tid, sbr, sbi);
+  QOC_BG_LOADB(0);
   if (NBUF == 2) {
     bg_store<T, OPA == 1, KS>(lds + 0 * L::PLANE, lds + 1 * L::PLANE, tid, sar, sai);
     bg_store<T, OPB == 0, KS>(lds + 2 * L::PLANE, lds + 3 * L::PLANE, tid, sbr, sbi);
@@ -171,7 +219,7 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
     }
     if (s + 1 < nslab) {
       bg_load<T, OPA == 1, OPA == 1, KS>(Ab, ldA, row0, (s + 1) * L::BK, M, K, tid, sar, sai);
-      bg_load<T, OPB == 0, OPB == 1, KS>(Bb, ldB, col0, (s + 1) * L::BK, NC, K, tid, sbr, sbi);
+      QOC_BG_LOADB((s + 1) * L::BK);
     }
 #pragma unroll
     for (int q = 0; q < KS; ++q) {
@@ -235,6 +283,56 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
     }
   }
 
+#undef QOC_BG_LOADB
+  if (MODE == 2) {
+    // fused contraction: per (slice, j) partial sums of Re(conj(W) C) over this tile
+    const cx<T>* Wb = opd_ptr<T>(g.Wd, item);
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      const int rbase = row0 + wr + 16 * x;
+      const int jb = rbase / g.kb;
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {
+        const int col = col0 + wc + 16 * y + li;
+        double acc[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = rbase + MFT::drow(lane, i);
+          if (row < M && col < NC) {
+            double pr, pi;
+            if (M3) {
+              pr = (double)cr[x][y][i] - (double)ci[x][y][i];
+              pi = (double)cs[x][y][i] - (double)cr[x][y][i] - (double)ci[x][y][i];
+            } else {
+              pr = cr[x][y][i];
+              pi = ci[x][y][i];
+            }
+            const int j = row / g.kb;
+            const cx<T> wv = Wb[(row - j * g.kb) + (size_t)g.kb * col];
+            const double e = (double)wv.r * pr + (double)wv.i * pi;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] += (j - jb == q) ? e : 0.0;
+          }
+        }
+        int sl = 0, b = 0, t = 0;
+        if (col < NC) {
+          sl = col / g.cm;
+          b = sl / g.sps;
+          t = sl - b * g.sps;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          double v = acc[q];
+          v += __shfl_xor(v, 16);
+          v += __shfl_xor(v, 32);
+          const int j = jb + q;
+          if ((lane >> 4) == 0 && col < NC && t < g.cNt && j < g.cnu && j * g.kb < M && v != 0.0)
+            atomicAdd(g.dot + ((size_t)b * g.cNt + t) * g.cnu + j, v);
+        }
+      }
+    }
+    return;
+  }
   // ---- fused epilogue ----
   cx<T>* C1 = const_cast<cx<T>*>(opd_ptr<T>(g.C1, item));
   cx<T>* C2 = g.C2.p ? const_cast<cx<T>*>(opd_ptr<T>(g.C2, item)) : nullptr;
@@ -477,6 +575,21 @@ __global__ __launch_bounds__(256) void k_gen_contract(int N, int nu, long long u
       const double s = block_sum(acc[j], red);
       if (threadIdx.x == 0) dJdu[unit * nu + j] = s;  // u layout: b*nu*Nt + k*nu + j == unit*nu + j
     }
+  }
+}
+
+// Auxiliary generator layouts for the GEMM-shaped gradient of the LDS-resident path:
+//   AH  = [A0^H | A1^H | ... | A_nu^H]   (N x (nu+1) N, column blocks)
+//   Cst = [A1; A2; ...; A_nu]            (nu N x N, row blocks)
+template <typename T>
+__global__ void k_gen_aux(int N, int nu, const cx<T>* __restrict__ Agen, cx<T>* __restrict__ AH, cx<T>* __restrict__ Cst) {
+  const size_t NN = (size_t)N * N;
+  for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < NN * (nu + 1); g += (size_t)gridDim.x * blockDim.x) {
+    const size_t gi = g / NN, e = g - gi * NN;
+    const size_t r = e % N, c = e / N;
+    const cx<T> v = Agen[gi * NN + c + N * r];  // A_gi[c, r]
+    AH[gi * NN + e] = cx<T>{v.r, -v.i};          // A_gi^H[r, c]
+    if (gi > 0) Cst[(gi - 1) * N + r + (size_t)nu * N * c] = Agen[gi * NN + e];
   }
 }
 

@@ -86,6 +86,11 @@ struct qoc_ctx {
   double* d_Bs = nullptr;  // Nt x ns
   int ns = 0;
   double* d_cstage = nullptr;  // host-pointer variants: B x ns x nu coefficients / gradient
+  // GEMM-shaped gradient of the LDS-resident path (order 3): generator layouts + P/Q/W workspace
+  void* d_AH = nullptr;    // (nu+1) x N*N: [A0^H | A1^H | ...]
+  void* d_Cst = nullptr;   // nu N x N: [A1; A2; ...]
+  void* d_gws = nullptr;   // 6 x N x B(Nt+1)m
+  bool grad_gemm = true;
   // exact (Fréchet) gradient mode workspace, allocated on first use
   void* d_fws = nullptr;
   size_t fws_bytes = 0;
@@ -223,6 +228,8 @@ void mark_end(qoc_ctx* c, int idx) {
 
 template <typename T>
 int frechet_grad(qoc_ctx* c, double* d_dJdu);
+template <typename T>
+int grad_gemm_o3(qoc_ctx* c, double* d_dJdu);
 
 template <typename T>
 int run_forward(qoc_ctx* c) {
@@ -256,6 +263,12 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
   if (order == QOC_DUKDP_EXACT) {
     mk = mark_begin(c, 3);
     int r = frechet_grad<T>(c, d_dJdu);
+    mark_end(c, mk);
+    return r;
+  }
+  if (order == 3 && c->grad_gemm) {
+    mk = mark_begin(c, 3);
+    int r = grad_gemm_o3<T>(c, d_dJdu);
     mark_end(c, mk);
     return r;
   }
@@ -315,7 +328,7 @@ GemmArgs gemm_args(int M, int K, int Ncol, int nitems) {
 }
 
 template <typename T>
-int big_gemm(qoc_ctx* c, int opa, int opb, GemmArgs g) {
+int big_gemm(qoc_ctx* c, int opa, int opb, GemmArgs g, int mode = 0) {
   g.tiles_m = (g.M + BG_BM - 1) / BG_BM;
   g.tiles = g.tiles_m * ((g.Ncol + BG_BN - 1) / BG_BN);
   const long long total = (long long)g.nitems * g.tiles;
@@ -327,7 +340,9 @@ int big_gemm(qoc_ctx* c, int opa, int opb, GemmArgs g) {
     gm.b = take_event(c);
     (void)hipEventRecord(gm.a, c->stream);
   }
-  if (opa == 0 && opb == 0) hipLaunchKernelGGL((k_bgemm<T, 0, 0>), grid, blk, 0, c->stream, g);
+  if (mode == 1) hipLaunchKernelGGL((k_bgemm<T, 0, 0, true, 1, 2, 1>), grid, blk, 0, c->stream, g);
+  else if (mode == 2) hipLaunchKernelGGL((k_bgemm<T, 0, 0, true, 1, 2, 2>), grid, blk, 0, c->stream, g);
+  else if (opa == 0 && opb == 0) hipLaunchKernelGGL((k_bgemm<T, 0, 0>), grid, blk, 0, c->stream, g);
   else if (opa == 1 && opb == 0) hipLaunchKernelGGL((k_bgemm<T, 1, 0>), grid, blk, 0, c->stream, g);
   else if (opa == 0 && opb == 1) hipLaunchKernelGGL((k_bgemm<T, 0, 1>), grid, blk, 0, c->stream, g);
   else hipLaunchKernelGGL((k_bgemm<T, 1, 1>), grid, blk, 0, c->stream, g);
@@ -653,6 +668,70 @@ int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
   return QOC_OK;
 }
 
+// Order-3 gradient of the LDS-resident path as GEMMs over every (seed, slice) at once.  With the state
+// matrix Xall = [x_0 .. x_Nt] of all seeds (N x B(Nt+1)m, the d_X buffer as is) and
+// X_k v = A0 v + sum_j u_jk A_j v = [A0 | A1 | ...] [v; u_1k v; ...]:
+//   P1 = X Xall, P2 = X P1, Q1 = X^H Lsh (Lsh = λ_{k+1} columns), and from the epilogues
+//   W2 = λ/6, W0 = λ + Q1/2 + Q2/6, W1 = λ/2 + Q1/6 (Q2 = X^H Q1 is never stored);
+//   dJdu[k, j] = sum_a Re<W_a, A_j P_a>  (k_bgemm MODE 2 epilogue, [A1; A2; ...] x P_a).
+// Same contraction as k_grad / the reference's expm_jacobian! order 3, on MFMA with the generators
+// shared by every GEMM.
+template <typename T>
+int grad_gemm_o3(qoc_ctx* c, double* d_dJdu) {
+  const int N = c->N, m = c->m, nu = c->nu, Nt = c->Nt;
+  const size_t Nm = (size_t)N * m, esz = c->esz;
+  const long long cols = (long long)c->B * (Nt + 1) * m - m;  // the last seed's x_Nt column block is unused
+  const size_t bufN = (size_t)N * ((size_t)c->B * (Nt + 1) * m);
+  auto buf = [&](int i) { return mk_opd(c->d_gws, (size_t)i * bufN, esz, 0); };
+  const Opd Xall = mk_opd(c->d_X, 0, esz, 0), Lsh = mk_opd(c->d_L, Nm, esz, 0);
+  const Opd P1 = buf(0), P2 = buf(1), Q1 = buf(2), W0 = buf(3), W1 = buf(4), W2 = buf(5);
+  HIPCHK(c, hipMemsetAsync(d_dJdu, 0, (size_t)c->B * Nt * nu * sizeof(double), c->stream));
+  auto comb = [&](const void* Gmat, const Opd& Bsrc) {
+    GemmArgs g = gemm_args(N, (nu + 1) * N, (int)cols, 1);
+    g.A = mk_opd(Gmat, 0, esz, 0);
+    g.B = Bsrc;
+    g.uc = c->d_u;
+    g.kb = N;
+    g.cm = m;
+    g.sps = Nt + 1;
+    g.cNt = Nt;
+    g.cnu = nu;
+    return g;
+  };
+  int r;
+  GemmArgs g = comb(c->d_A, Xall);
+  g.C1 = P1;
+  if ((r = big_gemm<T>(c, 0, 0, g, 1))) return r;  // P1 = X x
+  g = comb(c->d_A, P1);
+  g.C1 = P2;
+  if ((r = big_gemm<T>(c, 0, 0, g, 1))) return r;  // P2 = X P1
+  g = comb(c->d_AH, Lsh);
+  g.C1 = Q1;
+  g.C2 = W2; g.alpha2 = 0.0; g.nY = 1; g.Y[0] = Lsh; g.w2[0] = 1.0 / 6;
+  if ((r = big_gemm<T>(c, 0, 0, g, 1))) return r;  // Q1 = X^H λ, W2 = λ/6
+  g = comb(c->d_AH, Q1);
+  g.nY = 2; g.Y[0] = Lsh; g.Y[1] = Q1;
+  g.C1 = W0; g.alpha1 = 1.0 / 6; g.w1[0] = 1.0; g.w1[1] = 0.5;
+  g.C2 = W1; g.alpha2 = 0.0; g.w2[0] = 0.5; g.w2[1] = 1.0 / 6;
+  if ((r = big_gemm<T>(c, 0, 0, g, 1))) return r;  // W0, W1 (Q2 consumed in the epilogue)
+  const Opd Pa[3] = {Xall, P1, P2}, Wa[3] = {W0, W1, W2};
+  for (int a = 0; a < 3; ++a) {
+    GemmArgs h = gemm_args(nu * N, N, (int)cols, 1);
+    h.A = mk_opd(c->d_Cst, 0, esz, 0);
+    h.B = Pa[a];
+    h.C1 = Pa[a];  // not written in MODE 2
+    h.kb = N;
+    h.cm = m;
+    h.sps = Nt + 1;
+    h.cNt = Nt;
+    h.cnu = nu;
+    h.dot = d_dJdu;
+    h.Wd = Wa[a];
+    if ((r = big_gemm<T>(c, 0, 0, h, 2))) return r;  // dJdu += Re<W_a, A_j P_a>
+  }
+  return QOC_OK;
+}
+
 // Exact gradient (QOC_DUKDP_EXACT): one Fréchet derivative per slice from the 2N x 2N block exponential
 // (qoc_frechet.hpp), k_expm when 2N fits the LDS-resident kernel, the GEMM pipeline otherwise.
 template <typename T>
@@ -798,6 +877,14 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
     if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return bail(e, "hipMalloc");
     c->dev_bytes += a.bytes;
   }
+  c->grad_gemm = !c->big && N >= 6 && nu <= 8 && !(getenv("QOC_GRAD_KERNEL") && atoi(getenv("QOC_GRAD_KERNEL")) != 0);
+  if (c->grad_gemm) {
+    const size_t cols = (size_t)B * (Nt + 1) * m;
+    if ((e = hipMalloc(&c->d_AH, (nu + 1) * NN * c->esz)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&c->d_Cst, nu * NN * c->esz)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&c->d_gws, 6 * (size_t)N * cols * c->esz)) != hipSuccess) return bail(e, "hipMalloc");
+    c->dev_bytes += (2 * nu + 1) * NN * c->esz + 6 * (size_t)N * cols * c->esz;
+  }
   if (c->big) {
     // chunk of slices sized to a workspace of <= 8 GiB (and <= 1/8 of what is free)
     size_t freeb = 0, totalb = 0;
@@ -827,7 +914,7 @@ void qoc_destroy(qoc_ctx* c) {
   hipSetDevice(c->dev);
   if (c->stream) hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
-                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws};
+                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& m : c->marks) {
@@ -861,6 +948,16 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
     r = upload(c, Aj[j], (char*)c->d_A + (j + 1) * NN * c->esz, NN);
   }
   if (r != QOC_OK) return r;
+  if (c->d_AH) {
+    const unsigned blocks = (unsigned)std::min<size_t>(((c->nu + 1) * NN + 255) / 256, 2048);
+    if (c->prec == QOC_FP64)
+      hipLaunchKernelGGL((k_gen_aux<double>), dim3(blocks), dim3(256), 0, c->stream, c->N, c->nu,
+                         (const cx<double>*)c->d_A, (cx<double>*)c->d_AH, (cx<double>*)c->d_Cst);
+    else
+      hipLaunchKernelGGL((k_gen_aux<float>), dim3(blocks), dim3(256), 0, c->stream, c->N, c->nu,
+                         (const cx<float>*)c->d_A, (cx<float>*)c->d_AH, (cx<float>*)c->d_Cst);
+    HIPCHK(c, hipGetLastError());
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_gen = true;
   c->have_prop = false;

@@ -61,6 +61,9 @@ void run(int N, double scale, int units) {
              st[12 + 4 * pn] - st[11 + 4 * pn], (pn < 2 && st[14 + 4 * pn] ? st[14 + 4 * pn] : st[30]) - st[12 + 4 * pn]);
   printf("   first GEMM (wave0) %llu   GJ block p0=20: publish %llu  W %llu  mfma %llu\n", st[21] - st[20],
          st[41] - st[40], st[42] - st[41], st[43] - st[42]);
+  if (st[44])
+    printf("   GJ16 block p0=16: publish %llu  Dinv %llu  W %llu  update %llu\n", st[45] - st[44], st[46] - st[45],
+           st[47] - st[46], st[48] - st[47]);
   (void)hipMemset(0, 0, 0);
   {
     unsigned long long z[64] = {0};
