@@ -137,6 +137,11 @@ struct Expm {
       C.i[q] = v4{0, 0, 0, 0};
     }
     if (!owns(0, wave)) return;
+    // 3-multiply complex product (Gauss): C.r accumulates ar br, C.i accumulates ai bi, S accumulates
+    // (ar+ai)(br+bi); Re = ar br - ai bi, Im = S - ar br - ai bi.  25 % fewer MFMAs than 4 products.
+    v4 S[MT];
+#pragma unroll
+    for (int q = 0; q < MT; ++q) S[q] = v4{0, 0, 0, 0};
     Frag cur, nxt;
     load_frag(N, 0, Ar, Ai, Br, Bi, cur, wave, lane);
     for (int kk = 0; kk < N; kk += 4) {
@@ -145,17 +150,17 @@ struct Expm {
       for (int q = 0; q < MT; ++q) {
         if (ROWMAP || owns(q, wave)) {
           C.r[q] = M::mma(cur.ar[q], cur.br[q], C.r[q]);
-          C.i[q] = M::mma(cur.ar[q], cur.bi[q], C.i[q]);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < MT; ++q) {
-        if (ROWMAP || owns(q, wave)) {
-          C.r[q] = M::mma(-cur.ai[q], cur.bi[q], C.r[q]);
-          C.i[q] = M::mma(cur.ai[q], cur.br[q], C.i[q]);
+          C.i[q] = M::mma(cur.ai[q], cur.bi[q], C.i[q]);
+          S[q] = M::mma(cur.ar[q] + cur.ai[q], cur.br[q] + cur.bi[q], S[q]);
         }
       }
       cur = nxt;
+    }
+#pragma unroll
+    for (int q = 0; q < MT; ++q) {
+      const v4 pr = C.r[q] - C.i[q];
+      C.i[q] = S[q] - C.r[q] - C.i[q];
+      C.r[q] = pr;
     }
   }
 
