@@ -103,6 +103,13 @@ int qoc_get_propagator(qoc_ctx* ctx, int seed, int k, double* U_out);   /* Uk_ve
  * hist[di*64 + s], di = index of degree in {3,5,7,9,13}.  Used for the FLOP accounting. */
 int qoc_pade_histogram(qoc_ctx* ctx, long long* hist, int reset);
 
+/* Exponential algorithm actually executed by the LDS-resident path: by default a degree m = 3r+2
+ * Taylor polynomial (Paterson-Stockmeyer, 2 + r GEMMs, no linear solve) with s squarings, chosen so
+ * that the truncation tail is <= 2^-53 (same result as the reference's Padé to fp rounding; set
+ * QOC_EXPM_PADE=1 at qoc_create for the Padé + solve algorithm).  hist[(r-2)*64 + s], r = 2..8
+ * (7*64 entries).  qoc_pade_histogram keeps reporting the Padé (d, s) the reference would select. */
+int qoc_taylor_histogram(qoc_ctx* ctx, long long* hist, int reset);
+
 /* Live per-kernel timing: when enabled, hipEvents are recorded on qoc_stream around each hot-path
  * kernel (phase 0 k_expm, 1 k_chain_fwd, 2 k_chain_bwd, 3 k_grad).  qoc_phase_times synchronises the
  * stream and returns the accumulated milliseconds and launch counts per phase. */

@@ -52,7 +52,8 @@ struct qoc_ctx {
   cx<double>* d_coef = nullptr;  // B*m
   double* d_dJdu = nullptr;  // B*nu*Nt
   int* d_flag = nullptr;
-  unsigned long long* d_hist = nullptr;  // 5*64
+  unsigned long long* d_hist = nullptr;  // 5*64 reference (Padé) selection + 7*64 executed Taylor (r, s)
+  int expm_alg = 1;                      // 1 Taylor / Paterson-Stockmeyer (default), 0 Padé (QOC_EXPM_PADE=1)
   double* d_stage = nullptr;             // host->device staging (fp64 complex), max(B*N*m, (nu+1)*N*N)*2
   size_t stage_elems = 0;
   std::vector<double> h_u;
@@ -131,28 +132,36 @@ bool expm_supported(int N, int prec) {
   return lds <= 160 * 1024;
 }
 
-template <typename T, int NT>
+template <typename T, int NT, int ALG>
 hipError_t launch_expm_t(hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
-                         const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq) {
+                         const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq,
+                         unsigned long long* thist) {
   const size_t lds = Expm<T, NT>::lds_bytes(N);
-  hipError_t e = hipFuncSetAttribute((const void*)k_expm<T, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipError_t e =
+      hipFuncSetAttribute((const void*)k_expm<T, NT, ALG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_expm<T, NT>), dim3(nunits), dim3(256), lds, s, N, nu, nunits, (const cx<T>*)Agen, u,
-                     (const cx<T>*)Ain, (cx<T>*)Uout, hist, deg, sq);
+  hipLaunchKernelGGL((k_expm<T, NT, ALG>), dim3(nunits), dim3(256), lds, s, N, nu, nunits, (const cx<T>*)Agen, u,
+                     (const cx<T>*)Ain, (cx<T>*)Uout, hist, deg, sq, thist);
   return hipGetLastError();
 }
 
+// alg 0: Padé + solve (reference algorithm), alg 1: Taylor / Paterson-Stockmeyer (no solve).
 hipError_t launch_expm(int prec, hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
-                       const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq) {
+                       const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq, int alg = 0,
+                       unsigned long long* thist = nullptr) {
   const int NT = (N + 15) / 16;
+#define QOC_LX(TT, NTT)                                                                                   \
+  return alg ? launch_expm_t<TT, NTT, 1>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq, thist)     \
+             : launch_expm_t<TT, NTT, 0>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq, thist)
   if (prec == QOC_FP64) {
-    if (NT == 1) return launch_expm_t<double, 1>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq);
-    if (NT == 2) return launch_expm_t<double, 2>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq);
-    return launch_expm_t<double, 3>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq);
+    if (NT == 1) QOC_LX(double, 1);
+    if (NT == 2) QOC_LX(double, 2);
+    QOC_LX(double, 3);
   }
-  if (NT == 1) return launch_expm_t<float, 1>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq);
-  if (NT == 2) return launch_expm_t<float, 2>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq);
-  return launch_expm_t<float, 3>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq);
+  if (NT == 1) QOC_LX(float, 1);
+  if (NT == 2) QOC_LX(float, 2);
+  QOC_LX(float, 3);
+#undef QOC_LX
 }
 
 template <typename T>
@@ -235,7 +244,7 @@ template <typename T>
 int run_forward(qoc_ctx* c) {
   int mk = mark_begin(c, 0);
   hipError_t e = launch_expm(c->prec, c->stream, c->N, c->nu, c->B * c->Nt, c->d_A, c->d_u, nullptr, c->d_U,
-                             c->d_hist, nullptr, nullptr);
+                             c->d_hist, nullptr, nullptr, c->expm_alg, c->d_hist + 5 * 64);
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm launch: %s", hipGetErrorString(e));
   const size_t lds = chain_lds(c);
@@ -778,7 +787,8 @@ int frechet_grad(qoc_ctx* c, double* d_dJdu) {
                        blocks, alpha);
     HIPCHK(c, hipGetLastError());
     if (small) {
-      hipError_t e = launch_expm(c->prec, c->stream, n2, 0, cnt, nullptr, nullptr, blocks, E, nullptr, nullptr, nullptr);
+      hipError_t e = launch_expm(c->prec, c->stream, n2, 0, cnt, nullptr, nullptr, blocks, E, nullptr, nullptr, nullptr,
+                                 c->expm_alg);
       if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm (Frechet block): %s", hipGetErrorString(e));
     } else {
       HIPCHK(c, hipMemsetAsync(red, 0, sizeof(double), c->stream));
@@ -871,7 +881,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
       {(void**)&c->d_coef, (size_t)B * m * sizeof(cx<double>)},
       {(void**)&c->d_dJdu, (size_t)B * nu * Nt * sizeof(double)},
       {(void**)&c->d_flag, sizeof(int)},
-      {(void**)&c->d_hist, 5 * 64 * sizeof(unsigned long long)},
+      {(void**)&c->d_hist, 12 * 64 * sizeof(unsigned long long)},
   };
   for (auto& a : allocs) {
     if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return bail(e, "hipMalloc");
@@ -903,7 +913,8 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
     c->dev_bytes += (size_t)ch * per_item + ((size_t)ch + 8) * sizeof(double);
   }
   hipMemset(c->d_pmask, 0, Nm);
-  hipMemset(c->d_hist, 0, 5 * 64 * sizeof(unsigned long long));
+  hipMemset(c->d_hist, 0, 12 * 64 * sizeof(unsigned long long));
+  c->expm_alg = (getenv("QOC_EXPM_PADE") && atoi(getenv("QOC_EXPM_PADE")) != 0) ? 0 : 1;
   hipMemset(c->d_L, 0, (size_t)B * (Nt + 1) * Nm * c->esz);
   *out = c;
   return QOC_OK;
@@ -1264,6 +1275,15 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[1] = c->chunk;
   info[2] = c->ns_iters;
   info[3] = (long long)c->dev_bytes;
+  return QOC_OK;
+}
+
+int qoc_taylor_histogram(qoc_ctx* c, long long* hist, int reset) {
+  if (!c || !hist) return fail(c, QOC_ERR_ARG, "null argument");
+  HIPCHK(c, hipSetDevice(c->dev));
+  HIPCHK(c, hipMemcpyAsync(hist, c->d_hist + 5 * 64, 7 * 64 * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+  if (reset) HIPCHK(c, hipMemsetAsync(c->d_hist + 5 * 64, 0, 7 * 64 * sizeof(long long), c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return QOC_OK;
 }
 

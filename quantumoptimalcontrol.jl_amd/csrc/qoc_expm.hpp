@@ -48,6 +48,55 @@ __constant__ double kPade13[14] = {64764752532480000.0, 32382376266240000.0, 777
                                    670442572800.0, 33522128640.0, 1323241920.0, 40840800.0,
                                    960960.0, 16380.0, 182.0, 1.0};
 
+// Taylor / Paterson-Stockmeyer alternative (ALG = 1): degree m = 3r + 2, r = 2..8, cost 2 + r GEMMs
+// (A2, A3, then r Horner products in A3).  kTaylorTheta[r - 2]: largest ||A||_1 with
+// sum_{k>m} ||A||^k / k! <= 2^-53 (computed with scipy, tools note in DESIGN.md).
+__constant__ double kTaylorTheta[7] = {0.069933, 0.247240, 0.553491, 0.978345, 1.504147, 2.113468, 2.791345};
+__constant__ double kInvFact[27] = {1.0,
+                                    1.0,
+                                    0.5,
+                                    0.16666666666666666,
+                                    0.041666666666666664,
+                                    0.008333333333333333,
+                                    0.001388888888888889,
+                                    0.0001984126984126984,
+                                    2.48015873015873e-05,
+                                    2.7557319223985893e-06,
+                                    2.755731922398589e-07,
+                                    2.505210838544172e-08,
+                                    2.08767569878681e-09,
+                                    1.6059043836821613e-10,
+                                    1.1470745597729725e-11,
+                                    7.647163731819816e-13,
+                                    4.779477332387385e-14,
+                                    2.8114572543455206e-15,
+                                    1.5619206968586225e-16,
+                                    8.22063524662433e-18,
+                                    4.110317623312165e-19,
+                                    1.9572941063391263e-20,
+                                    8.896791392450574e-22,
+                                    3.8681701706306835e-23,
+                                    1.6117375710961184e-24,
+                                    6.446950284384474e-26,
+                                    2.4795962632247976e-27};
+
+// (r, s) minimising 2 + r + s with ||A / 2^s||_1 <= theta_r (ties: fewer squarings).
+__device__ __forceinline__ void taylor_select(double nA, int& r, int& s) {
+  int best = 1 << 30;
+  r = 2;
+  s = 0;
+  for (int rr = 2; rr <= 8; ++rr) {
+    int ss = 0;
+    if (nA > kTaylorTheta[rr - 2]) ss = (int)ceil(log2(nA / kTaylorTheta[rr - 2]));
+    const int cost = 2 + rr + ss;
+    if (cost < best || (cost == best && ss < s)) {
+      best = cost;
+      r = rr;
+      s = ss;
+    }
+  }
+}
+
 __device__ __forceinline__ int degree_index(int d) {
   return d == 3 ? 0 : d == 5 ? 1 : d == 7 ? 2 : d == 9 ? 3 : 4;
 }
@@ -802,11 +851,16 @@ struct Expm {
 // ---------------------------------------------------------------------------
 // The kernel.  unit = blockIdx.x.  Either generators (Agen, u) or explicit matrices (Ain).
 // ---------------------------------------------------------------------------
-template <typename T, int NT>
+// ALG 0: Higham-2005 Padé + solve (the reference's ExponentialUtilities algorithm; degree / squarings
+//        reported through deg_out / sq_out).  ALG 1: Taylor degree 3r+2 by Paterson-Stockmeyer + s
+//        squarings (no linear solve); same result to fp rounding, counted in thist[(r-2)*64 + s].
+// hist always receives the Padé (d, s) the reference would select (reference-equivalent accounting).
+template <typename T, int NT, int ALG = 0>
 __global__ __launch_bounds__(256, 2) void k_expm(int N, int nu, int nunits, const cx<T>* __restrict__ Agen,
                                                  const double* __restrict__ u, const cx<T>* __restrict__ Ain,
                                                  cx<T>* __restrict__ Uout, unsigned long long* __restrict__ hist,
-                                                 int* __restrict__ deg_out, int* __restrict__ sq_out) {
+                                                 int* __restrict__ deg_out, int* __restrict__ sq_out,
+                                                 unsigned long long* __restrict__ thist = nullptr) {
   using E = Expm<T, NT>;
   using Tiles = typename E::Tiles;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -858,6 +912,82 @@ __global__ __launch_bounds__(256, 2) void k_expm(int N, int nu, int nunits, cons
     if (hist) atomicAdd(&hist[degree_index(d) * 64 + (sq < 63 ? sq : 63)], 1ULL);
     if (deg_out) deg_out[unit] = d;
     if (sq_out) sq_out[unit] = sq;
+  }
+  if (ALG == 1) {
+    // ---- Taylor / Paterson-Stockmeyer path ----
+    int tr, ts;
+    taylor_select(nA, tr, ts);
+    if (tid == 0 && thist) atomicAdd(&thist[(tr - 2) * 64 + (ts < 63 ? ts : 63)], 1ULL);
+    const T tscale = (T)ldexp(1.0, -ts);
+    if (ts > 0) {
+      for (int e = tid; e < NN; e += 256) {
+        re(0)[e] *= tscale;
+        im(0)[e] *= tscale;
+      }
+      __syncthreads();
+    }
+    QOC_STAMP(1);
+    Tiles D, A2r, V, Ar;
+    // A at this wave's own tile positions (registers): the B_i below need A and A2 element-wise
+#pragma unroll
+    for (int q = 0; q < E::MT; ++q) {
+      const int col = E::tcol(q, wave, lane);
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int row = E::trow(q, wave, lane, ii);
+        const int e = min(row, N - 1) + N * min(col, N - 1);
+        Ar.r[q][ii] = re(0)[e];
+        Ar.i[q][ii] = im(0)[e];
+      }
+    }
+    E::gemm(N, re(0), im(0), re(0), im(0), A2r, wave, lane);  // A2 (kept in registers)
+    QOC_STAMP(50);
+    E::store(N, re(1), im(1), A2r, wave, lane);
+    __syncthreads();
+    E::gemm(N, re(1), im(1), re(0), im(0), D, wave, lane);  // A3 = A2 A
+    QOC_STAMP(51);
+    E::store(N, re(2), im(2), D, wave, lane);               // A3 -> B2; B1 is free once all waves pass
+    // B_i = c_{3i} I + c_{3i+1} A + c_{3i+2} A2 at this wave's own tile positions
+    auto add_B = [&](Tiles& X, int i, bool init) __attribute__((always_inline)) {
+      const T c0 = (T)kInvFact[3 * i], c1 = (T)kInvFact[3 * i + 1], c2 = (T)kInvFact[3 * i + 2];
+#pragma unroll
+      for (int q = 0; q < E::MT; ++q) {
+        if (E::owns(q, wave)) {
+          const int col = E::tcol(q, wave, lane);
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            const int row = E::trow(q, wave, lane, ii);
+            const T br = c1 * Ar.r[q][ii] + c2 * A2r.r[q][ii] + (row == col ? c0 : T(0));
+            const T bi = c1 * Ar.i[q][ii] + c2 * A2r.i[q][ii];
+            X.r[q][ii] = init ? br : X.r[q][ii] + br;
+            X.i[q][ii] = init ? bi : X.i[q][ii] + bi;
+          }
+        }
+      }
+    };
+    add_B(V, tr, true);  // Horner start: B_r
+    for (int i = tr - 1; i >= 0; --i) {
+      __syncthreads();  // B1 readers (previous GEMM / A3 GEMM) are done
+      E::store(N, re(1), im(1), V, wave, lane);
+      __syncthreads();
+      E::gemm(N, re(2), im(2), re(1), im(1), V, wave, lane);  // A3 * (B_{i+1} + A3 (...)), polynomials commute
+      add_B(V, i, false);
+    }
+    __syncthreads();
+    E::store(N, re(1), im(1), V, wave, lane);  // X -> B1
+    __syncthreads();
+    QOC_STAMP(5);
+    for (int q2 = 0; q2 < ts; ++q2) {
+      E::gemm(N, re(1), im(1), re(1), im(1), D, wave, lane);
+      __syncthreads();
+      E::store(N, re(1), im(1), D, wave, lane);
+      __syncthreads();
+    }
+    QOC_STAMP(6);
+    cx<T>* out = Uout + (size_t)unit * NN;
+    for (int e = tid; e < NN; e += 256) out[e] = cx<T>{re(1)[e], im(1)[e]};
+    QOC_STAMP(7);
+    return;
   }
   QOC_STAMP(1);
   const T scale = (T)ldexp(1.0, -sq);

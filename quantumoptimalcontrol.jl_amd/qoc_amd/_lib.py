@@ -49,6 +49,7 @@ SIGNATURES = {
     "qoc_set_profiling": (C.c_int, [_vp, C.c_int]),
     "qoc_phase_times": (C.c_int, [_vp, _dp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_pade_histogram": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
+    "qoc_taylor_histogram": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_get_info": (C.c_int, [_vp, C.POINTER(C.c_longlong)]),
     "qoc_set_spline_basis": (C.c_int, [_vp, _dp, C.c_int]),
     "qoc_eval_spline_dev": (C.c_int, [_vp, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),

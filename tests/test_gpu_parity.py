@@ -307,3 +307,29 @@ def test_compressed_states_give_identical_results(built_lib):
     np.testing.assert_allclose(J1, J0, rtol=0, atol=1e-13)
     np.testing.assert_allclose(g1, g0, rtol=1e-11, atol=1e-14)
     np.testing.assert_allclose(systems.decompress_states(x1N, v), x0N, rtol=0, atol=1e-13)
+
+
+def test_taylor_default_and_pade_option_agree(built_lib, monkeypatch):
+    """The LDS path runs the Taylor/Paterson-Stockmeyer exponential by default (no solve); QOC_EXPM_PADE=1
+    selects the reference's Padé + solve.  Both match the oracle; the histograms record what ran."""
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=20, Nt=12)
+    u = systems.cavity_controls(2, prob.Nt, seed=2)
+    out = {}
+    for pade in ("0", "1"):
+        monkeypatch.setenv("QOC_EXPM_PADE", pade)
+        e = _engine(prob, 2)
+        J = e.propagate(u)
+        g = e.grape_sensitivity(u, 3)
+        out[pade] = (J, g, e.pade_histogram(), e.taylor_histogram())
+        e.close()
+    J0, g0, ph0, th0 = out["0"]
+    J1, g1, ph1, th1 = out["1"]
+    assert th0 == {(14, 0): 24} and th1 == {}
+    assert ph0 == ph1 == {(7, 0): 24}
+    np.testing.assert_allclose(J0, J1, rtol=0, atol=1e-13)
+    np.testing.assert_allclose(g0, g1, rtol=1e-11, atol=1e-15)
+    for b in range(2):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        assert abs(J0[b] - Jr) <= 1e-12
+        assert np.linalg.norm(g0[b] - gr) / np.linalg.norm(gr) <= 1e-10

@@ -8,8 +8,8 @@
 #include "../quantumoptimalcontrol.jl_amd/csrc/qoc_expm.hpp"
 using namespace qoc;
 
-template <int NT>
-void run(int N, double scale, int units) {
+template <int NT, int ALG = 0>
+void run(int N, double scale, int units, std::vector<cx<double>>* keep = nullptr) {
   using E = Expm<double, NT>;
   std::vector<cx<double>> A((size_t)units * N * N);
   srand(1);
@@ -35,14 +35,14 @@ void run(int N, double scale, int units) {
   (void)hipMalloc(&dX, A.size() * 16);
   (void)hipMemcpy(dA, A.data(), A.size() * 16, hipMemcpyHostToDevice);
   size_t lds = E::lds_bytes(N);
-  (void)hipFuncSetAttribute((const void*)k_expm<double, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  (void)hipFuncSetAttribute((const void*)k_expm<double, NT, ALG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   for (int it = 0; it < 3; ++it) {
     (void)hipEventRecord(a);
-    hipLaunchKernelGGL((k_expm<double, NT>), dim3(units), dim3(256), lds, 0, N, 0, units, nullptr, nullptr, dA, dX,
-                       nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL((k_expm<double, NT, ALG>), dim3(units), dim3(256), lds, 0, N, 0, units, nullptr, nullptr, dA,
+                       dX, nullptr, nullptr, nullptr, nullptr);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
   }
@@ -50,8 +50,26 @@ void run(int N, double scale, int units) {
   (void)hipEventElapsedTime(&ms, a, b);
   unsigned long long st[64];
   (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_probe), sizeof(st));
-  printf("N=%d scale=%.3g units=%d lds=%zu  wall %.3f ms  (%.3f us/unit/CU-slot)\n", N, scale, units, lds, ms,
-         ms * 1e3 / units * 256);
+  printf("N=%d scale=%.3g units=%d ALG=%d lds=%zu  wall %.3f ms  (%.3f us/unit/CU-slot)\n", N, scale, units, ALG, lds,
+         ms, ms * 1e3 / units * 256);
+  if (keep) {
+    std::vector<cx<double>> X(A.size());
+    (void)hipMemcpy(X.data(), dX, X.size() * 16, hipMemcpyDeviceToHost);
+    if (keep->empty()) {
+      *keep = X;
+    } else {
+      double md = 0;
+      for (size_t i = 0; i < X.size(); ++i)
+        md = std::max(md, std::abs(X[i].r - (*keep)[i].r) + std::abs(X[i].i - (*keep)[i].i));
+      printf("   max |Taylor - Pade| = %.3g\n", md);
+    }
+  }
+  if (ALG == 1) {
+    printf("   form+norm %llu  A2 %llu  A3 %llu  Horner %llu  squarings %llu  store %llu\n", st[1] - st[0],
+           st[50] - st[1], st[51] - st[50], st[5] - st[51], st[6] - st[5], st[7] - st[6]);
+    goto done;
+  }
+  {
   const char* names[] = {"form+norm", "pade gemms", "Q/P store", "LU solve", "squarings", "store"};
   int idx[] = {0, 1, 2, 3, 5, 6, 7};
   for (int i = 0; i < 6; ++i) printf("   %-12s %8llu cycles(memtime)\n", names[i], st[idx[i + 1]] - st[idx[i]]);
@@ -64,6 +82,8 @@ void run(int N, double scale, int units) {
   if (st[44])
     printf("   GJ16 block p0=16: publish %llu  Dinv %llu  W %llu  update %llu\n", st[45] - st[44], st[46] - st[45],
            st[47] - st[46], st[48] - st[47]);
+  }
+done:
   (void)hipMemset(0, 0, 0);
   {
     unsigned long long z[64] = {0};
@@ -74,10 +94,26 @@ void run(int N, double scale, int units) {
 }
 
 int main(int argc, char** argv) {
-  run<1>(9, 0.1, 256 * 64);
-  run<2>(27, 30.0, 256 * 64);
-  run<3>(40, 0.5, 256 * 64);
-  run<3>(40, 0.5, 256);  // one workgroup per CU: uncontended phase costs
-  run<3>(40, 4.0, 256 * 16);
+  {
+    std::vector<cx<double>> k;
+    run<1, 0>(9, 0.11, 256 * 64, &k);
+    run<1, 1>(9, 0.11, 256 * 64, &k);
+  }
+  {
+    std::vector<cx<double>> k;
+    run<2, 0>(27, 30.0, 256 * 64, &k);
+    run<2, 1>(27, 30.0, 256 * 64, &k);
+  }
+  {
+    std::vector<cx<double>> k;
+    run<3, 0>(40, 0.33, 256 * 64, &k);
+    run<3, 1>(40, 0.33, 256 * 64, &k);
+  }
+  run<3, 1>(40, 0.33, 256);  // one workgroup per CU: uncontended phase costs
+  {
+    std::vector<cx<double>> k;
+    run<3, 0>(40, 4.0, 256 * 16, &k);
+    run<3, 1>(40, 4.0, 256 * 16, &k);
+  }
   return 0;
 }
