@@ -39,8 +39,14 @@ WORKLOADS = {
 
 
 def expm_flops(N, hist):
-    """Algorithmic FLOPs of the exponentials actually executed (degree-minimal GEMMs + LU solve)."""
+    """Algorithmic FLOPs of Padé exponentials (degree-minimal GEMMs + LU solve) for a (d, s) histogram."""
     return sum(cnt * (8.0 * N ** 3 * (GEMMS_PER_DEGREE[d] + s) + (40.0 / 3.0) * N ** 3) for (d, s), cnt in hist.items())
+
+
+def taylor_flops(N, thist):
+    """Algorithmic FLOPs of the executed Taylor / Paterson-Stockmeyer exponentials: degree m = 3r+2 costs
+    2 + r complex GEMMs (A2, A3, r Horner products in A3) plus s squarings, 8 N^3 flops each."""
+    return sum(cnt * 8.0 * N ** 3 * (2 + (m - 2) // 3 + s) for (m, s), cnt in thist.items())
 
 
 def ref_eval_flops(N, m, nu, hist_per_eval, order=3):
@@ -53,8 +59,12 @@ def ref_eval_flops(N, m, nu, hist_per_eval, order=3):
 
 
 def grad_flops(N, m, nu, Nt, B, order):
-    """Executed algorithmic FLOPs of k_grad: (order-1) X and X^H matvecs on x and λ, nu*order A_j matvecs."""
+    """Executed algorithmic FLOPs of the gradient phase.  Order 3 (the Ipopt path) runs as GEMMs over all
+    slices: 4 generator-combine GEMMs (N x (nu+1)N per state column: P1, P2, Q1, Q2) and 3 contraction
+    GEMMs (nu N x N: A_j P_a).  Other orders: k_grad's (order-1) X and X^H matvecs + nu*order A_j matvecs."""
     mv = 8.0 * N * N * m
+    if order == 3:
+        return B * Nt * mv * (4 * (nu + 1) + 3 * nu)
     return B * Nt * (2 * (order - 1) * mv + nu * order * mv)
 
 
@@ -179,6 +189,7 @@ def main():
     torch.cuda.synchronize()
 
     eng.pade_histogram(reset=True)
+    eng.taylor_histogram(reset=True)
     eng.phase_times(reset=True)
     info0 = eng.info()
     if info0["path"] == "large_n":
@@ -204,6 +215,7 @@ def main():
 
     phases = eng.phase_times()
     hist = eng.pade_histogram()
+    thist = eng.taylor_histogram()
     K = args.steps
     N, m, nu, Nt = prob.N, prob.m, prob.nu, prob.Nt
     esz = 16 if prob.precision == "fp64" else 8
@@ -224,7 +236,8 @@ def main():
             traffic_all = {}
     if not large:
         models = {
-            "k_expm": ("mfma", expm_flops(N, hist_launch) / 1e12, "TFLOP/s", peak),
+            "k_expm": ("mfma", (taylor_flops(N, {k: v / K for k, v in thist.items()}) if thist
+                                else expm_flops(N, hist_launch)) / 1e12, "TFLOP/s", peak),
             "k_grad": ("mfma", grad_flops(N, m, nu, Nt, B, args.order) / 1e12, "TFLOP/s", peak),
             "k_chain_fwd": ("hbm", chain_bytes(N, m, Nt, B, esz) / 1e9, "GB/s", PEAK_HBM_GBS),
             "k_chain_bwd": ("hbm", (chain_bytes(N, m, Nt, B, esz) + B * (Nt + 1) * N * m * esz) / 1e9, "GB/s",
@@ -316,6 +329,7 @@ def main():
             "cpu_baseline": cpu,
             "kernels": kern,
             "pade_hist_per_step": {f"d{d}s{s}": v / K for (d, s), v in sorted(hist.items())},
+            "taylor_hist_per_step": {f"m{mm}s{s}": v / K for (mm, s), v in sorted(thist.items())},
             "ref_equiv_gflop_per_eval": ref_f / 1e9,
             "ref_equiv_tflops": ref_f * value / 1e12,
             "parity_vs_cpu_port": parity,
