@@ -247,9 +247,12 @@ def main():
         # phases of the chunked GEMM pipeline (each a sequence of launches); executed GEMM FLOPs
         nchunks = math.ceil(B * Nt / info1["chunk"])
         ns_it = (info1["ns_iters"] - info0["ns_iters"]) / max(nchunks * K, 1)
-        g_expm = sum(c * (GEMMS_PER_DEGREE[d] + s) for (d, s), c in hist_launch.items())
-        slices = sum(hist_launch.values())
-        f_expm = 8.0 * N ** 3 * (g_expm + slices * (2 * ns_it + 1))
+        if thist:
+            f_expm = taylor_flops(N, {k: v / K for k, v in thist.items()})
+        else:
+            g_expm = sum(c * (GEMMS_PER_DEGREE[d] + s) for (d, s), c in hist_launch.items())
+            slices = sum(hist_launch.values())
+            f_expm = 8.0 * N ** 3 * (g_expm + slices * (2 * ns_it + 1))
         f_chain = 8.0 * N * N * m * B * Nt
         f_grad = 8.0 * N * N * m * B * Nt * (2 * (args.order - 1) + args.order)
         models = {
