@@ -88,7 +88,8 @@ struct qoc_ctx {
   double* d_Bs = nullptr;  // Nt x ns
   int ns = 0;
   double* d_cstage = nullptr;  // host-pointer variants: B x ns x nu coefficients / gradient
-  // GEMM-shaped gradient of the LDS-resident path (order 3): generator layouts + P/Q/W workspace
+  // GEMM-shaped gradient of the LDS-resident path (order 3, N >= 32: below that the 64-row GEMM tiles
+  // are mostly padding and the per-slice k_grad is faster): generator layouts + P/Q/W workspace
   void* d_AH = nullptr;    // (nu+1) x N*N: [A0^H | A1^H | ...]
   void* d_Cst = nullptr;   // nu N x N: [A1; A2; ...]
   void* d_gws = nullptr;   // 6 x N x B(Nt+1)m
@@ -951,7 +952,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
     if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return bail(e, "hipMalloc");
     c->dev_bytes += a.bytes;
   }
-  c->grad_gemm = !c->big && N >= 6 && nu <= 8 && !(getenv("QOC_GRAD_KERNEL") && atoi(getenv("QOC_GRAD_KERNEL")) != 0);
+  c->grad_gemm = !c->big && N >= 32 && nu <= 8 && !(getenv("QOC_GRAD_KERNEL") && atoi(getenv("QOC_GRAD_KERNEL")) != 0);
   if (c->grad_gemm) {
     const size_t cols = (size_t)B * (Nt + 1) * m;
     if ((e = hipMalloc(&c->d_AH, (nu + 1) * NN * c->esz)) != hipSuccess) return bail(e, "hipMalloc");

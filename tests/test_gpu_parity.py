@@ -333,3 +333,28 @@ def test_taylor_default_and_pade_option_agree(built_lib, monkeypatch):
         Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
         assert abs(J0[b] - Jr) <= 1e-12
         assert np.linalg.norm(g0[b] - gr) / np.linalg.norm(gr) <= 1e-10
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_gemm_gradient_n40_penalty_and_precision(built_lib, precision):
+    """N >= 32 selects the GEMM-shaped order-3 gradient (generator-combine + fused contraction); cover it
+    with the guard-state penalty (λ carries dL/dx) in both precisions, and check it against k_grad."""
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=20, Nt=16)
+    u = systems.cavity_controls(3, prob.Nt, seed=11)
+    pen = (list(range(30, 40)), [0, 1], 0.23)
+    _check(prob, u, precision=precision, penalty=pen)
+
+
+def test_gemm_gradient_equals_per_slice_kernel(built_lib, monkeypatch):
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=20, Nt=10)
+    u = systems.cavity_controls(2, prob.Nt, seed=12)
+    res = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("QOC_GRAD_KERNEL", env)
+        e = _engine(prob, 2)
+        e.propagate(u)
+        res.append(e.grape_sensitivity(u, 3))
+        e.close()
+    np.testing.assert_allclose(res[0], res[1], rtol=1e-12, atol=1e-15)
