@@ -120,6 +120,27 @@ int qoc_phase_times(qoc_ctx* ctx, double* ms_out /*[4]*/, long long* launches_ou
  * GEMM item) of the k_bgemm launches recorded while profiling was enabled. */
 int qoc_gemm_stats(qoc_ctx* ctx, double* ms, long long* launches, double* flops, int reset);
 
+/* Propagation method.  QOC_PROP_EXPM (default): U_k = exp(A_k) per slice.
+ * QOC_PROP_TSIT5: the reference's ODE path propagate_pwc / compute_pwc_gradient
+ * (src/gradient_computations.jl:108-169): nsub fixed Tsit5 steps per slice (the reference's
+ * dt = 0.1 Δt is nsub = 10) for the states and, backwards, for the co-states dλ/dτ = -A_k^H λ; the
+ * gradient contraction is unchanged.  LDS-resident sizes (N <= 64), trace / external costs. */
+#define QOC_PROP_EXPM 0
+#define QOC_PROP_TSIT5 1
+int qoc_set_propagation(qoc_ctx* ctx, int method, int nsub);
+
+/* Continuous-envelope propagation with fixed-step Tsit5 (wrap_envelope, src/QuantumOptimalControl.jl:43-54;
+ * examples/two_qubit_tunable_bus.jl:58-67): dx/dt = (A0 + sum_j c_j(t) A_j) x, t in [0, tgate], step dt,
+ * with c(t) from the pulse `kind` and per-seed parameters params[b*np ...] (src/parameterized_pulses.jl).
+ * The generators are used as set (not Δt-scaled).  x_out (optional, B x N x m interleaved complex,
+ * column-major per seed) receives x(tgate); J_out (optional, B) the trace cost when one is set.  QOC_ENV_TUNABLE_BUS: [t_plateau, t_rise_fall, theta0, omega_Phi, A], nu = 1;
+ * QOC_ENV_DRAG (u_drag): [tgate, sigma, A, xi], nu = 2 (Re, Im); QOC_ENV_SINEBASIS: [Tgate, p1x, p1y, ...], nu = 2. */
+#define QOC_ENV_TUNABLE_BUS 0
+#define QOC_ENV_DRAG 1
+#define QOC_ENV_SINEBASIS 2
+int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np, double tgate, double dt,
+                           double* J_out, double* x_out);
+
 /* Engine facts: info[0] = path (0 = LDS-resident kernels, 1 = large-N chunked GEMM pipeline),
  * info[1] = slices per chunk (large-N), info[2] = Newton-Schulz iterations executed so far (large-N),
  * info[3] = device bytes allocated by the context.  QOC_FORCE_LARGE_N=1 in the environment at

@@ -499,3 +499,134 @@ def spline_constraints(c, ns):
         Dp[1:ns] = D
         J[1] = (Dp[:ns] - Dp[1:]).ravel(order="F") / g[1]
     return g, J
+
+
+# ---------------------------------------------------------------------------
+# ODE path: fixed-step Tsit5
+#   propagate_pwc / compute_pwc_gradient (src/gradient_computations.jl:108-169) and the
+#   continuous-envelope propagation of examples/two_qubit_tunable_bus.jl:10-67.
+# Tsit5 is OrdinaryDiffEq's Tsitouras (2011) 5(4) pair (third-party, absent here); the tableau is
+# restated below and pinned by the reference's known answer 0.937218 (two_qubit_tunable_bus.jl:67,
+# reproduced to 0.9372181 by tests/test_oracle.py::test_tsit5_tunable_bus_known_answer).
+# ---------------------------------------------------------------------------
+TSIT5_C = (0.0, 0.161, 0.327, 0.9, 0.9800255409045097, 1.0, 1.0)
+TSIT5_A = ((),
+           (0.161,),
+           (-0.008480655492356989, 0.335480655492357),
+           (2.897153057105493, -6.359448489975075, 4.3622954328695815),
+           (5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525),
+           (5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383),
+           (0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081,
+            2.324710524099774))  # last row = b (FSAL)
+
+
+def tsit5_fixed(f, x0, t0, dt, nsteps):
+    """nsteps fixed Tsit5 steps of size dt (adaptive=false) from t0; f(x, t) -> dx/dt.  FSAL: the
+    seventh stage at x_{n+1} is the next step's first stage."""
+    x = np.array(x0, dtype=np.complex128, copy=True)
+    t = t0
+    k1 = f(x, t)
+    for s in range(nsteps):
+        ks = [k1]
+        for i in range(1, 7):
+            xi = x + dt * sum(TSIT5_A[i][j] * ks[j] for j in range(i))
+            ks.append(f(xi, t + TSIT5_C[i] * dt))
+        x = x + dt * sum(TSIT5_A[6][j] * ks[j] for j in range(6))
+        k1 = ks[6]
+        t = t0 + (s + 1) * dt
+    return x
+
+
+def cos_envelope(t_plateau, t_rise_fall, t):
+    """src/parameterized_pulses.jl cos_envelope."""
+    if t_rise_fall / 2 < t <= t_rise_fall / 2 + t_plateau:
+        return 1.0
+    if t <= t_rise_fall / 2:
+        return 0.5 * (1 - math.cos(2 * math.pi * t / t_rise_fall))
+    return 0.5 * (1 - math.cos(2 * math.pi * (t - t_plateau) / t_rise_fall))
+
+
+def tunable_bus_envelope(p, t):
+    """examples/two_qubit_tunable_bus.jl:10-18: sqrt|cos(pi (theta0 + A delta(t) cos(omega t)))|."""
+    t_plateau, t_rise_fall, th0, w, amp = p
+    d = cos_envelope(t_plateau, t_rise_fall, t)
+    return math.sqrt(abs(math.cos(math.pi * (th0 + amp * d * math.cos(w * t)))))
+
+
+def drag_envelope(p, t):
+    """src/parameterized_pulses.jl:1-13 u_drag -> reim: (A Ωx, A Ωy)."""
+    tgate, sigma, amp, xi = p[:4]
+    x = t - tgate / 2
+    tmp = math.exp(-x * x / (2 * sigma ** 2))
+    return (amp * (tmp - math.exp(-tgate ** 2 / (8 * sigma ** 2))), amp * (-xi * x / sigma ** 2 * tmp))
+
+
+def sinebasis_envelope(p, t):
+    """src/parameterized_pulses.jl:15-25 u_sinebasis -> reim: sum_k p_{2k}, p_{2k+1} sinpi(k t / Tgate)."""
+    T = p[0]
+    ox = oy = 0.0
+    for k in range(1, len(p) // 2 + 1):
+        bk = math.sin(math.pi * k * t / T)
+        ox += p[2 * k - 1] * bk
+        oy += p[2 * k] * bk
+    return (ox, oy)
+
+
+def propagate_envelope(A0, A, envelope, p, x0, tgate, dt):
+    """dx/dt = (A0 + sum_j c_j(t) A_j) x with c(t) = envelope(p, t) (scalar or sequence), fixed-step Tsit5
+    (examples/two_qubit_tunable_bus.jl:58-60; wrap_envelope, src/QuantumOptimalControl.jl:43-54)."""
+    A0 = np.asarray(A0, dtype=np.complex128)
+    A = [np.asarray(a, dtype=np.complex128) for a in A]
+
+    def f(x, t):
+        cv = np.atleast_1d(envelope(p, t))
+        return A0 @ x + sum(cv[j] * (A[j] @ x) for j in range(len(A)))
+    nsteps = int(round(tgate / dt))
+    return tsit5_fixed(f, x0, 0.0, dt, nsteps)
+
+
+def propagate_pwc_ode(A0, A, u, x0, nsub=10):
+    """propagate_pwc (src/gradient_computations.jl:108-128) on the Δt-prescaled generators: slice k is
+    dx/dτ = A_k x over τ ∈ [k, k+1] with nsub fixed Tsit5 steps (the reference's dt = 0.1Δt, its
+    PeriodicCallback switching u at every Δt).  Returns the Nt+1 slice-boundary states."""
+    u = np.asarray(u, dtype=np.float64)
+    x = np.asarray(x0, dtype=np.complex128)
+    if x.ndim == 1:
+        x = x[:, None]
+    xs = [x.copy()]
+    for k in range(u.shape[1]):
+        Ak = np.asarray(A0, dtype=np.complex128) + sum(u[j, k] * np.asarray(A[j]) for j in range(len(A)))
+        x = tsit5_fixed(lambda y, t: Ak @ y, x, 0.0, 1.0 / nsub, nsub)
+        xs.append(x.copy())
+    return xs
+
+
+def grape_eval_ode(A0, A, u, x0, x_target, n=None, order=3, nsub=10, penalty=None):
+    """compute_pwc_gradient (src/gradient_computations.jl:130-169) with the exp path's conventions:
+    states x_k from propagate_pwc_ode, co-states by the backward adjoint ODE dλ/dτ = -A_k^H λ (fixed
+    Tsit5, nsub steps per slice, + dL/dx at slice boundaries as in the exp path), and
+    dJdu[j, k] = _compute_u_sensitivity(x_k, λ_{k+1}, expm_jacobian(A_k)[j]).  Returns (J, dJdu)."""
+    u = np.asarray(u, dtype=np.float64)
+    Nt = u.shape[1]
+    Jf, dJf = setup_infidelity(x_target, n)
+    L = dL = None
+    if penalty is not None:
+        L, dL = setup_state_penalty(*penalty)
+    xs = propagate_pwc_ode(A0, A, u, x0, nsub)
+    J = Jf(xs[-1]) + (sum(L(xk) for xk in xs) if L is not None else 0.0)
+    lam = [None] * (Nt + 1)
+    lam[Nt] = np.asarray(dJf(xs[Nt]), dtype=np.complex128)
+    if dL is not None:
+        lam[Nt] = lam[Nt] + dL(xs[Nt])
+    for k in range(Nt - 1, -1, -1):
+        Ak = np.asarray(A0, dtype=np.complex128) + sum(u[j, k] * np.asarray(A[j]) for j in range(len(A)))
+        AkH = Ak.conj().T
+        lam[k] = tsit5_fixed(lambda y, t: AkH @ y, lam[k + 1], 0.0, 1.0 / nsub, nsub)
+        if dL is not None:
+            lam[k] = lam[k] + dL(xs[k])
+    dJdu = np.zeros_like(u)
+    for k in range(Nt):
+        dU = expm_jacobian(A0, A, u[:, k], order=order)
+        for j in range(len(A)):
+            dJdu[j, k] = compute_u_sensitivity(xs[k], lam[k + 1], dU[j])
+    return J, dJdu

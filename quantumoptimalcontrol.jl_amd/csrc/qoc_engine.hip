@@ -20,6 +20,7 @@
 #include "qoc_chain.hpp"
 #include "qoc_expm.hpp"
 #include "qoc_frechet.hpp"
+#include "qoc_ode.hpp"
 #include "qoc_spline.hpp"
 
 using namespace qoc;
@@ -54,6 +55,8 @@ struct qoc_ctx {
   int* d_flag = nullptr;
   unsigned long long* d_hist = nullptr;  // 5*64 reference (Padé) selection + 7*64 executed Taylor (r, s)
   int expm_alg = 1;                      // 1 Taylor / Paterson-Stockmeyer (default), 0 Padé (QOC_EXPM_PADE=1)
+  int prop_method = 0;                   // QOC_PROP_EXPM / QOC_PROP_TSIT5
+  int nsub = 10;                         // Tsit5 steps per slice (reference dt = 0.1 Δt)
   double* d_stage = nullptr;             // host->device staging (fp64 complex), max(B*N*m, (nu+1)*N*N)*2
   size_t stage_elems = 0;
   std::vector<double> h_u;
@@ -243,7 +246,13 @@ template <typename T>
 int grad_gemm_o3(qoc_ctx* c, double* d_dJdu);
 
 template <typename T>
+int ode_forward(qoc_ctx* c);
+template <typename T>
+int ode_adjoint(qoc_ctx* c);
+
+template <typename T>
 int run_forward(qoc_ctx* c) {
+  if (c->prop_method == QOC_PROP_TSIT5) return ode_forward<T>(c);
   int mk = mark_begin(c, 0);
   hipError_t e = launch_expm(c->prec, c->stream, c->N, c->nu, c->B * c->Nt, c->d_A, c->d_u, nullptr, c->d_U,
                              c->d_hist, nullptr, nullptr, c->expm_alg, c->d_hist + 5 * 64);
@@ -264,13 +273,19 @@ int run_forward(qoc_ctx* c) {
 template <typename T>
 int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
   size_t lds = chain_lds(c);
-  HIPCHK(c, hipFuncSetAttribute((const void*)k_chain_bwd<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  int mk = mark_begin(c, 2);
-  hipLaunchKernelGGL((k_chain_bwd<T>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
-                     (const cx<T>*)c->d_U, (const cx<T>*)c->d_X, (cx<T>*)c->d_L, (const cx<T>*)c->d_Xt, c->cost_kind,
-                     (const cx<double>*)c->d_coef, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu);
-  mark_end(c, mk);
-  HIPCHK(c, hipGetLastError());
+  int mk;
+  if (c->prop_method == QOC_PROP_TSIT5) {
+    int r = ode_adjoint<T>(c);
+    if (r) return r;
+  } else {
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_chain_bwd<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    mk = mark_begin(c, 2);
+    hipLaunchKernelGGL((k_chain_bwd<T>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
+                       (const cx<T>*)c->d_U, (const cx<T>*)c->d_X, (cx<T>*)c->d_L, (const cx<T>*)c->d_Xt, c->cost_kind,
+                       (const cx<double>*)c->d_coef, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu);
+    mark_end(c, mk);
+    HIPCHK(c, hipGetLastError());
+  }
   if (order == QOC_DUKDP_EXACT) {
     mk = mark_begin(c, 3);
     int r = frechet_grad<T>(c, d_dJdu);
@@ -874,6 +889,60 @@ int frechet_grad(qoc_ctx* c, double* d_dJdu) {
   return QOC_OK;
 }
 
+// ---- ODE path (fixed-step Tsit5, qoc_ode.hpp) ------------------------------------------------
+template <typename T>
+int ode_forward(qoc_ctx* c) {
+  const int W = std::min(c->m, 4);
+  const size_t lds = (size_t)c->N * c->N * c->esz;
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_ode_pwc<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int mk = mark_begin(c, 1);
+  hipLaunchKernelGGL((k_ode_pwc<T>), dim3(c->B), dim3(64 * W), lds, c->stream, c->N, c->m, c->nu, c->Nt, c->nsub, 0,
+                     (const cx<T>*)c->d_A, (const double*)c->d_u, (const cx<T>*)c->d_x0, c->x0_per_seed,
+                     (cx<T>*)c->d_X, (const cx<T>*)c->d_X, (const unsigned char*)nullptr, 0.0);
+  HIPCHK(c, hipGetLastError());
+  const bool pen = c->mu != 0.0;
+  if (pen) {
+    hipLaunchKernelGGL((k_penalty_sum<T>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
+                       (const cx<T>*)c->d_X, c->d_pmask, c->mu, c->d_J);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (c->cost_kind == QOC_COST_TRACE) {
+    hipLaunchKernelGGL((k_trace_cost<T>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
+                       (const cx<T>*)c->d_X, (const cx<T>*)c->d_Xt, c->cost_n, pen ? 1 : 0, c->d_J, c->d_coef);
+    HIPCHK(c, hipGetLastError());
+  } else if (!pen) {
+    HIPCHK(c, hipMemsetAsync(c->d_J, 0, (size_t)c->B * sizeof(double), c->stream));
+  }
+  mark_end(c, mk);
+  return QOC_OK;
+}
+
+template <typename T>
+int ode_adjoint(qoc_ctx* c) {
+  const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
+  const size_t Nm = (size_t)N * m;
+  const bool pen = c->mu != 0.0;
+  const unsigned eb = (unsigned)std::min<size_t>((Nm * B + 255) / 256, 8192);
+  int mk = mark_begin(c, 2);
+  if (c->cost_kind == QOC_COST_TRACE) {
+    hipLaunchKernelGGL((k_lambda_final<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, (const cx<T>*)c->d_Xt,
+                       (const cx<double>*)c->d_coef, (cx<T>*)c->d_L);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (pen) {
+    hipLaunchKernelGGL((k_penalty_grad<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, Nt,
+                       (const cx<T>*)c->d_X, c->d_pmask, 2.0 * c->mu, (cx<T>*)c->d_L);
+    HIPCHK(c, hipGetLastError());
+  }
+  const int W = std::min(m, 4);
+  hipLaunchKernelGGL((k_ode_pwc<T>), dim3(B), dim3(64 * W), (size_t)N * N * c->esz, c->stream, N, m, c->nu, Nt,
+                     c->nsub, 1, (const cx<T>*)c->d_A, (const double*)c->d_u, (const cx<T>*)c->d_x0, c->x0_per_seed,
+                     (cx<T>*)c->d_L, (const cx<T>*)c->d_X, pen ? c->d_pmask : nullptr, 2.0 * c->mu);
+  HIPCHK(c, hipGetLastError());
+  mark_end(c, mk);
+  return QOC_OK;
+}
+
 int forward(qoc_ctx* c) {
   if (c->big) return c->prec == QOC_FP64 ? big_forward<double>(c) : big_forward<float>(c);
   return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
@@ -1059,6 +1128,8 @@ int qoc_set_cost(qoc_ctx* c, int kind, const double* X_target, double n) {
     return fail(c, QOC_ERR_ARG, "unknown cost kind %d", kind);
   if (kind == QOC_COST_ZCAL && c->m != 4)
     return fail(c, QOC_ERR_ARG, "Only works for two-qubit gates, x_target must have four columns");
+  if (kind == QOC_COST_ZCAL && c->prop_method == QOC_PROP_TSIT5)
+    return fail(c, QOC_ERR_UNSUPPORTED, "z-calibrated cost is not implemented on the Tsit5 path");
   if (kind == QOC_COST_ZCAL && c->big)
     return fail(c, QOC_ERR_UNSUPPORTED, "z-calibrated cost is not implemented on the large-N path");
   if (kind != QOC_COST_EXTERNAL && !X_target) return fail(c, QOC_ERR_ARG, "X_target is null");
@@ -1211,6 +1282,7 @@ int qoc_get_costates(qoc_ctx* c, int seed, int k, double* lam_out) {
 int qoc_get_propagator(qoc_ctx* c, int seed, int k, double* U_out) {
   if (!c || !U_out) return fail(c, QOC_ERR_ARG, "null argument");
   if (!c->have_prop) return fail(c, QOC_ERR_STATE, "no propagators");
+  if (c->prop_method == QOC_PROP_TSIT5) return fail(c, QOC_ERR_STATE, "the Tsit5 path does not form propagators");
   if (seed < 0 || seed >= c->B || k < 0 || k >= c->Nt) return fail(c, QOC_ERR_ARG, "index out of range");
   HIPCHK(c, hipSetDevice(c->dev));
   const size_t NN = (size_t)c->N * c->N;
@@ -1331,6 +1403,81 @@ int qoc_spline_constraints_dev(qoc_ctx* c, const double* d_c, double* d_g, doubl
   HIPCHK(c, hipSetDevice(c->dev));
   hipLaunchKernelGGL(k_spline_constraints, dim3(c->B), dim3(256), 0, c->stream, c->ns, c->nu, d_c, d_g, d_gjac);
   HIPCHK(c, hipGetLastError());
+  return QOC_OK;
+}
+
+int qoc_set_propagation(qoc_ctx* c, int method, int nsub) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  if (method != QOC_PROP_EXPM && method != QOC_PROP_TSIT5) return fail(c, QOC_ERR_ARG, "unknown method %d", method);
+  if (method == QOC_PROP_TSIT5) {
+    if (nsub < 1) return fail(c, QOC_ERR_ARG, "nsub must be >= 1 (got %d)", nsub);
+    if (c->big || c->N > 64)
+      return fail(c, QOC_ERR_UNSUPPORTED, "the Tsit5 path runs on the LDS-resident sizes (N <= 64)");
+    if (c->cost_kind == QOC_COST_ZCAL)
+      return fail(c, QOC_ERR_UNSUPPORTED, "z-calibrated cost is not implemented on the Tsit5 path");
+    c->nsub = nsub;
+  }
+  c->prop_method = method;
+  c->have_prop = false;
+  return QOC_OK;
+}
+
+int qoc_propagate_envelope(qoc_ctx* c, int kind, const double* params, int np, double tgate, double dt, double* J_out,
+                           double* x_out) {
+  int r = check_ready(c);
+  if (r) return r;
+  if (!params || np < 1 || np > 64) return fail(c, QOC_ERR_ARG, "bad parameter array");
+  if (kind < QOC_ENV_TUNABLE_BUS || kind > QOC_ENV_SINEBASIS) return fail(c, QOC_ERR_ARG, "unknown envelope %d", kind);
+  const int need_nu = kind == QOC_ENV_TUNABLE_BUS ? 1 : 2;
+  if (c->nu != need_nu) return fail(c, QOC_ERR_ARG, "envelope %d drives %d controls, context has nu=%d", kind, need_nu, c->nu);
+  if (c->big || c->N > 64) return fail(c, QOC_ERR_UNSUPPORTED, "the Tsit5 path runs on the LDS-resident sizes (N <= 64)");
+  if (c->cost_kind == QOC_COST_ZCAL) return fail(c, QOC_ERR_UNSUPPORTED, "z-calibrated cost on the Tsit5 path");
+  if (!(dt > 0) || !(tgate > 0)) return fail(c, QOC_ERR_ARG, "tgate and dt must be positive");
+  const long long nsteps = (long long)std::llround(tgate / dt);
+  const size_t env_lds = (size_t)(c->nu + 1) * c->N * c->N * c->esz;
+  if (env_lds > 160 * 1024) return fail(c, QOC_ERR_UNSUPPORTED, "generators (%zu B) exceed the 160 KiB LDS", env_lds);
+  if (c->prec == QOC_FP64)
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_ode_envelope<double>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)env_lds));
+  else
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_ode_envelope<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)env_lds));
+  double* dP = nullptr;
+  HIPCHK(c, hipMalloc((void**)&dP, (size_t)c->B * np * sizeof(double)));
+  hipError_t e = hipMemcpy(dP, params, (size_t)c->B * np * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    const int W = std::min(c->m, 4);
+    const size_t lds = env_lds;
+    if (c->prec == QOC_FP64)
+      hipLaunchKernelGGL((k_ode_envelope<double>), dim3(c->B), dim3(64 * W), lds, c->stream, c->N, c->m, c->nu, c->Nt,
+                         kind, (const double*)dP, np, dt, nsteps, (const cx<double>*)c->d_A,
+                         (const cx<double>*)c->d_x0, c->x0_per_seed, (cx<double>*)c->d_X);
+    else
+      hipLaunchKernelGGL((k_ode_envelope<float>), dim3(c->B), dim3(64 * W), lds, c->stream, c->N, c->m, c->nu, c->Nt,
+                         kind, (const double*)dP, np, dt, nsteps, (const cx<float>*)c->d_A,
+                         (const cx<float>*)c->d_x0, c->x0_per_seed, (cx<float>*)c->d_X);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess && c->cost_kind == QOC_COST_TRACE) {
+    if (c->prec == QOC_FP64)
+      hipLaunchKernelGGL((k_trace_cost<double>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
+                         (const cx<double>*)c->d_X, (const cx<double>*)c->d_Xt, c->cost_n, 0, c->d_J, c->d_coef);
+    else
+      hipLaunchKernelGGL((k_trace_cost<float>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
+                         (const cx<float>*)c->d_X, (const cx<float>*)c->d_Xt, c->cost_n, 0, c->d_J, c->d_coef);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess && J_out && c->cost_kind == QOC_COST_TRACE)
+    e = hipMemcpy(J_out, c->d_J, c->B * sizeof(double), hipMemcpyDeviceToHost);
+  hipFree(dP);
+  if (e == hipSuccess && x_out) {
+    const size_t Nm = (size_t)c->N * c->m;
+    for (int b = 0; b < c->B; ++b) {
+      int r2 = download(c, (char*)c->d_X + ((size_t)b * (c->Nt + 1) + c->Nt) * Nm * c->esz, x_out + 2 * Nm * b, Nm);
+      if (r2) return r2;
+    }
+  }
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "qoc_propagate_envelope: %s", hipGetErrorString(e));
+  c->have_prop = false;  // states other than x(tgate) are not stored
   return QOC_OK;
 }
 

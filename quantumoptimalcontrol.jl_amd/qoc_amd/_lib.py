@@ -23,6 +23,9 @@ QOC_DUKDP_EXACT = 0
 QOC_COST_TRACE = 0
 QOC_COST_ZCAL = 1
 QOC_COST_EXTERNAL = 2
+QOC_PROP_EXPM = 0
+QOC_PROP_TSIT5 = 1
+QOC_ENV = {"tunable_bus": 0, "drag": 1, "sinebasis": 2}
 
 # Every symbol include/qoc.h declares, with (restype, argtypes).
 _dp = C.POINTER(C.c_double)
@@ -50,6 +53,8 @@ SIGNATURES = {
     "qoc_phase_times": (C.c_int, [_vp, _dp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_pade_histogram": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_taylor_histogram": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
+    "qoc_set_propagation": (C.c_int, [_vp, C.c_int, C.c_int]),
+    "qoc_propagate_envelope": (C.c_int, [_vp, C.c_int, _dp, C.c_int, C.c_double, C.c_double, _dp, _dp]),
     "qoc_get_info": (C.c_int, [_vp, C.POINTER(C.c_longlong)]),
     "qoc_set_spline_basis": (C.c_int, [_vp, _dp, C.c_int]),
     "qoc_eval_spline_dev": (C.c_int, [_vp, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),

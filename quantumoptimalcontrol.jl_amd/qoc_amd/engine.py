@@ -141,6 +141,30 @@ class GrapeEngine:
         self._chk(self._lib.qoc_set_state_penalty(self._h, P.ctypes.data_as(ip), len(P), Cc.ctypes.data_as(ip),
                                                   len(Cc), float(mu)))
 
+    def set_propagation(self, method: str = "expm", nsub: int = 10):
+        """'expm' (U_k = exp(A_k), default) or 'tsit5': the reference's ODE path (propagate_pwc /
+        compute_pwc_gradient, src/gradient_computations.jl:108-169) with nsub fixed Tsit5 steps per
+        slice (the reference's dt = 0.1 Δt is nsub = 10)."""
+        m = {"expm": L.QOC_PROP_EXPM, "tsit5": L.QOC_PROP_TSIT5}[method]
+        self._chk(self._lib.qoc_set_propagation(self._h, m, int(nsub)))
+        self.prop_method = method
+
+    def propagate_envelope(self, kind: str, params, tgate: float, dt: float):
+        """Continuous pulse c(t) (wrap_envelope, src/QuantumOptimalControl.jl:43-54) integrated with
+        fixed-step Tsit5 on [0, tgate]: params (B, np) per seed -> (J (B,) or None, x(tgate) (B, N, m))."""
+        P = np.ascontiguousarray(params, dtype=np.float64)
+        if P.ndim == 1:
+            P = P[None]
+        if P.shape[0] != self.B:
+            raise ValueError(f"params must be (B={self.B}, np), got {P.shape}")
+        J = np.zeros(self.B)
+        X = np.zeros(2 * self.B * self.N * self.m)
+        self._chk(self._lib.qoc_propagate_envelope(self._h, L.QOC_ENV[kind], _ptr(P), P.shape[1], float(tgate),
+                                                   float(dt), _ptr(J), _ptr(X)))
+        Xc = X.view(np.complex128).reshape(self.B, self.N * self.m)
+        xs = np.stack([_from_cm(x, self.N, self.m) for x in Xc])
+        return (J if self.cost_kind == "trace" else None), xs
+
     # ---- hot path (host arrays) ---------------------------------------------------
     def propagate(self, u) -> np.ndarray:
         """Forward pass for all seeds; returns J (B,) = Jfinal(x_N) + sum_k L(x_k)."""

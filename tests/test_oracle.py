@@ -326,3 +326,35 @@ def test_exact_gradient_matches_finite_differences_and_adjoint_identity():
     _, Lz = O.expm_frechet_block(Ak, Z)
     for j in range(2):
         assert abs(np.real(np.trace(prob.A[j] @ Lz)) - g[j, k]) < 1e-12
+
+
+# ---- ODE path (fixed-step Tsit5), SURVEY.md §8f item 3 ----------------------------------------
+def test_tsit5_tunable_bus_known_answer():
+    """examples/two_qubit_tunable_bus.jl:58-67: |<200|x(350)>|^2 'should be something like 0.937218'."""
+    H0, Hc, qb = S.tunable_bus_model()
+    x0 = qb.columns(["110"])[:, 0].astype(complex)
+    xt = qb.columns(["200"])[:, 0].astype(complex)
+    i1, i2 = int(np.argmax(np.abs(x0))), int(np.argmax(np.abs(xt)))
+    w_phi = abs(H0[i1, i1] - H0[i2, i2]) + (-0.002) * 2 * math.pi
+    p0 = [300.0, 50.0, 0.25, w_phi, 0.13]
+    x = O.propagate_envelope(-1j * H0, [-1j * Hc], O.tunable_bus_envelope, p0, x0, 350.0, 1e-3)
+    assert abs(abs(np.vdot(x, xt)) ** 2 - 0.937218) < 5e-7
+
+
+def test_tsit5_order_and_pwc_ode_matches_expm_path():
+    # 5th order: halving the step reduces the error by ~32
+    rng = np.random.default_rng(3)
+    H = rng.standard_normal((6, 6)) + 1j * rng.standard_normal((6, 6))
+    A = -1j * (H + H.conj().T) / 4
+    x0 = rng.standard_normal(6) + 1j * rng.standard_normal(6)
+    ex = sl.expm(A) @ x0
+    e1 = np.abs(O.tsit5_fixed(lambda y, t: A @ y, x0, 0.0, 1 / 8, 8) - ex).max()
+    e2 = np.abs(O.tsit5_fixed(lambda y, t: A @ y, x0, 0.0, 1 / 16, 16) - ex).max()
+    assert 20 < e1 / e2 < 50
+    # PWC ODE gradient (nsub = 10) agrees with the expm path to the integrator's accuracy
+    prob = S.zz_problem(30, tgate=3.0)
+    u = S.zz_controls(1, 30, 3.0, seed=2)[0]
+    J1, g1, _ = O.grape_eval(prob.A0, prob.A, u, prob.x0, prob.x_target, prob.n, order=3)
+    J2, g2 = O.grape_eval_ode(prob.A0, prob.A, u, prob.x0, prob.x_target, prob.n, order=3, nsub=10)
+    assert abs(J1 - J2) < 1e-9
+    assert np.linalg.norm(g1 - g2) / np.linalg.norm(g1) < 1e-7
