@@ -4,6 +4,7 @@ Mirrors (same names, argument meaning and error behaviour):
   * ``setup_grape_cache(A0, x0, u_size)``                 src/gradient_computations.jl:79-96
   * ``propagate(A0, A, u, x0, cache)``                     src/gradient_computations.jl:2-32
   * ``grape_sensitivity(A0, A, dJfinal_dx, u, x0, cache; dUkdp_order=3, dL_dx)``  :35-77
+  * ``propagate_pwc``, ``compute_pwc_gradient`` (the ODE/Tsit5 path)  :108-169
   * ``setup_infidelity``, ``setup_infidelity_zcalibrated``, ``setup_state_penalty``
                                                           src/penalty_fcns.jl:1-42
 so ``examples/ipopt_callbacks_exp.jl`` reads the same with this module in place of
@@ -224,3 +225,43 @@ def grape_sensitivity(A0, A, dJfinal_dx, u, x0, cache: MI355XCache, dUkdp_order=
     dJdu = e.grape_sensitivity(u, dUkdp_order, lambda_final=lam)
     cache.dJdu = dJdu[0] if u.ndim == 2 else dJdu
     return cache.dJdu
+
+
+# ---------------------------------------------------------------------------
+# ODE path (src/gradient_computations.jl:108-169): fixed-step Tsit5 on the GPU
+# ---------------------------------------------------------------------------
+def _nsub(Δt, dt):
+    nsub = 10 if dt is None else int(round(Δt / dt))
+    if nsub < 1 or (dt is not None and abs(nsub * dt - Δt) > 1e-9 * Δt):
+        raise ValueError(f"dt = {dt} must divide Δt = {Δt}")
+    return nsub
+
+
+def propagate_pwc(A0, A, x0, u, Δt, cache: MI355XCache | None = None, dt=None):
+    """propagate_pwc (src/gradient_computations.jl:108-128): dx/dt = (A0 + sum_j u_jk A_j) x on
+    [kΔt, (k+1)Δt) with fixed Tsit5 steps dt (default 0.1Δt).  A0, A are the physical generators
+    (-iH, not Δt-scaled) in place of the reference's `f` closure; returns the slice-boundary states."""
+    u = np.asarray(u, dtype=np.float64)
+    if cache is None:
+        cache = setup_grape_cache(A0, x0, u.shape[-2:], B=1 if u.ndim == 2 else u.shape[0])
+    e = cache.engine
+    e.set_propagation("tsit5", _nsub(Δt, dt))
+    return propagate(Δt * np.asarray(A0, dtype=np.complex128), [Δt * np.asarray(a, dtype=np.complex128) for a in A],
+                     u, x0, cache)
+
+
+def compute_pwc_gradient(dJfinal_dx, u, Δt, A0, A, cache: MI355XCache, dUkdp_order=2, dt=None, x0=None):
+    """compute_pwc_gradient (src/gradient_computations.jl:130-169): co-states by the adjoint ODE
+    dλ/dt = -A_k^H λ with the same fixed steps, then dJdu[j, k] from expm_jacobian! of order
+    dUkdp_order.  dUkdp_order = 0 returns after the co-state sweep, as the reference does (:152).
+    Call after propagate_pwc with the same u (the stale-u check of grape_sensitivity applies)."""
+    e = cache.engine
+    nsub = _nsub(Δt, dt)
+    if (getattr(e, "prop_method", "expm"), getattr(e, "nsub", None)) != ("tsit5", nsub):
+        raise ValueError("compute_pwc_gradient needs the states of propagate_pwc with the same dt")
+    A0s = Δt * np.asarray(A0, dtype=np.complex128)
+    As = [Δt * np.asarray(a, dtype=np.complex128) for a in A]
+    x0 = e.x0 if x0 is None else x0
+    if dUkdp_order == 0:  # :152
+        return cache.dJdu if cache.dJdu is not None else np.zeros_like(np.asarray(u, dtype=np.float64))
+    return grape_sensitivity(A0s, As, dJfinal_dx, u, x0, cache, dUkdp_order=dUkdp_order)

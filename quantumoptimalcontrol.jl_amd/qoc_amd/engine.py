@@ -147,7 +147,7 @@ class GrapeEngine:
         slice (the reference's dt = 0.1 Δt is nsub = 10)."""
         m = {"expm": L.QOC_PROP_EXPM, "tsit5": L.QOC_PROP_TSIT5}[method]
         self._chk(self._lib.qoc_set_propagation(self._h, m, int(nsub)))
-        self.prop_method = method
+        self.prop_method, self.nsub = method, int(nsub)
 
     def propagate_envelope(self, kind: str, params, tgate: float, dt: float):
         """Continuous pulse c(t) (wrap_envelope, src/QuantumOptimalControl.jl:43-54) integrated with

@@ -101,6 +101,30 @@ def test_pwc_tsit5_switch_back_to_expm(built_lib):
     e.close()
 
 
+def test_reference_shaped_propagate_pwc_and_gradient(built_lib):
+    """Q.propagate_pwc / Q.compute_pwc_gradient called like the reference (physical generators, Δt,
+    dt = 0.1Δt, dJfinal_dx closure) == oracle on the Δt-prescaled problem."""
+    import qoc_amd as Q
+    from qoc_amd import systems as S
+    Δt = 0.1
+    prob = S.zz_problem(20, tgate=2.0)
+    A0 = prob.A0 / Δt
+    A = [a / Δt for a in prob.A]
+    u = S.zz_controls(1, 20, 2.0, seed=7)[0]
+    cache = Q.setup_grape_cache(A0, prob.x0, u.shape)
+    x = Q.propagate_pwc(A0, A, prob.x0, u, Δt, cache)
+    _, dJf = Q.setup_infidelity(prob.x_target, prob.n)
+    g = Q.compute_pwc_gradient(dJf, u, Δt, A0, A, cache, dUkdp_order=2)
+    _, gr = O.grape_eval_ode(prob.A0, prob.A, u, prob.x0, prob.x_target, prob.n, order=2, nsub=10)
+    xs = O.propagate_pwc_ode(prob.A0, prob.A, u, prob.x0, nsub=10)
+    assert np.abs(x[-1] - xs[-1]).max() < 1e-12
+    assert np.linalg.norm(g - gr) / np.linalg.norm(gr) <= 1e-10
+    with pytest.raises(Q.StaleCacheError):
+        Q.compute_pwc_gradient(dJf, u + 0.01, Δt, A0, A, cache)
+    with pytest.raises(ValueError):
+        Q.propagate_pwc(A0, A, prob.x0, u, Δt, cache, dt=0.03)
+
+
 def test_tsit5_unsupported_configurations(built_lib, monkeypatch):
     from qoc_amd import GrapeEngine, QOCError, systems
     prob = systems.zz_problem(10)
