@@ -57,6 +57,7 @@ struct qoc_ctx {
   int expm_alg = 1;                      // 1 Taylor / Paterson-Stockmeyer (default), 0 Padé (QOC_EXPM_PADE=1)
   int prop_method = 0;                   // QOC_PROP_EXPM / QOC_PROP_TSIT5
   int nsub = 10;                         // Tsit5 steps per slice (reference dt = 0.1 Δt)
+  int ode_kernel = 0;                    // 0 register-resident rows when N fits, 1 LDS rows (QOC_ODE_LDS=1)
   double* d_stage = nullptr;             // host->device staging (fp64 complex), max(B*N*m, (nu+1)*N*N)*2
   size_t stage_elems = 0;
   std::vector<double> h_u;
@@ -890,15 +891,29 @@ int frechet_grad(qoc_ctx* c, double* d_dJdu) {
 }
 
 // ---- ODE path (fixed-step Tsit5, qoc_ode.hpp) ------------------------------------------------
+// k_ode_pwc instantiation by N: register-resident rows up to 48 (fp64) / 64 (fp32), LDS beyond
+template <typename T>
+void launch_ode_pwc(qoc_ctx* c, int adjoint, cx<T>* S, const unsigned char* pmask, double two_mu) {
+  const int N = c->N, W = std::min(c->m, 4);
+  const size_t lds = (((size_t)N * N * c->esz + 15) & ~(size_t)15) + (size_t)W * 64 * c->esz;
+  auto go = [&](auto kern) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(c->B), dim3(64 * W), lds, c->stream, N, c->m, c->nu, c->Nt, c->nsub, adjoint,
+                       (const cx<T>*)c->d_A, (const double*)c->d_u, (const cx<T>*)c->d_x0, c->x0_per_seed, S,
+                       (const cx<T>*)c->d_X, pmask, two_mu);
+  };
+  if (c->ode_kernel == 1) go(k_ode_pwc<T, 0>);
+  else if (N <= 16) go(k_ode_pwc<T, 16>);
+  else if (N <= 32) go(k_ode_pwc<T, 32>);
+  else if (N <= 48) go(k_ode_pwc<T, 48>);
+  else if (sizeof(T) == 4) go(k_ode_pwc<T, 64>);
+  else go(k_ode_pwc<T, 0>);
+}
+
 template <typename T>
 int ode_forward(qoc_ctx* c) {
-  const int W = std::min(c->m, 4);
-  const size_t lds = (size_t)c->N * c->N * c->esz;
-  HIPCHK(c, hipFuncSetAttribute((const void*)k_ode_pwc<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int mk = mark_begin(c, 1);
-  hipLaunchKernelGGL((k_ode_pwc<T>), dim3(c->B), dim3(64 * W), lds, c->stream, c->N, c->m, c->nu, c->Nt, c->nsub, 0,
-                     (const cx<T>*)c->d_A, (const double*)c->d_u, (const cx<T>*)c->d_x0, c->x0_per_seed,
-                     (cx<T>*)c->d_X, (const cx<T>*)c->d_X, (const unsigned char*)nullptr, 0.0);
+  launch_ode_pwc<T>(c, 0, (cx<T>*)c->d_X, nullptr, 0.0);
   HIPCHK(c, hipGetLastError());
   const bool pen = c->mu != 0.0;
   if (pen) {
@@ -934,10 +949,7 @@ int ode_adjoint(qoc_ctx* c) {
                        (const cx<T>*)c->d_X, c->d_pmask, 2.0 * c->mu, (cx<T>*)c->d_L);
     HIPCHK(c, hipGetLastError());
   }
-  const int W = std::min(m, 4);
-  hipLaunchKernelGGL((k_ode_pwc<T>), dim3(B), dim3(64 * W), (size_t)N * N * c->esz, c->stream, N, m, c->nu, Nt,
-                     c->nsub, 1, (const cx<T>*)c->d_A, (const double*)c->d_u, (const cx<T>*)c->d_x0, c->x0_per_seed,
-                     (cx<T>*)c->d_L, (const cx<T>*)c->d_X, pen ? c->d_pmask : nullptr, 2.0 * c->mu);
+  launch_ode_pwc<T>(c, 1, (cx<T>*)c->d_L, pen ? c->d_pmask : nullptr, 2.0 * c->mu);
   HIPCHK(c, hipGetLastError());
   mark_end(c, mk);
   return QOC_OK;
@@ -1049,6 +1061,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   hipMemset(c->d_pmask, 0, Nm);
   hipMemset(c->d_hist, 0, 12 * 64 * sizeof(unsigned long long));
   c->expm_alg = (getenv("QOC_EXPM_PADE") && atoi(getenv("QOC_EXPM_PADE")) != 0) ? 0 : 1;
+  c->ode_kernel = (getenv("QOC_ODE_LDS") && atoi(getenv("QOC_ODE_LDS")) != 0) ? 1 : 0;
   hipMemset(c->d_L, 0, (size_t)B * (Nt + 1) * Nm * c->esz);
   *out = c;
   return QOC_OK;

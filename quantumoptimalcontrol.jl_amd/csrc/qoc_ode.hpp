@@ -26,18 +26,61 @@ __constant__ double kTsitA[7][6] = {
     {5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401, -0.028269050394068383, 0},
     {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081, 2.324710524099774}};
 
-// y_lane = sum_j M[lane + N j] x_j  (M column-major N x N in LDS, x distributed one element per lane)
+// y_lane = sum_j M[lane + N j] x_j  (M column-major N x N in LDS, x distributed one element per lane).
+// Eight LDS loads are issued ahead of their FMAs and two accumulators break the FMA dependency chain.
 template <typename T>
 __device__ __forceinline__ cx<T> ode_matvec(int N, const cx<T>* __restrict__ M, cx<T> x, int lane) {
-  cx<T> y = {0, 0};
+  cx<T> y0 = {0, 0}, y1 = {0, 0};
   const int row = lane < N ? lane : 0;
-  for (int j = 0; j < N; ++j) {
+  int j = 0;
+  for (; j + 8 <= N; j += 8) {
+    cx<T> a[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) a[t] = M[row + N * (j + t)];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const T xr = bcast(x.r, j + t), xi = bcast(x.i, j + t);
+      cx<T>& y = (t & 1) ? y1 : y0;
+      y.r += a[t].r * xr - a[t].i * xi;
+      y.i += a[t].r * xi + a[t].i * xr;
+    }
+  }
+  for (; j < N; ++j) {
     const T xr = bcast(x.r, j), xi = bcast(x.i, j);
     const cx<T> a = M[row + N * j];
-    y.r += a.r * xr - a.i * xi;
-    y.i += a.r * xi + a.i * xr;
+    y0.r += a.r * xr - a.i * xi;
+    y0.i += a.r * xi + a.i * xr;
   }
-  return y;
+  return cx<T>{y0.r + y1.r, y0.i + y1.i};
+}
+
+// Same product with the lane's row of M held in registers (arow[j] = M[lane, j], zero-padded to NB
+// and zero rows for lanes >= N, so those lanes stay at x = 0).  x goes through a wave-private LDS
+// slot and comes back as broadcast ds_reads (no SGPR traffic), eight at a time; the uniform guard
+// skips whole blocks of eight beyond N.
+template <typename T, int NB>
+__device__ __forceinline__ cx<T> ode_matvec_reg(int N, const cx<T> (&arow)[NB], cx<T> x, cx<T>* __restrict__ xs,
+                                                int lane) {
+  xs[lane] = x;  // LDS operations of one wave complete in order: the reads below see this write
+  cx<T> y0 = {0, 0}, y1 = {0, 0};
+#pragma unroll
+  for (int jb = 0; jb < NB; jb += 8) {
+    if (jb < N) {
+      cx<T> xv[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) xv[t] = xs[jb + t];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const cx<T> a = arow[jb + t];
+        cx<T>& y = (t & 1) ? y1 : y0;
+        y.r = fma(a.r, xv[t].r, y.r);
+        y.r = fma(-a.i, xv[t].i, y.r);
+        y.i = fma(a.r, xv[t].i, y.i);
+        y.i = fma(a.i, xv[t].r, y.i);
+      }
+    }
+  }
+  return cx<T>{y0.r + y1.r, y0.i + y1.i};
 }
 
 // One Tsit5 step of size h for dx/dt = F(x, stage time), F given as a functor (mat-vec(s)).
@@ -71,8 +114,9 @@ __device__ __forceinline__ void tsit5_step(cx<T>& x, cx<T>& k1, T h, double t, R
 // Slice-by-slice PWC propagation.  Forward (adjoint = 0): S[b][0] = x0, S[b][k+1] from S[b][k].
 // Adjoint: S = Lam holds λ_Nt already (cost gradient + penalty); λ_k from λ_{k+1} under A_k^H, then
 // += 2 mu mask .* x_k (the exp path's dL/dx convention).  Block = 64 * W threads, wave w owns
-// columns w, w + W, ...
-template <typename T>
+// columns w, w + W, ...  NB > 0: each lane keeps its row of A_k (N <= NB) in registers for the
+// slice's nsub * 6 stage products; NB = 0: the rows are read from LDS.
+template <typename T, int NB>
 __global__ __launch_bounds__(256) void k_ode_pwc(int N, int m, int nu, int Nt, int nsub, int adjoint,
                                                  const cx<T>* __restrict__ Agen, const double* __restrict__ u,
                                                  const cx<T>* __restrict__ x0, int x0_per_seed, cx<T>* __restrict__ S,
@@ -107,20 +151,46 @@ __global__ __launch_bounds__(256) void k_ode_pwc(int N, int m, int nu, int Nt, i
       Ak[e] = a;
     }
     __syncthreads();
-    for (int col = wave; col < m; col += W) {
-      const size_t in = (size_t)(adjoint ? k + 1 : k) * Nm + (size_t)N * col;
-      const size_t outo = (size_t)(adjoint ? k : k + 1) * Nm + (size_t)N * col;
-      cx<T> x = lane < N ? Sb[in + lane] : cx<T>{0, 0};
-      auto rhs = [&](cx<T> y, double) __attribute__((always_inline)) { return ode_matvec<T>(N, Ak, y, lane); };
-      cx<T> k1 = rhs(x, 0.0);
-      for (int s = 0; s < nsub; ++s) tsit5_step<T>(x, k1, h, 0.0, rhs);
-      if (lane < N) {
-        if (adjoint && pmask && pmask[(size_t)N * col + lane]) {
-          const cx<T> xv = Xb[outo + lane];
-          x.r += (T)two_mu * xv.r;
-          x.i += (T)two_mu * xv.i;
+    if constexpr (NB > 0) {
+      static_assert(NB % 8 == 0, "row blocks of eight");
+      cx<T>* xs = reinterpret_cast<cx<T>*>(smem + ((NN * sizeof(cx<T>) + 15) & ~(size_t)15)) + 64 * wave;
+      cx<T> arow[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) arow[j] = (lane < N && j < N) ? Ak[lane + N * j] : cx<T>{0, 0};
+      for (int col = wave; col < m; col += W) {
+        const size_t in = (size_t)(adjoint ? k + 1 : k) * Nm + (size_t)N * col;
+        const size_t outo = (size_t)(adjoint ? k : k + 1) * Nm + (size_t)N * col;
+        cx<T> x = lane < N ? Sb[in + lane] : cx<T>{0, 0};
+        auto rhs = [&](cx<T> y, double) __attribute__((always_inline)) {
+          return ode_matvec_reg<T, NB>(N, arow, y, xs, lane);
+        };
+        cx<T> k1 = rhs(x, 0.0);
+        for (int s = 0; s < nsub; ++s) tsit5_step<T>(x, k1, h, 0.0, rhs);
+        if (lane < N) {
+          if (adjoint && pmask && pmask[(size_t)N * col + lane]) {
+            const cx<T> xv = Xb[outo + lane];
+            x.r += (T)two_mu * xv.r;
+            x.i += (T)two_mu * xv.i;
+          }
+          Sb[outo + lane] = x;
         }
-        Sb[outo + lane] = x;
+      }
+    } else {
+      for (int col = wave; col < m; col += W) {
+        const size_t in = (size_t)(adjoint ? k + 1 : k) * Nm + (size_t)N * col;
+        const size_t outo = (size_t)(adjoint ? k : k + 1) * Nm + (size_t)N * col;
+        cx<T> x = lane < N ? Sb[in + lane] : cx<T>{0, 0};
+        auto rhs = [&](cx<T> y, double) __attribute__((always_inline)) { return ode_matvec<T>(N, Ak, y, lane); };
+        cx<T> k1 = rhs(x, 0.0);
+        for (int s = 0; s < nsub; ++s) tsit5_step<T>(x, k1, h, 0.0, rhs);
+        if (lane < N) {
+          if (adjoint && pmask && pmask[(size_t)N * col + lane]) {
+            const cx<T> xv = Xb[outo + lane];
+            x.r += (T)two_mu * xv.r;
+            x.i += (T)two_mu * xv.i;
+          }
+          Sb[outo + lane] = x;
+        }
       }
     }
   }
