@@ -19,6 +19,7 @@
 #include "qoc_bgemm.hpp"
 #include "qoc_chain.hpp"
 #include "qoc_expm.hpp"
+#include "qoc_expm_rr.hpp"
 #include "qoc_frechet.hpp"
 #include "qoc_ode.hpp"
 #include "qoc_spline.hpp"
@@ -138,6 +139,35 @@ bool expm_supported(int N, int prec) {
   return lds <= 160 * 1024;
 }
 
+template <typename T, int NT, int KS>
+hipError_t launch_expm_rr_k(hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
+                            const void* Ain, void* Uout, unsigned long long* hist, unsigned long long* thist) {
+  const size_t lds = ExpmRR<T, NT>::lds_bytes(N);
+  hipError_t e =
+      hipFuncSetAttribute((const void*)k_expm_rr<T, NT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_expm_rr<T, NT, KS>), dim3(nunits), dim3(64 * NT), lds, s, N, nu, nunits, (const cx<T>*)Agen, u,
+                     (const cx<T>*)Ain, (cx<T>*)Uout, hist, thist);
+  return hipGetLastError();
+}
+
+// k-steps: f64 ceil(N/4) (compile-time, one of the 4 values for this NT), f32 all 4 NT.
+template <typename T, int NT>
+hipError_t launch_expm_rr_t(hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
+                            const void* Ain, void* Uout, unsigned long long* hist, unsigned long long* thist) {
+  const int ks = sizeof(T) == 8 ? (N + 3) / 4 : 4 * NT;
+#define QOC_RRK(K) \
+  if (ks == (K)) return launch_expm_rr_k<T, NT, (K)>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, thist)
+  if constexpr (sizeof(T) == 8) {
+    QOC_RRK(4 * NT - 3);
+    QOC_RRK(4 * NT - 2);
+    QOC_RRK(4 * NT - 1);
+  }
+  QOC_RRK(4 * NT);
+#undef QOC_RRK
+  return hipErrorInvalidValue;
+}
+
 template <typename T, int NT, int ALG>
 hipError_t launch_expm_t(hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
                          const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq,
@@ -156,8 +186,11 @@ hipError_t launch_expm(int prec, hipStream_t s, int N, int nu, int nunits, const
                        const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq, int alg = 0,
                        unsigned long long* thist = nullptr) {
   const int NT = (N + 15) / 16;
+  // Taylor: the register-resident kernel (qoc_expm_rr.hpp) unless QOC_EXPM_LDS=1 asks for the LDS one.
+  static const bool rr = !(getenv("QOC_EXPM_LDS") && atoi(getenv("QOC_EXPM_LDS")) != 0);
 #define QOC_LX(TT, NTT)                                                                                   \
-  return alg ? launch_expm_t<TT, NTT, 1>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq, thist)     \
+  return alg ? (rr ? launch_expm_rr_t<TT, NTT>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, thist)          \
+                   : launch_expm_t<TT, NTT, 1>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq, thist)) \
              : launch_expm_t<TT, NTT, 0>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq, thist)
   if (prec == QOC_FP64) {
     if (NT == 1) QOC_LX(double, 1);

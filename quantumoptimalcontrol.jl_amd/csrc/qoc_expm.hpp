@@ -32,7 +32,16 @@ __device__ unsigned long long g_probe[64];
     __builtin_amdgcn_sched_barrier(0);                                          \
     if (blockIdx.x == 7 && threadIdx.x == 0) g_probe[i] = t_;                   \
   } while (0)
+#define QOC_RTSTAMP(i)                                                          \
+  do {                                                                          \
+    unsigned long long t_;                                                      \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    if (blockIdx.x == 7 && threadIdx.x == 0) g_probe[i] = t_;                   \
+  } while (0)
 #else
+#define QOC_RTSTAMP(i) \
+  do {                 \
+  } while (0)
 #define QOC_STAMP(i) \
   do {               \
   } while (0)

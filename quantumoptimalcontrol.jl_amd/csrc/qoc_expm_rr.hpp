@@ -1,0 +1,322 @@
+// qoc_expm_rr.hpp — register-resident Taylor exponential (the default GRAPE exponential).
+//
+// Replaces ExponentialUtilities.exponential!(Ak, ExpMethodHigham2005(), cache) at
+// src/gradient_computations.jl:24 (A_k formation :18-22) with the degree m = 3r+2 Taylor polynomial
+// evaluated by Paterson-Stockmeyer (see qoc_expm.hpp: taylor_select, kTaylorTheta), re-organised so
+// that the running matrix never leaves the registers:
+//
+//   * one workgroup of NT waves per (seed, slice) unit; wave w OWNS rows [16w, 16w+16) of every
+//     matrix.  Its registers hold X^T tiles (t, w) in the MFMA D layout, i.e. lane l holds
+//     X[16w + (l&15)][16t + drow(l, e)] for t < NT, e < 4;
+//   * the product of an owned matrix X with a shared matrix B (row-major in LDS) is computed as
+//     (X B)^T = B^T X^T: the MFMA A operand is B^T, read from LDS, and the B operand is X^T, whose
+//     fragment for k-step (t, e) is exactly register (t, e) of the D layout — no data movement;
+//   * polynomials in A commute, so the Horner step V <- A3 V + B_i is computed as V A3 + B_i with
+//     A3 shared in LDS and V in registers: the r Horner GEMMs need no barrier and no LDS store;
+//   * B_i = c_{3i} I + c_{3i+1} A + c_{3i+2} A2 is folded into the accumulator initialisation;
+//   * LDS holds A, A2 (for the B_i) and the current right operand (A3, then the squaring operand),
+//     row-major with ld = N; operand reads are unmasked (columns >= N read the next row or the
+//     slack, which only reaches result columns >= N, and those are zeroed after every product), so
+//     the loads of k-step s+1 stay in flight under the MFMAs of k-step s;
+//   * squarings store the owned rows (ping-pong between two LDS buffers, one barrier each);
+//   * U_k goes straight from registers to HBM (column-major, 16 consecutive rows per lane group).
+//
+// The Padé + solve kernel (k_expm ALG 0, the reference algorithm) stays in qoc_expm.hpp.
+#pragma once
+#include "qoc_expm.hpp"
+
+namespace qoc {
+
+// Sum over the 16 lanes of a DPP row (xor 1, xor 2, half mirror, mirror); result in every lane.
+__device__ __forceinline__ float dpp_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xf, 0xf, false));  // row_mirror
+  return v;
+}
+
+template <typename T, int NT>
+struct ExpmRR {
+  static constexpr int NMAX = 16 * NT;
+  using M = MF<T>;
+  using v4 = typename M::v4;
+
+  struct Own {  // X[16w + (l&15)][16t + drow(l, e)], re / im; zero outside N x N
+    v4 r[NT], i[NT];
+  };
+
+  // Rows of an LDS operand that the k-steps touch (rows N..R-1 are kept zero): f64 executes
+  // ceil(N/4) k-steps (k < 4 ceil(N/4)), f32 all 4 NT (its k order interleaves the lane groups).
+  static __host__ __device__ int rows(int N) { return sizeof(T) == 8 ? 4 * ((N + 3) / 4) : NMAX; }
+  static __host__ __device__ int plane(int N) { return rows(N) * N; }
+  // 3 matrices (A, A2, operand) x re/im planes, read slack for the last row, column partial sums.
+  static __host__ __device__ size_t lds_bytes(int N) {
+    return ((size_t)6 * plane(N) + NMAX) * sizeof(T) + (size_t)NT * NMAX * sizeof(double) + 16;
+  }
+
+  // k index of k-step s = 4 tk + e for this lane (f64: 16tk + 4e + (l>>4); f32: 16tk + 4(l>>4) + e).
+  static __device__ __forceinline__ int kidx(int s, int lane) { return 16 * (s >> 2) + M::drow(lane, s & 3); }
+
+  // Zero the entries of result columns >= N (they may hold products of the unmasked reads).
+  static __device__ __forceinline__ void mask_cols(int N, Own& X, int lane) {
+    // tiles t < NT-1 lie inside N (NT = ceil(N / 16))
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool ok = 16 * (NT - 1) + M::drow(lane, e) < N;
+      X.r[NT - 1][e] = ok ? X.r[NT - 1][e] : T(0);
+      X.i[NT - 1][e] = ok ? X.i[NT - 1][e] : T(0);
+    }
+  }
+
+  // out = X B + init, with X owned (registers, zero outside N) and B shared (row-major LDS, ld = N).
+  // KS k-steps (compile time, branch-free); one k-step of look-ahead on the operand loads.
+  template <int KS>
+  static __device__ __forceinline__ void rmul(int N, const Own& X, const T* __restrict__ Br,
+                                              const T* __restrict__ Bi, Own& out, const Own& init, int lane) {
+    v4 rr[NT], ii[NT], S[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      rr[t] = init.r[t];
+      ii[t] = v4{0, 0, 0, 0};
+      S[t] = init.r[t] + init.i[t];
+    }
+    const int base = lane & 15;
+    T pr[KS][NT], pi[KS][NT];
+    auto load = [&](int s) __attribute__((always_inline)) {
+      const int a = kidx(s, lane) * N + base;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        pr[s][t] = Br[a + 16 * t];
+        pi[s][t] = Bi[a + 16 * t];
+      }
+    };
+    load(0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      __builtin_amdgcn_sched_barrier(0);  // keep the look-ahead at one k-step (register pressure)
+      if (s + 1 < KS) load(s + 1);
+      const T qr = X.r[s >> 2][s & 3], qi = X.i[s >> 2][s & 3], qs = qr + qi;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        rr[t] = M::mma(pr[s][t], qr, rr[t]);
+        ii[t] = M::mma(pi[s][t], qi, ii[t]);
+        S[t] = M::mma(pr[s][t] + pi[s][t], qs, S[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      out.r[t] = rr[t] - ii[t];
+      out.i[t] = S[t] - rr[t] - ii[t];
+    }
+    mask_cols(N, out, lane);
+  }
+
+  static __device__ __forceinline__ void zero(Own& X) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      X.r[t] = v4{0, 0, 0, 0};
+      X.i[t] = v4{0, 0, 0, 0};
+    }
+  }
+  static __device__ __forceinline__ void scale(Own& X, T a) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      X.r[t] *= a;
+      X.i[t] *= a;
+    }
+  }
+
+  // Owned rows -> row-major LDS (ld = N).  Rows N..rows(N)-1 are written too (zeros), which keeps
+  // every row a k-step reads finite.
+  static __device__ __forceinline__ void store_own(int N, const Own& X, T* Br, T* Bi, int row, int lane) {
+    if (row >= rows(N)) return;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = 16 * t + M::drow(lane, e);
+        if (t < NT - 1 || col < N) {  // tiles t < NT-1 lie inside N
+          Br[row * N + col] = X.r[t][e];
+          Bi[row * N + col] = X.i[t][e];
+        }
+      }
+  }
+};
+
+// ALG 1 (Taylor) kernel.  unit = blockIdx.x.  Either generators (Agen, u) or explicit matrices (Ain).
+// hist receives the Padé (d, s) the reference would select (reference-equivalent accounting), thist the
+// executed Taylor (r, s).  KS: k-steps per product (see ExpmRR::rows).
+template <typename T, int NT, int KS>
+__global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunits, const cx<T>* __restrict__ Agen,
+                                                        const double* __restrict__ u, const cx<T>* __restrict__ Ain,
+                                                        cx<T>* __restrict__ Uout, unsigned long long* __restrict__ hist,
+                                                        unsigned long long* __restrict__ thist) {
+  using E = ExpmRR<T, NT>;
+  using Own = typename E::Own;
+  using M = typename E::M;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int unit = blockIdx.x;
+  if (unit >= nunits) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int NN = N * N, PL = E::plane(N);
+  const int row = 16 * wave + (lane & 15);
+  const bool rok = row < N;
+  T* Ar = reinterpret_cast<T*>(smem);  // A_k (unscaled)
+  T* Ai = Ar + PL;
+  T* Br = Ai + PL;  // A2 (scaled)
+  T* Bi = Br + PL;
+  T* Xr = Bi + PL;  // A3 (scaled), then the squaring operand (ping-pong with A)
+  T* Xi = Xr + PL;
+  float* colf = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(Xi + PL + E::NMAX));
+
+  QOC_STAMP(0);
+  QOC_RTSTAMP(60);
+  // ---- own rows of A_k (src/gradient_computations.jl:18-22), straight from HBM/L2 ----
+  Own V;
+  {
+    // all loads of one generator in flight together (generator-major order)
+    const size_t r0 = (size_t)min(row, N - 1);
+    const cx<T>* src = Agen ? Agen : Ain + (size_t)unit * NN;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const cx<T> a = src[r0 + (size_t)N * min(16 * t + M::drow(lane, e), N - 1)];
+        V.r[t][e] = a.r;
+        V.i[t][e] = a.i;
+      }
+    if (Agen) {
+      const double* uu = u + (size_t)unit * nu;
+      for (int j = 0; j < nu; ++j) {
+        const T uj = (T)uu[j];
+        const cx<T>* G = Agen + (size_t)(j + 1) * NN;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const cx<T> g = G[r0 + (size_t)N * min(16 * t + M::drow(lane, e), N - 1)];
+            V.r[t][e] += uj * g.r;
+            V.i[t][e] += uj * g.i;
+          }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = rok && 16 * t + M::drow(lane, e) < N;
+        V.r[t][e] = ok ? V.r[t][e] : T(0);
+        V.i[t][e] = ok ? V.i[t][e] : T(0);
+      }
+  }
+  QOC_STAMP(1);
+  E::store_own(N, V, Ar, Ai, row, lane);
+
+  // ---- ||A_k||_1 (selects (r, s) only): an fp32 upper bound, column sums over this wave's 16 rows
+  // by DPP, then over waves through LDS; every wave reduces redundantly (one barrier) ----
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xr = (float)V.r[t][e], xi = (float)V.i[t][e];
+      const float cs = dpp_sum16(sqrtf(xr * xr + xi * xi));
+      if ((lane & 15) == 0) colf[wave * E::NMAX + 16 * t + M::drow(lane, e)] = cs;
+    }
+  __syncthreads();
+  double nA;
+  {
+    float c = 0.f;
+    if (lane < N) {
+#pragma unroll
+      for (int w = 0; w < NT; ++w) c += colf[w * E::NMAX + lane];
+    }
+    // the fp32 sqrt / sums are within 2^-17 relative for N <= 64: the scaled value bounds ||A||_1
+    nA = (double)__uint_as_float(wave_max_u32(__float_as_uint(c))) * (1.0 + 1.0 / 65536.0);
+  }
+
+  QOC_STAMP(2);
+  int tr, ts;
+  taylor_select(nA, tr, ts);
+  if (tid == 0) {
+    int d, sq = 0;
+    if (nA <= 2.1) {
+      d = nA > 0.95 ? 9 : nA > 0.25 ? 7 : nA > 0.015 ? 5 : 3;
+    } else {
+      d = 13;
+      const double s = log2(nA / 5.4);
+      sq = s > 0 ? (int)ceil(s) : 0;
+    }
+    if (hist) atomicAdd(&hist[degree_index(d) * 64 + (sq < 63 ? sq : 63)], 1ULL);
+    if (thist) atomicAdd(&thist[(tr - 2) * 64 + (ts < 63 ? ts : 63)], 1ULL);
+  }
+  const T sc = (T)ldexp(1.0, -ts);  // exact power-of-two scaling
+
+  // As = 2^-s A (owned); A2 = As As = 2^-s (As A); A3 = A2 As = 2^-s (A2 A)
+  Own Z, W;
+  E::zero(Z);
+  E::scale(V, sc);
+  E::template rmul<KS>(N, V, Ar, Ai, W, Z, lane);
+  E::scale(W, sc);
+  E::store_own(N, W, Br, Bi, row, lane);
+  E::template rmul<KS>(N, W, Ar, Ai, V, Z, lane);
+  E::scale(V, sc);
+  E::store_own(N, V, Xr, Xi, row, lane);
+  __syncthreads();
+
+  // B_i at the owned positions: c0 I + c1 As + c2 A2 (As exactly rescaled from bufA)
+  const int ra = min(row, N - 1) * N;
+  auto make_B = [&](int i, Own& B) __attribute__((always_inline)) {
+    const T c0 = (T)kInvFact[3 * i], c1 = (T)kInvFact[3 * i + 1] * sc, c2 = (T)kInvFact[3 * i + 2];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // columns >= N read the next row: that reaches only result columns >= N (masked by rmul)
+        const int col = 16 * t + M::drow(lane, e);
+        const int a = ra + col;
+        const T br = c1 * Ar[a] + c2 * Br[a] + (row == col ? c0 : T(0));
+        const T bi = c1 * Ai[a] + c2 * Bi[a];
+        B.r[t][e] = rok ? br : T(0);
+        B.i[t][e] = rok ? bi : T(0);
+      }
+  };
+  QOC_STAMP(3);
+  make_B(tr, V);  // Horner start
+  for (int i = tr - 1; i >= 0; --i) {
+    if (i == 1) QOC_STAMP(7);
+    make_B(i, W);
+    if (i == 1) QOC_STAMP(8);
+    E::template rmul<KS>(N, V, Xr, Xi, V, W, lane);
+    if (i == 1) QOC_STAMP(9);  // V <- V A3 + B_i  (= A3 V + B_i: polynomials in A commute)
+  }
+
+  // ---- squarings: ping-pong bufA / bufX, one barrier each (plus one: Horner still reads both) ----
+  QOC_STAMP(4);
+  if (ts > 0) __syncthreads();
+  for (int q = 0; q < ts; ++q) {
+    T* Sr = (q & 1) ? Xr : Ar;
+    T* Si = (q & 1) ? Xi : Ai;
+    E::store_own(N, V, Sr, Si, row, lane);
+    __syncthreads();
+    E::template rmul<KS>(N, V, Sr, Si, V, Z, lane);
+  }
+
+  QOC_STAMP(5);
+  // ---- U_k -> HBM, column-major (Julia layout) ----
+  if (rok) {
+    cx<T>* out = Uout + (size_t)unit * NN;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = 16 * t + M::drow(lane, e);
+        if (col < N) out[row + (size_t)N * col] = cx<T>{V.r[t][e], V.i[t][e]};
+      }
+  }
+  QOC_STAMP(6);
+  QOC_RTSTAMP(61);
+}
+
+}  // namespace qoc

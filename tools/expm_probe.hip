@@ -5,7 +5,7 @@
 #include <cstdlib>
 #include <vector>
 #include <cmath>
-#include "../quantumoptimalcontrol.jl_amd/csrc/qoc_expm.hpp"
+#include "../quantumoptimalcontrol.jl_amd/csrc/qoc_expm_rr.hpp"
 using namespace qoc;
 
 template <int NT, int ALG = 0>
@@ -93,27 +93,94 @@ done:
   (void)hipFree(dX);
 }
 
+template <int NT>
+void run_rr(int N, double scale, int units, std::vector<cx<double>>* keep) {
+  using E = ExpmRR<double, NT>;
+  std::vector<cx<double>> A((size_t)units * N * N);
+  srand(1);
+  for (int u = 0; u < units; ++u) {
+    std::vector<cx<double>> H((size_t)N * N);
+    for (int j = 0; j < N; ++j)
+      for (int i = 0; i <= j; ++i) {
+        double re = rand() / (double)RAND_MAX - 0.5, im = (i == j) ? 0 : rand() / (double)RAND_MAX - 0.5;
+        H[i + N * j] = {re, im};
+        H[j + N * i] = {re, -im};
+      }
+    double nrm = 0;
+    for (int j = 0; j < N; ++j) {
+      double s = 0;
+      for (int i = 0; i < N; ++i) s += std::hypot(H[i + N * j].r, H[i + N * j].i);
+      nrm = std::max(nrm, s);
+    }
+    for (int e = 0; e < N * N; ++e) A[(size_t)u * N * N + e] = {H[e].i * scale / nrm, -H[e].r * scale / nrm};
+  }
+  cx<double>*dA, *dX;
+  (void)hipMalloc(&dA, A.size() * 16);
+  (void)hipMalloc(&dX, A.size() * 16);
+  (void)hipMemcpy(dA, A.data(), A.size() * 16, hipMemcpyHostToDevice);
+  size_t lds = E::lds_bytes(N);
+  (void)hipFuncSetAttribute((const void*)k_expm_rr<double, NT, (NT == 3 ? 10 : NT == 2 ? 7 : 3)>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  for (int it = 0; it < 3; ++it) {
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL((k_expm_rr<double, NT, (NT == 3 ? 10 : NT == 2 ? 7 : 3)>), dim3(units), dim3(64 * NT), lds, 0, N, 0, units, nullptr, nullptr, dA,
+                       dX, nullptr, nullptr);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+  }
+  float ms;
+  (void)hipEventElapsedTime(&ms, a, b);
+  printf("RR N=%d scale=%.3g units=%d lds=%zu  wall %.3f ms  (%.3f us/unit/CU)\n", N, scale, units, lds, ms, ms * 1e3 / units * 256);
+  std::vector<cx<double>> X(A.size());
+  (void)hipMemcpy(X.data(), dX, X.size() * 16, hipMemcpyDeviceToHost);
+  double md = 0;
+  for (size_t i = 0; i < X.size(); ++i)
+    md = std::max(md, std::abs(X[i].r - (*keep)[i].r) + std::abs(X[i].i - (*keep)[i].i));
+  printf("   max |RR - Pade| = %.3g\n", md);
+  {
+    unsigned long long st[64];
+    (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_probe), sizeof(st));
+    printf("   load A %llu  norm %llu  A2+A3 %llu  Horner %llu  squarings %llu  store %llu\n", st[1] - st[0], st[2] - st[1],
+           st[3] - st[2], st[4] - st[3], st[5] - st[4], st[6] - st[5]);
+    printf("   one Horner step: make_B %llu  rmul %llu\n", st[8] - st[7], st[9] - st[8]);
+    printf("   block lifetime %llu memtime ticks, %llu realtime ticks -> %.3f GHz\n", st[6] - st[0], st[61] - st[60],
+           (double)(st[6] - st[0]) / (double)(st[61] - st[60]) / 10.0);
+  }
+  (void)hipFree(dA);
+  (void)hipFree(dX);
+}
+
 int main(int argc, char** argv) {
   {
     std::vector<cx<double>> k;
     run<1, 0>(9, 0.11, 256 * 64, &k);
     run<1, 1>(9, 0.11, 256 * 64, &k);
+    run_rr<1>(9, 0.11, 256 * 64, &k);
   }
   {
     std::vector<cx<double>> k;
     run<2, 0>(27, 30.0, 256 * 64, &k);
     run<2, 1>(27, 30.0, 256 * 64, &k);
+    run_rr<2>(27, 30.0, 256 * 64, &k);
   }
   {
     std::vector<cx<double>> k;
     run<3, 0>(40, 0.33, 256 * 64, &k);
     run<3, 1>(40, 0.33, 256 * 64, &k);
+    run_rr<3>(40, 0.33, 256 * 64, &k);
+    run_rr<3>(40, 0.33, 256, &k);
+    run_rr<3>(40, 0.33, 512, &k);
+    run_rr<3>(40, 0.33, 768, &k);
+    run_rr<3>(40, 0.33, 1024, &k);
   }
   run<3, 1>(40, 0.33, 256);  // one workgroup per CU: uncontended phase costs
   {
     std::vector<cx<double>> k;
     run<3, 0>(40, 4.0, 256 * 16, &k);
     run<3, 1>(40, 4.0, 256 * 16, &k);
+    run_rr<3>(40, 4.0, 256 * 16, &k);
   }
   return 0;
 }

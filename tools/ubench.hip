@@ -76,6 +76,71 @@ __global__ void k_div(double* out, int iters) {
   if (threadIdx.x == 0 && blockIdx.x == 0) g_t[5] = t1 - t0;
   out[threadIdx.x] = a;
 }
+
+__global__ void k_mfma_valu(double* out, int iters, int nf) {
+  d4 a0 = {0,0,0,0}, a1 = a0, a2 = a0, a3 = a0;
+  double x = threadIdx.x * 1e-3, y = 1.0 + threadIdx.x * 1e-4;
+  double b0 = threadIdx.x, b1 = b0 + 1, b2 = b0 + 2, b3 = b0 + 3, b4 = b0 + 4, b5 = b0 + 5, b6 = b0 + 6, b7 = b0 + 7;
+  const double m = 0.999999, c = 1e-7;
+  unsigned long long t0, t1;
+  STAMP(t0);
+  for (int i = 0; i < iters; ++i) {
+    a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, a0, 0, 0, 0);
+    b0 = fma(b0, m, c); b1 = fma(b1, m, c); b2 = fma(b2, m, c); b3 = fma(b3, m, c);
+    a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, a1, 0, 0, 0);
+    b4 = fma(b4, m, c); b5 = fma(b5, m, c); b6 = fma(b6, m, c); b7 = fma(b7, m, c);
+    a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, a2, 0, 0, 0);
+    b0 = fma(b0, m, c); b1 = fma(b1, m, c); b2 = fma(b2, m, c); b3 = fma(b3, m, c);
+    a3 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, a3, 0, 0, 0);
+    b4 = fma(b4, m, c); b5 = fma(b5, m, c); b6 = fma(b6, m, c); b7 = fma(b7, m, c);
+  }
+  STAMP(t1);
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_t[6] = t1 - t0;
+  out[threadIdx.x] = a0[0] + a1[1] + a2[2] + a3[3] + b0 + b1 + b2 + b3 + b4 + b5 + b6 + b7;
+}
+__global__ void k_mfma_multi(double* out, int iters, int slot) {
+  d4 a0 = {0,0,0,0}, a1 = a0, a2 = a0, a3 = a0;
+  double x = threadIdx.x * 1e-3, y = 1.0 + threadIdx.x * 1e-4;
+  unsigned long long t0, t1;
+  __syncthreads();
+  STAMP(t0);
+  for (int i = 0; i < iters; ++i) {
+    a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, a0, 0, 0, 0);
+    a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, a1, 0, 0, 0);
+    a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, a2, 0, 0, 0);
+    a3 = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, a3, 0, 0, 0);
+  }
+  __syncthreads();
+  STAMP(t1);
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_t[slot] = t1 - t0;
+  out[threadIdx.x] = a0[0] + a1[1] + a2[2] + a3[3];
+}
+__global__ void k_mfma44(double* out, int iters) {
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  double x = threadIdx.x * 1e-3, y = 1.0 + threadIdx.x * 1e-4;
+  unsigned long long t0, t1;
+  STAMP(t0);
+  for (int i = 0; i < iters; ++i) {
+    a0 = __builtin_amdgcn_mfma_f64_4x4x4f64(x, y, a0, 0, 0, 0);
+    a1 = __builtin_amdgcn_mfma_f64_4x4x4f64(x, y, a1, 0, 0, 0);
+    a2 = __builtin_amdgcn_mfma_f64_4x4x4f64(x, y, a2, 0, 0, 0);
+    a3 = __builtin_amdgcn_mfma_f64_4x4x4f64(x, y, a3, 0, 0, 0);
+  }
+  STAMP(t1);
+  if (threadIdx.x == 0 && blockIdx.x == 0) g_t[10] = t1 - t0;
+  out[threadIdx.x] = a0 + a1 + a2 + a3;
+}
+__global__ void k_rt(double* out) {
+  unsigned long long t0, t1, r0, r1;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r0)::"memory");
+  STAMP(t0);
+  double a = threadIdx.x;
+  for (int i = 0; i < 200000; ++i) a = fma(a, 0.9999, 1e-7);
+  STAMP(t1);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
+  if (threadIdx.x == 0) { g_t[11] = t1 - t0; g_t[12] = r1 - r0; }
+  out[threadIdx.x] = a;
+}
 int main() {
   double* d; (void)hipMalloc(&d, 1 << 20);
   const int it = 1000;
@@ -93,5 +158,17 @@ int main() {
   printf("ds_read_b64 dependent chain:     %.1f cycles/iter\n", t[3] / (1.0 * it));
   printf("__syncthreads (4 waves):         %.1f cycles\n", t[4] / (1.0 * it));
   printf("f64 reciprocal dependent chain:  %.1f cycles/iter\n", t[5] / (1.0 * it));
+  hipLaunchKernelGGL(k_mfma_valu, dim3(1), dim3(64), 0, 0, d, it, 0);
+  hipLaunchKernelGGL(k_mfma_multi, dim3(1), dim3(256), 0, 0, d, it, 7);
+  hipLaunchKernelGGL(k_mfma_multi, dim3(1), dim3(512), 0, 0, d, it, 8);
+  hipLaunchKernelGGL(k_mfma_multi, dim3(1), dim3(1024), 0, 0, d, it, 9);
+  hipLaunchKernelGGL(k_mfma44, dim3(1), dim3(64), 0, 0, d, it);
+  hipLaunchKernelGGL(k_rt, dim3(1), dim3(64), 0, 0, d);
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(g_t), sizeof(t));
+  printf("mfma x4 + 16 v_fma_f64 interleaved (1 wave): %.1f cycles/iter (mfma-only x4 = %.1f)\n", t[6] / (1.0 * it), t[0] / (1.0 * it));
+  printf("mfma x4, 4 waves: %.1f cycles/iter; 8 waves %.1f; 16 waves %.1f\n", t[7] / (1.0 * it), t[8] / (1.0 * it), t[9] / (1.0 * it));
+  printf("mfma_f64_4x4x4 independent x4: %.1f cycles/instr\n", t[10] / (4.0 * it));
+  printf("memtime vs realtime: %llu memtime ticks, %llu realtime (100MHz) ticks -> %.3f GHz\n", t[11], t[12], t[11] / (t[12] * 0.01) / 1e3);
   return 0;
 }
