@@ -32,6 +32,18 @@ __device__ unsigned long long g_probe[64];
     __builtin_amdgcn_sched_barrier(0);                                          \
     if (blockIdx.x == 7 && threadIdx.x == 0) g_probe[i] = t_;                   \
   } while (0)
+__device__ unsigned long long g_life[3 * 65536];
+#define QOC_LIFE(slot)                                                                           \
+  do {                                                                                           \
+    unsigned long long t_;                                                                       \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+    unsigned hw_;                                                                                \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                           \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) {                                                \
+      g_life[3 * blockIdx.x + slot] = t_;                                                        \
+      g_life[3 * blockIdx.x + 2] = hw_;                                                          \
+    }                                                                                            \
+  } while (0)
 #define QOC_RTSTAMP(i)                                                          \
   do {                                                                          \
     unsigned long long t_;                                                      \
@@ -40,6 +52,9 @@ __device__ unsigned long long g_probe[64];
   } while (0)
 #else
 #define QOC_RTSTAMP(i) \
+  do {                 \
+  } while (0)
+#define QOC_LIFE(slot) \
   do {                 \
   } while (0)
 #define QOC_STAMP(i) \

@@ -15,7 +15,7 @@
 //     A3 shared in LDS and V in registers: the r Horner GEMMs need no barrier and no LDS store;
 //   * B_i = c_{3i} I + c_{3i+1} A + c_{3i+2} A2 is folded into the accumulator initialisation;
 //   * LDS holds A, A2 (for the B_i) and the current right operand (A3, then the squaring operand),
-//     row-major with ld = N; operand reads are unmasked (columns >= N read the next row or the
+//     row-major with row pitch ldp(N) (odd for f64); operand reads are unmasked (columns >= N read the next row or the
 //     slack, which only reaches result columns >= N, and those are zeroed after every product), so
 //     the loads of k-step s+1 stay in flight under the MFMAs of k-step s;
 //   * squarings store the owned rows (ping-pong between two LDS buffers, one barrier each);
@@ -49,10 +49,14 @@ struct ExpmRR {
   // Rows of an LDS operand that the k-steps touch (rows N..R-1 are kept zero): f64 executes
   // ceil(N/4) k-steps (k < 4 ceil(N/4)), f32 all 4 NT (its k order interleaves the lane groups).
   static __host__ __device__ int rows(int N) { return sizeof(T) == 8 ? 4 * ((N + 3) / 4) : NMAX; }
-  static __host__ __device__ int plane(int N) { return rows(N) * N; }
-  // 3 matrices (A, A2, operand) x re/im planes, read slack for the last row, column partial sums.
+  // Row pitch.  f64: odd, so the 16 rows one store_own / make_B instruction touches fall on distinct
+  // banks.  f32: a multiple of 4 — the 4 consecutive columns a lane owns (drow = 4 (l>>4) + e) are
+  // merged into 16-byte LDS accesses, which must stay 16-byte aligned.
+  static __host__ __device__ int ldp(int N) { return sizeof(T) == 8 ? (N | 1) : ((N + 3) & ~3); }
+  static __host__ __device__ int plane(int N) { return rows(N) * ldp(N); }
+  // 3 matrices (A, A2, operand) x re/im planes, read slack past the last row, fp32 column partial sums.
   static __host__ __device__ size_t lds_bytes(int N) {
-    return ((size_t)6 * plane(N) + NMAX) * sizeof(T) + (size_t)NT * NMAX * sizeof(double) + 16;
+    return ((size_t)6 * plane(N) + 16) * sizeof(T) + (size_t)NT * NMAX * sizeof(float) + 16;
   }
 
   // k index of k-step s = 4 tk + e for this lane (f64: 16tk + 4e + (l>>4); f32: 16tk + 4(l>>4) + e).
@@ -69,7 +73,7 @@ struct ExpmRR {
     }
   }
 
-  // out = X B + init, with X owned (registers, zero outside N) and B shared (row-major LDS, ld = N).
+  // out = X B + init, with X owned (registers, zero outside N) and B shared (row-major LDS, pitch ldp(N)).
   // KS k-steps (compile time, branch-free); one k-step of look-ahead on the operand loads.
   template <int KS>
   static __device__ __forceinline__ void rmul(int N, const Own& X, const T* __restrict__ Br,
@@ -84,7 +88,7 @@ struct ExpmRR {
     const int base = lane & 15;
     T pr[KS][NT], pi[KS][NT];
     auto load = [&](int s) __attribute__((always_inline)) {
-      const int a = kidx(s, lane) * N + base;
+      const int a = kidx(s, lane) * ldp(N) + base;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         pr[s][t] = Br[a + 16 * t];
@@ -127,7 +131,7 @@ struct ExpmRR {
     }
   }
 
-  // Owned rows -> row-major LDS (ld = N).  Rows N..rows(N)-1 are written too (zeros), which keeps
+  // Owned rows -> row-major LDS (pitch ldp(N)).  Rows N..rows(N)-1 are written too (zeros), which keeps
   // every row a k-step reads finite.
   static __device__ __forceinline__ void store_own(int N, const Own& X, T* Br, T* Bi, int row, int lane) {
     if (row >= rows(N)) return;
@@ -137,8 +141,8 @@ struct ExpmRR {
       for (int e = 0; e < 4; ++e) {
         const int col = 16 * t + M::drow(lane, e);
         if (t < NT - 1 || col < N) {  // tiles t < NT-1 lie inside N
-          Br[row * N + col] = X.r[t][e];
-          Bi[row * N + col] = X.i[t][e];
+          Br[row * ldp(N) + col] = X.r[t][e];
+          Bi[row * ldp(N) + col] = X.i[t][e];
         }
       }
   }
@@ -169,10 +173,11 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
   T* Bi = Br + PL;
   T* Xr = Bi + PL;  // A3 (scaled), then the squaring operand (ping-pong with A)
   T* Xi = Xr + PL;
-  float* colf = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(Xi + PL + E::NMAX));
+  float* colf = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(Xi + PL + 16));
 
   QOC_STAMP(0);
   QOC_RTSTAMP(60);
+  QOC_LIFE(0);
   // ---- own rows of A_k (src/gradient_computations.jl:18-22), straight from HBM/L2 ----
   Own V;
   {
@@ -266,7 +271,7 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
   __syncthreads();
 
   // B_i at the owned positions: c0 I + c1 As + c2 A2 (As exactly rescaled from bufA)
-  const int ra = min(row, N - 1) * N;
+  const int ra = min(row, N - 1) * E::ldp(N);
   auto make_B = [&](int i, Own& B) __attribute__((always_inline)) {
     const T c0 = (T)kInvFact[3 * i], c1 = (T)kInvFact[3 * i + 1] * sc, c2 = (T)kInvFact[3 * i + 2];
 #pragma unroll
@@ -317,6 +322,7 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
   }
   QOC_STAMP(6);
   QOC_RTSTAMP(61);
+  QOC_LIFE(1);
 }
 
 }  // namespace qoc

@@ -145,6 +145,20 @@ void run_rr(int N, double scale, int units, std::vector<cx<double>>* keep) {
     printf("   load A %llu  norm %llu  A2+A3 %llu  Horner %llu  squarings %llu  store %llu\n", st[1] - st[0], st[2] - st[1],
            st[3] - st[2], st[4] - st[3], st[5] - st[4], st[6] - st[5]);
     printf("   one Horner step: make_B %llu  rmul %llu\n", st[8] - st[7], st[9] - st[8]);
+    if (units <= 65536) {
+      std::vector<unsigned long long> L(3 * (size_t)units);
+      (void)hipMemcpyFromSymbol(L.data(), HIP_SYMBOL(g_life), L.size() * 8);
+      unsigned long long t0 = ~0ull, t1 = 0;
+      double life = 0;
+      for (int u = 0; u < units; ++u) {
+        t0 = std::min(t0, L[3 * u]);
+        t1 = std::max(t1, L[3 * u + 1]);
+        life += (double)(L[3 * u + 1] - L[3 * u]);
+      }
+      // average number of resident WGs = sum of lifetimes / (span x CUs)
+      printf("   all WGs: span %.1f us, mean lifetime %.2f us, mean resident WGs per CU %.2f\n", (t1 - t0) / 100.0,
+             life / units / 100.0, life / ((double)(t1 - t0) * 256.0));
+    }
     printf("   block lifetime %llu memtime ticks, %llu realtime ticks -> %.3f GHz\n", st[6] - st[0], st[61] - st[60],
            (double)(st[6] - st[0]) / (double)(st[61] - st[60]) / 10.0);
   }

@@ -14,7 +14,7 @@ __global__ __launch_bounds__(64 * NT, 2) void k_rmul(int N, int iters, double* o
   double* Br = (double*)smem;
   double* Bi = Br + E::plane(N);
   for (int e = threadIdx.x; e < E::plane(N); e += blockDim.x) {
-    const int r = e / N, c = e % N;
+    const int r = e / E::ldp(N), c = e % E::ldp(N);
     Br[e] = (r < N && c < N) ? 0.01 * ((e * 7) % 13) / N : 0.0;
     Bi[e] = (r < N && c < N) ? 0.01 * ((e * 5) % 11) / N : 0.0;
   }
