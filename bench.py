@@ -43,10 +43,15 @@ def expm_flops(N, hist):
     return sum(cnt * (8.0 * N ** 3 * (GEMMS_PER_DEGREE[d] + s) + (40.0 / 3.0) * N ** 3) for (d, s), cnt in hist.items())
 
 
+def taylor_gemms(m):
+    """Complex GEMMs of one executed Taylor polynomial: m = 12 is the 4-product scheme (A2, A3, B4^2,
+    (B2 + A6) A6); m = 3r+2 is Paterson-Stockmeyer (A2, A3, r Horner products in A3)."""
+    return 4 if m == 12 else 2 + (m - 2) // 3
+
+
 def taylor_flops(N, thist):
-    """Algorithmic FLOPs of the executed Taylor / Paterson-Stockmeyer exponentials: degree m = 3r+2 costs
-    2 + r complex GEMMs (A2, A3, r Horner products in A3) plus s squarings, 8 N^3 flops each."""
-    return sum(cnt * 8.0 * N ** 3 * (2 + (m - 2) // 3 + s) for (m, s), cnt in thist.items())
+    """Algorithmic FLOPs of the executed Taylor exponentials: taylor_gemms(m) + s squarings, 8 N^3 each."""
+    return sum(cnt * 8.0 * N ** 3 * (taylor_gemms(m) + s) for (m, s), cnt in thist.items())
 
 
 def ref_eval_flops(N, m, nu, hist_per_eval, order=3):

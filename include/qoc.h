@@ -103,11 +103,14 @@ int qoc_get_propagator(qoc_ctx* ctx, int seed, int k, double* U_out);   /* Uk_ve
  * hist[di*64 + s], di = index of degree in {3,5,7,9,13}.  Used for the FLOP accounting. */
 int qoc_pade_histogram(qoc_ctx* ctx, long long* hist, int reset);
 
-/* Exponential algorithm actually executed by the LDS-resident path: by default a degree m = 3r+2
- * Taylor polynomial (Paterson-Stockmeyer, 2 + r GEMMs, no linear solve) with s squarings, chosen so
- * that the truncation tail is <= 2^-53 (same result as the reference's Padé to fp rounding; set
- * QOC_EXPM_PADE=1 at qoc_create for the Padé + solve algorithm).  hist[(r-2)*64 + s], r = 2..8
- * (7*64 entries).  qoc_pade_histogram keeps reporting the Padé (d, s) the reference would select. */
+/* Exponential algorithm actually executed (no linear solve; same result as the reference's Padé to
+ * fp rounding; QOC_EXPM_PADE=1 at qoc_create selects the Padé + solve algorithm).  8*64 entries:
+ *   hist[(r-2)*64 + s], r = 2..8: degree m = 3r+2 Taylor by Paterson-Stockmeyer (2 + r GEMMs) with s
+ *     squarings (large-N pipeline; LDS kernel with QOC_EXPM_LDS=1);
+ *   hist[7*64 + s]: degree-12 Taylor in 4 GEMMs (Bader-Blanes-Casas form) with s squarings (the
+ *     default register-resident kernel).
+ * The truncation tail is <= 2^-53 in every case.  qoc_pade_histogram keeps reporting the Padé (d, s)
+ * the reference would select. */
 int qoc_taylor_histogram(qoc_ctx* ctx, long long* hist, int reset);
 
 /* Live per-kernel timing: when enabled, hipEvents are recorded on qoc_stream around each hot-path

@@ -54,8 +54,8 @@ struct qoc_ctx {
   cx<double>* d_coef = nullptr;  // B*m
   double* d_dJdu = nullptr;  // B*nu*Nt
   int* d_flag = nullptr;
-  unsigned long long* d_hist = nullptr;  // 5*64 reference (Padé) selection + 7*64 executed Taylor (r, s)
-  int expm_alg = 1;                      // 1 Taylor / Paterson-Stockmeyer (default), 0 Padé (QOC_EXPM_PADE=1)
+  unsigned long long* d_hist = nullptr;  // 5*64 reference (Padé) selection + 8*64 executed Taylor (r, s) / T12 s
+  int expm_alg = 1;  // 1 Taylor: register-resident T12 (default), 2 LDS Paterson-Stockmeyer (QOC_EXPM_LDS=1), 0 Padé (QOC_EXPM_PADE=1)
   int prop_method = 0;                   // QOC_PROP_EXPM / QOC_PROP_TSIT5
   int nsub = 10;                         // Tsit5 steps per slice (reference dt = 0.1 Δt)
   int ode_kernel = 0;                    // 0 register-resident rows when N fits, 1 LDS rows (QOC_ODE_LDS=1)
@@ -86,7 +86,7 @@ struct qoc_ctx {
   void* d_ws = nullptr;         // chunk workspace
   double* d_red = nullptr;      // per-item reductions (chunk + 8 doubles)
   long long big_hist[5 * 64] = {};
-  long long big_thist[7 * 64] = {};  // executed Taylor (r, s) on the large-N path
+  long long big_thist[8 * 64] = {};  // executed Taylor (r, s) on the large-N path
   long long ns_iters = 0;       // Newton-Schulz iterations executed (all chunks)
   size_t dev_bytes = 0;
   // spline parameterisation (examples/ipopt_callbacks_exp.jl:13-14, 28)
@@ -181,13 +181,13 @@ hipError_t launch_expm_t(hipStream_t s, int N, int nu, int nunits, const void* A
   return hipGetLastError();
 }
 
-// alg 0: Padé + solve (reference algorithm), alg 1: Taylor / Paterson-Stockmeyer (no solve).
+// alg 0: Padé + solve (reference algorithm); alg 1: register-resident Taylor T12; alg 2: LDS Paterson-Stockmeyer.
 hipError_t launch_expm(int prec, hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
                        const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq, int alg = 0,
                        unsigned long long* thist = nullptr) {
   const int NT = (N + 15) / 16;
-  // Taylor: the register-resident kernel (qoc_expm_rr.hpp) unless QOC_EXPM_LDS=1 asks for the LDS one.
-  static const bool rr = !(getenv("QOC_EXPM_LDS") && atoi(getenv("QOC_EXPM_LDS")) != 0);
+  // alg 1: the register-resident T12 kernel (qoc_expm_rr.hpp); alg 2: the LDS Paterson-Stockmeyer one.
+  const bool rr = alg == 1;
 #define QOC_LX(TT, NTT)                                                                                   \
   return alg ? (rr ? launch_expm_rr_t<TT, NTT>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, thist)          \
                    : launch_expm_t<TT, NTT, 1>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq, thist)) \
@@ -507,7 +507,7 @@ int expm_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, doubl
   }
   const int di = d == 3 ? 0 : d == 5 ? 1 : d == 7 ? 2 : d == 9 ? 3 : 4;
   if (count_hist) c->big_hist[di * 64 + std::min(sq, 63)] += cnt;
-  if (c->expm_alg == 1) return taylor_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, nA, count_hist);
+  if (c->expm_alg != 0) return taylor_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, nA, count_hist);
   const double* C = d == 3 ? hPade3 : d == 5 ? hPade5 : d == 7 ? hPade7 : d == 9 ? hPade9 : hPade13;
   const double sc = std::ldexp(1.0, -sq);
   GemmArgs g;
@@ -1060,7 +1060,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
       {(void**)&c->d_coef, (size_t)B * m * sizeof(cx<double>)},
       {(void**)&c->d_dJdu, (size_t)B * nu * Nt * sizeof(double)},
       {(void**)&c->d_flag, sizeof(int)},
-      {(void**)&c->d_hist, 12 * 64 * sizeof(unsigned long long)},
+      {(void**)&c->d_hist, 13 * 64 * sizeof(unsigned long long)},
   };
   for (auto& a : allocs) {
     if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return bail(e, "hipMalloc");
@@ -1092,8 +1092,10 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
     c->dev_bytes += (size_t)ch * per_item + ((size_t)ch + 8) * sizeof(double);
   }
   hipMemset(c->d_pmask, 0, Nm);
-  hipMemset(c->d_hist, 0, 12 * 64 * sizeof(unsigned long long));
-  c->expm_alg = (getenv("QOC_EXPM_PADE") && atoi(getenv("QOC_EXPM_PADE")) != 0) ? 0 : 1;
+  hipMemset(c->d_hist, 0, 13 * 64 * sizeof(unsigned long long));
+  c->expm_alg = (getenv("QOC_EXPM_PADE") && atoi(getenv("QOC_EXPM_PADE")) != 0) ? 0
+                : (getenv("QOC_EXPM_LDS") && atoi(getenv("QOC_EXPM_LDS")) != 0)   ? 2
+                                                                                   : 1;
   c->ode_kernel = (getenv("QOC_ODE_LDS") && atoi(getenv("QOC_ODE_LDS")) != 0) ? 1 : 0;
   hipMemset(c->d_L, 0, (size_t)B * (Nt + 1) * Nm * c->esz);
   *out = c;
@@ -1539,10 +1541,10 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
 int qoc_taylor_histogram(qoc_ctx* c, long long* hist, int reset) {
   if (!c || !hist) return fail(c, QOC_ERR_ARG, "null argument");
   HIPCHK(c, hipSetDevice(c->dev));
-  HIPCHK(c, hipMemcpyAsync(hist, c->d_hist + 5 * 64, 7 * 64 * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
-  if (reset) HIPCHK(c, hipMemsetAsync(c->d_hist + 5 * 64, 0, 7 * 64 * sizeof(long long), c->stream));
+  HIPCHK(c, hipMemcpyAsync(hist, c->d_hist + 5 * 64, 8 * 64 * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+  if (reset) HIPCHK(c, hipMemsetAsync(c->d_hist + 5 * 64, 0, 8 * 64 * sizeof(long long), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  for (int i = 0; i < 7 * 64; ++i) hist[i] += c->big_thist[i];
+  for (int i = 0; i < 8 * 64; ++i) hist[i] += c->big_thist[i];
   if (reset) std::memset(c->big_thist, 0, sizeof(c->big_thist));
   return QOC_OK;
 }

@@ -121,6 +121,19 @@ __device__ __forceinline__ void taylor_select(double nA, int& r, int& s) {
   }
 }
 
+// Degree-12 Taylor polynomial in 4 matrix products (the scheme of Bader, Blanes & Casas 2019,
+// coefficients re-derived here: tools/derive_t12.py):
+//   A2 = A A, A3 = A2 A, B_j = x_j0 I + x_j1 A + x_j2 A2 + x_j3 A3,
+//   A6 = B3 + B4 B4,  T12 = B1 + (B2 + A6) A6  ==  sum_{k<=12} A^k / k!  exactly.
+// kTheta12: largest ||A||_1 with sum_{k>12} ||A||^k / k! <= 2^-53.
+__constant__ double kT12[4][4] = {
+    {1.0, 0.99999999999276613715098, -0.13243184210109929356121, -0.050548416421727518977426},
+    {5.5174437753406856228547, 1.3093238729673181077940, 0.0043247187525051520919919, 0.0096586056829351321677927},
+    {0.0, 1.3110895450078318461208e-12, 0.097250029534075019542638, 0.0068219250901116764187357},
+    {0.0, 0.13181061013830184015682, 0.020278555405892590793357, 0.0067595184686308635977856}};
+constexpr double kTheta12 = 0.3352136878286148;
+constexpr int kT12Row = 7;  // executed-histogram row of T12 (rows 0..6: Paterson-Stockmeyer r = 2..8)
+
 __device__ __forceinline__ int degree_index(int d) {
   return d == 3 ? 0 : d == 5 ? 1 : d == 7 ? 2 : d == 9 ? 3 : 4;
 }

@@ -242,8 +242,9 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
   }
 
   QOC_STAMP(2);
-  int tr, ts;
-  taylor_select(nA, tr, ts);
+  // ---- T12 = Taylor degree 12 in 4 products (kT12, qoc_expm.hpp), s squarings ----
+  int ts = 0;
+  if (nA > kTheta12) ts = (int)ceil(log2(nA / kTheta12));
   if (tid == 0) {
     int d, sq = 0;
     if (nA <= 2.1) {
@@ -254,26 +255,23 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
       sq = s > 0 ? (int)ceil(s) : 0;
     }
     if (hist) atomicAdd(&hist[degree_index(d) * 64 + (sq < 63 ? sq : 63)], 1ULL);
-    if (thist) atomicAdd(&thist[(tr - 2) * 64 + (ts < 63 ? ts : 63)], 1ULL);
+    if (thist) atomicAdd(&thist[kT12Row * 64 + (ts < 63 ? ts : 63)], 1ULL);
   }
   const T sc = (T)ldexp(1.0, -ts);  // exact power-of-two scaling
 
-  // As = 2^-s A (owned); A2 = As As = 2^-s (As A); A3 = A2 As = 2^-s (A2 A)
-  Own Z, W;
+  // As = 2^-s A (owned); A2 = As As = 2^-s (As A); A3 = A2 As = 2^-s (A2 A)   [products 1, 2]
+  Own Z, W, V3;
   E::zero(Z);
   E::scale(V, sc);
   E::template rmul<KS>(N, V, Ar, Ai, W, Z, lane);
   E::scale(W, sc);
-  E::store_own(N, W, Br, Bi, row, lane);
-  E::template rmul<KS>(N, W, Ar, Ai, V, Z, lane);
-  E::scale(V, sc);
-  E::store_own(N, V, Xr, Xi, row, lane);
-  __syncthreads();
+  E::template rmul<KS>(N, W, Ar, Ai, V3, Z, lane);
+  E::scale(V3, sc);
 
-  // B_i at the owned positions: c0 I + c1 As + c2 A2 (As exactly rescaled from bufA)
+  // B_j = x_j0 I + x_j1 As + x_j2 A2 + x_j3 A3 at the owned positions (As re-read from bufA).
   const int ra = min(row, N - 1) * E::ldp(N);
-  auto make_B = [&](int i, Own& B) __attribute__((always_inline)) {
-    const T c0 = (T)kInvFact[3 * i], c1 = (T)kInvFact[3 * i + 1] * sc, c2 = (T)kInvFact[3 * i + 2];
+  auto make_B = [&](const double* x, Own& B) __attribute__((always_inline)) {
+    const T x0 = (T)x[0], x1 = (T)x[1] * sc, x2 = (T)x[2], x3 = (T)x[3];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -281,28 +279,61 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
         // columns >= N read the next row: that reaches only result columns >= N (masked by rmul)
         const int col = 16 * t + M::drow(lane, e);
         const int a = ra + col;
-        const T br = c1 * Ar[a] + c2 * Br[a] + (row == col ? c0 : T(0));
-        const T bi = c1 * Ai[a] + c2 * Bi[a];
+        const T br = x1 * Ar[a] + x2 * W.r[t][e] + x3 * V3.r[t][e] + (row == col ? x0 : T(0));
+        const T bi = x1 * Ai[a] + x2 * W.i[t][e] + x3 * V3.i[t][e];
         B.r[t][e] = rok ? br : T(0);
         B.i[t][e] = rok ? bi : T(0);
       }
   };
+  // Park an owned matrix in LDS at its own (row-major) positions; only the writing lane reads it back
+  // (masked: entries outside N x N come back zero).
+  auto put = [&](const Own& X, T* Pr, T* Pi) __attribute__((always_inline)) { E::store_own(N, X, Pr, Pi, row, lane); };
+  auto get = [&](Own& X, const T* Pr, const T* Pi) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = 16 * t + M::drow(lane, e);
+        const bool ok = rok && (t < NT - 1 || col < N);
+        const int a = ra + min(col, N - 1);
+        const T xr = Pr[a], xi = Pi[a];
+        X.r[t][e] = ok ? xr : T(0);
+        X.i[t][e] = ok ? xi : T(0);
+      }
+  };
   QOC_STAMP(3);
-  make_B(tr, V);  // Horner start
-  for (int i = tr - 1; i >= 0; --i) {
-    if (i == 1) QOC_STAMP(7);
-    make_B(i, W);
-    if (i == 1) QOC_STAMP(8);
-    E::template rmul<KS>(N, V, Xr, Xi, V, W, lane);
-    if (i == 1) QOC_STAMP(9);  // V <- V A3 + B_i  (= A3 V + B_i: polynomials in A commute)
+  Own B4, B3;
+  make_B(kT12[3], B4);
+  E::store_own(N, B4, Br, Bi, row, lane);  // B4 -> buffer 2 (operand of product 3)
+  {
+    Own B2;
+    make_B(kT12[1], B2);
+    put(B2, Xr, Xi);  // B2 -> buffer 3 (own positions)
   }
-
-  // ---- squarings: ping-pong bufA / bufX, one barrier each (plus one: Horner still reads both) ----
+  make_B(kT12[2], B3);
+  Own B1;
+  make_B(kT12[0], B1);
+  __syncthreads();  // every wave is done with A (buffer 1) and buffer 2 is complete
+  put(B1, Ar, Ai);  // B1 -> buffer 1 (own positions)
+  E::template rmul<KS>(N, B4, Br, Bi, V, B3, lane);  // A6 = B3 + B4 B4   [product 3]
+  __syncthreads();                                    // buffer 2 (B4) readers are done
+  E::store_own(N, V, Br, Bi, row, lane);              // A6 -> buffer 2
+  get(W, Xr, Xi);                                     // B2
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    W.r[t] += V.r[t];
+    W.i[t] += V.i[t];
+  }
+  get(B1, Ar, Ai);
+  __syncthreads();
+  E::template rmul<KS>(N, W, Br, Bi, V, B1, lane);  // T12 = B1 + (B2 + A6) A6   [product 4]
+  // ---- squarings: ping-pong buffers 3 / 1 (buffer 2 may still be read by product 4), one barrier
+  // each, plus one first: other waves may not have read back their B1 / B2 yet ----
   QOC_STAMP(4);
   if (ts > 0) __syncthreads();
   for (int q = 0; q < ts; ++q) {
-    T* Sr = (q & 1) ? Xr : Ar;
-    T* Si = (q & 1) ? Xi : Ai;
+    T* Sr = (q & 1) ? Ar : Xr;
+    T* Si = (q & 1) ? Ai : Xi;
     E::store_own(N, V, Sr, Si, row, lane);
     __syncthreads();
     E::template rmul<KS>(N, V, Sr, Si, V, Z, lane);
