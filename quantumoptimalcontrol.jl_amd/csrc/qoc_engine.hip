@@ -21,6 +21,7 @@
 #include "qoc_expm.hpp"
 #include "qoc_expm_rr.hpp"
 #include "qoc_frechet.hpp"
+#include "qoc_grad_rr.hpp"
 #include "qoc_ode.hpp"
 #include "qoc_spline.hpp"
 
@@ -99,6 +100,8 @@ struct qoc_ctx {
   void* d_Cst = nullptr;   // nu N x N: [A1; A2; ...]
   void* d_gws = nullptr;   // 6 x N x B(Nt+1)m
   bool grad_gemm = true;
+  bool grad_rr = false;  // fused register-resident order-3 gradient (qoc_grad_rr.hpp)
+  int ncu = 256;         // compute units of the device (persistent-grid sizing)
   // exact (Fréchet) gradient mode workspace, allocated on first use
   void* d_fws = nullptr;
   size_t fws_bytes = 0;
@@ -278,6 +281,8 @@ template <typename T>
 int frechet_grad(qoc_ctx* c, double* d_dJdu);
 template <typename T>
 int grad_gemm_o3(qoc_ctx* c, double* d_dJdu);
+template <typename T>
+int grad_rr_o3(qoc_ctx* c, double* d_dJdu);
 
 template <typename T>
 int ode_forward(qoc_ctx* c);
@@ -323,6 +328,12 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
   if (order == QOC_DUKDP_EXACT) {
     mk = mark_begin(c, 3);
     int r = frechet_grad<T>(c, d_dJdu);
+    mark_end(c, mk);
+    return r;
+  }
+  if (order == 3 && c->grad_rr) {
+    mk = mark_begin(c, 3);
+    int r = grad_rr_o3<T>(c, d_dJdu);
     mark_end(c, mk);
     return r;
   }
@@ -855,6 +866,55 @@ int grad_gemm_o3(qoc_ctx* c, double* d_dJdu) {
   return QOC_OK;
 }
 
+// Fused order-3 gradient (qoc_grad_rr.hpp): k_grad_rr_q (co-state side -> W0, W1 in the state layout)
+// then k_grad_rr_p (state side + contraction -> dJdu).  Persistent grids of 4-wave workgroups.
+template <typename T, int NT, int KS, int NU>
+int grad_rr_launch(qoc_ctx* c, double* d_dJdu) {
+  using G = GradRR<T, NT>;
+  const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
+  const size_t lds = G::lds_bytes(N, NU);
+  const long long units = (long long)B * Nt, ntiles = (units + 16 / m - 1) / (16 / m);
+  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+  const int grid = (int)std::max<long long>(1, std::min<long long>((ntiles + 3) / 4, (long long)c->ncu * per_cu));
+  const size_t bufN = (size_t)N * ((size_t)B * (Nt + 1) * m);
+  cx<T>* W0 = (cx<T>*)c->d_gws;
+  cx<T>* W1 = W0 + bufN;
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_q<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_p<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((k_grad_rr_q<T, NT, KS, NU>), dim3(grid), dim3(256), lds, c->stream, N, m, Nt, B,
+                     (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_L, W0, W1);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL((k_grad_rr_p<T, NT, KS, NU>), dim3(grid), dim3(256), lds, c->stream, N, m, Nt, B,
+                     (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, (const cx<T>*)W0,
+                     (const cx<T>*)W1, d_dJdu);
+  HIPCHK(c, hipGetLastError());
+  return QOC_OK;
+}
+
+template <typename T, int NT, int NU>
+int grad_rr_nt(qoc_ctx* c, double* d_dJdu) {
+  const int ks = sizeof(T) == 8 ? (c->N + 3) / 4 : 4 * NT;
+  if constexpr (sizeof(T) == 8) {
+    if (ks == 4 * NT - 3) return grad_rr_launch<T, NT, 4 * NT - 3, NU>(c, d_dJdu);
+    if (ks == 4 * NT - 2) return grad_rr_launch<T, NT, 4 * NT - 2, NU>(c, d_dJdu);
+    if (ks == 4 * NT - 1) return grad_rr_launch<T, NT, 4 * NT - 1, NU>(c, d_dJdu);
+  }
+  return grad_rr_launch<T, NT, 4 * NT, NU>(c, d_dJdu);
+}
+
+template <typename T>
+int grad_rr_o3(qoc_ctx* c, double* d_dJdu) {
+  const int NT = (c->N + 15) / 16;
+  if (c->nu == 1) {
+    if (NT == 1) return grad_rr_nt<T, 1, 1>(c, d_dJdu);
+    if (NT == 2) return grad_rr_nt<T, 2, 1>(c, d_dJdu);
+    return grad_rr_nt<T, 3, 1>(c, d_dJdu);
+  }
+  if (NT == 1) return grad_rr_nt<T, 1, 2>(c, d_dJdu);
+  if (NT == 2) return grad_rr_nt<T, 2, 2>(c, d_dJdu);
+  return grad_rr_nt<T, 3, 2>(c, d_dJdu);
+}
+
 // Exact gradient (QOC_DUKDP_EXACT): one Fréchet derivative per slice from the 2N x 2N block exponential
 // (qoc_frechet.hpp), k_expm when 2N fits the LDS-resident kernel, the GEMM pipeline otherwise.
 template <typename T>
@@ -1066,7 +1126,22 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
     if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return bail(e, "hipMalloc");
     c->dev_bytes += a.bytes;
   }
-  c->grad_gemm = !c->big && N >= 32 && nu <= 8 && !(getenv("QOC_GRAD_KERNEL") && atoi(getenv("QOC_GRAD_KERNEL")) != 0);
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
+  }
+  const bool env_kernel = getenv("QOC_GRAD_KERNEL") && atoi(getenv("QOC_GRAD_KERNEL")) != 0;
+  const bool env_gemm = getenv("QOC_GRAD_GEMM") && atoi(getenv("QOC_GRAD_GEMM")) != 0;
+  const size_t grr_lds = (size_t)2 * (nu + 1) * N * (precision == QOC_FP64 ? (N | 1) : ((N + 3) & ~3)) *
+                         (precision == QOC_FP64 ? 8 : 4);
+  c->grad_rr = !c->big && N <= 48 && (m == 1 || m == 2 || m == 4 || m == 8 || m == 16) && (nu == 1 || nu == 2) &&
+               grr_lds <= 160 * 1024 && !env_kernel && !env_gemm;
+  c->grad_gemm = !c->grad_rr && !c->big && N >= 32 && nu <= 8 && !env_kernel;
+  if (c->grad_rr) {
+    const size_t cols = (size_t)B * (Nt + 1) * m;
+    if ((e = hipMalloc(&c->d_gws, 2 * (size_t)N * cols * c->esz)) != hipSuccess) return bail(e, "hipMalloc");
+    c->dev_bytes += 2 * (size_t)N * cols * c->esz;
+  }
   if (c->grad_gemm) {
     const size_t cols = (size_t)B * (Nt + 1) * m;
     if ((e = hipMalloc(&c->d_AH, (nu + 1) * NN * c->esz)) != hipSuccess) return bail(e, "hipMalloc");

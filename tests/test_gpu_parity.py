@@ -338,26 +338,50 @@ def test_taylor_default_and_pade_option_agree(built_lib, monkeypatch):
         assert np.linalg.norm(g0[b] - gr) / np.linalg.norm(gr) <= 1e-10
 
 
+@pytest.mark.parametrize("path", ["fused", "gemm"])
 @pytest.mark.parametrize("precision", ["fp64", "fp32"])
-def test_gemm_gradient_n40_penalty_and_precision(built_lib, precision):
-    """N >= 32 selects the GEMM-shaped order-3 gradient (generator-combine + fused contraction); cover it
-    with the guard-state penalty (λ carries dL/dx) in both precisions, and check it against k_grad."""
+def test_gemm_gradient_n40_penalty_and_precision(built_lib, monkeypatch, precision, path):
+    """The order-3 gradient at N = 40: the fused register-resident kernels (default) and the GEMM-shaped
+    path (QOC_GRAD_GEMM=1: generator-combine + fused contraction), with the guard-state penalty (λ
+    carries dL/dx), in both precisions, against the oracle."""
     from qoc_amd import systems
+    monkeypatch.setenv("QOC_GRAD_GEMM", "1" if path == "gemm" else "0")
     prob = systems.cavity_problem(N_cavity=20, Nt=16)
     u = systems.cavity_controls(3, prob.Nt, seed=11)
     pen = (list(range(30, 40)), [0, 1], 0.23)
     _check(prob, u, precision=precision, penalty=pen)
 
 
-def test_gemm_gradient_equals_per_slice_kernel(built_lib, monkeypatch):
+@pytest.mark.parametrize("which", ["cavity40", "zz", "tunable_bus", "ragged"])
+def test_fused_gradient_equals_per_slice_kernel(built_lib, monkeypatch, which):
+    """Fused gradient (default), GEMM path and per-slice k_grad agree to rounding: m = 2, 4, 1, nu = 2, 1,
+    and a ragged tile count (B * Nt not a multiple of the 16/m units per tile) with N = 23."""
     from qoc_amd import systems
-    prob = systems.cavity_problem(N_cavity=20, Nt=10)
-    u = systems.cavity_controls(2, prob.Nt, seed=12)
+    if which == "cavity40":
+        prob = systems.cavity_problem(N_cavity=20, Nt=10)
+        u = systems.cavity_controls(2, prob.Nt, seed=12)
+    elif which == "zz":
+        prob = systems.zz_problem(Nt=30)
+        u = systems.zz_controls(3, prob.Nt, tgate=1.2, seed=4)
+    elif which == "tunable_bus":
+        prob = systems.tunable_bus_problem(Nt=21)
+        u = systems.tunable_bus_controls(3, prob.Nt, seed=5)
+    else:
+        import dataclasses
+        p0 = systems.synthetic_problem(N=23, nu=2, Nt=7, seed=3, precision="fp64")
+        prob = dataclasses.replace(p0, x0=p0.x0[:, :2].copy(), x_target=p0.x_target[:, :2].copy(), n=2.0)
+        u = systems.synthetic_controls(3, prob.Nt, nu=2, seed=3) * 0.2
     res = []
-    for env in ("0", "1"):
-        monkeypatch.setenv("QOC_GRAD_KERNEL", env)
-        e = _engine(prob, 2)
+    for env in ({}, {"QOC_GRAD_GEMM": "1"}, {"QOC_GRAD_KERNEL": "1"}):
+        for k in ("QOC_GRAD_GEMM", "QOC_GRAD_KERNEL"):
+            monkeypatch.setenv(k, env.get(k, "0"))
+        e = _engine(prob, u.shape[0])
         e.propagate(u)
         res.append(e.grape_sensitivity(u, 3))
         e.close()
-    np.testing.assert_allclose(res[0], res[1], rtol=1e-12, atol=1e-15)
+    scale = np.abs(res[2]).max()
+    np.testing.assert_allclose(res[0], res[2], rtol=0, atol=1e-12 * scale)
+    np.testing.assert_allclose(res[1], res[2], rtol=0, atol=1e-12 * scale)
+    for b in range(u.shape[0]):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        assert np.linalg.norm(res[0][b] - gr) / np.linalg.norm(gr) <= 1e-10
