@@ -281,8 +281,10 @@ def main():
                    "frac": ach / pk}
     if not large:
         dom = max(per_launch, key=per_launch.get)
-        # the exponential phase runs k_expm_rr (register-resident T12) unless QOC_EXPM_LDS / QOC_EXPM_PADE
-        kname = "k_expm_rr" if dom == "k_expm" and any(mm == 12 for (mm, _) in thist) else dom
+        # the exponential phase runs the register-resident kernels (k_expm_rr: T12 / Paterson-Stockmeyer)
+        # unless QOC_EXPM_LDS or QOC_EXPM_PADE selects the LDS kernel k_expm
+        lds_expm = any(os.environ.get(v, "0") not in ("", "0") for v in ("QOC_EXPM_LDS", "QOC_EXPM_PADE"))
+        kname = "k_expm_rr" if dom == "k_expm" and not lds_expm else dom
         roof = {"kernel": kname, "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
                 "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
                 "traffic": traffic_all.get(kname, traffic_all.get(dom)), "ms_per_launch": kern[dom]["ms_per_launch"]}

@@ -101,6 +101,8 @@ struct qoc_ctx {
   void* d_gws = nullptr;   // 6 x N x B(Nt+1)m
   bool grad_gemm = true;
   bool grad_rr = false;  // fused register-resident order-3 gradient (qoc_grad_rr.hpp)
+  int* d_ps = nullptr;   // k_expm_rr pass-2 counter + list of Paterson-Stockmeyer units
+  double a0norm = 0.0;   // ||A0||_1 of the generators (host-side, at qoc_set_generators)
   int ncu = 256;         // compute units of the device (persistent-grid sizing)
   // exact (Fréchet) gradient mode workspace, allocated on first use
   void* d_fws = nullptr;
@@ -142,25 +144,45 @@ bool expm_supported(int N, int prec) {
   return lds <= 160 * 1024;
 }
 
+// Two launches: the T12 pass over every unit, then the Paterson-Stockmeyer pass over the units the
+// first one listed (||A_k||_1 > 4 theta_12); ps = {list (>= nunits ints), counter}.
 template <typename T, int NT, int KS>
 hipError_t launch_expm_rr_k(hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
-                            const void* Ain, void* Uout, unsigned long long* hist, unsigned long long* thist) {
+                            const void* Ain, void* Uout, unsigned long long* hist, unsigned long long* thist,
+                            int* ps, bool mix) {
   const size_t lds = ExpmRR<T, NT>::lds_bytes(N);
+  if (mix) {  // one pass, T12 or Paterson-Stockmeyer per slice inline
+    hipError_t e =
+        hipFuncSetAttribute((const void*)k_expm_rr_mix<T, NT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_expm_rr_mix<T, NT, KS>), dim3(nunits), dim3(64 * NT), lds, s, N, nu, nunits,
+                       (const cx<T>*)Agen, u, (const cx<T>*)Ain, (cx<T>*)Uout, hist, thist);
+    return hipGetLastError();
+  }
   hipError_t e =
       hipFuncSetAttribute((const void*)k_expm_rr<T, NT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_expm_rr_ps<T, NT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  int* list = ps + 1;
+  if ((e = hipMemsetAsync(ps, 0, sizeof(int), s)) != hipSuccess) return e;
   hipLaunchKernelGGL((k_expm_rr<T, NT, KS>), dim3(nunits), dim3(64 * NT), lds, s, N, nu, nunits, (const cx<T>*)Agen, u,
-                     (const cx<T>*)Ain, (cx<T>*)Uout, hist, thist);
+                     (const cx<T>*)Ain, (cx<T>*)Uout, hist, thist, list, ps);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const int grid = nunits;  // pass 2 exits at once past the listed count
+  hipLaunchKernelGGL((k_expm_rr_ps<T, NT, KS>), dim3(grid), dim3(64 * NT), lds, s, N, nu, (const cx<T>*)Agen, u,
+                     (const cx<T>*)Ain, (cx<T>*)Uout, hist, thist, (const int*)list, (const int*)ps);
   return hipGetLastError();
 }
 
 // k-steps: f64 ceil(N/4) (compile-time, one of the 4 values for this NT), f32 all 4 NT.
 template <typename T, int NT>
 hipError_t launch_expm_rr_t(hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
-                            const void* Ain, void* Uout, unsigned long long* hist, unsigned long long* thist) {
+                            const void* Ain, void* Uout, unsigned long long* hist, unsigned long long* thist, int* ps,
+                            bool mix) {
   const int ks = sizeof(T) == 8 ? (N + 3) / 4 : 4 * NT;
 #define QOC_RRK(K) \
-  if (ks == (K)) return launch_expm_rr_k<T, NT, (K)>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, thist)
+  if (ks == (K)) return launch_expm_rr_k<T, NT, (K)>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, thist, ps, mix)
   if constexpr (sizeof(T) == 8) {
     QOC_RRK(4 * NT - 3);
     QOC_RRK(4 * NT - 2);
@@ -187,12 +209,12 @@ hipError_t launch_expm_t(hipStream_t s, int N, int nu, int nunits, const void* A
 // alg 0: Padé + solve (reference algorithm); alg 1: register-resident Taylor T12; alg 2: LDS Paterson-Stockmeyer.
 hipError_t launch_expm(int prec, hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
                        const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq, int alg = 0,
-                       unsigned long long* thist = nullptr) {
+                       unsigned long long* thist = nullptr, int* ps = nullptr, bool mix = false) {
   const int NT = (N + 15) / 16;
   // alg 1: the register-resident T12 kernel (qoc_expm_rr.hpp); alg 2: the LDS Paterson-Stockmeyer one.
-  const bool rr = alg == 1;
+  const bool rr = alg == 1 && ps;  // the register-resident kernel needs the pass-2 list (ctx workspace)
 #define QOC_LX(TT, NTT)                                                                                   \
-  return alg ? (rr ? launch_expm_rr_t<TT, NTT>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, thist)          \
+  return alg ? (rr ? launch_expm_rr_t<TT, NTT>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, thist, ps, mix) \
                    : launch_expm_t<TT, NTT, 1>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq, thist)) \
              : launch_expm_t<TT, NTT, 0>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq, thist)
   if (prec == QOC_FP64) {
@@ -294,7 +316,8 @@ int run_forward(qoc_ctx* c) {
   if (c->prop_method == QOC_PROP_TSIT5) return ode_forward<T>(c);
   int mk = mark_begin(c, 0);
   hipError_t e = launch_expm(c->prec, c->stream, c->N, c->nu, c->B * c->Nt, c->d_A, c->d_u, nullptr, c->d_U,
-                             c->d_hist, nullptr, nullptr, c->expm_alg, c->d_hist + 5 * 64);
+                             c->d_hist, nullptr, nullptr, c->expm_alg, c->d_hist + 5 * 64, c->d_ps,
+                             c->a0norm > 4.0 * kTheta12);
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm launch: %s", hipGetErrorString(e));
   const size_t lds = chain_lds(c);
@@ -962,7 +985,7 @@ int frechet_grad(qoc_ctx* c, double* d_dJdu) {
     HIPCHK(c, hipGetLastError());
     if (small) {
       hipError_t e = launch_expm(c->prec, c->stream, n2, 0, cnt, nullptr, nullptr, blocks, E, nullptr, nullptr, nullptr,
-                                 c->expm_alg);
+                                 c->expm_alg, nullptr, c->d_ps);
       if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm (Frechet block): %s", hipGetErrorString(e));
     } else {
       HIPCHK(c, hipMemsetAsync(red, 0, sizeof(double), c->stream));
@@ -1121,6 +1144,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
       {(void**)&c->d_dJdu, (size_t)B * nu * Nt * sizeof(double)},
       {(void**)&c->d_flag, sizeof(int)},
       {(void**)&c->d_hist, 13 * 64 * sizeof(unsigned long long)},
+      {(void**)&c->d_ps, ((size_t)std::max<long long>((long long)B * Nt, 16384) + 1) * sizeof(int)},
   };
   for (auto& a : allocs) {
     if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return bail(e, "hipMalloc");
@@ -1182,7 +1206,7 @@ void qoc_destroy(qoc_ctx* c) {
   hipSetDevice(c->dev);
   if (c->stream) hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
-                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws};
+                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_ps};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& m : c->marks) {
@@ -1227,6 +1251,15 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  {  // ||A0||_1 (host copy): selects the one-pass k_expm_rr_mix when every slice has large norm anyway
+    double nrm = 0.0;
+    for (int col = 0; col < c->N; ++col) {
+      double sum = 0.0;
+      for (int row = 0; row < c->N; ++row) sum += std::hypot(A0[2 * (row + (size_t)c->N * col)], A0[2 * (row + (size_t)c->N * col) + 1]);
+      nrm = std::max(nrm, sum);
+    }
+    c->a0norm = nrm;
+  }
   c->have_gen = true;
   c->have_prop = false;
   return QOC_OK;

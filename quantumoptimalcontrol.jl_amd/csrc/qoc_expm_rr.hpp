@@ -151,18 +151,19 @@ struct ExpmRR {
 // ALG 1 (Taylor) kernel.  unit = blockIdx.x.  Either generators (Agen, u) or explicit matrices (Ain).
 // hist receives the Padé (d, s) the reference would select (reference-equivalent accounting), thist the
 // executed Taylor (r, s).  KS: k-steps per product (see ExpmRR::rows).
-template <typename T, int NT, int KS>
-__global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunits, const cx<T>* __restrict__ Agen,
-                                                        const double* __restrict__ u, const cx<T>* __restrict__ Ain,
-                                                        cx<T>* __restrict__ Uout, unsigned long long* __restrict__ hist,
-                                                        unsigned long long* __restrict__ thist) {
+template <typename T, int NT, int KS, int MODE>
+__device__ __forceinline__ void expm_rr_unit(int unit, int N, int nu, const cx<T>* __restrict__ Agen,
+                                             const double* __restrict__ u, const cx<T>* __restrict__ Ain,
+                                             cx<T>* __restrict__ Uout, unsigned long long* __restrict__ hist,
+                                             unsigned long long* __restrict__ thist, int* __restrict__ ps_list,
+                                             int* __restrict__ ps_count) {
   using E = ExpmRR<T, NT>;
   using Own = typename E::Own;
   using M = typename E::M;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int unit = blockIdx.x;
-  if (unit >= nunits) return;
-  const int tid = threadIdx.x, lane = tid & 63;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // opaque: in the persistent pass nothing derived is hoisted out of the unit loop
+  const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int NN = N * N, PL = E::plane(N);
   const int row = 16 * wave + (lane & 15);
@@ -175,6 +176,7 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
   T* Xi = Xr + PL;
   float* colf = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(Xi + PL + 16));
 
+  auto mask_own = [&](Own& X) __attribute__((always_inline)) { E::mask_cols(N, X, lane); };
   QOC_STAMP(0);
   QOC_RTSTAMP(60);
   QOC_LIFE(0);
@@ -242,9 +244,25 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
   }
 
   QOC_STAMP(2);
-  // ---- T12 = Taylor degree 12 in 4 products (kT12, qoc_expm.hpp), s squarings ----
+  // ---- T12 = Taylor degree 12 in 4 products (kT12, qoc_expm.hpp) with s squarings; when T12 would
+  // need >= 3 squarings (||A||_1 > 4 theta_12), Paterson-Stockmeyer degree 3r+2 instead (taylor_select:
+  // about the same GEMM count, fewer squarings, so 2^s times less rounding growth) ----
   int ts = 0;
   if (nA > kTheta12) ts = (int)ceil(log2(nA / kTheta12));
+  int tr = 0;  // 0: T12; 2..8: Paterson-Stockmeyer r
+  // MODE 0: T12 only (A2 / A3 from registers), larger norms listed for the Paterson-Stockmeyer pass;
+  // MODE 1: Paterson-Stockmeyer only (the listed units); MODE 2: both inline (T12 reading A2 / A3 back
+  // from LDS, so that no register state crosses the algorithm branch).
+  if (MODE == 0) {
+    if (ts >= 3) {
+      if (tid == 0) ps_list[atomicAdd(ps_count, 1)] = unit;
+      return;
+    }
+  } else if (MODE == 1 || ts >= 3) {
+    taylor_select(nA, tr, ts);
+  }
+  tr = __builtin_amdgcn_readfirstlane(tr);
+  ts = __builtin_amdgcn_readfirstlane(ts);
   if (tid == 0) {
     int d, sq = 0;
     if (nA <= 2.1) {
@@ -255,7 +273,7 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
       sq = s > 0 ? (int)ceil(s) : 0;
     }
     if (hist) atomicAdd(&hist[degree_index(d) * 64 + (sq < 63 ? sq : 63)], 1ULL);
-    if (thist) atomicAdd(&thist[kT12Row * 64 + (ts < 63 ? ts : 63)], 1ULL);
+    if (thist) atomicAdd(&thist[(tr ? tr - 2 : kT12Row) * 64 + (ts < 63 ? ts : 63)], 1ULL);
   }
   const T sc = (T)ldexp(1.0, -ts);  // exact power-of-two scaling
 
@@ -268,26 +286,15 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
   E::template rmul<KS>(N, W, Ar, Ai, V3, Z, lane);
   E::scale(V3, sc);
 
-  // B_j = x_j0 I + x_j1 As + x_j2 A2 + x_j3 A3 at the owned positions (As re-read from bufA).
-  const int ra = min(row, N - 1) * E::ldp(N);
-  auto make_B = [&](const double* x, Own& B) __attribute__((always_inline)) {
-    const T x0 = (T)x[0], x1 = (T)x[1] * sc, x2 = (T)x[2], x3 = (T)x[3];
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        // columns >= N read the next row: that reaches only result columns >= N (masked by rmul)
-        const int col = 16 * t + M::drow(lane, e);
-        const int a = ra + col;
-        const T br = x1 * Ar[a] + x2 * W.r[t][e] + x3 * V3.r[t][e] + (row == col ? x0 : T(0));
-        const T bi = x1 * Ai[a] + x2 * W.i[t][e] + x3 * V3.i[t][e];
-        B.r[t][e] = rok ? br : T(0);
-        B.i[t][e] = rok ? bi : T(0);
-      }
-  };
-  // Park an owned matrix in LDS at its own (row-major) positions; only the writing lane reads it back
-  // (masked: entries outside N x N come back zero).
-  auto put = [&](const Own& X, T* Pr, T* Pi) __attribute__((always_inline)) { E::store_own(N, X, Pr, Pi, row, lane); };
+  // Paterson-Stockmeyer pass: A3 -> buffer 3 (row-major, its operand), A2 -> buffer 2 at the owned
+  // rows (read back by make_Bps).  The T12 pass uses A2 / A3 from registers.
+  if constexpr (MODE != 0) {
+    E::store_own(N, V3, Xr, Xi, row, lane);
+    E::store_own(N, W, Br, Bi, row, lane);
+  }
+  const int ra = min(row, N - 1) * E::ldp(N);  // owned row; columns >= N read junk that reaches only
+                                                // result columns >= N (masked by rmul)
+  // Park / fetch an owned matrix at its own (row-major) positions; only the writing lane reads it back.
   auto get = [&](Own& X, const T* Pr, const T* Pi) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -302,33 +309,135 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
       }
   };
   QOC_STAMP(3);
-  Own B4, B3;
-  make_B(kT12[3], B4);
-  E::store_own(N, B4, Br, Bi, row, lane);  // B4 -> buffer 2 (operand of product 3)
-  {
-    Own B2;
-    make_B(kT12[1], B2);
-    put(B2, Xr, Xi);  // B2 -> buffer 3 (own positions)
-  }
-  make_B(kT12[2], B3);
-  Own B1;
-  make_B(kT12[0], B1);
-  __syncthreads();  // every wave is done with A (buffer 1) and buffer 2 is complete
-  put(B1, Ar, Ai);  // B1 -> buffer 1 (own positions)
-  E::template rmul<KS>(N, B4, Br, Bi, V, B3, lane);  // A6 = B3 + B4 B4   [product 3]
-  __syncthreads();                                    // buffer 2 (B4) readers are done
-  E::store_own(N, V, Br, Bi, row, lane);              // A6 -> buffer 2
-  get(W, Xr, Xi);                                     // B2
+  if constexpr (MODE == 0) {
+    // ---- T12: B_j = x_j0 I + x_j1 As + x_j2 A2 + x_j3 A3 at the owned positions (As from buffer 1,
+    // A2 / A3 from registers); B4 -> buffer 2 and B2 -> buffer 3 over this lane's own rows ----
+    auto make_B = [&](const double* x, Own& B) __attribute__((always_inline)) {
+      const T x0 = (T)x[0], x1 = (T)x[1] * sc, x2 = (T)x[2], x3 = (T)x[3];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    W.r[t] += V.r[t];
-    W.i[t] += V.i[t];
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = 16 * t + M::drow(lane, e);
+          const int a = ra + col;
+          const T br = x1 * Ar[a] + x2 * W.r[t][e] + x3 * V3.r[t][e] + (row == col ? x0 : T(0));
+          const T bi = x1 * Ai[a] + x2 * W.i[t][e] + x3 * V3.i[t][e];
+          B.r[t][e] = rok ? br : T(0);
+          B.i[t][e] = rok ? bi : T(0);
+        }
+    };
+    Own B4, B3;
+    make_B(kT12[3], B4);
+    mask_own(B4);
+    E::store_own(N, B4, Br, Bi, row, lane);  // B4 -> buffer 2 (operand of product 3)
+    {
+      Own B2;
+      make_B(kT12[1], B2);
+      E::store_own(N, B2, Xr, Xi, row, lane);  // B2 -> buffer 3 (own positions)
+    }
+    make_B(kT12[2], B3);
+    Own B1;
+    make_B(kT12[0], B1);
+    __syncthreads();                                    // A (buffer 1) readers done, buffer 2 = B4 complete
+    E::store_own(N, B1, Ar, Ai, row, lane);             // B1 -> buffer 1 (own positions)
+    E::template rmul<KS>(N, B4, Br, Bi, V, B3, lane);  // A6 = B3 + B4 B4   [product 3]
+    __syncthreads();                                    // buffer 2 (B4) readers are done
+    E::store_own(N, V, Br, Bi, row, lane);              // A6 -> buffer 2
+    get(W, Xr, Xi);                                     // B2
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      W.r[t] += V.r[t];
+      W.i[t] += V.i[t];
+    }
+    get(B1, Ar, Ai);
+    __syncthreads();
+    E::template rmul<KS>(N, W, Br, Bi, V, B1, lane);  // T12 = B1 + (B2 + A6) A6   [product 4]
+  } else if (MODE == 2 && !tr) {
+    // ---- T12 with A2 / A3 read back from LDS: one pass over the owned positions, B4 -> buffer 2 and
+    // B2 -> buffer 3 in place of this lane's A2 / A3, B3 and B1 in registers ----
+    Own B4, B3, B1;
+    {
+      const double* x1 = kT12[0];
+      const double* x2 = kT12[1];
+      const double* x3 = kT12[2];
+      const double* x4 = kT12[3];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = 16 * t + M::drow(lane, e);
+          const int a = ra + col;
+          const T pr = Ar[a] * sc, pi = Ai[a] * sc, qr = Br[a], qi = Bi[a], wr = Xr[a], wi = Xi[a];
+          const bool dg = row == col;
+          auto comb = [&](const double* x, T& br, T& bi) __attribute__((always_inline)) {
+            br = (T)x[1] * pr + (T)x[2] * qr + (T)x[3] * wr + (dg ? (T)x[0] : T(0));
+            bi = (T)x[1] * pi + (T)x[2] * qi + (T)x[3] * wi;
+            br = rok ? br : T(0);
+            bi = rok ? bi : T(0);
+          };
+          T r4, i4, r2, i2, r3, i3, r1, i1;
+          comb(x4, r4, i4);
+          comb(x2, r2, i2);
+          comb(x3, r3, i3);
+          comb(x1, r1, i1);
+          B4.r[t][e] = r4;
+          B4.i[t][e] = i4;
+          B3.r[t][e] = r3;
+          B3.i[t][e] = i3;
+          B1.r[t][e] = r1;
+          B1.i[t][e] = i1;
+          if (rok && (t < NT - 1 || col < N)) {  // same positions this lane just read
+            Br[a] = r4;
+            Bi[a] = i4;
+            Xr[a] = r2;
+            Xi[a] = i2;
+          }
+        }
+    }
+    mask_own(B4);
+    mask_own(B3);
+    mask_own(B1);
+    __syncthreads();                                    // A (buffer 1) readers done, buffer 2 = B4 complete
+    E::store_own(N, B1, Ar, Ai, row, lane);             // B1 -> buffer 1 (own positions)
+    E::template rmul<KS>(N, B4, Br, Bi, V, B3, lane);  // A6 = B3 + B4 B4   [product 3]
+    __syncthreads();                                    // buffer 2 (B4) readers are done
+    E::store_own(N, V, Br, Bi, row, lane);              // A6 -> buffer 2
+    get(W, Xr, Xi);                                     // B2
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      W.r[t] += V.r[t];
+      W.i[t] += V.i[t];
+    }
+    get(B1, Ar, Ai);
+    __syncthreads();
+    E::template rmul<KS>(N, W, Br, Bi, V, B1, lane);  // T12 = B1 + (B2 + A6) A6   [product 4]
+  } else {
+    // ---- Paterson-Stockmeyer: V <- V A3 + B_i, B_i = c_3i I + c_3i+1 As + c_3i+2 A2 (A3 the LDS operand,
+    // As / A2 read back at the owned positions), barrier-free Horner ----
+    __syncthreads();  // buffer 3 complete
+    auto make_Bps = [&](int i, Own& B) __attribute__((always_inline)) {
+      const T c0 = (T)kInvFact[3 * i], c1 = (T)kInvFact[3 * i + 1] * sc, c2 = (T)kInvFact[3 * i + 2];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = 16 * t + M::drow(lane, e);
+          const int a = ra + col;
+          const T br = c1 * Ar[a] + c2 * Br[a] + (row == col ? c0 : T(0));
+          const T bi = c1 * Ai[a] + c2 * Bi[a];
+          B.r[t][e] = rok ? br : T(0);
+          B.i[t][e] = rok ? bi : T(0);
+        }
+    };
+    Own Bx;
+    make_Bps(tr, V);
+    for (int i = tr - 1; i >= 0; --i) {
+      make_Bps(i, Bx);
+      E::template rmul<KS>(N, V, Xr, Xi, V, Bx, lane);  // = A3 V + B_i (polynomials in A commute)
+    }
   }
-  get(B1, Ar, Ai);
-  __syncthreads();
-  E::template rmul<KS>(N, W, Br, Bi, V, B1, lane);  // T12 = B1 + (B2 + A6) A6   [product 4]
-  // ---- squarings: ping-pong buffers 3 / 1 (buffer 2 may still be read by product 4), one barrier
-  // each, plus one first: other waves may not have read back their B1 / B2 yet ----
+  // ---- squarings: ping-pong buffers 3 / 1 (buffer 2 may still be read by the last product), one
+  // barrier each, plus one first: other waves may still read buffers 1 / 3 ----
   QOC_STAMP(4);
   if (ts > 0) __syncthreads();
   for (int q = 0; q < ts; ++q) {
@@ -354,6 +463,46 @@ __global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunit
   QOC_STAMP(6);
   QOC_RTSTAMP(61);
   QOC_LIFE(1);
+}
+
+
+// ALG 1 (Taylor), two passes.  Pass 0 (MODE 0): one workgroup per unit; slices with ||A_k||_1 <= 4 theta_12
+// run T12 (+ <= 2 squarings), the others are appended to ps_list.  Pass 1 (MODE 1): one workgroup per
+// listed slice runs Paterson-Stockmeyer (taylor_select).  k_expm_rr_mix does both inline in one pass
+// (T12 reading A2 / A3 back from LDS); the engine launches it when the norms are large anyway
+// (||A_0||_1 > 4 theta_12), saving pass 0's A_k loads and norms on every slice.  Units are either generators
+// (Agen, u) or explicit matrices (Ain).  hist: the Padé (d, s) the reference would select; thist: the
+// executed Taylor (r, s) / T12 s.  KS: k-steps per product (see ExpmRR::rows).
+template <typename T, int NT, int KS>
+__global__ __launch_bounds__(64 * NT, 2) void k_expm_rr(int N, int nu, int nunits, const cx<T>* __restrict__ Agen,
+                                                        const double* __restrict__ u, const cx<T>* __restrict__ Ain,
+                                                        cx<T>* __restrict__ Uout, unsigned long long* __restrict__ hist,
+                                                        unsigned long long* __restrict__ thist, int* __restrict__ ps_list,
+                                                        int* __restrict__ ps_count) {
+  const int unit = blockIdx.x;
+  if (unit >= nunits) return;
+  expm_rr_unit<T, NT, KS, 0>(unit, N, nu, Agen, u, Ain, Uout, hist, thist, ps_list, ps_count);
+}
+template <typename T, int NT, int KS>
+__global__ __launch_bounds__(64 * NT, 2) void k_expm_rr_mix(int N, int nu, int nunits, const cx<T>* __restrict__ Agen,
+                                                            const double* __restrict__ u, const cx<T>* __restrict__ Ain,
+                                                            cx<T>* __restrict__ Uout, unsigned long long* __restrict__ hist,
+                                                            unsigned long long* __restrict__ thist) {
+  const int unit = blockIdx.x;
+  if (unit >= nunits) return;
+  expm_rr_unit<T, NT, KS, 2>(unit, N, nu, Agen, u, Ain, Uout, hist, thist, nullptr, nullptr);
+}
+template <typename T, int NT, int KS>
+__global__ __launch_bounds__(64 * NT, 2) void k_expm_rr_ps(int N, int nu, const cx<T>* __restrict__ Agen,
+                                                           const double* __restrict__ u, const cx<T>* __restrict__ Ain,
+                                                           cx<T>* __restrict__ Uout, unsigned long long* __restrict__ hist,
+                                                           unsigned long long* __restrict__ thist,
+                                                           const int* __restrict__ ps_list, const int* __restrict__ ps_count) {
+  // one workgroup per listed unit (grid = nunits; workgroups past the count exit at once — cheaper than a
+  // persistent loop, which serialises the phases of consecutive units)
+  const int i = blockIdx.x;
+  if (i >= *ps_count) return;
+  expm_rr_unit<T, NT, KS, 1>(ps_list[i], N, nu, Agen, u, Ain, Uout, hist, thist, nullptr, nullptr);
 }
 
 }  // namespace qoc

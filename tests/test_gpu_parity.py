@@ -385,3 +385,32 @@ def test_fused_gradient_equals_per_slice_kernel(built_lib, monkeypatch, which):
     for b in range(u.shape[0]):
         Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
         assert np.linalg.norm(res[0][b] - gr) / np.linalg.norm(gr) <= 1e-10
+
+
+@pytest.mark.parametrize("which", ["two_pass", "mix"])
+def test_t12_and_paterson_stockmeyer_passes(built_lib, which):
+    """Slices with ||A_k||_1 > 4 theta_12 run Paterson-Stockmeyer (fewer squarings than T12): through the
+    second pass over the listed units when ||A0||_1 is small (cavity with a few large controls), or in the
+    one-pass mixed kernel when ||A0||_1 is large (tunable bus).  Both match the oracle; the executed
+    histogram shows which scheme ran."""
+    from qoc_amd import systems
+    if which == "two_pass":
+        prob = systems.cavity_problem(N_cavity=12, Nt=24)
+        u = systems.cavity_controls(3, prob.Nt, seed=21)
+        u[:, :, ::3] *= 60.0  # every third slice: ||A_k||_1 of a few units
+    else:
+        prob = systems.tunable_bus_problem(Nt=200)
+        u = systems.tunable_bus_controls(2, prob.Nt, seed=22)
+    e = _engine(prob, u.shape[0])
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    th = e.taylor_histogram()
+    e.close()
+    t12 = sum(v for (mm, _), v in th.items() if mm == 12)
+    ps = sum(v for (mm, _), v in th.items() if mm != 12)
+    assert t12 + ps == u.shape[0] * prob.Nt
+    assert ps > 0 and (t12 > 0 if which == "two_pass" else t12 == 0)
+    for b in range(u.shape[0]):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        assert abs(J[b] - Jr) <= 1e-12
+        assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10

@@ -7,6 +7,7 @@
 #include <cmath>
 #include "../quantumoptimalcontrol.jl_amd/csrc/qoc_expm_rr.hpp"
 using namespace qoc;
+static int* g_ps = nullptr;  // pass-2 counter + list
 
 template <int NT, int ALG = 0>
 void run(int N, double scale, int units, std::vector<cx<double>>* keep = nullptr) {
@@ -125,8 +126,13 @@ void run_rr(int N, double scale, int units, std::vector<cx<double>>* keep) {
   (void)hipEventCreate(&b);
   for (int it = 0; it < 3; ++it) {
     (void)hipEventRecord(a);
+    if (!g_ps) (void)hipMalloc(&g_ps, (1 << 20) * sizeof(int));
+    (void)hipMemset(g_ps, 0, 4);
     hipLaunchKernelGGL((k_expm_rr<double, NT, (NT == 3 ? 10 : NT == 2 ? 7 : 3)>), dim3(units), dim3(64 * NT), lds, 0, N, 0, units, nullptr, nullptr, dA,
-                       dX, nullptr, nullptr);
+                       dX, nullptr, nullptr, g_ps + 1, g_ps);
+    (void)hipFuncSetAttribute((const void*)k_expm_rr_ps<double, NT, (NT == 3 ? 10 : NT == 2 ? 7 : 3)>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_expm_rr_ps<double, NT, (NT == 3 ? 10 : NT == 2 ? 7 : 3)>), dim3(units), dim3(64 * NT), lds, 0, N, 0, nullptr, nullptr, dA,
+                       dX, nullptr, nullptr, g_ps + 1, g_ps);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
   }
@@ -142,9 +148,8 @@ void run_rr(int N, double scale, int units, std::vector<cx<double>>* keep) {
   {
     unsigned long long st[64];
     (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_probe), sizeof(st));
-    printf("   load A %llu  norm %llu  A2+A3 %llu  Horner %llu  squarings %llu  store %llu\n", st[1] - st[0], st[2] - st[1],
+    printf("   load A %llu  norm %llu  A2+A3 %llu  B's+products 3,4 %llu  squarings %llu  store %llu\n", st[1] - st[0], st[2] - st[1],
            st[3] - st[2], st[4] - st[3], st[5] - st[4], st[6] - st[5]);
-    printf("   one Horner step: make_B %llu  rmul %llu\n", st[8] - st[7], st[9] - st[8]);
     if (units <= 65536) {
       std::vector<unsigned long long> L(3 * (size_t)units);
       (void)hipMemcpyFromSymbol(L.data(), HIP_SYMBOL(g_life), L.size() * 8);

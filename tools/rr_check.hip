@@ -7,6 +7,7 @@
 #include <complex>
 #include "../quantumoptimalcontrol.jl_amd/csrc/qoc_expm_rr.hpp"
 using namespace qoc;
+static int* g_ps = nullptr;  // pass-2 counter + list
 typedef std::complex<double> C;
 static std::vector<C> expm_ref(const std::vector<C>& A, int N) {
   // scaling and squaring with a long Taylor series (reference quality for ||A|| ~ 1)
@@ -44,7 +45,11 @@ void check(int N, double scale, int units) {
   (void)hipMemset(dX, 0xff, A.size() * sizeof(cx<T>));
   const size_t lds = ExpmRR<T, NT>::lds_bytes(N);
   (void)hipFuncSetAttribute((const void*)k_expm_rr<T, NT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((k_expm_rr<T, NT, KS>), dim3(units), dim3(64 * NT), lds, 0, N, 0, units, nullptr, nullptr, dA, dX, nullptr, nullptr);
+  if (!g_ps) (void)hipMalloc(&g_ps, (1 << 20) * sizeof(int));
+    (void)hipMemset(g_ps, 0, 4);
+    hipLaunchKernelGGL((k_expm_rr<T, NT, KS>), dim3(units), dim3(64 * NT), lds, 0, N, 0, units, nullptr, nullptr, dA, dX, nullptr, nullptr, g_ps + 1, g_ps);
+    (void)hipFuncSetAttribute((const void*)k_expm_rr_ps<T, NT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_expm_rr_ps<T, NT, KS>), dim3(units), dim3(64 * NT), lds, 0, N, 0, nullptr, nullptr, dA, dX, nullptr, nullptr, g_ps + 1, g_ps);
   hipError_t e = hipDeviceSynchronize();
   std::vector<cx<T>> X(A.size());
   (void)hipMemcpy(X.data(), dX, X.size() * sizeof(cx<T>), hipMemcpyDeviceToHost);
