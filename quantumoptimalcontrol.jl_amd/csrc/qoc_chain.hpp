@@ -18,8 +18,8 @@
 
 namespace qoc {
 
-constexpr int CHAIN_THREADS = 256;
-// U elements prefetched per thread: N*N <= 256*PREF (fp32 N <= 64; fp64 N <= 45, which covers the
+constexpr int CHAIN_THREADS = 256;  // (512 measured slower: more shuffle/barrier work per serial step)
+// U elements prefetched per thread: N*N <= CHAIN_THREADS*PREF (fp32 N <= 64; fp64 N <= 45, which covers the
 // fp64 k_expm envelope N <= 44).  Larger fp64 arrays were not promoted to registers (scratch).
 template <typename T>
 struct ChainPref {
@@ -174,45 +174,46 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
     Xb[o] = v;
     if (pmask && pmask[o]) pen += (double)v.r * v.r + (double)v.i * v.i;
   }
-  // U_k is double-buffered in LDS; the HBM loads run two slices ahead in registers (preA/preB).
-  UPref<T> preA, preB;
-  prefetch_u(Ub, NN, preA);
-  commit_u(ub, N, preA);
-  if (Nt > 1) prefetch_u(Ub + NN, NN, preA);
-  if (Nt > 2) prefetch_u(Ub + 2 * (size_t)NN, NN, preB);
+  // U_k is double-buffered in LDS; the HBM loads run CHAIN_AHEAD slices ahead in registers (one
+  // workgroup per CU: the register file has room, and the chain is bound by HBM latency per step).
+  // Step k commits U_{k+1} from Q[k & 3] and refills that set with U_{k+5}; the loop is unrolled by 4 so
+  // the register sets (and the vmcnt waits) are compile-time.
+  UPref<T> Q0, Q1, Q2, Q3;
+  prefetch_u(Ub, NN, Q0);
+  commit_u(ub, N, Q0);
+  if (Nt > 1) prefetch_u(Ub + (size_t)1 * NN, NN, Q0);
+  if (Nt > 2) prefetch_u(Ub + (size_t)2 * NN, NN, Q1);
+  if (Nt > 3) prefetch_u(Ub + (size_t)3 * NN, NN, Q2);
+  if (Nt > 4) prefetch_u(Ub + (size_t)4 * NN, NN, Q3);
   __syncthreads();
-#define QOC_FWD_STEP(KK, PNEXT)                                                    \
-  do {                                                                             \
-    const int k_ = (KK);                                                           \
-    if (k_ == 500) QOC_STAMP(50);                                                  \
-    const cx<T>* cur = ub + (k_ & 1) * LDU;                                        \
-    const cx<T>* xc = xb + (k_ & 1) * Nm;                                          \
-    cx<T>* xn = xb + ((k_ + 1) & 1) * Nm;                                          \
-    cx<T>* Xk = Xb + (size_t)(k_ + 1) * Nm;                                        \
-    for (int o = o0; o < Nm; o += ostride) {                                       \
-      const int i = o % N, c = o / N;                                              \
-      const cx<T> y = chain_dot<T, false>(cur, xc + N * c, N, i, part, S);         \
-      if (part == 0) {                                                             \
-        xn[o] = y;                                                                 \
-        Xk[o] = y;                                                                 \
-        if (pmask && pmask[o]) pen += (double)y.r * y.r + (double)y.i * y.i;       \
-      }                                                                            \
-    }                                                                              \
-    if (k_ == 500) QOC_STAMP(51);                                                  \
-    if (k_ + 1 < Nt) commit_u(ub + ((k_ + 1) & 1) * LDU, N, PNEXT);                \
-    if (k_ == 500) QOC_STAMP(52);                                                  \
-    if (k_ + 3 < Nt) prefetch_u(Ub + (size_t)(k_ + 3) * NN, NN, PNEXT);            \
-    if (k_ == 500) QOC_STAMP(53);                                                  \
-    lds_barrier();                                                                 \
-    if (k_ == 500) QOC_STAMP(54);                                                  \
-  } while (0)
+  auto fwd_step = [&](int k_, UPref<T>& PN) __attribute__((always_inline)) {
+    const cx<T>* cur = ub + (k_ & 1) * LDU;
+    const cx<T>* xc = xb + (k_ & 1) * Nm;
+    cx<T>* xn = xb + ((k_ + 1) & 1) * Nm;
+    cx<T>* Xk = Xb + (size_t)(k_ + 1) * Nm;
+    for (int o = o0; o < Nm; o += ostride) {
+      const int i = o % N, c = o / N;
+      const cx<T> y = chain_dot<T, false>(cur, xc + N * c, N, i, part, S);
+      if (part == 0) {
+        xn[o] = y;
+        Xk[o] = y;
+        if (pmask && pmask[o]) pen += (double)y.r * y.r + (double)y.i * y.i;
+      }
+    }
+    if (k_ + 1 < Nt) commit_u(ub + ((k_ + 1) & 1) * LDU, N, PN);  // U_{k+1}
+    if (k_ + 5 < Nt) prefetch_u(Ub + (size_t)(k_ + 5) * NN, NN, PN);
+    lds_barrier();
+  };
   int k = 0;
-  for (; k + 1 < Nt; k += 2) {
-    QOC_FWD_STEP(k, preA);
-    QOC_FWD_STEP(k + 1, preB);
+  for (; k + 3 < Nt; k += 4) {
+    fwd_step(k, Q0);
+    fwd_step(k + 1, Q1);
+    fwd_step(k + 2, Q2);
+    fwd_step(k + 3, Q3);
   }
-  if (k < Nt) QOC_FWD_STEP(k, preA);
-#undef QOC_FWD_STEP
+  if (k < Nt) fwd_step(k, Q0);
+  if (k + 1 < Nt) fwd_step(k + 1, Q1);
+  if (k + 2 < Nt) fwd_step(k + 2, Q2);
   const cx<T>* xN = xb + (Nt & 1) * Nm;
   // ---- costs on x_N ----
   const double psum = block_sum(pen, red) * mu;
@@ -300,43 +301,50 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
     l0[o] = v;
     Lb[(size_t)Nt * Nm + o] = v;
   }
-  UPref<T> preA, preB;
-  prefetch_u(Ub + (size_t)(Nt - 1) * NN, NN, preA);
-  commit_u(ub + ((Nt - 1) & 1) * LDU, N, preA);
-  if (Nt > 1) prefetch_u(Ub + (size_t)(Nt - 2) * NN, NN, preA);
-  if (Nt > 2) prefetch_u(Ub + (size_t)(Nt - 3) * NN, NN, preB);
-  __syncthreads();
-#define QOC_BWD_STEP(KK, PNEXT)                                                    \
-  do {                                                                             \
-    const int k_ = (KK);                                                           \
-    const cx<T>* cur = ub + (k_ & 1) * LDU;                                        \
-    const cx<T>* lc = lb + ((k_ + 1) & 1) * Nm;                                    \
-    cx<T>* ln = lb + (k_ & 1) * Nm;                                                \
-    cx<T>* Lk = Lb + (size_t)k_ * Nm;                                              \
-    for (int o = o0; o < Nm; o += ostride) {                                       \
-      const int i = o % N, c = o / N;                                              \
-      cx<T> y = chain_dot<T, true>(cur, lc + N * c, N, i, part, S);                \
-      if (part == 0) {                                                             \
-        if (pmask && pmask[o]) {                                                   \
-          const cx<T> xv = Xb[(size_t)k_ * Nm + o];                                \
-          y.r += tmu * xv.r;                                                       \
-          y.i += tmu * xv.i;                                                       \
-        }                                                                          \
-        ln[o] = y;                                                                 \
-        Lk[o] = y;                                                                 \
-      }                                                                            \
-    }                                                                              \
-    if (k_ > 0) commit_u(ub + ((k_ - 1) & 1) * LDU, N, PNEXT);                     \
-    if (k_ >= 3) prefetch_u(Ub + (size_t)(k_ - 3) * NN, NN, PNEXT);                \
-    lds_barrier();                                                                 \
-  } while (0)
-  int k = Nt - 1;
-  for (; k >= 1; k -= 2) {
-    QOC_BWD_STEP(k, preA);
-    QOC_BWD_STEP(k - 1, preB);
+  // Step i (k = Nt-1-i) commits U_{k-1} from Q[i & 3] and refills that set with U_{k-5}; unrolled by 4.
+  UPref<T> Q0, Q1, Q2, Q3;
+  {
+    UPref<T> P;
+    prefetch_u(Ub + (size_t)(Nt - 1) * NN, NN, P);
+    commit_u(ub + ((Nt - 1) & 1) * LDU, N, P);
   }
-  if (k == 0) QOC_BWD_STEP(0, preA);
-#undef QOC_BWD_STEP
+  if (Nt > 1) prefetch_u(Ub + (size_t)(Nt - 2) * NN, NN, Q0);
+  if (Nt > 2) prefetch_u(Ub + (size_t)(Nt - 3) * NN, NN, Q1);
+  if (Nt > 3) prefetch_u(Ub + (size_t)(Nt - 4) * NN, NN, Q2);
+  if (Nt > 4) prefetch_u(Ub + (size_t)(Nt - 5) * NN, NN, Q3);
+  __syncthreads();
+  auto bwd_step = [&](int k_, UPref<T>& PN) __attribute__((always_inline)) {
+    const cx<T>* cur = ub + (k_ & 1) * LDU;
+    const cx<T>* lc = lb + ((k_ + 1) & 1) * Nm;
+    cx<T>* ln = lb + (k_ & 1) * Nm;
+    cx<T>* Lk = Lb + (size_t)k_ * Nm;
+    for (int o = o0; o < Nm; o += ostride) {
+      const int i = o % N, c = o / N;
+      cx<T> y = chain_dot<T, true>(cur, lc + N * c, N, i, part, S);
+      if (part == 0) {
+        if (pmask && pmask[o]) {
+          const cx<T> xv = Xb[(size_t)k_ * Nm + o];
+          y.r += tmu * xv.r;
+          y.i += tmu * xv.i;
+        }
+        ln[o] = y;
+        Lk[o] = y;
+      }
+    }
+    if (k_ > 0) commit_u(ub + ((k_ - 1) & 1) * LDU, N, PN);      // U_{k-1}
+    if (k_ >= 5) prefetch_u(Ub + (size_t)(k_ - 5) * NN, NN, PN);  // U_{k-5}: consumed 4 steps later
+    lds_barrier();
+  };
+  int i = 0;
+  for (; i + 3 < Nt; i += 4) {
+    bwd_step(Nt - 1 - i, Q0);
+    bwd_step(Nt - 2 - i, Q1);
+    bwd_step(Nt - 3 - i, Q2);
+    bwd_step(Nt - 4 - i, Q3);
+  }
+  if (i < Nt) bwd_step(Nt - 1 - i, Q0);
+  if (i + 1 < Nt) bwd_step(Nt - 2 - i, Q1);
+  if (i + 2 < Nt) bwd_step(Nt - 3 - i, Q2);
 }
 
 // ---------------------------------------------------------------------------

@@ -1104,7 +1104,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   if (precision != QOC_FP64 && precision != QOC_FP32) return fail(nullptr, QOC_ERR_ARG, "invalid precision");
   // LDS-resident kernels when the problem fits them, the chunked GEMM pipeline otherwise
   const bool small = expm_supported(N, precision) && N <= kChainMaxN &&
-                     N * N <= CHAIN_THREADS * (precision == QOC_FP64 ? 8 : 16) && N * m <= 4 * CHAIN_THREADS;
+                     N * N <= CHAIN_THREADS * (precision == QOC_FP64 ? ChainPref<double>::value : ChainPref<float>::value) && N * m <= 4 * CHAIN_THREADS;
   const bool force_big = getenv("QOC_FORCE_LARGE_N") && atoi(getenv("QOC_FORCE_LARGE_N")) != 0;
   if ((!small || force_big) && nu > 8)
     return fail(nullptr, QOC_ERR_UNSUPPORTED, "large-N path supports nu <= 8 (got %d)", nu);
