@@ -338,20 +338,27 @@ __device__ __forceinline__ void expm_rr_unit(int unit, int N, int nu, const cx<T
     make_B(kT12[2], B3);
     Own B1;
     make_B(kT12[0], B1);
+    QOC_STAMP(10);
     __syncthreads();                                    // A (buffer 1) readers done, buffer 2 = B4 complete
+    QOC_STAMP(11);
     E::store_own(N, B1, Ar, Ai, row, lane);             // B1 -> buffer 1 (own positions)
     E::template rmul<KS>(N, B4, Br, Bi, V, B3, lane);  // A6 = B3 + B4 B4   [product 3]
-    __syncthreads();                                    // buffer 2 (B4) readers are done
-    E::store_own(N, V, Br, Bi, row, lane);              // A6 -> buffer 2
+    QOC_STAMP(12);
+    // A6 -> buffer 3 over this wave's B2 rows (read back first; other waves only touch their own rows
+    // of buffer 3 until the barrier), so buffer 2 (B4, still read by product 3 elsewhere) stays intact
     get(W, Xr, Xi);                                     // B2
+    E::store_own(N, V, Xr, Xi, row, lane);              // A6 -> buffer 3
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       W.r[t] += V.r[t];
       W.i[t] += V.i[t];
     }
     get(B1, Ar, Ai);
-    __syncthreads();
-    E::template rmul<KS>(N, W, Br, Bi, V, B1, lane);  // T12 = B1 + (B2 + A6) A6   [product 4]
+    QOC_STAMP(14);
+    __syncthreads();                                    // buffer 3 = A6 complete
+    QOC_STAMP(15);
+    E::template rmul<KS>(N, W, Xr, Xi, V, B1, lane);  // T12 = B1 + (B2 + A6) A6   [product 4]
+    QOC_STAMP(16);
   } else if (MODE == 2 && !tr) {
     // ---- T12 with A2 / A3 read back from LDS: one pass over the owned positions, B4 -> buffer 2 and
     // B2 -> buffer 3 in place of this lane's A2 / A3, B3 and B1 in registers ----
@@ -436,8 +443,9 @@ __device__ __forceinline__ void expm_rr_unit(int unit, int N, int nu, const cx<T
       E::template rmul<KS>(N, V, Xr, Xi, V, Bx, lane);  // = A3 V + B_i (polynomials in A commute)
     }
   }
-  // ---- squarings: ping-pong buffers 3 / 1 (buffer 2 may still be read by the last product), one
-  // barrier each, plus one first: other waves may still read buffers 1 / 3 ----
+  // ---- squarings: ping-pong buffers 3 / 1, one barrier each, plus one first (the last product may still
+  // be reading buffer 3 in other waves) ----
+
   QOC_STAMP(4);
   if (ts > 0) __syncthreads();
   for (int q = 0; q < ts; ++q) {

@@ -150,6 +150,9 @@ void run_rr(int N, double scale, int units, std::vector<cx<double>>* keep) {
     (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_probe), sizeof(st));
     printf("   load A %llu  norm %llu  A2+A3 %llu  B's+products 3,4 %llu  squarings %llu  store %llu\n", st[1] - st[0], st[2] - st[1],
            st[3] - st[2], st[4] - st[3], st[5] - st[4], st[6] - st[5]);
+    if (st[16])
+      printf("   T12: make_B x4 %llu  bar %llu  B1 store + P3 %llu  A6 store + gets %llu  bar %llu  P4 %llu\n",
+             st[10] - st[3], st[11] - st[10], st[12] - st[11], st[14] - st[12], st[15] - st[14], st[16] - st[15]);
     if (units <= 65536) {
       std::vector<unsigned long long> L(3 * (size_t)units);
       (void)hipMemcpyFromSymbol(L.data(), HIP_SYMBOL(g_life), L.size() * 8);
