@@ -9,22 +9,44 @@
 //                 contracted through matrix-vector products instead of forming dU_j:
 //                   λ^† X^b A_j X^a x = <(X^†)^b λ, A_j X^a x>,  coefficient 1/(a+b+1)!.
 //
-// One workgroup per seed for the chains (the time axis is a serial recurrence);
-// U_k is staged through double-buffered LDS with the next slice prefetched into
-// registers while the current matvec runs.
+// One workgroup per seed for the chains (the time axis is a serial recurrence); each thread keeps
+// its slice of U_k .. U_{k+3} in registers (no LDS staging of U), the state goes through LDS.
 #pragma once
 #include "qoc_common.hpp"
 #include "qoc_expm.hpp"  // QOC_STAMP (diagnostic builds only)
 
 namespace qoc {
 
-constexpr int CHAIN_THREADS = 256;  // (512 measured slower: more shuffle/barrier work per serial step)
-// U elements prefetched per thread: N*N <= CHAIN_THREADS*PREF (fp32 N <= 64; fp64 N <= 45, which covers the
-// fp64 k_expm envelope N <= 44).  Larger fp64 arrays were not promoted to registers (scratch).
-template <typename T>
-struct ChainPref {
-  static constexpr int value = sizeof(T) == 8 ? 8 : 16;
+constexpr int CHAIN_THREADS = 256;
+
+// Chain thread layout (ChainRegs): a thread owns output row i and part p of the inner index, j = p + S q
+// (q < JT), of row i of U_k (forward) or of column i (backward, U^H).  Its JT elements of the next D slices
+// U_k .. U_{k+D-1} stay in registers (D rotating sets, the HBM loads D steps ahead), so U never goes through
+// LDS; only the N x m state does (broadcast reads).  The S partial sums of a row are reduced in registers
+// (DPP / row swaps).  Host-side selection: chain_shape().
+struct ChainShape {
+  int S, JT, CB;
 };
+// Waves split the work as G row blocks (64 / S rows each) x CGN column groups (G = 1: 4 groups, G = 2: 2,
+// else 1; waves beyond G x CGN only copy the state out).  CB: state columns per matvec pass of one wave
+// (their latencies interleave), 4 when a wave has >= 4 columns and the shape leaves registers for them.
+__host__ __device__ inline int chain_groups(int N, int S) {
+  const int G = (N + 64 / S - 1) / (64 / S);
+  return G == 1 ? 4 : G == 2 ? 2 : 1;
+}
+__host__ __device__ inline ChainShape chain_shape(int N, int m, bool fp64) {
+  const int S = N <= 16 ? 4 : N <= 32 ? 8 : 4;
+  const int cpw = (m + chain_groups(N, S) - 1) / chain_groups(N, S);  // columns per wave
+  const int cb = cpw >= 4 ? 4 : 1;
+  if (N <= 32) return {S, 4, cb};
+  const int J = (N + 3) / 4;
+  return {4, J <= 10 ? 10 : J <= 12 ? 12 : (fp64 ? 0 : 16), 1};  // JT 0: outside the register envelope
+}
+// Largest N the register-resident chains take (fp64: 12 complex per set, fp32: 16).
+template <typename T>
+constexpr int chain_max_n() {
+  return sizeof(T) == 8 ? 48 : 64;
+}
 
 enum { COST_TRACE = 0, COST_ZCAL = 1, COST_EXTERNAL = 2 };
 
@@ -84,143 +106,262 @@ __device__ inline void optimal_calibration(const cx<double> m[4], double tol, do
   *th1 = pm + al * xm;
 }
 
-// Cooperative copy of an N x N column-major complex matrix into LDS with leading dimension N+1,
-// staged through registers (separate re/im scalars, unconditional clamped loads: a conditionally
-// written array of 16-byte structs was demoted to scratch by the compiler).
-template <typename T>
-struct UPref {
-  T r[ChainPref<T>::value], i[ChainPref<T>::value];
+// Sum over the S adjacent lanes of one row's parts (DPP within a 16-lane row); result in every lane.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)u, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int S, typename T>
+__device__ __forceinline__ T part_sum(T v) {
+  if (S > 1) v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (S > 2) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (S > 4) v += dpp_mov<0x141>(v);  // row_half_mirror
+  if (S > 8) v += dpp_mov<0x140>(v);  // row_mirror
+  return v;
+}
+
+// v(l) + v(l ^ W) for W = 16 / 32 with the gfx950 row / half swaps (v_permlane16/32_swap: exchanging a
+// register with itself leaves the two halves of the pair in the two results).
+template <int W>
+__device__ __forceinline__ unsigned swap_pair_sum_u(unsigned v, unsigned& other) {
+  const auto r = W == 16 ? __builtin_amdgcn_permlane16_swap(v, v, false, false)
+                         : __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  other = r[1];
+  return r[0];
+}
+template <int W>
+__device__ __forceinline__ float swap_sum(float v) {
+  unsigned o;
+  const unsigned a = swap_pair_sum_u<W>(__float_as_uint(v), o);
+  return __uint_as_float(a) + __uint_as_float(o);
+}
+template <int W>
+__device__ __forceinline__ double swap_sum(double v) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  unsigned olo, ohi;
+  const unsigned lo = swap_pair_sum_u<W>((unsigned)u, olo);
+  const unsigned hi = swap_pair_sum_u<W>((unsigned)(u >> 32), ohi);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo)) +
+         __longlong_as_double((long long)(((unsigned long long)ohi << 32) | olo));
+}
+
+// One thread's JT elements of a propagator (the four prefetch sets rotate through these).
+template <typename T, int JT>
+struct USet {
+  T r[JT], i[JT];
 };
-template <typename T>
-__device__ __forceinline__ void prefetch_u(const cx<T>* __restrict__ src, int NN, UPref<T>& pre) {
-#pragma unroll
-  for (int r = 0; r < ChainPref<T>::value; ++r) {
-    const int e = min((int)threadIdx.x + CHAIN_THREADS * r, NN - 1);
-    const cx<T> v = src[e];
-    pre.r[r] = v.r;
-    pre.i[r] = v.i;
-  }
-}
-template <typename T>
-__device__ __forceinline__ void commit_u(cx<T>* __restrict__ dst, int N, const UPref<T>& pre) {
-  const int NN = N * N;
-#pragma unroll
-  for (int r = 0; r < ChainPref<T>::value; ++r) {
-    const int e = threadIdx.x + CHAIN_THREADS * r;
-    if (e < NN) {
-      const int j = e / N, i = e - j * N;
-      dst[i + (N + 1) * j] = cx<T>{pre.r[r], pre.i[r]};
-    }
-  }
-}
 
-// Lanes cooperating on one output of the matvec: largest power of two S with S * Nm <= 256
-// (adjacent lanes of one wave, reduced with shuffles).
-__device__ __forceinline__ int chain_split(int Nm) {
-  int S = 1;
-  while (S < 8 && 2 * S * Nm <= CHAIN_THREADS) S <<= 1;
-  return S;
-}
+// Padded column count of the LDS state (a multiple of the column block CB).
+__host__ __device__ constexpr int chain_mpad(int m, int CB) { return (m + CB - 1) / CB * CB; }
 
-// y[i,c] = sum_j M(i,j) v[j,c] for this thread's (output, part); CONJT selects M = U^H.
-template <typename T, bool CONJT>
-__device__ __forceinline__ cx<T> chain_dot(const cx<T>* __restrict__ Um, const cx<T>* __restrict__ v, int N, int i,
-                                           int part, int S) {
-  cx<T> a0 = {0, 0}, a1 = {0, 0}, a2 = {0, 0}, a3 = {0, 0};
-  const int LD = N + 1;
-  int j = part;
-  for (; j + 3 * S < N; j += 4 * S) {
-    if (CONJT) {
-      a0 = cfmaconj(a0, Um[j + LD * i], v[j]);
-      a1 = cfmaconj(a1, Um[j + S + LD * i], v[j + S]);
-      a2 = cfmaconj(a2, Um[j + 2 * S + LD * i], v[j + 2 * S]);
-      a3 = cfmaconj(a3, Um[j + 3 * S + LD * i], v[j + 3 * S]);
+// Chain state in LDS: column c of x at xs + XS * c (c < chain_mpad(m)), XS = S * JT >= N, rows >= N and
+// columns >= m held at zero so that the clamped (finite) U elements of padded columns contribute nothing.
+// ROWFAST (forward): lane l of wave w owns row i = w R + l % R (R = 64 / S) and part p = l / R, so that one
+// load instruction reads R consecutive rows of a column of U (coalesced); the parts are reduced with lane
+// shuffles.  Otherwise (backward, U^H = columns of U): i = tid / S, p = tid % S, consecutive lanes read
+// consecutive elements of a column; the parts are adjacent lanes (DPP).
+template <typename T, int S, int JT, int CB, bool ROWFAST>
+struct ChainRegs {
+  static constexpr int XS = S * JT;
+  // prefetch depth: slices of U in flight per thread (register sets, <= 128-160 VGPRs in all, so that the
+  // small shapes still fit two workgroups per CU); their steps are short and need more sets in flight
+  static constexpr int RPS = JT * 2 * (int)sizeof(T) / 4;  // VGPRs per set
+  static constexpr int D = RPS <= 16 ? (128 / RPS > 16 ? 16 : 128 / RPS) : 160 / RPS;
+  static constexpr int R = 64 / S;  // rows per wave
+  int i, p;
+  bool act;         // owns a valid row (of a computing wave)
+  bool busy;        // this wave computes (else its U loads all hit one address)
+  int c_begin, c_step;  // this wave's columns: c_begin + c_step t (+ CB block)
+  __device__ __forceinline__ void setup(int N) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int G = (N + R - 1) / R, CGN = chain_groups(N, S);
+    const int rb = w % G, cg = w / G;
+    if (ROWFAST) {
+      i = rb * R + l % R;
+      p = l / R;
     } else {
-      a0 = cfma(a0, Um[i + LD * j], v[j]);
-      a1 = cfma(a1, Um[i + LD * (j + S)], v[j + S]);
-      a2 = cfma(a2, Um[i + LD * (j + 2 * S)], v[j + 2 * S]);
-      a3 = cfma(a3, Um[i + LD * (j + 3 * S)], v[j + 3 * S]);
+      i = rb * R + l / S;
+      p = l % S;
+    }
+    busy = w < G * CGN;
+    act = busy && i < N;
+    c_begin = w < G * CGN ? cg * CB : 1 << 30;
+    c_step = CGN * CB;
+  }
+  __device__ __forceinline__ T psum(T v) const {
+    if (ROWFAST) {  // parts at lane offsets R, 2R, ..: rotate within 16-lane rows, then swap rows / halves
+      if (R <= 8) v += dpp_mov<0x128>(v);  // row_ror:8
+      if (R <= 4) v += dpp_mov<0x124>(v);  // row_ror:4
+      return swap_sum<32>(swap_sum<16>(v));
+    }
+    return part_sum<S>(v);
+  }
+  // U[row, col] offsets: forward reads row i (U[i + N j]); backward reads column i (U[j + N i]).
+  __device__ __forceinline__ int off(int N, int q, bool conj_t) const {
+    const int ic = min(i, N - 1), j = min(p + S * q, N - 1);
+    return busy ? (conj_t ? j + N * ic : ic + N * j) : 0;
+  }
+  __device__ __forceinline__ void load(const cx<T>* __restrict__ Uk, int N, bool conj_t, USet<T, JT>& Q) const {
+#pragma unroll
+    for (int q = 0; q < JT; ++q) {
+      const cx<T> v = Uk[off(N, q, conj_t)];
+      Q.r[q] = v.r;
+      Q.i[q] = v.i;
     }
   }
-  for (; j < N; j += S) a0 = CONJT ? cfmaconj(a0, Um[j + LD * i], v[j]) : cfma(a0, Um[i + LD * j], v[j]);
-  a0.r += a1.r + a2.r + a3.r;
-  a0.i += a1.i + a2.i + a3.i;
-  for (int off = 1; off < S; off <<= 1) {
-    a0.r += __shfl_xor(a0.r, off);
-    a0.i += __shfl_xor(a0.i, off);
+  // State copy-out slots: the waves outside the G x CGN computing ones when there are any (and they suffice),
+  // else all threads; slot r of a thread is state element xo[r] (-1: none) at LDS index xi[r] of the padded
+  // layout, with its state-penalty mask bit (read once, up front).
+  int xi[4], xo[4];
+  bool pm[4];
+  __device__ __forceinline__ void setup_slots(int N, int m, const unsigned char* __restrict__ pmask) {
+    const int G = (N + R - 1) / R, busy = 64 * G * chain_groups(N, S);
+    const int base = busy < CHAIN_THREADS && N * m <= 4 * (CHAIN_THREADS - busy) ? busy : 0;
+    const int nthr = CHAIN_THREADS - base;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = (int)threadIdx.x - base + nthr * r;
+      const bool ok = (int)threadIdx.x >= base && o < N * m;
+      xo[r] = ok ? o : -1;
+      xi[r] = ok ? XS * (o / N) + o % N : 0;
+      pm[r] = ok && pmask && pmask[o];
+    }
   }
-  return a0;
-}
+  // Wait for set Q here, in straight-line code: redefining the registers through an opaque asm leaves no
+  // load pending on them inside the (runtime) column loop, where the waitcnt pass would otherwise drain
+  // every outstanding prefetch (vmcnt(0)) at each use.
+  __device__ __forceinline__ void settle(USet<T, JT>& Q) const {
+#pragma unroll
+    for (int q = 0; q < JT; ++q) asm volatile("" : "+v"(Q.r[q]), "+v"(Q.i[q]));
+  }
+  // y[b] = sum_q op(U)[i, p + S q] x[p + S q, c0 + b] over the S parts, b < CB; op = identity or
+  // conjugate (U^H read by columns).  All LDS reads are issued before the first FMA.
+  template <bool CONJ>
+  __device__ __forceinline__ void dot(const USet<T, JT>& Q, const cx<T>* __restrict__ xs, int c0, cx<T> (&y)[CB]) const {
+    cx<T> xv[CB][JT];
+#pragma unroll
+    for (int b = 0; b < CB; ++b)
+#pragma unroll
+      for (int q = 0; q < JT; ++q) xv[b][q] = xs[XS * (c0 + b) + p + S * q];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < CB; ++b) {
+      T ar0 = 0, ai0 = 0, ar1 = 0, ai1 = 0;
+#pragma unroll
+      for (int q = 0; q < JT; ++q) {  // 4 accumulating FMAs per complex term (no separate products)
+        const cx<T> x = xv[b][q];
+        T& ar = (q & 1) ? ar1 : ar0;
+        T& ai = (q & 1) ? ai1 : ai0;
+        ar = fma(Q.r[q], x.r, ar);
+        ai = fma(Q.r[q], x.i, ai);
+        if (CONJ) {  // conj(u) x
+          ar = fma(Q.i[q], x.i, ar);
+          ai = fma(-Q.i[q], x.r, ai);
+        } else {
+          ar = fma(-Q.i[q], x.i, ar);
+          ai = fma(Q.i[q], x.r, ai);
+        }
+      }
+      y[b] = cx<T>{ar0 + ar1, ai0 + ai1};
+    }
+#pragma unroll
+    for (int b = 0; b < CB; ++b) {
+      y[b].r = psum(y[b].r);
+      y[b].i = psum(y[b].i);
+    }
+  }
+};
 
-template <typename T>
+template <typename T, int S, int JT, int CB>
 __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
     int N, int m, int Nt, const cx<T>* __restrict__ U, const cx<T>* __restrict__ x0, int x0_per_seed,
     cx<T>* __restrict__ X, const cx<T>* __restrict__ Xt, int cost_kind, double n_norm,
     const unsigned char* __restrict__ pmask, double mu, double* __restrict__ Jout, cx<double>* __restrict__ coef) {
+  using R = ChainRegs<T, S, JT, CB, true>;
+  constexpr int XS = R::XS, D = R::D;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int NN = N * N, Nm = N * m, LDU = N * (N + 1);
-  cx<T>* ub = reinterpret_cast<cx<T>*>(smem);  // 2 x N(N+1)
-  cx<T>* xb = ub + 2 * LDU;                     // 2 x N*m
-  double* red = reinterpret_cast<double*>(xb + 2 * Nm);
+  const int NN = N * N, Nm = N * m, XB = XS * chain_mpad(m, CB);
+  cx<T>* xb = reinterpret_cast<cx<T>*>(smem);  // 2 x m columns of XS (zero-padded)
+  double* red = reinterpret_cast<double*>(xb + 2 * XB);
   const cx<T>* Ub = U + (size_t)b * Nt * NN;
   cx<T>* Xb = X + (size_t)b * (Nt + 1) * Nm;
   const cx<T>* x0b = x0 + (x0_per_seed ? (size_t)b * Nm : 0);
-  const int S = chain_split(Nm), part = tid % S, o0 = tid / S, ostride = CHAIN_THREADS / S;
-  double pen = 0.0;
-  for (int o = tid; o < Nm; o += CHAIN_THREADS) {
-    const cx<T> v = x0b[o];
-    xb[o] = v;
-    Xb[o] = v;
-    if (pmask && pmask[o]) pen += (double)v.r * v.r + (double)v.i * v.i;
+  R rg;
+  rg.setup(N);
+  // U_0..U_3 in flight before anything else
+  USet<T, JT> Q[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) rg.load(Ub + (size_t)min(d, Nt - 1) * NN, N, false, Q[d]);
+  rg.setup_slots(N, m, pmask);
+  for (int e = tid; e < 2 * XB; e += CHAIN_THREADS) {
+    const int c = (e % XB) / XS, r = e % XS;
+    xb[e] = e < XB && r < N && c < m ? x0b[r + N * c] : cx<T>{0, 0};
   }
-  // U_k is double-buffered in LDS; the HBM loads run CHAIN_AHEAD slices ahead in registers (one
-  // workgroup per CU: the register file has room, and the chain is bound by HBM latency per step).
-  // Step k commits U_{k+1} from Q[k & 3] and refills that set with U_{k+5}; the loop is unrolled by 4 so
-  // the register sets (and the vmcnt waits) are compile-time.
-  UPref<T> Q0, Q1, Q2, Q3;
-  prefetch_u(Ub, NN, Q0);
-  commit_u(ub, N, Q0);
-  if (Nt > 1) prefetch_u(Ub + (size_t)1 * NN, NN, Q0);
-  if (Nt > 2) prefetch_u(Ub + (size_t)2 * NN, NN, Q1);
-  if (Nt > 3) prefetch_u(Ub + (size_t)3 * NN, NN, Q2);
-  if (Nt > 4) prefetch_u(Ub + (size_t)4 * NN, NN, Q3);
   __syncthreads();
-  auto fwd_step = [&](int k_, UPref<T>& PN) __attribute__((always_inline)) {
-    const cx<T>* cur = ub + (k_ & 1) * LDU;
-    const cx<T>* xc = xb + (k_ & 1) * Nm;
-    cx<T>* xn = xb + ((k_ + 1) & 1) * Nm;
-    cx<T>* Xk = Xb + (size_t)(k_ + 1) * Nm;
-    for (int o = o0; o < Nm; o += ostride) {
-      const int i = o % N, c = o / N;
-      const cx<T> y = chain_dot<T, false>(cur, xc + N * c, N, i, part, S);
-      if (part == 0) {
-        xn[o] = y;
-        Xk[o] = y;
-        if (pmask && pmask[o]) pen += (double)y.r * y.r + (double)y.i * y.i;
+  // x_k -> HBM (and its state penalty) from the LDS copy, in straight-line code: no global memory
+  // operation sits inside the runtime column loop below (see settle()).
+  double pen = 0.0;
+  auto copy_out = [&](const cx<T>* xs, int k_) __attribute__((always_inline)) {
+    cx<T>* Xk = Xb + (size_t)k_ * Nm;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (rg.xo[r] >= 0) {
+        const cx<T> v = xs[rg.xi[r]];
+        Xk[rg.xo[r]] = v;
+        if (rg.pm[r]) pen += (double)v.r * v.r + (double)v.i * v.i;
       }
+  };
+  // Step k: x_{k+1} = U_k x_k with U_k in register set k % D, which is then refilled with U_{k+D}.
+  QOC_CT_DECL;
+  auto fwd_step = [&](int k_, USet<T, JT>& Q) __attribute__((always_inline)) {
+    const cx<T>* xc = xb + (k_ & 1) * XB;
+    cx<T>* xn = xb + ((k_ + 1) & 1) * XB;
+    QOC_CT(0);
+    copy_out(xc, k_);
+    QOC_CT(1);
+    rg.settle(Q);
+    QOC_CT(2);
+    for (int c0 = rg.c_begin; c0 < m; c0 += rg.c_step) {
+      cx<T> y[CB];
+      rg.template dot<false>(Q, xc, c0, y);
+#pragma unroll
+      for (int bb = 0; bb < CB; ++bb)
+        if (rg.act && rg.p == 0 && c0 + bb < m) xn[XS * (c0 + bb) + rg.i] = y[bb];
     }
-    if (k_ + 1 < Nt) commit_u(ub + ((k_ + 1) & 1) * LDU, N, PN);  // U_{k+1}
-    if (k_ + 5 < Nt) prefetch_u(Ub + (size_t)(k_ + 5) * NN, NN, PN);
+    QOC_CT(3);
+    // unconditional (clamped) refill: a conditional one leaves the waitcnt pass unable to count the newer
+    // loads, and it then waits for every prefetch at the next use
+    rg.load(Ub + (size_t)min(k_ + D, Nt - 1) * NN, N, false, Q);
+    QOC_CT(4);
     lds_barrier();
+    QOC_CT(5);
   };
   int k = 0;
-  for (; k + 3 < Nt; k += 4) {
-    fwd_step(k, Q0);
-    fwd_step(k + 1, Q1);
-    fwd_step(k + 2, Q2);
-    fwd_step(k + 3, Q3);
+  for (; k + D - 1 < Nt; k += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) fwd_step(k + d, Q[d]);
   }
-  if (k < Nt) fwd_step(k, Q0);
-  if (k + 1 < Nt) fwd_step(k + 1, Q1);
-  if (k + 2 < Nt) fwd_step(k + 2, Q2);
-  const cx<T>* xN = xb + (Nt & 1) * Nm;
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d)
+    if (k + d < Nt) fwd_step(k + d, Q[d]);
+  copy_out(xb + (Nt & 1) * XB, Nt);
+  QOC_CT_DUMP();
+  const cx<T>* xNp = xb + (Nt & 1) * XB;
+  auto xN = [&](int o) { return xNp[XS * (o / N) + o % N]; };
   // ---- costs on x_N ----
   const double psum = block_sum(pen, red) * mu;
   if (cost_kind == COST_TRACE) {
     double orr = 0, oii = 0;
     for (int o = tid; o < Nm; o += CHAIN_THREADS) {
-      const cx<T> t = Xt[o], v = xN[o];
+      const cx<T> t = Xt[o], v = xN(o);
       orr += (double)t.r * v.r + (double)t.i * v.i;
       oii += (double)t.r * v.i - (double)t.i * v.r;
     }
@@ -236,7 +377,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
     for (int c = 0; c < 4; ++c) {
       double orr = 0, oii = 0;
       for (int i = tid; i < N; i += CHAIN_THREADS) {
-        const cx<T> t = Xt[i + N * c], v = xN[i + N * c];
+        const cx<T> t = Xt[i + N * c], v = xN(i + N * c);
         orr += (double)t.r * v.r + (double)t.i * v.i;
         oii += (double)t.r * v.i - (double)t.i * v.r;
       }
@@ -266,85 +407,90 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
   }
 }
 
-template <typename T>
+template <typename T, int S, int JT, int CB>
 __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
     int N, int m, int Nt, const cx<T>* __restrict__ U, const cx<T>* __restrict__ X, cx<T>* __restrict__ Lam,
     const cx<T>* __restrict__ Xt, int cost_kind, const cx<double>* __restrict__ coef,
     const unsigned char* __restrict__ pmask, double mu) {
+  using R = ChainRegs<T, S, JT, CB, false>;
+  constexpr int XS = R::XS, D = R::D;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int NN = N * N, Nm = N * m, LDU = N * (N + 1);
-  cx<T>* ub = reinterpret_cast<cx<T>*>(smem);
-  cx<T>* lb = ub + 2 * LDU;  // 2 x N*m
+  const int NN = N * N, Nm = N * m, XB = XS * chain_mpad(m, CB);
+  cx<T>* lb = reinterpret_cast<cx<T>*>(smem);  // 2 x m columns of XS (zero-padded)
   const cx<T>* Ub = U + (size_t)b * Nt * NN;
   const cx<T>* Xb = X + (size_t)b * (Nt + 1) * Nm;
   cx<T>* Lb = Lam + (size_t)b * (Nt + 1) * Nm;
   const T tmu = (T)(2.0 * mu);
-  const int S = chain_split(Nm), part = tid % S, o0 = tid / S, ostride = CHAIN_THREADS / S;
-  // λ_{Nt+1} = dJfinal/dx(x_N) (+ dL/dx(x_N)), stored in buffer (Nt & 1)
-  cx<T>* l0 = lb + (Nt & 1) * Nm;
-  for (int o = tid; o < Nm; o += CHAIN_THREADS) {
-    cx<T> v;
-    if (cost_kind == COST_EXTERNAL) {
-      v = Lb[(size_t)Nt * Nm + o];
-    } else {
-      const cx<double> cf = coef[(size_t)b * m + o / N];
-      const cx<T> t = Xt[o];
-      v.r = (T)(cf.r * t.r - cf.i * t.i);
-      v.i = (T)(cf.r * t.i + cf.i * t.r);
-    }
-    if (pmask && pmask[o]) {
-      const cx<T> xv = Xb[(size_t)Nt * Nm + o];
-      v.r += tmu * xv.r;
-      v.i += tmu * xv.i;
-    }
-    l0[o] = v;
-    Lb[(size_t)Nt * Nm + o] = v;
-  }
-  // Step i (k = Nt-1-i) commits U_{k-1} from Q[i & 3] and refills that set with U_{k-5}; unrolled by 4.
-  UPref<T> Q0, Q1, Q2, Q3;
-  {
-    UPref<T> P;
-    prefetch_u(Ub + (size_t)(Nt - 1) * NN, NN, P);
-    commit_u(ub + ((Nt - 1) & 1) * LDU, N, P);
-  }
-  if (Nt > 1) prefetch_u(Ub + (size_t)(Nt - 2) * NN, NN, Q0);
-  if (Nt > 2) prefetch_u(Ub + (size_t)(Nt - 3) * NN, NN, Q1);
-  if (Nt > 3) prefetch_u(Ub + (size_t)(Nt - 4) * NN, NN, Q2);
-  if (Nt > 4) prefetch_u(Ub + (size_t)(Nt - 5) * NN, NN, Q3);
-  __syncthreads();
-  auto bwd_step = [&](int k_, UPref<T>& PN) __attribute__((always_inline)) {
-    const cx<T>* cur = ub + (k_ & 1) * LDU;
-    const cx<T>* lc = lb + ((k_ + 1) & 1) * Nm;
-    cx<T>* ln = lb + (k_ & 1) * Nm;
-    cx<T>* Lk = Lb + (size_t)k_ * Nm;
-    for (int o = o0; o < Nm; o += ostride) {
-      const int i = o % N, c = o / N;
-      cx<T> y = chain_dot<T, true>(cur, lc + N * c, N, i, part, S);
-      if (part == 0) {
-        if (pmask && pmask[o]) {
-          const cx<T> xv = Xb[(size_t)k_ * Nm + o];
-          y.r += tmu * xv.r;
-          y.i += tmu * xv.i;
-        }
-        ln[o] = y;
-        Lk[o] = y;
+  R rg;
+  rg.setup(N);
+  // Step i (k = Nt-1-i) uses U_k from register set i % D and refills it with U_{k-D} (U^H: columns of U).
+  USet<T, JT> Q[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) rg.load(Ub + (size_t)max(Nt - 1 - d, 0) * NN, N, true, Q[d]);
+  rg.setup_slots(N, m, pmask);
+  // λ_{Nt+1} = dJfinal/dx(x_N) (+ dL/dx(x_N)) -> buffer (Nt & 1); everything else zero
+  for (int e = tid; e < 2 * XB; e += CHAIN_THREADS) {
+    const int c = (e % XB) / XS, r = e % XS, o = r + N * c;
+    cx<T> v = {0, 0};
+    if (e / XB == (Nt & 1) && r < N && c < m) {
+      if (cost_kind == COST_EXTERNAL) {
+        v = Lb[(size_t)Nt * Nm + o];
+      } else {
+        const cx<double> cf = coef[(size_t)b * m + c];
+        const cx<T> t = Xt[o];
+        v.r = (T)(cf.r * t.r - cf.i * t.i);
+        v.i = (T)(cf.r * t.i + cf.i * t.r);
+      }
+      if (pmask && pmask[o]) {
+        const cx<T> xv = Xb[(size_t)Nt * Nm + o];
+        v.r += tmu * xv.r;
+        v.i += tmu * xv.i;
       }
     }
-    if (k_ > 0) commit_u(ub + ((k_ - 1) & 1) * LDU, N, PN);      // U_{k-1}
-    if (k_ >= 5) prefetch_u(Ub + (size_t)(k_ - 5) * NN, NN, PN);  // U_{k-5}: consumed 4 steps later
+    lb[e] = v;
+  }
+  __syncthreads();
+  auto copy_out = [&](const cx<T>* ls, int k_) __attribute__((always_inline)) {
+    cx<T>* Lk = Lb + (size_t)k_ * Nm;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (rg.xo[r] >= 0) Lk[rg.xo[r]] = ls[rg.xi[r]];
+  };
+  auto bwd_step = [&](int k_, USet<T, JT>& Q) __attribute__((always_inline)) {
+    const cx<T>* lc = lb + ((k_ + 1) & 1) * XB;
+    cx<T>* ln = lb + (k_ & 1) * XB;
+    copy_out(lc, k_ + 1);
+    rg.settle(Q);
+    for (int c0 = rg.c_begin; c0 < m; c0 += rg.c_step) {
+      cx<T> y[CB];
+      rg.template dot<true>(Q, lc, c0, y);
+#pragma unroll
+      for (int bb = 0; bb < CB; ++bb)
+        if (rg.act && rg.p == 0 && c0 + bb < m) ln[XS * (c0 + bb) + rg.i] = y[bb];
+    }
+    rg.load(Ub + (size_t)max(k_ - D, 0) * NN, N, true, Q);  // unconditional (see k_chain_fwd)
     lds_barrier();
+    if (pmask) {  // + dL/dx(x_k) (src/gradient_computations.jl:55-57); drains the prefetch (optional path)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (rg.pm[r]) {
+          const cx<T> xv = Xb[(size_t)k_ * Nm + rg.xo[r]];
+          ln[rg.xi[r]].r += tmu * xv.r;
+          ln[rg.xi[r]].i += tmu * xv.i;
+        }
+      __syncthreads();
+    }
   };
   int i = 0;
-  for (; i + 3 < Nt; i += 4) {
-    bwd_step(Nt - 1 - i, Q0);
-    bwd_step(Nt - 2 - i, Q1);
-    bwd_step(Nt - 3 - i, Q2);
-    bwd_step(Nt - 4 - i, Q3);
+  for (; i + D - 1 < Nt; i += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) bwd_step(Nt - 1 - i - d, Q[d]);
   }
-  if (i < Nt) bwd_step(Nt - 1 - i, Q0);
-  if (i + 1 < Nt) bwd_step(Nt - 2 - i, Q1);
-  if (i + 2 < Nt) bwd_step(Nt - 3 - i, Q2);
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d)
+    if (i + d < Nt) bwd_step(Nt - 1 - i - d, Q[d]);
+  copy_out(lb, 0);
 }
 
 // ---------------------------------------------------------------------------

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/qoc.h"
@@ -270,8 +271,31 @@ int download(qoc_ctx* ctx, const void* dev, double* host, size_t nelem) {
 }
 
 size_t chain_lds(const qoc_ctx* c) {
-  return (size_t)(2 * c->N * (c->N + 1) + 2 * c->N * c->m) * c->esz + 64 * sizeof(double);
+  const ChainShape sh = chain_shape(c->N, c->m, c->prec == QOC_FP64);
+  return (size_t)(2 * sh.S * sh.JT * chain_mpad(c->m, sh.CB)) * c->esz + 64 * sizeof(double);
 }
+
+// k_chain_fwd / k_chain_bwd instantiated per thread shape (chain_shape): (S, JT, CB) = (4, 4, 1|4),
+// (8, 4, 1|4), (4, 10, 1), (4, 12, 1), fp32 also (4, 16, 1).
+template <typename T, typename F>
+hipError_t chain_dispatch(int N, int m, F&& f) {
+  using std::integral_constant;
+  const ChainShape sh = chain_shape(N, m, sizeof(T) == 8);
+  if (sh.JT == 4) {
+    if (sh.S == 4)
+      return sh.CB == 4 ? f(integral_constant<int, 4>(), integral_constant<int, 4>(), integral_constant<int, 4>())
+                        : f(integral_constant<int, 4>(), integral_constant<int, 4>(), integral_constant<int, 1>());
+    return sh.CB == 4 ? f(integral_constant<int, 8>(), integral_constant<int, 4>(), integral_constant<int, 4>())
+                      : f(integral_constant<int, 8>(), integral_constant<int, 4>(), integral_constant<int, 1>());
+  }
+  if (sh.JT == 10) return f(integral_constant<int, 4>(), integral_constant<int, 10>(), integral_constant<int, 1>());
+  if (sh.JT == 12) return f(integral_constant<int, 4>(), integral_constant<int, 12>(), integral_constant<int, 1>());
+  if constexpr (sizeof(T) == 4) {
+    if (sh.JT == 16) return f(integral_constant<int, 4>(), integral_constant<int, 16>(), integral_constant<int, 1>());
+  }
+  return hipErrorInvalidValue;
+}
+
 size_t grad_lds(const qoc_ctx* c, int order) {
   return (size_t)(c->N * (c->N + 1) + 2 * order * c->N * c->m) * c->esz + 64 * sizeof(double);
 }
@@ -321,14 +345,20 @@ int run_forward(qoc_ctx* c) {
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm launch: %s", hipGetErrorString(e));
   const size_t lds = chain_lds(c);
-  HIPCHK(c, hipFuncSetAttribute((const void*)k_chain_fwd<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   mk = mark_begin(c, 1);
-  hipLaunchKernelGGL((k_chain_fwd<T>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
-                     (const cx<T>*)c->d_U, (const cx<T>*)c->d_x0, c->x0_per_seed, (cx<T>*)c->d_X,
-                     (const cx<T>*)c->d_Xt, c->cost_kind, c->cost_n, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu,
-                     c->d_J, c->d_coef);
+  e = chain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_) {
+    constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value;
+    hipError_t r = hipFuncSetAttribute((const void*)k_chain_fwd<T, S, JT, CB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL((k_chain_fwd<T, S, JT, CB>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
+                       (const cx<T>*)c->d_U, (const cx<T>*)c->d_x0, c->x0_per_seed, (cx<T>*)c->d_X,
+                       (const cx<T>*)c->d_Xt, c->cost_kind, c->cost_n, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu,
+                       c->d_J, c->d_coef);
+    return hipGetLastError();
+  });
   mark_end(c, mk);
-  HIPCHK(c, hipGetLastError());
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_chain_fwd launch: %s", hipGetErrorString(e));
   return QOC_OK;
 }
 
@@ -340,13 +370,19 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
     int r = ode_adjoint<T>(c);
     if (r) return r;
   } else {
-    HIPCHK(c, hipFuncSetAttribute((const void*)k_chain_bwd<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     mk = mark_begin(c, 2);
-    hipLaunchKernelGGL((k_chain_bwd<T>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
-                       (const cx<T>*)c->d_U, (const cx<T>*)c->d_X, (cx<T>*)c->d_L, (const cx<T>*)c->d_Xt, c->cost_kind,
-                       (const cx<double>*)c->d_coef, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu);
+    const hipError_t e = chain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_) {
+      constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value;
+      hipError_t r = hipFuncSetAttribute((const void*)k_chain_bwd<T, S, JT, CB>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (r != hipSuccess) return r;
+      hipLaunchKernelGGL((k_chain_bwd<T, S, JT, CB>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
+                         (const cx<T>*)c->d_U, (const cx<T>*)c->d_X, (cx<T>*)c->d_L, (const cx<T>*)c->d_Xt,
+                         c->cost_kind, (const cx<double>*)c->d_coef, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu);
+      return hipGetLastError();
+    });
     mark_end(c, mk);
-    HIPCHK(c, hipGetLastError());
+    if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_chain_bwd launch: %s", hipGetErrorString(e));
   }
   if (order == QOC_DUKDP_EXACT) {
     mk = mark_begin(c, 3);
@@ -1104,7 +1140,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   if (precision != QOC_FP64 && precision != QOC_FP32) return fail(nullptr, QOC_ERR_ARG, "invalid precision");
   // LDS-resident kernels when the problem fits them, the chunked GEMM pipeline otherwise
   const bool small = expm_supported(N, precision) && N <= kChainMaxN &&
-                     N * N <= CHAIN_THREADS * (precision == QOC_FP64 ? ChainPref<double>::value : ChainPref<float>::value) && N * m <= 4 * CHAIN_THREADS;
+                     N <= (precision == QOC_FP64 ? chain_max_n<double>() : chain_max_n<float>()) && N * m <= 4 * CHAIN_THREADS;
   const bool force_big = getenv("QOC_FORCE_LARGE_N") && atoi(getenv("QOC_FORCE_LARGE_N")) != 0;
   if ((!small || force_big) && nu > 8)
     return fail(nullptr, QOC_ERR_UNSUPPORTED, "large-N path supports nu <= 8 (got %d)", nu);

@@ -50,7 +50,34 @@ __device__ unsigned long long g_life[3 * 65536];
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
     if (blockIdx.x == 7 && threadIdx.x == 0) g_probe[i] = t_;                   \
   } while (0)
+// per-phase cycle accumulators of one thread (block 7, thread 0), dumped to g_probe[32 + i]
+#define QOC_CT_DECL                  \
+  unsigned long long qoc_acc_[8] = {}; \
+  unsigned long long qoc_last_ = 0
+#define QOC_CT(i)                                                              \
+  do {                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                         \
+    unsigned long long t_;                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                         \
+    if (i) qoc_acc_[i] += t_ - qoc_last_;                                      \
+    qoc_last_ = t_;                                                            \
+  } while (0)
+#define QOC_CT_DUMP()                                                          \
+  do {                                                                         \
+    if (blockIdx.x == 7 && threadIdx.x == 0)                                   \
+      for (int i_ = 0; i_ < 8; ++i_) g_probe[32 + i_] = qoc_acc_[i_];          \
+  } while (0)
 #else
+#define QOC_CT_DECL \
+  do {              \
+  } while (0)
+#define QOC_CT(i) \
+  do {            \
+  } while (0)
+#define QOC_CT_DUMP() \
+  do {                \
+  } while (0)
 #define QOC_RTSTAMP(i) \
   do {                 \
   } while (0)
