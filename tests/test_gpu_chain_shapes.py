@@ -1,0 +1,68 @@
+"""GPU parity across the register-resident chain shapes (csrc/qoc_chain.hpp, chain_shape()).
+
+Each case picks N, m and Nt so that another (S, JT, CB) instance, wave split (row blocks x column groups,
+idle copy-out waves) or prefetch tail (Nt < D, Nt not a multiple of D) runs; J and dJdu (order 3) are
+checked against the oracle at the SURVEY §8c tolerances (fp64: |ΔJ| <= 1e-12, rel ||ΔdJdu|| <= 1e-10;
+fp32: 1e-4 / 1e-3).  Synthetic GUE generators, controls scaled by 0.2.
+"""
+import dataclasses
+
+import numpy as np
+import pytest
+
+import qoc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(N, m, Nt, seed, precision):
+    from qoc_amd import systems
+    p0 = systems.synthetic_problem(N=N, nu=2, Nt=Nt, seed=seed, precision=precision)
+    return dataclasses.replace(p0, x0=p0.x0[:, :m].copy(), x_target=p0.x_target[:, :m].copy(), n=float(m))
+
+
+def _check(N, m, Nt, B=3, precision="fp64", penalty=None, seed=0):
+    from qoc_amd import GrapeEngine, systems
+    prob = _problem(N, m, Nt, seed, precision)
+    u = systems.synthetic_controls(B, Nt, nu=2, seed=seed) * 0.2
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B, precision=precision)
+    e.set_cost_trace(prob.x_target, prob.n)
+    if penalty is not None:
+        e.set_state_penalty(*penalty)
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    e.close()
+    tolJ, tolg = (1e-12, 1e-10) if precision == "fp64" else (1e-4, 1e-3)
+    for b in range(B):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3, penalty=penalty)
+        assert abs(J[b] - Jr) <= tolJ, (b, J[b], Jr)
+        rel = np.linalg.norm(g[b] - gr) / max(np.linalg.norm(gr), 1e-300)
+        assert rel <= tolg, (b, rel)
+
+
+@pytest.mark.parametrize("N,m,Nt", [
+    (3, 1, 1),     # S=4 JT=4, one row block, 4 column groups, Nt = 1 < D
+    (9, 4, 2),     # zz-like: one column per wave
+    (16, 5, 3),    # CB = 1 with 2 columns on one wave
+    (16, 16, 9),   # CB = 4, four columns per wave
+    (17, 1, 9),    # S=8, 3 row blocks, idle copy-out wave
+    (17, 4, 5),
+    (32, 8, 17),   # 4 row blocks (no idle wave), CB = 4, Nt = 2 D + 1
+    (33, 2, 4),    # S=4 JT=10
+    (40, 3, 9),
+    (44, 1, 6),    # JT=12, D = 3
+])
+def test_chain_shapes_fp64(built_lib, N, m, Nt):
+    _check(N, m, Nt)
+
+
+def test_chain_penalty_on_split_waves(built_lib):
+    """State penalty (copy-out slots on the idle wave carry the mask bits; the backward adds dL/dx)."""
+    N, m = 17, 3
+    rows = [0, 3, 5, 16]
+    _check(N, m, 11, penalty=(rows, [0, 2], 0.29))
+
+
+@pytest.mark.parametrize("N,m,Nt", [(50, 2, 5), (64, 4, 7)])
+def test_chain_shapes_fp32(built_lib, N, m, Nt):
+    _check(N, m, Nt, precision="fp32")
