@@ -66,3 +66,31 @@ def test_chain_penalty_on_split_waves(built_lib):
 @pytest.mark.parametrize("N,m,Nt", [(50, 2, 5), (64, 4, 7)])
 def test_chain_shapes_fp32(built_lib, N, m, Nt):
     _check(N, m, Nt, precision="fp32")
+
+
+def _check_nu(N, m, nu, Nt, B, seed=1):
+    """Full pipeline with nu generators (synthetic GUE, scaled controls) against the oracle."""
+    from qoc_amd import GrapeEngine, systems
+    p0 = systems.synthetic_problem(N=N, nu=nu, Nt=Nt, seed=seed, precision="fp64")
+    prob = dataclasses.replace(p0, x0=p0.x0[:, :m].copy(), x_target=p0.x_target[:, :m].copy(), n=float(m))
+    u = systems.synthetic_controls(B, Nt, nu=nu, seed=seed) * 0.2
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
+    e.set_cost_trace(prob.x_target, prob.n)
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    e.close()
+    for b in range(B):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        assert abs(J[b] - Jr) <= 1e-12, (b, J[b], Jr)
+        assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10, b
+
+
+@pytest.mark.parametrize("N,m,nu,Nt,B", [
+    (12, 2, 1, 1, 1),    # a single slice, a single seed
+    (12, 3, 3, 4, 2),    # nu = 3, m = 3: outside the fused gradient's m / nu set (per-slice k_grad)
+    (12, 12, 2, 3, 2),   # m = N (gate problem: all basis states)
+    (20, 16, 2, 2, 1),   # m = 16 fused tile of one unit per tile
+    (24, 1, 5, 3, 2),    # nu = 5
+])
+def test_pipeline_unusual_dimensions(built_lib, N, m, nu, Nt, B):
+    _check_nu(N, m, nu, Nt, B)
