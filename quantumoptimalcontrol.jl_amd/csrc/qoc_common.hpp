@@ -48,6 +48,13 @@ struct MF<double> {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
   }
   static __device__ __forceinline__ int drow(int lane, int i) { return (lane >> 4) + 4 * i; }
+  // v_mfma_f64_4x4x4_4b (16 cycles, the same FMA rate as 16x16x4): block b = (l >> 2) & 3; A[m][k] at lane
+  // m + 4b + 16k, B[k][n] at n + 4b + 16k, D[m][n] at n + 4b + 16m (measured, tools/mfma4_layout.hip).  With
+  // the blocks side by side along n, B is the 16x16x4 B fragment and D is one register (m-quad) of the
+  // 16x16x4 D layout; A carries rows 4q + (l & 3) of that quad.
+  static __device__ __forceinline__ double mma4(double a, double b, double c) {
+    return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+  }
 };
 
 template <>

@@ -75,9 +75,18 @@ struct ExpmRR {
 
   // out = X B + init, with X owned (registers, zero outside N) and B shared (row-major LDS, pitch ldp(N)).
   // KS k-steps (compile time, branch-free); one k-step of look-ahead on the operand loads.
+  // fp64: the last row tile holds LQ = KS - 4 (NT - 1) valid row quads (KS = ceil(N / 4)); when LQ < 4 it
+  // runs as LQ v_mfma_f64_4x4x4_4b per component (16 cycles each) instead of one 16x16x4 (64 cycles).
+  template <int KS>
+  static constexpr int last_quads() {
+    return sizeof(T) == 8 ? KS - 4 * (NT - 1) : 4;
+  }
   template <int KS>
   static __device__ __forceinline__ void rmul(int N, const Own& X, const T* __restrict__ Br,
                                               const T* __restrict__ Bi, Own& out, const Own& init, int lane) {
+    constexpr int LQ = last_quads<KS>();
+    constexpr bool Q4 = LQ < 4;
+    constexpr int NF = Q4 ? NT - 1 : NT;  // full 16-row tiles
     v4 rr[NT], ii[NT], S[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -87,12 +96,21 @@ struct ExpmRR {
     }
     const int base = lane & 15;
     T pr[KS][NT], pi[KS][NT];
+    T qpr[KS][Q4 ? LQ : 1], qpi[KS][Q4 ? LQ : 1];
     auto load = [&](int s) __attribute__((always_inline)) {
       const int a = kidx(s, lane) * ldp(N) + base;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
+      for (int t = 0; t < NF; ++t) {
         pr[s][t] = Br[a + 16 * t];
         pi[s][t] = Bi[a + 16 * t];
+      }
+      if constexpr (Q4) {
+        const int a4 = kidx(s, lane) * ldp(N) + 16 * (NT - 1) + (lane & 3);
+#pragma unroll
+        for (int q = 0; q < LQ; ++q) {
+          qpr[s][q] = Br[a4 + 4 * q];
+          qpi[s][q] = Bi[a4 + 4 * q];
+        }
       }
     };
     load(0);
@@ -102,10 +120,18 @@ struct ExpmRR {
       if (s + 1 < KS) load(s + 1);
       const T qr = X.r[s >> 2][s & 3], qi = X.i[s >> 2][s & 3], qs = qr + qi;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
+      for (int t = 0; t < NF; ++t) {
         rr[t] = M::mma(pr[s][t], qr, rr[t]);
         ii[t] = M::mma(pi[s][t], qi, ii[t]);
         S[t] = M::mma(pr[s][t] + pi[s][t], qs, S[t]);
+      }
+      if constexpr (Q4) {
+#pragma unroll
+        for (int q = 0; q < LQ; ++q) {
+          rr[NT - 1][q] = M::mma4(qpr[s][q], qr, rr[NT - 1][q]);
+          ii[NT - 1][q] = M::mma4(qpi[s][q], qi, ii[NT - 1][q]);
+          S[NT - 1][q] = M::mma4(qpr[s][q] + qpi[s][q], qs, S[NT - 1][q]);
+        }
       }
     }
 #pragma unroll
