@@ -64,6 +64,9 @@ struct MF<float> {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
   }
   static __device__ __forceinline__ int drow(int lane, int i) { return ((lane >> 4) << 2) + i; }
+  // fp32 tiles never take the 4x4x4 path (its k order interleaves the lane groups); present so that the
+  // constant-false branches compile
+  static __device__ __forceinline__ float mma4(float, float, float c) { return c; }
 };
 
 // Uniform-lane broadcast (v_readlane -> SGPR).

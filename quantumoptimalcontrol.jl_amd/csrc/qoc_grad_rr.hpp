@@ -15,6 +15,8 @@
 //   * the contraction with A_j runs one row tile at a time and reduces in registers; one lane per
 //     unit writes dJdu.  No intermediate touches HBM: per unit only x_k, λ_{k+1}, u_k in, dJdu out.
 #pragma once
+#include <type_traits>
+
 #include "qoc_common.hpp"
 
 namespace qoc {
@@ -34,6 +36,11 @@ struct GradRR {
     return (size_t)2 * (nu + 1) * N * ldp(N) * sizeof(T);
   }
   static __device__ __forceinline__ int kidx(int s, int lane) { return 16 * (s >> 2) + M::drow(lane, s & 3); }
+  // fp64: valid row quads of the last row tile (KS = ceil(N / 4)); < 4 runs it on 4x4x4 blocks
+  template <int KS>
+  static constexpr int last_quads() {
+    return sizeof(T) == 8 ? KS - 4 * (NT - 1) : 4;
+  }
 
   static __device__ __forceinline__ void mask_rows(int N, Own& X, int lane) {  // rows >= N -> 0 (last tile)
 #pragma unroll
@@ -51,24 +58,35 @@ struct GradRR {
   static __device__ __forceinline__ void xmul(int N, const T* __restrict__ Gr, const T* __restrict__ Gi,
                                               const double* uj, const Own& V, Own& out, int lane) {
     const int ld = ldp(N), PL = N * ld;
-    int li = lane & 15;
-    asm volatile("" : "+v"(li));  // opaque: keeps the operand addresses from being hoisted out of the tile loop
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
+    int li = lane & 15, l3 = lane & 3;
+    asm volatile("" : "+v"(li), "+v"(l3));  // opaque: keeps the operand addresses from being hoisted out of the tile loop
+    // the last row tile with LQ < 4 valid row quads runs as LQ v_mfma_f64_4x4x4_4b (MF<double>::mma4)
+    constexpr int LQ = last_quads<KS>();
+    constexpr bool Q4 = LQ < 4;
+    auto tile = [&](int t, auto quads) __attribute__((always_inline)) {
+      constexpr int QN = decltype(quads)::value;  // 0: one 16x16x4 per k-step; else QN 4x4x4 blocks
+      constexpr int NQ = QN ? QN : 1;
       const int pc = min(16 * t + li, N - 1);  // clamped row of the A operand
       v4 rr = v4{0, 0, 0, 0}, ii = v4{0, 0, 0, 0}, S = v4{0, 0, 0, 0};
+      T qrr[NQ], qii[NQ], qS[NQ];  // 4x4x4 accumulators (one register of the 16x16 D layout each)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) qrr[q] = qii[q] = qS[q] = T(0);
 #pragma unroll
       for (int j = 0; j <= NU; ++j) {
         T cj = j == 0 ? T(1) : (T)uj[j - 1];
         asm volatile("" : "+v"(cj));  // opaque per row tile: c_j V is recomputed, not kept for every tile
         const T* gr = Gr + (size_t)j * PL;
         const T* gi = Gi + (size_t)j * PL;
-        T pr[KS], pi[KS];
+        T pr[KS][NQ], pi[KS][NQ];
         auto load = [&](int s) __attribute__((always_inline)) {
           const int k = min(kidx(s, lane), N - 1);
-          const int a = HERM ? pc * ld + k : k * ld + pc;
-          pr[s] = gr[a];
-          pi[s] = gi[a];
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const int pq = QN ? min(16 * t + 4 * q + l3, N - 1) : pc;
+            const int a = HERM ? pq * ld + k : k * ld + pq;
+            pr[s][q] = gr[a];
+            pi[s][q] = gi[a];
+          }
         };
         load(0);
 #pragma unroll
@@ -76,9 +94,26 @@ struct GradRR {
           __builtin_amdgcn_sched_barrier(0);  // one k-step of look-ahead (register pressure)
           if (s + 1 < KS) load(s + 1);
           const T qr = cj * V.r[s >> 2][s & 3], qi = cj * V.i[s >> 2][s & 3];
-          rr = M::mma(pr[s], qr, rr);
-          ii = M::mma(pi[s], qi, ii);
-          S = M::mma(HERM ? pr[s] - pi[s] : pr[s] + pi[s], qr + qi, S);
+          if constexpr (QN == 0) {
+            rr = M::mma(pr[s][0], qr, rr);
+            ii = M::mma(pi[s][0], qi, ii);
+            S = M::mma(HERM ? pr[s][0] - pi[s][0] : pr[s][0] + pi[s][0], qr + qi, S);
+          } else {
+#pragma unroll
+            for (int q = 0; q < QN; ++q) {
+              qrr[q] = M::mma4(pr[s][q], qr, qrr[q]);
+              qii[q] = M::mma4(pi[s][q], qi, qii[q]);
+              qS[q] = M::mma4(HERM ? pr[s][q] - pi[s][q] : pr[s][q] + pi[s][q], qr + qi, qS[q]);
+            }
+          }
+        }
+      }
+      if constexpr (QN > 0) {
+#pragma unroll
+        for (int q = 0; q < QN; ++q) {
+          rr[q] = qrr[q];
+          ii[q] = qii[q];
+          S[q] = qS[q];
         }
       }
       if (HERM) {  // conj(a) q: Re = rr + ii, Im = S - rr + ii with S = (ar - ai)(qr + qi)
@@ -88,7 +123,10 @@ struct GradRR {
         out.r[t] = rr - ii;
         out.i[t] = S - rr - ii;
       }
-    }
+    };
+#pragma unroll
+    for (int t = 0; t < (Q4 ? NT - 1 : NT); ++t) tile(t, std::integral_constant<int, 0>());
+    if constexpr (Q4) tile(NT - 1, std::integral_constant<int, Q4 ? LQ : 0>());
     mask_rows(N, out, lane);
   }
 
@@ -97,22 +135,32 @@ struct GradRR {
   static __device__ __forceinline__ void contract(int N, const T* __restrict__ Gr, const T* __restrict__ Gi,
                                                   const Own& V, const Own& W, double* sj, int lane) {
     const int ld = ldp(N), PL = N * ld;
-    int li = lane & 15;
-    asm volatile("" : "+v"(li));  // see xmul
+    int li = lane & 15, l3 = lane & 3;
+    asm volatile("" : "+v"(li), "+v"(l3));  // see xmul
 #pragma unroll
     for (int j = 1; j <= NU; ++j) {
       const T* gr = Gr + (size_t)j * PL;
       const T* gi = Gi + (size_t)j * PL;
       double acc = 0.0;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
+      constexpr int LQ = last_quads<KS>();
+      constexpr bool Q4 = LQ < 4;
+      auto tile = [&](int t, auto quads) __attribute__((always_inline)) {
+        constexpr int QN = decltype(quads)::value;  // 0: 16x16x4; else QN 4x4x4 blocks (partial last tile)
+        constexpr int NQ = QN ? QN : 1;
         const int pc = min(16 * t + li, N - 1);
         v4 rr = v4{0, 0, 0, 0}, ii = v4{0, 0, 0, 0}, S = v4{0, 0, 0, 0};
-        T pr[KS], pi[KS];
+        T qrr[NQ], qii[NQ], qS[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) qrr[q] = qii[q] = qS[q] = T(0);
+        T pr[KS][NQ], pi[KS][NQ];
         auto load = [&](int s) __attribute__((always_inline)) {
-          const int a = min(kidx(s, lane), N - 1) * ld + pc;
-          pr[s] = gr[a];
-          pi[s] = gi[a];
+          const int k = min(kidx(s, lane), N - 1);
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const int a = k * ld + (QN ? min(16 * t + 4 * q + l3, N - 1) : pc);
+            pr[s][q] = gr[a];
+            pi[s][q] = gi[a];
+          }
         };
         load(0);
 #pragma unroll
@@ -120,9 +168,26 @@ struct GradRR {
           __builtin_amdgcn_sched_barrier(0);
           if (s + 1 < KS) load(s + 1);
           const T qr = V.r[s >> 2][s & 3], qi = V.i[s >> 2][s & 3];
-          rr = M::mma(pr[s], qr, rr);
-          ii = M::mma(pi[s], qi, ii);
-          S = M::mma(pr[s] + pi[s], qr + qi, S);
+          if constexpr (QN == 0) {
+            rr = M::mma(pr[s][0], qr, rr);
+            ii = M::mma(pi[s][0], qi, ii);
+            S = M::mma(pr[s][0] + pi[s][0], qr + qi, S);
+          } else {
+#pragma unroll
+            for (int q = 0; q < QN; ++q) {
+              qrr[q] = M::mma4(pr[s][q], qr, qrr[q]);
+              qii[q] = M::mma4(pi[s][q], qi, qii[q]);
+              qS[q] = M::mma4(pr[s][q] + pi[s][q], qr + qi, qS[q]);
+            }
+          }
+        }
+        if constexpr (QN > 0) {
+#pragma unroll
+          for (int q = 0; q < QN; ++q) {
+            rr[q] = qrr[q];
+            ii[q] = qii[q];
+            S[q] = qS[q];
+          }
         }
         // W is zero outside N, so the junk rows >= N of this tile contribute nothing
 #pragma unroll
@@ -131,7 +196,10 @@ struct GradRR {
           acc += (double)W.r[t][e] * dr + (double)W.i[t][e] * di;
         }
         asm volatile("" : "+v"(acc));  // materialise now: otherwise the tile's products are kept (spilled) to the end
-      }
+      };
+#pragma unroll
+      for (int t = 0; t < (Q4 ? NT - 1 : NT); ++t) tile(t, std::integral_constant<int, 0>());
+      if constexpr (Q4) tile(NT - 1, std::integral_constant<int, Q4 ? LQ : 0>());
       sj[j - 1] += acc;
     }
   }
