@@ -40,7 +40,8 @@ __host__ __device__ inline ChainShape chain_shape(int N, int m, bool fp64) {
   const int cb = cpw >= 4 ? 4 : 1;
   if (N <= 32) return {S, 4, cb};
   const int J = (N + 3) / 4;
-  return {4, J <= 10 ? 10 : J <= 12 ? 12 : (fp64 ? 0 : 16), 1};  // JT 0: outside the register envelope
+  // N > 32: one row block per wave (G >= 3, CGN = 1); two columns per pass when m >= 2
+  return {4, J <= 10 ? 10 : J <= 12 ? 12 : (fp64 ? 0 : 16), m >= 2 ? 2 : 1};  // JT 0: outside the envelope
 }
 // Largest N the register-resident chains take (fp64: 12 complex per set, fp32: 16).
 template <typename T>

@@ -57,6 +57,7 @@ struct qoc_ctx {
   double* d_dJdu = nullptr;  // B*nu*Nt
   int* d_flag = nullptr;
   unsigned long long* d_hist = nullptr;  // 5*64 reference (Padé) selection + 8*64 executed Taylor (r, s) / T12 s
+  int chain_cb_fwd = 0, chain_cb_bwd = 0;  // 0: chain_shape's column block; QOC_CHAIN_CB_FWD / _BWD = 1 | 2 (N > 32)
   int expm_alg = 1;  // 1 Taylor: register-resident T12 (default), 2 LDS Paterson-Stockmeyer (QOC_EXPM_LDS=1), 0 Padé (QOC_EXPM_PADE=1)
   int prop_method = 0;                   // QOC_PROP_EXPM / QOC_PROP_TSIT5
   int nsub = 10;                         // Tsit5 steps per slice (reference dt = 0.1 Δt)
@@ -276,11 +277,12 @@ size_t chain_lds(const qoc_ctx* c) {
 }
 
 // k_chain_fwd / k_chain_bwd instantiated per thread shape (chain_shape): (S, JT, CB) = (4, 4, 1|4),
-// (8, 4, 1|4), (4, 10, 1), (4, 12, 1), fp32 also (4, 16, 1).
+// (8, 4, 1|4), (4, 10, 1|2), (4, 12, 1|2), fp32 also (4, 16, 1|2).
 template <typename T, typename F>
-hipError_t chain_dispatch(int N, int m, F&& f) {
+hipError_t chain_dispatch(int N, int m, int cb_override, F&& f) {
   using std::integral_constant;
-  const ChainShape sh = chain_shape(N, m, sizeof(T) == 8);
+  ChainShape sh = chain_shape(N, m, sizeof(T) == 8);
+  if (cb_override > 0 && sh.JT >= 10) sh.CB = cb_override == 2 ? 2 : 1;  // tuning knob (QOC_CHAIN_CB_*)
   if (sh.JT == 4) {
     if (sh.S == 4)
       return sh.CB == 4 ? f(integral_constant<int, 4>(), integral_constant<int, 4>(), integral_constant<int, 4>())
@@ -288,10 +290,16 @@ hipError_t chain_dispatch(int N, int m, F&& f) {
     return sh.CB == 4 ? f(integral_constant<int, 8>(), integral_constant<int, 4>(), integral_constant<int, 4>())
                       : f(integral_constant<int, 8>(), integral_constant<int, 4>(), integral_constant<int, 1>());
   }
-  if (sh.JT == 10) return f(integral_constant<int, 4>(), integral_constant<int, 10>(), integral_constant<int, 1>());
-  if (sh.JT == 12) return f(integral_constant<int, 4>(), integral_constant<int, 12>(), integral_constant<int, 1>());
+  if (sh.JT == 10)
+    return sh.CB == 2 ? f(integral_constant<int, 4>(), integral_constant<int, 10>(), integral_constant<int, 2>())
+                      : f(integral_constant<int, 4>(), integral_constant<int, 10>(), integral_constant<int, 1>());
+  if (sh.JT == 12)
+    return sh.CB == 2 ? f(integral_constant<int, 4>(), integral_constant<int, 12>(), integral_constant<int, 2>())
+                      : f(integral_constant<int, 4>(), integral_constant<int, 12>(), integral_constant<int, 1>());
   if constexpr (sizeof(T) == 4) {
-    if (sh.JT == 16) return f(integral_constant<int, 4>(), integral_constant<int, 16>(), integral_constant<int, 1>());
+    if (sh.JT == 16)
+      return sh.CB == 2 ? f(integral_constant<int, 4>(), integral_constant<int, 16>(), integral_constant<int, 2>())
+                        : f(integral_constant<int, 4>(), integral_constant<int, 16>(), integral_constant<int, 1>());
   }
   return hipErrorInvalidValue;
 }
@@ -346,7 +354,7 @@ int run_forward(qoc_ctx* c) {
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm launch: %s", hipGetErrorString(e));
   const size_t lds = chain_lds(c);
   mk = mark_begin(c, 1);
-  e = chain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_) {
+  e = chain_dispatch<T>(c->N, c->m, c->chain_cb_fwd, [&](auto S_, auto JT_, auto CB_) {
     constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value;
     hipError_t r = hipFuncSetAttribute((const void*)k_chain_fwd<T, S, JT, CB>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
@@ -371,7 +379,7 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
     if (r) return r;
   } else {
     mk = mark_begin(c, 2);
-    const hipError_t e = chain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_) {
+    const hipError_t e = chain_dispatch<T>(c->N, c->m, c->chain_cb_bwd, [&](auto S_, auto JT_, auto CB_) {
       constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value;
       hipError_t r = hipFuncSetAttribute((const void*)k_chain_bwd<T, S, JT, CB>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1228,6 +1236,8 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   }
   hipMemset(c->d_pmask, 0, Nm);
   hipMemset(c->d_hist, 0, 13 * 64 * sizeof(unsigned long long));
+  c->chain_cb_fwd = getenv("QOC_CHAIN_CB_FWD") ? atoi(getenv("QOC_CHAIN_CB_FWD")) : 0;
+  c->chain_cb_bwd = getenv("QOC_CHAIN_CB_BWD") ? atoi(getenv("QOC_CHAIN_CB_BWD")) : 0;
   c->expm_alg = (getenv("QOC_EXPM_PADE") && atoi(getenv("QOC_EXPM_PADE")) != 0) ? 0
                 : (getenv("QOC_EXPM_LDS") && atoi(getenv("QOC_EXPM_LDS")) != 0)   ? 2
                                                                                    : 1;
