@@ -273,7 +273,9 @@ int download(qoc_ctx* ctx, const void* dev, double* host, size_t nelem) {
 
 size_t chain_lds(const qoc_ctx* c) {
   const ChainShape sh = chain_shape(c->N, c->m, c->prec == QOC_FP64);
-  return (size_t)(2 * sh.S * sh.JT * chain_mpad(c->m, sh.CB)) * c->esz + 64 * sizeof(double);
+  // sized for the largest column block either direction may use (chain_dispatch's override: 2 at JT >= 10)
+  const int cb = sh.JT >= 10 ? 2 : sh.CB;
+  return (size_t)(2 * sh.S * sh.JT * chain_mpad(c->m, cb)) * c->esz + 64 * sizeof(double);
 }
 
 // k_chain_fwd / k_chain_bwd instantiated per thread shape (chain_shape): (S, JT, CB) = (4, 4, 1|4),
