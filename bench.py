@@ -2,7 +2,7 @@
 """bench.py — GRAPE gradient evals/sec on MI355X (BASELINE.json metric).
 
 One *step* = one GRAPE gradient eval of every seed resident on this GPU:
-propagate (Padé exponentials + forward chain + trace cost) + grape_sensitivity
+propagate (exponentials + forward chain + trace cost) + grape_sensitivity
 (order-3 Taylor Jacobian contraction + co-state chain) — Ipopt's f + f_grad of
 examples/ipopt_callbacks_exp.jl:11-31 without the spline map.  Inputs (u) are resident
 in HBM before the timed region.  Seeds are sharded across ranks (weak scaling); the only

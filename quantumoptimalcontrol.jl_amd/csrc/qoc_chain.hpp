@@ -174,7 +174,7 @@ struct ChainRegs {
   // prefetch depth: slices of U in flight per thread (register sets, <= 128-160 VGPRs in all, so that the
   // small shapes still fit two workgroups per CU); their steps are short and need more sets in flight
   static constexpr int RPS = JT * 2 * (int)sizeof(T) / 4;  // VGPRs per set
-  static constexpr int D = RPS <= 16 ? (128 / RPS > 16 ? 16 : 128 / RPS) : 160 / RPS;
+  static constexpr int D = RPS <= 16 ? (112 / RPS > 16 ? 16 : 112 / RPS) : 160 / RPS;
   static constexpr int R = 64 / S;  // rows per wave
   int i, p;
   bool act;         // owns a valid row (of a computing wave)
@@ -244,22 +244,28 @@ struct ChainRegs {
   }
   // y[b] = sum_q op(U)[i, p + S q] x[p + S q, c0 + b] over the S parts, b < CB; op = identity or
   // conjugate (U^H read by columns).  All LDS reads are issued before the first FMA.
-  template <bool CONJ>
-  __device__ __forceinline__ void dot(const USet<T, JT>& Q, const cx<T>* __restrict__ xs, int c0, cx<T> (&y)[CB]) const {
+  // With REFILL, element q of the next propagator set (Qn, from Uk) is loaded right after the FMAs that
+  // consume element q of this block, so the HBM load issue interleaves with the arithmetic.
+  template <bool CONJ, bool REFILL = false>
+  __device__ __forceinline__ void dot(const USet<T, JT>& Q, const cx<T>* __restrict__ xs, int c0, cx<T> (&y)[CB],
+                                      USet<T, JT>* Qn = nullptr, const cx<T>* __restrict__ Uk = nullptr, int N = 0,
+                                      bool conj_t = false) const {
     cx<T> xv[CB][JT];
 #pragma unroll
     for (int b = 0; b < CB; ++b)
 #pragma unroll
       for (int q = 0; q < JT; ++q) xv[b][q] = xs[XS * (c0 + b) + p + S * q];
     __builtin_amdgcn_sched_barrier(0);
+    T ar0[CB], ai0[CB], ar1[CB], ai1[CB];
 #pragma unroll
-    for (int b = 0; b < CB; ++b) {
-      T ar0 = 0, ai0 = 0, ar1 = 0, ai1 = 0;
+    for (int b = 0; b < CB; ++b) ar0[b] = ai0[b] = ar1[b] = ai1[b] = T(0);
 #pragma unroll
-      for (int q = 0; q < JT; ++q) {  // 4 accumulating FMAs per complex term (no separate products)
+    for (int q = 0; q < JT; ++q) {  // 4 accumulating FMAs per complex term (no separate products)
+#pragma unroll
+      for (int b = 0; b < CB; ++b) {
         const cx<T> x = xv[b][q];
-        T& ar = (q & 1) ? ar1 : ar0;
-        T& ai = (q & 1) ? ai1 : ai0;
+        T& ar = (q & 1) ? ar1[b] : ar0[b];
+        T& ai = (q & 1) ? ai1[b] : ai0[b];
         ar = fma(Q.r[q], x.r, ar);
         ai = fma(Q.r[q], x.i, ai);
         if (CONJ) {  // conj(u) x
@@ -270,8 +276,16 @@ struct ChainRegs {
           ai = fma(Q.i[q], x.r, ai);
         }
       }
-      y[b] = cx<T>{ar0 + ar1, ai0 + ai1};
+      if constexpr (REFILL) {
+        const cx<T> v = Uk[off(N, q, conj_t)];
+        Qn->r[q] = v.r;
+        Qn->i[q] = v.i;
+        __builtin_amdgcn_sched_group_barrier(0x002, 4 * CB, 0);  // this element's FMAs, then
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);       // its load
+      }
     }
+#pragma unroll
+    for (int b = 0; b < CB; ++b) y[b] = cx<T>{ar0[b] + ar1[b], ai0[b] + ai1[b]};
 #pragma unroll
     for (int b = 0; b < CB; ++b) {
       y[b].r = psum(y[b].r);
@@ -298,9 +312,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
   R rg;
   rg.setup(N);
   // U_0..U_3 in flight before anything else
-  USet<T, JT> Q[D];
+  USet<T, JT> Q[D];  // Q[D-1] is filled by step 0
 #pragma unroll
-  for (int d = 0; d < D; ++d) rg.load(Ub + (size_t)min(d, Nt - 1) * NN, N, false, Q[d]);
+  for (int d = 0; d < D - 1; ++d) rg.load(Ub + (size_t)min(d, Nt - 1) * NN, N, false, Q[d]);
   rg.setup_slots(N, m, pmask);
   for (int e = tid; e < 2 * XB; e += CHAIN_THREADS) {
     const int c = (e % XB) / XS, r = e % XS;
@@ -320,9 +334,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
         if (rg.pm[r]) pen += (double)v.r * v.r + (double)v.i * v.i;
       }
   };
-  // Step k: x_{k+1} = U_k x_k with U_k in register set k % D, which is then refilled with U_{k+D}.
   QOC_CT_DECL;
-  auto fwd_step = [&](int k_, USet<T, JT>& Q) __attribute__((always_inline)) {
+  // Step k uses set Q and refills Qn (the set step k-1 used) with U_{k+D-1}: an unconditional (clamped)
+  // refill — a conditional one leaves the waitcnt pass unable to count the newer loads — interleaved
+  // with the first column block's FMAs.  Waves with no column block still run one (clamped, unused).
+  const int cfirst = min(rg.c_begin, chain_mpad(m, CB) - CB);
+  auto fwd_step = [&](int k_, USet<T, JT>& Q, USet<T, JT>& Qn) __attribute__((always_inline)) {
     const cx<T>* xc = xb + (k_ & 1) * XB;
     cx<T>* xn = xb + ((k_ + 1) & 1) * XB;
     QOC_CT(0);
@@ -330,7 +347,14 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
     QOC_CT(1);
     rg.settle(Q);
     QOC_CT(2);
-    for (int c0 = rg.c_begin; c0 < m; c0 += rg.c_step) {
+    {
+      cx<T> y[CB];
+      rg.template dot<false, true>(Q, xc, cfirst, y, &Qn, Ub + (size_t)min(k_ + D - 1, Nt - 1) * NN, N, false);
+#pragma unroll
+      for (int bb = 0; bb < CB; ++bb)
+        if (rg.act && rg.p == 0 && cfirst == rg.c_begin && cfirst + bb < m) xn[XS * (cfirst + bb) + rg.i] = y[bb];
+    }
+    for (int c0 = rg.c_begin + rg.c_step; c0 < m; c0 += rg.c_step) {
       cx<T> y[CB];
       rg.template dot<false>(Q, xc, c0, y);
 #pragma unroll
@@ -338,9 +362,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
         if (rg.act && rg.p == 0 && c0 + bb < m) xn[XS * (c0 + bb) + rg.i] = y[bb];
     }
     QOC_CT(3);
-    // unconditional (clamped) refill: a conditional one leaves the waitcnt pass unable to count the newer
-    // loads, and it then waits for every prefetch at the next use
-    rg.load(Ub + (size_t)min(k_ + D, Nt - 1) * NN, N, false, Q);
     QOC_CT(4);
     lds_barrier();
     QOC_CT(5);
@@ -348,11 +369,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
   int k = 0;
   for (; k + D - 1 < Nt; k += D) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) fwd_step(k + d, Q[d]);
+    for (int d = 0; d < D; ++d) fwd_step(k + d, Q[d], Q[(d + D - 1) % D]);
   }
 #pragma unroll
   for (int d = 0; d < D - 1; ++d)
-    if (k + d < Nt) fwd_step(k + d, Q[d]);
+    if (k + d < Nt) fwd_step(k + d, Q[d], Q[(d + D - 1) % D]);
   copy_out(xb + (Nt & 1) * XB, Nt);
   QOC_CT_DUMP();
   const cx<T>* xNp = xb + (Nt & 1) * XB;
@@ -426,9 +447,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
   R rg;
   rg.setup(N);
   // Step i (k = Nt-1-i) uses U_k from register set i % D and refills it with U_{k-D} (U^H: columns of U).
-  USet<T, JT> Q[D];
+  USet<T, JT> Q[D];  // Q[D-1] is filled by step 0
 #pragma unroll
-  for (int d = 0; d < D; ++d) rg.load(Ub + (size_t)max(Nt - 1 - d, 0) * NN, N, true, Q[d]);
+  for (int d = 0; d < D - 1; ++d) rg.load(Ub + (size_t)max(Nt - 1 - d, 0) * NN, N, true, Q[d]);
   rg.setup_slots(N, m, pmask);
   // λ_{Nt+1} = dJfinal/dx(x_N) (+ dL/dx(x_N)) -> buffer (Nt & 1); everything else zero
   for (int e = tid; e < 2 * XB; e += CHAIN_THREADS) {
@@ -458,19 +479,26 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
     for (int r = 0; r < 4; ++r)
       if (rg.xo[r] >= 0) Lk[rg.xo[r]] = ls[rg.xi[r]];
   };
-  auto bwd_step = [&](int k_, USet<T, JT>& Q) __attribute__((always_inline)) {
+  const int cfirst = min(rg.c_begin, chain_mpad(m, CB) - CB);
+  auto bwd_step = [&](int k_, USet<T, JT>& Q, USet<T, JT>& Qn) __attribute__((always_inline)) {
     const cx<T>* lc = lb + ((k_ + 1) & 1) * XB;
     cx<T>* ln = lb + (k_ & 1) * XB;
     copy_out(lc, k_ + 1);
     rg.settle(Q);
-    for (int c0 = rg.c_begin; c0 < m; c0 += rg.c_step) {
+    {  // first column block with the refill of Qn (U_{k-D+1}) interleaved, as in k_chain_fwd
+      cx<T> y[CB];
+      rg.template dot<true, true>(Q, lc, cfirst, y, &Qn, Ub + (size_t)max(k_ - D + 1, 0) * NN, N, true);
+#pragma unroll
+      for (int bb = 0; bb < CB; ++bb)
+        if (rg.act && rg.p == 0 && cfirst == rg.c_begin && cfirst + bb < m) ln[XS * (cfirst + bb) + rg.i] = y[bb];
+    }
+    for (int c0 = rg.c_begin + rg.c_step; c0 < m; c0 += rg.c_step) {
       cx<T> y[CB];
       rg.template dot<true>(Q, lc, c0, y);
 #pragma unroll
       for (int bb = 0; bb < CB; ++bb)
         if (rg.act && rg.p == 0 && c0 + bb < m) ln[XS * (c0 + bb) + rg.i] = y[bb];
     }
-    rg.load(Ub + (size_t)max(k_ - D, 0) * NN, N, true, Q);  // unconditional (see k_chain_fwd)
     lds_barrier();
     if (pmask) {  // + dL/dx(x_k) (src/gradient_computations.jl:55-57); drains the prefetch (optional path)
 #pragma unroll
@@ -486,11 +514,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
   int i = 0;
   for (; i + D - 1 < Nt; i += D) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) bwd_step(Nt - 1 - i - d, Q[d]);
+    for (int d = 0; d < D; ++d) bwd_step(Nt - 1 - i - d, Q[d], Q[(d + D - 1) % D]);
   }
 #pragma unroll
   for (int d = 0; d < D - 1; ++d)
-    if (i + d < Nt) bwd_step(Nt - 1 - i - d, Q[d]);
+    if (i + d < Nt) bwd_step(Nt - 1 - i - d, Q[d], Q[(d + D - 1) % D]);
   copy_out(lb, 0);
 }
 

@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libqoc_mi355x.so")
+# QOC_LIB_PATH: another build of the same library (same-box A/B comparisons of kernel variants)
+LIB_PATH = os.environ.get("QOC_LIB_PATH") or os.path.join(_HERE, "libqoc_mi355x.so")
 
 QOC_OK = 0
 QOC_ERR_ARG = -1
