@@ -100,7 +100,9 @@ int qoc_get_states(qoc_ctx* ctx, int seed, int k, double* x_out);       /* k in 
 int qoc_get_costates(qoc_ctx* ctx, int seed, int k, double* lam_out);
 int qoc_get_propagator(qoc_ctx* ctx, int seed, int k, double* U_out);   /* Uk_vec[k+1], k in [0,Nt) */
 /* Histogram of selected (Padé degree, squarings) since the last reset:
- * hist[di*64 + s], di = index of degree in {3,5,7,9,13}.  Used for the FLOP accounting. */
+ * hist[di*64 + s], di = index of degree in {3,5,7,9,13}.  Used for the FLOP accounting.  Under
+ * QOC_CHAIN_TAYLOR (no exponential is formed) it is evaluated at call time from the last propagated u,
+ * counted once per forward pass since the reset. */
 int qoc_pade_histogram(qoc_ctx* ctx, long long* hist, int reset);
 
 /* Exponential algorithm actually executed (no linear solve; same result as the reference's Padé to
@@ -146,9 +148,27 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
 
 /* Engine facts: info[0] = path (0 = LDS-resident kernels, 1 = large-N chunked GEMM pipeline),
  * info[1] = slices per chunk (large-N), info[2] = Newton-Schulz iterations executed so far (large-N),
- * info[3] = device bytes allocated by the context.  QOC_FORCE_LARGE_N=1 in the environment at
- * qoc_create selects the large-N path for any size (testing). */
-int qoc_get_info(qoc_ctx* ctx, long long* info /*[4]*/);
+ * info[3] = device bytes allocated by the context, info[4] = chain mode (QOC_CHAIN_PROPAGATORS /
+ * QOC_CHAIN_TAYLOR), info[5..7] reserved (0).  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
+ * selects the large-N path for any size (testing). */
+int qoc_get_info(qoc_ctx* ctx, long long* info /*[8]*/);
+
+/* How the chains x_{k+1} = U_k x_k (src/gradient_computations.jl:27-29) and λ_k = U_k^H λ_{k+1} (:52-58)
+ * apply the slice exponentials:
+ *   QOC_CHAIN_PROPAGATORS: form every U_k = exp(A_k) (register-resident Taylor / Padé on MFMA, the
+ *     reference's structure), then the serial products;
+ *   QOC_CHAIN_TAYLOR: apply exp(A_k) to the N x m state directly (shifted, truncated Taylor series with the
+ *     degree chosen per slice for a tail <= 2^-53 / 2^-24) — no U_k is formed (qoc_get_propagator computes
+ *     one on demand).  N <= 48 (fp64) / 64 (fp32), nu <= 8;
+ *   QOC_CHAIN_AUTO: Taylor when ||A0 - μ I||_1 <= 1 (few terms per slice), else propagators (the default,
+ *     chosen at qoc_set_generators; QOC_CHAIN=taylor|expm in the environment overrides it).
+ * The states, co-states, J and dJdu agree to rounding either way. */
+#define QOC_CHAIN_AUTO (-1)
+#define QOC_CHAIN_PROPAGATORS 0
+#define QOC_CHAIN_TAYLOR 1
+int qoc_set_chain(qoc_ctx* ctx, int mode);
+/* Taylor terms executed per direction (Σ over slices of P s) since the last reset (QOC_CHAIN_TAYLOR). */
+int qoc_chain_terms(qoc_ctx* ctx, long long* terms, int reset);
 
 /* Standalone ops on the same kernels. */
 /* exponential!(A, ExpMethodHigham2005()) for `count` independent N x N matrices

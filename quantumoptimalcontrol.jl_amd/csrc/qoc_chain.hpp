@@ -153,6 +153,63 @@ __device__ __forceinline__ double swap_sum(double v) {
          __longlong_as_double((long long)(((unsigned long long)ohi << 32) | olo));
 }
 
+// Terminal cost J and the coefficients of λ_N = dJ/dx (src/penalty_fcns.jl:15-42, src/fidelities.jl:48-56,81-137)
+// from x_N (xN(o), o = row + N col, any layout) for one seed; psum = μ Σ_k Σ_{P,C} |x_k|² of this seed (already
+// reduced).  Called by every thread of the workgroup (block reductions).  COST_EXTERNAL: J = psum, coef = 0.
+template <typename T, typename XN>
+__device__ __forceinline__ void chain_costs(int N, int m, const cx<T>* __restrict__ Xt, XN&& xN, int cost_kind,
+                                            double n_norm, double psum, double* red, double* Jout,
+                                            cx<double>* __restrict__ coef) {
+  const int tid = threadIdx.x, nthr = blockDim.x, Nm = N * m;
+  if (cost_kind == COST_TRACE) {
+    double orr = 0, oii = 0;
+    for (int o = tid; o < Nm; o += nthr) {
+      const cx<T> t = Xt[o], v = xN(o);
+      orr += (double)t.r * v.r + (double)t.i * v.i;
+      oii += (double)t.r * v.i - (double)t.i * v.r;
+    }
+    orr = block_sum(orr, red);
+    oii = block_sum(oii, red);
+    if (tid == 0) {
+      const double n2 = n_norm * n_norm;
+      *Jout = 1.0 - (orr * orr + oii * oii) / n2 + psum;
+      for (int c = 0; c < m; ++c) coef[c] = cx<double>{-2.0 * orr / n2, -2.0 * oii / n2};
+    }
+  } else if (cost_kind == COST_ZCAL) {
+    cx<double> mm[4];
+    for (int c = 0; c < 4; ++c) {
+      double orr = 0, oii = 0;
+      for (int i = tid; i < N; i += nthr) {
+        const cx<T> t = Xt[i + N * c], v = xN(i + N * c);
+        orr += (double)t.r * v.r + (double)t.i * v.i;
+        oii += (double)t.r * v.i - (double)t.i * v.r;
+      }
+      mm[c].r = block_sum(orr, red);
+      mm[c].i = block_sum(oii, red);
+    }
+    if (tid == 0) {
+      double F, th;
+      optimal_calibration(mm, 1e-9, &F, &th);
+      *Jout = 1.0 - F * F / 16.0 + psum;
+      const cx<double> e = {cos(th), sin(th)}, em = {cos(th), -sin(th)};
+      const cx<double> v1 = {mm[0].r + e.r * mm[1].r - e.i * mm[1].i, mm[0].i + e.r * mm[1].i + e.i * mm[1].r};
+      const cx<double> v2 = {mm[2].r + e.r * mm[3].r - e.i * mm[3].i, mm[2].i + e.r * mm[3].i + e.i * mm[3].r};
+      const double a1 = sqrt(v1.r * v1.r + v1.i * v1.i), a2 = sqrt(v2.r * v2.r + v2.i * v2.i);
+      const cx<double> g[4] = {{v1.r / a1, v1.i / a1},
+                               {(v1.r * em.r - v1.i * em.i) / a1, (v1.r * em.i + v1.i * em.r) / a1},
+                               {v2.r / a2, v2.i / a2},
+                               {(v2.r * em.r - v2.i * em.i) / a2, (v2.r * em.i + v2.i * em.r) / a2}};
+      const double sc = -2.0 * F / 16.0;
+      for (int c = 0; c < 4; ++c) coef[c] = cx<double>{sc * g[c].r, sc * g[c].i};
+    }
+  } else {
+    if (tid == 0) {
+      *Jout = psum;
+      for (int c = 0; c < m; ++c) coef[c] = cx<double>{0, 0};
+    }
+  }
+}
+
 // One thread's JT elements of a propagator (the four prefetch sets rotate through these).
 template <typename T, int JT>
 struct USet {
@@ -377,56 +434,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
   copy_out(xb + (Nt & 1) * XB, Nt);
   QOC_CT_DUMP();
   const cx<T>* xNp = xb + (Nt & 1) * XB;
-  auto xN = [&](int o) { return xNp[XS * (o / N) + o % N]; };
-  // ---- costs on x_N ----
-  const double psum = block_sum(pen, red) * mu;
-  if (cost_kind == COST_TRACE) {
-    double orr = 0, oii = 0;
-    for (int o = tid; o < Nm; o += CHAIN_THREADS) {
-      const cx<T> t = Xt[o], v = xN(o);
-      orr += (double)t.r * v.r + (double)t.i * v.i;
-      oii += (double)t.r * v.i - (double)t.i * v.r;
-    }
-    orr = block_sum(orr, red);
-    oii = block_sum(oii, red);
-    if (tid == 0) {
-      const double n2 = n_norm * n_norm;
-      Jout[b] = 1.0 - (orr * orr + oii * oii) / n2 + psum;
-      for (int c = 0; c < m; ++c) coef[(size_t)b * m + c] = cx<double>{-2.0 * orr / n2, -2.0 * oii / n2};
-    }
-  } else if (cost_kind == COST_ZCAL) {
-    cx<double> mm[4];
-    for (int c = 0; c < 4; ++c) {
-      double orr = 0, oii = 0;
-      for (int i = tid; i < N; i += CHAIN_THREADS) {
-        const cx<T> t = Xt[i + N * c], v = xN(i + N * c);
-        orr += (double)t.r * v.r + (double)t.i * v.i;
-        oii += (double)t.r * v.i - (double)t.i * v.r;
-      }
-      mm[c].r = block_sum(orr, red);
-      mm[c].i = block_sum(oii, red);
-    }
-    if (tid == 0) {
-      double F, th;
-      optimal_calibration(mm, 1e-9, &F, &th);
-      Jout[b] = 1.0 - F * F / 16.0 + psum;
-      const cx<double> e = {cos(th), sin(th)}, em = {cos(th), -sin(th)};
-      const cx<double> v1 = {mm[0].r + e.r * mm[1].r - e.i * mm[1].i, mm[0].i + e.r * mm[1].i + e.i * mm[1].r};
-      const cx<double> v2 = {mm[2].r + e.r * mm[3].r - e.i * mm[3].i, mm[2].i + e.r * mm[3].i + e.i * mm[3].r};
-      const double a1 = sqrt(v1.r * v1.r + v1.i * v1.i), a2 = sqrt(v2.r * v2.r + v2.i * v2.i);
-      const cx<double> g[4] = {{v1.r / a1, v1.i / a1},
-                               {(v1.r * em.r - v1.i * em.i) / a1, (v1.r * em.i + v1.i * em.r) / a1},
-                               {v2.r / a2, v2.i / a2},
-                               {(v2.r * em.r - v2.i * em.i) / a2, (v2.r * em.i + v2.i * em.r) / a2}};
-      const double sc = -2.0 * F / 16.0;
-      for (int c = 0; c < 4; ++c) coef[(size_t)b * m + c] = cx<double>{sc * g[c].r, sc * g[c].i};
-    }
-  } else {
-    if (tid == 0) {
-      Jout[b] = psum;
-      for (int c = 0; c < m; ++c) coef[(size_t)b * m + c] = cx<double>{0, 0};
-    }
-  }
+  chain_costs<T>(N, m, Xt, [&](int o) { return xNp[XS * (o / N) + o % N]; }, cost_kind, n_norm, block_sum(pen, red) * mu,
+                 red, Jout + b, coef + (size_t)b * m);
 }
 
 template <typename T, int S, int JT, int CB>

@@ -25,6 +25,7 @@
 #include "qoc_grad_rr.hpp"
 #include "qoc_ode.hpp"
 #include "qoc_spline.hpp"
+#include "qoc_tchain.hpp"
 
 using namespace qoc;
 
@@ -106,6 +107,15 @@ struct qoc_ctx {
   int* d_ps = nullptr;   // k_expm_rr pass-2 counter + list of Paterson-Stockmeyer units
   double a0norm = 0.0;   // ||A0||_1 of the generators (host-side, at qoc_set_generators)
   int ncu = 256;         // compute units of the device (persistent-grid sizing)
+  // Taylor-action chains (qoc_tchain.hpp): x_{k+1} = exp(A_k) x_k applied to the state, no U_k formed.
+  // chain_mode 1 selects them (QOC_CHAIN=taylor / expm overrides the automatic choice at qoc_set_generators)
+  int chain_mode = 0;            // 0: propagators (k_expm + k_chain_*), 1: Taylor action (k_tchain_*)
+  bool tchain_ok = false;        // the shape fits the Taylor-action kernels
+  void* d_At = nullptr;          // (nu+1) N x N shifted generators Ã_j = A_j - μ_j I
+  TStep* d_steps = nullptr;      // B x Nt (P, s, e^{μ_k})
+  unsigned long long* d_terms = nullptr;  // Σ P s per forward (executed Taylor terms per direction)
+  TChainParams tprm{};
+  long long props_since_reset = 0;  // forward passes since the last Padé-histogram reset (chain mode 1)
   // exact (Fréchet) gradient mode workspace, allocated on first use
   void* d_fws = nullptr;
   size_t fws_bytes = 0;
@@ -344,10 +354,15 @@ template <typename T>
 int ode_forward(qoc_ctx* c);
 template <typename T>
 int ode_adjoint(qoc_ctx* c);
+template <typename T>
+int tchain_forward(qoc_ctx* c);
+template <typename T>
+int tchain_backward(qoc_ctx* c);
 
 template <typename T>
 int run_forward(qoc_ctx* c) {
   if (c->prop_method == QOC_PROP_TSIT5) return ode_forward<T>(c);
+  if (c->chain_mode == 1) return tchain_forward<T>(c);
   int mk = mark_begin(c, 0);
   hipError_t e = launch_expm(c->prec, c->stream, c->N, c->nu, c->B * c->Nt, c->d_A, c->d_u, nullptr, c->d_U,
                              c->d_hist, nullptr, nullptr, c->expm_alg, c->d_hist + 5 * 64, c->d_ps,
@@ -378,6 +393,9 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
   int mk;
   if (c->prop_method == QOC_PROP_TSIT5) {
     int r = ode_adjoint<T>(c);
+    if (r) return r;
+  } else if (c->chain_mode == 1) {
+    int r = tchain_backward<T>(c);
     if (r) return r;
   } else {
     mk = mark_begin(c, 2);
@@ -1117,6 +1135,219 @@ int ode_adjoint(qoc_ctx* c) {
   return QOC_OK;
 }
 
+// ---- Taylor-action chains (qoc_tchain.hpp) -----------------------------------------------------
+size_t tchain_lds(const qoc_ctx* c) {
+  const TShape sh = tchain_shape(c->N, c->m, c->prec == QOC_FP64);
+  return (size_t)(c->nu + 1) * c->N * c->N * c->esz + (size_t)2 * sh.S * sh.JT * chain_mpad(c->m, sh.CB) * c->esz +
+         64 * sizeof(double);
+}
+
+// k_tchain_* instantiated per (S, JT) x (CB, NP) in {(1, 1), (2, 1), (2, 2), (2, 4)}.
+template <typename T, typename F>
+hipError_t tchain_dispatch(int N, int m, F&& f) {
+  using std::integral_constant;
+  const TShape sh = tchain_shape(N, m, sizeof(T) == 8);
+  auto cbnp = [&](auto S_, auto JT_) -> hipError_t {
+    if (sh.CB == 1 && sh.NP == 1) return f(S_, JT_, integral_constant<int, 1>(), integral_constant<int, 1>());
+    if (sh.CB == 2 && sh.NP == 1) return f(S_, JT_, integral_constant<int, 2>(), integral_constant<int, 1>());
+    if (sh.CB == 2 && sh.NP == 2) return f(S_, JT_, integral_constant<int, 2>(), integral_constant<int, 2>());
+    if (sh.CB == 2 && sh.NP == 4) return f(S_, JT_, integral_constant<int, 2>(), integral_constant<int, 4>());
+    return hipErrorInvalidValue;
+  };
+  if (sh.JT == 4)
+    return sh.S == 4 ? cbnp(integral_constant<int, 4>(), integral_constant<int, 4>())
+                     : cbnp(integral_constant<int, 8>(), integral_constant<int, 4>());
+  if (sh.JT == 10) return cbnp(integral_constant<int, 4>(), integral_constant<int, 10>());
+  if (sh.JT == 12) return cbnp(integral_constant<int, 4>(), integral_constant<int, 12>());
+  if constexpr (sizeof(T) == 4) {
+    if (sh.JT == 16) return cbnp(integral_constant<int, 4>(), integral_constant<int, 16>());
+  }
+  return hipErrorInvalidValue;
+}
+
+TChainArgs tchain_args(qoc_ctx* c) {
+  TChainArgs g{};
+  g.N = c->N;
+  g.m = c->m;
+  g.nu = c->nu;
+  g.Nt = c->Nt;
+  g.At = c->d_At;
+  g.u = c->d_u;
+  g.steps = c->d_steps;
+  g.x0 = c->d_x0;
+  g.x0_per_seed = c->x0_per_seed;
+  g.X = c->d_X;
+  g.L = c->d_L;
+  g.Xt = c->d_Xt;
+  g.cost_kind = c->cost_kind;
+  g.n_norm = c->cost_n;
+  g.pmask = c->mu != 0.0 ? c->d_pmask : nullptr;
+  g.mu = c->mu;
+  g.J = c->d_J;
+  g.coef = c->d_coef;
+  return g;
+}
+
+// fp64: the MFMA formulation (k_tchain_mf_*), one wave per (16-row block, column pair); fp32: the VALU one.
+bool tchain_mf(const qoc_ctx* c) {
+  return c->prec == QOC_FP64 && tchain_mf_kq(c->N) > 0 && tchain_mf_waves(c->N, c->m) <= 16 &&
+         tchain_mf_lds(c->N, c->m, c->nu) <= 160 * 1024;
+}
+template <typename F>
+hipError_t tchain_mf_dispatch(int N, F&& f) {
+  using std::integral_constant;
+  switch (tchain_mf_kq(N)) {
+    case 3: return f(integral_constant<int, 3>());
+    case 4: return f(integral_constant<int, 4>());
+    case 6: return f(integral_constant<int, 6>());
+    case 8: return f(integral_constant<int, 8>());
+    case 10: return f(integral_constant<int, 10>());
+    case 12: return f(integral_constant<int, 12>());
+  }
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+int tchain_forward(qoc_ctx* c) {
+  const long long units = (long long)c->B * c->Nt;
+  int mk = mark_begin(c, 0);
+  const unsigned pb = (unsigned)std::min<long long>((units + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_tchain_prep, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u, c->tprm,
+                     c->d_steps, c->d_terms);
+  mark_end(c, mk);
+  HIPCHK(c, hipGetLastError());
+  const TChainArgs g = tchain_args(c);
+  if (tchain_mf(c)) {
+    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
+    const int threads = 64 * tchain_mf_waves(c->N, c->m);
+    mk = mark_begin(c, 1);
+    hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
+      constexpr int KQ = decltype(KQ_)::value;
+      hipError_t r = hipFuncSetAttribute((const void*)k_tchain_mf_fwd<KQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (r != hipSuccess) return r;
+      hipLaunchKernelGGL((k_tchain_mf_fwd<KQ>), dim3(c->B), dim3(threads), lds, c->stream, g);
+      return hipGetLastError();
+    });
+    mark_end(c, mk);
+    if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_mf_fwd launch: %s", hipGetErrorString(e));
+    c->props_since_reset++;
+    return QOC_OK;
+  }
+  const size_t lds = tchain_lds(c);
+  mk = mark_begin(c, 1);
+  hipError_t e = tchain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_, auto NP_) {
+    constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value,
+                  NP = decltype(NP_)::value;
+    hipError_t r = hipFuncSetAttribute((const void*)k_tchain_fwd<T, S, JT, CB, NP>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL((k_tchain_fwd<T, S, JT, CB, NP>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, g);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_fwd launch: %s", hipGetErrorString(e));
+  c->props_since_reset++;
+  return QOC_OK;
+}
+
+template <typename T>
+int tchain_backward(qoc_ctx* c) {
+  const TChainArgs g = tchain_args(c);
+  if (tchain_mf(c)) {
+    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
+    const int threads = 64 * tchain_mf_waves(c->N, c->m);
+    int mk = mark_begin(c, 2);
+    hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
+      constexpr int KQ = decltype(KQ_)::value;
+      hipError_t r = hipFuncSetAttribute((const void*)k_tchain_mf_bwd<KQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (r != hipSuccess) return r;
+      hipLaunchKernelGGL((k_tchain_mf_bwd<KQ>), dim3(c->B), dim3(threads), lds, c->stream, g);
+      return hipGetLastError();
+    });
+    mark_end(c, mk);
+    if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_mf_bwd launch: %s", hipGetErrorString(e));
+    return QOC_OK;
+  }
+  const size_t lds = tchain_lds(c);
+  int mk = mark_begin(c, 2);
+  hipError_t e = tchain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_, auto NP_) {
+    constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value,
+                  NP = decltype(NP_)::value;
+    hipError_t r = hipFuncSetAttribute((const void*)k_tchain_bwd<T, S, JT, CB, NP>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL((k_tchain_bwd<T, S, JT, CB, NP>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, g);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_bwd launch: %s", hipGetErrorString(e));
+  return QOC_OK;
+}
+
+// Taylor-tail thresholds: θ_P = largest β with Σ_{t>P} β^t / t! <= tol.
+double taylor_tail(double b, int P) {
+  double term = 1.0, sum = 0.0;
+  for (int t = 1; t <= P + 60; ++t) {
+    term *= b / t;
+    if (t > P) sum += term;
+  }
+  return sum;
+}
+void tchain_thresholds(TChainParams& prm, int prec) {
+  const double tol = prec == QOC_FP64 ? std::ldexp(1.0, -53) : std::ldexp(1.0, -24);
+  for (int P = 1; P <= TCHAIN_PMAX; ++P) {
+    double lo = 0.0, hi = 64.0;
+    for (int it = 0; it < 200; ++it) {
+      const double mid = 0.5 * (lo + hi);
+      (taylor_tail(mid, P) <= tol ? lo : hi) = mid;
+    }
+    prm.theta[P] = lo;
+  }
+  prm.theta[0] = 0.0;
+  prm.theta_max = prm.theta[prec == QOC_FP64 ? 24 : 12];
+}
+
+// Scalar shift μ of a generator (column-major interleaved complex, N x N) that minimises ||A - μ I||_1 over a few
+// candidates (0, trace / N, the centre of the diagonal's bounding box); returns the shifted norm.
+double choose_shift(const double* A, int N, double& mr, double& mi) {
+  std::vector<double> off(N, 0.0);
+  double tr_r = 0, tr_i = 0, rmin = 1e300, rmax = -1e300, imin = 1e300, imax = -1e300;
+  for (int col = 0; col < N; ++col) {
+    for (int row = 0; row < N; ++row) {
+      const double re = A[2 * (row + (size_t)N * col)], im = A[2 * (row + (size_t)N * col) + 1];
+      if (row == col) {
+        tr_r += re;
+        tr_i += im;
+        rmin = std::min(rmin, re);
+        rmax = std::max(rmax, re);
+        imin = std::min(imin, im);
+        imax = std::max(imax, im);
+      } else {
+        off[col] += std::hypot(re, im);
+      }
+    }
+  }
+  auto norm = [&](double sr, double si) {
+    double n = 0.0;
+    for (int col = 0; col < N; ++col) {
+      const double re = A[2 * (col + (size_t)N * col)], im = A[2 * (col + (size_t)N * col) + 1];
+      n = std::max(n, off[col] + std::hypot(re - sr, im - si));
+    }
+    return n;
+  };
+  const double cand[3][2] = {{0.0, 0.0}, {tr_r / N, tr_i / N}, {0.5 * (rmin + rmax), 0.5 * (imin + imax)}};
+  double best = 1e300;
+  for (auto& cd : cand) {
+    const double n = norm(cd[0], cd[1]);
+    if (n < best) {
+      best = n;
+      mr = cd[0];
+      mi = cd[1];
+    }
+  }
+  return best;
+}
+
 int forward(qoc_ctx* c) {
   if (c->big) return c->prec == QOC_FP64 ? big_forward<double>(c) : big_forward<float>(c);
   return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
@@ -1219,6 +1450,23 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
     if ((e = hipMalloc(&c->d_gws, 6 * (size_t)N * cols * c->esz)) != hipSuccess) return bail(e, "hipMalloc");
     c->dev_bytes += (2 * nu + 1) * NN * c->esz + 6 * (size_t)N * cols * c->esz;
   }
+  {
+    const TShape sh = tchain_shape(N, m, precision == QOC_FP64);
+    const size_t tl = (size_t)(nu + 1) * NN * c->esz + (size_t)2 * sh.S * sh.JT * chain_mpad(m, sh.CB) * c->esz + 512;
+    const bool valu_ok = sh.JT > 0 && sh.NP > 0 && tl <= 160 * 1024;
+    const bool mf_ok = precision == QOC_FP64 && tchain_mf_kq(N) > 0 && tchain_mf_waves(N, m) <= 16 &&
+                       tchain_mf_lds(N, m, nu) <= 160 * 1024;
+    c->tchain_ok = !c->big && nu <= TCHAIN_NUMAX && (precision == QOC_FP64 ? mf_ok || valu_ok : valu_ok);
+    if (c->tchain_ok) {
+      const size_t bytes[3] = {(nu + 1) * NN * c->esz, (size_t)B * Nt * sizeof(TStep), sizeof(unsigned long long)};
+      void** ptrs[3] = {&c->d_At, (void**)&c->d_steps, (void**)&c->d_terms};
+      for (int i = 0; i < 3; ++i) {
+        if ((e = hipMalloc(ptrs[i], bytes[i])) != hipSuccess) return bail(e, "hipMalloc");
+        c->dev_bytes += bytes[i];
+      }
+      hipMemset(c->d_terms, 0, sizeof(unsigned long long));
+    }
+  }
   if (c->big) {
     // chunk of slices sized to a workspace of <= 8 GiB (and <= 1/8 of what is free)
     size_t freeb = 0, totalb = 0;
@@ -1254,7 +1502,7 @@ void qoc_destroy(qoc_ctx* c) {
   hipSetDevice(c->dev);
   if (c->stream) hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
-                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_ps};
+                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_ps, c->d_At, c->d_steps, c->d_terms};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& m : c->marks) {
@@ -1307,6 +1555,33 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
       nrm = std::max(nrm, sum);
     }
     c->a0norm = nrm;
+  }
+  if (c->tchain_ok) {  // shifted generators Ã_j = A_j - μ_j I and their norms for the Taylor-action chains
+    tchain_thresholds(c->tprm, c->prec);
+    std::vector<double> sh(2 * NN);
+    for (int j = 0; j <= c->nu && r == QOC_OK; ++j) {
+      const double* G = j == 0 ? A0 : Aj[j - 1];
+      double mr = 0, mi = 0;
+      c->tprm.nrm[j] = choose_shift(G, c->N, mr, mi);
+      c->tprm.mur[j] = mr;
+      c->tprm.mui[j] = mi;
+      std::memcpy(sh.data(), G, 2 * NN * sizeof(double));
+      for (int d = 0; d < c->N; ++d) {
+        sh[2 * (d + (size_t)c->N * d)] -= mr;
+        sh[2 * (d + (size_t)c->N * d) + 1] -= mi;
+      }
+      r = upload(c, sh.data(), (char*)c->d_At + j * NN * c->esz, NN);
+      if (r == QOC_OK) HIPCHK(c, hipStreamSynchronize(c->stream));  // sh is reused
+    }
+    if (r != QOC_OK) return r;
+    // the Taylor action wins while the slices need few terms (cavity / zz: ||Ã_0||_1 <= 0.2); large norms
+    // (tunable bus: ~5 after the shift) keep the propagators on MFMA
+    const char* env = getenv("QOC_CHAIN");
+    if (env && !std::strcmp(env, "taylor")) c->chain_mode = 1;
+    else if (env && !std::strcmp(env, "expm")) c->chain_mode = 0;
+    else c->chain_mode = c->tprm.nrm[0] <= 1.0 ? 1 : 0;
+  } else {
+    c->chain_mode = 0;
   }
   c->have_gen = true;
   c->have_prop = false;
@@ -1489,8 +1764,14 @@ int qoc_get_propagator(qoc_ctx* c, int seed, int k, double* U_out) {
   if (c->prop_method == QOC_PROP_TSIT5) return fail(c, QOC_ERR_STATE, "the Tsit5 path does not form propagators");
   if (seed < 0 || seed >= c->B || k < 0 || k >= c->Nt) return fail(c, QOC_ERR_ARG, "index out of range");
   HIPCHK(c, hipSetDevice(c->dev));
-  const size_t NN = (size_t)c->N * c->N;
-  return download(c, (char*)c->d_U + ((size_t)seed * c->Nt + k) * NN * c->esz, U_out, NN);
+  const size_t NN = (size_t)c->N * c->N, unit = (size_t)seed * c->Nt + k;
+  if (c->chain_mode == 1) {  // the Taylor-action chains form no propagators: exp(A_k) of this slice on demand
+    hipError_t e = launch_expm(c->prec, c->stream, c->N, c->nu, 1, c->d_A, c->d_u + unit * c->nu, nullptr,
+                               (char*)c->d_U + unit * NN * c->esz, nullptr, nullptr, nullptr, c->expm_alg,
+                               c->d_hist + 5 * 64, c->d_ps, c->a0norm > 4.0 * kTheta12);
+    if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm (propagator on demand): %s", hipGetErrorString(e));
+  }
+  return download(c, (char*)c->d_U + unit * NN * c->esz, U_out, NN);
 }
 
 int qoc_set_profiling(qoc_ctx* c, int enable) {
@@ -1691,6 +1972,31 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[1] = c->chunk;
   info[2] = c->ns_iters;
   info[3] = (long long)c->dev_bytes;
+  info[4] = c->chain_mode;
+  return QOC_OK;
+}
+
+int qoc_set_chain(qoc_ctx* c, int mode) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  if (mode != QOC_CHAIN_AUTO && mode != QOC_CHAIN_PROPAGATORS && mode != QOC_CHAIN_TAYLOR)
+    return fail(c, QOC_ERR_ARG, "unknown chain mode %d", mode);
+  if (mode == QOC_CHAIN_TAYLOR && !c->tchain_ok)
+    return fail(c, QOC_ERR_UNSUPPORTED, "Taylor-action chains need N <= 48 (fp64) / 64 (fp32), nu <= 8 and the "
+                                        "generators within the 160 KiB LDS");
+  if (mode == QOC_CHAIN_AUTO) mode = c->tchain_ok && c->have_gen && c->tprm.nrm[0] <= 1.0 ? 1 : 0;
+  c->chain_mode = mode;
+  c->have_prop = false;
+  return QOC_OK;
+}
+
+int qoc_chain_terms(qoc_ctx* c, long long* terms, int reset) {
+  if (!c || !terms) return fail(c, QOC_ERR_ARG, "null argument");
+  *terms = 0;
+  if (!c->d_terms) return QOC_OK;
+  HIPCHK(c, hipSetDevice(c->dev));
+  HIPCHK(c, hipMemcpyAsync(terms, c->d_terms, sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+  if (reset) HIPCHK(c, hipMemsetAsync(c->d_terms, 0, sizeof(long long), c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return QOC_OK;
 }
 
@@ -1708,6 +2014,28 @@ int qoc_taylor_histogram(qoc_ctx* c, long long* hist, int reset) {
 int qoc_pade_histogram(qoc_ctx* c, long long* hist, int reset) {
   if (!c || !hist) return fail(c, QOC_ERR_ARG, "null argument");
   HIPCHK(c, hipSetDevice(c->dev));
+  if (c->chain_mode == 1 && c->prop_method == QOC_PROP_EXPM) {
+    // no exponentials ran: the Padé choice for the last propagated u, once per forward pass since the last reset
+    std::memset(hist, 0, 5 * 64 * sizeof(long long));
+    if (c->props_since_reset > 0 && c->have_gen) {
+      HIPCHK(c, hipMemsetAsync(c->d_hist, 0, 5 * 64 * sizeof(long long), c->stream));
+      const long long units = (long long)c->B * c->Nt;
+      const unsigned blocks = (unsigned)std::min<long long>((units + 3) / 4, 8192);
+      if (c->prec == QOC_FP64)
+        hipLaunchKernelGGL((k_pade_units<double>), dim3(blocks), dim3(256), 0, c->stream, c->N, c->nu, units,
+                           (const cx<double>*)c->d_A, (const double*)c->d_u, c->d_hist);
+      else
+        hipLaunchKernelGGL((k_pade_units<float>), dim3(blocks), dim3(256), 0, c->stream, c->N, c->nu, units,
+                           (const cx<float>*)c->d_A, (const double*)c->d_u, c->d_hist);
+      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, hipMemcpyAsync(hist, c->d_hist, 5 * 64 * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->d_hist, 0, 5 * 64 * sizeof(long long), c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      for (int i = 0; i < 5 * 64; ++i) hist[i] *= c->props_since_reset;
+    }
+    if (reset) c->props_since_reset = 0;
+    return QOC_OK;
+  }
   HIPCHK(c, hipMemcpyAsync(hist, c->d_hist, 5 * 64 * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
   if (reset) HIPCHK(c, hipMemsetAsync(c->d_hist, 0, 5 * 64 * sizeof(long long), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

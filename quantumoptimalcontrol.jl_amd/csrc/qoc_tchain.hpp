@@ -1,0 +1,813 @@
+// qoc_tchain.hpp — propagation by the action of the slice exponential ("Taylor-action chains").
+//
+// The reference forms every propagator U_k = exponential!(A_k) (src/gradient_computations.jl:17-25) and then
+// uses it only in the serial chains x_{k+1} = U_k x_k (:27-29) and λ_k = U_k^H λ_{k+1} (:52-58).  With m << N
+// state columns (cavity m = 2, zz m = 4) forming U_k costs ~4 N^3 CMAC per slice while its action on the state
+// costs P N^2 m (P ~ 10-13 Taylor terms).  These kernels apply the exponential to the state directly:
+//
+//   exp(A_k) v = e^{μ_k} (exp(Ã_k / s))^s v,   Ã_k = A_k - μ_k I = Ã_0 + Σ_j u_jk Ã_j,
+//   exp(Ã/s) v ≈ Σ_{t <= P} (Ã/s)^t v / t!   (Horner-free: z_t = (Ã/s) z_{t-1} / t, acc += z_t)
+//
+// with Ã_j = A_j - μ_j I (host-chosen scalar shifts that shrink ||Ã_j||_1; e^{μ} is an exact scalar factor)
+// and (P, s) from the bound β_k = ||Ã_0||_1 + Σ_j |u_jk| ||Ã_j||_1 >= ||Ã_k||_1: s = ⌈β_k / θ_max⌉ and the
+// smallest P whose Taylor tail Σ_{t>P} (β/s)^t / t! is <= 2^-53 (fp64) / 2^-24 (fp32) — the same backward
+// error bound the reference's Padé selection meets (ExpMethodHigham2005), so x_k and λ_k agree with the
+// reference's U_k products to rounding.  The backward sweep uses exp(A)^H = conj(e^{μ}) exp(Ã^H).
+//
+// One workgroup per seed (the time axis is a serial recurrence).  Thread layout (as the propagator chains,
+// qoc_chain.hpp): a thread owns output row i and part p of the inner index j = p + S q (q < JT); its JT
+// elements of Ã_k are formed each step from the generators (LDS) into registers, and each Taylor term is one
+// matvec with the state read from LDS (broadcast), a register reduction over the S parts, and one barrier.
+// No propagator is ever written: per slice the HBM traffic is the state (and u), not 16 N^2 bytes of U_k.
+#pragma once
+#include "qoc_chain.hpp"
+
+namespace qoc {
+
+// Diagnostic cycle stamps of the term loop (tools/tchain_probe.hip builds with -DQOC_PROBE; empty otherwise).
+#ifdef QOC_PROBE
+__device__ unsigned long long g_tc[16];
+#define TC_T(var)                                                                \
+  unsigned long long var;                                                        \
+  do {                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+  } while (0)
+#define TC_ADD(slot, v) \
+  do {                  \
+    if (blockIdx.x == 7 && threadIdx.x == 0) g_tc[slot] += (v); \
+  } while (0)
+#else
+#define TC_T(var) \
+  do {            \
+  } while (0)
+#define TC_ADD(slot, v) \
+  do {                  \
+  } while (0)
+#endif
+
+// Per-(seed, slice) step data written by k_tchain_prep: e^{μ_k} and the (P, s) choice.
+struct TStep {
+  double pr, pi;  // e^{μ_k}
+  int P, s;       // Taylor terms per substep, substeps
+  double pad;     // 32-byte records (two 16-byte loads)
+};
+
+constexpr int TCHAIN_PMAX = 30;  // thresholds θ_P for P = 1..TCHAIN_PMAX
+constexpr int TCHAIN_NUMAX = 8;  // controls per slice the Taylor-action chains take
+
+// Per-step inputs of the chains (TStep + u_k), fetched one step ahead through VECTOR loads: scalar loads would
+// miss the scalar cache on every new step (an L2 / HBM round trip on the critical path), and an outstanding
+// scalar load shares lgkmcnt with the LDS traffic of the Taylor terms, forcing lgkmcnt(0) drains there.
+struct TPre {
+  double pr, pi;
+  int P, s;
+  double u[TCHAIN_NUMAX];
+};
+__device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const double* __restrict__ uk, int nu, TPre& d) {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // per-lane (VGPR) address: global_load, not s_load
+  const double4 v = *reinterpret_cast<const double4*>(reinterpret_cast<const double*>(st) + z);
+  d.pr = v.x;
+  d.pi = v.y;
+  const long long ps = __double_as_longlong(v.z);
+  d.P = (int)(ps & 0xffffffff);
+  d.s = (int)(ps >> 32);
+#pragma unroll
+  for (int j = 0; j < TCHAIN_NUMAX; ++j) d.u[j] = j < nu ? uk[j + z] : 0.0;
+}
+
+struct TChainParams {
+  double nrm[9];              // ||Ã_j||_1, j = 0..nu
+  double mur[9], mui[9];      // shifts μ_j
+  double theta[TCHAIN_PMAX + 1];  // θ_P: largest β whose degree-P Taylor tail is within tolerance (θ_0 unused)
+  double theta_max;           // substep bound (β / s <= theta_max)
+};
+
+// (P, s, e^{μ}) per unit, plus Σ P s (executed Taylor terms per direction) for the roofline accounting.
+__global__ void k_tchain_prep(int nu, long long units, const double* __restrict__ u, const TChainParams prm,
+                              TStep* __restrict__ steps, unsigned long long* __restrict__ terms) {
+  unsigned long long cnt = 0;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < units; e += (long long)gridDim.x * blockDim.x) {
+    double beta = prm.nrm[0], mr = prm.mur[0], mi = prm.mui[0];
+    for (int j = 0; j < nu; ++j) {
+      const double uj = u[e * nu + j];
+      beta += fabs(uj) * prm.nrm[j + 1];
+      mr += uj * prm.mur[j + 1];
+      mi += uj * prm.mui[j + 1];
+    }
+    int s = 1;
+    if (beta > prm.theta_max) {
+      s = (int)ceil(beta / prm.theta_max);
+      beta /= s;
+    }
+    int P = 1;
+    while (P < TCHAIN_PMAX && prm.theta[P] < beta) ++P;
+    const double er = exp(mr);
+    steps[e] = TStep{er * cos(mi), er * sin(mi), P, s, 0.0};
+    cnt += (unsigned long long)(P * s);
+  }
+  // one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(terms, cnt);
+}
+
+struct TChainArgs {
+  int N, m, nu, Nt;
+  const void* At;          // (nu+1) N x N shifted generators Ã_j, column-major (device precision)
+  const double* u;         // B x Nt x nu
+  const TStep* steps;      // B x Nt
+  const void* x0;          // N x m or B x N x m
+  int x0_per_seed;
+  void* X;                 // B x (Nt+1) x N x m states
+  void* L;                 // B x (Nt+1) x N x m co-states
+  const void* Xt;          // N x m target
+  int cost_kind;
+  double n_norm;
+  const unsigned char* pmask;  // N x m state-penalty mask (nullptr: no penalty)
+  double mu;
+  double* J;               // B
+  cx<double>* coef;        // B x m
+};
+
+// Thread layout of the Taylor-action chains.  Waves split the rows into G blocks of R = 64 / S rows and the
+// columns into CGN groups (G = 1: 4 groups, G = 2: 2, else 1); each computing wave walks its columns in
+// blocks of CB (NP blocks at most).  Host-side selection: tchain_shape().
+struct TShape {
+  int S, JT, CB, NP;
+};
+__host__ __device__ inline TShape tchain_shape(int N, int m, bool fp64) {
+  const int S = N <= 16 ? 4 : N <= 32 ? 8 : 4;
+  const int R = 64 / S, G = (N + R - 1) / R, CGN = G == 1 ? 4 : G == 2 ? 2 : 1;
+  const int JT = N <= 16 ? 4 : N <= 32 ? 4 : N <= 40 ? 10 : N <= 48 ? 12 : (fp64 ? 0 : 16);
+  const int cpw = (m + CGN - 1) / CGN;  // columns per computing wave
+  const int CB = JT >= 10 ? (cpw >= 2 ? 2 : 1) : (cpw >= 2 ? 2 : 1);
+  const int NP = (cpw + CB - 1) / CB;
+  return {S, JT, CB, NP <= 1 ? 1 : NP <= 2 ? 2 : NP <= 4 ? 4 : 0};  // NP 0: outside the envelope
+}
+
+template <typename T, int S, int JT, int CB, int NP>
+struct TChain {
+  static constexpr int XS = S * JT;  // LDS state column stride (rows >= N held at zero)
+  static constexpr int R = 64 / S;   // rows per wave
+  // N <= 16 (S = 4, JT = 4): every row of a column lives in one wave and the columns are split over the
+  // waves, so a wave only ever reads back what it wrote itself — LDS operations of one wave complete in
+  // order, and no workgroup barrier is needed between Taylor terms.
+  static constexpr bool SOLO = S == 4 && JT == 4;
+  static __device__ __forceinline__ void sync() {
+    if constexpr (SOLO) {
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      lds_barrier();
+    }
+  }
+  int i, p, c_begin, c_step;
+  bool act, busy;
+
+  __device__ __forceinline__ void setup(int N) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int G = (N + R - 1) / R, CGN = G == 1 ? 4 : G == 2 ? 2 : 1;
+    const int rb = w % G, cg = w / G;
+    i = rb * R + l % R;
+    p = l / R;
+    busy = w < G * CGN;
+    act = busy && i < N;
+    c_begin = busy ? cg * CB : 1 << 20;
+    c_step = CGN * CB;
+  }
+  // sum over the S parts of a row (lane offsets R, 2R, ..): row rotations, then row / half swaps
+  __device__ __forceinline__ T psum(T v) const {
+    if (R <= 8) v += dpp_mov<0x128>(v);  // row_ror:8
+    if (R <= 4) v += dpp_mov<0x124>(v);  // row_ror:4
+    return swap_sum<32>(swap_sum<16>(v));
+  }
+  // a[q] = Ã_k[i, p + S q] (forward) from the generators in LDS (column-major: G_j[r + N c]); the backward
+  // kernels keep the conjugate transposes there, so the same read gives Ã_k^H.  Zero outside N x N.
+  __device__ __forceinline__ void form(int N, int nu, const cx<T>* __restrict__ gen, const double (&uk)[TCHAIN_NUMAX],
+                                       T scale, cx<T> (&a)[JT]) const {
+    const int NN = N * N, ic = min(i, N - 1);
+#pragma unroll
+    for (int q = 0; q < JT; ++q) a[q] = gen[ic + N * min(p + S * q, N - 1)];
+#pragma unroll
+    for (int j = 0; j < TCHAIN_NUMAX; ++j) {
+      if (j >= nu) break;
+      const T uj = (T)uk[j];
+      const cx<T>* Gj = gen + (size_t)(j + 1) * NN;
+#pragma unroll
+      for (int q = 0; q < JT; ++q) {
+        const cx<T> g = Gj[ic + N * min(p + S * q, N - 1)];
+        a[q].r += uj * g.r;
+        a[q].i += uj * g.i;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < JT; ++q) {
+      const bool ok = act && p + S * q < N;
+      a[q].r = ok ? a[q].r * scale : T(0);
+      a[q].i = ok ? a[q].i * scale : T(0);
+    }
+  }
+  // z[b] = Σ_j a_j y[j, c0 + b] over all parts (every lane of the row gets the sum)
+  __device__ __forceinline__ void matvec(const cx<T> (&a)[JT], const cx<T>* __restrict__ ys, int c0, cx<T> (&z)[CB]) const {
+    cx<T> yv[CB][JT];
+#pragma unroll
+    for (int b = 0; b < CB; ++b)
+#pragma unroll
+      for (int q = 0; q < JT; ++q) yv[b][q] = ys[XS * (c0 + b) + p + S * q];
+    T ar0[CB], ai0[CB], ar1[CB], ai1[CB];
+#pragma unroll
+    for (int b = 0; b < CB; ++b) ar0[b] = ai0[b] = ar1[b] = ai1[b] = T(0);
+#pragma unroll
+    for (int q = 0; q < JT; ++q)
+#pragma unroll
+      for (int b = 0; b < CB; ++b) {
+        const cx<T> y = yv[b][q];
+        T& ar = (q & 1) ? ar1[b] : ar0[b];
+        T& ai = (q & 1) ? ai1[b] : ai0[b];
+        ar = fma(a[q].r, y.r, ar);
+        ai = fma(a[q].r, y.i, ai);
+        ar = fma(-a[q].i, y.i, ar);
+        ai = fma(a[q].i, y.r, ai);
+      }
+#pragma unroll
+    for (int b = 0; b < CB; ++b) {
+      z[b].r = psum(ar0[b] + ar1[b]);
+      z[b].i = psum(ai0[b] + ai1[b]);
+    }
+  }
+
+  // One slice: state y (LDS buffer `cur`, rows >= N zero) -> e^{μ} exp(Ã/s)^s y, left in buffer `cur` on return
+  // and in acc (this lane's rows / columns).  Per substep P barriers.  `ph`: e^{μ} (forward) or its conjugate.
+  __device__ __forceinline__ void step(int N, int m, const cx<T> (&a)[JT], cx<T>* __restrict__ yb, int XB, int& cur,
+                                       int P, int s, cx<double> ph, cx<T> (&acc)[NP][CB]) const {
+    for (int sub = 0; sub < s; ++sub) {
+      const cx<T>* y0 = yb + cur * XB;
+#pragma unroll
+      for (int ps = 0; ps < NP; ++ps) {
+        const int c0 = c_begin + c_step * ps;
+#pragma unroll
+        for (int b = 0; b < CB; ++b) acc[ps][b] = (c0 < m) ? y0[XS * (c0 + b) + min(i, XS - 1)] : cx<T>{0, 0};
+      }
+      for (int t = 1; t <= P; ++t) {
+        TC_T(t0);
+        const cx<T>* ys = yb + cur * XB;
+        cx<T>* yn = yb + (cur ^ 1) * XB;
+        // 1/t in registers: a scalar-memory table read here would share lgkmcnt with the LDS reads and make
+        // the compiler drain all of them (lgkmcnt(0)) before the first FMA
+        const T inv = T(1) / (T)t;
+#pragma unroll
+        for (int ps = 0; ps < NP; ++ps) {
+          const int c0 = c_begin + c_step * ps;
+          if (c0 < m) {
+            cx<T> z[CB];
+            matvec(a, ys, c0, z);
+            TC_T(t1);
+            TC_ADD(0, t1 - t0);
+#pragma unroll
+            for (int b = 0; b < CB; ++b) {
+              z[b].r *= inv;
+              z[b].i *= inv;
+              acc[ps][b].r += z[b].r;
+              acc[ps][b].i += z[b].i;
+              if (t < P && act && p == 0 && c0 + b < m) yn[XS * (c0 + b) + i] = z[b];
+            }
+          }
+        }
+        TC_T(t2);
+        if (t < P) {
+          sync();
+          cur ^= 1;
+        }
+        TC_T(t3);
+        TC_ADD(1, t2 - t0);
+        TC_ADD(2, t3 - t2);
+        TC_ADD(3, 1);
+      }
+      // substep result -> the buffer the last term did not read (its readers passed the previous barrier)
+      const bool last = sub == s - 1;
+      cx<T>* yn = yb + (cur ^ 1) * XB;
+#pragma unroll
+      for (int ps = 0; ps < NP; ++ps) {
+        const int c0 = c_begin + c_step * ps;
+#pragma unroll
+        for (int b = 0; b < CB; ++b) {
+          if (last) {
+            const cx<T> v = acc[ps][b];
+            acc[ps][b] = cx<T>{(T)(ph.r * v.r - ph.i * v.i), (T)(ph.r * v.i + ph.i * v.r)};
+          }
+          if (act && p == 0 && c0 < m && c0 + b < m) yn[XS * (c0 + b) + i] = acc[ps][b];
+        }
+      }
+      sync();
+      cur ^= 1;
+    }
+  }
+};
+
+// x_{k+1} = exp(A_k) x_k for every slice of one seed (src/gradient_computations.jl:27-29), states -> HBM, then
+// the terminal cost (+ state penalty) as k_chain_fwd.
+template <typename T, int S, int JT, int CB, int NP>
+__global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_fwd(const TChainArgs g) {
+  using C = TChain<T, S, JT, CB, NP>;
+  constexpr int XS = C::XS;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, b = blockIdx.x, tid = threadIdx.x;
+  const int NN = N * N, Nm = N * m, XB = XS * chain_mpad(m, CB);
+  cx<T>* gen = reinterpret_cast<cx<T>*>(smem);
+  cx<T>* yb = gen + (size_t)(nu + 1) * NN;
+  double* red = reinterpret_cast<double*>(yb + 2 * XB);
+  const cx<T>* At = (const cx<T>*)g.At;
+  const cx<T>* x0b = (const cx<T>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0);
+  cx<T>* Xb = (cx<T>*)g.X + (size_t)b * (Nt + 1) * Nm;
+  const double* ub = g.u + (size_t)b * Nt * nu;
+  const TStep* stb = g.steps + (size_t)b * Nt;
+  C rg;
+  rg.setup(N);
+  for (int e = tid; e < (nu + 1) * NN; e += CHAIN_THREADS) gen[e] = At[e];
+  for (int e = tid; e < 2 * XB; e += CHAIN_THREADS) {
+    const int c = (e % XB) / XS, r = e % XS;
+    yb[e] = e < XB && r < N && c < m ? x0b[r + N * c] : cx<T>{0, 0};
+  }
+  // this lane's state elements: columns c_begin + c_step ps + bb of row i (written by p == 0 lanes)
+  bool own[NP][CB], pen_m[NP][CB];
+#pragma unroll
+  for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+    for (int bb = 0; bb < CB; ++bb) {
+      const int c = rg.c_begin + rg.c_step * ps + bb;
+      own[ps][bb] = rg.act && rg.p == 0 && c < m;
+      pen_m[ps][bb] = own[ps][bb] && g.pmask && g.pmask[rg.i + N * c];
+    }
+  double pen = 0.0;
+  auto store = [&](const cx<T> (&v)[NP][CB], int k_) __attribute__((always_inline)) {
+    cx<T>* Xk = Xb + (size_t)k_ * Nm;
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+      for (int bb = 0; bb < CB; ++bb)
+        if (own[ps][bb]) {
+          Xk[rg.i + N * (rg.c_begin + rg.c_step * ps + bb)] = v[ps][bb];
+          if (pen_m[ps][bb]) pen += (double)v[ps][bb].r * v[ps][bb].r + (double)v[ps][bb].i * v[ps][bb].i;
+        }
+  };
+  __syncthreads();
+  cx<T> acc[NP][CB];
+#pragma unroll
+  for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+    for (int bb = 0; bb < CB; ++bb) {
+      const int c = rg.c_begin + rg.c_step * ps + bb;
+      acc[ps][bb] = c < m ? yb[XS * c + min(rg.i, XS - 1)] : cx<T>{0, 0};
+    }
+  store(acc, 0);
+  int cur = 0;
+  TPre nx;
+  tpre_load(stb, ub, nu, nx);
+  for (int k = 0; k < Nt; ++k) {
+    const TPre st = nx;
+    if (k + 1 < Nt) tpre_load(stb + k + 1, ub + (size_t)(k + 1) * nu, nu, nx);
+    const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
+    cx<T> a[JT];
+    rg.form(N, nu, gen, st.u, ns > 1 ? (T)(1.0 / ns) : T(1), a);
+    rg.step(N, m, a, yb, XB, cur, P, ns, cx<double>{st.pr, st.pi}, acc);
+    store(acc, k + 1);
+  }
+  __syncthreads();  // SOLO shapes skip the per-term barriers: x_N of every wave visible to all
+  const cx<T>* xNp = yb + cur * XB;
+  chain_costs<T>(N, m, (const cx<T>*)g.Xt, [&](int o) { return xNp[XS * (o / N) + o % N]; }, g.cost_kind, g.n_norm,
+                 block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * m);
+}
+
+// λ_k = exp(A_k)^H λ_{k+1} + dL/dx(x_k) for every slice of one seed (src/gradient_computations.jl:46-58); the
+// generators in LDS are the conjugate transposes Ã_j^H.
+template <typename T, int S, int JT, int CB, int NP>
+__global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_bwd(const TChainArgs g) {
+  using C = TChain<T, S, JT, CB, NP>;
+  constexpr int XS = C::XS;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, b = blockIdx.x, tid = threadIdx.x;
+  const int NN = N * N, Nm = N * m, XB = XS * chain_mpad(m, CB);
+  cx<T>* gen = reinterpret_cast<cx<T>*>(smem);
+  cx<T>* yb = gen + (size_t)(nu + 1) * NN;
+  const cx<T>* At = (const cx<T>*)g.At;
+  const cx<T>* Xb = (const cx<T>*)g.X + (size_t)b * (Nt + 1) * Nm;
+  cx<T>* Lb = (cx<T>*)g.L + (size_t)b * (Nt + 1) * Nm;
+  const cx<T>* Xt = (const cx<T>*)g.Xt;
+  const double* ub = g.u + (size_t)b * Nt * nu;
+  const TStep* stb = g.steps + (size_t)b * Nt;
+  const T tmu = (T)(2.0 * g.mu);
+  C rg;
+  rg.setup(N);
+  for (int e = tid; e < (nu + 1) * NN; e += CHAIN_THREADS) {
+    const int j = e / NN, rc = e - j * NN, r = rc % N, c = rc / N;
+    const cx<T> v = At[(size_t)j * NN + c + N * r];  // (Ã_j^H)[r, c] = conj(Ã_j[c, r])
+    gen[e] = cx<T>{v.r, -v.i};
+  }
+  // λ_{Nt} = dJfinal/dx(x_N) (+ dL/dx(x_N)) -> buffer 0, also to HBM
+  for (int e = tid; e < 2 * XB; e += CHAIN_THREADS) {
+    const int c = (e % XB) / XS, r = e % XS, o = r + N * c;
+    cx<T> v = {0, 0};
+    if (e < XB && r < N && c < m) {
+      if (g.cost_kind == COST_EXTERNAL) {
+        v = Lb[(size_t)Nt * Nm + o];
+      } else {
+        const cx<double> cf = g.coef[(size_t)b * m + c];
+        const cx<T> t = Xt[o];
+        v.r = (T)(cf.r * t.r - cf.i * t.i);
+        v.i = (T)(cf.r * t.i + cf.i * t.r);
+      }
+      if (g.pmask && g.pmask[o]) {
+        const cx<T> xv = Xb[(size_t)Nt * Nm + o];
+        v.r += tmu * xv.r;
+        v.i += tmu * xv.i;
+      }
+      Lb[(size_t)Nt * Nm + o] = v;
+    }
+    yb[e] = v;
+  }
+  bool own[NP][CB], pen_m[NP][CB];
+#pragma unroll
+  for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+    for (int bb = 0; bb < CB; ++bb) {
+      const int c = rg.c_begin + rg.c_step * ps + bb;
+      own[ps][bb] = rg.act && rg.p == 0 && c < m;
+      pen_m[ps][bb] = own[ps][bb] && g.pmask && g.pmask[rg.i + N * c];
+    }
+  __syncthreads();
+  int cur = 0;
+  cx<T> acc[NP][CB];
+  TPre nx;
+  tpre_load(stb + Nt - 1, ub + (size_t)(Nt - 1) * nu, nu, nx);
+  for (int k = Nt - 1; k >= 0; --k) {
+    const TPre st = nx;
+    if (k > 0) tpre_load(stb + k - 1, ub + (size_t)(k - 1) * nu, nu, nx);
+    const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
+    cx<T> xk[NP][CB];  // x_k for the penalty (loaded ahead of the Taylor terms)
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+      for (int bb = 0; bb < CB; ++bb)
+        xk[ps][bb] = pen_m[ps][bb] ? Xb[(size_t)k * Nm + rg.i + N * (rg.c_begin + rg.c_step * ps + bb)] : cx<T>{0, 0};
+    cx<T> a[JT];
+    rg.form(N, nu, gen, st.u, ns > 1 ? (T)(1.0 / ns) : T(1), a);
+    rg.step(N, m, a, yb, XB, cur, P, ns, cx<double>{st.pr, -st.pi}, acc);
+    cx<T>* Lk = Lb + (size_t)k * Nm;
+    bool any_pen = false;
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+      for (int bb = 0; bb < CB; ++bb) {
+        if (pen_m[ps][bb]) {
+          acc[ps][bb].r += tmu * xk[ps][bb].r;
+          acc[ps][bb].i += tmu * xk[ps][bb].i;
+          any_pen = true;
+          yb[cur * XB + XS * (rg.c_begin + rg.c_step * ps + bb) + rg.i] = acc[ps][bb];
+        }
+        if (own[ps][bb]) Lk[rg.i + N * (rg.c_begin + rg.c_step * ps + bb)] = acc[ps][bb];
+      }
+    if (g.pmask) {  // the penalised entries of the state changed after the step's last barrier
+      (void)any_pen;
+      C::sync();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// fp64: the Taylor terms on v_mfma_f64_4x4x4_4b.  One wave per (16-row block, column pair): the four blocks of
+// the instruction are the wave's four row quads, K runs over the k-quads, so no cross-lane reduction is needed.
+// Complex arithmetic as two real products into one accumulator: with B = [yr0, yi0, yr1, yi1] (the column pair,
+// one real column per n) and B' = [-yi0, yr0, -yi1, yr1],  Ar B + Ai B' = [Re, Im, Re, Im] of A y.  The state
+// lives in LDS twice (y and y') so that both operands are plain ds_read_b64s.  With one wave per SIMD an fp64
+// VALU instruction issues every ~8 cycles; a 4x4x4 MFMA does 256 FMAs in 16, so the matvec runs at ~4x the
+// VALU formulation's issue rate and the part sums disappear.
+// Lane roles (tools/mfma4_layout.hip): A[m][k] at lane m + 4b + 16k, B[k][n] at n + 4b + 16k, D[m][n] at
+// n + 4b + 16m (b = (l >> 2) & 3).
+// ---------------------------------------------------------------------------------------------------------
+__host__ __device__ inline int tchain_mf_kq(int N) {  // k-quads per product, bucketed (zero padding is exact)
+  const int q = (N + 3) / 4;
+  return q <= 3 ? 3 : q <= 4 ? 4 : q <= 6 ? 6 : q <= 8 ? 8 : q <= 10 ? 10 : q <= 12 ? 12 : 0;
+}
+__host__ __device__ inline int tchain_mf_waves(int N, int m) { return ((N + 15) / 16) * ((m + 1) / 2); }
+__host__ inline size_t tchain_mf_lds(int N, int m, int nu) {
+  const int KQ = tchain_mf_kq(N), CP = (m + 1) / 2;
+  return (size_t)(nu + 1) * N * N * 16 + (size_t)2 * 2 * CP * 4 * KQ * 4 * 8 + 64 * 8;
+}
+
+template <int KQ>
+struct TChainMF {
+  static constexpr int RP = 4 * KQ;  // padded rows of the LDS state
+  int rowA, rowD, n, kl, cp, G, CP;
+  bool solo;  // one row block (N <= 16): each wave owns its column pair outright, no workgroup barriers
+  bool actD;  // this lane's D element is a real state entry (row < N, column < m)
+  int colD;   // complex column of the D element
+
+  __device__ __forceinline__ void setup(int N, int m) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    G = (N + 15) / 16;
+    CP = (m + 1) / 2;
+    solo = G == 1;
+    const int rb = w % G;
+    cp = w / G;
+    const int blk = (l >> 2) & 3;
+    rowA = 16 * rb + 4 * blk + (l & 3);
+    kl = l >> 4;
+    rowD = 16 * rb + 4 * blk + (l >> 4);
+    n = l & 3;
+    colD = 2 * cp + (n >> 1);
+    actD = rowD < N && colD < m;
+  }
+  // LDS state: [buf][y | y'][cp][RP rows][4]
+  static __device__ __forceinline__ double* ybuf(double* yb, int CP, int buf, int prime) {
+    return yb + (size_t)((buf * 2 + prime) * CP) * RP * 4;
+  }
+  // a = Ã_k (or its conjugate transpose, whichever the LDS generators hold) at A-operand positions
+  __device__ __forceinline__ void form(int N, int nu, const cx<double>* __restrict__ gen, const double (&uk)[TCHAIN_NUMAX],
+                                       double scale, double (&ar)[KQ], double (&ai)[KQ]) const {
+    const int NN = N * N, rc = min(rowA, N - 1);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      const cx<double> v = gen[rc + N * min(4 * q + kl, N - 1)];
+      ar[q] = v.r;
+      ai[q] = v.i;
+    }
+#pragma unroll
+    for (int j = 0; j < TCHAIN_NUMAX; ++j) {
+      if (j >= nu) break;
+      const double uj = uk[j];
+      const cx<double>* Gj = gen + (size_t)(j + 1) * NN;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        const cx<double> v = Gj[rc + N * min(4 * q + kl, N - 1)];
+        ar[q] += uj * v.r;
+        ai[q] += uj * v.i;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      const bool ok = rowA < N && 4 * q + kl < N;
+      ar[q] = ok ? ar[q] * scale : 0.0;
+      ai[q] = ok ? ai[q] * scale : 0.0;
+    }
+  }
+  // D = A y for this wave's rows and column pair (y from buffer `buf`)
+  __device__ __forceinline__ double matvec(const double (&ar)[KQ], const double (&ai)[KQ], const double* __restrict__ y,
+                                           const double* __restrict__ yp) const {
+    double bv[KQ], bp[KQ];
+    const int base = (cp * RP + kl) * 4 + n;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) bv[q] = y[base + 16 * q];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) bp[q] = yp[base + 16 * q];
+    // two accumulation chains, alternating, so consecutive MFMAs never depend on each other; the Ar products
+    // first (their operands arrive first)
+    double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      double& d = (q & 1) ? d1 : d0;
+      d = MF<double>::mma4(ar[q], bv[q], d);
+    }
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      double& d = ((q + KQ) & 1) ? d1 : d0;
+      d = MF<double>::mma4(ai[q], bp[q], d);
+    }
+    return d0 + d1;
+  }
+  // write this lane's element v (re or im of its complex entry) into y and its rotated copy into y'
+  __device__ __forceinline__ void put(double* y, double* yp, double v) const {
+    if (rowD < RP) {
+      const int o = (cp * RP + rowD) * 4;
+      y[o + n] = v;
+      yp[o + (n ^ 1)] = (n & 1) ? -v : v;  // y' = [-yi, yr]: re (n even) -> slot n+1 as is; im -> slot n-1 negated
+    }
+  }
+  __device__ __forceinline__ void sync() const {
+    if (solo) {  // LDS operations of one wave complete in order
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      lds_barrier();
+    }
+  }
+
+  // One slice (see TChain::step); acc = this lane's D element of the state.
+  __device__ __forceinline__ void step(int N, const double (&ar)[KQ], const double (&ai)[KQ], double* yb,
+                                       const double* __restrict__ invt, int& cur, int P, int s, cx<double> ph,
+                                       double& acc) const {
+    for (int sub = 0; sub < s; ++sub) {
+      acc = actD ? ybuf(yb, CP, cur, 0)[(cp * RP + rowD) * 4 + n] : 0.0;
+      for (int t = 1; t <= P; ++t) {
+        TC_T(t0);
+        const double inv = invt[t];  // 1/t from LDS (an fp64 division is ~12 dependent VALU ops)
+        const double z = matvec(ar, ai, ybuf(yb, CP, cur, 0), ybuf(yb, CP, cur, 1)) * inv;
+        acc += z;
+        TC_T(t1);
+        if (t < P) {
+          if (actD) put(ybuf(yb, CP, cur ^ 1, 0), ybuf(yb, CP, cur ^ 1, 1), z);
+          TC_T(t2);
+          sync();
+          cur ^= 1;
+          TC_T(t3);
+          TC_ADD(4, t1 - t0);
+          TC_ADD(5, t2 - t1);
+          TC_ADD(6, t3 - t2);
+          TC_ADD(7, 1);
+        }
+      }
+      if (sub == s - 1) {  // e^{μ} (complex): the partner element (re <-> im) is the neighbouring lane
+        const double o = dpp_mov<0xB1>(acc);  // quad_perm [1,0,3,2]
+        acc = (n & 1) ? ph.r * acc + ph.i * o : ph.r * acc - ph.i * o;
+      }
+      if (actD) put(ybuf(yb, CP, cur ^ 1, 0), ybuf(yb, CP, cur ^ 1, 1), acc);
+      sync();
+      cur ^= 1;
+    }
+  }
+};
+
+template <int KQ>
+__global__ __launch_bounds__(1024) void k_tchain_mf_fwd(const TChainArgs g) {
+  using C = TChainMF<KQ>;
+  constexpr int RP = C::RP;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  const int NN = N * N, Nm = N * m, CP = (m + 1) / 2;
+  cx<double>* gen = reinterpret_cast<cx<double>*>(smem);
+  double* yb = reinterpret_cast<double*>(gen + (size_t)(nu + 1) * NN);
+  double* red = yb + (size_t)2 * 2 * CP * RP * 4;
+  double* invt = red + 16;
+  const cx<double>* At = (const cx<double>*)g.At;
+  const cx<double>* x0b = (const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0);
+  for (int e = tid; e <= TCHAIN_PMAX; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
+  cx<double>* Xb = (cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm;
+  const double* ub = g.u + (size_t)b * Nt * nu;
+  const TStep* stb = g.steps + (size_t)b * Nt;
+  C rg;
+  rg.setup(N, m);
+  for (int e = tid; e < (nu + 1) * NN; e += nthr) gen[e] = At[e];
+  const int YB = 2 * 2 * CP * RP * 4;
+  for (int e = tid; e < YB; e += nthr) yb[e] = 0.0;
+  __syncthreads();
+  for (int o = tid; o < CP * RP * 4; o += nthr) {  // x0 -> y, y' of buffer 0
+    const int c2 = o / (RP * 4), r = (o / 4) % RP, nn = o % 4, col = 2 * c2 + (nn >> 1);
+    if (r < N && col < m) {
+      const cx<double> v = x0b[r + N * col];
+      yb[o] = (nn & 1) ? v.i : v.r;
+      yb[CP * RP * 4 + (c2 * RP + r) * 4 + (nn ^ 1)] = (nn & 1) ? -v.i : v.r;
+    }
+  }
+  const bool pen_m = rg.actD && g.pmask && g.pmask[rg.rowD + N * rg.colD];
+  double pen = 0.0;
+  auto store = [&](double v, int k_) __attribute__((always_inline)) {
+    if (rg.actD) {
+      reinterpret_cast<double*>(Xb + (size_t)k_ * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = v;
+      if (pen_m) pen += v * v;
+    }
+  };
+  __syncthreads();
+  double acc = rg.actD ? yb[(rg.cp * RP + rg.rowD) * 4 + rg.n] : 0.0;
+  store(acc, 0);
+#ifdef QOC_PROBE
+  const unsigned long long c0_ = __builtin_amdgcn_s_memtime(), r0_ = __builtin_amdgcn_s_memrealtime();
+#endif
+  int cur = 0;
+  TPre nx;
+  tpre_load(stb, ub, nu, nx);
+  for (int k = 0; k < Nt; ++k) {
+    const TPre st = nx;
+    if (k + 1 < Nt) tpre_load(stb + k + 1, ub + (size_t)(k + 1) * nu, nu, nx);
+    const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
+    double ar[KQ], ai[KQ];
+    rg.form(N, nu, gen, st.u, ns > 1 ? 1.0 / ns : 1.0, ar, ai);
+    rg.step(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, st.pi}, acc);
+    store(acc, k + 1);
+  }
+  __syncthreads();
+#ifdef QOC_PROBE
+  if (blockIdx.x == 7 && threadIdx.x == 0) {
+    g_tc[8] = __builtin_amdgcn_s_memtime() - c0_;
+    g_tc[9] = __builtin_amdgcn_s_memrealtime() - r0_;
+  }
+#endif
+  const double* yN = C::ybuf(yb, CP, cur, 0);
+  chain_costs<double>(N, m, (const cx<double>*)g.Xt,
+                      [&](int o) {
+                        const int r = o % N, col = o / N, q = ((col >> 1) * RP + r) * 4 + 2 * (col & 1);
+                        return cx<double>{yN[q], yN[q + 1]};
+                      },
+                      g.cost_kind, g.n_norm, block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * m);
+}
+
+template <int KQ>
+__global__ __launch_bounds__(1024) void k_tchain_mf_bwd(const TChainArgs g) {
+  using C = TChainMF<KQ>;
+  constexpr int RP = C::RP;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  const int NN = N * N, Nm = N * m, CP = (m + 1) / 2;
+  cx<double>* gen = reinterpret_cast<cx<double>*>(smem);
+  double* yb = reinterpret_cast<double*>(gen + (size_t)(nu + 1) * NN);
+  double* invt = yb + (size_t)2 * 2 * CP * RP * 4 + 16;
+  for (int e = tid; e <= TCHAIN_PMAX; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
+  const cx<double>* At = (const cx<double>*)g.At;
+  const cx<double>* Xb = (const cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm;
+  cx<double>* Lb = (cx<double>*)g.L + (size_t)b * (Nt + 1) * Nm;
+  const cx<double>* Xt = (const cx<double>*)g.Xt;
+  const double* ub = g.u + (size_t)b * Nt * nu;
+  const TStep* stb = g.steps + (size_t)b * Nt;
+  const double tmu = 2.0 * g.mu;
+  C rg;
+  rg.setup(N, m);
+  for (int e = tid; e < (nu + 1) * NN; e += nthr) {
+    const int j = e / NN, rc = e - j * NN, r = rc % N, c = rc / N;
+    const cx<double> v = At[(size_t)j * NN + c + N * r];  // (Ã_j^H)[r, c] = conj(Ã_j[c, r])
+    gen[e] = cx<double>{v.r, -v.i};
+  }
+  const int YB = 2 * 2 * CP * RP * 4;
+  for (int e = tid; e < YB; e += nthr) yb[e] = 0.0;
+  __syncthreads();
+  // λ_{Nt} = dJfinal/dx(x_N) (+ dL/dx(x_N)) -> buffer 0 and HBM
+  for (int o = tid; o < Nm; o += nthr) {
+    const int r = o % N, col = o / N;
+    cx<double> v;
+    if (g.cost_kind == COST_EXTERNAL) {
+      v = Lb[(size_t)Nt * Nm + o];
+    } else {
+      const cx<double> cf = g.coef[(size_t)b * m + col], t = Xt[o];
+      v = cx<double>{cf.r * t.r - cf.i * t.i, cf.r * t.i + cf.i * t.r};
+    }
+    if (g.pmask && g.pmask[o]) {
+      const cx<double> xv = Xb[(size_t)Nt * Nm + o];
+      v.r += tmu * xv.r;
+      v.i += tmu * xv.i;
+    }
+    Lb[(size_t)Nt * Nm + o] = v;
+    const int q = ((col >> 1) * RP + r) * 4 + 2 * (col & 1);
+    yb[q] = v.r;
+    yb[q + 1] = v.i;
+    yb[CP * RP * 4 + q + 1] = v.r;
+    yb[CP * RP * 4 + q] = -v.i;
+  }
+  const bool pen_m = rg.actD && g.pmask && g.pmask[rg.rowD + N * rg.colD];
+  __syncthreads();
+  int cur = 0;
+  double acc = 0.0;
+  TPre nx;
+  tpre_load(stb + Nt - 1, ub + (size_t)(Nt - 1) * nu, nu, nx);
+  for (int k = Nt - 1; k >= 0; --k) {
+    const TPre st = nx;
+    if (k > 0) tpre_load(stb + k - 1, ub + (size_t)(k - 1) * nu, nu, nx);
+    const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
+    const double xk = pen_m ? reinterpret_cast<const double*>(Xb + (size_t)k * Nm + rg.rowD + N * rg.colD)[rg.n & 1] : 0.0;
+    double ar[KQ], ai[KQ];
+    rg.form(N, nu, gen, st.u, ns > 1 ? 1.0 / ns : 1.0, ar, ai);
+    rg.step(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, -st.pi}, acc);
+    if (pen_m) {
+      acc += tmu * xk;
+      rg.put(C::ybuf(yb, rg.CP, cur, 0), C::ybuf(yb, rg.CP, cur, 1), acc);
+    }
+    if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)k * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = acc;
+    if (g.pmask) rg.sync();  // the penalised entries changed after the step's last barrier
+  }
+}
+
+// Reference-equivalent accounting (the Taylor-action path forms no A_k norm of its own): the Padé (d, s) that
+// ExpMethodHigham2005 would select for ||A_k||_1 (qoc_expm.hpp / k_expm_rr use the same rule), one wave per unit,
+// lane = column (N <= 64).
+template <typename T>
+__global__ void k_pade_units(int N, int nu, long long units, const cx<T>* __restrict__ Agen, const double* __restrict__ u,
+                             unsigned long long* __restrict__ hist) {
+  const int lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+  const int NN = N * N;
+  for (long long e = (long long)blockIdx.x * wpb + (threadIdx.x >> 6); e < units; e += (long long)gridDim.x * wpb) {
+    double cs = 0.0;
+    if (lane < N) {
+      for (int r = 0; r < N; ++r) {
+        double ar = Agen[r + N * lane].r, ai = Agen[r + N * lane].i;
+        for (int j = 0; j < nu; ++j) {
+          const double uj = u[e * nu + j];
+          ar += uj * Agen[(size_t)(j + 1) * NN + r + N * lane].r;
+          ai += uj * Agen[(size_t)(j + 1) * NN + r + N * lane].i;
+        }
+        cs += sqrt(ar * ar + ai * ai);
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) cs = fmax(cs, __shfl_xor(cs, off));
+    if (lane == 0) {
+      int d, sq = 0;
+      if (cs <= 2.1) {
+        d = cs > 0.95 ? 9 : cs > 0.25 ? 7 : cs > 0.015 ? 5 : 3;
+      } else {
+        d = 13;
+        const double sl = log2(cs / 5.4);
+        sq = sl > 0 ? (int)ceil(sl) : 0;
+      }
+      atomicAdd(&hist[degree_index(d) * 64 + (sq < 63 ? sq : 63)], 1ULL);
+    }
+  }
+}
+
+}  // namespace qoc

@@ -27,6 +27,7 @@ QOC_COST_EXTERNAL = 2
 QOC_PROP_EXPM = 0
 QOC_PROP_TSIT5 = 1
 QOC_ENV = {"tunable_bus": 0, "drag": 1, "sinebasis": 2}
+QOC_CHAIN = {"auto": -1, "propagators": 0, "taylor": 1}
 
 # Every symbol include/qoc.h declares, with (restype, argtypes).
 _dp = C.POINTER(C.c_double)
@@ -57,6 +58,8 @@ SIGNATURES = {
     "qoc_set_propagation": (C.c_int, [_vp, C.c_int, C.c_int]),
     "qoc_propagate_envelope": (C.c_int, [_vp, C.c_int, _dp, C.c_int, C.c_double, C.c_double, _dp, _dp]),
     "qoc_get_info": (C.c_int, [_vp, C.POINTER(C.c_longlong)]),
+    "qoc_set_chain": (C.c_int, [_vp, C.c_int]),
+    "qoc_chain_terms": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_set_spline_basis": (C.c_int, [_vp, _dp, C.c_int]),
     "qoc_eval_spline_dev": (C.c_int, [_vp, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "qoc_eval_spline": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp]),

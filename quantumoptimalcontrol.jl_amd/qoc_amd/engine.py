@@ -263,10 +263,22 @@ class GrapeEngine:
 
     def info(self) -> dict:
         """Which pipeline the context runs (qoc_get_info): 'lds' kernels or the 'large_n' GEMM path."""
-        v = np.zeros(4, dtype=np.int64)
+        v = np.zeros(8, dtype=np.int64)
         self._chk(self._lib.qoc_get_info(self._h, v.ctypes.data_as(C.POINTER(C.c_longlong))))
         return {"path": "large_n" if v[0] else "lds", "chunk": int(v[1]), "ns_iters": int(v[2]),
-                "device_bytes": int(v[3])}
+                "device_bytes": int(v[3]), "chain": "taylor" if v[4] == 1 else "propagators"}
+
+    def set_chain(self, mode: str = "auto"):
+        """How the chains apply exp(A_k) (include/qoc.h qoc_set_chain): 'propagators' forms every U_k (the
+        reference's structure), 'taylor' applies the exponential to the state directly, 'auto' chooses by
+        the generator norms."""
+        self._chk(self._lib.qoc_set_chain(self._h, L.QOC_CHAIN[mode]))
+
+    def chain_terms(self, reset: bool = False) -> int:
+        """Taylor terms executed per direction since the last reset (Taylor-action chains)."""
+        v = C.c_longlong()
+        self._chk(self._lib.qoc_chain_terms(self._h, C.byref(v), int(reset)))
+        return int(v.value)
 
     def gemm_stats(self, reset: bool = False) -> dict:
         """Large-N path: live HIP-event time / launches / algorithmic FLOPs of the k_bgemm launches."""

@@ -2,6 +2,9 @@
 
 Tolerances (fp64 GPU vs fp64 restatement): |ΔJ| <= 1e-12 and
 ||ΔdJdu||_F / ||dJdu||_F <= 1e-10 per seed; fp32: |ΔJ| <= 1e-4, rel 1e-3.
+
+Both chain modes run the hot-path cases: 'propagators' (every U_k = exp(A_k) formed on MFMA, then the serial
+products — the reference's structure) and 'taylor' (the exponential applied to the state, no U_k).
 """
 import numpy as np
 import pytest
@@ -11,16 +14,22 @@ import qoc_oracle as O
 pytestmark = pytest.mark.gpu
 
 
-def _engine(prob, B, precision="fp64"):
+CHAINS = ["propagators", "taylor"]
+
+
+def _engine(prob, B, precision="fp64", chain=None):
     from qoc_amd import GrapeEngine
     e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B, precision=precision)
     e.set_cost_trace(prob.x_target, prob.n)
+    if chain is not None:
+        e.set_chain(chain)
+        assert e.info()["chain"] == chain
     return e
 
 
-def _check(prob, u, order=3, precision="fp64", penalty=None):
+def _check(prob, u, order=3, precision="fp64", penalty=None, chain=None):
     B = u.shape[0]
-    e = _engine(prob, B, precision)
+    e = _engine(prob, B, precision, chain)
     if penalty is not None:
         e.set_state_penalty(*penalty)
     J = e.propagate(u)
@@ -60,51 +69,59 @@ def test_expm_general_matrix(built_lib):
         assert np.abs(x - Xr).max() < 1e-12
 
 
-def test_cavity_small_parity(built_lib):
+@pytest.mark.parametrize("chain", CHAINS)
+def test_cavity_small_parity(built_lib, chain):
     from qoc_amd import systems
     prob = systems.cavity_problem(N_cavity=6, Nt=30)
-    _check(prob, systems.cavity_controls(3, prob.Nt, seed=0))
+    _check(prob, systems.cavity_controls(3, prob.Nt, seed=0), chain=chain)
 
 
-def test_zz_parity(built_lib):
+@pytest.mark.parametrize("chain", CHAINS)
+def test_zz_parity(built_lib, chain):
     from qoc_amd import systems
     prob = systems.zz_problem(100)
-    _check(prob, systems.zz_controls(2, 100, 10.0, seed=0))
+    _check(prob, systems.zz_controls(2, 100, 10.0, seed=0), chain=chain)
 
 
-def test_cavity40_parity(built_lib):
+@pytest.mark.parametrize("chain", CHAINS)
+def test_cavity40_parity(built_lib, chain):
     from qoc_amd import systems
     prob = systems.cavity_problem(N_cavity=20, Nt=40)
-    _check(prob, systems.cavity_controls(2, prob.Nt, seed=5))
+    _check(prob, systems.cavity_controls(2, prob.Nt, seed=5), chain=chain)
 
 
-def test_tunable_bus_parity(built_lib):
+@pytest.mark.parametrize("chain", CHAINS)
+def test_tunable_bus_parity(built_lib, chain):
     from qoc_amd import systems
     prob = systems.tunable_bus_problem(Nt=60, tgate=350.0 * 60 / 2000)
-    _check(prob, systems.tunable_bus_controls(2, prob.Nt, seed=0))
+    _check(prob, systems.tunable_bus_controls(2, prob.Nt, seed=0), chain=chain)
 
 
+@pytest.mark.parametrize("chain", CHAINS)
 @pytest.mark.parametrize("order", [1, 2, 3, 4])
-def test_orders(built_lib, order):
+def test_orders(built_lib, order, chain):
     from qoc_amd import systems
     prob = systems.zz_problem(50, tgate=5.0)
-    _check(prob, systems.zz_controls(2, 50, 5.0, seed=order), order=order)
+    _check(prob, systems.zz_controls(2, 50, 5.0, seed=order), order=order, chain=chain)
 
 
-def test_state_penalty(built_lib):
+@pytest.mark.parametrize("chain", CHAINS)
+def test_state_penalty(built_lib, chain):
     from qoc_amd import systems
     prob = systems.zz_problem(40, tgate=4.0)
     qb = systems.QuantumBasis([3, 3])
     pen = (qb(["20", "21", "22"]), [0, 1, 2, 3], 0.37)
-    _check(prob, systems.zz_controls(2, 40, 4.0, seed=9), penalty=pen)
+    _check(prob, systems.zz_controls(2, 40, 4.0, seed=9), penalty=pen, chain=chain)
 
 
-def test_zcalibrated_cost(built_lib):
+@pytest.mark.parametrize("chain", CHAINS)
+def test_zcalibrated_cost(built_lib, chain):
     """setup_infidelity_zcalibrated on the device (golden section in k_chain_fwd)."""
     from qoc_amd import GrapeEngine, systems
     prob = systems.zz_problem(40, tgate=4.0)
     u = systems.zz_controls(3, 40, 4.0, seed=21)
     e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=3)
+    e.set_chain(chain)
     e.set_cost_zcalibrated(prob.x_target)
     J = e.propagate(u)
     g = e.grape_sensitivity(u, 3)
@@ -191,19 +208,22 @@ def test_reference_shaped_api(built_lib):
     assert np.linalg.norm(g2 - gr2) / np.linalg.norm(gr2) < 1e-10
 
 
-def test_fp32_small(built_lib):
+@pytest.mark.parametrize("chain", CHAINS)
+def test_fp32_small(built_lib, chain):
     from qoc_amd import systems
     prob = systems.cavity_problem(N_cavity=10, Nt=40)
-    _check(prob, systems.cavity_controls(2, 40, seed=8), precision="fp32")
+    _check(prob, systems.cavity_controls(2, 40, seed=8), precision="fp32", chain=chain)
 
 
-def test_per_seed_x0(built_lib):
+@pytest.mark.parametrize("chain", CHAINS)
+def test_per_seed_x0(built_lib, chain):
     from qoc_amd import GrapeEngine, systems
     prob = systems.zz_problem(20, tgate=2.0)
     u = systems.zz_controls(2, 20, 2.0, seed=2)
     rng = np.random.default_rng(5)
     x0s = np.stack([np.linalg.qr(rng.standard_normal((9, 4)) + 1j * rng.standard_normal((9, 4)))[0] for _ in range(2)])
     e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2)
+    e.set_chain(chain)
     e.set_x0(x0s, per_seed=True)
     e.set_cost_trace(prob.x_target, 4)
     J = e.propagate(u)
@@ -320,7 +340,7 @@ def test_taylor_default_and_pade_option_agree(built_lib, monkeypatch):
     for mode, env in (("t12", {}), ("ps", {"QOC_EXPM_LDS": "1"}), ("pade", {"QOC_EXPM_PADE": "1"})):
         for k in ("QOC_EXPM_LDS", "QOC_EXPM_PADE"):
             monkeypatch.setenv(k, env.get(k, "0"))
-        e = _engine(prob, 2)
+        e = _engine(prob, 2, chain="propagators")
         J = e.propagate(u)
         g = e.grape_sensitivity(u, 3)
         out[mode] = (J, g, e.pade_histogram(), e.taylor_histogram())
@@ -401,7 +421,7 @@ def test_t12_and_paterson_stockmeyer_passes(built_lib, which):
     else:
         prob = systems.tunable_bus_problem(Nt=200)
         u = systems.tunable_bus_controls(2, prob.Nt, seed=22)
-    e = _engine(prob, u.shape[0])
+    e = _engine(prob, u.shape[0], chain="propagators")
     J = e.propagate(u)
     g = e.grape_sensitivity(u, 3)
     th = e.taylor_histogram()
@@ -414,3 +434,51 @@ def test_t12_and_paterson_stockmeyer_passes(built_lib, which):
         Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
         assert abs(J[b] - Jr) <= 1e-12
         assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
+
+
+def test_taylor_chain_accounting_and_propagator_on_demand(built_lib):
+    """Taylor-action chains: the executed-term counter, the reference-equivalent Padé histogram (evaluated
+    from the propagated u) and qoc_get_propagator (formed on demand) against the oracle."""
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=20, Nt=12)
+    u = systems.cavity_controls(2, prob.Nt, seed=2)
+    e = _engine(prob, 2)
+    assert e.info()["chain"] == "taylor"  # auto: ||A0 - mu I||_1 ~ 0.15
+    e.chain_terms(reset=True)
+    e.pade_histogram(reset=True)
+    e.propagate(u)
+    e.grape_sensitivity(u, 3)
+    terms = e.chain_terms()
+    assert 9 * 24 <= terms <= 14 * 24, terms  # P = 10..13 per slice at these norms
+    assert e.pade_histogram() == {(7, 0): 24}
+    for b, k in ((0, 0), (1, 11), (1, 5)):
+        U = e.propagator(k, seed=b)
+        Ak = prob.A0 + sum(u[b, j, k] * prob.A[j] for j in range(2))
+        Ur, _, _ = O.expm_higham2005(Ak)
+        assert np.abs(U - Ur).max() < 1e-13
+    e.close()
+
+
+@pytest.mark.parametrize("chain", CHAINS)
+def test_external_cost_and_costates(built_lib, chain):
+    """QOC_COST_EXTERNAL (caller's λ_N) and the stored co-states / states through both chain modes."""
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=8, Nt=25)
+    u = systems.cavity_controls(2, prob.Nt, seed=31)
+    from qoc_amd import GrapeEngine
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2)
+    e.set_chain(chain)
+    e.set_cost_external()
+    e.propagate(u)
+    rng = np.random.default_rng(3)
+    lam = rng.standard_normal((2, prob.N, prob.m)) + 1j * rng.standard_normal((2, prob.N, prob.m))
+    g = e.grape_sensitivity(u, 3, lambda_final=lam)
+    for b in range(2):
+        cache = O.setup_grape_cache(prob.A0, prob.x0, u[b].shape)
+        O.propagate(prob.A0, prob.A, u[b], prob.x0, cache)
+        gr = O.grape_sensitivity(prob.A0, prob.A, lambda x, lb=lam[b]: lb, cache.u, prob.x0, cache, dUkdp_order=3)
+        assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
+        for k in (0, 9, prob.Nt):
+            assert np.abs(e.state(k, seed=b) - cache.x[k]).max() < 1e-13
+            assert np.abs(e.costate(k, seed=b) - cache.lam[k]).max() < 1e-12
+    e.close()
