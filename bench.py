@@ -104,16 +104,54 @@ def cpu_baseline_large(prob, u_all, order, nthreads, target_s=12.0):
     }, (Jc, gc, n2)
 
 
+def cpu_facts():
+    """CPU model, visible / usable cores (the box's nproc counts the whole machine; the job's share is its
+    affinity mask and OMP_NUM_THREADS)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, aff
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: the job's CPU share (OMP_NUM_THREADS, set by the launcher to the cores
+    allotted to one GPU), else every core in the affinity mask."""
+    _, _, aff = cpu_facts()
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(env, aff) if env > 0 else aff
+
+
 def cpu_baseline(prob, u_all, order, nthreads, target_s=12.0):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpuref  # checker / baseline only (oracle/)
     import numpy as np
+    model, ncpu, aff = cpu_facts()
     B = u_all.shape[0]
-    # calibration round: one seed per thread, seed-parallel
+    # calibration round (one seed per thread, seed-parallel) for both backends of the port: zgemm / zgesv from
+    # the image's OpenBLAS (the reference runs MKL's) and the in-repo loops; OpenBLAS pays a per-call overhead
+    # at small N and contends when many threads call it at once, so the faster backend is timed
     S = min(B, nthreads)
-    t = time.perf_counter()
-    J0, g0 = cpuref.grape_eval_batch(prob, u_all[:S], order=order, mode=0, nthreads=nthreads)
-    t1 = time.perf_counter() - t
+    calib = {}
+    for use in (True, False):
+        path = cpuref.use_blas(use)
+        if use and not path:
+            continue
+        t = time.perf_counter()
+        cpuref.grape_eval_batch(prob, u_all[:S], order=order, mode=0, nthreads=nthreads)
+        calib[path] = time.perf_counter() - t
+    blas = min(calib, key=calib.get)
+    cpuref.use_blas(blas is not None)
+    t1 = calib[blas]
     # timed sample: ~target_s of CPU work, i.e. `total` evals over the first S2 seeds (repeated passes
     # when the batch has fewer seeds than that)
     total = int(max(S, S * round(target_s / max(t1, 1e-3))))
@@ -132,12 +170,17 @@ def cpu_baseline(prob, u_all, order, nthreads, target_s=12.0):
     cpuref.grape_eval_batch(prob, u_all[:1], order=order, mode=1, nthreads=nthreads)
     faithful = 1.0 / (time.perf_counter() - t)
     best = max(seed_par, faithful)
+    blas_name = (f"OpenBLAS 0.3.29 zgemm/zgesv ({os.path.basename(blas)}, 1 BLAS thread per call)" if blas
+                 else "its own complex loops")
+    alt = "; ".join(f"{'OpenBLAS' if k else 'loops'} {S / v:.3g} evals/s" for k, v in calib.items())
+    blas_name += f" (faster backend in the calibration round: {alt})"
     return {
         "value": best,
         "unit": "evals/s",
         "cores": nthreads,
         "kind": "port",
-        "sample": (f"oracle/cpu_ref.c (gcc -O3, OpenMP): {done} evals over the first {S2} of this rank's seeds, "
+        "sample": (f"oracle/cpu_ref.c (gcc -O3, OpenMP) with {blas_name} on {nthreads} threads of a {model} "
+                   f"(nproc {ncpu}, affinity {aff}): {done} evals over the first {S2} of this rank's seeds, "
                    f"seed-parallel {seed_par:.3g} evals/s ({t2:.1f} s); reference-faithful k-parallel mode on 1 seed "
                    f"{faithful:.3g} evals/s; faster mode reported"),
     }, (J, g, S2)
@@ -185,10 +228,16 @@ def main():
     gathered = torch.empty(2 * world, dtype=torch.float64, device=dev)
     stream = torch.cuda.ExternalStream(eng.stream(), device=dev)
     seed_offset = torch.arange(B, dtype=torch.float64, device=dev) + rank * B
+    # the one exchange: best (J, global seed) over all ranks, RCCL inside libqoc_mi355x.so (qoc_allgather_best);
+    # torch.distributed's all_gather (also RCCL) only if the library cannot load RCCL
+    from qoc_amd import multi
+    transport = "rccl-libqoc" if multi.init_engine_comm(eng, rank * B) else "torch.distributed"
 
     def step():
         eng.eval_device(u_d.data_ptr(), args.order, J_d.data_ptr(), g_d.data_ptr())
-        if world > 1:
+        if transport == "rccl-libqoc":
+            eng.allgather_best_device(best_d.data_ptr())  # on the engine stream, after its kernels
+        elif world > 1:
             with torch.cuda.stream(stream):  # ordered after the engine's kernels
                 jm, idx = torch.min(J_d, 0)
                 best_d[0] = jm
@@ -202,6 +251,7 @@ def main():
 
     eng.pade_histogram(reset=True)
     eng.taylor_histogram(reset=True)
+    eng.chain_terms(reset=True)
     eng.phase_times(reset=True)
     info0 = eng.info()
     if info0["path"] == "large_n":
@@ -228,6 +278,7 @@ def main():
     phases = eng.phase_times()
     hist = eng.pade_histogram()
     thist = eng.taylor_histogram()
+    terms = eng.chain_terms()  # Taylor-action chains: Σ P s over all slices, per direction
     K = args.steps
     N, m, nu, Nt = prob.N, prob.m, prob.nu, prob.Nt
     esz = 16 if prob.precision == "fp64" else 8
@@ -246,7 +297,18 @@ def main():
             traffic_all = json.load(open(traffic_file))
         except Exception:
             traffic_all = {}
-    if not large:
+    taylor = info1.get("chain") == "taylor" and not large
+    if taylor:
+        # Taylor-action chains (csrc/qoc_tchain.hpp): no exponential kernel; the chains carry the Taylor terms,
+        # each an N x N by N x m complex matvec (8 N^2 m flops) on v_mfma_f64_4x4x4 (fp64) / VALU (fp32)
+        tl = terms / K
+        models = {
+            "k_expm": ("mfma", 0.0, "TFLOP/s", peak),  # k_tchain_prep: (P, s, e^mu) per slice, no flops counted
+            "k_grad": ("mfma", grad_flops(N, m, nu, Nt, B, args.order) / 1e12, "TFLOP/s", peak),
+            "k_chain_fwd": ("mfma", 8.0 * N * N * m * tl / 1e12, "TFLOP/s", peak),
+            "k_chain_bwd": ("mfma", 8.0 * N * N * m * tl / 1e12, "TFLOP/s", peak),
+        }
+    elif not large:
         models = {
             "k_expm": ("mfma", (taylor_flops(N, {k: v / K for k, v in thist.items()}) if thist
                                 else expm_flops(N, hist_launch)) / 1e12, "TFLOP/s", peak),
@@ -279,11 +341,27 @@ def main():
         ach = work / t if t > 0 else 0.0
         kern[k] = {"ms_per_launch": per_launch[k], "bound": bound, "achieved": ach, "unit": unit, "peak": pk,
                    "frac": ach / pk}
-    if not large:
+    names = {"k_expm": "k_expm_rr", "k_chain_fwd": "k_chain_fwd", "k_chain_bwd": "k_chain_bwd", "k_grad": "k_grad_rr"}
+    if taylor:
+        mf = prob.precision == "fp64"
+        names = {"k_expm": "k_tchain_prep", "k_chain_fwd": "k_tchain_mf_fwd" if mf else "k_tchain_fwd",
+                 "k_chain_bwd": "k_tchain_mf_bwd" if mf else "k_tchain_bwd", "k_grad": "k_grad_rr"}
+        for k in ("k_chain_fwd", "k_chain_bwd"):
+            # serial Taylor terms of one seed per launch and the time each takes (the chains' critical path)
+            kern[k]["kernel"] = names[k]
+            kern[k]["terms_per_seed"] = terms / K / B
+            kern[k]["ns_per_serial_term"] = per_launch[k] * 1e6 / max(terms / K / B, 1e-9)
+        dom = max(("k_chain_fwd", "k_chain_bwd", "k_grad"), key=lambda k: per_launch[k])
+        roof = {"kernel": names[dom], "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
+                "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
+                "traffic": traffic_all.get(names[dom]), "ms_per_launch": kern[dom]["ms_per_launch"],
+                "note": ("latency-bound serial recurrence (one workgroup per seed, Taylor terms in sequence): "
+                         "achieved = executed matvec flops / launch time")}
+    elif not large:
         dom = max(per_launch, key=per_launch.get)
         # the exponential phase runs the register-resident kernels (k_expm_rr: T12 / Paterson-Stockmeyer)
         # unless QOC_EXPM_LDS or QOC_EXPM_PADE selects the LDS kernel k_expm
-        lds_expm = any(os.environ.get(v, "0") not in ("", "0") for v in ("QOC_EXPM_LDS", "QOC_EXPM_PADE"))
+        lds_expm = info1.get("expm") != "taylor_rr"  # the reference's Padé or the LDS Paterson-Stockmeyer: k_expm
         kname = dom
         if dom == "k_expm" and not lds_expm:
             # one-pass k_expm_rr_mix when ||A_0||_1 > 4 theta_12 (tunable bus), else k_expm_rr (+ its
@@ -305,10 +383,11 @@ def main():
                 "ns_iters_per_chunk": ns_it, "chunk": info1["chunk"]}
     ref_f = ref_eval_flops(N, m, nu, {k: v / B for k, v in hist_launch.items()}, args.order)
 
+    best = best_d.cpu().numpy().tolist() if world > 1 or transport == "rccl-libqoc" else None
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        nthreads = cpu_threads()
         try:
             if large:
                 cpu, (Jc, gc, n2) = cpu_baseline_large(prob, u_all, args.order, nthreads, args.cpu_seconds)
@@ -357,6 +436,7 @@ def main():
             "ref_equiv_tflops": ref_f * value / 1e12,
             "parity_vs_cpu_port": parity,
             "engine": info1,
+            "best_over_ranks": {"J": best[0], "seed": int(best[1]), "transport": transport} if best else None,
         }
         if cpu and cpu.get("value"):
             out["speedup_vs_cpu"] = value / cpu["value"]

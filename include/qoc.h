@@ -76,6 +76,13 @@ int qoc_propagate(qoc_ctx* ctx, const double* u, double* J_out);
 int qoc_grape_sensitivity(qoc_ctx* ctx, const double* u, int dUkdp_order,
                           const double* lambda_final, double* dJdu_out);
 
+/* A caller's state-penalty gradient that is not a built-in penalty (any Julia closure dL_dx,
+ * src/gradient_computations.jl:47-49, 55-57): dLdx holds dL_dx(x_k) for every seed and k = 0..Nt
+ * (B x (Nt+1) x N x m, the states' layout), added to λ_k by the following grape_sensitivity calls until cleared
+ * with NULL.  The host evaluates the closure on the states (qoc_get_states); J's sum(L, x) stays with the
+ * caller.  Not on the Tsit5 path (compute_pwc_gradient has no dL_dx). */
+int qoc_set_costate_source(qoc_ctx* ctx, const double* dLdx);
+
 /* Device-pointer variants (inputs already resident in HBM, asynchronous on qoc_stream). */
 int qoc_propagate_dev(qoc_ctx* ctx, const double* d_u, double* d_J);
 int qoc_grape_sensitivity_dev(qoc_ctx* ctx, const double* d_u, int dUkdp_order, double* d_dJdu);
@@ -149,7 +156,8 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
 /* Engine facts: info[0] = path (0 = LDS-resident kernels, 1 = large-N chunked GEMM pipeline),
  * info[1] = slices per chunk (large-N), info[2] = Newton-Schulz iterations executed so far (large-N),
  * info[3] = device bytes allocated by the context, info[4] = chain mode (QOC_CHAIN_PROPAGATORS /
- * QOC_CHAIN_TAYLOR), info[5..7] reserved (0).  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
+ * QOC_CHAIN_TAYLOR), info[5] = exponential the propagators run (0 the reference's Padé + solve, 1 register-
+ * resident Taylor / Paterson-Stockmeyer, 2 LDS Paterson-Stockmeyer), info[6..7] reserved (0).  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
  * selects the large-N path for any size (testing). */
 int qoc_get_info(qoc_ctx* ctx, long long* info /*[8]*/);
 
@@ -169,6 +177,21 @@ int qoc_get_info(qoc_ctx* ctx, long long* info /*[8]*/);
 int qoc_set_chain(qoc_ctx* ctx, int mode);
 /* Taylor terms executed per direction (Σ over slices of P s) since the last reset (QOC_CHAIN_TAYLOR). */
 int qoc_chain_terms(qoc_ctx* ctx, long long* terms, int reset);
+
+/* Multi-GPU epilogue: seeds are sharded contiguously over ranks, one context per GPU; the
+ * only exchange is an all-gather of each rank's best (J, global seed id) over RCCL (xGMI), 16 bytes per rank.
+ * qoc_comm_unique_id (one rank) creates the RCCL unique id (QOC_UNIQUE_ID_BYTES opaque bytes) that the caller
+ * distributes (MPI / Distributed.jl / torch.distributed); every rank then calls qoc_comm_init with its rank
+ * and the global id of its seed 0.  qoc_allgather_best returns the best J of the last propagate over all
+ * ranks and its global seed (lowest seed on ties); without qoc_comm_init it covers this context alone.
+ * RCCL is loaded on first use (librccl.so.1); two ranks cannot share one GPU (RCCL rejects duplicate
+ * devices).  The _dev variant writes (J_best, seed) as two doubles to device memory on qoc_stream without
+ * synchronising. */
+#define QOC_UNIQUE_ID_BYTES 128
+int qoc_comm_unique_id(void* id_out);
+int qoc_comm_init(qoc_ctx* ctx, int world, int rank, const void* id, long long seed_offset);
+int qoc_allgather_best(qoc_ctx* ctx, double* J_best, int* seed_best);
+int qoc_allgather_best_dev(qoc_ctx* ctx, double* d_out);
 
 /* Standalone ops on the same kernels. */
 /* exponential!(A, ExpMethodHigham2005()) for `count` independent N x N matrices

@@ -16,8 +16,14 @@
  *
  * Two timing modes: mode 0 = seed-parallel (one seed per thread),
  * mode 1 = reference-faithful (exponentials OpenMP-parallel over k, like Threads.@threads at :17).
+ *
+ * BLAS/LAPACK: the reference calls zgemm (mul!) and zgesv (exponential!'s solve) of MKL
+ * (examples/zz_coupling_ipopt_exp.jl:2).  qocref_set_blas(path) dlopens an OpenBLAS (the one scipy ships in
+ * this image) and routes every N x N product and the Padé solve through its zgemm_ / zgesv_ (one BLAS thread
+ * per call, the parallelism is OpenMP over seeds or slices); without it the loops below are used.
  */
 #include <complex.h>
+#include <dlfcn.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -26,6 +32,43 @@
 #endif
 
 typedef double complex cd;
+
+typedef void (*zgemm_fn)(const char*, const char*, const int*, const int*, const int*, const cd*, const cd*,
+                         const int*, const cd*, const int*, const cd*, cd*, const int*);
+typedef void (*zgesv_fn)(const int*, const int*, cd*, const int*, int*, cd*, const int*, int*);
+static zgemm_fn blas_zgemm = NULL;
+static zgesv_fn blas_zgesv = NULL;
+
+/* Returns 0 when zgemm and zgesv were found (symbol prefix: "" or "scipy_"). */
+int qocref_set_blas(const char* path) {
+  blas_zgemm = NULL;
+  blas_zgesv = NULL;
+  if (!path || !*path) return 0;
+  void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) return -1;
+  const char* pre[2] = {"scipy_", ""};
+  for (int i = 0; i < 2 && !blas_zgemm; ++i) {
+    char nm[64];
+    strcpy(nm, pre[i]);
+    strcat(nm, "zgemm_");
+    blas_zgemm = (zgemm_fn)dlsym(h, nm);
+    strcpy(nm, pre[i]);
+    strcat(nm, "zgesv_");
+    blas_zgesv = (zgesv_fn)dlsym(h, nm);
+    void (*nt)(int) = NULL;
+    strcpy(nm, pre[i]);
+    strcat(nm, "openblas_set_num_threads");
+    nt = (void (*)(int))dlsym(h, nm);
+    if (nt) nt(1);
+  }
+  if (!blas_zgemm || !blas_zgesv) {
+    blas_zgemm = NULL;
+    blas_zgesv = NULL;
+    return -2;
+  }
+  return 0;
+}
+int qocref_have_blas(void) { return blas_zgemm != NULL; }
 
 static const double P3[4] = {120.0, 60.0, 12.0, 1.0};
 static const double P5[6] = {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0};
@@ -38,6 +81,10 @@ static const double P13[14] = {64764752532480000.0, 32382376266240000.0, 7771770
 
 /* C = alpha*A*B + beta*C, column-major N x N (zgemm-shaped loop order j,l,i). */
 static void gemm(int N, const cd* A, const cd* B, cd* C, cd alpha, cd beta) {
+  if (blas_zgemm) {
+    blas_zgemm("N", "N", &N, &N, &N, &alpha, A, &N, B, &N, &beta, C, &N);
+    return;
+  }
   for (int j = 0; j < N; ++j) {
     cd* c = C + (size_t)N * j;
     if (beta == 0.0)
@@ -54,6 +101,11 @@ static void gemm(int N, const cd* A, const cd* B, cd* C, cd alpha, cd beta) {
 
 /* y = A x  (N x N times N x m) */
 static void gemm_nm(int N, int m, const cd* A, const cd* X, cd* Y) {
+  if (blas_zgemm) {
+    const cd one = 1.0, zero = 0.0;
+    blas_zgemm("N", "N", &N, &m, &N, &one, A, &N, X, &N, &zero, Y, &N);
+    return;
+  }
   for (int c = 0; c < m; ++c) {
     cd* y = Y + (size_t)N * c;
     memset(y, 0, sizeof(cd) * N);
@@ -67,6 +119,11 @@ static void gemm_nm(int N, int m, const cd* A, const cd* X, cd* Y) {
 
 /* y = A^H x */
 static void gemm_h_nm(int N, int m, const cd* A, const cd* X, cd* Y) {
+  if (blas_zgemm) {
+    const cd one = 1.0, zero = 0.0;
+    blas_zgemm("C", "N", &N, &m, &N, &one, A, &N, X, &N, &zero, Y, &N);
+    return;
+  }
   for (int c = 0; c < m; ++c)
     for (int i = 0; i < N; ++i) {
       cd s = 0;
@@ -80,6 +137,12 @@ static void gemm_h_nm(int N, int m, const cd* A, const cd* X, cd* Y) {
 /* Solve Q X = P in place (X overwrites P); LU with partial pivoting, izamax rule (|re|+|im|). */
 static void gesv(int N, cd* Q, cd* P) {
   int* piv = (int*)malloc(sizeof(int) * N);
+  if (blas_zgesv) {
+    int info = 0;
+    blas_zgesv(&N, &N, Q, &N, piv, P, &N, &info);
+    free(piv);
+    return;
+  }
   for (int p = 0; p < N; ++p) {
     int r = p;
     double best = -1.0;

@@ -26,7 +26,34 @@ def load():
         _lib.qocref_expm.argtypes = [C.c_int, _dp, _dp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         _lib.qocref_expm_jacobian.argtypes = [C.c_int, C.c_int, _dp, _dp, _dp, C.c_int, C.c_double, _dp]
         _lib.qocref_max_threads.restype = C.c_int
+        _lib.qocref_set_blas.argtypes = [C.c_char_p]
+        _lib.qocref_have_blas.restype = C.c_int
     return _lib
+
+
+def find_openblas():
+    """The OpenBLAS that scipy/numpy ship in this image (LP64 first: its zgemm_ takes 32-bit ints)."""
+    import glob
+    for pkg in ("scipy", "numpy"):
+        try:
+            mod = __import__(pkg)
+        except Exception:
+            continue
+        libdir = os.path.join(os.path.dirname(os.path.dirname(mod.__file__)), pkg + ".libs")
+        for f in sorted(glob.glob(os.path.join(libdir, "libscipy_openblas-*.so")) +
+                        glob.glob(os.path.join(libdir, "libopenblas*.so*"))):
+            return f
+    return None
+
+
+def use_blas(enable=True):
+    """Route the C port's zgemm / zgesv through the bundled OpenBLAS; returns its path or None."""
+    lib = load()
+    path = find_openblas() if enable else None
+    if path and lib.qocref_set_blas(path.encode()) == 0:
+        return path
+    lib.qocref_set_blas(None)
+    return None
 
 
 def _cm(a):

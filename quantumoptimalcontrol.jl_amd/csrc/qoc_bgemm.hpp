@@ -530,6 +530,18 @@ __global__ void k_penalty_sum(int N, int m, int Nt, const cx<T>* __restrict__ X,
 
 // λ_k[b] += 2 mu mask .* x_k[b] for one slice index k, all seeds.
 template <typename T>
+__global__ void k_add_source(int N, int m, int Nt, int B, int k, const cx<T>* __restrict__ src, cx<T>* __restrict__ Lam) {
+  const size_t Nm = (size_t)N * m;
+  for (size_t gi = blockIdx.x * (size_t)blockDim.x + threadIdx.x; gi < Nm * B; gi += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(gi / Nm);
+    const size_t at = ((size_t)b * (Nt + 1) + k) * Nm + (gi - (size_t)b * Nm);
+    cx<T> l = Lam[at];
+    l.r += src[at].r;
+    l.i += src[at].i;
+    Lam[at] = l;
+  }
+}
+template <typename T>
 __global__ void k_penalty_grad(int N, int m, int Nt, int B, int k, const cx<T>* __restrict__ X,
                                const unsigned char* __restrict__ pmask, double two_mu, cx<T>* __restrict__ Lam) {
   const size_t Nm = (size_t)N * m;

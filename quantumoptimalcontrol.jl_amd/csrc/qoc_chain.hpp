@@ -442,7 +442,7 @@ template <typename T, int S, int JT, int CB>
 __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
     int N, int m, int Nt, const cx<T>* __restrict__ U, const cx<T>* __restrict__ X, cx<T>* __restrict__ Lam,
     const cx<T>* __restrict__ Xt, int cost_kind, const cx<double>* __restrict__ coef,
-    const unsigned char* __restrict__ pmask, double mu) {
+    const unsigned char* __restrict__ pmask, double mu, const cx<T>* __restrict__ src) {
   using R = ChainRegs<T, S, JT, CB, false>;
   constexpr int XS = R::XS, D = R::D;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -477,6 +477,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
         const cx<T> xv = Xb[(size_t)Nt * Nm + o];
         v.r += tmu * xv.r;
         v.i += tmu * xv.i;
+      }
+      if (src) {  // caller's dL/dx(x_N) (qoc_set_costate_source)
+        const cx<T> sv = src[((size_t)b * (Nt + 1) + Nt) * Nm + o];
+        v.r += sv.r;
+        v.i += sv.i;
       }
     }
     lb[e] = v;
@@ -516,6 +521,17 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
           const cx<T> xv = Xb[(size_t)k_ * Nm + rg.xo[r]];
           ln[rg.xi[r]].r += tmu * xv.r;
           ln[rg.xi[r]].i += tmu * xv.i;
+        }
+      __syncthreads();
+    }
+    if (src) {  // + the caller's dL/dx(x_k)
+      const cx<T>* sk = src + ((size_t)b * (Nt + 1) + k_) * Nm;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (rg.xo[r] >= 0) {
+          const cx<T> sv = sk[rg.xo[r]];
+          ln[rg.xi[r]].r += sv.r;
+          ln[rg.xi[r]].i += sv.i;
         }
       __syncthreads();
     }

@@ -4,6 +4,7 @@
 // all per-slice propagators, states and co-states live in HBM for the whole batch of
 // seeds, and the hot path (propagate + grape_sensitivity) is four kernel launches on
 // one HIP stream:  k_expm -> k_chain_fwd  |  k_chain_bwd -> k_grad.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -19,6 +20,7 @@
 #include "../../include/qoc.h"
 #include "qoc_bgemm.hpp"
 #include "qoc_chain.hpp"
+#include "qoc_comm.hpp"
 #include "qoc_expm.hpp"
 #include "qoc_expm_rr.hpp"
 #include "qoc_frechet.hpp"
@@ -49,6 +51,8 @@ struct qoc_ctx {
   double cost_n = 1.0;
   unsigned char* d_pmask = nullptr;
   double mu = 0.0;
+  void* d_src = nullptr;   // B x (Nt+1) x N x m caller's dL/dx(x_k) (qoc_set_costate_source), device precision
+  bool src_on = false;
   double* d_u = nullptr;     // B*nu*Nt, u of the last propagate
   void* d_U = nullptr;       // B*Nt*N*N
   void* d_X = nullptr;       // B*(Nt+1)*N*m
@@ -106,16 +110,28 @@ struct qoc_ctx {
   bool grad_rr = false;  // fused register-resident order-3 gradient (qoc_grad_rr.hpp)
   int* d_ps = nullptr;   // k_expm_rr pass-2 counter + list of Paterson-Stockmeyer units
   double a0norm = 0.0;   // ||A0||_1 of the generators (host-side, at qoc_set_generators)
+  // exponential that runs: expm_alg, except that when every slice has a large norm (||A0||_1 > 4 theta_12,
+  // tunable bus: ||A_k||_1 ~ 30) the default register-resident Taylor hands over to the reference's own Padé-13
+  // + solve (k_expm ALG 0): over 2000 chained slices only the same algorithm holds |ΔJ| <= 1e-12 against the
+  // reference (Paterson-Stockmeyer: 1.6e-12).  QOC_EXPM_PS=1 keeps Paterson-Stockmeyer there (1.8x faster).
+  int expm_run = 1;
+  bool expm_ps = false;
   int ncu = 256;         // compute units of the device (persistent-grid sizing)
   // Taylor-action chains (qoc_tchain.hpp): x_{k+1} = exp(A_k) x_k applied to the state, no U_k formed.
   // chain_mode 1 selects them (QOC_CHAIN=taylor / expm overrides the automatic choice at qoc_set_generators)
   int chain_mode = 0;            // 0: propagators (k_expm + k_chain_*), 1: Taylor action (k_tchain_*)
+  int chain_req = QOC_CHAIN_AUTO;  // what qoc_set_chain asked for (kept across qoc_set_generators)
   bool tchain_ok = false;        // the shape fits the Taylor-action kernels
   void* d_At = nullptr;          // (nu+1) N x N shifted generators Ã_j = A_j - μ_j I
   TStep* d_steps = nullptr;      // B x Nt (P, s, e^{μ_k})
   unsigned long long* d_terms = nullptr;  // Σ P s per forward (executed Taylor terms per direction)
   TChainParams tprm{};
   long long props_since_reset = 0;  // forward passes since the last Padé-histogram reset (chain mode 1)
+  // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
+  ncclComm_t comm = nullptr;
+  int world = 1, rank = 0;
+  long long seed_offset = 0;   // global id of this context's seed 0
+  double* d_best = nullptr;    // [2 local | 2 x world gathered | 2 result]
   // exact (Fréchet) gradient mode workspace, allocated on first use
   void* d_fws = nullptr;
   size_t fws_bytes = 0;
@@ -365,7 +381,7 @@ int run_forward(qoc_ctx* c) {
   if (c->chain_mode == 1) return tchain_forward<T>(c);
   int mk = mark_begin(c, 0);
   hipError_t e = launch_expm(c->prec, c->stream, c->N, c->nu, c->B * c->Nt, c->d_A, c->d_u, nullptr, c->d_U,
-                             c->d_hist, nullptr, nullptr, c->expm_alg, c->d_hist + 5 * 64, c->d_ps,
+                             c->d_hist, nullptr, nullptr, c->expm_run, c->d_hist + 5 * 64, c->d_ps,
                              c->a0norm > 4.0 * kTheta12);
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm launch: %s", hipGetErrorString(e));
@@ -406,7 +422,8 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
       if (r != hipSuccess) return r;
       hipLaunchKernelGGL((k_chain_bwd<T, S, JT, CB>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
                          (const cx<T>*)c->d_U, (const cx<T>*)c->d_X, (cx<T>*)c->d_L, (const cx<T>*)c->d_Xt,
-                         c->cost_kind, (const cx<double>*)c->d_coef, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu);
+                         c->cost_kind, (const cx<double>*)c->d_coef, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu,
+                         c->src_on ? (const cx<T>*)c->d_src : nullptr);
       return hipGetLastError();
     });
     mark_end(c, mk);
@@ -790,6 +807,11 @@ int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
                        (const cx<T>*)c->d_X, c->d_pmask, 2.0 * c->mu, (cx<T>*)c->d_L);
     HIPCHK(c, hipGetLastError());
   }
+  if (c->src_on) {
+    hipLaunchKernelGGL((k_add_source<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, Nt, (const cx<T>*)c->d_src,
+                       (cx<T>*)c->d_L);
+    HIPCHK(c, hipGetLastError());
+  }
   // λ_k = U_k^H λ_{k+1} (+ dL/dx(x_k))
   for (int k = Nt - 1; k >= 0; --k) {
     GemmArgs g = gemm_args(N, N, m, B);
@@ -800,6 +822,11 @@ int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
     if (pen) {
       hipLaunchKernelGGL((k_penalty_grad<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, k,
                          (const cx<T>*)c->d_X, c->d_pmask, 2.0 * c->mu, (cx<T>*)c->d_L);
+      HIPCHK(c, hipGetLastError());
+    }
+    if (c->src_on) {
+      hipLaunchKernelGGL((k_add_source<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, k, (const cx<T>*)c->d_src,
+                         (cx<T>*)c->d_L);
       HIPCHK(c, hipGetLastError());
     }
   }
@@ -1185,6 +1212,7 @@ TChainArgs tchain_args(qoc_ctx* c) {
   g.mu = c->mu;
   g.J = c->d_J;
   g.coef = c->d_coef;
+  g.src = c->src_on ? c->d_src : nullptr;
   return g;
 }
 
@@ -1348,11 +1376,33 @@ double choose_shift(const double* A, int N, double& mr, double& mi) {
   return best;
 }
 
+// RCCL, resolved on first use (librccl.so.1 of the ROCm install).
+RcclApi& rccl() {
+  static RcclApi api;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (h) {
+      api.getUniqueId = (decltype(api.getUniqueId))dlsym(h, "ncclGetUniqueId");
+      api.commInitRank = (decltype(api.commInitRank))dlsym(h, "ncclCommInitRank");
+      api.allGather = (decltype(api.allGather))dlsym(h, "ncclAllGather");
+      api.commDestroy = (decltype(api.commDestroy))dlsym(h, "ncclCommDestroy");
+      api.getErrorString = (decltype(api.getErrorString))dlsym(h, "ncclGetErrorString");
+      api.ok = api.getUniqueId && api.commInitRank && api.allGather && api.commDestroy && api.getErrorString;
+    }
+  }
+  return api;
+}
+
 int forward(qoc_ctx* c) {
   if (c->big) return c->prec == QOC_FP64 ? big_forward<double>(c) : big_forward<float>(c);
   return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
 }
 int backward(qoc_ctx* c, int order, double* d_dJdu) {
+  if (c->src_on && c->prop_method == QOC_PROP_TSIT5)
+    return fail(c, QOC_ERR_UNSUPPORTED, "a co-state source (dL_dx) is not part of the Tsit5 path (compute_pwc_gradient)");
   if (c->big)
     return c->prec == QOC_FP64 ? big_backward<double>(c, order, d_dJdu) : big_backward<float>(c, order, d_dJdu);
   return c->prec == QOC_FP64 ? run_backward<double>(c, order, d_dJdu) : run_backward<float>(c, order, d_dJdu);
@@ -1488,6 +1538,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   hipMemset(c->d_hist, 0, 13 * 64 * sizeof(unsigned long long));
   c->chain_cb_fwd = getenv("QOC_CHAIN_CB_FWD") ? atoi(getenv("QOC_CHAIN_CB_FWD")) : 0;
   c->chain_cb_bwd = getenv("QOC_CHAIN_CB_BWD") ? atoi(getenv("QOC_CHAIN_CB_BWD")) : 0;
+  c->expm_ps = getenv("QOC_EXPM_PS") && atoi(getenv("QOC_EXPM_PS")) != 0;
   c->expm_alg = (getenv("QOC_EXPM_PADE") && atoi(getenv("QOC_EXPM_PADE")) != 0) ? 0
                 : (getenv("QOC_EXPM_LDS") && atoi(getenv("QOC_EXPM_LDS")) != 0)   ? 2
                                                                                    : 1;
@@ -1501,8 +1552,10 @@ void qoc_destroy(qoc_ctx* c) {
   if (!c) return;
   hipSetDevice(c->dev);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->comm && rccl().commDestroy) rccl().commDestroy(c->comm);
+  if (c->d_best) hipFree(c->d_best);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
-                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_ps, c->d_At, c->d_steps, c->d_terms};
+                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& m : c->marks) {
@@ -1555,6 +1608,7 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
       nrm = std::max(nrm, sum);
     }
     c->a0norm = nrm;
+    c->expm_run = (c->expm_alg == 1 && nrm > 4.0 * kTheta12 && !c->expm_ps) ? 0 : c->expm_alg;
   }
   if (c->tchain_ok) {  // shifted generators Ã_j = A_j - μ_j I and their norms for the Taylor-action chains
     tchain_thresholds(c->tprm, c->prec);
@@ -1577,7 +1631,8 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
     // the Taylor action wins while the slices need few terms (cavity / zz: ||Ã_0||_1 <= 0.2); large norms
     // (tunable bus: ~5 after the shift) keep the propagators on MFMA
     const char* env = getenv("QOC_CHAIN");
-    if (env && !std::strcmp(env, "taylor")) c->chain_mode = 1;
+    if (c->chain_req != QOC_CHAIN_AUTO) c->chain_mode = c->chain_req;
+    else if (env && !std::strcmp(env, "taylor")) c->chain_mode = 1;
     else if (env && !std::strcmp(env, "expm")) c->chain_mode = 0;
     else c->chain_mode = c->tprm.nrm[0] <= 1.0 ? 1 : 0;
   } else {
@@ -1638,8 +1693,31 @@ int qoc_set_state_penalty(qoc_ctx* c, const int* P, int np, const int* C, int nc
     }
   }
   HIPCHK(c, hipSetDevice(c->dev));
+  // kernels queued by the asynchronous entry points may still read the mask: finish them first (the engine
+  // stream is non-blocking, a null-stream copy would not wait for it)
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(c->d_pmask, mask.data(), mask.size(), hipMemcpyHostToDevice));
   c->mu = mu;  // affects J of the next propagate and dL/dx of the next sensitivity
+  return QOC_OK;
+}
+
+int qoc_set_costate_source(qoc_ctx* c, const double* dLdx) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  HIPCHK(c, hipSetDevice(c->dev));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // queued backward kernels may still read the old source
+  if (!dLdx) {
+    c->src_on = false;
+    return QOC_OK;
+  }
+  const size_t n = (size_t)c->B * (c->Nt + 1) * c->N * c->m;
+  if (!c->d_src) {
+    HIPCHK(c, hipMalloc(&c->d_src, n * c->esz));
+    c->dev_bytes += n * c->esz;
+  }
+  int r = upload(c, dLdx, c->d_src, n);
+  if (r) return r;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->src_on = true;
   return QOC_OK;
 }
 
@@ -1767,7 +1845,7 @@ int qoc_get_propagator(qoc_ctx* c, int seed, int k, double* U_out) {
   const size_t NN = (size_t)c->N * c->N, unit = (size_t)seed * c->Nt + k;
   if (c->chain_mode == 1) {  // the Taylor-action chains form no propagators: exp(A_k) of this slice on demand
     hipError_t e = launch_expm(c->prec, c->stream, c->N, c->nu, 1, c->d_A, c->d_u + unit * c->nu, nullptr,
-                               (char*)c->d_U + unit * NN * c->esz, nullptr, nullptr, nullptr, c->expm_alg,
+                               (char*)c->d_U + unit * NN * c->esz, nullptr, nullptr, nullptr, c->expm_run,
                                c->d_hist + 5 * 64, c->d_ps, c->a0norm > 4.0 * kTheta12);
     if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm (propagator on demand): %s", hipGetErrorString(e));
   }
@@ -1832,6 +1910,7 @@ int qoc_set_spline_basis(qoc_ctx* c, const double* Bs, int ns) {
   if (!c || !Bs) return fail(c, QOC_ERR_ARG, "null argument");
   if (ns < 1) return fail(c, QOC_ERR_ARG, "nsplines must be >= 1 (got %d)", ns);
   HIPCHK(c, hipSetDevice(c->dev));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // queued spline kernels may still read the old basis
   if (c->d_Bs) HIPCHK(c, hipFree(c->d_Bs));
   if (c->d_cstage) HIPCHK(c, hipFree(c->d_cstage));
   c->d_Bs = nullptr;
@@ -1973,6 +2052,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[2] = c->ns_iters;
   info[3] = (long long)c->dev_bytes;
   info[4] = c->chain_mode;
+  info[5] = c->big ? c->expm_alg : c->expm_run;  // the large-N pipeline keeps its own (Taylor / Padé) choice
   return QOC_OK;
 }
 
@@ -1983,9 +2063,85 @@ int qoc_set_chain(qoc_ctx* c, int mode) {
   if (mode == QOC_CHAIN_TAYLOR && !c->tchain_ok)
     return fail(c, QOC_ERR_UNSUPPORTED, "Taylor-action chains need N <= 48 (fp64) / 64 (fp32), nu <= 8 and the "
                                         "generators within the 160 KiB LDS");
+  c->chain_req = mode;
   if (mode == QOC_CHAIN_AUTO) mode = c->tchain_ok && c->have_gen && c->tprm.nrm[0] <= 1.0 ? 1 : 0;
   c->chain_mode = mode;
   c->have_prop = false;
+  return QOC_OK;
+}
+
+int qoc_comm_unique_id(void* id_out) {
+  if (!id_out) return fail(nullptr, QOC_ERR_ARG, "id_out is null");
+  RcclApi& r = rccl();
+  if (!r.ok) return fail(nullptr, QOC_ERR_UNSUPPORTED, "RCCL (librccl.so.1) not available");
+  ncclUniqueId id;
+  const ncclResult_t e = r.getUniqueId(&id);
+  if (e != ncclSuccess) return fail(nullptr, QOC_ERR_HIP, "ncclGetUniqueId: %s", r.getErrorString(e));
+  std::memcpy(id_out, &id, sizeof(id));
+  return QOC_OK;
+}
+
+int qoc_comm_init(qoc_ctx* c, int world, int rank, const void* id, long long seed_offset) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  if (world < 1 || rank < 0 || rank >= world) return fail(c, QOC_ERR_ARG, "invalid rank %d of %d", rank, world);
+  if (world > 1 && !id) return fail(c, QOC_ERR_ARG, "unique id is null");
+  HIPCHK(c, hipSetDevice(c->dev));
+  RcclApi& r = rccl();
+  if (c->comm) {
+    r.commDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  if (c->d_best) HIPCHK(c, hipFree(c->d_best));
+  c->d_best = nullptr;
+  HIPCHK(c, hipMalloc((void**)&c->d_best, (size_t)(4 + 2 * world) * sizeof(double)));
+  c->world = world;
+  c->rank = rank;
+  c->seed_offset = seed_offset;
+  if (world > 1) {
+    if (!r.ok) return fail(c, QOC_ERR_UNSUPPORTED, "RCCL (librccl.so.1) not available");
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    const ncclResult_t e = r.commInitRank(&c->comm, world, uid, rank);
+    if (e != ncclSuccess) {
+      c->comm = nullptr;
+      return fail(c, QOC_ERR_HIP, "ncclCommInitRank (rank %d of %d): %s", rank, world, r.getErrorString(e));
+    }
+  }
+  return QOC_OK;
+}
+
+int qoc_allgather_best_dev(qoc_ctx* c, double* d_out) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  HIPCHK(c, hipSetDevice(c->dev));
+  if (!c->d_best) {  // no communicator: this context alone (world 1, seed offset 0)
+    HIPCHK(c, hipMalloc((void**)&c->d_best, 6 * sizeof(double)));
+    c->world = 1;
+    c->rank = 0;
+  }
+  double* res = c->d_best + 2 + 2 * c->world;
+  hipLaunchKernelGGL(k_argmin_seed, dim3(1), dim3(256), 0, c->stream, (const double*)c->d_J, c->B, c->seed_offset,
+                     c->d_best);
+  HIPCHK(c, hipGetLastError());
+  if (c->world > 1) {
+    const ncclResult_t e = rccl().allGather(c->d_best, c->d_best + 2, 2, ncclFloat64, c->comm, c->stream);
+    if (e != ncclSuccess) return fail(c, QOC_ERR_HIP, "ncclAllGather: %s", rccl().getErrorString(e));
+    hipLaunchKernelGGL(k_pick_best, dim3(1), dim3(64), 0, c->stream, (const double*)(c->d_best + 2), c->world, res);
+  } else {
+    HIPCHK(c, hipMemcpyAsync(res, c->d_best, 2 * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIPCHK(c, hipGetLastError());
+  if (d_out) HIPCHK(c, hipMemcpyAsync(d_out, res, 2 * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  return QOC_OK;
+}
+
+int qoc_allgather_best(qoc_ctx* c, double* J_best, int* seed_best) {
+  int r = qoc_allgather_best_dev(c, nullptr);
+  if (r) return r;
+  double h[2];
+  HIPCHK(c, hipMemcpyAsync(h, c->d_best + 2 + 2 * c->world, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (J_best) *J_best = h[0];
+  if (seed_best) *seed_best = (int)h[1];
   return QOC_OK;
 }
 

@@ -129,6 +129,7 @@ struct TChainArgs {
   double mu;
   double* J;               // B
   cx<double>* coef;        // B x m
+  const void* src;         // B x (Nt+1) x N x m caller's dL/dx(x_k) added to λ_k (nullptr: none)
 };
 
 // Thread layout of the Taylor-action chains.  Waves split the rows into G blocks of R = 64 / S rows and the
@@ -398,6 +399,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_bwd(const TChainArgs g
   const double* ub = g.u + (size_t)b * Nt * nu;
   const TStep* stb = g.steps + (size_t)b * Nt;
   const T tmu = (T)(2.0 * g.mu);
+  const cx<T>* srcb = g.src ? (const cx<T>*)g.src + (size_t)b * (Nt + 1) * Nm : nullptr;
   C rg;
   rg.setup(N);
   for (int e = tid; e < (nu + 1) * NN; e += CHAIN_THREADS) {
@@ -423,6 +425,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_bwd(const TChainArgs g
         v.r += tmu * xv.r;
         v.i += tmu * xv.i;
       }
+      if (srcb) {
+        const cx<T> sv = srcb[(size_t)Nt * Nm + o];
+        v.r += sv.r;
+        v.i += sv.i;
+      }
       Lb[(size_t)Nt * Nm + o] = v;
     }
     yb[e] = v;
@@ -445,12 +452,21 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_bwd(const TChainArgs g
     const TPre st = nx;
     if (k > 0) tpre_load(stb + k - 1, ub + (size_t)(k - 1) * nu, nu, nx);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
-    cx<T> xk[NP][CB];  // x_k for the penalty (loaded ahead of the Taylor terms)
+    cx<T> xk[NP][CB];  // 2 mu x_k (penalty) + the caller's dL/dx(x_k), loaded ahead of the Taylor terms
 #pragma unroll
     for (int ps = 0; ps < NP; ++ps)
 #pragma unroll
-      for (int bb = 0; bb < CB; ++bb)
-        xk[ps][bb] = pen_m[ps][bb] ? Xb[(size_t)k * Nm + rg.i + N * (rg.c_begin + rg.c_step * ps + bb)] : cx<T>{0, 0};
+      for (int bb = 0; bb < CB; ++bb) {
+        const size_t o = (size_t)k * Nm + rg.i + N * (rg.c_begin + rg.c_step * ps + bb);
+        cx<T> v = pen_m[ps][bb] ? Xb[o] : cx<T>{0, 0};
+        v.r *= tmu;
+        v.i *= tmu;
+        if (srcb && own[ps][bb]) {
+          v.r += srcb[o].r;
+          v.i += srcb[o].i;
+        }
+        xk[ps][bb] = v;
+      }
     cx<T> a[JT];
     rg.form(N, nu, gen, st.u, ns > 1 ? (T)(1.0 / ns) : T(1), a);
     rg.step(N, m, a, yb, XB, cur, P, ns, cx<double>{st.pr, -st.pi}, acc);
@@ -460,15 +476,15 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_bwd(const TChainArgs g
     for (int ps = 0; ps < NP; ++ps)
 #pragma unroll
       for (int bb = 0; bb < CB; ++bb) {
-        if (pen_m[ps][bb]) {
-          acc[ps][bb].r += tmu * xk[ps][bb].r;
-          acc[ps][bb].i += tmu * xk[ps][bb].i;
+        if (pen_m[ps][bb] || (srcb && own[ps][bb])) {
+          acc[ps][bb].r += xk[ps][bb].r;
+          acc[ps][bb].i += xk[ps][bb].i;
           any_pen = true;
           yb[cur * XB + XS * (rg.c_begin + rg.c_step * ps + bb) + rg.i] = acc[ps][bb];
         }
         if (own[ps][bb]) Lk[rg.i + N * (rg.c_begin + rg.c_step * ps + bb)] = acc[ps][bb];
       }
-    if (g.pmask) {  // the penalised entries of the state changed after the step's last barrier
+    if (g.pmask || srcb) {  // the penalised entries of the state changed after the step's last barrier
       (void)any_pen;
       C::sync();
     }
@@ -719,6 +735,7 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_bwd(const TChainArgs g) {
   const double* ub = g.u + (size_t)b * Nt * nu;
   const TStep* stb = g.steps + (size_t)b * Nt;
   const double tmu = 2.0 * g.mu;
+  const cx<double>* srcb = g.src ? (const cx<double>*)g.src + (size_t)b * (Nt + 1) * Nm : nullptr;
   C rg;
   rg.setup(N, m);
   for (int e = tid; e < (nu + 1) * NN; e += nthr) {
@@ -744,6 +761,10 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_bwd(const TChainArgs g) {
       v.r += tmu * xv.r;
       v.i += tmu * xv.i;
     }
+    if (srcb) {
+      v.r += srcb[(size_t)Nt * Nm + o].r;
+      v.i += srcb[(size_t)Nt * Nm + o].i;
+    }
     Lb[(size_t)Nt * Nm + o] = v;
     const int q = ((col >> 1) * RP + r) * 4 + 2 * (col & 1);
     yb[q] = v.r;
@@ -761,16 +782,18 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_bwd(const TChainArgs g) {
     const TPre st = nx;
     if (k > 0) tpre_load(stb + k - 1, ub + (size_t)(k - 1) * nu, nu, nx);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
-    const double xk = pen_m ? reinterpret_cast<const double*>(Xb + (size_t)k * Nm + rg.rowD + N * rg.colD)[rg.n & 1] : 0.0;
+    const size_t ok_ = (size_t)k * Nm + rg.rowD + N * rg.colD;
+    double xk = pen_m ? tmu * reinterpret_cast<const double*>(Xb + ok_)[rg.n & 1] : 0.0;
+    if (srcb && rg.actD) xk += reinterpret_cast<const double*>(srcb + ok_)[rg.n & 1];
     double ar[KQ], ai[KQ];
     rg.form(N, nu, gen, st.u, ns > 1 ? 1.0 / ns : 1.0, ar, ai);
     rg.step(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, -st.pi}, acc);
-    if (pen_m) {
-      acc += tmu * xk;
+    if (pen_m || (srcb && rg.actD)) {
+      acc += xk;
       rg.put(C::ybuf(yb, rg.CP, cur, 0), C::ybuf(yb, rg.CP, cur, 1), acc);
     }
     if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)k * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = acc;
-    if (g.pmask) rg.sync();  // the penalised entries changed after the step's last barrier
+    if (g.pmask || srcb) rg.sync();  // the penalised entries changed after the step's last barrier
   }
 }
 

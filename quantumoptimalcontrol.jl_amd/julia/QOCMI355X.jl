@@ -19,6 +19,7 @@ const libqoc = get(ENV, "QOC_MI355X_LIB", joinpath(@__DIR__, "..", "qoc_amd", "l
 
 const QOC_FP64 = Cint(0)
 const QOC_COST_TRACE = Cint(0)
+const QOC_COST_ZCAL = Cint(1)
 const QOC_COST_EXTERNAL = Cint(2)
 const QOC_ERR_STALE = Cint(-3)
 
@@ -122,21 +123,76 @@ end
 # evaluated here at x[end] and handed over as λ_{Nt+1} (QOC_COST_EXTERNAL).
 function QOC.grape_sensitivity(A0, A::Vector{<:AbstractMatrix}, dJfinal_dx, u, x0, cache::MI355XCache;
                                dUkdp_order=3, dL_dx=nothing)
-    dL_dx === nothing || dL_dx isa PenaltyGrad ||
-        error("dL_dx must come from QOCMI355X.setup_state_penalty (evaluated on the GPU)")
-    if dL_dx isa PenaltyGrad
-        P = Cint.(dL_dx.P .- 1); C = Cint.(dL_dx.C .- 1)
-        check(ccall((:qoc_set_state_penalty, libqoc), Cint,
-                    (Ptr{Cvoid}, Ptr{Cint}, Cint, Ptr{Cint}, Cint, Cdouble),
-                    cache.ctx, P, length(P), C, length(C), dL_dx.μ), cache.ctx)
+    # setup_state_penalty's gradient runs on the GPU; nothing clears a penalty left by an earlier call
+    # (:47-57 add nothing then); any other closure is evaluated here on every state and the GPU adds
+    # dL_dx(x[k]) to λ[k] (qoc_set_costate_source)
+    set_penalty!(cache, dL_dx isa PenaltyGrad ? dL_dx : nothing)
+    src = nothing
+    if !(dL_dx === nothing || dL_dx isa PenaltyGrad)
+        xs = cache.x
+        src = Array{ComplexF64}(undef, cache.N, cache.m, cache.Nt + 1)
+        for k in 1:cache.Nt+1
+            src[:, :, k] .= dL_dx(xs[k])
+        end
+        GC.@preserve src check(ccall((:qoc_set_costate_source, libqoc), Cint, (Ptr{Cvoid}, Ptr{ComplexF64}),
+                                     cache.ctx, src), cache.ctx)
     end
     λf = Matrix{ComplexF64}(dJfinal_dx(cache.x[end]))
     rc = ccall((:qoc_grape_sensitivity, libqoc), Cint,
                (Ptr{Cvoid}, Ptr{Float64}, Cint, Ptr{ComplexF64}, Ptr{Float64}),
                cache.ctx, Matrix{Float64}(u), dUkdp_order, λf, cache.dJdu)
+    src === nothing || ccall((:qoc_set_costate_source, libqoc), Cint, (Ptr{Cvoid}, Ptr{ComplexF64}), cache.ctx, C_NULL)
     check(rc, cache.ctx)   # QOC_ERR_STALE -> "Cache data from other control signal u"
     return cache.dJdu
 end
+
+function set_penalty!(cache::MI355XCache, dL_dx)
+    if dL_dx isa PenaltyGrad
+        P = Cint.(dL_dx.P .- 1); C = Cint.(dL_dx.C .- 1)
+        check(ccall((:qoc_set_state_penalty, libqoc), Cint,
+                    (Ptr{Cvoid}, Ptr{Cint}, Cint, Ptr{Cint}, Cint, Cdouble),
+                    cache.ctx, P, length(P), C, length(C), dL_dx.μ), cache.ctx)
+    else
+        check(ccall((:qoc_set_state_penalty, libqoc), Cint,
+                    (Ptr{Cvoid}, Ptr{Cint}, Cint, Ptr{Cint}, Cint, Cdouble),
+                    cache.ctx, C_NULL, 0, C_NULL, 0, 0.0), cache.ctx)
+    end
+end
+
+"""Trace infidelity J = 1 - |tr(X'x)|^2/n^2 and its gradient (src/penalty_fcns.jl:15-24), tagged so that the
+GPU path can evaluate them on the device; on host they behave like the reference's closures."""
+struct TraceJ
+    Xt::Matrix{ComplexF64}
+    n::Float64
+end
+struct TraceGrad
+    Xt::Matrix{ComplexF64}
+    n::Float64
+end
+(f::TraceJ)(x) = 1 - abs2(tr(f.Xt' * x)) / f.n^2
+(g::TraceGrad)(x) = (-2 * tr(g.Xt' * x) / g.n^2) .* g.Xt
+tr(A) = sum(A[i, i] for i in 1:minimum(size(A)))
+setup_infidelity(x_target, n=size(x_target, 2)) =
+    (TraceJ(Matrix{ComplexF64}(x_target), n), TraceGrad(Matrix{ComplexF64}(x_target), n))
+
+"""z-calibrated infidelity (src/penalty_fcns.jl:27-42): the reference's closures, tagged for the device."""
+struct ZCalJ
+    Xt::Matrix{ComplexF64}
+    J::Any
+end
+struct ZCalGrad
+    Xt::Matrix{ComplexF64}
+    dJ::Any
+end
+(f::ZCalJ)(x) = f.J(x)
+(g::ZCalGrad)(x) = g.dJ(x)
+function setup_infidelity_zcalibrated(x_target)
+    J, dJ = QOC.setup_infidelity_zcalibrated(x_target)
+    return ZCalJ(Matrix{ComplexF64}(x_target), J), ZCalGrad(Matrix{ComplexF64}(x_target), dJ)
+end
+
+# the reference's "no penalty" pair (examples/zz_coupling_ipopt_exp.jl:46: Returns(0), x -> 0*x)
+no_penalty(L) = L === nothing || (L isa Base.Returns && iszero(L.value))
 
 """Guard-state penalty whose gradient the GPU applies at every slice (src/penalty_fcns.jl:1-11)."""
 struct PenaltyGrad
@@ -153,12 +209,16 @@ end
 """
     setup_ipopt_callbacks(A0Δt, A1Δt, A2Δt, x0, u_prototype, (Jfinal, dJfinal_dx), (L, dL_dx), B; x_target, n)
 
-GPU version of examples/ipopt_callbacks_exp.jl:1-54 for the trace infidelity: f / f_grad evaluate
-u = transpose(B*c), the propagation and the sensitivity in one `qoc_eval_spline` call (the spline map
-runs on the device); g / g_jac are the reference's norm constraints.  Returns the same tuple.
+GPU version of examples/ipopt_callbacks_exp.jl:1-54: f = Jfinal(x[end]) + sum(L, x) and f_grad = B' dJdu'.
+With the tagged costs of this module (setup_infidelity / setup_infidelity_zcalibrated) and penalty
+(setup_state_penalty, or the reference's disabled Returns(0) pair) the spline map, the propagation, the cost
+and the sensitivity run in one `qoc_eval_spline` call on the device.  Any other cost closure is evaluated on
+the host at x[end] and handed over as λ_{Nt+1} (QOC_COST_EXTERNAL), exactly as the reference's f / f_grad do;
+a dL_dx the device cannot apply raises an error instead of being dropped.  g / g_jac are the reference's
+norm constraints.  Returns the same tuple.
 """
 function setup_ipopt_callbacks(A0Δt, A1Δt, A2Δt, x0, u_prototype, (Jfinal, dJfinal_dx), (L, dL_dx), B;
-                               x_target, n)
+                               x_target=nothing, n=nothing)
     nu = size(u_prototype, 1)
     ng = 2
     nx = length(x0)
@@ -169,19 +229,42 @@ function setup_ipopt_callbacks(A0Δt, A1Δt, A2Δt, x0, u_prototype, (Jfinal, dJ
     check(ccall((:qoc_create, libqoc), Cint, (Ref{Ptr{Cvoid}}, Cint, Cint, Cint, Cint, Cint, Cint, Cint),
                 ref, 0, size(A0Δt, 1), size(x0, 2), nu, Nt, 1, QOC_FP64), C_NULL)
     cache = MI355XCache(ref[], size(A0Δt, 1), size(x0, 2), nu, Nt)
-    upload!(cache, A0Δt, [A1Δt, A2Δt], complex(x0))
-    Xt = Matrix{ComplexF64}(x_target)
+    A = [A1Δt, A2Δt][1:nu]
+    upload!(cache, A0Δt, A, complex(x0))
+    # penalty: the device applies setup_state_penalty's; the reference's disabled pair adds nothing; any
+    # other (L, dL_dx) takes the host path below (sum(L, x) on the host, dL_dx through the co-state source)
+    device_penalty = dL_dx isa PenaltyGrad || no_penalty(L)
+    set_penalty!(cache, dL_dx isa PenaltyGrad ? dL_dx : nothing)
+    # cost: on the device when tagged, else the caller's closures on the host (x_target / n keywords: the
+    # trace infidelity, for callers that pass plain closures built from them)
+    if Jfinal isa TraceJ || (x_target !== nothing && !(Jfinal isa ZCalJ))
+        Xt = Jfinal isa TraceJ ? Jfinal.Xt : Matrix{ComplexF64}(x_target)
+        nn = Jfinal isa TraceJ ? Jfinal.n : (n === nothing ? size(Xt, 2) : n)
+        kind = QOC_COST_TRACE
+    elseif Jfinal isa ZCalJ
+        Xt, nn, kind = Jfinal.Xt, 4.0, QOC_COST_ZCAL
+    else
+        Xt, nn, kind = Matrix{ComplexF64}(undef, 0, 0), 1.0, QOC_COST_EXTERNAL
+    end
     check(ccall((:qoc_set_cost, libqoc), Cint, (Ptr{Cvoid}, Cint, Ptr{ComplexF64}, Cdouble),
-                cache.ctx, QOC_COST_TRACE, Xt, n), cache.ctx)
+                cache.ctx, kind, kind == QOC_COST_EXTERNAL ? C_NULL : Xt, nn), cache.ctx)
     Bm = Matrix{Float64}(B)
     check(ccall((:qoc_set_spline_basis, libqoc), Cint, (Ptr{Cvoid}, Ptr{Float64}, Cint),
                 cache.ctx, Bm, nsplines), cache.ctx)
     c_prev = fill(NaN, nc)
     J = Ref{Cdouble}(0.0)
     dJdc = zeros(nc)
-    evaluate!(c) = check(ccall((:qoc_eval_spline, libqoc), Cint,
-                               (Ptr{Cvoid}, Ptr{Float64}, Cint, Ref{Cdouble}, Ptr{Float64}),
-                               cache.ctx, c, 3, J, dJdc), cache.ctx)
+    evaluate!(c) = if kind != QOC_COST_EXTERNAL && device_penalty
+        check(ccall((:qoc_eval_spline, libqoc), Cint,
+                    (Ptr{Cvoid}, Ptr{Float64}, Cint, Ref{Cdouble}, Ptr{Float64}),
+                    cache.ctx, c, 3, J, dJdc), cache.ctx)
+    else  # examples/ipopt_callbacks_exp.jl:14-18, 27-28 with the caller's closures
+        u = Matrix(transpose(Bm * reshape(c, nsplines, nu)))
+        x = QOC.propagate(A0Δt, A, u, x0, cache)
+        J[] = Jfinal(x[end]) + (no_penalty(L) ? 0.0 : sum(L, x))
+        dJdu = QOC.grape_sensitivity(A0Δt, A, dJfinal_dx, cache.u, x0, cache; dUkdp_order=3, dL_dx=dL_dx)
+        dJdc .= (Bm' * transpose(dJdu))[:]
+    end
     f = function (c::Vector{Float64})
         c_prev .= c
         evaluate!(c)

@@ -20,11 +20,11 @@ from .api import (  # noqa: F401
     setup_infidelity_zcalibrated,
     setup_state_penalty,
 )
-from .engine import GrapeEngine, expm, expm_jacobian  # noqa: F401
+from .engine import GrapeEngine, comm_unique_id, expm, expm_jacobian  # noqa: F401
 from .optimize import SplineGrape, minimize_batched  # noqa: F401
 
 __all__ = [
-    "GrapeEngine", "MI355XCache", "QOCError", "StaleCacheError", "expm", "expm_jacobian",
+    "GrapeEngine", "MI355XCache", "comm_unique_id", "QOCError", "StaleCacheError", "expm", "expm_jacobian",
     "grape_sensitivity", "propagate", "setup_bilinear_matrices", "setup_grape_cache",
     "setup_infidelity", "setup_infidelity_zcalibrated", "setup_state_penalty", "systems",
     "SplineGrape", "minimize_batched", "propagate_pwc", "compute_pwc_gradient",

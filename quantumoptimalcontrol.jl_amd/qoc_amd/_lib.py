@@ -43,6 +43,7 @@ SIGNATURES = {
     "qoc_set_x0": (C.c_int, [_vp, _dp, C.c_int]),
     "qoc_set_cost": (C.c_int, [_vp, C.c_int, _dp, C.c_double]),
     "qoc_set_state_penalty": (C.c_int, [_vp, _ip, C.c_int, _ip, C.c_int, C.c_double]),
+    "qoc_set_costate_source": (C.c_int, [_vp, _dp]),
     "qoc_propagate": (C.c_int, [_vp, _dp, _dp]),
     "qoc_grape_sensitivity": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp]),
     "qoc_propagate_dev": (C.c_int, [_vp, _vp, _vp]),
@@ -59,6 +60,10 @@ SIGNATURES = {
     "qoc_propagate_envelope": (C.c_int, [_vp, C.c_int, _dp, C.c_int, C.c_double, C.c_double, _dp, _dp]),
     "qoc_get_info": (C.c_int, [_vp, C.POINTER(C.c_longlong)]),
     "qoc_set_chain": (C.c_int, [_vp, C.c_int]),
+    "qoc_comm_unique_id": (C.c_int, [_vp]),
+    "qoc_comm_init": (C.c_int, [_vp, C.c_int, C.c_int, _vp, C.c_longlong]),
+    "qoc_allgather_best": (C.c_int, [_vp, _dp, _ip]),
+    "qoc_allgather_best_dev": (C.c_int, [_vp, _vp]),
     "qoc_chain_terms": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_set_spline_basis": (C.c_int, [_vp, _dp, C.c_int]),
     "qoc_eval_spline_dev": (C.c_int, [_vp, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),

@@ -190,10 +190,17 @@ def setup_grape_cache(A0, x0, u_size, B=1, precision="fp64", device=0) -> MI355X
 
 
 def propagate(A0, A, u, x0, cache: MI355XCache | None = None):
-    """Forward PWC propagation (src/gradient_computations.jl:2-32); returns the lazy x series."""
+    """Forward PWC propagation (src/gradient_computations.jl:2-32), U_k = exp(A_k); returns the lazy x series.
+    A cache last used by propagate_pwc (Tsit5) is switched back to the exponential."""
     u = np.asarray(u, dtype=np.float64)
     if cache is None:
         cache = setup_grape_cache(A0, x0, u.shape[-2:], B=1 if u.ndim == 2 else u.shape[0])
+    if getattr(cache.engine, "prop_method", "expm") != "expm":
+        cache.engine.set_propagation("expm")
+    return _propagate(A0, A, u, x0, cache)
+
+
+def _propagate(A0, A, u, x0, cache: MI355XCache):
     e = cache.engine
     e.set_generators(A0, A)
     x0 = np.asarray(x0, dtype=np.complex128)
@@ -213,16 +220,21 @@ def grape_sensitivity(A0, A, dJfinal_dx, u, x0, cache: MI355XCache, dUkdp_order=
     if not cache._propagated or u.shape != cache.u.shape or not np.array_equal(u, cache.u):
         raise StaleCacheError(-3, "Cache data from other control signal u")          # :37-39
     e = cache.engine
-    if dL_dx is not None:
-        if getattr(dL_dx, "kind", None) != "penalty":
-            raise NotImplementedError("dL_dx must come from setup_state_penalty (evaluated on the GPU)")
+    B = e.B
+    src = None
+    if dL_dx is not None and getattr(dL_dx, "kind", None) == "penalty":
         m = dL_dx.meta
-        e.set_state_penalty(m["P"], m["C"], m["mu"])
+        e.set_state_penalty(m["P"], m["C"], m["mu"])  # applied on the GPU at every slice
     else:
         e.set_state_penalty([], [], 0.0)
-    B = e.B
+        if dL_dx is not None:  # any other closure: evaluated here on every state, added to λ_k on the GPU
+            src = np.stack([[np.asarray(dL_dx(e.state(k, b)), dtype=np.complex128) for k in range(e.Nt + 1)]
+                            for b in range(B)])
+    e.set_costate_source(src)
     lam = np.stack([np.asarray(dJfinal_dx(e.state(-1, b)), dtype=np.complex128) for b in range(B)])  # :46
     dJdu = e.grape_sensitivity(u, dUkdp_order, lambda_final=lam)
+    if src is not None:
+        e.set_costate_source(None)
     cache.dJdu = dJdu[0] if u.ndim == 2 else dJdu
     return cache.dJdu
 
@@ -246,8 +258,8 @@ def propagate_pwc(A0, A, x0, u, Δt, cache: MI355XCache | None = None, dt=None):
         cache = setup_grape_cache(A0, x0, u.shape[-2:], B=1 if u.ndim == 2 else u.shape[0])
     e = cache.engine
     e.set_propagation("tsit5", _nsub(Δt, dt))
-    return propagate(Δt * np.asarray(A0, dtype=np.complex128), [Δt * np.asarray(a, dtype=np.complex128) for a in A],
-                     u, x0, cache)
+    return _propagate(Δt * np.asarray(A0, dtype=np.complex128), [Δt * np.asarray(a, dtype=np.complex128) for a in A],
+                      u, x0, cache)
 
 
 def compute_pwc_gradient(dJfinal_dx, u, Δt, A0, A, cache: MI355XCache, dUkdp_order=2, dt=None, x0=None):

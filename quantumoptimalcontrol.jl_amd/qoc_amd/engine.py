@@ -141,6 +141,20 @@ class GrapeEngine:
         self._chk(self._lib.qoc_set_state_penalty(self._h, P.ctypes.data_as(ip), len(P), Cc.ctypes.data_as(ip),
                                                   len(Cc), float(mu)))
 
+    def set_costate_source(self, dLdx):
+        """dL_dx(x_k) of a caller's penalty closure for every seed and k = 0..Nt ((B, Nt+1, N, m) complex, or
+        (Nt+1, N, m) for B = 1), added to λ_k by the following grape_sensitivity calls; None clears it."""
+        if dLdx is None:
+            self._chk(self._lib.qoc_set_costate_source(self._h, None))
+            return
+        d = np.asarray(dLdx, dtype=np.complex128)
+        if d.ndim == 3:
+            d = d[None]
+        if d.shape != (self.B, self.Nt + 1, self.N, self.m):
+            raise ValueError(f"dL_dx values must be (B, Nt+1, N, m) = {(self.B, self.Nt + 1, self.N, self.m)}")
+        flat = np.ascontiguousarray(np.transpose(d, (0, 1, 3, 2))).ravel().view(np.float64)
+        self._chk(self._lib.qoc_set_costate_source(self._h, _ptr(flat)))
+
     def set_propagation(self, method: str = "expm", nsub: int = 10):
         """'expm' (U_k = exp(A_k), default) or 'tsit5': the reference's ODE path (propagate_pwc /
         compute_pwc_gradient, src/gradient_computations.jl:108-169) with nsub fixed Tsit5 steps per
@@ -266,13 +280,32 @@ class GrapeEngine:
         v = np.zeros(8, dtype=np.int64)
         self._chk(self._lib.qoc_get_info(self._h, v.ctypes.data_as(C.POINTER(C.c_longlong))))
         return {"path": "large_n" if v[0] else "lds", "chunk": int(v[1]), "ns_iters": int(v[2]),
-                "device_bytes": int(v[3]), "chain": "taylor" if v[4] == 1 else "propagators"}
+                "device_bytes": int(v[3]), "chain": "taylor" if v[4] == 1 else "propagators",
+                "expm": {0: "pade", 1: "taylor_rr", 2: "ps_lds"}.get(int(v[5]), "?")}
 
     def set_chain(self, mode: str = "auto"):
         """How the chains apply exp(A_k) (include/qoc.h qoc_set_chain): 'propagators' forms every U_k (the
         reference's structure), 'taylor' applies the exponential to the state directly, 'auto' chooses by
         the generator norms."""
         self._chk(self._lib.qoc_set_chain(self._h, L.QOC_CHAIN[mode]))
+
+    # ---- multi-GPU epilogue (include/qoc.h qoc_comm_* / qoc_allgather_best) -------------
+    def comm_init(self, world: int, rank: int, unique_id: bytes | None, seed_offset: int):
+        """Join the RCCL communicator of `world` ranks (unique_id: the QOC_UNIQUE_ID_BYTES bytes one rank made
+        with comm_unique_id(); None for world = 1).  seed_offset: global id of this context's seed 0."""
+        buf = C.create_string_buffer(bytes(unique_id), 128) if unique_id is not None else None
+        self._chk(self._lib.qoc_comm_init(self._h, int(world), int(rank), buf, int(seed_offset)))
+
+    def allgather_best(self):
+        """(J_best, global seed) of the last propagate over every rank of the communicator."""
+        J = C.c_double()
+        s = C.c_int()
+        self._chk(self._lib.qoc_allgather_best(self._h, C.byref(J), C.byref(s)))
+        return J.value, s.value
+
+    def allgather_best_device(self, d_out: int):
+        """Same, written as two doubles to device memory on the engine stream (no host synchronisation)."""
+        self._chk(self._lib.qoc_allgather_best_dev(self._h, C.c_void_p(d_out)))
 
     def chain_terms(self, reset: bool = False) -> int:
         """Taylor terms executed per direction since the last reset (Taylor-action chains)."""
@@ -303,6 +336,14 @@ class GrapeEngine:
                 if h[di * 64 + s]:
                     out[(d, s)] = int(h[di * 64 + s])
         return out
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (128 bytes) for qoc_comm_init; made on one rank and sent to the others."""
+    lib = L.load()
+    buf = C.create_string_buffer(128)
+    L.check(lib.qoc_comm_unique_id(buf))
+    return buf.raw
 
 
 def expm(A, precision: str = "fp64", device: int = 0, return_degrees: bool = False):

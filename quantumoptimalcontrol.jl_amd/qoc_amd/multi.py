@@ -1,7 +1,12 @@
 """Multi-GPU epilogue: seeds are sharded contiguously over ranks (one process per GPU); the
 only exchange on the path is an all-gather of each rank's best (J, global seed id)
-(SURVEY.md §8e).  On ROCm ``torch.distributed``'s "nccl" backend is RCCL over xGMI; the same
-code runs on "gloo" for the CPU tests.
+(SURVEY.md §8e).
+
+Two transports with the same result:
+  * ``init_engine_comm`` + ``GrapeEngine.allgather_best[_device]``: RCCL inside libqoc_mi355x.so
+    (include/qoc.h qoc_comm_init / qoc_allgather_best) — what a Julia caller binds; torch.distributed only
+    carries the 128-byte unique id;
+  * ``gather_best``: torch.distributed (RCCL on ROCm's "nccl" backend, or "gloo" for CPU tests).
 """
 from __future__ import annotations
 
@@ -33,3 +38,29 @@ def gather_best(J_local, seed_offset: int, out=None):
     allv = out.view(world, 2)
     r = int(torch.argmin(allv[:, 0]))
     return float(allv[r, 0]), int(allv[r, 1])
+
+
+def init_engine_comm(engine, seed_offset: int) -> bool:
+    """Join the engine's RCCL communicator over the default process group: rank 0 makes the unique id and
+    torch.distributed broadcasts it.  Returns False (and leaves the engine on its own) when RCCL is missing."""
+    import torch.distributed as dist
+
+    from . import _lib
+    from .engine import comm_unique_id
+
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    if world == 1:
+        engine.comm_init(1, 0, None, seed_offset)
+        return True
+    box = [None]
+    if rank == 0:
+        try:
+            box[0] = comm_unique_id()
+        except _lib.QOCError:
+            box[0] = b""
+    dist.broadcast_object_list(box, src=0)
+    if not box[0]:
+        return False
+    engine.comm_init(world, rank, box[0], seed_offset)
+    return True

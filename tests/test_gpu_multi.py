@@ -1,0 +1,90 @@
+"""Multi-GPU epilogue on the one-GPU box.
+
+* qoc_allgather_best through the C ABI (RCCL communicator of one rank): the best (J, global seed) of the last
+  propagate equals the argmin over the engine's J.
+* Two ranks sharing the one device, each propagating its contiguous shard of the seeds through its own engine:
+  the gathered best equals the single-process argmin over the full batch.  RCCL rejects two ranks on one GPU
+  ("Duplicate GPU detected"), so these two ranks exchange over gloo (qoc_amd.multi.gather_best); the RCCL
+  all-gather itself runs in the driver's multi-GPU bench (bench.py, transport "rccl-libqoc").
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+B_TOTAL, NT = 12, 40
+
+
+def _problem():
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=8, Nt=NT)
+    u = systems.cavity_controls(B_TOTAL, NT, seed=17) * 4.0  # spread the fidelities
+    return prob, u
+
+
+def test_allgather_best_world1_c_abi(built_lib):
+    from qoc_amd import GrapeEngine
+    prob, u = _problem()
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, NT, B=B_TOTAL)
+    e.set_cost_trace(prob.x_target, prob.n)
+    J = e.propagate(u)
+    assert e.allgather_best() == (J.min(), int(np.argmin(J)))  # no communicator: this context alone
+    e.comm_init(1, 0, None, 1000)
+    Jb, sb = e.allgather_best()
+    assert Jb == J.min() and sb == 1000 + int(np.argmin(J))
+    e.close()
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "quantumoptimalcontrol.jl_amd"))
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from qoc_amd import GrapeEngine, multi
+    prob, u = _problem()
+    start, stop = multi.shard(B_TOTAL, rank, world)
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, NT, B=stop - start)
+    e.set_cost_trace(prob.x_target, prob.n)
+    J = e.propagate(u[start:stop])
+    res = multi.gather_best(torch.from_numpy(J), start)
+    e.close()
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_two_ranks_share_the_gpu_and_gather_the_global_best(built_lib):
+    import torch.multiprocessing as mp
+    from qoc_amd import GrapeEngine
+    prob, u = _problem()
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, NT, B=B_TOTAL)
+    e.set_cost_trace(prob.x_target, prob.n)
+    J = e.propagate(u)
+    e.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, (Jb, sb) in out:
+        assert sb == int(np.argmin(J))
+        assert abs(Jb - J.min()) <= 1e-13

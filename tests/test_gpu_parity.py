@@ -408,7 +408,7 @@ def test_fused_gradient_equals_per_slice_kernel(built_lib, monkeypatch, which):
 
 
 @pytest.mark.parametrize("which", ["two_pass", "mix"])
-def test_t12_and_paterson_stockmeyer_passes(built_lib, which):
+def test_t12_and_paterson_stockmeyer_passes(built_lib, monkeypatch, which):
     """Slices with ||A_k||_1 > 4 theta_12 run Paterson-Stockmeyer (fewer squarings than T12): through the
     second pass over the listed units when ||A0||_1 is small (cavity with a few large controls), or in the
     one-pass mixed kernel when ||A0||_1 is large (tunable bus).  Both match the oracle; the executed
@@ -419,6 +419,7 @@ def test_t12_and_paterson_stockmeyer_passes(built_lib, which):
         u = systems.cavity_controls(3, prob.Nt, seed=21)
         u[:, :, ::3] *= 60.0  # every third slice: ||A_k||_1 of a few units
     else:
+        monkeypatch.setenv("QOC_EXPM_PS", "1")  # large norms default to the reference's Padé-13 otherwise
         prob = systems.tunable_bus_problem(Nt=200)
         u = systems.tunable_bus_controls(2, prob.Nt, seed=22)
     e = _engine(prob, u.shape[0], chain="propagators")
@@ -482,3 +483,54 @@ def test_external_cost_and_costates(built_lib, chain):
             assert np.abs(e.state(k, seed=b) - cache.x[k]).max() < 1e-13
             assert np.abs(e.costate(k, seed=b) - cache.lam[k]).max() < 1e-12
     e.close()
+
+
+def test_large_norm_slices_default_to_the_reference_pade(built_lib):
+    """||A0||_1 > 4 theta_12 (tunable bus): the propagators run the reference's Padé-13 + solve by default (no
+    Taylor scheme in the executed histogram) and match the oracle."""
+    from qoc_amd import systems
+    prob = systems.tunable_bus_problem(Nt=120)
+    u = systems.tunable_bus_controls(2, prob.Nt, seed=23)
+    e = _engine(prob, 2)
+    assert e.info()["chain"] == "propagators"
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    assert e.taylor_histogram() == {}
+    assert sum(v for (d, _), v in e.pade_histogram().items() if d == 13) == 2 * prob.Nt
+    e.close()
+    for b in range(2):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        assert abs(J[b] - Jr) <= 1e-12
+        assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
+
+
+@pytest.mark.parametrize("path", ["propagators", "taylor", "large_n"])
+def test_arbitrary_dL_dx_closure(built_lib, monkeypatch, path):
+    """A penalty gradient that is not setup_state_penalty's (src/gradient_computations.jl:47-49, 55-57 accept
+    any closure): the host evaluates it on every state, the GPU adds dL_dx(x_k) to λ_k in the backward chain
+    (qoc_set_costate_source).  Against the oracle with the same closure, through the reference-shaped API."""
+    import qoc_amd as Q
+    from qoc_amd import systems
+    if path == "large_n":
+        monkeypatch.setenv("QOC_FORCE_LARGE_N", "1")
+    prob = systems.zz_problem(24, tgate=2.4)
+    u = systems.zz_controls(1, 24, 2.4, seed=6)[0]
+    rng = np.random.default_rng(2)
+    W = rng.uniform(0.0, 0.4, size=(prob.N, prob.m))
+    dL = lambda x: W * x + 0.05 * np.conj(x) ** 0 * x[0, 0]  # noqa: E731  (not a tagged penalty)
+    cache = Q.setup_grape_cache(prob.A0, prob.x0, u.shape)
+    if path != "large_n":
+        cache.engine.set_chain(path)
+    Q.propagate(prob.A0, prob.A, u, prob.x0, cache)
+    Jf, dJf = O.setup_infidelity(prob.x_target, 4)
+    g = Q.grape_sensitivity(prob.A0, prob.A, dJf, cache.u, prob.x0, cache, dUkdp_order=3, dL_dx=dL)
+    c2 = O.setup_grape_cache(prob.A0, prob.x0, u.shape)
+    O.propagate(prob.A0, prob.A, u, prob.x0, c2)
+    gr = O.grape_sensitivity(prob.A0, prob.A, dJf, c2.u, prob.x0, c2, dUkdp_order=3, dL_dx=dL)
+    assert np.linalg.norm(g - gr) / np.linalg.norm(gr) < 1e-10
+    for k in (0, 11, 24):
+        assert np.abs(cache.lam[k] - c2.lam[k]).max() < 1e-12
+    # the source is cleared afterwards: an unpenalised call matches the oracle without dL_dx
+    g0 = Q.grape_sensitivity(prob.A0, prob.A, dJf, cache.u, prob.x0, cache, dUkdp_order=3)
+    gr0 = O.grape_sensitivity(prob.A0, prob.A, dJf, c2.u, prob.x0, c2, dUkdp_order=3)
+    assert np.linalg.norm(g0 - gr0) / np.linalg.norm(gr0) < 1e-10
