@@ -577,6 +577,12 @@ struct TChainMF {
     for (int q = 0; q < KQ; ++q) bv[q] = y[base + 16 * q];
 #pragma unroll
     for (int q = 0; q < KQ; ++q) bp[q] = yp[base + 16 * q];
+    // the scheduler keeps ~2 reads ahead of the MFMAs; issuing all of them first (QOC_TCHAIN_EAGER_READS) measured
+    // slower on the same box (N = 40: 499 vs 464 ns per term, tools/tchain_probe.hip), the three waves' bursts
+    // queue in the LDS ahead of the first operands
+#ifdef QOC_TCHAIN_EAGER_READS
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     // two accumulation chains, alternating, so consecutive MFMAs never depend on each other; the Ar products
     // first (their operands arrive first)
     double d0 = 0.0, d1 = 0.0;

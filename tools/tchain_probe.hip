@@ -39,22 +39,26 @@ void run(int N, int m, int Nt, int B, int P) {
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   float ms = 0;
-  unsigned long long z[16] = {};
   for (int it = 0; it < 3; ++it) {
+#ifdef QOC_PROBE
+    unsigned long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tc), z, sizeof(z));
+#endif
     (void)hipEventRecord(a);
     hipLaunchKernelGGL((k_tchain_fwd<double, S, JT, CB, NP>), dim3(B), dim3(CHAIN_THREADS), lds, 0, g);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     (void)hipEventElapsedTime(&ms, a, b);
   }
+  printf("N=%d m=%d Nt=%d B=%d P=%d (S=%d JT=%d CB=%d): %.3f ms = %.3f us/step, %.0f ns/term\n", N, m, Nt, B, P, S, JT, CB, ms,
+         ms * 1e3 / Nt, ms * 1e6 / Nt / P);
+#ifdef QOC_PROBE
   unsigned long long tc[16];
   (void)hipMemcpyFromSymbol(tc, HIP_SYMBOL(g_tc), sizeof(tc));
   const double nt = (double)tc[3];
-  printf("N=%d m=%d Nt=%d B=%d P=%d (S=%d JT=%d CB=%d): %.3f ms = %.3f us/step, %.0f ns/term\n", N, m, Nt, B, P, S, JT, CB, ms,
-         ms * 1e3 / Nt, ms * 1e6 / Nt / P);
   printf("   per term (s_memtime units): matvec %.0f  matvec+store %.0f  barrier %.0f  (terms %.0f)\n", tc[0] / nt,
          tc[1] / nt, tc[2] / nt, nt);
+#endif
 }
 
 template <int KQ>
@@ -89,9 +93,11 @@ void run_mf(int N, int m, int Nt, int B, int P) {
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   float ms = 0;
-  unsigned long long z[16] = {};
   for (int it = 0; it < 3; ++it) {
+#ifdef QOC_PROBE
+    unsigned long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tc), z, sizeof(z));
+#endif
     (void)hipEventRecord(a);
     hipLaunchKernelGGL((k_tchain_mf_fwd<KQ>), dim3(B), dim3(64 * tchain_mf_waves(N, m)), lds, 0, g);
     (void)hipEventRecord(b);
@@ -100,11 +106,13 @@ void run_mf(int N, int m, int Nt, int B, int P) {
   }
   printf("MFMA N=%d m=%d Nt=%d B=%d P=%d (KQ=%d, %d waves): %.3f ms = %.3f us/step, %.0f ns/term\n", N, m, Nt, B, P, KQ,
          tchain_mf_waves(N, m), ms, ms * 1e3 / Nt, ms * 1e6 / Nt / P);
+#ifdef QOC_PROBE
   unsigned long long tc[16];
   (void)hipMemcpyFromSymbol(tc, HIP_SYMBOL(g_tc), sizeof(tc));
   const double nt = (double)tc[7];
   printf("   per term (s_memtime): matvec %.0f  put %.0f  barrier %.0f  (terms %.0f); clock %.2f GHz\n", tc[4] / nt, tc[5] / nt,
          tc[6] / nt, nt, (double)tc[8] / ((double)tc[9] * 10.0));
+#endif
 }
 
 int main() {
