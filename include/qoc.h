@@ -157,7 +157,8 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
  * info[1] = slices per chunk (large-N), info[2] = Newton-Schulz iterations executed so far (large-N),
  * info[3] = device bytes allocated by the context, info[4] = chain mode (QOC_CHAIN_PROPAGATORS /
  * QOC_CHAIN_TAYLOR), info[5] = exponential the propagators run (0 the reference's Padé + solve, 1 register-
- * resident Taylor / Paterson-Stockmeyer, 2 LDS Paterson-Stockmeyer), info[6..7] reserved (0).  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
+ * resident Taylor / Paterson-Stockmeyer, 2 LDS Paterson-Stockmeyer), info[6] = 1 when the Taylor-action chains
+ * use Chebyshev terms (skew-Hermitian generators, fp64; QOC_TCHAIN_POLY=taylor keeps Taylor), info[7] reserved.  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
  * selects the large-N path for any size (testing). */
 int qoc_get_info(qoc_ctx* ctx, long long* info /*[8]*/);
 

@@ -126,6 +126,10 @@ struct qoc_ctx {
   TStep* d_steps = nullptr;      // B x Nt (P, s, e^{μ_k})
   unsigned long long* d_terms = nullptr;  // Σ P s per forward (executed Taylor terms per direction)
   TChainParams tprm{};
+  bool cheb_ok = false;          // generators skew-Hermitian with imaginary shifts: Chebyshev applies
+  bool cheb = false;             // Chebyshev terms (k_tchain_prep_cheb) instead of Taylor (QOC_TCHAIN_POLY=taylor)
+  bool cheb_ran = false;         // what the last forward pass used (the backward pass reuses its steps)
+  double* d_tcoef = nullptr;     // B x Nt x TCHEB_STRIDE Chebyshev coefficients (allocated on first use)
   long long props_since_reset = 0;  // forward passes since the last Padé-histogram reset (chain mode 1)
   // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
   ncclComm_t comm = nullptr;
@@ -1213,6 +1217,7 @@ TChainArgs tchain_args(qoc_ctx* c) {
   g.J = c->d_J;
   g.coef = c->d_coef;
   g.src = c->src_on ? c->d_src : nullptr;
+  g.tcoef = c->d_tcoef;
   return g;
 }
 
@@ -1238,12 +1243,23 @@ hipError_t tchain_mf_dispatch(int N, F&& f) {
 template <typename T>
 int tchain_forward(qoc_ctx* c) {
   const long long units = (long long)c->B * c->Nt;
+  const bool cheb = c->cheb && tchain_mf(c);
+  if (cheb && !c->d_tcoef) {
+    const size_t bytes = (size_t)units * TCHEB_STRIDE * sizeof(double);
+    HIPCHK(c, hipMalloc((void**)&c->d_tcoef, bytes));
+    c->dev_bytes += bytes;
+  }
   int mk = mark_begin(c, 0);
   const unsigned pb = (unsigned)std::min<long long>((units + 255) / 256, 2048);
-  hipLaunchKernelGGL(k_tchain_prep, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u, c->tprm,
-                     c->d_steps, c->d_terms);
+  if (cheb)
+    hipLaunchKernelGGL(k_tchain_prep_cheb, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u,
+                       c->tprm, c->d_steps, c->d_tcoef, c->d_terms);
+  else
+    hipLaunchKernelGGL(k_tchain_prep, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u, c->tprm,
+                       c->d_steps, c->d_terms);
   mark_end(c, mk);
   HIPCHK(c, hipGetLastError());
+  c->cheb_ran = cheb;
   const TChainArgs g = tchain_args(c);
   if (tchain_mf(c)) {
     const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
@@ -1251,9 +1267,10 @@ int tchain_forward(qoc_ctx* c) {
     mk = mark_begin(c, 1);
     hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
-      hipError_t r = hipFuncSetAttribute((const void*)k_tchain_mf_fwd<KQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      auto kern = cheb ? k_tchain_mf_fwd<KQ, true> : k_tchain_mf_fwd<KQ, false>;
+      hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (r != hipSuccess) return r;
-      hipLaunchKernelGGL((k_tchain_mf_fwd<KQ>), dim3(c->B), dim3(threads), lds, c->stream, g);
+      hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);
       return hipGetLastError();
     });
     mark_end(c, mk);
@@ -1287,9 +1304,11 @@ int tchain_backward(qoc_ctx* c) {
     int mk = mark_begin(c, 2);
     hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
-      hipError_t r = hipFuncSetAttribute((const void*)k_tchain_mf_bwd<KQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      // the (P, s, coefficients) of the forward pass are reused: the same polynomial as the states'
+      auto kern = c->cheb_ran ? k_tchain_mf_bwd<KQ, true> : k_tchain_mf_bwd<KQ, false>;
+      hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (r != hipSuccess) return r;
-      hipLaunchKernelGGL((k_tchain_mf_bwd<KQ>), dim3(c->B), dim3(threads), lds, c->stream, g);
+      hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);
       return hipGetLastError();
     });
     mark_end(c, mk);
@@ -1554,6 +1573,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->comm && rccl().commDestroy) rccl().commDestroy(c->comm);
   if (c->d_best) hipFree(c->d_best);
+  if (c->d_tcoef) hipFree(c->d_tcoef);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
                   c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src};
   for (void* p : ptrs)
@@ -1628,6 +1648,23 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
       if (r == QOC_OK) HIPCHK(c, hipStreamSynchronize(c->stream));  // sh is reused
     }
     if (r != QOC_OK) return r;
+    // Chebyshev needs every Ã_j skew-Hermitian (A_j^H = -A_j, Schrödinger generators -i H Δt) with an imaginary
+    // shift, so that Ã_k = -i H̃_k has its spectrum on the imaginary axis within the bound β_k
+    bool skew = true;
+    for (int j = 0; j <= c->nu && skew; ++j) {
+      const double* G = j == 0 ? A0 : Aj[j - 1];
+      double amax = 0.0, dev = 0.0;
+      for (int col = 0; col < c->N; ++col)
+        for (int row = 0; row < c->N; ++row) {
+          const size_t a = 2 * (row + (size_t)c->N * col), b = 2 * (col + (size_t)c->N * row);
+          amax = std::max(amax, std::hypot(G[a], G[a + 1]));
+          dev = std::max(dev, std::hypot(G[a] + G[b], G[a + 1] - G[b + 1]));  // |A + A^H|
+        }
+      skew = dev <= 1e-13 * std::max(amax, 1e-300) && std::fabs(c->tprm.mur[j]) <= 1e-13 * std::max(amax, 1e-300);
+    }
+    c->cheb_ok = skew;
+    const char* poly = getenv("QOC_TCHAIN_POLY");
+    c->cheb = skew && !(poly && !std::strcmp(poly, "taylor"));
     // the Taylor action wins while the slices need few terms (cavity / zz: ||Ã_0||_1 <= 0.2); large norms
     // (tunable bus: ~5 after the shift) keep the propagators on MFMA
     const char* env = getenv("QOC_CHAIN");
@@ -2053,6 +2090,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[3] = (long long)c->dev_bytes;
   info[4] = c->chain_mode;
   info[5] = c->big ? c->expm_alg : c->expm_run;  // the large-N pipeline keeps its own (Taylor / Padé) choice
+  info[6] = c->chain_mode == 1 && c->cheb && tchain_mf(c) ? 1 : 0;  // Taylor-action chains: Chebyshev terms
   return QOC_OK;
 }
 

@@ -50,9 +50,14 @@ __device__ unsigned long long g_tc[16];
 // Per-(seed, slice) step data written by k_tchain_prep: e^{μ_k} and the (P, s) choice.
 struct TStep {
   double pr, pi;  // e^{μ_k}
-  int P, s;       // Taylor terms per substep, substeps
-  double pad;     // 32-byte records (two 16-byte loads)
+  int P, s;       // terms per substep, substeps
+  double scale;   // operand scale: Taylor 1/s, Chebyshev 2/β (32-byte records: two 16-byte loads)
 };
+
+// Chebyshev coefficients per slice (c_0 = J_0(ρ), c_t = 2 J_t(ρ)), one 64-double record per slice: lane t of the
+// chain reads c_t (a register), the term loop takes it with v_readlane.
+constexpr int TCHEB_PMAX = 60;
+constexpr int TCHEB_STRIDE = 64;
 
 constexpr int TCHAIN_PMAX = 30;  // thresholds θ_P for P = 1..TCHAIN_PMAX
 constexpr int TCHAIN_NUMAX = 8;  // controls per slice the Taylor-action chains take
@@ -63,9 +68,12 @@ constexpr int TCHAIN_NUMAX = 8;  // controls per slice the Taylor-action chains 
 struct TPre {
   double pr, pi;
   int P, s;
+  double scale;
+  double cl;  // Chebyshev: c_t of this lane's t = lane (v_readlane'd by the term loop)
   double u[TCHAIN_NUMAX];
 };
-__device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const double* __restrict__ uk, int nu, TPre& d) {
+__device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const double* __restrict__ uk, int nu, TPre& d,
+                                          const double* __restrict__ ce = nullptr) {
   int z;
   asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // per-lane (VGPR) address: global_load, not s_load
   const double4 v = *reinterpret_cast<const double4*>(reinterpret_cast<const double*>(st) + z);
@@ -74,6 +82,8 @@ __device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const do
   const long long ps = __double_as_longlong(v.z);
   d.P = (int)(ps & 0xffffffff);
   d.s = (int)(ps >> 32);
+  d.scale = v.w;
+  d.cl = ce ? ce[threadIdx.x & 63] : 0.0;
 #pragma unroll
   for (int j = 0; j < TCHAIN_NUMAX; ++j) d.u[j] = j < nu ? uk[j + z] : 0.0;
 }
@@ -105,10 +115,93 @@ __global__ void k_tchain_prep(int nu, long long units, const double* __restrict_
     int P = 1;
     while (P < TCHAIN_PMAX && prm.theta[P] < beta) ++P;
     const double er = exp(mr);
-    steps[e] = TStep{er * cos(mi), er * sin(mi), P, s, 0.0};
+    steps[e] = TStep{er * cos(mi), er * sin(mi), P, s, 1.0 / s};
     cnt += (unsigned long long)(P * s);
   }
   // one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(terms, cnt);
+}
+
+// Chebyshev variant (skew-Hermitian generators, Ã_k = -i H̃_k with spectrum within [-ρ, ρ], ρ = β_k):
+//   exp(Ã) v = J_0(ρ) y_0 + 2 Σ_{t>=1} J_t(ρ) y_t,  y_0 = v, y_1 = Â v / 2, y_{t+1} = Â y_t + y_{t-1},  Â = (2/ρ) Ã
+// (the Jacobi-Anger expansion of e^{-iρx} with y_t = (-i)^t T_t(H̃/ρ) v: real coefficients, |y_t| <= |v|, so no
+// cancellation and no substeps up to ρ ~ 40); P = the smallest with 2 Σ_{t>P} |J_t(ρ)| <= 2^-53.
+__device__ void bessel_j(double rho, int K, double* j) {  // J_0..J_K(ρ)
+  if (rho <= 2.0) {  // power series (no cancellation for ρ <= 2); stops once J_k < 1e-40 (k > ρ: decreasing)
+    const double h = 0.5 * rho, h2 = -h * h;
+    double lead = 1.0;  // (ρ/2)^k / k!
+    for (int k = 0; k <= K; ++k) {
+      if (k) lead *= h / k;
+      if (lead < 1e-40) {
+        for (int q = k; q <= K; ++q) j[q] = 0.0;
+        return;
+      }
+      double term = lead, sum = lead;
+      for (int m = 1; m < 40 && fabs(term) > 1e-22 * fabs(sum); ++m) {
+        term *= h2 / (m * (double)(m + k));
+        sum += term;
+      }
+      j[k] = sum;
+    }
+    return;
+  }
+  // Miller's backward recurrence, normalised by J_0 + 2 Σ J_2k = 1
+  int K0 = (int)(rho + 4.0 * cbrt(rho)) + 30;  // J_k negligible beyond ρ + O(ρ^(1/3))
+  for (int q = K0; q <= K; ++q) j[q] = 0.0;
+  K0 += K0 & 1;
+  double jp = 0.0, jc = 1e-280, norm = 0.0;
+  for (int k = K0; k >= 1; --k) {
+    const double jm = (2.0 * k / rho) * jc - jp;
+    jp = jc;
+    jc = jm;  // J_{k-1} (unnormalised)
+    if (k - 1 <= K) j[k - 1] = jc;
+    if (((k - 1) & 1) == 0) norm += (k - 1 ? 2.0 : 1.0) * jc;
+    if (fabs(jc) > 1e250) {  // rescale to stay finite
+      jc *= 1e-250;
+      jp *= 1e-250;
+      norm *= 1e-250;
+      for (int q = k - 1; q <= K && q <= K0; ++q) j[q] *= 1e-250;
+    }
+  }
+  for (int k = 0; k <= K; ++k) j[k] /= norm;
+}
+
+__global__ void k_tchain_prep_cheb(int nu, long long units, const double* __restrict__ u, const TChainParams prm,
+                                   TStep* __restrict__ steps, double* __restrict__ coef,
+                                   unsigned long long* __restrict__ terms) {
+  unsigned long long cnt = 0;
+  const double tol = 1.1102230246251565e-16;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < units; e += (long long)gridDim.x * blockDim.x) {
+    double beta = prm.nrm[0], mr = prm.mur[0], mi = prm.mui[0];
+    for (int j = 0; j < nu; ++j) {
+      const double uj = u[e * nu + j];
+      beta += fabs(uj) * prm.nrm[j + 1];
+      mr += uj * prm.mur[j + 1];
+      mi += uj * prm.mui[j + 1];
+    }
+    beta = fmax(beta, 1e-300);
+    int s = 1;
+    if (beta > 25.0) s = (int)ceil(beta / 25.0);  // substeps only beyond ρ = 25 (P <= 58 < TCHEB_PMAX)
+    const double rho = beta / s;
+    double j[TCHEB_PMAX + 2];
+    bessel_j(rho, TCHEB_PMAX + 1, j);
+    double tail = 0.0;
+    int P = 0;
+    for (int k = TCHEB_PMAX + 1; k >= 1; --k) {  // smallest P with 2 Σ_{t>P} |J_t| <= tol
+      tail += 2.0 * fabs(j[k]);                 // Σ_{t>=k}
+      if (tail > tol) {
+        P = k < TCHEB_PMAX ? k : TCHEB_PMAX;
+        break;
+      }
+    }
+    double* ce = coef + (size_t)e * TCHEB_STRIDE;
+    ce[0] = j[0];
+    for (int k = 1; k <= P; ++k) ce[k] = 2.0 * j[k];
+    const double er = exp(mr);
+    steps[e] = TStep{er * cos(mi), er * sin(mi), P, s, 2.0 / beta};
+    cnt += (unsigned long long)(P * s);
+  }
   for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
   if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(terms, cnt);
 }
@@ -130,6 +223,7 @@ struct TChainArgs {
   double* J;               // B
   cx<double>* coef;        // B x m
   const void* src;         // B x (Nt+1) x N x m caller's dL/dx(x_k) added to λ_k (nullptr: none)
+  const double* tcoef;     // B x Nt x TCHEB_STRIDE Chebyshev coefficients (Chebyshev variant)
 };
 
 // Thread layout of the Taylor-action chains.  Waves split the rows into G blocks of R = 64 / S rows and the
@@ -371,7 +465,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_fwd(const TChainArgs g
     if (k + 1 < Nt) tpre_load(stb + k + 1, ub + (size_t)(k + 1) * nu, nu, nx);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     cx<T> a[JT];
-    rg.form(N, nu, gen, st.u, ns > 1 ? (T)(1.0 / ns) : T(1), a);
+    rg.form(N, nu, gen, st.u, (T)st.scale, a);
     rg.step(N, m, a, yb, XB, cur, P, ns, cx<double>{st.pr, st.pi}, acc);
     store(acc, k + 1);
   }
@@ -468,7 +562,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_bwd(const TChainArgs g
         xk[ps][bb] = v;
       }
     cx<T> a[JT];
-    rg.form(N, nu, gen, st.u, ns > 1 ? (T)(1.0 / ns) : T(1), a);
+    rg.form(N, nu, gen, st.u, (T)st.scale, a);
     rg.step(N, m, a, yb, XB, cur, P, ns, cx<double>{st.pr, -st.pi}, acc);
     cx<T>* Lk = Lb + (size_t)k * Nm;
     bool any_pen = false;
@@ -509,7 +603,8 @@ __host__ __device__ inline int tchain_mf_kq(int N) {  // k-quads per product, bu
 __host__ __device__ inline int tchain_mf_waves(int N, int m) { return ((N + 15) / 16) * ((m + 1) / 2); }
 __host__ inline size_t tchain_mf_lds(int N, int m, int nu) {
   const int KQ = tchain_mf_kq(N), CP = (m + 1) / 2;
-  return (size_t)(nu + 1) * N * N * 16 + (size_t)2 * 2 * CP * 4 * KQ * 4 * 8 + 64 * 8;
+  // generators, 2 x (y, y') state buffers, then 16 reduction doubles + 48 for 1/t + 64 per wave (coefficients)
+  return (size_t)(nu + 1) * N * N * 16 + (size_t)2 * 2 * CP * 4 * KQ * 4 * 8 + (64 + 64 * tchain_mf_waves(N, m)) * 8;
 }
 
 template <int KQ>
@@ -615,17 +710,37 @@ struct TChainMF {
     }
   }
 
-  // One slice (see TChain::step); acc = this lane's D element of the state.
+  // One slice (see TChain::step); acc = this lane's D element of the state.  CHEB: the Chebyshev recurrence
+  // with this lane's coefficient register cl (lane t holds c_t); else Taylor (1/t from the LDS table invt).
+  template <bool CHEB>
   __device__ __forceinline__ void step(int N, const double (&ar)[KQ], const double (&ai)[KQ], double* yb,
                                        const double* __restrict__ invt, int& cur, int P, int s, cx<double> ph,
-                                       double& acc) const {
+                                       double& acc, double cl, double* __restrict__ cw) const {
+    if constexpr (CHEB) {  // this step's coefficients -> the wave's own LDS slot (in-order LDS: no barrier)
+      cw[threadIdx.x & 63] = cl;
+      __builtin_amdgcn_wave_barrier();
+    }
     for (int sub = 0; sub < s; ++sub) {
-      acc = actD ? ybuf(yb, CP, cur, 0)[(cp * RP + rowD) * 4 + n] : 0.0;
+      const double y0 = actD ? ybuf(yb, CP, cur, 0)[(cp * RP + rowD) * 4 + n] : 0.0;
+      double ym1 = y0, ym2 = 0.0;  // y_{t-1}, y_{t-2} (Chebyshev)
+      acc = CHEB ? cw[0] * y0 : y0;
       for (int t = 1; t <= P; ++t) {
         TC_T(t0);
-        const double inv = invt[t];  // 1/t from LDS (an fp64 division is ~12 dependent VALU ops)
-        const double z = matvec(ar, ai, ybuf(yb, CP, cur, 0), ybuf(yb, CP, cur, 1)) * inv;
-        acc += z;
+        // the term's coefficient (1/t or c_t) read first: left to the scheduler it is issued after the last MFMA
+        // and its LDS latency lands in front of the state write and the barrier
+        const double ct = CHEB ? cw[t] : invt[t];
+        __builtin_amdgcn_sched_barrier(0);
+        const double D = matvec(ar, ai, ybuf(yb, CP, cur, 0), ybuf(yb, CP, cur, 1));
+        double z;
+        if constexpr (CHEB) {
+          z = t == 1 ? 0.5 * D : D + ym2;
+          ym2 = ym1;
+          ym1 = z;
+          acc += ct * z;
+        } else {
+          z = D * ct;  // 1/t from LDS (an fp64 division is ~12 dependent VALU ops)
+          acc += z;
+        }
         TC_T(t1);
         if (t < P) {
           if (actD) put(ybuf(yb, CP, cur ^ 1, 0), ybuf(yb, CP, cur ^ 1, 1), z);
@@ -650,7 +765,7 @@ struct TChainMF {
   }
 };
 
-template <int KQ>
+template <int KQ, bool CHEB>
 __global__ __launch_bounds__(1024) void k_tchain_mf_fwd(const TChainArgs g) {
   using C = TChainMF<KQ>;
   constexpr int RP = C::RP;
@@ -661,6 +776,7 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_fwd(const TChainArgs g) {
   double* yb = reinterpret_cast<double*>(gen + (size_t)(nu + 1) * NN);
   double* red = yb + (size_t)2 * 2 * CP * RP * 4;
   double* invt = red + 16;
+  double* cw = invt + 48 + 64 * (tid >> 6);  // per-wave Chebyshev coefficient slot
   const cx<double>* At = (const cx<double>*)g.At;
   const cx<double>* x0b = (const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0);
   for (int e = tid; e <= TCHAIN_PMAX; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
@@ -696,15 +812,16 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_fwd(const TChainArgs g) {
   const unsigned long long c0_ = __builtin_amdgcn_s_memtime(), r0_ = __builtin_amdgcn_s_memrealtime();
 #endif
   int cur = 0;
+  const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
   TPre nx;
-  tpre_load(stb, ub, nu, nx);
+  tpre_load(stb, ub, nu, nx, ceb);
   for (int k = 0; k < Nt; ++k) {
     const TPre st = nx;
-    if (k + 1 < Nt) tpre_load(stb + k + 1, ub + (size_t)(k + 1) * nu, nu, nx);
+    if (k + 1 < Nt) tpre_load(stb + k + 1, ub + (size_t)(k + 1) * nu, nu, nx, CHEB ? ceb + (size_t)(k + 1) * TCHEB_STRIDE : nullptr);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     double ar[KQ], ai[KQ];
-    rg.form(N, nu, gen, st.u, ns > 1 ? 1.0 / ns : 1.0, ar, ai);
-    rg.step(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, st.pi}, acc);
+    rg.form(N, nu, gen, st.u, st.scale, ar, ai);
+    rg.template step<CHEB>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, st.pi}, acc, st.cl, cw);
     store(acc, k + 1);
   }
   __syncthreads();
@@ -723,7 +840,7 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_fwd(const TChainArgs g) {
                       g.cost_kind, g.n_norm, block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * m);
 }
 
-template <int KQ>
+template <int KQ, bool CHEB>
 __global__ __launch_bounds__(1024) void k_tchain_mf_bwd(const TChainArgs g) {
   using C = TChainMF<KQ>;
   constexpr int RP = C::RP;
@@ -733,6 +850,7 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_bwd(const TChainArgs g) {
   cx<double>* gen = reinterpret_cast<cx<double>*>(smem);
   double* yb = reinterpret_cast<double*>(gen + (size_t)(nu + 1) * NN);
   double* invt = yb + (size_t)2 * 2 * CP * RP * 4 + 16;
+  double* cw = invt + 48 + 64 * (tid >> 6);  // per-wave Chebyshev coefficient slot
   for (int e = tid; e <= TCHAIN_PMAX; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
   const cx<double>* At = (const cx<double>*)g.At;
   const cx<double>* Xb = (const cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm;
@@ -782,18 +900,19 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_bwd(const TChainArgs g) {
   __syncthreads();
   int cur = 0;
   double acc = 0.0;
+  const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
   TPre nx;
-  tpre_load(stb + Nt - 1, ub + (size_t)(Nt - 1) * nu, nu, nx);
+  tpre_load(stb + Nt - 1, ub + (size_t)(Nt - 1) * nu, nu, nx, CHEB ? ceb + (size_t)(Nt - 1) * TCHEB_STRIDE : nullptr);
   for (int k = Nt - 1; k >= 0; --k) {
     const TPre st = nx;
-    if (k > 0) tpre_load(stb + k - 1, ub + (size_t)(k - 1) * nu, nu, nx);
+    if (k > 0) tpre_load(stb + k - 1, ub + (size_t)(k - 1) * nu, nu, nx, CHEB ? ceb + (size_t)(k - 1) * TCHEB_STRIDE : nullptr);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     const size_t ok_ = (size_t)k * Nm + rg.rowD + N * rg.colD;
     double xk = pen_m ? tmu * reinterpret_cast<const double*>(Xb + ok_)[rg.n & 1] : 0.0;
     if (srcb && rg.actD) xk += reinterpret_cast<const double*>(srcb + ok_)[rg.n & 1];
     double ar[KQ], ai[KQ];
-    rg.form(N, nu, gen, st.u, ns > 1 ? 1.0 / ns : 1.0, ar, ai);
-    rg.step(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, -st.pi}, acc);
+    rg.form(N, nu, gen, st.u, st.scale, ar, ai);
+    rg.template step<CHEB>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, -st.pi}, acc, st.cl, cw);
     if (pen_m || (srcb && rg.actD)) {
       acc += xk;
       rg.put(C::ybuf(yb, rg.CP, cur, 0), C::ybuf(yb, rg.CP, cur, 1), acc);

@@ -281,7 +281,8 @@ class GrapeEngine:
         self._chk(self._lib.qoc_get_info(self._h, v.ctypes.data_as(C.POINTER(C.c_longlong))))
         return {"path": "large_n" if v[0] else "lds", "chunk": int(v[1]), "ns_iters": int(v[2]),
                 "device_bytes": int(v[3]), "chain": "taylor" if v[4] == 1 else "propagators",
-                "expm": {0: "pade", 1: "taylor_rr", 2: "ps_lds"}.get(int(v[5]), "?")}
+                "expm": {0: "pade", 1: "taylor_rr", 2: "ps_lds"}.get(int(v[5]), "?"),
+                "chain_poly": "chebyshev" if v[6] else "taylor"}
 
     def set_chain(self, mode: str = "auto"):
         """How the chains apply exp(A_k) (include/qoc.h qoc_set_chain): 'propagators' forms every U_k (the

@@ -534,3 +534,49 @@ def test_arbitrary_dL_dx_closure(built_lib, monkeypatch, path):
     g0 = Q.grape_sensitivity(prob.A0, prob.A, dJf, cache.u, prob.x0, cache, dUkdp_order=3)
     gr0 = O.grape_sensitivity(prob.A0, prob.A, dJf, c2.u, prob.x0, c2, dUkdp_order=3)
     assert np.linalg.norm(g0 - gr0) / np.linalg.norm(gr0) < 1e-10
+
+
+@pytest.mark.parametrize("poly", ["chebyshev", "taylor"])
+@pytest.mark.parametrize("which", ["cavity40", "synthetic_large_norm"])
+def test_taylor_action_polynomials(built_lib, monkeypatch, poly, which):
+    """The Taylor-action chains' two polynomials: Chebyshev (default for skew-Hermitian generators; ||A||_1 up to
+    ~4 here without substeps) and Taylor (QOC_TCHAIN_POLY=taylor; substeps at large norms), both vs the oracle."""
+    import dataclasses
+    from qoc_amd import systems
+    if poly == "taylor":
+        monkeypatch.setenv("QOC_TCHAIN_POLY", "taylor")
+    if which == "cavity40":
+        prob = systems.cavity_problem(N_cavity=20, Nt=30)
+        u = systems.cavity_controls(2, prob.Nt, seed=41)
+    else:
+        p0 = systems.synthetic_problem(N=33, nu=2, Nt=9, seed=4, precision="fp64")
+        prob = dataclasses.replace(p0, x0=p0.x0[:, :3].copy(), x_target=p0.x_target[:, :3].copy(), n=3.0)
+        u = systems.synthetic_controls(2, prob.Nt, nu=2, seed=4)
+    e = _engine(prob, 2, chain="taylor")
+    assert e.info()["chain_poly"] == poly
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    e.close()
+    for b in range(2):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        assert abs(J[b] - Jr) <= 1e-12
+        assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
+
+
+def test_taylor_action_non_skew_hermitian_generators(built_lib):
+    """Damped generators (A0 = -i H dt - gamma I, not skew-Hermitian): the Taylor polynomial runs (Chebyshev
+    needs a spectrum on the imaginary axis), states no longer unitary; against the oracle."""
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=10, Nt=20)
+    import dataclasses
+    prob = dataclasses.replace(prob, A0=prob.A0 - 0.01 * np.eye(prob.N))
+    u = systems.cavity_controls(2, prob.Nt, seed=42)
+    e = _engine(prob, 2, chain="taylor")
+    assert e.info()["chain_poly"] == "taylor"
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    e.close()
+    for b in range(2):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        assert abs(J[b] - Jr) <= 1e-12
+        assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10

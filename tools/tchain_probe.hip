@@ -14,7 +14,7 @@ void run(int N, int m, int Nt, int B, int P) {
   std::vector<cx<double>> A((nu + 1) * NN);
   for (size_t e = 0; e < A.size(); ++e) A[e] = {((e * 7919) % 97) / (97.0 * N) - 0.5 / N, ((e * 104729) % 89) / (89.0 * N) - 0.5 / N};
   std::vector<double> u((size_t)B * Nt * nu, 0.01);
-  std::vector<TStep> st((size_t)B * Nt, TStep{1.0, 0.0, P, 1, 0.0});
+  std::vector<TStep> st((size_t)B * Nt, TStep{1.0, 0.0, P, 1, 1.0});
   std::vector<cx<double>> x0((size_t)N * m, cx<double>{1.0 / N, 0});
   cx<double>*dA, *dx0, *dX, *dcoef;
   double *dJ, *du;
@@ -68,7 +68,7 @@ void run_mf(int N, int m, int Nt, int B, int P) {
   std::vector<cx<double>> A((nu + 1) * NN);
   for (size_t e = 0; e < A.size(); ++e) A[e] = {((e * 7919) % 97) / (97.0 * N) - 0.5 / N, ((e * 104729) % 89) / (89.0 * N) - 0.5 / N};
   std::vector<double> u((size_t)B * Nt * nu, 0.01);
-  std::vector<TStep> st((size_t)B * Nt, TStep{1.0, 0.0, P, 1, 0.0});
+  std::vector<TStep> st((size_t)B * Nt, TStep{1.0, 0.0, P, 1, 1.0});
   std::vector<cx<double>> x0((size_t)N * m, cx<double>{1.0 / N, 0});
   cx<double>*dA, *dx0, *dX, *dcoef;
   double *dJ, *du;
@@ -88,7 +88,7 @@ void run_mf(int N, int m, int Nt, int B, int P) {
   g.N = N; g.m = m; g.nu = nu; g.Nt = Nt; g.At = dA; g.u = du; g.steps = dst; g.x0 = dx0; g.X = dX; g.L = dX;
   g.Xt = dx0; g.cost_kind = 2; g.n_norm = 1.0; g.J = dJ; g.coef = (cx<double>*)dcoef;
   const size_t lds = tchain_mf_lds(N, m, nu);
-  (void)hipFuncSetAttribute((const void*)k_tchain_mf_fwd<KQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  (void)hipFuncSetAttribute((const void*)k_tchain_mf_fwd<KQ, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
@@ -99,7 +99,7 @@ void run_mf(int N, int m, int Nt, int B, int P) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tc), z, sizeof(z));
 #endif
     (void)hipEventRecord(a);
-    hipLaunchKernelGGL((k_tchain_mf_fwd<KQ>), dim3(B), dim3(64 * tchain_mf_waves(N, m)), lds, 0, g);
+    hipLaunchKernelGGL((k_tchain_mf_fwd<KQ, false>), dim3(B), dim3(64 * tchain_mf_waves(N, m)), lds, 0, g);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     (void)hipEventElapsedTime(&ms, a, b);
