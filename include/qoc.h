@@ -52,6 +52,9 @@ typedef struct qoc_ctx qoc_ctx;
 int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, int precision);
 void qoc_destroy(qoc_ctx* ctx);
 const char* qoc_last_error(const qoc_ctx* ctx);
+/* sha256 of the sources (csrc/ and include/qoc.h) this library was compiled from ("unknown" when built
+ * without the hash); the bindings refuse a library whose hash differs from the sources beside it. */
+const char* qoc_source_hash(void);
 void* qoc_stream(qoc_ctx* ctx);                 /* hipStream_t the engine launches on */
 int qoc_synchronize(qoc_ctx* ctx);
 

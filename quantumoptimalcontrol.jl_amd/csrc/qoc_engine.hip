@@ -1438,9 +1438,15 @@ int check_ready(qoc_ctx* c) {
 
 }  // namespace
 
+#ifndef QOC_SOURCE_HASH
+#define QOC_SOURCE_HASH "unknown"
+#endif
+
 extern "C" {
 
 const char* qoc_last_error(const qoc_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+const char* qoc_source_hash(void) { return QOC_SOURCE_HASH; }
 
 int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, int precision) {
   if (!out) return fail(nullptr, QOC_ERR_ARG, "out is null");

@@ -37,6 +37,7 @@ SIGNATURES = {
     "qoc_create": (C.c_int, [C.POINTER(_vp), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
     "qoc_destroy": (None, [_vp]),
     "qoc_last_error": (C.c_char_p, [_vp]),
+    "qoc_source_hash": (C.c_char_p, []),
     "qoc_stream": (_vp, [_vp]),
     "qoc_synchronize": (C.c_int, [_vp]),
     "qoc_set_generators": (C.c_int, [_vp, _dp, C.POINTER(_dp)]),
@@ -100,6 +101,13 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if not os.environ.get("QOC_LIB_PATH"):  # variant builds for A/B runs carry no hash
+        from ._srchash import source_hash
+        want = source_hash()
+        have = lib.qoc_source_hash().decode().removeprefix("qoc-src-")
+        if want is not None and have != want:
+            raise QOCError(QOC_ERR_STATE, f"{LIB_PATH} was built from other sources (hash {have[:12]}, tree "
+                                          f"{want[:12]}); run __graft_entry__.build()")
     _lib = lib
     return lib
 

@@ -26,6 +26,26 @@ def test_library_builds_loads_and_exports_every_declared_symbol(built_lib):
     assert set(_lib.SIGNATURES) == set(syms)
 
 
+def test_library_is_built_from_the_sources_in_the_tree(built_lib, tmp_path, monkeypatch):
+    """The library carries the sha256 of csrc/ + include/qoc.h; load() refuses one built from other sources."""
+    from qoc_amd import _lib, _srchash
+    assert built_lib.qoc_source_hash().decode() == "qoc-src-" + _srchash.source_hash()
+    # a tree whose sources differ by one byte no longer matches the library
+    src = tmp_path / "pkg" / "csrc"
+    src.mkdir(parents=True)
+    for f in _srchash.source_files()[:-1]:
+        (src / os.path.basename(f)).write_bytes(open(f, "rb").read())
+    hdr = tmp_path / "include"
+    hdr.mkdir()
+    (hdr / "qoc.h").write_bytes(open(_srchash.HEADER, "rb").read() + b"\n")
+    monkeypatch.setattr(_srchash, "CSRC", str(src))
+    monkeypatch.setattr(_srchash, "HEADER", str(hdr / "qoc.h"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.QOCError, match="built from other sources"):
+        _lib.load()
+    monkeypatch.setattr(_lib, "_lib", built_lib)
+
+
 def test_last_error_without_context(built_lib):
     msg = built_lib.qoc_last_error(None)
     assert isinstance(msg, bytes)
