@@ -432,8 +432,11 @@ def main():
             "kernels": kern,
             "pade_hist_per_step": {f"d{d}s{s}": v / K for (d, s), v in sorted(hist.items())},
             "taylor_hist_per_step": {f"m{mm}s{s}": v / K for (mm, s), v in sorted(thist.items())},
-            "ref_equiv_gflop_per_eval": ref_f / 1e9,
-            "ref_equiv_tflops": ref_f * value / 1e12,
+            # the reference algorithm's flops per eval (SURVEY §8d F_eval, Padé (d, s) counted on the device)
+            # times this engine's eval rate: a reference-equivalent RATE, not a utilisation figure (the engine
+            # executes far fewer flops than that formula; see "roofline" for the executed work)
+            "reference_equivalent": {"gflop_per_eval": ref_f / 1e9, "rate_tflops": ref_f * value / 1e12,
+                                     "note": "reference-algorithm flops x eval rate; not executed work, may exceed peak"},
             "parity_vs_cpu_port": parity,
             "engine": info1,
             "best_over_ranks": {"J": best[0], "seed": int(best[1]), "transport": transport} if best else None,

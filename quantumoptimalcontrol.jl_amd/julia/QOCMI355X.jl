@@ -214,8 +214,9 @@ With the tagged costs of this module (setup_infidelity / setup_infidelity_zcalib
 (setup_state_penalty, or the reference's disabled Returns(0) pair) the spline map, the propagation, the cost
 and the sensitivity run in one `qoc_eval_spline` call on the device.  Any other cost closure is evaluated on
 the host at x[end] and handed over as λ_{Nt+1} (QOC_COST_EXTERNAL), exactly as the reference's f / f_grad do;
-a dL_dx the device cannot apply raises an error instead of being dropped.  g / g_jac are the reference's
-norm constraints.  Returns the same tuple.
+any other penalty pair is evaluated on the host too: sum(L, x) in f, and dL_dx(x[k]) for every slice added to
+the co-states on the device (qoc_set_costate_source).  g / g_jac are the reference's norm constraints.
+Returns the same tuple.
 """
 function setup_ipopt_callbacks(A0Δt, A1Δt, A2Δt, x0, u_prototype, (Jfinal, dJfinal_dx), (L, dL_dx), B;
                                x_target=nothing, n=nothing)
