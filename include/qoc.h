@@ -63,7 +63,7 @@ int qoc_set_generators(qoc_ctx* ctx, const double* A0, const double* const* Aj);
 /* x0 (N x m) shared by all seeds (per_seed = 0) or B x N x m (per_seed = 1) — propagate :14. */
 int qoc_set_x0(qoc_ctx* ctx, const double* x0, int per_seed);
 /* Terminal cost: kind QOC_COST_TRACE (X_target N x m, normalisation n),
- * QOC_COST_ZCAL (m must be 4), QOC_COST_EXTERNAL (X_target may be NULL). */
+ * QOC_COST_ZCAL (m must be 4; every propagation path), QOC_COST_EXTERNAL (X_target may be NULL). */
 int qoc_set_cost(qoc_ctx* ctx, int kind, const double* X_target, double n);
 /* Guard-state penalty L = mu sum |x[P,C]|^2 (src/penalty_fcns.jl:1-11); 0-based indices; mu = 0 disables. */
 int qoc_set_state_penalty(qoc_ctx* ctx, const int* P, int np, const int* C, int nc, double mu);
@@ -85,6 +85,18 @@ int qoc_grape_sensitivity(qoc_ctx* ctx, const double* u, int dUkdp_order,
  * with NULL.  The host evaluates the closure on the states (qoc_get_states); J's sum(L, x) stays with the
  * caller.  Not on the Tsit5 path (compute_pwc_gradient has no dL_dx). */
 int qoc_set_costate_source(qoc_ctx* ctx, const double* dLdx);
+
+/* compress_states / decompress_states (src/utils.jl:96-109) inside the engine.  When the generators keep the
+ * two row blocks rows1 / rows2 (a partition of the N rows) apart, and the state's columns cols1 live only on
+ * rows1 and cols2 only on rows2 (a partition of the m columns), the engine packs both blocks into
+ * max(nc1, nc2) columns: the chains and the gradient run on the packed states, and every host-side state
+ * argument (x0, X_target, lambda_final, dLdx, penalty columns) and result (qoc_get_states / costates) keeps the
+ * caller's N x m layout.  J and dJdu equal the unpacked problem's.  0-based indices; nr1 = nr2 = 0 turns packing
+ * off.  Errors: QOC_ERR_ARG when the index lists do not partition rows / columns, the generators couple the blocks,
+ * or x0 has an entry outside its block.  Re-packs an x0 / target / penalty already set; a co-state source must be
+ * set again.  Co-states come back projected on the blocks (the rest never reaches the gradient). */
+int qoc_set_compression(qoc_ctx* ctx, const int* rows1, int nr1, const int* cols1, int nc1, const int* rows2,
+                        int nr2, const int* cols2, int nc2);
 
 /* Device-pointer variants (inputs already resident in HBM, asynchronous on qoc_stream). */
 int qoc_propagate_dev(qoc_ctx* ctx, const double* d_u, double* d_J);
@@ -161,7 +173,7 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
  * info[3] = device bytes allocated by the context, info[4] = chain mode (QOC_CHAIN_PROPAGATORS /
  * QOC_CHAIN_TAYLOR), info[5] = exponential the propagators run (0 the reference's Padé + solve, 1 register-
  * resident Taylor / Paterson-Stockmeyer, 2 LDS Paterson-Stockmeyer), info[6] = 1 when the Taylor-action chains
- * use Chebyshev terms (skew-Hermitian generators, fp64; QOC_TCHAIN_POLY=taylor keeps Taylor), info[7] reserved.  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
+ * use Chebyshev terms (skew-Hermitian generators, fp64; QOC_TCHAIN_POLY=taylor keeps Taylor), info[7] = state columns the kernels run on (m, or max(nc1, nc2) with qoc_set_compression).  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
  * selects the large-N path for any size (testing). */
 int qoc_get_info(qoc_ctx* ctx, long long* info /*[8]*/);
 

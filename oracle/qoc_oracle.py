@@ -431,14 +431,15 @@ def infidelity(U_target, Uf, calibration="lms_phase"):
 # ---------------------------------------------------------------------------
 # Batched convenience used by the parity tests and bench cpu_baseline
 # ---------------------------------------------------------------------------
-def grape_eval(A0, A, u, x0, x_target, n=None, order=3, penalty=None):
+def grape_eval(A0, A, u, x0, x_target, n=None, order=3, penalty=None, cost=None):
     """One GRAPE gradient eval = propagate + J + grape_sensitivity.
 
     Mirrors the Ipopt callbacks f / f_grad (examples/ipopt_callbacks_exp.jl:11-31)
-    without the spline map.  ``penalty`` = (P, C, mu) enables the state penalty.
+    without the spline map.  ``penalty`` = (P, C, mu) enables the state penalty; ``cost`` = (Jfinal,
+    dJfinal_dx) replaces the trace infidelity of x_target (e.g. setup_infidelity_zcalibrated).
     Returns (J, dJdu, cache).
     """
-    Jf, dJf = setup_infidelity(x_target, n)
+    Jf, dJf = cost if cost is not None else setup_infidelity(x_target, n)
     L = dL = None
     if penalty is not None:
         L, dL = setup_state_penalty(*penalty)
@@ -601,14 +602,15 @@ def propagate_pwc_ode(A0, A, u, x0, nsub=10):
     return xs
 
 
-def grape_eval_ode(A0, A, u, x0, x_target, n=None, order=3, nsub=10, penalty=None):
+def grape_eval_ode(A0, A, u, x0, x_target, n=None, order=3, nsub=10, penalty=None, cost=None):
     """compute_pwc_gradient (src/gradient_computations.jl:130-169) with the exp path's conventions:
     states x_k from propagate_pwc_ode, co-states by the backward adjoint ODE dλ/dτ = -A_k^H λ (fixed
     Tsit5, nsub steps per slice, + dL/dx at slice boundaries as in the exp path), and
-    dJdu[j, k] = _compute_u_sensitivity(x_k, λ_{k+1}, expm_jacobian(A_k)[j]).  Returns (J, dJdu)."""
+    dJdu[j, k] = _compute_u_sensitivity(x_k, λ_{k+1}, expm_jacobian(A_k)[j]).  ``cost`` as in grape_eval.
+    Returns (J, dJdu)."""
     u = np.asarray(u, dtype=np.float64)
     Nt = u.shape[1]
-    Jf, dJf = setup_infidelity(x_target, n)
+    Jf, dJf = cost if cost is not None else setup_infidelity(x_target, n)
     L = dL = None
     if penalty is not None:
         L, dL = setup_state_penalty(*penalty)

@@ -469,46 +469,6 @@ __global__ __launch_bounds__(256) void k_form_norm(int N, int nu, long long unit
   if (lane == 0 && nmax) atomicMax(nmax, (unsigned long long)__double_as_longlong(best));
 }
 
-// λ_N = coef_b * Xt (trace cost) written to Lam[b][Nt] for all seeds.
-template <typename T>
-__global__ void k_lambda_final(int N, int m, int Nt, int B, const cx<T>* __restrict__ Xt,
-                               const cx<double>* __restrict__ coef, cx<T>* __restrict__ Lam) {
-  const size_t Nm = (size_t)N * m;
-  for (size_t gi = blockIdx.x * (size_t)blockDim.x + threadIdx.x; gi < Nm * B; gi += (size_t)gridDim.x * blockDim.x) {
-    const int b = (int)(gi / Nm);
-    const size_t o = gi - (size_t)b * Nm;
-    const cx<double> cf = coef[(size_t)b * m + o / N];
-    const cx<T> t = Xt[o];
-    Lam[((size_t)b * (Nt + 1) + Nt) * Nm + o] =
-        cx<T>{(T)(cf.r * t.r - cf.i * t.i), (T)(cf.r * t.i + cf.i * t.r)};
-  }
-}
-
-// Trace cost on x_N for every seed (one workgroup per seed): J = 1 - |tr(Xt' x_N)|^2 / n^2, added to
-// J[b] when accumulate != 0 (penalty already stored there); coef = -2 tr(Xt' x_N) / n^2 per column.
-template <typename T>
-__global__ void k_trace_cost(int N, int m, int Nt, const cx<T>* __restrict__ X, const cx<T>* __restrict__ Xt,
-                             double n_norm, int accumulate, double* __restrict__ J, cx<double>* __restrict__ coef) {
-  __shared__ double red[8];
-  const int b = blockIdx.x;
-  const size_t Nm = (size_t)N * m;
-  const cx<T>* xN = X + ((size_t)b * (Nt + 1) + Nt) * Nm;
-  double orr = 0, oii = 0;
-  for (size_t o = threadIdx.x; o < Nm; o += blockDim.x) {
-    const cx<T> t = Xt[o], v = xN[o];
-    orr += (double)t.r * v.r + (double)t.i * v.i;
-    oii += (double)t.r * v.i - (double)t.i * v.r;
-  }
-  orr = block_sum(orr, red);
-  oii = block_sum(oii, red);
-  if (threadIdx.x == 0) {
-    const double n2 = n_norm * n_norm;
-    const double j = 1.0 - (orr * orr + oii * oii) / n2;
-    J[b] = accumulate ? J[b] + j : j;
-    for (int c = 0; c < m; ++c) coef[(size_t)b * m + c] = cx<double>{-2.0 * orr / n2, -2.0 * oii / n2};
-  }
-}
-
 // Guard-state penalty over all stored states: J[b] = mu * sum_{k, masked} |x_k|^2 (one WG per seed).
 template <typename T>
 __global__ void k_penalty_sum(int N, int m, int Nt, const cx<T>* __restrict__ X, const unsigned char* __restrict__ pmask,

@@ -153,13 +153,31 @@ __device__ __forceinline__ double swap_sum(double v) {
          __longlong_as_double((long long)(((unsigned long long)ohi << 32) | olo));
 }
 
+// Row sectors of a packed state (compress_states, src/utils.jl:96-109): the engine's m columns hold two
+// parity sectors, rows with rsec[r] = 0 carrying the original columns cols1 and rows with rsec[r] = 1 the
+// columns cols2.  zmap[c] = s m + i: original column c of a two-qubit target (z-calibrated cost) lives in packed
+// column i on the rows of sector s.  rsec == nullptr: no packing (one sector).
+struct Sectors {
+  const unsigned char* rsec = nullptr;
+  int zmap[4] = {0, 1, 2, 3};
+};
+__device__ __forceinline__ int sector_of(const Sectors& sc, int row) { return sc.rsec ? sc.rsec[row] : 0; }
+
+// λ_N coefficient of element (row, col): coefficients are stored per seed as 2 m entries, [sector][column].
+__device__ __forceinline__ cx<double> lam_coef(const cx<double>* coef_b, const Sectors& sc, int m, int row, int col) {
+  return coef_b[sector_of(sc, row) * m + col];
+}
+
 // Terminal cost J and the coefficients of λ_N = dJ/dx (src/penalty_fcns.jl:15-42, src/fidelities.jl:48-56,81-137)
 // from x_N (xN(o), o = row + N col, any layout) for one seed; psum = μ Σ_k Σ_{P,C} |x_k|² of this seed (already
 // reduced).  Called by every thread of the workgroup (block reductions).  COST_EXTERNAL: J = psum, coef = 0.
+// coef: 2 m entries per seed ([sector][column], see lam_coef).  Packed states (sc.rsec): the trace over the
+// packed columns equals the original trace (the entries outside the two sectors are zero); the z-calibrated
+// overlaps m_c = <Xt_c, x_c> of the four original columns are sums over one sector's rows of a packed column.
 template <typename T, typename XN>
 __device__ __forceinline__ void chain_costs(int N, int m, const cx<T>* __restrict__ Xt, XN&& xN, int cost_kind,
                                             double n_norm, double psum, double* red, double* Jout,
-                                            cx<double>* __restrict__ coef) {
+                                            cx<double>* __restrict__ coef, const Sectors& sc = Sectors()) {
   const int tid = threadIdx.x, nthr = blockDim.x, Nm = N * m;
   if (cost_kind == COST_TRACE) {
     double orr = 0, oii = 0;
@@ -173,14 +191,16 @@ __device__ __forceinline__ void chain_costs(int N, int m, const cx<T>* __restric
     if (tid == 0) {
       const double n2 = n_norm * n_norm;
       *Jout = 1.0 - (orr * orr + oii * oii) / n2 + psum;
-      for (int c = 0; c < m; ++c) coef[c] = cx<double>{-2.0 * orr / n2, -2.0 * oii / n2};
+      for (int c = 0; c < 2 * m; ++c) coef[c] = cx<double>{-2.0 * orr / n2, -2.0 * oii / n2};
     }
   } else if (cost_kind == COST_ZCAL) {
     cx<double> mm[4];
     for (int c = 0; c < 4; ++c) {
+      const int s = sc.rsec ? sc.zmap[c] / m : -1, col = sc.rsec ? sc.zmap[c] % m : c;
       double orr = 0, oii = 0;
       for (int i = tid; i < N; i += nthr) {
-        const cx<T> t = Xt[i + N * c], v = xN(i + N * c);
+        if (s >= 0 && sc.rsec[i] != s) continue;
+        const cx<T> t = Xt[i + N * col], v = xN(i + N * col);
         orr += (double)t.r * v.r + (double)t.i * v.i;
         oii += (double)t.r * v.i - (double)t.i * v.r;
       }
@@ -199,14 +219,55 @@ __device__ __forceinline__ void chain_costs(int N, int m, const cx<T>* __restric
                                {(v1.r * em.r - v1.i * em.i) / a1, (v1.r * em.i + v1.i * em.r) / a1},
                                {v2.r / a2, v2.i / a2},
                                {(v2.r * em.r - v2.i * em.i) / a2, (v2.r * em.i + v2.i * em.r) / a2}};
-      const double sc = -2.0 * F / 16.0;
-      for (int c = 0; c < 4; ++c) coef[c] = cx<double>{sc * g[c].r, sc * g[c].i};
+      const double sc2 = -2.0 * F / 16.0;
+      for (int c = 0; c < 2 * m; ++c) coef[c] = cx<double>{0, 0};
+      for (int c = 0; c < 4; ++c) {
+        const cx<double> v = {sc2 * g[c].r, sc2 * g[c].i};
+        if (sc.rsec) {
+          coef[sc.zmap[c]] = v;
+        } else {
+          coef[c] = v;
+          coef[m + c] = v;
+        }
+      }
     }
   } else {
     if (tid == 0) {
       *Jout = psum;
-      for (int c = 0; c < m; ++c) coef[c] = cx<double>{0, 0};
+      for (int c = 0; c < 2 * m; ++c) coef[c] = cx<double>{0, 0};
     }
+  }
+}
+
+// Terminal cost of the stored x_N for every seed (one workgroup per seed) on the paths whose forward pass has
+// no fused epilogue (large-N GEMM pipeline, Tsit5): J[b] = cost (+ J[b] when accumulate: the state penalty is
+// already stored there) and the λ_N coefficients.
+template <typename T>
+__global__ void k_terminal_cost(int N, int m, int Nt, const cx<T>* __restrict__ X, const cx<T>* __restrict__ Xt,
+                                int cost_kind, double n_norm, int accumulate, double* __restrict__ J,
+                                cx<double>* __restrict__ coef, Sectors sc) {
+  __shared__ double red[8];
+  const int b = blockIdx.x;
+  const size_t Nm = (size_t)N * m;
+  const cx<T>* xN = X + ((size_t)b * (Nt + 1) + Nt) * Nm;
+  const double psum = accumulate ? J[b] : 0.0;
+  __syncthreads();  // every thread has read J[b] before thread 0 overwrites it
+  chain_costs<T>(N, m, Xt, [&](int o) { return xN[o]; }, cost_kind, n_norm, psum, red, J + b,
+                 coef + (size_t)b * 2 * m, sc);
+}
+
+// λ_N = dJ/dx(x_N) = coef ⊙ Xt for every seed -> Lam[b][Nt] (device-side costs).
+template <typename T>
+__global__ void k_lambda_final(int N, int m, int Nt, int B, const cx<T>* __restrict__ Xt,
+                               const cx<double>* __restrict__ coef, cx<T>* __restrict__ Lam, Sectors sc) {
+  const size_t Nm = (size_t)N * m;
+  for (size_t gi = blockIdx.x * (size_t)blockDim.x + threadIdx.x; gi < Nm * B; gi += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(gi / Nm);
+    const size_t o = gi - (size_t)b * Nm;
+    const cx<double> cf = lam_coef(coef + (size_t)b * 2 * m, sc, m, (int)(o % N), (int)(o / N));
+    const cx<T> t = Xt[o];
+    Lam[((size_t)b * (Nt + 1) + Nt) * Nm + o] =
+        cx<T>{(T)(cf.r * t.r - cf.i * t.i), (T)(cf.r * t.i + cf.i * t.r)};
   }
 }
 
@@ -355,7 +416,8 @@ template <typename T, int S, int JT, int CB>
 __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
     int N, int m, int Nt, const cx<T>* __restrict__ U, const cx<T>* __restrict__ x0, int x0_per_seed,
     cx<T>* __restrict__ X, const cx<T>* __restrict__ Xt, int cost_kind, double n_norm,
-    const unsigned char* __restrict__ pmask, double mu, double* __restrict__ Jout, cx<double>* __restrict__ coef) {
+    const unsigned char* __restrict__ pmask, double mu, double* __restrict__ Jout, cx<double>* __restrict__ coef,
+    Sectors sc) {
   using R = ChainRegs<T, S, JT, CB, true>;
   constexpr int XS = R::XS, D = R::D;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -435,14 +497,14 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_fwd(
   QOC_CT_DUMP();
   const cx<T>* xNp = xb + (Nt & 1) * XB;
   chain_costs<T>(N, m, Xt, [&](int o) { return xNp[XS * (o / N) + o % N]; }, cost_kind, n_norm, block_sum(pen, red) * mu,
-                 red, Jout + b, coef + (size_t)b * m);
+                 red, Jout + b, coef + (size_t)b * 2 * m, sc);
 }
 
 template <typename T, int S, int JT, int CB>
 __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
     int N, int m, int Nt, const cx<T>* __restrict__ U, const cx<T>* __restrict__ X, cx<T>* __restrict__ Lam,
     const cx<T>* __restrict__ Xt, int cost_kind, const cx<double>* __restrict__ coef,
-    const unsigned char* __restrict__ pmask, double mu, const cx<T>* __restrict__ src) {
+    const unsigned char* __restrict__ pmask, double mu, const cx<T>* __restrict__ src, Sectors sc) {
   using R = ChainRegs<T, S, JT, CB, false>;
   constexpr int XS = R::XS, D = R::D;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -468,7 +530,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_chain_bwd(
       if (cost_kind == COST_EXTERNAL) {
         v = Lb[(size_t)Nt * Nm + o];
       } else {
-        const cx<double> cf = coef[(size_t)b * m + c];
+        const cx<double> cf = lam_coef(coef + (size_t)b * 2 * m, sc, m, r, c);
         const cx<T> t = Xt[o];
         v.r = (T)(cf.r * t.r - cf.i * t.i);
         v.i = (T)(cf.r * t.i + cf.i * t.r);

@@ -139,6 +139,19 @@ struct qoc_ctx {
   // exact (Fréchet) gradient mode workspace, allocated on first use
   void* d_fws = nullptr;
   size_t fws_bytes = 0;
+  // packed states (compress_states, src/utils.jl:96-109): two parity sectors share the kernels' columns, so the
+  // chains and the gradient run on m = max(n1, n2) columns instead of the caller's m_user = n1 + n2
+  int m_user = 0;                       // columns of the caller's states (qoc_create's m)
+  bool packed = false;
+  std::vector<unsigned char> h_rsec;    // N row sectors (0 / 1)
+  std::vector<int> pk_cols[2];          // original columns of sector s: packed column i holds pk_cols[s][i]
+  std::vector<int> pk_pos[2];           // m_user: packed column of original column c in sector s, or -1
+  int zmap[4] = {0, 1, 2, 3};           // z-calibrated cost: original column c -> s m + i
+  unsigned char* d_rsec = nullptr;
+  bool grad_rr_any_m = false;           // the fused gradient fits apart from the column count
+  // caller-layout copies, re-packed when the packing changes
+  std::vector<double> h_gen, h_x0, h_Xt;
+  std::vector<int> h_pen_rows, h_pen_cols;
   bool have_gen = false, have_x0 = false, have_cost = false, have_prop = false;
   std::string err;
 };
@@ -301,6 +314,101 @@ int download(qoc_ctx* ctx, const void* dev, double* host, size_t nelem) {
   return QOC_OK;
 }
 
+// ---- packed states (compress_states / decompress_states, src/utils.jl:96-109) ----------------------------
+// The caller's N x m_user states hold two parity sectors: rows with h_rsec[r] = s are nonzero only in the
+// original columns pk_cols[s].  With generators that keep the two row sets apart (block-diagonal), packed
+// column i = (rows of sector 0 from column pk_cols[0][i]) + (rows of sector 1 from pk_cols[1][i]) propagates
+// exactly like the two original columns, so every kernel runs on m = max(n1, n2) columns.
+bool grad_rr_cols(int m) { return m == 1 || m == 2 || m == 4 || m == 8 || m == 16; }
+
+Sectors sectors(const qoc_ctx* c) {
+  Sectors s;
+  if (c->packed) {
+    s.rsec = c->d_rsec;
+    for (int q = 0; q < 4; ++q) s.zmap[q] = c->zmap[q];
+  }
+  return s;
+}
+
+// caller layout (N x m_user, interleaved complex, column-major) -> the kernels' N x m layout.  Entries outside
+// the two blocks are dropped; `what` != nullptr makes a nonzero one an error (initial states: dropping one would
+// change the result; targets and co-state inputs only ever meet zeros there, see qoc_set_compression).
+int pack_states(qoc_ctx* c, const double* in, double* out, const char* what) {
+  const int N = c->N, m = c->m;
+  if (!c->packed) {
+    std::memcpy(out, in, (size_t)2 * N * m * sizeof(double));
+    return QOC_OK;
+  }
+  std::fill(out, out + (size_t)2 * N * m, 0.0);
+  for (int r = 0; r < N; ++r) {
+    const int s = c->h_rsec[r];
+    for (int oc = 0; oc < c->m_user; ++oc) {
+      const double* v = in + 2 * (r + (size_t)N * oc);
+      const int i = c->pk_pos[s][oc];
+      if (i >= 0) {
+        out[2 * (r + (size_t)N * i)] = v[0];
+        out[2 * (r + (size_t)N * i) + 1] = v[1];
+      } else if (what && (v[0] != 0.0 || v[1] != 0.0)) {
+        return fail(c, QOC_ERR_ARG, "%s has a nonzero entry (row %d, column %d) outside the compress_states blocks",
+                    what, r, oc);
+      }
+    }
+  }
+  return QOC_OK;
+}
+
+void unpack_states(const qoc_ctx* c, const double* in, double* out) {
+  const int N = c->N;
+  std::fill(out, out + (size_t)2 * N * c->m_user, 0.0);
+  for (int r = 0; r < N; ++r) {
+    const auto& cols = c->pk_cols[c->h_rsec[r]];
+    for (size_t i = 0; i < cols.size(); ++i) {
+      out[2 * (r + (size_t)N * cols[i])] = in[2 * (r + N * i)];
+      out[2 * (r + (size_t)N * cols[i]) + 1] = in[2 * (r + N * i) + 1];
+    }
+  }
+}
+
+// `count` consecutive N x m_user blocks -> packed device blocks (N x m each)
+int upload_states(qoc_ctx* c, const double* host, void* dev, size_t count, const char* what) {
+  const size_t Nm = (size_t)c->N * c->m, Nmu = (size_t)c->N * c->m_user;
+  if (!c->packed) return upload(c, host, dev, count * Nm);
+  std::vector<double> buf(2 * Nm * count);
+  for (size_t q = 0; q < count; ++q) {
+    int r = pack_states(c, host + 2 * Nmu * q, buf.data() + 2 * Nm * q, what);
+    if (r) return r;
+  }
+  int r = upload(c, buf.data(), dev, count * Nm);
+  if (r) return r;
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // buf is released on return
+  return QOC_OK;
+}
+
+// one packed device block -> N x m_user host block
+int download_states(qoc_ctx* c, const void* dev, double* host) {
+  const size_t Nm = (size_t)c->N * c->m;
+  if (!c->packed) return download(c, dev, host, Nm);
+  std::vector<double> buf(2 * Nm);
+  int r = download(c, dev, buf.data(), Nm);
+  if (r) return r;
+  unpack_states(c, buf.data(), host);
+  return QOC_OK;
+}
+
+// the generators keep the two row sectors apart (compress_states applies)
+bool gens_block_diagonal(const qoc_ctx* c) {
+  const int N = c->N;
+  const size_t NN = (size_t)N * N;
+  for (int j = 0; j <= c->nu; ++j)
+    for (int col = 0; col < N; ++col)
+      for (int row = 0; row < N; ++row)
+        if (c->h_rsec[row] != c->h_rsec[col]) {
+          const double* v = c->h_gen.data() + 2 * (j * NN + row + (size_t)N * col);
+          if (v[0] != 0.0 || v[1] != 0.0) return false;
+        }
+  return true;
+}
+
 size_t chain_lds(const qoc_ctx* c) {
   const ChainShape sh = chain_shape(c->N, c->m, c->prec == QOC_FP64);
   // sized for the largest column block either direction may use (chain_dispatch's override: 2 at JT >= 10)
@@ -399,7 +507,7 @@ int run_forward(qoc_ctx* c) {
     hipLaunchKernelGGL((k_chain_fwd<T, S, JT, CB>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
                        (const cx<T>*)c->d_U, (const cx<T>*)c->d_x0, c->x0_per_seed, (cx<T>*)c->d_X,
                        (const cx<T>*)c->d_Xt, c->cost_kind, c->cost_n, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu,
-                       c->d_J, c->d_coef);
+                       c->d_J, c->d_coef, sectors(c));
     return hipGetLastError();
   });
   mark_end(c, mk);
@@ -427,7 +535,7 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
       hipLaunchKernelGGL((k_chain_bwd<T, S, JT, CB>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
                          (const cx<T>*)c->d_U, (const cx<T>*)c->d_X, (cx<T>*)c->d_L, (const cx<T>*)c->d_Xt,
                          c->cost_kind, (const cx<double>*)c->d_coef, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu,
-                         c->src_on ? (const cx<T>*)c->d_src : nullptr);
+                         c->src_on ? (const cx<T>*)c->d_src : nullptr, sectors(c));
       return hipGetLastError();
     });
     mark_end(c, mk);
@@ -782,9 +890,9 @@ int big_forward(qoc_ctx* c) {
                        c->d_pmask, c->mu, c->d_J);
     HIPCHK(c, hipGetLastError());
   }
-  if (c->cost_kind == QOC_COST_TRACE) {
-    hipLaunchKernelGGL((k_trace_cost<T>), dim3(B), dim3(256), 0, c->stream, N, m, Nt, (const cx<T>*)c->d_X,
-                       (const cx<T>*)c->d_Xt, c->cost_n, pen ? 1 : 0, c->d_J, c->d_coef);
+  if (c->cost_kind != QOC_COST_EXTERNAL) {
+    hipLaunchKernelGGL((k_terminal_cost<T>), dim3(B), dim3(256), 0, c->stream, N, m, Nt, (const cx<T>*)c->d_X,
+                       (const cx<T>*)c->d_Xt, c->cost_kind, c->cost_n, pen ? 1 : 0, c->d_J, c->d_coef, sectors(c));
     HIPCHK(c, hipGetLastError());
   } else if (!pen) {
     HIPCHK(c, hipMemsetAsync(c->d_J, 0, (size_t)B * sizeof(double), c->stream));
@@ -801,9 +909,9 @@ int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
   const unsigned eb = (unsigned)std::min<size_t>((Nm * B + 255) / 256, 8192);
   int r;
   int mk = mark_begin(c, 2);
-  if (c->cost_kind == QOC_COST_TRACE) {
+  if (c->cost_kind != QOC_COST_EXTERNAL) {
     hipLaunchKernelGGL((k_lambda_final<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, (const cx<T>*)c->d_Xt,
-                       (const cx<double>*)c->d_coef, (cx<T>*)c->d_L);
+                       (const cx<double>*)c->d_coef, (cx<T>*)c->d_L, sectors(c));
     HIPCHK(c, hipGetLastError());
   }
   if (pen) {
@@ -1132,9 +1240,10 @@ int ode_forward(qoc_ctx* c) {
                        (const cx<T>*)c->d_X, c->d_pmask, c->mu, c->d_J);
     HIPCHK(c, hipGetLastError());
   }
-  if (c->cost_kind == QOC_COST_TRACE) {
-    hipLaunchKernelGGL((k_trace_cost<T>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
-                       (const cx<T>*)c->d_X, (const cx<T>*)c->d_Xt, c->cost_n, pen ? 1 : 0, c->d_J, c->d_coef);
+  if (c->cost_kind != QOC_COST_EXTERNAL) {
+    hipLaunchKernelGGL((k_terminal_cost<T>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
+                       (const cx<T>*)c->d_X, (const cx<T>*)c->d_Xt, c->cost_kind, c->cost_n, pen ? 1 : 0, c->d_J,
+                       c->d_coef, sectors(c));
     HIPCHK(c, hipGetLastError());
   } else if (!pen) {
     HIPCHK(c, hipMemsetAsync(c->d_J, 0, (size_t)c->B * sizeof(double), c->stream));
@@ -1150,9 +1259,9 @@ int ode_adjoint(qoc_ctx* c) {
   const bool pen = c->mu != 0.0;
   const unsigned eb = (unsigned)std::min<size_t>((Nm * B + 255) / 256, 8192);
   int mk = mark_begin(c, 2);
-  if (c->cost_kind == QOC_COST_TRACE) {
+  if (c->cost_kind != QOC_COST_EXTERNAL) {
     hipLaunchKernelGGL((k_lambda_final<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, (const cx<T>*)c->d_Xt,
-                       (const cx<double>*)c->d_coef, (cx<T>*)c->d_L);
+                       (const cx<double>*)c->d_coef, (cx<T>*)c->d_L, sectors(c));
     HIPCHK(c, hipGetLastError());
   }
   if (pen) {
@@ -1218,6 +1327,7 @@ TChainArgs tchain_args(qoc_ctx* c) {
   g.coef = c->d_coef;
   g.src = c->src_on ? c->d_src : nullptr;
   g.tcoef = c->d_tcoef;
+  g.sc = sectors(c);
   return g;
 }
 
@@ -1465,6 +1575,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   c->dev = device;
   c->N = N;
   c->m = m;
+  c->m_user = m;
   c->nu = nu;
   c->Nt = Nt;
   c->B = B;
@@ -1492,7 +1603,8 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
       {&c->d_X, (size_t)B * (Nt + 1) * Nm * c->esz},
       {&c->d_L, (size_t)B * (Nt + 1) * Nm * c->esz},
       {(void**)&c->d_J, (size_t)B * sizeof(double)},
-      {(void**)&c->d_coef, (size_t)B * m * sizeof(cx<double>)},
+      {(void**)&c->d_coef, (size_t)B * 2 * m * sizeof(cx<double>)},
+      {(void**)&c->d_rsec, (size_t)N},
       {(void**)&c->d_dJdu, (size_t)B * nu * Nt * sizeof(double)},
       {(void**)&c->d_flag, sizeof(int)},
       {(void**)&c->d_hist, 13 * 64 * sizeof(unsigned long long)},
@@ -1510,8 +1622,8 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   const bool env_gemm = getenv("QOC_GRAD_GEMM") && atoi(getenv("QOC_GRAD_GEMM")) != 0;
   const size_t grr_lds = (size_t)2 * (nu + 1) * N * (precision == QOC_FP64 ? (N | 1) : ((N + 3) & ~3)) *
                          (precision == QOC_FP64 ? 8 : 4);
-  c->grad_rr = !c->big && N <= 48 && (m == 1 || m == 2 || m == 4 || m == 8 || m == 16) && (nu == 1 || nu == 2) &&
-               grr_lds <= 160 * 1024 && !env_kernel && !env_gemm;
+  c->grad_rr_any_m = !c->big && N <= 48 && (nu == 1 || nu == 2) && grr_lds <= 160 * 1024 && !env_kernel && !env_gemm;
+  c->grad_rr = c->grad_rr_any_m && grad_rr_cols(m);
   c->grad_gemm = !c->grad_rr && !c->big && N >= 32 && nu <= 8 && !env_kernel;
   if (c->grad_rr) {
     const size_t cols = (size_t)B * (Nt + 1) * m;
@@ -1581,7 +1693,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->d_best) hipFree(c->d_best);
   if (c->d_tcoef) hipFree(c->d_tcoef);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
-                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src};
+                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& m : c->marks) {
@@ -1609,6 +1721,19 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
   if (!c || !A0 || !Aj) return fail(c, QOC_ERR_ARG, "null argument");
   HIPCHK(c, hipSetDevice(c->dev));
   const size_t NN = (size_t)c->N * c->N;
+  {  // host copy (compress_states needs block-diagonal generators; checked here and at qoc_set_compression)
+    std::vector<double> g((size_t)(c->nu + 1) * 2 * NN);
+    std::memcpy(g.data(), A0, 2 * NN * sizeof(double));
+    for (int j = 0; j < c->nu; ++j) {
+      if (!Aj[j]) return fail(c, QOC_ERR_ARG, "A[%d] is null", j);
+      std::memcpy(g.data() + (j + 1) * 2 * NN, Aj[j], 2 * NN * sizeof(double));
+    }
+    g.swap(c->h_gen);
+    if (c->packed && !gens_block_diagonal(c)) {
+      g.swap(c->h_gen);
+      return fail(c, QOC_ERR_ARG, "generators couple the two compress_states row blocks");
+    }
+  }
   int r = upload(c, A0, c->d_A, NN);
   for (int j = 0; j < c->nu && r == QOC_OK; ++j) {
     if (!Aj[j]) return fail(c, QOC_ERR_ARG, "A[%d] is null", j);
@@ -1689,10 +1814,11 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
 int qoc_set_x0(qoc_ctx* c, const double* x0, int per_seed) {
   if (!c || !x0) return fail(c, QOC_ERR_ARG, "null argument");
   HIPCHK(c, hipSetDevice(c->dev));
-  const size_t Nm = (size_t)c->N * c->m;
-  int r = upload(c, x0, c->d_x0, per_seed ? (size_t)c->B * Nm : Nm);
+  const size_t Nmu = (size_t)c->N * c->m_user, cnt = per_seed ? (size_t)c->B : 1;
+  int r = upload_states(c, x0, c->d_x0, cnt, "x0");
   if (r != QOC_OK) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->h_x0.assign(x0, x0 + 2 * Nmu * cnt);
   c->x0_per_seed = per_seed ? 1 : 0;
   c->have_x0 = true;
   c->have_prop = false;
@@ -1703,19 +1829,18 @@ int qoc_set_cost(qoc_ctx* c, int kind, const double* X_target, double n) {
   if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
   if (kind != QOC_COST_TRACE && kind != QOC_COST_ZCAL && kind != QOC_COST_EXTERNAL)
     return fail(c, QOC_ERR_ARG, "unknown cost kind %d", kind);
-  if (kind == QOC_COST_ZCAL && c->m != 4)
+  if (kind == QOC_COST_ZCAL && c->m_user != 4)
     return fail(c, QOC_ERR_ARG, "Only works for two-qubit gates, x_target must have four columns");
-  if (kind == QOC_COST_ZCAL && c->prop_method == QOC_PROP_TSIT5)
-    return fail(c, QOC_ERR_UNSUPPORTED, "z-calibrated cost is not implemented on the Tsit5 path");
-  if (kind == QOC_COST_ZCAL && c->big)
-    return fail(c, QOC_ERR_UNSUPPORTED, "z-calibrated cost is not implemented on the large-N path");
   if (kind != QOC_COST_EXTERNAL && !X_target) return fail(c, QOC_ERR_ARG, "X_target is null");
   if (kind == QOC_COST_TRACE && !(n != 0.0)) return fail(c, QOC_ERR_ARG, "normalisation n must be nonzero");
   HIPCHK(c, hipSetDevice(c->dev));
   if (X_target) {
-    int r = upload(c, X_target, c->d_Xt, (size_t)c->N * c->m);
+    int r = upload_states(c, X_target, c->d_Xt, 1, nullptr);
     if (r != QOC_OK) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->h_Xt.assign(X_target, X_target + (size_t)2 * c->N * c->m_user);
+  } else {
+    c->h_Xt.clear();
   }
   c->cost_kind = kind;
   c->cost_n = n;
@@ -1731,10 +1856,14 @@ int qoc_set_state_penalty(qoc_ctx* c, const int* P, int np, const int* C, int nc
   for (int a = 0; a < np; ++a) {
     if (P[a] < 0 || P[a] >= c->N) return fail(c, QOC_ERR_ARG, "penalty row %d out of range", P[a]);
     for (int bb = 0; bb < nc; ++bb) {
-      if (C[bb] < 0 || C[bb] >= c->m) return fail(c, QOC_ERR_ARG, "penalty column %d out of range", C[bb]);
-      mask[P[a] + (size_t)c->N * C[bb]] = 1;
+      if (C[bb] < 0 || C[bb] >= c->m_user) return fail(c, QOC_ERR_ARG, "penalty column %d out of range", C[bb]);
+      // packed: an entry outside the two blocks is identically zero (no penalty, no gradient)
+      const int col = c->packed ? c->pk_pos[c->h_rsec[P[a]]][C[bb]] : C[bb];
+      if (col >= 0) mask[P[a] + (size_t)c->N * col] = 1;
     }
   }
+  c->h_pen_rows.assign(P, P + np);
+  c->h_pen_cols.assign(C, C + nc);
   HIPCHK(c, hipSetDevice(c->dev));
   // kernels queued by the asynchronous entry points may still read the mask: finish them first (the engine
   // stream is non-blocking, a null-stream copy would not wait for it)
@@ -1752,15 +1881,105 @@ int qoc_set_costate_source(qoc_ctx* c, const double* dLdx) {
     c->src_on = false;
     return QOC_OK;
   }
-  const size_t n = (size_t)c->B * (c->Nt + 1) * c->N * c->m;
+  const size_t cnt = (size_t)c->B * (c->Nt + 1), n = cnt * c->N * c->m_user;  // allocated for m_user >= m
   if (!c->d_src) {
     HIPCHK(c, hipMalloc(&c->d_src, n * c->esz));
     c->dev_bytes += n * c->esz;
   }
-  int r = upload(c, dLdx, c->d_src, n);
+  int r = upload_states(c, dLdx, c->d_src, cnt, nullptr);
   if (r) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->src_on = true;
+  return QOC_OK;
+}
+
+int qoc_set_compression(qoc_ctx* c, const int* rows1, int nr1, const int* cols1, int nc1, const int* rows2, int nr2,
+                        const int* cols2, int nc2) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  HIPCHK(c, hipSetDevice(c->dev));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // queued kernels may still read the packed buffers
+  const int N = c->N, mu_ = c->m_user;
+  std::vector<unsigned char> rsec;
+  std::vector<int> cols[2], pos[2];
+  const bool on = nr1 > 0 || nr2 > 0;
+  if (on) {
+    if (!rows1 || !cols1 || !rows2 || !cols2 || nr1 < 0 || nr2 < 0 || nc1 < 0 || nc2 < 0)
+      return fail(c, QOC_ERR_ARG, "null or negative index list");
+    if (nr1 + nr2 != N) return fail(c, QOC_ERR_ARG, "the two row blocks must partition the %d rows (got %d + %d)", N, nr1, nr2);
+    if (nc1 + nc2 != mu_)
+      return fail(c, QOC_ERR_ARG, "the two column sets must partition the %d columns (got %d + %d)", mu_, nc1, nc2);
+    rsec.assign(N, 255);
+    for (int s = 0; s < 2; ++s)
+      for (int a = 0; a < (s ? nr2 : nr1); ++a) {
+        const int r = (s ? rows2 : rows1)[a];
+        if (r < 0 || r >= N || rsec[r] != 255) return fail(c, QOC_ERR_ARG, "row %d out of range or in both blocks", r);
+        rsec[r] = (unsigned char)s;
+      }
+    for (int s = 0; s < 2; ++s) pos[s].assign(mu_, -1);
+    std::vector<char> seen(mu_, 0);
+    for (int s = 0; s < 2; ++s)
+      for (int a = 0; a < (s ? nc2 : nc1); ++a) {
+        const int oc = (s ? cols2 : cols1)[a];
+        if (oc < 0 || oc >= mu_ || seen[oc]) return fail(c, QOC_ERR_ARG, "column %d out of range or in both sets", oc);
+        seen[oc] = 1;
+        pos[s][oc] = (int)cols[s].size();
+        cols[s].push_back(oc);
+      }
+  }
+  // install, validate against the generators and x0 already set, roll back on error
+  auto old_rsec = c->h_rsec;
+  std::vector<int> old_cols[2] = {c->pk_cols[0], c->pk_cols[1]}, old_pos[2] = {c->pk_pos[0], c->pk_pos[1]};
+  const bool old_packed = c->packed;
+  const int old_m = c->m;
+  auto restore = [&]() {
+    c->h_rsec = old_rsec;
+    for (int s = 0; s < 2; ++s) {
+      c->pk_cols[s] = old_cols[s];
+      c->pk_pos[s] = old_pos[s];
+    }
+    c->packed = old_packed;
+    c->m = old_m;
+  };
+  c->packed = on;
+  c->m = on ? std::max<int>(std::max<int>((int)cols[0].size(), (int)cols[1].size()), 1) : mu_;
+  c->h_rsec = rsec;
+  for (int s = 0; s < 2; ++s) {
+    c->pk_cols[s] = cols[s];
+    c->pk_pos[s] = pos[s];
+  }
+  if (on && c->have_gen && !gens_block_diagonal(c)) {
+    restore();
+    return fail(c, QOC_ERR_ARG, "generators couple the two compress_states row blocks");
+  }
+  if (on && mu_ == 4)
+    for (int oc = 0; oc < 4; ++oc) c->zmap[oc] = pos[0][oc] >= 0 ? pos[0][oc] : c->m + pos[1][oc];
+  std::string saved_err = c->err;
+  int r = QOC_OK;
+  if (on) HIPCHK(c, hipMemcpy(c->d_rsec, rsec.data(), N, hipMemcpyHostToDevice));
+  if (c->have_x0) r = upload_states(c, c->h_x0.data(), c->d_x0, c->x0_per_seed ? (size_t)c->B : 1, "x0");
+  if (r == QOC_OK && c->have_cost && !c->h_Xt.empty()) r = upload_states(c, c->h_Xt.data(), c->d_Xt, 1, nullptr);
+  if (r != QOC_OK) {
+    saved_err = c->err;
+    restore();
+    if (c->have_x0) upload_states(c, c->h_x0.data(), c->d_x0, c->x0_per_seed ? (size_t)c->B : 1, nullptr);
+    if (c->have_cost && !c->h_Xt.empty()) upload_states(c, c->h_Xt.data(), c->d_Xt, 1, nullptr);
+    c->err = saved_err;
+    return r;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (!c->h_pen_rows.empty() || c->mu != 0.0) {
+    const std::vector<int> P = c->h_pen_rows, C = c->h_pen_cols;
+    r = qoc_set_state_penalty(c, P.data(), (int)P.size(), C.data(), (int)C.size(), c->mu);
+    if (r) return r;
+  }
+  c->src_on = false;  // a co-state source must be set again in the new layout
+  c->grad_rr = c->grad_rr_any_m && grad_rr_cols(c->m);
+  if (c->grad_rr && !c->d_gws) {  // the fused gradient's W0/W1 workspace (qoc_create sized none for m_user)
+    const size_t bytes = 2 * (size_t)N * c->B * (c->Nt + 1) * mu_ * c->esz;
+    HIPCHK(c, hipMalloc(&c->d_gws, bytes));
+    c->dev_bytes += bytes;
+  }
+  c->have_prop = false;
   return QOC_OK;
 }
 
@@ -1846,9 +2065,10 @@ int qoc_grape_sensitivity(qoc_ctx* c, const double* u, int order, const double* 
   if (c->cost_kind == QOC_COST_EXTERNAL) {
     if (!lambda_final) return fail(c, QOC_ERR_ARG, "lambda_final is required for QOC_COST_EXTERNAL");
     // λ_{Nt+1} for every seed lives at Lam[b][Nt]
-    const size_t Nm = (size_t)c->N * c->m;
+    const size_t Nm = (size_t)c->N * c->m, Nmu = (size_t)c->N * c->m_user;
     for (int b = 0; b < c->B; ++b) {
-      r = upload(c, lambda_final + 2 * Nm * b, (char*)c->d_L + ((size_t)b * (c->Nt + 1) + c->Nt) * Nm * c->esz, Nm);
+      r = upload_states(c, lambda_final + 2 * Nmu * b, (char*)c->d_L + ((size_t)b * (c->Nt + 1) + c->Nt) * Nm * c->esz,
+                        1, nullptr);
       if (r) return r;
     }
   }
@@ -1867,7 +2087,7 @@ int qoc_get_states(qoc_ctx* c, int seed, int k, double* x_out) {
   if (seed < 0 || seed >= c->B || k < 0 || k > c->Nt) return fail(c, QOC_ERR_ARG, "index out of range");
   HIPCHK(c, hipSetDevice(c->dev));
   const size_t Nm = (size_t)c->N * c->m;
-  return download(c, (char*)c->d_X + ((size_t)seed * (c->Nt + 1) + k) * Nm * c->esz, x_out, Nm);
+  return download_states(c, (char*)c->d_X + ((size_t)seed * (c->Nt + 1) + k) * Nm * c->esz, x_out);
 }
 
 int qoc_get_costates(qoc_ctx* c, int seed, int k, double* lam_out) {
@@ -1876,7 +2096,7 @@ int qoc_get_costates(qoc_ctx* c, int seed, int k, double* lam_out) {
   if (seed < 0 || seed >= c->B || k < 0 || k > c->Nt) return fail(c, QOC_ERR_ARG, "index out of range");
   HIPCHK(c, hipSetDevice(c->dev));
   const size_t Nm = (size_t)c->N * c->m;
-  return download(c, (char*)c->d_L + ((size_t)seed * (c->Nt + 1) + k) * Nm * c->esz, lam_out, Nm);
+  return download_states(c, (char*)c->d_L + ((size_t)seed * (c->Nt + 1) + k) * Nm * c->esz, lam_out);
 }
 
 int qoc_get_propagator(qoc_ctx* c, int seed, int k, double* U_out) {
@@ -2020,8 +2240,6 @@ int qoc_set_propagation(qoc_ctx* c, int method, int nsub) {
     if (nsub < 1) return fail(c, QOC_ERR_ARG, "nsub must be >= 1 (got %d)", nsub);
     if (c->big || c->N > 64)
       return fail(c, QOC_ERR_UNSUPPORTED, "the Tsit5 path runs on the LDS-resident sizes (N <= 64)");
-    if (c->cost_kind == QOC_COST_ZCAL)
-      return fail(c, QOC_ERR_UNSUPPORTED, "z-calibrated cost is not implemented on the Tsit5 path");
     c->nsub = nsub;
   }
   c->prop_method = method;
@@ -2038,7 +2256,6 @@ int qoc_propagate_envelope(qoc_ctx* c, int kind, const double* params, int np, d
   const int need_nu = kind == QOC_ENV_TUNABLE_BUS ? 1 : 2;
   if (c->nu != need_nu) return fail(c, QOC_ERR_ARG, "envelope %d drives %d controls, context has nu=%d", kind, need_nu, c->nu);
   if (c->big || c->N > 64) return fail(c, QOC_ERR_UNSUPPORTED, "the Tsit5 path runs on the LDS-resident sizes (N <= 64)");
-  if (c->cost_kind == QOC_COST_ZCAL) return fail(c, QOC_ERR_UNSUPPORTED, "z-calibrated cost on the Tsit5 path");
   if (!(dt > 0) || !(tgate > 0)) return fail(c, QOC_ERR_ARG, "tgate and dt must be positive");
   const long long nsteps = (long long)std::llround(tgate / dt);
   const size_t env_lds = (size_t)(c->nu + 1) * c->N * c->N * c->esz;
@@ -2063,23 +2280,25 @@ int qoc_propagate_envelope(qoc_ctx* c, int kind, const double* params, int np, d
                          (const cx<float>*)c->d_x0, c->x0_per_seed, (cx<float>*)c->d_X);
     e = hipGetLastError();
   }
-  if (e == hipSuccess && c->cost_kind == QOC_COST_TRACE) {
+  if (e == hipSuccess && c->cost_kind != QOC_COST_EXTERNAL) {
     if (c->prec == QOC_FP64)
-      hipLaunchKernelGGL((k_trace_cost<double>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
-                         (const cx<double>*)c->d_X, (const cx<double>*)c->d_Xt, c->cost_n, 0, c->d_J, c->d_coef);
+      hipLaunchKernelGGL((k_terminal_cost<double>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
+                         (const cx<double>*)c->d_X, (const cx<double>*)c->d_Xt, c->cost_kind, c->cost_n, 0, c->d_J,
+                         c->d_coef, sectors(c));
     else
-      hipLaunchKernelGGL((k_trace_cost<float>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
-                         (const cx<float>*)c->d_X, (const cx<float>*)c->d_Xt, c->cost_n, 0, c->d_J, c->d_coef);
+      hipLaunchKernelGGL((k_terminal_cost<float>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
+                         (const cx<float>*)c->d_X, (const cx<float>*)c->d_Xt, c->cost_kind, c->cost_n, 0, c->d_J,
+                         c->d_coef, sectors(c));
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  if (e == hipSuccess && J_out && c->cost_kind == QOC_COST_TRACE)
+  if (e == hipSuccess && J_out && c->cost_kind != QOC_COST_EXTERNAL)
     e = hipMemcpy(J_out, c->d_J, c->B * sizeof(double), hipMemcpyDeviceToHost);
   hipFree(dP);
   if (e == hipSuccess && x_out) {
-    const size_t Nm = (size_t)c->N * c->m;
+    const size_t Nm = (size_t)c->N * c->m, Nmu = (size_t)c->N * c->m_user;
     for (int b = 0; b < c->B; ++b) {
-      int r2 = download(c, (char*)c->d_X + ((size_t)b * (c->Nt + 1) + c->Nt) * Nm * c->esz, x_out + 2 * Nm * b, Nm);
+      int r2 = download_states(c, (char*)c->d_X + ((size_t)b * (c->Nt + 1) + c->Nt) * Nm * c->esz, x_out + 2 * Nmu * b);
       if (r2) return r2;
     }
   }
@@ -2097,6 +2316,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[4] = c->chain_mode;
   info[5] = c->big ? c->expm_alg : c->expm_run;  // the large-N pipeline keeps its own (Taylor / Padé) choice
   info[6] = c->chain_mode == 1 && c->cheb && tchain_mf(c) ? 1 : 0;  // Taylor-action chains: Chebyshev terms
+  info[7] = c->m;  // state columns the kernels run on (< the caller's m when compress_states packing is on)
   return QOC_OK;
 }
 

@@ -221,7 +221,8 @@ struct TChainArgs {
   const unsigned char* pmask;  // N x m state-penalty mask (nullptr: no penalty)
   double mu;
   double* J;               // B
-  cx<double>* coef;        // B x m
+  cx<double>* coef;        // B x 2m λ_N coefficients ([sector][column], chain_costs)
+  Sectors sc;              // row sectors of a packed state (compress_states)
   const void* src;         // B x (Nt+1) x N x m caller's dL/dx(x_k) added to λ_k (nullptr: none)
   const double* tcoef;     // B x Nt x TCHEB_STRIDE Chebyshev coefficients (Chebyshev variant)
 };
@@ -472,7 +473,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_fwd(const TChainArgs g
   __syncthreads();  // SOLO shapes skip the per-term barriers: x_N of every wave visible to all
   const cx<T>* xNp = yb + cur * XB;
   chain_costs<T>(N, m, (const cx<T>*)g.Xt, [&](int o) { return xNp[XS * (o / N) + o % N]; }, g.cost_kind, g.n_norm,
-                 block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * m);
+                 block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * 2 * m, g.sc);
 }
 
 // λ_k = exp(A_k)^H λ_{k+1} + dL/dx(x_k) for every slice of one seed (src/gradient_computations.jl:46-58); the
@@ -509,7 +510,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_bwd(const TChainArgs g
       if (g.cost_kind == COST_EXTERNAL) {
         v = Lb[(size_t)Nt * Nm + o];
       } else {
-        const cx<double> cf = g.coef[(size_t)b * m + c];
+        const cx<double> cf = lam_coef(g.coef + (size_t)b * 2 * m, g.sc, m, r, c);
         const cx<T> t = Xt[o];
         v.r = (T)(cf.r * t.r - cf.i * t.i);
         v.i = (T)(cf.r * t.i + cf.i * t.r);
@@ -837,7 +838,7 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_fwd(const TChainArgs g) {
                         const int r = o % N, col = o / N, q = ((col >> 1) * RP + r) * 4 + 2 * (col & 1);
                         return cx<double>{yN[q], yN[q + 1]};
                       },
-                      g.cost_kind, g.n_norm, block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * m);
+                      g.cost_kind, g.n_norm, block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * 2 * m, g.sc);
 }
 
 template <int KQ, bool CHEB>
@@ -877,7 +878,7 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_bwd(const TChainArgs g) {
     if (g.cost_kind == COST_EXTERNAL) {
       v = Lb[(size_t)Nt * Nm + o];
     } else {
-      const cx<double> cf = g.coef[(size_t)b * m + col], t = Xt[o];
+      const cx<double> cf = lam_coef(g.coef + (size_t)b * 2 * m, g.sc, m, r, col), t = Xt[o];
       v = cx<double>{cf.r * t.r - cf.i * t.i, cf.r * t.i + cf.i * t.r};
     }
     if (g.pmask && g.pmask[o]) {

@@ -45,6 +45,7 @@ SIGNATURES = {
     "qoc_set_cost": (C.c_int, [_vp, C.c_int, _dp, C.c_double]),
     "qoc_set_state_penalty": (C.c_int, [_vp, _ip, C.c_int, _ip, C.c_int, C.c_double]),
     "qoc_set_costate_source": (C.c_int, [_vp, _dp]),
+    "qoc_set_compression": (C.c_int, [_vp, _ip, C.c_int, _ip, C.c_int, _ip, C.c_int, _ip, C.c_int]),
     "qoc_propagate": (C.c_int, [_vp, _dp, _dp]),
     "qoc_grape_sensitivity": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp]),
     "qoc_propagate_dev": (C.c_int, [_vp, _vp, _vp]),

@@ -159,7 +159,7 @@ class MI355XCache:
     ``.dJdu`` — are exposed; ``x``/``lam`` fetch lazily from HBM.
     """
 
-    def __init__(self, A0, x0, u_size, B=1, precision="fp64", device=0):
+    def __init__(self, A0, x0, u_size, B=1, precision="fp64", device=0, compress=None):
         nu, Nt = u_size
         x0 = np.asarray(x0, dtype=np.complex128)
         if x0.ndim == 1:
@@ -167,6 +167,8 @@ class MI355XCache:
         placeholder = [np.zeros_like(np.asarray(A0, dtype=np.complex128)) for _ in range(nu)]
         self.engine = GrapeEngine(A0, placeholder, x0, Nt, B, precision, device)
         self.engine.set_cost_external()
+        if compress is not None:
+            self.engine.set_compression(compress)
         self.u = np.zeros((nu, Nt)) if B == 1 else np.zeros((B, nu, Nt))
         self.dJdu = None
         self._penalty = None
@@ -184,9 +186,11 @@ class MI355XCache:
         return _LazySeries(self, which, seed)
 
 
-def setup_grape_cache(A0, x0, u_size, B=1, precision="fp64", device=0) -> MI355XCache:
-    """Workspace on the GPU (src/gradient_computations.jl:79-96); errors on a dimension mismatch."""
-    return MI355XCache(A0, x0, u_size, B, precision, device)
+def setup_grape_cache(A0, x0, u_size, B=1, precision="fp64", device=0, compress=None) -> MI355XCache:
+    """Workspace on the GPU (src/gradient_computations.jl:79-96); errors on a dimension mismatch.
+    compress = ((rows1, cols1), (rows2, cols2)) (0-based, compress_states' v, src/utils.jl:96-109) runs the
+    kernels on the packed columns; x, λ, dL_dx and dJfinal_dx keep the caller's layout."""
+    return MI355XCache(A0, x0, u_size, B, precision, device, compress)
 
 
 def propagate(A0, A, u, x0, cache: MI355XCache | None = None):

@@ -155,6 +155,23 @@ class GrapeEngine:
         flat = np.ascontiguousarray(np.transpose(d, (0, 1, 3, 2))).ravel().view(np.float64)
         self._chk(self._lib.qoc_set_costate_source(self._h, _ptr(flat)))
 
+    def set_compression(self, v):
+        """compress_states inside the engine (src/utils.jl:96-109, include/qoc.h qoc_set_compression):
+        v = ((rows1, cols1), (rows2, cols2)) with 0-based index sequences, as systems.compress_states takes
+        it; the chains and the gradient then run on max(n1, n2) packed columns while every argument and
+        result keeps the (N, m) layout.  None turns packing off."""
+        ip = C.POINTER(C.c_int)
+        if v is None:
+            self._chk(self._lib.qoc_set_compression(self._h, None, 0, None, 0, None, 0, None, 0))
+            return
+        (r1, c1), (r2, c2) = v
+        arrs = [np.ascontiguousarray(list(a), dtype=np.int32) for a in (r1, c1, r2, c2)]
+        self._keep_cmp = arrs
+        args = []
+        for a in arrs:
+            args += [a.ctypes.data_as(ip), len(a)]
+        self._chk(self._lib.qoc_set_compression(self._h, *args))
+
     def set_propagation(self, method: str = "expm", nsub: int = 10):
         """'expm' (U_k = exp(A_k), default) or 'tsit5': the reference's ODE path (propagate_pwc /
         compute_pwc_gradient, src/gradient_computations.jl:108-169) with nsub fixed Tsit5 steps per
@@ -282,7 +299,7 @@ class GrapeEngine:
         return {"path": "large_n" if v[0] else "lds", "chunk": int(v[1]), "ns_iters": int(v[2]),
                 "device_bytes": int(v[3]), "chain": "taylor" if v[4] == 1 else "propagators",
                 "expm": {0: "pade", 1: "taylor_rr", 2: "ps_lds"}.get(int(v[5]), "?"),
-                "chain_poly": "chebyshev" if v[6] else "taylor"}
+                "chain_poly": "chebyshev" if v[6] else "taylor", "kernel_m": int(v[7])}
 
     def set_chain(self, mode: str = "auto"):
         """How the chains apply exp(A_k) (include/qoc.h qoc_set_chain): 'propagators' forms every U_k (the

@@ -299,6 +299,22 @@ def tunable_bus_problem(Nt=2000, tgate=350.0) -> Problem:
     return Problem("two_qubit_tunable_bus", A0, [A1], x0, xt, 1.0, Nt, "fp64")
 
 
+def tunable_bus_cz_problem(Nt=2000, tgate=350.0) -> Problem:
+    """The tunable-bus model driven as a CZ gate on the four computational states |q1 c q2> = |000>, |001>,
+    |100>, |101> (coupler in 0; m = 4, the z-calibrated cost's two-qubit case).  The Hamiltonian conserves
+    excitation number, so it is block-diagonal in the parity of the basis index: TUNABLE_BUS_PARITY is the
+    compress_states spec of test/test_utils.jl:23 (rows 1:2:27 with columns [1, 4], rows 2:2:26 with [2, 3],
+    here 0-based)."""
+    H0, Hc, qb = tunable_bus_model()
+    dt = tgate / Nt
+    x0 = qb.columns(["000", "001", "100", "101"]).astype(np.complex128)
+    xt = x0 @ gate_unitary("CZ").astype(np.complex128)
+    return Problem("two_qubit_tunable_bus_cz", -1j * H0 * dt, [-1j * Hc * dt], x0, xt, 4.0, Nt, "fp64")
+
+
+TUNABLE_BUS_PARITY = ((list(range(0, 27, 2)), [0, 3]), (list(range(1, 27, 2)), [1, 2]))
+
+
 def tunable_bus_controls(B, Nt, seed=0) -> np.ndarray:
     rng = np.random.default_rng(seed)
     return rng.uniform(0.3, 1.0, size=(B, 1, Nt))

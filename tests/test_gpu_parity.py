@@ -114,24 +114,42 @@ def test_state_penalty(built_lib, chain):
     _check(prob, systems.zz_controls(2, 40, 4.0, seed=9), penalty=pen, chain=chain)
 
 
-@pytest.mark.parametrize("chain", CHAINS)
-def test_zcalibrated_cost(built_lib, chain):
-    """setup_infidelity_zcalibrated on the device (golden section in k_chain_fwd)."""
+# z-calibrated cost: the phase θ comes from a golden-section search stopped at bracket width ZCAL_TOL
+# (src/fidelities.jl:81-137, restated in qoc_chain.hpp optimal_calibration and qoc_oracle.optimal_calibration).
+# Its iterates branch on comparisons of objective values that the GPU and the oracle compute to ~1e-16, so the
+# two may stop at different points of the last bracket: |Δθ| <= ZCAL_TOL.  J is stationary in θ at the optimum
+# (ΔJ = O(Δθ^2) ~ 1e-18, so J is held to the 1e-12 bar), but λ_N = dJ/dx carries e^{iθ} linearly: dJdu moves by
+# up to |Δθ| |∂dJdu/∂θ| ~ ZCAL_TOL ||dJdu||.  The gradient bound is therefore 10 x ZCAL_TOL, not the 1e-10 bar.
+ZCAL_TOL = 1e-9
+
+
+@pytest.mark.parametrize("path", ["propagators", "taylor", "large_n", "tsit5"])
+def test_zcalibrated_cost(built_lib, path, monkeypatch):
+    """setup_infidelity_zcalibrated on the device, on every propagation path (src/penalty_fcns.jl:27-42 works
+    for any propagation): fused in the chain epilogues, or k_terminal_cost after the large-N / Tsit5 forward."""
     from qoc_amd import GrapeEngine, systems
+    if path == "large_n":
+        monkeypatch.setenv("QOC_FORCE_LARGE_N", "1")
     prob = systems.zz_problem(40, tgate=4.0)
     u = systems.zz_controls(3, 40, 4.0, seed=21)
     e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=3)
-    e.set_chain(chain)
+    if path in ("propagators", "taylor"):
+        e.set_chain(path)
+    if path == "tsit5":
+        e.set_propagation("tsit5", 8)
+    assert (e.info()["path"] == "large_n") == (path == "large_n")
     e.set_cost_zcalibrated(prob.x_target)
     J = e.propagate(u)
     g = e.grape_sensitivity(u, 3)
-    Jz, dJz = O.setup_infidelity_zcalibrated(prob.x_target)
+    cost = O.setup_infidelity_zcalibrated(prob.x_target)
     for b in range(3):
-        cache = O.setup_grape_cache(prob.A0, prob.x0, u[b].shape)
-        x = O.propagate(prob.A0, prob.A, u[b], prob.x0, cache)
-        gr = O.grape_sensitivity(prob.A0, prob.A, dJz, cache.u, prob.x0, cache, dUkdp_order=3)
-        assert abs(J[b] - Jz(x[-1])) < 1e-11
-        assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) < 1e-8
+        if path == "tsit5":
+            Jr, gr = O.grape_eval_ode(prob.A0, prob.A, u[b], prob.x0, prob.x_target, order=3, nsub=8, cost=cost)
+        else:
+            Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, order=3, cost=cost)
+        assert abs(J[b] - Jr) <= 1e-12, (b, J[b] - Jr)
+        rel = np.linalg.norm(g[b] - gr) / np.linalg.norm(gr)
+        assert rel <= 10 * ZCAL_TOL, (b, rel)
     e.close()
 
 
@@ -284,49 +302,6 @@ def test_exact_gradient_large_n_path(built_lib, monkeypatch):
         _, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order="exact")
         assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
     e.close()
-
-
-def test_compressed_states_give_identical_results(built_lib):
-    """compress_states (src/utils.jl:96-109): a parity-structured problem propagated with m = 2 packed
-    columns gives the same J, dJdu and (decompressed) states as the m = 4 original."""
-    from qoc_amd import GrapeEngine, systems
-    rng = np.random.default_rng(8)
-    N, Nt = 12, 15
-    r1, r2 = list(range(0, N, 2)), list(range(1, N, 2))
-
-    def block_gen(scale):
-        H = np.zeros((N, N), complex)
-        for r in (r1, r2):
-            G = rng.standard_normal((len(r), len(r))) + 1j * rng.standard_normal((len(r), len(r)))
-            H[np.ix_(r, r)] = (G + G.conj().T) / 2
-        return -1j * scale * H
-    A0, A = block_gen(0.2), [block_gen(0.05), block_gen(0.05)]
-    v = ((r1, [0, 3]), (r2, [1, 2]))
-
-    def structured(M):
-        M = M.copy()
-        M[np.ix_(r1, [1, 2])] = 0
-        M[np.ix_(r2, [0, 3])] = 0
-        return M
-    x0 = structured(np.eye(N, dtype=complex)[:, :4] + np.eye(N, dtype=complex)[:, 4:8])
-    Z = rng.standard_normal((N, 4)) + 1j * rng.standard_normal((N, 4))
-    xt = structured(Z)
-    full = systems.Problem("parity", A0, A, x0, xt, 4.0, Nt, "fp64")
-    comp = systems.compress_problem(full, v)
-    assert comp.x0.shape[1] == 2
-    u = rng.uniform(-1, 1, size=(2, 2, Nt))
-    res = []
-    for p in (full, comp):
-        e = GrapeEngine(p.A0, p.A, p.x0, Nt, B=2)
-        e.set_cost_trace(p.x_target, p.n)
-        J = e.propagate(u)
-        g = e.grape_sensitivity(u, 3)
-        res.append((J, g, e.state(Nt, seed=1)))
-        e.close()
-    (J0, g0, x0N), (J1, g1, x1N) = res
-    np.testing.assert_allclose(J1, J0, rtol=0, atol=1e-13)
-    np.testing.assert_allclose(g1, g0, rtol=1e-11, atol=1e-14)
-    np.testing.assert_allclose(systems.decompress_states(x1N, v), x0N, rtol=0, atol=1e-13)
 
 
 def test_taylor_default_and_pade_option_agree(built_lib, monkeypatch):
