@@ -293,6 +293,40 @@ def setup_infidelity_zcalibrated(x_target):
     return J, dJ_dx
 
 
+def setup_infidelity_zcalibrated_shifted(x_target, dtheta):
+    """setup_infidelity_zcalibrated with the rrule's calibration phase moved by dtheta from the golden-section
+    optimum (J unchanged).  The golden section (src/fidelities.jl:105-137) compares objective values of a flat
+    maximum, so it fixes θ only to ~sqrt(eps): two correct implementations differ by such a shift, and the
+    gradient carries e^{iθ} linearly.  Used by zcal_gradient_match."""
+    X = np.asarray(x_target, dtype=np.complex128)
+    J, _ = setup_infidelity_zcalibrated(X)
+
+    def dJ_dx(x):
+        m = [complex(v) for v in np.diag(X.conj().T @ x)]
+        F, th = optimal_calibration(m)
+        t = th[0] + dtheta
+        v1, v2 = m[0] + _cis(t) * m[1], m[2] + _cis(t) * m[3]
+        g = np.array([v1 / abs(v1), v1 / abs(v1) * _cis(-t), v2 / abs(v2), v2 / abs(v2) * _cis(-t)])
+        return (-2 * F / 16) * (X * g[None, :])
+    return J, dJ_dx
+
+
+def zcal_gradient_match(g, A0, A, u, x0, x_target, order=3, nsub=None, h=1e-6):
+    """Distance of a z-calibrated GRAPE gradient g from the oracle's family g(Δθ) of gradients at calibration
+    phases Δθ away from the oracle's own: fits g ≈ g(0) + Δθ g'(0) (g' by central difference) and returns
+    (relative residual, Δθ).  A correct implementation has residual ~ rounding and |Δθ| ~ sqrt(eps)."""
+    def grad(dt):
+        cost = setup_infidelity_zcalibrated_shifted(x_target, dt)
+        if nsub:
+            return grape_eval_ode(A0, A, u, x0, x_target, order=order, nsub=nsub, cost=cost)[1]
+        return grape_eval(A0, A, u, x0, x_target, order=order, cost=cost)[1]
+    g0, gp, gm = grad(0.0), grad(h), grad(-h)
+    d = (gp - gm) / (2 * h)
+    r = np.asarray(g) - g0
+    t = float(np.vdot(d, r).real / np.vdot(d, d).real)
+    return float(np.linalg.norm(r - t * d) / np.linalg.norm(g0)), t
+
+
 # ---------------------------------------------------------------------------
 # Phase-calibrated fidelities (src/fidelities.jl)
 # ---------------------------------------------------------------------------

@@ -61,15 +61,23 @@ struct GemmArgs {
 // Both operands are staged in LDS as [row or col][k] planes (re / im) with k contiguous.  K is
 // permuted inside each 16-deep sub-slab: at MFMA step t lane l multiplies k = 4 (l >> 4) + t, so a
 // lane's four k values are adjacent and one 16-byte LDS read (per 4 floats) fetches its fragment
-// for the sub-slab.  Rows are padded by 16 bytes: the 16 rows a lane group reads then fall on
-// distinct 16-byte bank slots.  A slab is KS sub-slabs (BK = 16 KS); NBUF = 2 double-buffers the
+// for the sub-slab.  A slab is KS sub-slabs (BK = 16 KS); NBUF = 2 double-buffers the
 // LDS image (one barrier per slab), NBUF = 1 uses one image and two barriers per slab but a smaller
 // LDS footprint (more workgroups per CU).
+// Bank layout.  fp32, KS = 1: rows of 16 floats (64 B, no padding) with the four 16-byte chunks of row r
+// XOR-swizzled by (r >> 1) & 3.  A ds_read_b128 lane group ({0-3,12-15,20-27}, ... : rows li, chunk kq =
+// l >> 4) then touches 16 distinct 16-byte slots of the 256-byte bank window, and the ds_write_b128 groups (8
+// contiguous lanes, 128-byte window) of both store layouts do too — conflict-free both ways.  (The previous
+// 16-byte row padding left 2-way conflicts in every read group: ~43 % of the LDS-active cycles in PMC.)
+// Otherwise rows are padded by 16 bytes.
 template <typename T, int KS>
 struct BgLay {
   static constexpr int BK = 16 * KS;
-  static constexpr int LDK = BK + 16 / (int)sizeof(T);  // row stride in elements
+  static constexpr bool SWZ = KS == 1 && sizeof(T) == 4;
+  static constexpr int LDK = SWZ ? BK : BK + 16 / (int)sizeof(T);  // row stride in elements
   static constexpr int PLANE = BG_BM * LDK;
+  // element offset of the 4-element chunk `ch` (k = 4 ch .. 4 ch + 3 of the slab) of row r
+  static __device__ __forceinline__ int off(int r, int ch) { return r * LDK + 4 * (SWZ ? (ch ^ ((r >> 1) & 3)) : ch); }
 };
 
 template <typename T>
@@ -117,8 +125,8 @@ __device__ __forceinline__ void bg_store(T* __restrict__ pre, T* __restrict__ pi
 #pragma unroll
   for (int j = 0; j < KS; ++j) {
     const int kg = (KCONT ? (tid & 3) : (tid >> 6)) + 4 * j;
-    *reinterpret_cast<V*>(pre + r * L::LDK + 4 * kg) = re[j];
-    *reinterpret_cast<V*>(pim + r * L::LDK + 4 * kg) = im[j];
+    *reinterpret_cast<V*>(pre + L::off(r, kg)) = re[j];
+    *reinterpret_cast<V*>(pim + L::off(r, kg)) = im[j];
   }
 }
 
@@ -226,13 +234,13 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
       V ar[2], ai[2], br[2], bi[2];
 #pragma unroll
       for (int x = 0; x < 2; ++x) {
-        const int o = (wr + 16 * x + li) * L::LDK + 16 * q + 4 * kq;
+        const int o = L::off(wr + 16 * x + li, 4 * q + kq);
         ar[x] = *reinterpret_cast<const V*>(cur + 0 * L::PLANE + o);
         ai[x] = *reinterpret_cast<const V*>(cur + 1 * L::PLANE + o);
       }
 #pragma unroll
       for (int y = 0; y < 2; ++y) {
-        const int o = (wc + 16 * y + li) * L::LDK + 16 * q + 4 * kq;
+        const int o = L::off(wc + 16 * y + li, 4 * q + kq);
         br[y] = *reinterpret_cast<const V*>(cur + 2 * L::PLANE + o);
         bi[y] = *reinterpret_cast<const V*>(cur + 3 * L::PLANE + o);
       }

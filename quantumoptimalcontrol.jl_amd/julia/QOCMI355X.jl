@@ -52,12 +52,15 @@ mutable struct MI355XCache
 end
 
 """
-    setup_grape_cache(A0, x0, u_size; device=0)
+    setup_grape_cache(A0, x0, u_size; device=0, compress=nothing)
 
 GPU-resident replacement of `QuantumOptimalControl.setup_grape_cache`
 (src/gradient_computations.jl:79-96).  Errors on a dimension mismatch like the reference.
+`compress = v` takes the reference's `compress_states` spec (src/utils.jl:96-109, 1-based, e.g.
+`((1:2:27, [1,4]), (2:2:26, [2,3]))`): the kernels then run on the packed columns while `x`, `dJfinal_dx`
+and `dL_dx` keep the caller's N x m layout (qoc_set_compression).
 """
-function setup_grape_cache(A0, x0, u_size; device::Integer=0)
+function setup_grape_cache(A0, x0, u_size; device::Integer=0, compress=nothing)
     size(x0, 1) == size(A0, 1) || error("Error when creating cache, A0 and x0 have incompatiable dimensions")
     nu, Nt = u_size
     ref = Ref{Ptr{Cvoid}}(C_NULL)
@@ -68,7 +71,16 @@ function setup_grape_cache(A0, x0, u_size; device::Integer=0)
     c = MI355XCache(ref[], size(A0, 1), size(x0, 2), nu, Nt)
     check(ccall((:qoc_set_cost, libqoc), Cint, (Ptr{Cvoid}, Cint, Ptr{ComplexF64}, Cdouble),
                 c.ctx, QOC_COST_EXTERNAL, C_NULL, 1.0), c.ctx)
+    compress === nothing || set_compression!(c, compress)
     return c
+end
+
+function set_compression!(c::MI355XCache, v)
+    (r1, c1), (r2, c2) = v
+    l = [Cint.(collect(a) .- 1) for a in (r1, c1, r2, c2)]   # 0-based
+    check(ccall((:qoc_set_compression, libqoc), Cint,
+                (Ptr{Cvoid}, Ptr{Cint}, Cint, Ptr{Cint}, Cint, Ptr{Cint}, Cint, Ptr{Cint}, Cint),
+                c.ctx, l[1], length(l[1]), l[2], length(l[2]), l[3], length(l[3]), l[4], length(l[4])), c.ctx)
 end
 
 function upload!(c::MI355XCache, A0, A, x0)

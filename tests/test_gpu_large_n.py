@@ -153,13 +153,3 @@ def test_synthetic_n256_fp64(built_lib):
     u = systems.synthetic_controls(1, 2, 2, seed=1)
     J, g, info, _ = _run(prob, u, precision="fp64")
     _compare(prob, u, J, g, tol=(1e-11, 1e-9))
-
-
-def test_large_n_zcal_unsupported(built_lib, monkeypatch):
-    from qoc_amd import GrapeEngine, QOCError, systems
-    monkeypatch.setenv("QOC_FORCE_LARGE_N", "1")
-    prob = systems.zz_problem(10)
-    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=1)
-    with pytest.raises(QOCError):
-        e.set_cost_zcalibrated(prob.x_target)
-    e.close()

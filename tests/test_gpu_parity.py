@@ -114,13 +114,13 @@ def test_state_penalty(built_lib, chain):
     _check(prob, systems.zz_controls(2, 40, 4.0, seed=9), penalty=pen, chain=chain)
 
 
-# z-calibrated cost: the phase θ comes from a golden-section search stopped at bracket width ZCAL_TOL
-# (src/fidelities.jl:81-137, restated in qoc_chain.hpp optimal_calibration and qoc_oracle.optimal_calibration).
-# Its iterates branch on comparisons of objective values that the GPU and the oracle compute to ~1e-16, so the
-# two may stop at different points of the last bracket: |Δθ| <= ZCAL_TOL.  J is stationary in θ at the optimum
-# (ΔJ = O(Δθ^2) ~ 1e-18, so J is held to the 1e-12 bar), but λ_N = dJ/dx carries e^{iθ} linearly: dJdu moves by
-# up to |Δθ| |∂dJdu/∂θ| ~ ZCAL_TOL ||dJdu||.  The gradient bound is therefore 10 x ZCAL_TOL, not the 1e-10 bar.
-ZCAL_TOL = 1e-9
+# z-calibrated cost: the calibration phase θ comes from a golden-section search over a flat maximum
+# (src/fidelities.jl:81-137).  Its iterates branch on comparisons of objective values that agree to ~1e-16 near
+# the optimum, so θ is fixed only to ~sqrt(eps) and two correct implementations (GPU, oracle) stop at phases a
+# few 1e-9..1e-8 apart.  J is stationary in θ (held to the 1e-12 bar); the gradient carries e^{iθ} linearly, so
+# it is compared with the oracle's gradient family g(Δθ) (qoc_oracle.zcal_gradient_match): the GPU gradient
+# must equal g(Δθ) for some |Δθ| <= 1e-6 to the 1e-10 bar.
+ZCAL_MAX_DTHETA = 1e-6
 
 
 @pytest.mark.parametrize("path", ["propagators", "taylor", "large_n", "tsit5"])
@@ -141,15 +141,14 @@ def test_zcalibrated_cost(built_lib, path, monkeypatch):
     e.set_cost_zcalibrated(prob.x_target)
     J = e.propagate(u)
     g = e.grape_sensitivity(u, 3)
-    cost = O.setup_infidelity_zcalibrated(prob.x_target)
+    Jz, _ = O.setup_infidelity_zcalibrated(prob.x_target)
+    nsub = 8 if path == "tsit5" else None
     for b in range(3):
-        if path == "tsit5":
-            Jr, gr = O.grape_eval_ode(prob.A0, prob.A, u[b], prob.x0, prob.x_target, order=3, nsub=8, cost=cost)
-        else:
-            Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, order=3, cost=cost)
-        assert abs(J[b] - Jr) <= 1e-12, (b, J[b] - Jr)
-        rel = np.linalg.norm(g[b] - gr) / np.linalg.norm(gr)
-        assert rel <= 10 * ZCAL_TOL, (b, rel)
+        xN = (O.propagate_pwc_ode(prob.A0, prob.A, u[b], prob.x0, nsub=8) if nsub else
+              O.propagate(prob.A0, prob.A, u[b], prob.x0))[-1]
+        assert abs(J[b] - Jz(xN)) <= 1e-12, (b, J[b] - Jz(xN))
+        res, dth = O.zcal_gradient_match(g[b], prob.A0, prob.A, u[b], prob.x0, prob.x_target, order=3, nsub=nsub)
+        assert res <= 1e-10 and abs(dth) <= ZCAL_MAX_DTHETA, (b, res, dth)
     e.close()
 
 

@@ -358,3 +358,18 @@ def test_tsit5_order_and_pwc_ode_matches_expm_path():
     J2, g2 = O.grape_eval_ode(prob.A0, prob.A, u, prob.x0, prob.x_target, prob.n, order=3, nsub=10)
     assert abs(J1 - J2) < 1e-9
     assert np.linalg.norm(g1 - g2) / np.linalg.norm(g1) < 1e-7
+
+
+def test_zcal_gradient_match_recovers_a_phase_shift():
+    """qoc_oracle.zcal_gradient_match (the z-cal GPU check): a gradient taken at a calibration phase 3e-9 away
+    from the golden-section optimum is recognised (Δθ recovered, residual at rounding level)."""
+    from qoc_amd import systems
+    prob = systems.tunable_bus_cz_problem(Nt=20, tgate=3.5)
+    u = systems.tunable_bus_controls(1, 20, seed=3)[0]
+    g = O.grape_eval(prob.A0, prob.A, u, prob.x0, prob.x_target, order=3,
+                     cost=O.setup_infidelity_zcalibrated_shifted(prob.x_target, 3e-9))[1]
+    res, dth = O.zcal_gradient_match(g, prob.A0, prob.A, u, prob.x0, prob.x_target, order=3)
+    assert res < 1e-12 and abs(dth - 3e-9) < 1e-12, (res, dth)
+    g0 = O.grape_eval(prob.A0, prob.A, u, prob.x0, prob.x_target, order=3,
+                      cost=O.setup_infidelity_zcalibrated(prob.x_target))[1]
+    assert np.linalg.norm(g - g0) / np.linalg.norm(g0) > 1e-10  # the shift is visible at the 1e-10 bar
