@@ -651,7 +651,10 @@ int big_lincomb(qoc_ctx* c, LinArgs a) {
 }
 
 // exp(A_k) for units [u0, u0+cnt) -> d_U.  Workspace buffers w(i), i < 8, of cnt x N x N.
+// Paterson-Stockmeyer degree m = 3r + 2 (r = 2..8): the largest ||A||_1 whose Taylor tail sum_{k>m} ||A||^k / k!
+// is <= 2^-53 (fp64) or 2^-24 (fp32, the unit roundoff of the arithmetic the fp32 pipeline runs in)
 static const double hTaylorTheta[7] = {0.069933, 0.247240, 0.553491, 0.978345, 1.504147, 2.113468, 2.791345};
+static const double hTaylorTheta32[7] = {0.648322, 1.31065, 2.099345, 2.969587, 3.894655, 4.858047, 5.849147};
 
 // Taylor / Paterson-Stockmeyer exponential on the GEMM pipeline (the large-N analogue of k_expm ALG 1):
 // degree m = 3r + 2 with (r, s) minimising 2 + r + s for the chunk's max norm; every B_i = c I + c' A + c'' A2
@@ -662,8 +665,9 @@ int taylor_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, con
   const size_t NN = (size_t)N * N, esz = c->esz;
   auto w = [&](int i) { return mk_opd(ws, (size_t)i * ws_items * NN, esz, (long long)NN); };
   int tr = 2, ts = 0, best = 1 << 30;
+  const double* th = sizeof(T) == 4 ? hTaylorTheta32 : hTaylorTheta;
   for (int rr = 2; rr <= 8; ++rr) {
-    const int ss = nA > hTaylorTheta[rr - 2] ? (int)std::ceil(std::log2(nA / hTaylorTheta[rr - 2])) : 0;
+    const int ss = nA > th[rr - 2] ? (int)std::ceil(std::log2(nA / th[rr - 2])) : 0;
     if (2 + rr + ss < best || (2 + rr + ss == best && ss < ts)) {
       best = 2 + rr + ss;
       tr = rr;
@@ -1377,7 +1381,8 @@ int tchain_forward(qoc_ctx* c) {
     mk = mark_begin(c, 1);
     hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
-      auto kern = cheb ? k_tchain_mf_fwd<KQ, true> : k_tchain_mf_fwd<KQ, false>;
+      auto kern = threads <= 512 ? (cheb ? k_tchain_mf_fwd<KQ, true, 512> : k_tchain_mf_fwd<KQ, false, 512>)
+                                 : (cheb ? k_tchain_mf_fwd<KQ, true, 1024> : k_tchain_mf_fwd<KQ, false, 1024>);
       hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (r != hipSuccess) return r;
       hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);
@@ -1415,7 +1420,8 @@ int tchain_backward(qoc_ctx* c) {
     hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
       // the (P, s, coefficients) of the forward pass are reused: the same polynomial as the states'
-      auto kern = c->cheb_ran ? k_tchain_mf_bwd<KQ, true> : k_tchain_mf_bwd<KQ, false>;
+      auto kern = threads <= 512 ? (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 512> : k_tchain_mf_bwd<KQ, false, 512>)
+                                 : (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 1024> : k_tchain_mf_bwd<KQ, false, 1024>);
       hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (r != hipSuccess) return r;
       hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);

@@ -602,6 +602,11 @@ __host__ __device__ inline int tchain_mf_kq(int N) {  // k-quads per product, bu
   return q <= 3 ? 3 : q <= 4 ? 4 : q <= 6 ? 6 : q <= 8 ? 8 : q <= 10 ? 10 : q <= 12 ? 12 : 0;
 }
 __host__ __device__ inline int tchain_mf_waves(int N, int m) { return ((N + 15) / 16) * ((m + 1) / 2); }
+// Launch bound of the MFMA chain kernels: a workgroup of <= 8 waves (cavity 3, zz 2) is compiled for 512 threads,
+// i.e. 256 VGPRs per wave (the KQ = 12 kernels use <= 241).  The former 1024-thread bound capped the waves at 128
+// VGPRs: from KQ = 6 up the formed A rows and the step data spilled to scratch (308 B per lane at KQ = 10), and the
+// reload's vmcnt(0) waited for the next step's prefetch in every slice (~3k cycles per slice at N = 40).
+__host__ __device__ inline int tchain_mf_maxt(int N, int m) { return tchain_mf_waves(N, m) <= 8 ? 512 : 1024; }
 __host__ inline size_t tchain_mf_lds(int N, int m, int nu) {
   const int KQ = tchain_mf_kq(N), CP = (m + 1) / 2;
   // generators, 2 x (y, y') state buffers, then 16 reduction doubles + 48 for 1/t + 64 per wave (coefficients)
@@ -645,16 +650,22 @@ struct TChainMF {
       ar[q] = v.r;
       ai[q] = v.i;
     }
+    // each generator's KQ elements are read into their own registers before any of them is used: with one
+    // register pair reused per element the compiler waited for every read in turn (lgkmcnt(0) after each
+    // ds_read_b128, ~KQ LDS latencies per generator and slice)
 #pragma unroll
     for (int j = 0; j < TCHAIN_NUMAX; ++j) {
       if (j >= nu) break;
       const double uj = uk[j];
       const cx<double>* Gj = gen + (size_t)(j + 1) * NN;
+      cx<double> v[KQ];
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) v[q] = Gj[rc + N * min(4 * q + kl, N - 1)];
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int q = 0; q < KQ; ++q) {
-        const cx<double> v = Gj[rc + N * min(4 * q + kl, N - 1)];
-        ar[q] += uj * v.r;
-        ai[q] += uj * v.i;
+        ar[q] += uj * v[q].r;
+        ai[q] += uj * v[q].i;
       }
     }
 #pragma unroll
@@ -667,6 +678,27 @@ struct TChainMF {
   // D = A y for this wave's rows and column pair (y from buffer `buf`)
   __device__ __forceinline__ double matvec(const double (&ar)[KQ], const double (&ai)[KQ], const double* __restrict__ y,
                                            const double* __restrict__ yp) const {
+#ifdef QOC_TCHAIN_DPP_PRIME
+    // y' without LDS: B' = S P B with P the n <-> n^1 swap inside each lane quad (DPP quad_perm [1,0,3,2]) and
+    // S = diag(-1, +1, -1, +1) on the output columns, so Ai B' = S (Ai (P B)): the Ai products accumulate on
+    // their own chain and enter with the column sign.  Half the LDS reads per term, and put() writes y only.
+    // Measured slower (tools/tchain_probe.hip, same box: N = 40 Taylor 558 vs 466 ns per term, Chebyshev 666 vs
+    // 536; N = 9 equal): the DPP moves put VALU results in front of every second MFMA (VALU -> MFMA operand
+    // hazards), which costs more than the LDS reads they replace.  Kept as an option.
+    {
+      double bv[KQ];
+      const int base = (cp * RP + kl) * 4 + n;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) bv[q] = y[base + 16 * q];
+      double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        d0 = MF<double>::mma4(ar[q], bv[q], d0);
+        d1 = MF<double>::mma4(ai[q], dpp_mov<0xB1>(bv[q]), d1);
+      }
+      return (n & 1) ? d0 + d1 : d0 - d1;
+    }
+#endif
     double bv[KQ], bp[KQ];
     const int base = (cp * RP + kl) * 4 + n;
 #pragma unroll
@@ -699,7 +731,9 @@ struct TChainMF {
     if (rowD < RP) {
       const int o = (cp * RP + rowD) * 4;
       y[o + n] = v;
+#ifndef QOC_TCHAIN_DPP_PRIME
       yp[o + (n ^ 1)] = (n & 1) ? -v : v;  // y' = [-yi, yr]: re (n even) -> slot n+1 as is; im -> slot n-1 negated
+#endif
     }
   }
   __device__ __forceinline__ void sync() const {
@@ -766,8 +800,8 @@ struct TChainMF {
   }
 };
 
-template <int KQ, bool CHEB>
-__global__ __launch_bounds__(1024) void k_tchain_mf_fwd(const TChainArgs g) {
+template <int KQ, bool CHEB, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
   using C = TChainMF<KQ>;
   constexpr int RP = C::RP;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -817,13 +851,21 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_fwd(const TChainArgs g) {
   TPre nx;
   tpre_load(stb, ub, nu, nx, ceb);
   for (int k = 0; k < Nt; ++k) {
+    TC_T(s0);
     const TPre st = nx;
     if (k + 1 < Nt) tpre_load(stb + k + 1, ub + (size_t)(k + 1) * nu, nu, nx, CHEB ? ceb + (size_t)(k + 1) * TCHEB_STRIDE : nullptr);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     double ar[KQ], ai[KQ];
     rg.form(N, nu, gen, st.u, st.scale, ar, ai);
+    TC_T(s1);
     rg.template step<CHEB>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, st.pi}, acc, st.cl, cw);
+    TC_T(s2);
     store(acc, k + 1);
+    TC_T(s3);
+    TC_ADD(10, s1 - s0);
+    TC_ADD(11, s2 - s1);
+    TC_ADD(12, s3 - s2);
+    TC_ADD(13, 1);
   }
   __syncthreads();
 #ifdef QOC_PROBE
@@ -841,8 +883,8 @@ __global__ __launch_bounds__(1024) void k_tchain_mf_fwd(const TChainArgs g) {
                       g.cost_kind, g.n_norm, block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * 2 * m, g.sc);
 }
 
-template <int KQ, bool CHEB>
-__global__ __launch_bounds__(1024) void k_tchain_mf_bwd(const TChainArgs g) {
+template <int KQ, bool CHEB, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
   using C = TChainMF<KQ>;
   constexpr int RP = C::RP;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

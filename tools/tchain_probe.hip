@@ -61,7 +61,7 @@ void run(int N, int m, int Nt, int B, int P) {
 #endif
 }
 
-template <int KQ>
+template <int KQ, bool CHEB, int MAXT = 512>
 void run_mf(int N, int m, int Nt, int B, int P) {
   const int nu = 2;
   const size_t NN = (size_t)N * N;
@@ -78,17 +78,22 @@ void run_mf(int N, int m, int Nt, int B, int P) {
   (void)hipMalloc(&dst, st.size() * sizeof(TStep));
   (void)hipMalloc(&dx0, x0.size() * 16);
   (void)hipMalloc(&dX, (size_t)B * (Nt + 1) * N * m * 16);
-  (void)hipMalloc(&dcoef, (size_t)B * m * 16);
+  (void)hipMalloc(&dcoef, (size_t)B * 2 * m * 16);
   (void)hipMalloc(&dJ, B * 8);
   (void)hipMemcpy(dA, A.data(), A.size() * 16, hipMemcpyHostToDevice);
   (void)hipMemcpy(du, u.data(), u.size() * 8, hipMemcpyHostToDevice);
   (void)hipMemcpy(dst, st.data(), st.size() * sizeof(TStep), hipMemcpyHostToDevice);
   (void)hipMemcpy(dx0, x0.data(), x0.size() * 16, hipMemcpyHostToDevice);
+  double* dtc = nullptr;  // Chebyshev coefficients (any values: the timing does not depend on them)
+  std::vector<double> tc_h((size_t)B * Nt * TCHEB_STRIDE);
+  for (size_t e = 0; e < tc_h.size(); ++e) tc_h[e] = 1.0 / (1.0 + (double)(e % TCHEB_STRIDE));
+  (void)hipMalloc(&dtc, tc_h.size() * 8);
+  (void)hipMemcpy(dtc, tc_h.data(), tc_h.size() * 8, hipMemcpyHostToDevice);
   TChainArgs g{};
   g.N = N; g.m = m; g.nu = nu; g.Nt = Nt; g.At = dA; g.u = du; g.steps = dst; g.x0 = dx0; g.X = dX; g.L = dX;
-  g.Xt = dx0; g.cost_kind = 2; g.n_norm = 1.0; g.J = dJ; g.coef = (cx<double>*)dcoef;
+  g.Xt = dx0; g.cost_kind = 2; g.n_norm = 1.0; g.J = dJ; g.coef = (cx<double>*)dcoef; g.tcoef = dtc;
   const size_t lds = tchain_mf_lds(N, m, nu);
-  (void)hipFuncSetAttribute((const void*)k_tchain_mf_fwd<KQ, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  (void)hipFuncSetAttribute((const void*)k_tchain_mf_fwd<KQ, CHEB, MAXT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
@@ -99,31 +104,36 @@ void run_mf(int N, int m, int Nt, int B, int P) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tc), z, sizeof(z));
 #endif
     (void)hipEventRecord(a);
-    hipLaunchKernelGGL((k_tchain_mf_fwd<KQ, false>), dim3(B), dim3(64 * tchain_mf_waves(N, m)), lds, 0, g);
+    hipLaunchKernelGGL((k_tchain_mf_fwd<KQ, CHEB, MAXT>), dim3(B), dim3(64 * tchain_mf_waves(N, m)), lds, 0, g);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     (void)hipEventElapsedTime(&ms, a, b);
   }
-  printf("MFMA N=%d m=%d Nt=%d B=%d P=%d (KQ=%d, %d waves): %.3f ms = %.3f us/step, %.0f ns/term\n", N, m, Nt, B, P, KQ,
-         tchain_mf_waves(N, m), ms, ms * 1e3 / Nt, ms * 1e6 / Nt / P);
+  std::vector<double> xh((size_t)B * (Nt + 1) * N * m * 2);
+  (void)hipMemcpy(xh.data(), dX, xh.size() * 8, hipMemcpyDeviceToHost);
+  double cs = 0;
+  for (size_t e = 0; e < xh.size(); ++e) cs += xh[e] * (1.0 + (double)(e % 7));
+  printf("MFMA%s N=%d m=%d Nt=%d B=%d P=%d (KQ=%d, %d waves): %.3f ms = %.3f us/step, %.0f ns/term  checksum %.15e\n",
+         CHEB ? " cheb" : "", N, m, Nt, B, P, KQ, tchain_mf_waves(N, m), ms, ms * 1e3 / Nt, ms * 1e6 / Nt / P, cs);
+  (void)hipFree(dtc);
 #ifdef QOC_PROBE
   unsigned long long tc[16];
   (void)hipMemcpyFromSymbol(tc, HIP_SYMBOL(g_tc), sizeof(tc));
   const double nt = (double)tc[7];
   printf("   per term (s_memtime): matvec %.0f  put %.0f  barrier %.0f  (terms %.0f); clock %.2f GHz\n", tc[4] / nt, tc[5] / nt,
          tc[6] / nt, nt, (double)tc[8] / ((double)tc[9] * 10.0));
+  const double ns_ = (double)tc[13];
+  printf("   per slice: prefetch+form %.0f  step %.0f  store %.0f  (slices %.0f)\n", tc[10] / ns_, tc[11] / ns_, tc[12] / ns_, ns_);
 #endif
 }
 
 int main() {
-  run_mf<10>(40, 2, 1000, 256, 11);
-  run_mf<10>(40, 2, 1000, 8, 11);
-  run_mf<3>(9, 4, 500, 512, 9);
-  run_mf<3>(9, 4, 500, 8, 9);
-  run_mf<8>(27, 1, 2000, 512, 20);
-  run<4, 10, 2, 1>(40, 2, 1000, 256, 11);
-  run<4, 10, 2, 1>(40, 2, 1000, 8, 11);
-  run<4, 4, 1, 1>(9, 4, 500, 512, 9);
-  run<4, 4, 1, 1>(9, 4, 500, 8, 9);
+  run_mf<10, false>(40, 2, 1000, 256, 11);
+  run_mf<10, true>(40, 2, 1000, 256, 9);
+  run_mf<10, true>(40, 2, 1000, 256, 6);
+  run_mf<10, true>(40, 2, 1000, 256, 3);
+  run_mf<3, true>(9, 4, 500, 512, 8);
+  run_mf<3, true>(9, 4, 500, 512, 4);
+  run_mf<8, false>(27, 1, 2000, 512, 20);
   return 0;
 }
