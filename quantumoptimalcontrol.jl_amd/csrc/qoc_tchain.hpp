@@ -85,7 +85,10 @@ __device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const do
   d.scale = v.w;
   d.cl = ce ? ce[threadIdx.x & 63] : 0.0;
 #pragma unroll
-  for (int j = 0; j < TCHAIN_NUMAX; ++j) d.u[j] = j < nu ? uk[j + z] : 0.0;
+  for (int j = 0; j < TCHAIN_NUMAX; ++j) {  // clamped, unconditional loads: no branches around them
+    const double v = uk[min(j, nu - 1) + z];
+    d.u[j] = j < nu ? v : 0.0;
+  }
 }
 
 struct TChainParams {
@@ -462,14 +465,16 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_fwd(const TChainArgs g
   TPre nx;
   tpre_load(stb, ub, nu, nx);
   for (int k = 0; k < Nt; ++k) {
+    if (k > 0) store(acc, k);  // ahead of the prefetch (see k_tchain_mf_fwd)
     const TPre st = nx;
-    if (k + 1 < Nt) tpre_load(stb + k + 1, ub + (size_t)(k + 1) * nu, nu, nx);
+    const int kn = min(k + 1, Nt - 1);
+    tpre_load(stb + kn, ub + (size_t)kn * nu, nu, nx);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     cx<T> a[JT];
     rg.form(N, nu, gen, st.u, (T)st.scale, a);
     rg.step(N, m, a, yb, XB, cur, P, ns, cx<double>{st.pr, st.pi}, acc);
-    store(acc, k + 1);
   }
+  store(acc, Nt);
   __syncthreads();  // SOLO shapes skip the per-term barriers: x_N of every wave visible to all
   const cx<T>* xNp = yb + cur * XB;
   chain_costs<T>(N, m, (const cx<T>*)g.Xt, [&](int o) { return xNp[XS * (o / N) + o % N]; }, g.cost_kind, g.n_norm,
@@ -543,9 +548,19 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_bwd(const TChainArgs g
   cx<T> acc[NP][CB];
   TPre nx;
   tpre_load(stb + Nt - 1, ub + (size_t)(Nt - 1) * nu, nu, nx);
+  auto store_lam = [&](int k_) __attribute__((always_inline)) {
+    cx<T>* Lk = Lb + (size_t)k_ * Nm;
+#pragma unroll
+    for (int ps = 0; ps < NP; ++ps)
+#pragma unroll
+      for (int bb = 0; bb < CB; ++bb)
+        if (own[ps][bb]) Lk[rg.i + N * (rg.c_begin + rg.c_step * ps + bb)] = acc[ps][bb];
+  };
   for (int k = Nt - 1; k >= 0; --k) {
+    if (k < Nt - 1) store_lam(k + 1);  // ahead of the prefetch (see k_tchain_mf_fwd)
     const TPre st = nx;
-    if (k > 0) tpre_load(stb + k - 1, ub + (size_t)(k - 1) * nu, nu, nx);
+    const int kp = max(k - 1, 0);
+    tpre_load(stb + kp, ub + (size_t)kp * nu, nu, nx);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     cx<T> xk[NP][CB];  // 2 mu x_k (penalty) + the caller's dL/dx(x_k), loaded ahead of the Taylor terms
 #pragma unroll
@@ -565,7 +580,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_bwd(const TChainArgs g
     cx<T> a[JT];
     rg.form(N, nu, gen, st.u, (T)st.scale, a);
     rg.step(N, m, a, yb, XB, cur, P, ns, cx<double>{st.pr, -st.pi}, acc);
-    cx<T>* Lk = Lb + (size_t)k * Nm;
     bool any_pen = false;
 #pragma unroll
     for (int ps = 0; ps < NP; ++ps)
@@ -577,13 +591,13 @@ __global__ __launch_bounds__(CHAIN_THREADS) void k_tchain_bwd(const TChainArgs g
           any_pen = true;
           yb[cur * XB + XS * (rg.c_begin + rg.c_step * ps + bb) + rg.i] = acc[ps][bb];
         }
-        if (own[ps][bb]) Lk[rg.i + N * (rg.c_begin + rg.c_step * ps + bb)] = acc[ps][bb];
       }
     if (g.pmask || srcb) {  // the penalised entries of the state changed after the step's last barrier
       (void)any_pen;
       C::sync();
     }
   }
+  store_lam(0);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -705,10 +719,11 @@ struct TChainMF {
     for (int q = 0; q < KQ; ++q) bv[q] = y[base + 16 * q];
 #pragma unroll
     for (int q = 0; q < KQ; ++q) bp[q] = yp[base + 16 * q];
-    // the scheduler keeps ~2 reads ahead of the MFMAs; issuing all of them first (QOC_TCHAIN_EAGER_READS) measured
-    // slower on the same box (N = 40: 499 vs 464 ns per term, tools/tchain_probe.hip), the three waves' bursts
-    // queue in the LDS ahead of the first operands
-#ifdef QOC_TCHAIN_EAGER_READS
+    // all operand reads are issued before the first MFMA (left to itself the scheduler keeps one read ahead of the
+    // MFMAs, and each MFMA pair then waits out a read's LDS latency).  Same box, tools/tchain_probe.hip: N = 40
+    // 445 vs 451 ns per Chebyshev term, N = 9 310 vs 331 (with the register spills of the 1024-thread bound
+    // it had measured the other way).  QOC_TCHAIN_LAZY_READS restores the scheduler's order.
+#ifndef QOC_TCHAIN_LAZY_READS
     __builtin_amdgcn_sched_barrier(0);
 #endif
     // two accumulation chains, alternating, so consecutive MFMAs never depend on each other; the Ar products
@@ -852,21 +867,25 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
   tpre_load(stb, ub, nu, nx, ceb);
   for (int k = 0; k < Nt; ++k) {
     TC_T(s0);
+    // x_k (the previous slice's result) goes to HBM here, ahead of this slice's prefetch: the wait for the
+    // prefetch at the end of the slice (vmcnt, in issue order) then never waits for a just-issued store
+    if (k > 0) store(acc, k);
     const TPre st = nx;
-    if (k + 1 < Nt) tpre_load(stb + k + 1, ub + (size_t)(k + 1) * nu, nu, nx, CHEB ? ceb + (size_t)(k + 1) * TCHEB_STRIDE : nullptr);
+    const int kn = min(k + 1, Nt - 1);
+    tpre_load(stb + kn, ub + (size_t)kn * nu, nu, nx, CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     double ar[KQ], ai[KQ];
     rg.form(N, nu, gen, st.u, st.scale, ar, ai);
     TC_T(s1);
     rg.template step<CHEB>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, st.pi}, acc, st.cl, cw);
     TC_T(s2);
-    store(acc, k + 1);
     TC_T(s3);
     TC_ADD(10, s1 - s0);
     TC_ADD(11, s2 - s1);
     TC_ADD(12, s3 - s2);
     TC_ADD(13, 1);
   }
+  store(acc, Nt);
   __syncthreads();
 #ifdef QOC_PROBE
   if (blockIdx.x == 7 && threadIdx.x == 0) {
@@ -947,8 +966,11 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
   TPre nx;
   tpre_load(stb + Nt - 1, ub + (size_t)(Nt - 1) * nu, nu, nx, CHEB ? ceb + (size_t)(Nt - 1) * TCHEB_STRIDE : nullptr);
   for (int k = Nt - 1; k >= 0; --k) {
+    // λ_{k+1} (the previous slice's result) to HBM ahead of this slice's loads (see k_tchain_mf_fwd)
+    if (k < Nt - 1 && rg.actD) reinterpret_cast<double*>(Lb + (size_t)(k + 1) * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = acc;
     const TPre st = nx;
-    if (k > 0) tpre_load(stb + k - 1, ub + (size_t)(k - 1) * nu, nu, nx, CHEB ? ceb + (size_t)(k - 1) * TCHEB_STRIDE : nullptr);
+    const int kp = max(k - 1, 0);
+    tpre_load(stb + kp, ub + (size_t)kp * nu, nu, nx, CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     const size_t ok_ = (size_t)k * Nm + rg.rowD + N * rg.colD;
     double xk = pen_m ? tmu * reinterpret_cast<const double*>(Xb + ok_)[rg.n & 1] : 0.0;
@@ -960,9 +982,9 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
       acc += xk;
       rg.put(C::ybuf(yb, rg.CP, cur, 0), C::ybuf(yb, rg.CP, cur, 1), acc);
     }
-    if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)k * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = acc;
     if (g.pmask || srcb) rg.sync();  // the penalised entries changed after the step's last barrier
   }
+  if (rg.actD) reinterpret_cast<double*>(Lb + rg.rowD + N * rg.colD)[rg.n & 1] = acc;  // λ_0
 }
 
 // Reference-equivalent accounting (the Taylor-action path forms no A_k norm of its own): the Padé (d, s) that
