@@ -1511,6 +1511,58 @@ double choose_shift(const double* A, int N, double& mr, double& mi) {
   return best;
 }
 
+// Spectral interval of the Hermitian H = i A for a skew-Hermitian generator A (column-major interleaved N x N):
+// cyclic Jacobi on the real symmetric embedding [[Re H, -Im H], [Im H, Re H]], whose eigenvalues are H's, twice.
+// Host-side, once per qoc_set_generators (N <= 64).
+void herm_interval(const double* A, int N, double& lmin, double& lmax) {
+  const int n = 2 * N;
+  std::vector<double> S((size_t)n * n);
+  auto at = [&](int r, int c) -> double& { return S[(size_t)r * n + c]; };
+  for (int col = 0; col < N; ++col)
+    for (int row = 0; row < N; ++row) {
+      const double ar = A[2 * (row + (size_t)N * col)], ai = A[2 * (row + (size_t)N * col) + 1];
+      const double hr = -ai, hi = ar;  // H = i A
+      at(row, col) = hr;
+      at(row + N, col + N) = hr;
+      at(row + N, col) = hi;
+      at(row, col + N) = -hi;
+    }
+  for (int r = 0; r < n; ++r)  // exact symmetry (A is skew-Hermitian to rounding)
+    for (int c = r + 1; c < n; ++c) at(r, c) = at(c, r) = 0.5 * (at(r, c) + at(c, r));
+  double fro = 0.0;
+  for (double v : S) fro += v * v;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < n; ++p)
+      for (int q = p + 1; q < n; ++q) off += at(p, q) * at(p, q);
+    if (off <= 1e-32 * fro) break;
+    for (int p = 0; p < n; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        const double apq = at(p, q);
+        if (std::fabs(apq) < 1e-300) continue;
+        const double theta = (at(q, q) - at(p, p)) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+        const double cs = 1.0 / std::sqrt(t * t + 1.0), sn = t * cs;
+        for (int k = 0; k < n; ++k) {  // rows/columns p, q of the rotation J^T S J
+          const double skp = at(k, p), skq = at(k, q);
+          at(k, p) = cs * skp - sn * skq;
+          at(k, q) = sn * skp + cs * skq;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double spk = at(p, k), sqk = at(q, k);
+          at(p, k) = cs * spk - sn * sqk;
+          at(q, k) = sn * spk + cs * sqk;
+        }
+      }
+  }
+  lmin = 1e300;
+  lmax = -1e300;
+  for (int k = 0; k < n; ++k) {
+    lmin = std::min(lmin, at(k, k));
+    lmax = std::max(lmax, at(k, k));
+  }
+}
+
 // RCCL, resolved on first use (librccl.so.1 of the ROCm install).
 RcclApi& rccl() {
   static RcclApi api;
@@ -1769,24 +1821,8 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
   }
   if (c->tchain_ok) {  // shifted generators Ã_j = A_j - μ_j I and their norms for the Taylor-action chains
     tchain_thresholds(c->tprm, c->prec);
-    std::vector<double> sh(2 * NN);
-    for (int j = 0; j <= c->nu && r == QOC_OK; ++j) {
-      const double* G = j == 0 ? A0 : Aj[j - 1];
-      double mr = 0, mi = 0;
-      c->tprm.nrm[j] = choose_shift(G, c->N, mr, mi);
-      c->tprm.mur[j] = mr;
-      c->tprm.mui[j] = mi;
-      std::memcpy(sh.data(), G, 2 * NN * sizeof(double));
-      for (int d = 0; d < c->N; ++d) {
-        sh[2 * (d + (size_t)c->N * d)] -= mr;
-        sh[2 * (d + (size_t)c->N * d) + 1] -= mi;
-      }
-      r = upload(c, sh.data(), (char*)c->d_At + j * NN * c->esz, NN);
-      if (r == QOC_OK) HIPCHK(c, hipStreamSynchronize(c->stream));  // sh is reused
-    }
-    if (r != QOC_OK) return r;
-    // Chebyshev needs every Ã_j skew-Hermitian (A_j^H = -A_j, Schrödinger generators -i H Δt) with an imaginary
-    // shift, so that Ã_k = -i H̃_k has its spectrum on the imaginary axis within the bound β_k
+    // Chebyshev needs every Ã_j skew-Hermitian (A_j^H = -A_j, Schrödinger generators -i H Δt), so that
+    // Ã_k = -i H̃_k has its spectrum on the imaginary axis within the bound ρ_k
     bool skew = true;
     for (int j = 0; j <= c->nu && skew; ++j) {
       const double* G = j == 0 ? A0 : Aj[j - 1];
@@ -1797,18 +1833,61 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
           amax = std::max(amax, std::hypot(G[a], G[a + 1]));
           dev = std::max(dev, std::hypot(G[a] + G[b], G[a + 1] - G[b + 1]));  // |A + A^H|
         }
-      skew = dev <= 1e-13 * std::max(amax, 1e-300) && std::fabs(c->tprm.mur[j]) <= 1e-13 * std::max(amax, 1e-300);
+      skew = dev <= 1e-13 * std::max(amax, 1e-300);
     }
+    std::vector<double> sh(2 * NN);
+    for (int j = 0; j <= c->nu && r == QOC_OK; ++j) {
+      const double* G = j == 0 ? A0 : Aj[j - 1];
+      double mr = 0, mi = 0;
+      if (skew) {
+        // the centre of H_j's spectral interval [λmin, λmax] (H_j = i A_j): Ã_j = -i (H_j - c_j I), and by Weyl's
+        // inequality every H̃_k = Σ_j u_jk (H_j - c_j I) has its spectrum within ±(r_0 + Σ_j |u_jk| r_j),
+        // r_j = (λmax - λmin) / 2 — the Chebyshev interval, tighter than the 1-norm (tunable bus: ρ 14.2 vs 19.5)
+        double lmin, lmax;
+        herm_interval(G, c->N, lmin, lmax);
+        const double cen = 0.5 * (lmin + lmax), scale = std::max(std::fabs(lmin), std::fabs(lmax));
+        mr = 0.0;
+        mi = -cen;
+        c->tprm.rad[j] = 0.5 * (lmax - lmin) + 1e-13 * scale + 1e-300;  // Jacobi's error is ~N eps |H|
+      }
+      std::memcpy(sh.data(), G, 2 * NN * sizeof(double));
+      if (!skew) {
+        c->tprm.nrm[j] = choose_shift(G, c->N, mr, mi);
+      }
+      for (int d = 0; d < c->N; ++d) {
+        sh[2 * (d + (size_t)c->N * d)] -= mr;
+        sh[2 * (d + (size_t)c->N * d) + 1] -= mi;
+      }
+      if (skew) {  // 1-norm of the shifted generator (the Taylor variant's bound)
+        double nrm = 0.0;
+        for (int col = 0; col < c->N; ++col) {
+          double sum = 0.0;
+          for (int row = 0; row < c->N; ++row)
+            sum += std::hypot(sh[2 * (row + (size_t)c->N * col)], sh[2 * (row + (size_t)c->N * col) + 1]);
+          nrm = std::max(nrm, sum);
+        }
+        c->tprm.nrm[j] = nrm;
+      } else {
+        c->tprm.rad[j] = c->tprm.nrm[j];
+      }
+      c->tprm.mur[j] = mr;
+      c->tprm.mui[j] = mi;
+      r = upload(c, sh.data(), (char*)c->d_At + j * NN * c->esz, NN);
+      if (r == QOC_OK) HIPCHK(c, hipStreamSynchronize(c->stream));  // sh is reused
+    }
+    if (r != QOC_OK) return r;
     c->cheb_ok = skew;
     const char* poly = getenv("QOC_TCHAIN_POLY");
     c->cheb = skew && !(poly && !std::strcmp(poly, "taylor"));
-    // the Taylor action wins while the slices need few terms (cavity / zz: ||Ã_0||_1 <= 0.2); large norms
-    // (tunable bus: ~5 after the shift) keep the propagators on MFMA
+    // Taylor action by default while the slices need moderately many terms: Chebyshev (fp64, skew-Hermitian)
+    // up to ρ_0 = 25 without substeps (cavity 0.15, zz 0.05, tunable bus 9.1: measured faster than Padé-13
+    // propagators there too), the Taylor variant while ||Ã_0||_1 <= 1; larger norms form propagators on MFMA
+    const bool cheb_run = c->cheb && tchain_mf(c);
     const char* env = getenv("QOC_CHAIN");
     if (c->chain_req != QOC_CHAIN_AUTO) c->chain_mode = c->chain_req;
     else if (env && !std::strcmp(env, "taylor")) c->chain_mode = 1;
     else if (env && !std::strcmp(env, "expm")) c->chain_mode = 0;
-    else c->chain_mode = c->tprm.nrm[0] <= 1.0 ? 1 : 0;
+    else c->chain_mode = (cheb_run ? c->tprm.rad[0] <= 25.0 : c->tprm.nrm[0] <= 1.0) ? 1 : 0;
   } else {
     c->chain_mode = 0;
   }
@@ -2334,7 +2413,9 @@ int qoc_set_chain(qoc_ctx* c, int mode) {
     return fail(c, QOC_ERR_UNSUPPORTED, "Taylor-action chains need N <= 48 (fp64) / 64 (fp32), nu <= 8 and the "
                                         "generators within the 160 KiB LDS");
   c->chain_req = mode;
-  if (mode == QOC_CHAIN_AUTO) mode = c->tchain_ok && c->have_gen && c->tprm.nrm[0] <= 1.0 ? 1 : 0;
+  if (mode == QOC_CHAIN_AUTO)
+    mode = c->tchain_ok && c->have_gen &&
+                   (c->cheb && tchain_mf(c) ? c->tprm.rad[0] <= 25.0 : c->tprm.nrm[0] <= 1.0) ? 1 : 0;
   c->chain_mode = mode;
   c->have_prop = false;
   return QOC_OK;

@@ -92,7 +92,8 @@ __device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const do
 }
 
 struct TChainParams {
-  double nrm[9];              // ||Ã_j||_1, j = 0..nu
+  double nrm[9];              // ||Ã_j||_1, j = 0..nu (Taylor variant)
+  double rad[9];              // half-width of H_j's spectral interval, Ã_j = -i (H_j - c_j I) (Chebyshev variant)
   double mur[9], mui[9];      // shifts μ_j
   double theta[TCHAIN_PMAX + 1];  // θ_P: largest β whose degree-P Taylor tail is within tolerance (θ_0 unused)
   double theta_max;           // substep bound (β / s <= theta_max)
@@ -176,10 +177,10 @@ __global__ void k_tchain_prep_cheb(int nu, long long units, const double* __rest
   unsigned long long cnt = 0;
   const double tol = 1.1102230246251565e-16;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < units; e += (long long)gridDim.x * blockDim.x) {
-    double beta = prm.nrm[0], mr = prm.mur[0], mi = prm.mui[0];
+    double beta = prm.rad[0], mr = prm.mur[0], mi = prm.mui[0];  // ρ_k >= the spectral radius of H̃_k (Weyl)
     for (int j = 0; j < nu; ++j) {
       const double uj = u[e * nu + j];
-      beta += fabs(uj) * prm.nrm[j + 1];
+      beta += fabs(uj) * prm.rad[j + 1];
       mr += uj * prm.mur[j + 1];
       mi += uj * prm.mui[j + 1];
     }

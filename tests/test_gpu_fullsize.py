@@ -66,11 +66,13 @@ def test_cavity_full_size(built_lib, chain):
     _check_config("cavity", seeds, None if chain == "auto" else chain)
 
 
-def test_tunable_bus_full_size(built_lib):
+@pytest.mark.parametrize("chain", ["auto", "propagators"])
+def test_tunable_bus_full_size(built_lib, chain):
     """config 4: two_qubit_tunable_bus N=27, m=1, Nt=2000, B=512 per GPU, ||A_k||_1 ~ 30: every seed against
-    the C port (the large-norm slices' exponential holds the bar over 2000 chained slices)."""
-    info = _check_config("tunable_bus", list(range(512)))
-    assert info["chain"] == "propagators"
+    the C port, over 2000 chained slices: the default Chebyshev Taylor-action chains (spectral radius ~14 per
+    slice) and the propagators (the reference's Padé-13)."""
+    info = _check_config("tunable_bus", list(range(512)), None if chain == "auto" else chain)
+    assert info["chain"] == ("taylor" if chain == "auto" else "propagators")
 
 
 def test_synthetic_full_size_fp32(built_lib):

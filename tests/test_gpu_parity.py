@@ -460,13 +460,12 @@ def test_external_cost_and_costates(built_lib, chain):
 
 
 def test_large_norm_slices_default_to_the_reference_pade(built_lib):
-    """||A0||_1 > 4 theta_12 (tunable bus): the propagators run the reference's Padé-13 + solve by default (no
-    Taylor scheme in the executed histogram) and match the oracle."""
+    """||A0||_1 > 4 theta_12 (tunable bus): in propagator mode the exponentials run the reference's Padé-13 +
+    solve by default (no Taylor scheme in the executed histogram) and match the oracle."""
     from qoc_amd import systems
     prob = systems.tunable_bus_problem(Nt=120)
     u = systems.tunable_bus_controls(2, prob.Nt, seed=23)
-    e = _engine(prob, 2)
-    assert e.info()["chain"] == "propagators"
+    e = _engine(prob, 2, chain="propagators")
     J = e.propagate(u)
     g = e.grape_sensitivity(u, 3)
     assert e.taylor_histogram() == {}
