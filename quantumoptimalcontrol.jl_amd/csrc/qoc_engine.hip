@@ -1381,8 +1381,10 @@ int tchain_forward(qoc_ctx* c) {
     mk = mark_begin(c, 1);
     hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
-      auto kern = threads <= 512 ? (cheb ? k_tchain_mf_fwd<KQ, true, 512> : k_tchain_mf_fwd<KQ, false, 512>)
-                                 : (cheb ? k_tchain_mf_fwd<KQ, true, 1024> : k_tchain_mf_fwd<KQ, false, 1024>);
+      const int mt = tchain_mf_maxt(c->N, c->m, c->nu);
+      auto kern = mt == 256   ? (cheb ? k_tchain_mf_fwd<KQ, true, 256> : k_tchain_mf_fwd<KQ, false, 256>)
+                  : mt == 512 ? (cheb ? k_tchain_mf_fwd<KQ, true, 512> : k_tchain_mf_fwd<KQ, false, 512>)
+                              : (cheb ? k_tchain_mf_fwd<KQ, true, 1024> : k_tchain_mf_fwd<KQ, false, 1024>);
       hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (r != hipSuccess) return r;
       hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);
@@ -1420,8 +1422,10 @@ int tchain_backward(qoc_ctx* c) {
     hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
       // the (P, s, coefficients) of the forward pass are reused: the same polynomial as the states'
-      auto kern = threads <= 512 ? (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 512> : k_tchain_mf_bwd<KQ, false, 512>)
-                                 : (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 1024> : k_tchain_mf_bwd<KQ, false, 1024>);
+      const int mt = tchain_mf_maxt(c->N, c->m, c->nu);
+      auto kern = mt == 256   ? (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 256> : k_tchain_mf_bwd<KQ, false, 256>)
+                  : mt == 512 ? (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 512> : k_tchain_mf_bwd<KQ, false, 512>)
+                              : (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 1024> : k_tchain_mf_bwd<KQ, false, 1024>);
       hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (r != hipSuccess) return r;
       hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);

@@ -621,7 +621,11 @@ __host__ __device__ inline int tchain_mf_waves(int N, int m) { return ((N + 15) 
 // i.e. 256 VGPRs per wave (the KQ = 12 kernels use <= 241).  The former 1024-thread bound capped the waves at 128
 // VGPRs: from KQ = 6 up the formed A rows and the step data spilled to scratch (308 B per lane at KQ = 10), and the
 // reload's vmcnt(0) waited for the next step's prefetch in every slice (~3k cycles per slice at N = 40).
-__host__ __device__ inline int tchain_mf_maxt(int N, int m) { return tchain_mf_waves(N, m) <= 8 ? 512 : 1024; }
+// MAXT = 256 (<= 4 waves, nu <= 2) additionally keeps the generators in registers (REGS in the kernels).
+__host__ __device__ inline int tchain_mf_maxt(int N, int m, int nu) {
+  const int w = tchain_mf_waves(N, m);
+  return w <= 4 && nu <= 2 ? 256 : w <= 8 ? 512 : 1024;
+}
 __host__ inline size_t tchain_mf_lds(int N, int m, int nu) {
   const int KQ = tchain_mf_kq(N), CP = (m + 1) / 2;
   // generators, 2 x (y, y') state buffers, then 16 reduction doubles + 48 for 1/t + 64 per wave (coefficients)
@@ -688,6 +692,31 @@ struct TChainMF {
       const bool ok = rowA < N && 4 * q + kl < N;
       ar[q] = ok ? ar[q] * scale : 0.0;
       ai[q] = ok ? ai[q] * scale : 0.0;
+    }
+  }
+  // Register-resident generators (nu <= 2, 256-thread launch bound: one wave per SIMD, 512 VGPRs): this lane's
+  // A-operand elements of Ã_0..Ã_nu, read from LDS once; form_regs then builds a slice's rows with no LDS traffic.
+  __device__ __forceinline__ void load_gen(int N, int nu, const cx<double>* __restrict__ gen, double (&gr)[3][KQ],
+                                           double (&gi)[3][KQ]) const {
+    const int NN = N * N, rc = min(rowA, N - 1);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        const bool ok = j <= nu && rowA < N && 4 * q + kl < N;
+        const cx<double> v = gen[(size_t)min(j, nu) * NN + rc + N * min(4 * q + kl, N - 1)];
+        gr[j][q] = ok ? v.r : 0.0;
+        gi[j][q] = ok ? v.i : 0.0;
+      }
+  }
+  __device__ __forceinline__ void form_regs(const double (&gr)[3][KQ], const double (&gi)[3][KQ],
+                                            const double (&uk)[TCHAIN_NUMAX], double scale, double (&ar)[KQ],
+                                            double (&ai)[KQ]) const {
+    const double u1 = uk[0] * scale, u2 = uk[1] * scale;  // uk[j >= nu] = 0
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      ar[q] = fma(u2, gr[2][q], fma(u1, gr[1][q], scale * gr[0][q]));
+      ai[q] = fma(u2, gi[2][q], fma(u1, gi[1][q], scale * gi[0][q]));
     }
   }
   // D = A y for this wave's rows and column pair (y from buffer `buf`)
@@ -857,6 +886,9 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
     }
   };
   __syncthreads();
+  constexpr bool REGS = MAXT == 256;  // generators in registers (the dispatch picks MAXT = 256 only for nu <= 2)
+  double gr[3][KQ], gi[3][KQ];
+  if constexpr (REGS) rg.load_gen(N, nu, gen, gr, gi);
   double acc = rg.actD ? yb[(rg.cp * RP + rg.rowD) * 4 + rg.n] : 0.0;
   store(acc, 0);
 #ifdef QOC_PROBE
@@ -876,7 +908,8 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
     tpre_load(stb + kn, ub + (size_t)kn * nu, nu, nx, CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     double ar[KQ], ai[KQ];
-    rg.form(N, nu, gen, st.u, st.scale, ar, ai);
+    if constexpr (REGS) rg.form_regs(gr, gi, st.u, st.scale, ar, ai);
+    else rg.form(N, nu, gen, st.u, st.scale, ar, ai);
     TC_T(s1);
     rg.template step<CHEB>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, st.pi}, acc, st.cl, cw);
     TC_T(s2);
@@ -961,6 +994,9 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
   }
   const bool pen_m = rg.actD && g.pmask && g.pmask[rg.rowD + N * rg.colD];
   __syncthreads();
+  constexpr bool REGS = MAXT == 256;  // see k_tchain_mf_fwd
+  double gr[3][KQ], gi[3][KQ];
+  if constexpr (REGS) rg.load_gen(N, nu, gen, gr, gi);
   int cur = 0;
   double acc = 0.0;
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
@@ -977,7 +1013,8 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
     double xk = pen_m ? tmu * reinterpret_cast<const double*>(Xb + ok_)[rg.n & 1] : 0.0;
     if (srcb && rg.actD) xk += reinterpret_cast<const double*>(srcb + ok_)[rg.n & 1];
     double ar[KQ], ai[KQ];
-    rg.form(N, nu, gen, st.u, st.scale, ar, ai);
+    if constexpr (REGS) rg.form_regs(gr, gi, st.u, st.scale, ar, ai);
+    else rg.form(N, nu, gen, st.u, st.scale, ar, ai);
     rg.template step<CHEB>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, -st.pi}, acc, st.cl, cw);
     if (pen_m || (srcb && rg.actD)) {
       acc += xk;

@@ -61,7 +61,7 @@ void run(int N, int m, int Nt, int B, int P) {
 #endif
 }
 
-template <int KQ, bool CHEB, int MAXT = 512>
+template <int KQ, bool CHEB, int MAXT = 256>
 void run_mf(int N, int m, int Nt, int B, int P) {
   const int nu = 2;
   const size_t NN = (size_t)N * N;
