@@ -10,6 +10,9 @@ from . import systems  # noqa: F401
 from ._lib import QOCError, StaleCacheError  # noqa: F401
 from .api import (  # noqa: F401
     MI355XCache,
+    c2r,
+    generators_from_rhs,
+    r2c,
     compute_pwc_gradient,
     grape_sensitivity,
     propagate,

@@ -145,7 +145,8 @@ class _LazySeries:
         if not 0 <= k < n:
             raise IndexError(k)
         e = self._c.engine
-        return e.state(k, self._s) if self._w == "x" else e.costate(k, self._s)
+        v = e.state(k, self._s) if self._w == "x" else e.costate(k, self._s)
+        return c2r(v) if self._c.real_layout else v
 
     def __iter__(self):
         for k in range(len(self)):
@@ -161,9 +162,16 @@ class MI355XCache:
 
     def __init__(self, A0, x0, u_size, B=1, precision="fp64", device=0, compress=None):
         nu, Nt = u_size
-        x0 = np.asarray(x0, dtype=np.complex128)
+        x0 = np.asarray(x0)
         if x0.ndim == 1:
             x0 = x0[:, None]
+        n = np.shape(A0)[0]
+        # src/gradient_computations.jl:84-87: a real x0 is the complex2real layout (2N rows, re/im interleaved,
+        # src/utils.jl:8-13) of the ODE path; the states are then handed out in that layout too
+        self.real_layout = not np.iscomplexobj(x0)
+        if (self.real_layout and x0.shape[0] != 2 * n) or (not self.real_layout and x0.shape[0] != n):
+            raise ValueError("Error when creating cache, A0 and x0 have incompatiable dimensions")
+        x0 = r2c(x0) if self.real_layout else x0.astype(np.complex128)
         placeholder = [np.zeros_like(np.asarray(A0, dtype=np.complex128)) for _ in range(nu)]
         self.engine = GrapeEngine(A0, placeholder, x0, Nt, B, precision, device)
         self.engine.set_cost_external()
@@ -184,6 +192,27 @@ class MI355XCache:
 
     def series(self, which, seed):
         return _LazySeries(self, which, seed)
+
+    def __getitem__(self, i):
+        """The reference's positional fields (Julia cache[1] = x, cache[2] = λ, cache[3] = dJdu), 0-based here."""
+        return (self.x, self.lam, self.dJdu)[i]
+
+
+def c2r(x):
+    """complex2real (src/utils.jl:8-13): re / im interleaved along the rows, 2N x m."""
+    x = np.asarray(x)
+    out = np.empty((2 * x.shape[0],) + x.shape[1:], dtype=np.float64)
+    out[0::2] = x.real
+    out[1::2] = x.imag
+    return out
+
+
+def r2c(x):
+    """real2complex (src/utils.jl:14-19)."""
+    x = np.asarray(x, dtype=np.float64)
+    if x.shape[0] % 2:
+        raise ValueError("A must have an even number of rows")
+    return x[0::2] + 1j * x[1::2]
 
 
 def setup_grape_cache(A0, x0, u_size, B=1, precision="fp64", device=0, compress=None) -> MI355XCache:
@@ -207,9 +236,10 @@ def propagate(A0, A, u, x0, cache: MI355XCache | None = None):
 def _propagate(A0, A, u, x0, cache: MI355XCache):
     e = cache.engine
     e.set_generators(A0, A)
-    x0 = np.asarray(x0, dtype=np.complex128)
+    x0 = np.asarray(x0)
     if x0.ndim == 1:
         x0 = x0[:, None]
+    x0 = r2c(x0) if not np.iscomplexobj(x0) and x0.shape[0] == 2 * e.N else x0.astype(np.complex128)
     if not np.array_equal(x0, e.x0):
         e.set_x0(x0)
     e.propagate(u)
@@ -235,7 +265,8 @@ def grape_sensitivity(A0, A, dJfinal_dx, u, x0, cache: MI355XCache, dUkdp_order=
             src = np.stack([[np.asarray(dL_dx(e.state(k, b)), dtype=np.complex128) for k in range(e.Nt + 1)]
                             for b in range(B)])
     e.set_costate_source(src)
-    lam = np.stack([np.asarray(dJfinal_dx(e.state(-1, b)), dtype=np.complex128) for b in range(B)])  # :46
+    lam = np.stack([np.asarray(dJfinal_dx(e.state(-1, b)), dtype=np.complex128).reshape(e.N, -1)
+                    for b in range(B)])  # :46
     dJdu = e.grape_sensitivity(u, dUkdp_order, lambda_final=lam)
     if src is not None:
         e.set_costate_source(None)
@@ -253,10 +284,82 @@ def _nsub(Δt, dt):
     return nsub
 
 
-def propagate_pwc(A0, A, x0, u, Δt, cache: MI355XCache | None = None, dt=None):
-    """propagate_pwc (src/gradient_computations.jl:108-128): dx/dt = (A0 + sum_j u_jk A_j) x on
-    [kΔt, (k+1)Δt) with fixed Tsit5 steps dt (default 0.1Δt).  A0, A are the physical generators
-    (-iH, not Δt-scaled) in place of the reference's `f` closure; returns the slice-boundary states."""
+def generators_from_rhs(f, n, nu):
+    """The complex generators behind a reference right-hand side f(dx, x, p, t) (the examples' setup_dxdt: dx/dt
+    of one state column in the complex2real layout, p = u_k): sampled on the 2n basis vectors at p = 0 and
+    p = e_j.  Raises ValueError unless f is x -> (M0 + sum_j p_j M_j) x for complex matrices M (what
+    wrap_pwc's ODE is on the GRAPE path); the GPU then integrates that ODE."""
+    def call(dx, x, p):  # wrap_pwc passes (dx, x, p, t); Symbolics' in-place builds take (dx, x, p)
+        try:
+            f(dx, x, p, 0.0)
+        except TypeError:
+            f(dx, x, p)
+
+    def real_matrix(p):
+        R = np.zeros((2 * n, 2 * n))
+        for i in range(2 * n):
+            x = np.zeros(2 * n)
+            x[i] = 1.0
+            dx = np.zeros(2 * n)
+            call(dx, x, p)
+            R[:, i] = dx
+        return R
+
+    def to_complex(R):
+        M = R[0::2, 0::2] + 1j * R[1::2, 0::2]
+        if not (np.allclose(R[1::2, 1::2], M.real, rtol=0, atol=1e-14 * max(1.0, np.abs(R).max())) and
+                np.allclose(R[0::2, 1::2], -M.imag, rtol=0, atol=1e-14 * max(1.0, np.abs(R).max()))):
+            raise ValueError("the right-hand side is not a complex-linear map in the complex2real layout")
+        return M
+    R0 = real_matrix(np.zeros(nu))
+    M0 = to_complex(R0)
+    Ms = [to_complex(real_matrix(np.eye(nu)[j]) - R0) for j in range(nu)]
+    rng = np.random.default_rng(0)  # affine in p, linear in x: one random check
+    p, x = rng.standard_normal(nu), rng.standard_normal(2 * n)
+    dx = np.zeros(2 * n)
+    call(dx, x, p)
+    want = c2r((M0 + sum(p[j] * Ms[j] for j in range(nu))) @ r2c(x))
+    if not np.allclose(dx, want, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(want).max())):
+        raise ValueError("the right-hand side is not x -> (A0 + sum_j p_j A_j) x")
+    return M0, Ms
+
+
+class PwcSolution:
+    """What the reference's propagate_pwc returns (an ODESolution saved at [0, tgate]): .t and .u."""
+
+    def __init__(self, t, u):
+        self.t, self.u = t, u
+
+
+def propagate_pwc(*args, **kw):
+    """propagate_pwc (src/gradient_computations.jl:108-128) on the GPU, in both call forms:
+
+    * the reference's, propagate_pwc(f, x0, u, Δt, cache=None; dt): f(dx, x, p, t) the right-hand side on one
+      column in the complex2real layout (examples/models/setup_diffeq_rhs.jl), x0 real 2N x m.  The generators
+      are recovered from f (generators_from_rhs) and the result is the reference's solution object (.u =
+      [x(0), x(tgate)], real layout); the states of every slice are in cache.x;
+    * propagate_pwc(A0, A, x0, u, Δt, cache=None, dt=None) with the physical generators (-iH, not Δt-scaled).
+    dx/dt = (A0 + sum_j u_jk A_j) x on [kΔt, (k+1)Δt) with fixed Tsit5 steps dt (default 0.1Δt)."""
+    if callable(args[0]):
+        f, x0, u, Δt = args[:4]
+        cache = args[4] if len(args) > 4 else kw.pop("cache", None)
+        dt = kw.pop("dt", None)
+        u = np.asarray(u, dtype=np.float64)
+        x0 = np.asarray(x0)
+        if x0.ndim == 1:
+            x0 = x0[:, None]
+        if np.iscomplexobj(x0) or x0.shape[0] % 2:
+            raise ValueError("propagate_pwc(f, x0, ...) takes x0 in the complex2real layout (real, 2N rows)")
+        n = x0.shape[0] // 2
+        A0, A = generators_from_rhs(f, n, u.shape[-2])
+        if cache is None:
+            cache = setup_grape_cache(A0, x0, u.shape[-2:], B=1 if u.ndim == 2 else u.shape[0])
+        xs = _propagate_pwc(A0, A, x0, u, Δt, cache, dt)
+        return PwcSolution([0.0, Δt * u.shape[-1]], [xs[0], xs[-1]])
+    return _propagate_pwc(*args, **kw)
+
+
+def _propagate_pwc(A0, A, x0, u, Δt, cache: MI355XCache | None = None, dt=None):
     u = np.asarray(u, dtype=np.float64)
     if cache is None:
         cache = setup_grape_cache(A0, x0, u.shape[-2:], B=1 if u.ndim == 2 else u.shape[0])
@@ -266,11 +369,29 @@ def propagate_pwc(A0, A, x0, u, Δt, cache: MI355XCache | None = None, dt=None):
                       u, x0, cache)
 
 
-def compute_pwc_gradient(dJfinal_dx, u, Δt, A0, A, cache: MI355XCache, dUkdp_order=2, dt=None, x0=None):
+def compute_pwc_gradient(*args, dUkdp_order=2, dt=None, x0=None, **kw):
     """compute_pwc_gradient (src/gradient_computations.jl:130-169): co-states by the adjoint ODE
     dλ/dt = -A_k^H λ with the same fixed steps, then dJdu[j, k] from expm_jacobian! of order
     dUkdp_order.  dUkdp_order = 0 returns after the co-state sweep, as the reference does (:152).
-    Call after propagate_pwc with the same u (the stale-u check of grape_sensitivity applies)."""
+    Call after propagate_pwc with the same u (the stale-u check of grape_sensitivity applies).
+
+    Call forms: the reference's compute_pwc_gradient(dλdt, dJfinal_dx, u, Δt, A0, A, cache; dUkdp_order, dt),
+    where dλdt(dλ, λ, p, t) is the adjoint right-hand side in the complex2real layout (checked against -A^H
+    of the generators), and compute_pwc_gradient(dJfinal_dx, u, Δt, A0, A, cache, ...)."""
+    if len(args) >= 7 and callable(args[0]) and callable(args[1]):
+        dldt, dJfinal_dx, u, Δt, A0, A, cache = args[:7]
+        n = np.shape(A0)[0]
+        M0, Ms = generators_from_rhs(dldt, n, len(A))
+        tol = 1e-12 * max(1.0, np.abs(np.asarray(A0)).max())
+        if not (np.allclose(M0, -np.asarray(A0).conj().T, atol=tol) and
+                all(np.allclose(Mj, -np.asarray(a).conj().T, atol=tol) for Mj, a in zip(Ms, A))):
+            raise ValueError("dλdt is not the adjoint of the generators A0, A (dλ/dt = -A(u)^H λ)")
+    else:
+        dJfinal_dx, u, Δt, A0, A, cache = args[:6]
+    return _compute_pwc_gradient(dJfinal_dx, u, Δt, A0, A, cache, dUkdp_order, dt, x0)
+
+
+def _compute_pwc_gradient(dJfinal_dx, u, Δt, A0, A, cache: MI355XCache, dUkdp_order=2, dt=None, x0=None):
     e = cache.engine
     nsub = _nsub(Δt, dt)
     if (getattr(e, "prop_method", "expm"), getattr(e, "nsub", None)) != ("tsit5", nsub):

@@ -144,3 +144,36 @@ def test_compress_problem_rejects_coupling_generators():
     v = ((range(0, 9, 2), [0, 3]), (range(1, 9, 2), [1, 2]))
     with pytest.raises(ValueError, match="couple"):
         S.compress_problem(prob, v)
+
+
+def test_generators_recovered_from_reference_rhs_closures():
+    """propagate_pwc(f, ...) takes the reference's right-hand side closure (examples/models/setup_diffeq_rhs.jl:
+    rhs = (A0 + sum u_k A_k) x in the complex2real layout); the generators are recovered exactly, and
+    anything that is not such a map is refused."""
+    from qoc_amd import c2r, generators_from_rhs, r2c
+    rng = np.random.default_rng(3)
+    n = 5
+    A0 = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    A = [rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n)) for _ in range(2)]
+
+    def dxdt(dx, x, p, t):
+        dx[:] = c2r((A0 + p[0] * A[0] + p[1] * A[1]) @ r2c(x))
+    M0, Ms = generators_from_rhs(dxdt, n, 2)
+    assert np.abs(M0 - A0).max() < 1e-14 and all(np.abs(Mj - Aj).max() < 1e-14 for Mj, Aj in zip(Ms, A))
+
+    def dldt3(dl, l, p):  # Symbolics' in-place signature, adjoint equation
+        dl[:] = c2r(-(A0 + p[0] * A[0] + p[1] * A[1]).conj().T @ r2c(l))
+    M0, _ = generators_from_rhs(dldt3, n, 2)
+    assert np.abs(M0 + A0.conj().T).max() < 1e-14
+    x = rng.standard_normal((2 * n, 3))
+    assert np.array_equal(c2r(r2c(x)), x)
+
+    def conj_rhs(dx, x, p, t):  # x -> conj(x): real-linear, not complex-linear
+        dx[:] = c2r(np.conj(r2c(x)))
+    with pytest.raises(ValueError):
+        generators_from_rhs(conj_rhs, n, 2)
+
+    def quad(dx, x, p, t):  # not affine in p
+        dx[:] = c2r((A0 + p[0] ** 2 * A[0]) @ r2c(x))
+    with pytest.raises(ValueError):
+        generators_from_rhs(quad, n, 2)

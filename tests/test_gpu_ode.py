@@ -125,6 +125,44 @@ def test_reference_shaped_propagate_pwc_and_gradient(built_lib):
         Q.propagate_pwc(A0, A, prob.x0, u, Δt, cache, dt=0.03)
 
 
+def test_reference_call_form_with_rhs_closures_and_real_layout(built_lib):
+    """test/test_gradient_computation.jl:44-51 and examples/zz_coupling_ipopt_diffeq.jl:34-52, as written there:
+    cache = setup_grape_cache(A0, c2r(x0), (2, Nt)); sol = propagate_pwc(dxdt, c2r(x0), u, Δt, cache; dt);
+    compute_pwc_gradient(dλdt, dJfinal_dx, u, Δt, A0, [A1, A2], cache; dUkdp_order=3, dt), with dxdt / dλdt the
+    right-hand-side closures of examples/models/setup_diffeq_rhs.jl in the complex2real layout.  Against the
+    oracle on the same problem; states come back in the real layout (cache[0] is the reference's cache[1])."""
+    import qoc_amd as Q
+    from qoc_amd import systems as S
+    Δt = 0.1
+    prob = S.zz_problem(20, tgate=2.0)
+    A0 = prob.A0 / Δt
+    A = [a / Δt for a in prob.A]
+    u = S.zz_controls(1, 20, 2.0, seed=8)[0]
+
+    def dxdt(dx, x, p, t):
+        dx[:] = Q.c2r((A0 + p[0] * A[0] + p[1] * A[1]) @ Q.r2c(x))
+
+    def dldt(dl, l, p, t):
+        dl[:] = Q.c2r(-(A0 + p[0] * A[0] + p[1] * A[1]).conj().T @ Q.r2c(l))
+    x0r = Q.c2r(prob.x0)
+    cache = Q.setup_grape_cache(A0, x0r, u.shape)
+    sol = Q.propagate_pwc(dxdt, x0r, u, Δt, cache, dt=0.2 * Δt)
+    _, dJf = Q.setup_infidelity(prob.x_target, prob.n)
+    g = Q.compute_pwc_gradient(dldt, dJf, u, Δt, A0, A, cache, dUkdp_order=3, dt=0.2 * Δt)
+    _, gr = O.grape_eval_ode(prob.A0, prob.A, u, prob.x0, prob.x_target, prob.n, order=3, nsub=5)
+    xs = O.propagate_pwc_ode(prob.A0, prob.A, u, prob.x0, nsub=5)
+    assert sol.u[-1].shape == x0r.shape and not np.iscomplexobj(sol.u[-1])
+    assert np.abs(Q.r2c(sol.u[-1]) - xs[-1]).max() < 1e-12
+    assert np.abs(Q.r2c(cache[0][7]) - xs[7]).max() < 1e-12
+    assert np.linalg.norm(g - gr) / np.linalg.norm(gr) <= 1e-10
+    def wrong(dl, l, p, t):  # +A(u)^H: the adjoint equation with the sign flipped (for skew-Hermitian
+        dl[:] = Q.c2r((A0 + p[0] * A[0] + p[1] * A[1]).conj().T @ Q.r2c(l))  # generators dxdt itself is right)
+    with pytest.raises(ValueError, match="adjoint"):
+        Q.compute_pwc_gradient(wrong, dJf, u, Δt, A0, A, cache, dUkdp_order=3, dt=0.2 * Δt)
+    with pytest.raises(ValueError, match="incompatiable"):  # real x0 must have 2N rows (:84-87)
+        Q.setup_grape_cache(A0, np.ones((prob.N, 4)), u.shape)
+
+
 def test_tsit5_unsupported_configurations(built_lib, monkeypatch):
     from qoc_amd import GrapeEngine, QOCError, systems
     prob = systems.zz_problem(10)
