@@ -286,6 +286,10 @@ def main():
 
     # ---- roofline of each kernel, dominant one reported ----
     per_launch = {k: (ms / max(n, 1)) for k, (ms, n) in phases.items()}
+    # launches per step: the overlapped backward runs the chain and the gradient in slice ranges (several
+    # launches per step); per-launch work = per-step work / launches per step
+    lps = {k: max(n, 1) / K for k, (ms, n) in phases.items()}
+    per_step = {k: per_launch[k] * lps[k] for k in per_launch}
     hist_launch = {k: v / K for k, v in hist.items()}
     peak = PEAK_TFLOPS[prob.precision]
     info1 = eng.info()
@@ -337,10 +341,10 @@ def main():
         }
     kern = {}
     for k, (bound, work, unit, pk) in models.items():
-        t = per_launch[k] / 1e3
+        t = per_step[k] / 1e3
         ach = work / t if t > 0 else 0.0
-        kern[k] = {"ms_per_launch": per_launch[k], "bound": bound, "achieved": ach, "unit": unit, "peak": pk,
-                   "frac": ach / pk}
+        kern[k] = {"ms_per_launch": per_launch[k], "launches_per_step": lps[k], "bound": bound, "achieved": ach,
+                   "unit": unit, "peak": pk, "frac": ach / pk}
     names = {"k_expm": "k_expm_rr", "k_chain_fwd": "k_chain_fwd", "k_chain_bwd": "k_chain_bwd", "k_grad": "k_grad_rr"}
     if taylor:
         mf = prob.precision == "fp64"
@@ -350,15 +354,18 @@ def main():
             # serial Taylor terms of one seed per launch and the time each takes (the chains' critical path)
             kern[k]["kernel"] = names[k]
             kern[k]["terms_per_seed"] = terms / K / B
-            kern[k]["ns_per_serial_term"] = per_launch[k] * 1e6 / max(terms / K / B, 1e-9)
-        dom = max(("k_chain_fwd", "k_chain_bwd", "k_grad"), key=lambda k: per_launch[k])
+            kern[k]["ns_per_serial_term"] = per_step[k] * 1e6 / max(terms / K / B, 1e-9)
+        dom = max(("k_chain_fwd", "k_chain_bwd", "k_grad"), key=lambda k: per_step[k])
         roof = {"kernel": names[dom], "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
                 "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
                 "traffic": traffic_all.get(names[dom]), "ms_per_launch": kern[dom]["ms_per_launch"],
+                "launches_per_step": lps[dom],
                 "note": ("latency-bound serial recurrence (one workgroup per seed, Taylor terms in sequence): "
-                         "achieved = executed matvec flops / launch time")}
+                         "achieved = executed matvec flops / launch time"
+                         + ("; the backward chain runs in slice ranges, each range's gradient overlapped with "
+                            "the next range" if lps.get("k_chain_bwd", 1) > 1 else ""))}
     elif not large:
-        dom = max(per_launch, key=per_launch.get)
+        dom = max(per_step, key=per_step.get)
         # the exponential phase runs the register-resident kernels (k_expm_rr: T12 / Paterson-Stockmeyer)
         # unless QOC_EXPM_LDS or QOC_EXPM_PADE selects the LDS kernel k_expm
         lds_expm = info1.get("expm") != "taylor_rr"  # the reference's Padé or the LDS Paterson-Stockmeyer: k_expm

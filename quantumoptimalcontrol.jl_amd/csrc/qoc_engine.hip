@@ -43,6 +43,11 @@ struct qoc_ctx {
   int dev = 0, N = 0, m = 0, nu = 0, Nt = 0, B = 0, prec = QOC_FP64;
   size_t esz = 16;  // bytes per complex element on device
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;        // gradient ranges overlapped with the backward chain
+  std::vector<hipEvent_t> sync_ev;      // cross-stream ordering events (no timing)
+  int bwd_chunks = 4;                   // slice ranges of the overlapped backward chain (1: not overlapped)
+  double bwd_last_frac = 0.5;           // last range's length relative to the others
+  int bwd_prio = 0;                     // bit 0: s_setprio in the chain; bit 1: low-priority gradient stream
   void* d_A = nullptr;    // (nu+1) x N*N
   void* d_x0 = nullptr;   // N*m or B*N*m
   int x0_per_seed = 0;
@@ -460,15 +465,15 @@ hipEvent_t take_event(qoc_ctx* c) {
 }
 
 // RAII-less bracket: mark_begin returns the index of the pending mark, mark_end records its stop event.
-int mark_begin(qoc_ctx* c, int phase) {
+int mark_begin(qoc_ctx* c, int phase, hipStream_t s = nullptr) {
   if (!c->profiling) return -1;
   qoc_ctx::Mark m{phase, take_event(c), take_event(c)};
-  (void)hipEventRecord(m.a, c->stream);
+  (void)hipEventRecord(m.a, s ? s : c->stream);
   c->marks.push_back(m);
   return (int)c->marks.size() - 1;
 }
-void mark_end(qoc_ctx* c, int idx) {
-  if (idx >= 0) (void)hipEventRecord(c->marks[idx].b, c->stream);
+void mark_end(qoc_ctx* c, int idx, hipStream_t s = nullptr) {
+  if (idx >= 0) (void)hipEventRecord(c->marks[idx].b, s ? s : c->stream);
 }
 
 template <typename T>
@@ -476,7 +481,7 @@ int frechet_grad(qoc_ctx* c, double* d_dJdu);
 template <typename T>
 int grad_gemm_o3(qoc_ctx* c, double* d_dJdu);
 template <typename T>
-int grad_rr_o3(qoc_ctx* c, double* d_dJdu);
+int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk);
 
 template <typename T>
 int ode_forward(qoc_ctx* c);
@@ -485,7 +490,10 @@ int ode_adjoint(qoc_ctx* c);
 template <typename T>
 int tchain_forward(qoc_ctx* c);
 template <typename T>
-int tchain_backward(qoc_ctx* c);
+int tchain_backward(qoc_ctx* c, int k_lo = 0, int k_hi = -1);
+template <typename T>
+int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu);
+bool tchain_mf(const qoc_ctx* c);
 
 template <typename T>
 int run_forward(qoc_ctx* c) {
@@ -523,6 +531,7 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
     int r = ode_adjoint<T>(c);
     if (r) return r;
   } else if (c->chain_mode == 1) {
+    if (order == 3 && c->grad_rr && c->bwd_chunks > 1 && c->Nt >= 64 && tchain_mf(c)) return tchain_backward_overlapped<T>(c, d_dJdu);
     int r = tchain_backward<T>(c);
     if (r) return r;
   } else {
@@ -549,7 +558,7 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
   }
   if (order == 3 && c->grad_rr) {
     mk = mark_begin(c, 3);
-    int r = grad_rr_o3<T>(c, d_dJdu);
+    int r = grad_rr_o3<T>(c, d_dJdu, c->stream, 0, c->Nt);
     mark_end(c, mk);
     return r;
   }
@@ -1099,11 +1108,11 @@ int grad_gemm_o3(qoc_ctx* c, double* d_dJdu) {
 // Fused order-3 gradient (qoc_grad_rr.hpp): k_grad_rr_q (co-state side -> W0, W1 in the state layout)
 // then k_grad_rr_p (state side + contraction -> dJdu).  Persistent grids of 4-wave workgroups.
 template <typename T, int NT, int KS, int NU>
-int grad_rr_launch(qoc_ctx* c, double* d_dJdu) {
+int grad_rr_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk) {
   using G = GradRR<T, NT>;
   const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
   const size_t lds = G::lds_bytes(N, NU);
-  const long long units = (long long)B * Nt, ntiles = (units + 16 / m - 1) / (16 / m);
+  const long long units = (long long)B * nk, ntiles = (units + 16 / m - 1) / (16 / m);
   const int per_cu = lds <= 80 * 1024 ? 2 : 1;
   const int grid = (int)std::max<long long>(1, std::min<long long>((ntiles + 3) / 4, (long long)c->ncu * per_cu));
   const size_t bufN = (size_t)N * ((size_t)B * (Nt + 1) * m);
@@ -1111,10 +1120,10 @@ int grad_rr_launch(qoc_ctx* c, double* d_dJdu) {
   cx<T>* W1 = W0 + bufN;
   HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_q<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_p<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((k_grad_rr_q<T, NT, KS, NU>), dim3(grid), dim3(256), lds, c->stream, N, m, Nt, B,
+  hipLaunchKernelGGL((k_grad_rr_q<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
                      (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_L, W0, W1);
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL((k_grad_rr_p<T, NT, KS, NU>), dim3(grid), dim3(256), lds, c->stream, N, m, Nt, B,
+  hipLaunchKernelGGL((k_grad_rr_p<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
                      (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, (const cx<T>*)W0,
                      (const cx<T>*)W1, d_dJdu);
   HIPCHK(c, hipGetLastError());
@@ -1122,27 +1131,27 @@ int grad_rr_launch(qoc_ctx* c, double* d_dJdu) {
 }
 
 template <typename T, int NT, int NU>
-int grad_rr_nt(qoc_ctx* c, double* d_dJdu) {
+int grad_rr_nt(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk) {
   const int ks = sizeof(T) == 8 ? (c->N + 3) / 4 : 4 * NT;
   if constexpr (sizeof(T) == 8) {
-    if (ks == 4 * NT - 3) return grad_rr_launch<T, NT, 4 * NT - 3, NU>(c, d_dJdu);
-    if (ks == 4 * NT - 2) return grad_rr_launch<T, NT, 4 * NT - 2, NU>(c, d_dJdu);
-    if (ks == 4 * NT - 1) return grad_rr_launch<T, NT, 4 * NT - 1, NU>(c, d_dJdu);
+    if (ks == 4 * NT - 3) return grad_rr_launch<T, NT, 4 * NT - 3, NU>(c, d_dJdu, st, k0, nk);
+    if (ks == 4 * NT - 2) return grad_rr_launch<T, NT, 4 * NT - 2, NU>(c, d_dJdu, st, k0, nk);
+    if (ks == 4 * NT - 1) return grad_rr_launch<T, NT, 4 * NT - 1, NU>(c, d_dJdu, st, k0, nk);
   }
-  return grad_rr_launch<T, NT, 4 * NT, NU>(c, d_dJdu);
+  return grad_rr_launch<T, NT, 4 * NT, NU>(c, d_dJdu, st, k0, nk);
 }
 
 template <typename T>
-int grad_rr_o3(qoc_ctx* c, double* d_dJdu) {
+int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk) {
   const int NT = (c->N + 15) / 16;
   if (c->nu == 1) {
-    if (NT == 1) return grad_rr_nt<T, 1, 1>(c, d_dJdu);
-    if (NT == 2) return grad_rr_nt<T, 2, 1>(c, d_dJdu);
-    return grad_rr_nt<T, 3, 1>(c, d_dJdu);
+    if (NT == 1) return grad_rr_nt<T, 1, 1>(c, d_dJdu, st, k0, nk);
+    if (NT == 2) return grad_rr_nt<T, 2, 1>(c, d_dJdu, st, k0, nk);
+    return grad_rr_nt<T, 3, 1>(c, d_dJdu, st, k0, nk);
   }
-  if (NT == 1) return grad_rr_nt<T, 1, 2>(c, d_dJdu);
-  if (NT == 2) return grad_rr_nt<T, 2, 2>(c, d_dJdu);
-  return grad_rr_nt<T, 3, 2>(c, d_dJdu);
+  if (NT == 1) return grad_rr_nt<T, 1, 2>(c, d_dJdu, st, k0, nk);
+  if (NT == 2) return grad_rr_nt<T, 2, 2>(c, d_dJdu, st, k0, nk);
+  return grad_rr_nt<T, 3, 2>(c, d_dJdu, st, k0, nk);
 }
 
 // Exact gradient (QOC_DUKDP_EXACT): one Fréchet derivative per slice from the 2N x 2N block exponential
@@ -1332,6 +1341,8 @@ TChainArgs tchain_args(qoc_ctx* c) {
   g.src = c->src_on ? c->d_src : nullptr;
   g.tcoef = c->d_tcoef;
   g.sc = sectors(c);
+  g.k_lo = 0;
+  g.k_hi = c->Nt;
   return g;
 }
 
@@ -1413,9 +1424,14 @@ int tchain_forward(qoc_ctx* c) {
 }
 
 template <typename T>
-int tchain_backward(qoc_ctx* c) {
-  const TChainArgs g = tchain_args(c);
+int tchain_backward(qoc_ctx* c, int k_lo, int k_hi) {
+  TChainArgs g = tchain_args(c);
   if (tchain_mf(c)) {
+    if (k_hi >= 0) {  // a range of slices (tchain_backward_overlapped)
+      g.k_lo = k_lo;
+      g.k_hi = k_hi;
+      g.prio = c->bwd_prio & 1;
+    }
     const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
     const int threads = 64 * tchain_mf_waves(c->N, c->m);
     int mk = mark_begin(c, 2);
@@ -1448,6 +1464,47 @@ int tchain_backward(qoc_ctx* c) {
   });
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_bwd launch: %s", hipGetErrorString(e));
+  return QOC_OK;
+}
+
+// Backward chain in slice ranges with the gradient of each finished range on a second stream: the order-3
+// gradient of slices [k_lo, k_hi) needs only x_k and λ_{k+1}, so it runs while the chain works on the
+// next range (lower k).  The chain's workgroup (3 waves, ~84 KB LDS, <= 264 VGPRs at N = 40) leaves room on
+// each CU for one gradient workgroup, whose waves take the chain's MFMA idle cycles.  Chunk boundaries are
+// uniform in k except the last (exposed) range, bwd_last_frac of a uniform one.
+template <typename T>
+int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu) {
+  const int Nt = c->Nt, S = std::min(c->bwd_chunks, std::max(1, Nt / 32));  // ranges of >= ~32 slices
+  if (!c->stream2) {
+    int lo = 0, hi = 0;
+    HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(c, hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, (c->bwd_prio & 2) ? lo : 0));
+  }
+  while ((int)c->sync_ev.size() < S + 2) {
+    hipEvent_t e;
+    HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->sync_ev.push_back(e);
+  }
+  // k boundaries: kb[0] = Nt > kb[1] > ... > kb[S] = 0; the last range is shorter
+  std::vector<int> kb(S + 1);
+  const double last = std::max(0.05, std::min(1.0, c->bwd_last_frac)), w = Nt / (S - 1 + last);
+  for (int i = 0; i <= S; ++i) kb[i] = std::max(0, Nt - (int)std::lround(i * w));
+  kb[S] = 0;
+  HIPCHK(c, hipEventRecord(c->sync_ev[S], c->stream));  // stream2 starts after everything queued so far
+  HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[S], 0));
+  for (int i = 0; i < S; ++i) {
+    if (kb[i + 1] >= kb[i]) continue;
+    int r = tchain_backward<T>(c, kb[i + 1], kb[i]);
+    if (r) return r;
+    HIPCHK(c, hipEventRecord(c->sync_ev[i], c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[i], 0));
+    const int mk = mark_begin(c, 3, c->stream2);
+    r = grad_rr_o3<T>(c, d_dJdu, c->stream2, kb[i + 1], kb[i] - kb[i + 1]);
+    mark_end(c, mk, c->stream2);
+    if (r) return r;
+  }
+  HIPCHK(c, hipEventRecord(c->sync_ev[S + 1], c->stream2));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->sync_ev[S + 1], 0));
   return QOC_OK;
 }
 
@@ -1742,6 +1799,9 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
                 : (getenv("QOC_EXPM_LDS") && atoi(getenv("QOC_EXPM_LDS")) != 0)   ? 2
                                                                                    : 1;
   c->ode_kernel = (getenv("QOC_ODE_LDS") && atoi(getenv("QOC_ODE_LDS")) != 0) ? 1 : 0;
+  if (getenv("QOC_BWD_CHUNKS")) c->bwd_chunks = std::max(1, atoi(getenv("QOC_BWD_CHUNKS")));
+  if (getenv("QOC_BWD_LAST")) c->bwd_last_frac = atof(getenv("QOC_BWD_LAST"));
+  if (getenv("QOC_BWD_PRIO")) c->bwd_prio = atoi(getenv("QOC_BWD_PRIO"));
   hipMemset(c->d_L, 0, (size_t)B * (Nt + 1) * Nm * c->esz);
   *out = c;
   return QOC_OK;
@@ -1767,6 +1827,11 @@ void qoc_destroy(qoc_ctx* c) {
     hipEventDestroy(m.b);
   }
   for (auto e : c->event_pool) hipEventDestroy(e);
+  for (auto e : c->sync_ev) hipEventDestroy(e);
+  if (c->stream2) {
+    hipStreamSynchronize(c->stream2);
+    hipStreamDestroy(c->stream2);
+  }
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }

@@ -212,12 +212,15 @@ struct GradTile {
   bool ok;
   size_t bx, bl;  // x_k and λ_{k+1} column (c % m) offsets in the (Nt+1)-block state layout
 };
-__device__ __forceinline__ GradTile grad_tile(long long tile, int lane, int N, int m, int Nt, long long units) {
+// The units are the slices k0 .. k0+nk-1 of every seed (units = B nk); `unit` is the global b Nt + k.
+__device__ __forceinline__ GradTile grad_tile(long long tile, int lane, int N, int m, int Nt, int k0, int nk,
+                                              long long units) {
   GradTile g;
   const int c = lane & 15, upt = 16 / m;
-  g.unit = tile * upt + c / m;
-  g.ok = g.unit < units;
-  const long long un = g.ok ? g.unit : 0, b = un / Nt, k = un % Nt;
+  const long long ul = tile * upt + c / m;
+  g.ok = ul < units;
+  const long long un = g.ok ? ul : 0, b = un / nk, k = k0 + un % nk;
+  g.unit = b * Nt + k;
   g.bx = ((size_t)(b * (Nt + 1) + k) * m + c % m) * N;
   g.bl = g.bx + (size_t)m * N;
   return g;
@@ -268,7 +271,7 @@ __device__ __forceinline__ void grad_store(cx<T>* __restrict__ dst, size_t base,
 // Co-state side: Q1 = X^H λ, Q2 = X^H Q1 -> W0 = λ + Q1/2 + Q2/6, W1 = λ/2 + Q1/6, written in the
 // state layout (W0, W1 buffers shaped like X).
 template <typename T, int NT, int KS, int NU>
-__global__ __launch_bounds__(256, 2) void k_grad_rr_q(int N, int m, int Nt, int B, const cx<T>* __restrict__ Agen,
+__global__ __launch_bounds__(256, 2) void k_grad_rr_q(int N, int m, int Nt, int B, int k0, int nk, const cx<T>* __restrict__ Agen,
                                                       const double* __restrict__ u, const cx<T>* __restrict__ L,
                                                       cx<T>* __restrict__ W0, cx<T>* __restrict__ W1) {
   using G = GradRR<T, NT>;
@@ -279,12 +282,12 @@ __global__ __launch_bounds__(256, 2) void k_grad_rr_q(int N, int m, int Nt, int 
   T* Gr = reinterpret_cast<T*>(smem);
   T* Gi = Gr + (size_t)(NU + 1) * N * G::ldp(N);
   grad_gens_to_lds<T, NT>(N, NU, Agen, Gr, Gi);
-  const long long units = (long long)B * Nt, ntiles = (units + 16 / m - 1) / (16 / m);
+  const long long units = (long long)B * nk, ntiles = (units + 16 / m - 1) / (16 / m);
   for (long long tile = (long long)blockIdx.x * nw + wave; tile < ntiles; tile += (long long)gridDim.x * nw) {
-    const GradTile g = grad_tile(tile, lane, N, m, Nt, units);
+    const GradTile g = grad_tile(tile, lane, N, m, Nt, k0, nk, units);
     double uj[NU];
 #pragma unroll
-    for (int j = 0; j < NU; ++j) uj[j] = u[(g.ok ? g.unit : 0) * NU + j];
+    for (int j = 0; j < NU; ++j) uj[j] = u[g.unit * NU + j];
     Own Lam, Q1, Q2;
     grad_load<T, NT>(L, g.bl, g.ok, N, Lam, lane);
     G::template xmul<KS, NU, true>(N, Gr, Gi, uj, Lam, Q1, lane);
@@ -303,7 +306,7 @@ __global__ __launch_bounds__(256, 2) void k_grad_rr_q(int N, int m, int Nt, int 
 
 // State side and contraction: dJdu = Re[<W0, A_j x> + <W1, A_j P1> + <λ/6, A_j P2>], P1 = X x, P2 = X P1.
 template <typename T, int NT, int KS, int NU>
-__global__ __launch_bounds__(256, 2) void k_grad_rr_p(int N, int m, int Nt, int B, const cx<T>* __restrict__ Agen,
+__global__ __launch_bounds__(256, 2) void k_grad_rr_p(int N, int m, int Nt, int B, int k0, int nk, const cx<T>* __restrict__ Agen,
                                                       const double* __restrict__ u, const cx<T>* __restrict__ X,
                                                       const cx<T>* __restrict__ L, const cx<T>* __restrict__ W0,
                                                       const cx<T>* __restrict__ W1, double* __restrict__ dJdu) {
@@ -315,13 +318,13 @@ __global__ __launch_bounds__(256, 2) void k_grad_rr_p(int N, int m, int Nt, int 
   T* Gr = reinterpret_cast<T*>(smem);
   T* Gi = Gr + (size_t)(NU + 1) * N * G::ldp(N);
   grad_gens_to_lds<T, NT>(N, NU, Agen, Gr, Gi);
-  const long long units = (long long)B * Nt, ntiles = (units + 16 / m - 1) / (16 / m);
+  const long long units = (long long)B * nk, ntiles = (units + 16 / m - 1) / (16 / m);
   for (long long tile = (long long)blockIdx.x * nw + wave; tile < ntiles; tile += (long long)gridDim.x * nw) {
-    const GradTile g = grad_tile(tile, lane, N, m, Nt, units);
+    const GradTile g = grad_tile(tile, lane, N, m, Nt, k0, nk, units);
     double uj[NU], sj[NU], s2[NU];
 #pragma unroll
     for (int j = 0; j < NU; ++j) {
-      uj[j] = u[(g.ok ? g.unit : 0) * NU + j];
+      uj[j] = u[g.unit * NU + j];
       sj[j] = 0.0;
       s2[j] = 0.0;
     }

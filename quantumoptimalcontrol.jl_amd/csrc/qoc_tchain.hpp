@@ -229,6 +229,8 @@ struct TChainArgs {
   Sectors sc;              // row sectors of a packed state (compress_states)
   const void* src;         // B x (Nt+1) x N x m caller's dL/dx(x_k) added to λ_k (nullptr: none)
   const double* tcoef;     // B x Nt x TCHEB_STRIDE Chebyshev coefficients (Chebyshev variant)
+  int k_lo, k_hi;          // backward MFMA chain: slices k_hi-1 .. k_lo (k_hi < Nt: λ_{k_hi} read from L)
+  int prio;                // raise the chain waves' issue priority (gradient waves share the SIMDs)
 };
 
 // Thread layout of the Taylor-action chains.  Waves split the rows into G blocks of R = 64 / S rows and the
@@ -956,6 +958,7 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
   const TStep* stb = g.steps + (size_t)b * Nt;
   const double tmu = 2.0 * g.mu;
   const cx<double>* srcb = g.src ? (const cx<double>*)g.src + (size_t)b * (Nt + 1) * Nm : nullptr;
+  if (g.prio) __builtin_amdgcn_s_setprio(3);
   C rg;
   rg.setup(N, m);
   for (int e = tid; e < (nu + 1) * NN; e += nthr) {
@@ -966,26 +969,32 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
   const int YB = 2 * 2 * CP * RP * 4;
   for (int e = tid; e < YB; e += nthr) yb[e] = 0.0;
   __syncthreads();
-  // λ_{Nt} = dJfinal/dx(x_N) (+ dL/dx(x_N)) -> buffer 0 and HBM
+  // λ_{Nt} = dJfinal/dx(x_N) (+ dL/dx(x_N)) -> buffer 0 and HBM; a later range of slices starts from the
+  // λ_{k_hi} the previous range stored
+  const int k_lo = g.k_lo, k_hi = g.k_hi;
   for (int o = tid; o < Nm; o += nthr) {
     const int r = o % N, col = o / N;
     cx<double> v;
-    if (g.cost_kind == COST_EXTERNAL) {
+    if (k_hi < Nt) {
+      v = Lb[(size_t)k_hi * Nm + o];
+    } else if (g.cost_kind == COST_EXTERNAL) {
       v = Lb[(size_t)Nt * Nm + o];
     } else {
       const cx<double> cf = lam_coef(g.coef + (size_t)b * 2 * m, g.sc, m, r, col), t = Xt[o];
       v = cx<double>{cf.r * t.r - cf.i * t.i, cf.r * t.i + cf.i * t.r};
     }
-    if (g.pmask && g.pmask[o]) {
-      const cx<double> xv = Xb[(size_t)Nt * Nm + o];
-      v.r += tmu * xv.r;
-      v.i += tmu * xv.i;
+    if (k_hi == Nt) {
+      if (g.pmask && g.pmask[o]) {
+        const cx<double> xv = Xb[(size_t)Nt * Nm + o];
+        v.r += tmu * xv.r;
+        v.i += tmu * xv.i;
+      }
+      if (srcb) {
+        v.r += srcb[(size_t)Nt * Nm + o].r;
+        v.i += srcb[(size_t)Nt * Nm + o].i;
+      }
+      Lb[(size_t)Nt * Nm + o] = v;
     }
-    if (srcb) {
-      v.r += srcb[(size_t)Nt * Nm + o].r;
-      v.i += srcb[(size_t)Nt * Nm + o].i;
-    }
-    Lb[(size_t)Nt * Nm + o] = v;
     const int q = ((col >> 1) * RP + r) * 4 + 2 * (col & 1);
     yb[q] = v.r;
     yb[q + 1] = v.i;
@@ -1001,10 +1010,11 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
   double acc = 0.0;
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
   TPre nx;
-  tpre_load(stb + Nt - 1, ub + (size_t)(Nt - 1) * nu, nu, nx, CHEB ? ceb + (size_t)(Nt - 1) * TCHEB_STRIDE : nullptr);
-  for (int k = Nt - 1; k >= 0; --k) {
+  tpre_load(stb + k_hi - 1, ub + (size_t)(k_hi - 1) * nu, nu, nx,
+            CHEB ? ceb + (size_t)(k_hi - 1) * TCHEB_STRIDE : nullptr);
+  for (int k = k_hi - 1; k >= k_lo; --k) {
     // λ_{k+1} (the previous slice's result) to HBM ahead of this slice's loads (see k_tchain_mf_fwd)
-    if (k < Nt - 1 && rg.actD) reinterpret_cast<double*>(Lb + (size_t)(k + 1) * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = acc;
+    if (k < k_hi - 1 && rg.actD) reinterpret_cast<double*>(Lb + (size_t)(k + 1) * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = acc;
     const TPre st = nx;
     const int kp = max(k - 1, 0);
     tpre_load(stb + kp, ub + (size_t)kp * nu, nu, nx, CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
@@ -1022,7 +1032,7 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
     }
     if (g.pmask || srcb) rg.sync();  // the penalised entries changed after the step's last barrier
   }
-  if (rg.actD) reinterpret_cast<double*>(Lb + rg.rowD + N * rg.colD)[rg.n & 1] = acc;  // λ_0
+  if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)k_lo * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = acc;  // λ_{k_lo}
 }
 
 // Reference-equivalent accounting (the Taylor-action path forms no A_k norm of its own): the Padé (d, s) that

@@ -553,3 +553,34 @@ def test_taylor_action_non_skew_hermitian_generators(built_lib):
         Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
         assert abs(J[b] - Jr) <= 1e-12
         assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
+
+
+@pytest.mark.parametrize("ranges", [("4", "0.5"), ("3", "0.3")])
+def test_overlapped_backward_ranges_are_bit_identical(built_lib, monkeypatch, ranges):
+    """The backward chain in slice ranges with each range's gradient on a second stream (default for the
+    MFMA chains, Nt >= 64) gives bit-identical J, dJ/du and co-states to the single-launch backward
+    (QOC_BWD_CHUNKS=1), with a state penalty and a ragged Nt, and matches the oracle."""
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=10, Nt=131)
+    u = systems.cavity_controls(3, prob.Nt, seed=17)
+    pen = ([3, 7], [0], 0.2)
+    out = []
+    for chunks in ("1",) + (ranges[0],):
+        monkeypatch.setenv("QOC_BWD_CHUNKS", chunks)
+        monkeypatch.setenv("QOC_BWD_LAST", ranges[1])
+        e = _engine(prob, 3, chain="taylor")
+        e.set_state_penalty(*pen)
+        e.set_profiling(True)
+        J = e.propagate(u)
+        g = e.grape_sensitivity(u, 3)
+        launches = e.phase_times()["k_chain_bwd"][1]
+        lam = [e.costate(k, seed=b) for b in range(3) for k in range(prob.Nt + 1)]
+        e.close()
+        out.append((J, g, np.array(lam), launches))
+    assert out[0][3] == 1 and out[1][3] == int(ranges[0])
+    for a, b in zip(out[0][:3], out[1][:3]):
+        assert np.array_equal(a, b)
+    for b in range(3):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3, penalty=pen)
+        assert abs(out[1][0][b] - Jr) <= 1e-12
+        assert np.linalg.norm(out[1][1][b] - gr) / np.linalg.norm(gr) <= 1e-10
