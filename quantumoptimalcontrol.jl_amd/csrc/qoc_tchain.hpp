@@ -171,6 +171,63 @@ __device__ void bessel_j(double rho, int K, double* j) {  // J_0..J_K(ρ)
   for (int k = 0; k <= K; ++k) j[k] /= norm;
 }
 
+// ρ > 2: bessel_j's Miller recurrence in two passes with no array (a per-thread table of J_k lived in scratch):
+// pass 1 gets the normalisation and the number of rescalings R; pass 2 repeats the recurrence, which yields
+// J_t in descending t, i.e. in the order of the tail sum, so P and the coefficients ce[t] (J_0, 2 J_t) come out
+// of the same loop.  Every value goes through the same operations as in bessel_j (the rescalings that would
+// have reached the stored entry, then the division by the norm), so the coefficients are bitwise the same.
+__device__ int cheb_miller(double rho, double tol, double* __restrict__ ce) {
+  constexpr int K = TCHEB_PMAX + 1;
+  int K0 = (int)(rho + 4.0 * cbrt(rho)) + 30;
+  K0 += K0 & 1;
+  double jp = 0.0, jc = 1e-280, norm = 0.0;
+  int R = 0;
+  for (int k = K0; k >= 1; --k) {
+    const double jm = (2.0 * k / rho) * jc - jp;
+    jp = jc;
+    jc = jm;
+    if (((k - 1) & 1) == 0) norm += (k - 1 ? 2.0 : 1.0) * jc;
+    if (fabs(jc) > 1e250) {
+      jc *= 1e-250;
+      jp *= 1e-250;
+      norm *= 1e-250;
+      ++R;
+    }
+  }
+  for (int t = K0; t <= K; ++t) ce[t] = 0.0;  // J_t negligible
+  jp = 0.0;
+  jc = 1e-280;
+  int r = 0, P = 0;
+  bool found = false;
+  double tail = 0.0;
+  for (int k = K0; k >= 1; --k) {
+    const double jm = (2.0 * k / rho) * jc - jp;
+    jp = jc;
+    jc = jm;  // J_{k-1} (unnormalised)
+    const int t = k - 1;
+    const bool big = fabs(jc) > 1e250;
+    if (t <= K) {
+      double v = jc;
+      for (int q = r; q < R; ++q) v *= 1e-250;  // the rescalings at this and later iterations
+      v /= norm;
+      if (!found && t >= 1) {  // smallest P with 2 Σ_{t>P} |J_t| <= tol
+        tail += 2.0 * fabs(v);
+        if (tail > tol) {
+          P = t < TCHEB_PMAX ? t : TCHEB_PMAX;
+          found = true;
+        }
+      }
+      ce[t] = t ? 2.0 * v : v;
+    }
+    if (big) {
+      jc *= 1e-250;
+      jp *= 1e-250;
+      ++r;
+    }
+  }
+  return P;
+}
+
 __global__ void k_tchain_prep_cheb(int nu, long long units, const double* __restrict__ u, const TChainParams prm,
                                    TStep* __restrict__ steps, double* __restrict__ coef,
                                    unsigned long long* __restrict__ terms) {
@@ -188,20 +245,23 @@ __global__ void k_tchain_prep_cheb(int nu, long long units, const double* __rest
     int s = 1;
     if (beta > 25.0) s = (int)ceil(beta / 25.0);  // substeps only beyond ρ = 25 (P <= 58 < TCHEB_PMAX)
     const double rho = beta / s;
-    double j[TCHEB_PMAX + 2];
-    bessel_j(rho, TCHEB_PMAX + 1, j);
-    double tail = 0.0;
-    int P = 0;
-    for (int k = TCHEB_PMAX + 1; k >= 1; --k) {  // smallest P with 2 Σ_{t>P} |J_t| <= tol
-      tail += 2.0 * fabs(j[k]);                 // Σ_{t>=k}
-      if (tail > tol) {
-        P = k < TCHEB_PMAX ? k : TCHEB_PMAX;
-        break;
-      }
-    }
     double* ce = coef + (size_t)e * TCHEB_STRIDE;
-    ce[0] = j[0];
-    for (int k = 1; k <= P; ++k) ce[k] = 2.0 * j[k];
+    int P = 0;
+    if (rho <= 2.0) {
+      double* j = ce;  // J_0..J_K written in place (ascending), then scaled
+      bessel_j(rho, TCHEB_PMAX + 1, j);
+      double tail = 0.0;
+      for (int k = TCHEB_PMAX + 1; k >= 1; --k) {  // smallest P with 2 Σ_{t>P} |J_t| <= tol
+        tail += 2.0 * fabs(j[k]);                 // Σ_{t>=k}
+        if (tail > tol) {
+          P = k < TCHEB_PMAX ? k : TCHEB_PMAX;
+          break;
+        }
+      }
+      for (int k = 1; k <= P; ++k) ce[k] = 2.0 * j[k];
+    } else {
+      P = cheb_miller(rho, tol, ce);
+    }
     const double er = exp(mr);
     steps[e] = TStep{er * cos(mi), er * sin(mi), P, s, 2.0 / beta};
     cnt += (unsigned long long)(P * s);

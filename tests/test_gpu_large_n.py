@@ -153,3 +153,20 @@ def test_synthetic_n256_fp64(built_lib):
     u = systems.synthetic_controls(1, 2, 2, seed=1)
     J, g, info, _ = _run(prob, u, precision="fp64")
     _compare(prob, u, J, g, tol=(1e-11, 1e-9))
+
+
+@pytest.mark.parametrize("sandwich", ["0", "1"])
+def test_order3_gradient_forms(built_lib, monkeypatch, sandwich):
+    """The large-N order-3 gradient in both forms: seven N^2 m-GEMMs through P_a = X^a x and W_a (default for
+    m <= 2N/3), and five products of G = λ x^H (default for m > 2N/3; QOC_GRAD_SANDWICH forces either).
+    fp64, ragged N = 70 with m = 3 and m = N (chunk of 3 slices, ragged last chunk), penalty on."""
+    monkeypatch.setenv("QOC_CHUNK", "3")
+    monkeypatch.setenv("QOC_GRAD_SANDWICH", sandwich)
+    rng = np.random.default_rng(11)
+    for m in (3, 70):
+        prob = _gue_problem(70, m, 5, norm0=1.5, normj=0.5, seed=12 + m)
+        u = rng.uniform(-1, 1, size=(2, 2, prob.Nt))
+        pen = (list(range(60, 70)), list(range(min(m, 4))), 0.3)
+        J, g, info, _ = _run(prob, u, penalty=pen)
+        assert info["path"] == "large_n"
+        _compare(prob, u, J, g, penalty=pen)
