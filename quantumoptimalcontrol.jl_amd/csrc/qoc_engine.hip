@@ -665,6 +665,57 @@ int big_lincomb(qoc_ctx* c, LinArgs a) {
 static const double hTaylorTheta[7] = {0.069933, 0.247240, 0.553491, 0.978345, 1.504147, 2.113468, 2.791345};
 static const double hTaylorTheta32[7] = {0.648322, 1.31065, 2.099345, 2.969587, 3.894655, 4.858047, 5.849147};
 
+// T12 on the GEMM pipeline: Â = A / 2^s, Â2 = Â², A3 = Â2 Â, B_j = x_j0 I + x_j1 Â + x_j2 Â2 + x_j3 A3,
+// A6 = B3 + B4², T12 = B1 + (B2 + A6) A6, then s squarings.  Each B_j comes out of the A3 product's epilogue
+// (B1, B4, B3: its three outputs); B2 is carried as B2 = β B3 + (x_20 I + (x_21 − β x_31) Â + (x_22 − β x_32) Â2)
+// with β = x_23 / x_33, so that B2 + A6 leaves the B4² product's epilogue next to A6 (three addends).
+// Host copy of kT12 (qoc_expm.hpp).
+static const double hT12[4][4] = {
+    {1.0, 0.99999999999276613715098, -0.13243184210109929356121, -0.050548416421727518977426},
+    {5.5174437753406856228547, 1.3093238729673181077940, 0.0043247187525051520919919, 0.0096586056829351321677927},
+    {0.0, 1.3110895450078318461208e-12, 0.097250029534075019542638, 0.0068219250901116764187357},
+    {0.0, 0.13181061013830184015682, 0.020278555405892590793357, 0.0067595184686308635977856}};
+
+template <typename T>
+int t12_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, const Opd& Asrc, const Opd& dest, int ts,
+                   bool count_hist) {
+  const size_t NN = (size_t)N * N, esz = c->esz;
+  auto w = [&](int i) { return mk_opd(ws, (size_t)i * ws_items * NN, esz, (long long)NN); };
+  if (count_hist) c->big_thist[kT12Row * 64 + std::min(ts, 63)] += cnt;
+  const double sc = std::ldexp(1.0, -ts), (*x)[4] = hT12, beta = x[1][3] / x[2][3];
+  int r;
+  GemmArgs g = gemm_args(N, N, N, cnt);  // Â2 -> w1
+  g.A = Asrc; g.B = Asrc; g.C1 = w(1); g.alpha1 = sc * sc;
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  g = gemm_args(N, N, N, cnt);  // A3 = sc Â2 A:  B1 -> w2, B4 -> w3, B3 -> w4
+  g.A = w(1); g.B = Asrc;
+  g.nY = 2; g.Y[0] = Asrc; g.Y[1] = w(1);
+  g.C1 = w(2); g.alpha1 = x[0][3] * sc; g.w1[0] = x[0][1] * sc; g.w1[1] = x[0][2]; g.gamma1 = x[0][0];
+  g.C2 = w(3); g.alpha2 = x[3][3] * sc; g.w2[0] = x[3][1] * sc; g.w2[1] = x[3][2]; g.gamma2 = x[3][0];
+  g.C3 = w(4); g.alpha3 = x[2][3] * sc; g.w3[0] = x[2][1] * sc; g.w3[1] = x[2][2]; g.gamma3 = x[2][0];
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  g = gemm_args(N, N, N, cnt);  // B4²:  A6 = B4² + B3 -> w5,  B2 + A6 -> w6
+  g.A = w(3); g.B = w(3);
+  g.nY = 3; g.Y[0] = w(4); g.Y[1] = Asrc; g.Y[2] = w(1);
+  g.C1 = w(5); g.w1[0] = 1.0;
+  g.C2 = w(6); g.alpha2 = 1.0; g.w2[0] = 1.0 + beta; g.w2[1] = (x[1][1] - beta * x[2][1]) * sc;
+  g.w2[2] = x[1][2] - beta * x[2][2]; g.gamma2 = x[1][0];
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  g = gemm_args(N, N, N, cnt);  // T12 = (B2 + A6) A6 + B1
+  g.A = w(6); g.B = w(5); g.C1 = ts == 0 ? dest : w(7);
+  g.nY = 1; g.Y[0] = w(2); g.w1[0] = 1.0;
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  int xb = 7;
+  for (int q = 0; q < ts; ++q) {
+    const int nb = xb == 7 ? 1 : 7;
+    g = gemm_args(N, N, N, cnt);
+    g.A = w(xb); g.B = w(xb); g.C1 = q == ts - 1 ? dest : w(nb);
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+    xb = nb;
+  }
+  return QOC_OK;
+}
+
 // Taylor / Paterson-Stockmeyer exponential on the GEMM pipeline (the large-N analogue of k_expm ALG 1):
 // degree m = 3r + 2 with (r, s) minimising 2 + r + s for the chunk's max norm; every B_i = c I + c' A + c'' A2
 // is added in a GEMM epilogue, so the chunk costs exactly 2 + r + s GEMMs and no element-wise pass.
@@ -683,6 +734,12 @@ int taylor_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, con
       ts = ss;
     }
   }
+  // Degree-12 Taylor in 4 products (the T12 scheme of k_expm_rr, coefficients kT12) when it needs fewer GEMMs:
+  // 4 + s12 with θ12 = 1.5622 in fp32 (tail <= 2^-24) / kTheta12 in fp64.  Synthetic slices (||A||_1 in
+  // (1.3, 2.6]): 5 GEMMs instead of Paterson-Stockmeyer's 6.
+  const double th12 = sizeof(T) == 4 ? 1.562211457125874 : kTheta12;
+  const int s12 = nA > th12 ? (int)std::ceil(std::log2(nA / th12)) : 0;
+  if (4 + s12 < best && !getenv("QOC_BIG_NO_T12")) return t12_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, s12, count_hist);
   if (count_hist) c->big_thist[(tr - 2) * 64 + std::min(ts, 63)] += cnt;
   static const double f[27] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720, 1.0 / 5040, 1.0 / 40320,
                                2.755731922398589e-06, 2.755731922398589e-07, 2.505210838544172e-08,

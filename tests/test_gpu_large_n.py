@@ -170,3 +170,30 @@ def test_order3_gradient_forms(built_lib, monkeypatch, sandwich):
         J, g, info, _ = _run(prob, u, penalty=pen)
         assert info["path"] == "large_n"
         _compare(prob, u, J, g, penalty=pen)
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_large_n_t12_and_paterson_stockmeyer(built_lib, monkeypatch, precision):
+    """The large-N exponential picks the 4-product degree-12 Taylor scheme (histogram row m = 12) whenever it needs
+    fewer GEMMs than Paterson-Stockmeyer (m = 3r+2); QOC_BIG_NO_T12=1 keeps Paterson-Stockmeyer.  Both match the
+    oracle (fp64 bar, or the fp32 tolerance) on norms that need squarings."""
+    from qoc_amd import GrapeEngine
+    monkeypatch.setenv("QOC_CHUNK", "4")
+    rng = np.random.default_rng(31)
+    prob = _gue_problem(72, 4, 6, norm0=2.4, normj=0.6, seed=32)
+    u = rng.uniform(-1, 1, size=(2, 2, prob.Nt))
+    tol = (1e-12, 1e-10) if precision == "fp64" else (1e-4, 1e-3)
+    hists = {}
+    for off in ("0", "1"):
+        if off == "1":
+            monkeypatch.setenv("QOC_BIG_NO_T12", "1")
+        e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2, precision=precision)
+        assert e.info()["path"] == "large_n"
+        e.set_cost_trace(prob.x_target, prob.n)
+        J = e.propagate(u)
+        g = e.grape_sensitivity(u, 3)
+        hists[off] = e.taylor_histogram()
+        e.close()
+        _compare(prob, u, J, g, tol=tol)
+    assert hists["0"] and all(m == 12 for (m, _) in hists["0"]), hists
+    assert hists["1"] and all(m != 12 for (m, _) in hists["1"]), hists
