@@ -228,6 +228,49 @@ __device__ int cheb_miller(double rho, double tol, double* __restrict__ ce) {
   return P;
 }
 
+// ρ <= 2: bessel_j's power series, again without a table.  J_k depends only on k, so the tail sum runs over
+// descending k with each J_k recomputed (its (ρ/2)^k / k! by the same ascending product), and only the P + 1
+// coefficients are written.  Same operations per value as bessel_j, so the same P and coefficients.
+__device__ double bessel_series_k(double h, int k) {
+  double lead = 1.0;
+  for (int q = 1; q <= k; ++q) lead *= h / q;
+  const double h2 = -h * h;
+  double term = lead, sum = lead;
+  for (int m = 1; m < 40 && fabs(term) > 1e-22 * fabs(sum); ++m) {
+    term *= h2 / (m * (double)(m + k));
+    sum += term;
+  }
+  return sum;
+}
+
+__device__ int cheb_series(double rho, double tol, double* __restrict__ ce) {
+  constexpr int K = TCHEB_PMAX + 1;
+  const double h = 0.5 * rho;
+  int kz = K + 1;  // J_k = 0 for k >= kz (bessel_j stops once (ρ/2)^k / k! < 1e-40)
+  double lead = 1.0;
+  for (int k = 1; k <= K; ++k) {
+    lead *= h / k;
+    if (lead < 1e-40) {
+      kz = k;
+      break;
+    }
+  }
+  double tail = 0.0;
+  int P = 0;
+  for (int k = kz - 1; k >= 1; --k) {  // smallest P with 2 Σ_{t>P} |J_t| <= tol
+    tail += 2.0 * fabs(bessel_series_k(h, k));
+    if (tail > tol) {
+      P = k < TCHEB_PMAX ? k : TCHEB_PMAX;
+      break;
+    }
+  }
+  for (int k = 0; k <= P; ++k) {
+    const double v = bessel_series_k(h, k);
+    ce[k] = k ? 2.0 * v : v;
+  }
+  return P;
+}
+
 __global__ void k_tchain_prep_cheb(int nu, long long units, const double* __restrict__ u, const TChainParams prm,
                                    TStep* __restrict__ steps, double* __restrict__ coef,
                                    unsigned long long* __restrict__ terms) {
@@ -248,17 +291,7 @@ __global__ void k_tchain_prep_cheb(int nu, long long units, const double* __rest
     double* ce = coef + (size_t)e * TCHEB_STRIDE;
     int P = 0;
     if (rho <= 2.0) {
-      double* j = ce;  // J_0..J_K written in place (ascending), then scaled
-      bessel_j(rho, TCHEB_PMAX + 1, j);
-      double tail = 0.0;
-      for (int k = TCHEB_PMAX + 1; k >= 1; --k) {  // smallest P with 2 Σ_{t>P} |J_t| <= tol
-        tail += 2.0 * fabs(j[k]);                 // Σ_{t>=k}
-        if (tail > tol) {
-          P = k < TCHEB_PMAX ? k : TCHEB_PMAX;
-          break;
-        }
-      }
-      for (int k = 1; k <= P; ++k) ce[k] = 2.0 * j[k];
+      P = cheb_series(rho, tol, ce);
     } else {
       P = cheb_miller(rho, tol, ce);
     }
