@@ -736,7 +736,7 @@ int taylor_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, con
   }
   // Degree-12 Taylor in 4 products (the T12 scheme of k_expm_rr, coefficients kT12) when it needs fewer GEMMs:
   // 4 + s12 with θ12 = 1.5622 in fp32 (tail <= 2^-24) / kTheta12 in fp64.  Synthetic slices (||A||_1 in
-  // (1.3, 2.6]): 5 GEMMs instead of Paterson-Stockmeyer's 6.
+  // (3.1, 4.2]): 6 GEMMs instead of Paterson-Stockmeyer's 7.
   const double th12 = sizeof(T) == 4 ? 1.562211457125874 : kTheta12;
   const int s12 = nA > th12 ? (int)std::ceil(std::log2(nA / th12)) : 0;
   if (4 + s12 < best && !getenv("QOC_BIG_NO_T12")) return t12_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, s12, count_hist);
