@@ -48,6 +48,7 @@ struct qoc_ctx {
   int bwd_chunks = 4;                   // slice ranges of the overlapped backward chain (1: not overlapped)
   double bwd_last_frac = 0.5;           // last range's length relative to the others
   int bwd_prio = 0;                     // bit 0: s_setprio in the chain; bit 1: low-priority gradient stream
+  int bwd_prestate = 1;                 // 1: P1, P2 of every slice beside the first backward range (k_grad_rr_s)
   void* d_A = nullptr;    // (nu+1) x N*N
   void* d_x0 = nullptr;   // N*m or B*N*m
   int x0_per_seed = 0;
@@ -111,6 +112,8 @@ struct qoc_ctx {
   void* d_AH = nullptr;    // (nu+1) x N*N: [A0^H | A1^H | ...]
   void* d_Cst = nullptr;   // nu N x N: [A1; A2; ...]
   void* d_gws = nullptr;   // 6 x N x B(Nt+1)m
+  void* d_pws = nullptr;   // 2 x N x B(Nt+1)m: P1, P2 of the state-side gradient pass (bwd_prestate)
+  size_t pws_bytes = 0;
   bool grad_gemm = true;
   bool grad_rr = false;  // fused register-resident order-3 gradient (qoc_grad_rr.hpp)
   int* d_ps = nullptr;   // k_expm_rr pass-2 counter + list of Paterson-Stockmeyer units
@@ -481,7 +484,7 @@ int frechet_grad(qoc_ctx* c, double* d_dJdu);
 template <typename T>
 int grad_gemm_o3(qoc_ctx* c, double* d_dJdu);
 template <typename T>
-int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk);
+int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode = 0);
 
 template <typename T>
 int ode_forward(qoc_ctx* c);
@@ -1198,7 +1201,7 @@ int grad_gemm_o3(qoc_ctx* c, double* d_dJdu) {
 // Fused order-3 gradient (qoc_grad_rr.hpp): k_grad_rr_q (co-state side -> W0, W1 in the state layout)
 // then k_grad_rr_p (state side + contraction -> dJdu).  Persistent grids of 4-wave workgroups.
 template <typename T, int NT, int KS, int NU>
-int grad_rr_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk) {
+int grad_rr_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode) {
   using G = GradRR<T, NT>;
   const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
   const size_t lds = G::lds_bytes(N, NU);
@@ -1208,40 +1211,57 @@ int grad_rr_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk) {
   const size_t bufN = (size_t)N * ((size_t)B * (Nt + 1) * m);
   cx<T>* W0 = (cx<T>*)c->d_gws;
   cx<T>* W1 = W0 + bufN;
+  // mode 0: q + p;  1: state side only (k_grad_rr_s -> P1, P2 in d_pws);  2: q + p reading P1, P2
+  cx<T>* P1 = (cx<T>*)c->d_pws;
+  cx<T>* P2 = P1 ? P1 + bufN : nullptr;
+  if (mode == 1) {
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_s<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_grad_rr_s<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
+                       (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, P1, P2);
+    HIPCHK(c, hipGetLastError());
+    return QOC_OK;
+  }
   HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_q<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_p<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL((k_grad_rr_q<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
                      (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_L, W0, W1);
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL((k_grad_rr_p<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
-                     (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, (const cx<T>*)W0,
-                     (const cx<T>*)W1, d_dJdu);
+  if (mode == 2) {
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_p<T, NT, KS, NU, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_grad_rr_p<T, NT, KS, NU, true>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
+                       (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, (const cx<T>*)W0,
+                       (const cx<T>*)W1, d_dJdu, (const cx<T>*)P1, (const cx<T>*)P2);
+  } else {
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_p<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_grad_rr_p<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
+                       (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, (const cx<T>*)W0,
+                       (const cx<T>*)W1, d_dJdu);
+  }
   HIPCHK(c, hipGetLastError());
   return QOC_OK;
 }
 
 template <typename T, int NT, int NU>
-int grad_rr_nt(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk) {
+int grad_rr_nt(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode) {
   const int ks = sizeof(T) == 8 ? (c->N + 3) / 4 : 4 * NT;
   if constexpr (sizeof(T) == 8) {
-    if (ks == 4 * NT - 3) return grad_rr_launch<T, NT, 4 * NT - 3, NU>(c, d_dJdu, st, k0, nk);
-    if (ks == 4 * NT - 2) return grad_rr_launch<T, NT, 4 * NT - 2, NU>(c, d_dJdu, st, k0, nk);
-    if (ks == 4 * NT - 1) return grad_rr_launch<T, NT, 4 * NT - 1, NU>(c, d_dJdu, st, k0, nk);
+    if (ks == 4 * NT - 3) return grad_rr_launch<T, NT, 4 * NT - 3, NU>(c, d_dJdu, st, k0, nk, mode);
+    if (ks == 4 * NT - 2) return grad_rr_launch<T, NT, 4 * NT - 2, NU>(c, d_dJdu, st, k0, nk, mode);
+    if (ks == 4 * NT - 1) return grad_rr_launch<T, NT, 4 * NT - 1, NU>(c, d_dJdu, st, k0, nk, mode);
   }
-  return grad_rr_launch<T, NT, 4 * NT, NU>(c, d_dJdu, st, k0, nk);
+  return grad_rr_launch<T, NT, 4 * NT, NU>(c, d_dJdu, st, k0, nk, mode);
 }
 
 template <typename T>
-int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk) {
+int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode) {
   const int NT = (c->N + 15) / 16;
   if (c->nu == 1) {
-    if (NT == 1) return grad_rr_nt<T, 1, 1>(c, d_dJdu, st, k0, nk);
-    if (NT == 2) return grad_rr_nt<T, 2, 1>(c, d_dJdu, st, k0, nk);
-    return grad_rr_nt<T, 3, 1>(c, d_dJdu, st, k0, nk);
+    if (NT == 1) return grad_rr_nt<T, 1, 1>(c, d_dJdu, st, k0, nk, mode);
+    if (NT == 2) return grad_rr_nt<T, 2, 1>(c, d_dJdu, st, k0, nk, mode);
+    return grad_rr_nt<T, 3, 1>(c, d_dJdu, st, k0, nk, mode);
   }
-  if (NT == 1) return grad_rr_nt<T, 1, 2>(c, d_dJdu, st, k0, nk);
-  if (NT == 2) return grad_rr_nt<T, 2, 2>(c, d_dJdu, st, k0, nk);
-  return grad_rr_nt<T, 3, 2>(c, d_dJdu, st, k0, nk);
+  if (NT == 1) return grad_rr_nt<T, 1, 2>(c, d_dJdu, st, k0, nk, mode);
+  if (NT == 2) return grad_rr_nt<T, 2, 2>(c, d_dJdu, st, k0, nk, mode);
+  return grad_rr_nt<T, 3, 2>(c, d_dJdu, st, k0, nk, mode);
 }
 
 // Exact gradient (QOC_DUKDP_EXACT): one Fréchet derivative per slice from the 2N x 2N block exponential
@@ -1580,8 +1600,26 @@ int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu) {
   const double last = std::max(0.05, std::min(1.0, c->bwd_last_frac)), w = Nt / (S - 1 + last);
   for (int i = 0; i <= S; ++i) kb[i] = std::max(0, Nt - (int)std::lround(i * w));
   kb[S] = 0;
+  // state side first (QOC_BWD_PRESTATE): P1 = X x_k, P2 = X P1 of every slice need only the forward's states, so
+  // they run beside the first range, which otherwise has nothing beside it; each range then runs q + p (PRE).
+  const size_t pws = (size_t)2 * c->N * c->B * (Nt + 1) * c->m * c->esz;
+  const bool pre = c->bwd_prestate != 0;
+  if (pre && c->pws_bytes < pws) {
+    if (c->d_pws) HIPCHK(c, hipFree(c->d_pws));
+    c->d_pws = nullptr;
+    c->pws_bytes = 0;
+    HIPCHK(c, hipMalloc(&c->d_pws, pws));
+    c->pws_bytes = pws;
+    c->dev_bytes += pws;
+  }
   HIPCHK(c, hipEventRecord(c->sync_ev[S], c->stream));  // stream2 starts after everything queued so far
   HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[S], 0));
+  if (pre) {
+    const int mk = mark_begin(c, 3, c->stream2);
+    const int r = grad_rr_o3<T>(c, d_dJdu, c->stream2, 0, Nt, 1);
+    mark_end(c, mk, c->stream2);
+    if (r) return r;
+  }
   for (int i = 0; i < S; ++i) {
     if (kb[i + 1] >= kb[i]) continue;
     int r = tchain_backward<T>(c, kb[i + 1], kb[i]);
@@ -1589,7 +1627,7 @@ int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu) {
     HIPCHK(c, hipEventRecord(c->sync_ev[i], c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[i], 0));
     const int mk = mark_begin(c, 3, c->stream2);
-    r = grad_rr_o3<T>(c, d_dJdu, c->stream2, kb[i + 1], kb[i] - kb[i + 1]);
+    r = grad_rr_o3<T>(c, d_dJdu, c->stream2, kb[i + 1], kb[i] - kb[i + 1], pre ? 2 : 0);
     mark_end(c, mk, c->stream2);
     if (r) return r;
   }
@@ -1892,6 +1930,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   if (getenv("QOC_BWD_CHUNKS")) c->bwd_chunks = std::max(1, atoi(getenv("QOC_BWD_CHUNKS")));
   if (getenv("QOC_BWD_LAST")) c->bwd_last_frac = atof(getenv("QOC_BWD_LAST"));
   if (getenv("QOC_BWD_PRIO")) c->bwd_prio = atoi(getenv("QOC_BWD_PRIO"));
+  if (getenv("QOC_BWD_PRESTATE")) c->bwd_prestate = atoi(getenv("QOC_BWD_PRESTATE"));
   hipMemset(c->d_L, 0, (size_t)B * (Nt + 1) * Nm * c->esz);
   *out = c;
   return QOC_OK;
@@ -1905,7 +1944,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->d_best) hipFree(c->d_best);
   if (c->d_tcoef) hipFree(c->d_tcoef);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
-                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec};
+                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_pws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& m : c->marks) {

@@ -305,11 +305,14 @@ __global__ __launch_bounds__(256, 2) void k_grad_rr_q(int N, int m, int Nt, int 
 }
 
 // State side and contraction: dJdu = Re[<W0, A_j x> + <W1, A_j P1> + <λ/6, A_j P2>], P1 = X x, P2 = X P1.
-template <typename T, int NT, int KS, int NU>
+// PRE: P1 and P2 were computed beforehand by k_grad_rr_s (next to the first backward range) and are read here.
+template <typename T, int NT, int KS, int NU, bool PRE = false>
 __global__ __launch_bounds__(256, 2) void k_grad_rr_p(int N, int m, int Nt, int B, int k0, int nk, const cx<T>* __restrict__ Agen,
                                                       const double* __restrict__ u, const cx<T>* __restrict__ X,
                                                       const cx<T>* __restrict__ L, const cx<T>* __restrict__ W0,
-                                                      const cx<T>* __restrict__ W1, double* __restrict__ dJdu) {
+                                                      const cx<T>* __restrict__ W1, double* __restrict__ dJdu,
+                                                      const cx<T>* __restrict__ P1in = nullptr,
+                                                      const cx<T>* __restrict__ P2in = nullptr) {
   using G = GradRR<T, NT>;
   using Own = typename G::Own;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -332,11 +335,13 @@ __global__ __launch_bounds__(256, 2) void k_grad_rr_p(int N, int m, int Nt, int 
     grad_load<T, NT>(X, g.bx, g.ok, N, P, lane);
     grad_load<T, NT>(W0, g.bx, g.ok, N, W, lane);
     G::template contract<KS, NU>(N, Gr, Gi, P, W, sj, lane);
-    G::template xmul<KS, NU, false>(N, Gr, Gi, uj, P, Pn, lane);  // P1
+    if constexpr (PRE) grad_load<T, NT>(P1in, g.bx, g.ok, N, Pn, lane);
+    else G::template xmul<KS, NU, false>(N, Gr, Gi, uj, P, Pn, lane);  // P1
     asm volatile("" ::: "memory");  // keep the W loads here: hoisted above a product they add 48 live VGPRs
     grad_load<T, NT>(W1, g.bx, g.ok, N, W, lane);
     G::template contract<KS, NU>(N, Gr, Gi, Pn, W, sj, lane);
-    G::template xmul<KS, NU, false>(N, Gr, Gi, uj, Pn, P, lane);  // P2
+    if constexpr (PRE) grad_load<T, NT>(P2in, g.bx, g.ok, N, P, lane);
+    else G::template xmul<KS, NU, false>(N, Gr, Gi, uj, Pn, P, lane);  // P2
     asm volatile("" ::: "memory");
     grad_load<T, NT>(L, g.bl, g.ok, N, W, lane);
     G::template contract<KS, NU>(N, Gr, Gi, P, W, s2, lane);
@@ -350,6 +355,36 @@ __global__ __launch_bounds__(256, 2) void k_grad_rr_p(int N, int m, int Nt, int 
       for (int o = 1; o < m; o <<= 1) v += __shfl_xor(v, o);
       if (g.ok && lane < 16 && c % m == 0) dJdu[g.unit * NU + j] = v;
     }
+  }
+}
+
+// State side alone: P1 = X x, P2 = X P1 for the units of slices k0 .. k0+nk-1, written in the state layout.  It
+// needs only the forward's states, so it runs on the second stream beside the first backward range (which
+// otherwise has nothing beside it); k_grad_rr_p<PRE = true> then reads P1, P2 instead of forming them.
+template <typename T, int NT, int KS, int NU>
+__global__ __launch_bounds__(256, 2) void k_grad_rr_s(int N, int m, int Nt, int B, int k0, int nk, const cx<T>* __restrict__ Agen,
+                                                      const double* __restrict__ u, const cx<T>* __restrict__ X,
+                                                      cx<T>* __restrict__ P1out, cx<T>* __restrict__ P2out) {
+  using G = GradRR<T, NT>;
+  using Own = typename G::Own;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6;
+  T* Gr = reinterpret_cast<T*>(smem);
+  T* Gi = Gr + (size_t)(NU + 1) * N * G::ldp(N);
+  grad_gens_to_lds<T, NT>(N, NU, Agen, Gr, Gi);
+  const long long units = (long long)B * nk, ntiles = (units + 16 / m - 1) / (16 / m);
+  for (long long tile = (long long)blockIdx.x * nw + wave; tile < ntiles; tile += (long long)gridDim.x * nw) {
+    const GradTile g = grad_tile(tile, lane, N, m, Nt, k0, nk, units);
+    double uj[NU];
+#pragma unroll
+    for (int j = 0; j < NU; ++j) uj[j] = u[g.unit * NU + j];
+    Own P, Pn;
+    grad_load<T, NT>(X, g.bx, g.ok, N, P, lane);
+    G::template xmul<KS, NU, false>(N, Gr, Gi, uj, P, Pn, lane);
+    grad_store<T, NT>(P1out, g.bx, g.ok, N, Pn, lane);
+    G::template xmul<KS, NU, false>(N, Gr, Gi, uj, Pn, P, lane);
+    grad_store<T, NT>(P2out, g.bx, g.ok, N, P, lane);
   }
 }
 

@@ -555,11 +555,13 @@ def test_taylor_action_non_skew_hermitian_generators(built_lib):
         assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
 
 
-@pytest.mark.parametrize("ranges", [("4", "0.5"), ("3", "0.3")])
+@pytest.mark.parametrize("ranges", [("4", "0.5", "0"), ("3", "0.3", "0"), ("4", "0.5", "1"), ("3", "0.3", "1")])
 def test_overlapped_backward_ranges_are_bit_identical(built_lib, monkeypatch, ranges):
     """The backward chain in slice ranges with each range's gradient on a second stream (default for the
     MFMA chains, Nt >= 64) gives bit-identical J, dJ/du and co-states to the single-launch backward
-    (QOC_BWD_CHUNKS=1), with a state penalty and a ragged Nt, and matches the oracle."""
+    (QOC_BWD_CHUNKS=1), with a state penalty and a ragged Nt, and matches the oracle.  QOC_BWD_PRESTATE=1: the
+    state side (P1, P2) of every slice first, beside the first range (k_grad_rr_s), then q + p reading them."""
+    monkeypatch.setenv("QOC_BWD_PRESTATE", ranges[2])
     from qoc_amd import systems
     prob = systems.cavity_problem(N_cavity=10, Nt=131)
     u = systems.cavity_controls(3, prob.Nt, seed=17)

@@ -9,7 +9,7 @@ timeout -k 10 300 python bench.py > gpurun_out/${T}_bench_cavity.json 2> gpurun_
 for c in zz_batch tunable_bus synthetic; do
   timeout -k 10 300 python bench.py --config $c > gpurun_out/${T}_bench_$c.json 2> gpurun_out/${T}_bench_$c.err || exit 1
 done
-./tools/profile.sh cavity r02e || exit 1
-./tools/profile.sh zz_batch r02e || exit 1
+./tools/profile.sh cavity ${2:-r02e} || exit 1
+./tools/profile.sh zz_batch ${2:-r02e} || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || exit 1
 echo done
