@@ -48,7 +48,7 @@ struct qoc_ctx {
   int bwd_chunks = 4;                   // slice ranges of the overlapped backward chain (1: not overlapped)
   double bwd_last_frac = 0.5;           // last range's length relative to the others
   int bwd_prio = 0;                     // bit 0: s_setprio in the chain; bit 1: low-priority gradient stream
-  int bwd_prestate = 1;                 // 1: P1, P2 of every slice beside the first backward range (k_grad_rr_s)
+  int bwd_prestate = 2;                 // P1, P2 of every slice beside the first backward range (k_grad_rr_s): 0 off, 1 on, 2 auto
   void* d_A = nullptr;    // (nu+1) x N*N
   void* d_x0 = nullptr;   // N*m or B*N*m
   int x0_per_seed = 0;
@@ -1603,7 +1603,10 @@ int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu) {
   // state side first (QOC_BWD_PRESTATE): P1 = X x_k, P2 = X P1 of every slice need only the forward's states, so
   // they run beside the first range, which otherwise has nothing beside it; each range then runs q + p (PRE).
   const size_t pws = (size_t)2 * c->N * c->B * (Nt + 1) * c->m * c->esz;
-  const bool pre = c->bwd_prestate != 0;
+  // auto: only when a CU keeps room beside its chain waves (<= 3 per CU, or small N whose chain waves are
+  // light); measured: cavity (3 waves/CU) +1.3 %, zz +0.9 %, tunable bus (2 WGs x 2 waves/CU) -2.6 %
+  const long long chain_waves = (long long)((c->B + c->ncu - 1) / c->ncu) * tchain_mf_waves(c->N, c->m);
+  const bool pre = c->bwd_prestate == 1 || (c->bwd_prestate == 2 && (chain_waves <= 3 || c->N <= 16));
   if (pre && c->pws_bytes < pws) {
     if (c->d_pws) HIPCHK(c, hipFree(c->d_pws));
     c->d_pws = nullptr;
