@@ -682,7 +682,7 @@ __global__ __launch_bounds__(GRAD_THREADS) void k_grad(int N, int m, int nu, int
 // ---------------------------------------------------------------------------
 // Small helpers used by the host API.
 // ---------------------------------------------------------------------------
-__global__ void k_compare_u(const double* __restrict__ a, const double* __restrict__ b, size_t n, int* flag) {
+static __global__ void k_compare_u(const double* __restrict__ a, const double* __restrict__ b, size_t n, int* flag) {
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
     // bitwise comparison (the reference's `u != cache.u` is elementwise ==; NaN never occurs here)
     if (__double_as_longlong(a[e]) != __double_as_longlong(b[e])) atomicOr(flag, 1);
@@ -701,7 +701,7 @@ __global__ void k_cvt_out(const cx<T>* __restrict__ src, cx<double>* __restrict_
 }
 
 // C = alpha * A * B + beta * C  (naive, N x N complex fp64; standalone expm_jacobian only)
-__global__ void k_cgemm_naive(int N, const cx<double>* A, const cx<double>* B, cx<double>* C, double alpha,
+static __global__ void k_cgemm_naive(int N, const cx<double>* A, const cx<double>* B, cx<double>* C, double alpha,
                               double beta) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= N * N) return;
@@ -711,7 +711,7 @@ __global__ void k_cgemm_naive(int N, const cx<double>* A, const cx<double>* B, c
   C[e] = cx<double>{alpha * s.r + beta * C[e].r, alpha * s.i + beta * C[e].i};
 }
 // Y = sum_t w_t X_t
-__global__ void k_axpby(int n, cx<double>* Y, double a, const cx<double>* A, double b, const cx<double>* B) {
+static __global__ void k_axpby(int n, cx<double>* Y, double a, const cx<double>* A, double b, const cx<double>* B) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   cx<double> r = {a * A[e].r, a * A[e].i};

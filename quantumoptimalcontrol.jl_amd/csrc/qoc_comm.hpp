@@ -14,7 +14,7 @@
 namespace qoc {
 
 // (min J, its global seed id) over J[0..B) -> out[0..1]; one workgroup.
-__global__ void k_argmin_seed(const double* __restrict__ J, int B, long long seed_offset, double* __restrict__ out) {
+static __global__ void k_argmin_seed(const double* __restrict__ J, int B, long long seed_offset, double* __restrict__ out) {
   __shared__ double sv[16];
   __shared__ long long si[16];
   double best = __builtin_inf();
@@ -52,7 +52,7 @@ __global__ void k_argmin_seed(const double* __restrict__ J, int B, long long see
 }
 
 // Reduce the gathered (J, seed) pairs of `world` ranks to the best one (lowest seed on ties).
-__global__ void k_pick_best(const double* __restrict__ g, int world, double* __restrict__ out) {
+static __global__ void k_pick_best(const double* __restrict__ g, int world, double* __restrict__ out) {
   if (threadIdx.x != 0) return;
   double best = g[0], seed = g[1];
   for (int r = 1; r < world; ++r) {

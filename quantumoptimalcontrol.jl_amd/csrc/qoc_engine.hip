@@ -4,167 +4,16 @@
 // all per-slice propagators, states and co-states live in HBM for the whole batch of
 // seeds, and the hot path (propagate + grape_sensitivity) is four kernel launches on
 // one HIP stream:  k_expm -> k_chain_fwd  |  k_chain_bwd -> k_grad.
+//
+// The kernel launches live in the qoc_run*.hip translation units (see qoc_internal.hpp).
 #include <dlfcn.h>
-#include <hip/hip_runtime.h>
 
-#include <algorithm>
-#include <cmath>
-#include <cstdarg>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <string>
-#include <type_traits>
-#include <vector>
-
-#include "../../include/qoc.h"
-#include "qoc_bgemm.hpp"
-#include "qoc_chain.hpp"
-#include "qoc_comm.hpp"
-#include "qoc_expm.hpp"
-#include "qoc_expm_rr.hpp"
-#include "qoc_frechet.hpp"
-#include "qoc_grad_rr.hpp"
-#include "qoc_ode.hpp"
+#include "qoc_internal.hpp"
 #include "qoc_spline.hpp"
-#include "qoc_tchain.hpp"
 
-using namespace qoc;
-
-namespace {
+namespace qoc_host {
 
 thread_local std::string g_err;
-
-int fail(qoc_ctx* ctx, int code, const char* fmt, ...);
-
-}  // namespace
-
-struct qoc_ctx {
-  int dev = 0, N = 0, m = 0, nu = 0, Nt = 0, B = 0, prec = QOC_FP64;
-  size_t esz = 16;  // bytes per complex element on device
-  hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;        // gradient ranges overlapped with the backward chain
-  std::vector<hipEvent_t> sync_ev;      // cross-stream ordering events (no timing)
-  int bwd_chunks = 4;                   // slice ranges of the overlapped backward chain (1: not overlapped)
-  double bwd_last_frac = 0.5;           // last range's length relative to the others
-  int bwd_prio = 0;                     // bit 0: s_setprio in the chain; bit 1: low-priority gradient stream
-  int bwd_prestate = 2;                 // P1, P2 of every slice beside the first backward range (k_grad_rr_s): 0 off, 1 on, 2 auto
-  void* d_A = nullptr;    // (nu+1) x N*N
-  void* d_x0 = nullptr;   // N*m or B*N*m
-  int x0_per_seed = 0;
-  void* d_Xt = nullptr;   // N*m target
-  int cost_kind = QOC_COST_TRACE;
-  double cost_n = 1.0;
-  unsigned char* d_pmask = nullptr;
-  double mu = 0.0;
-  void* d_src = nullptr;   // B x (Nt+1) x N x m caller's dL/dx(x_k) (qoc_set_costate_source), device precision
-  bool src_on = false;
-  double* d_u = nullptr;     // B*nu*Nt, u of the last propagate
-  void* d_U = nullptr;       // B*Nt*N*N
-  void* d_X = nullptr;       // B*(Nt+1)*N*m
-  void* d_L = nullptr;       // B*(Nt+1)*N*m
-  double* d_J = nullptr;     // B
-  cx<double>* d_coef = nullptr;  // B*m
-  double* d_dJdu = nullptr;  // B*nu*Nt
-  int* d_flag = nullptr;
-  unsigned long long* d_hist = nullptr;  // 5*64 reference (Padé) selection + 8*64 executed Taylor (r, s) / T12 s
-  int chain_cb_fwd = 0, chain_cb_bwd = 0;  // 0: chain_shape's column block; QOC_CHAIN_CB_FWD / _BWD = 1 | 2 (N > 32)
-  int expm_alg = 1;  // 1 Taylor: register-resident T12 (default), 2 LDS Paterson-Stockmeyer (QOC_EXPM_LDS=1), 0 Padé (QOC_EXPM_PADE=1)
-  int prop_method = 0;                   // QOC_PROP_EXPM / QOC_PROP_TSIT5
-  int nsub = 10;                         // Tsit5 steps per slice (reference dt = 0.1 Δt)
-  int ode_kernel = 0;                    // 0 register-resident rows when N fits, 1 LDS rows (QOC_ODE_LDS=1)
-  double* d_stage = nullptr;             // host->device staging (fp64 complex), max(B*N*m, (nu+1)*N*N)*2
-  size_t stage_elems = 0;
-  std::vector<double> h_u;
-  // live per-kernel timing (hipEvents recorded on `stream` around each hot-path launch)
-  bool profiling = false;
-  struct Mark {
-    int phase;
-    hipEvent_t a, b;
-  };
-  std::vector<Mark> marks;
-  std::vector<hipEvent_t> event_pool;
-  double phase_ms[4] = {0, 0, 0, 0};
-  long long phase_n[4] = {0, 0, 0, 0};
-  // large-N path: every k_bgemm launch bracketed while profiling (algorithmic FLOPs per launch)
-  struct GMark {
-    hipEvent_t a, b;
-    double flops;
-  };
-  std::vector<GMark> gmarks;
-  double gemm_ms = 0, gemm_flops = 0;
-  long long gemm_n = 0;
-  // large-N path (N beyond the LDS-resident kernels): chunked batched-GEMM pipeline
-  bool big = false;
-  int chunk = 0;                // slices per chunk
-  void* d_ws = nullptr;         // chunk workspace
-  double* d_red = nullptr;      // per-item reductions (chunk + 8 doubles)
-  long long big_hist[5 * 64] = {};
-  long long big_thist[8 * 64] = {};  // executed Taylor (r, s) on the large-N path
-  long long ns_iters = 0;       // Newton-Schulz iterations executed (all chunks)
-  size_t dev_bytes = 0;
-  // spline parameterisation (examples/ipopt_callbacks_exp.jl:13-14, 28)
-  double* d_Bs = nullptr;  // Nt x ns
-  int ns = 0;
-  double* d_cstage = nullptr;  // host-pointer variants: B x ns x nu coefficients / gradient
-  // GEMM-shaped gradient of the LDS-resident path (order 3, N >= 32: below that the 64-row GEMM tiles
-  // are mostly padding and the per-slice k_grad is faster): generator layouts + P/Q/W workspace
-  void* d_AH = nullptr;    // (nu+1) x N*N: [A0^H | A1^H | ...]
-  void* d_Cst = nullptr;   // nu N x N: [A1; A2; ...]
-  void* d_gws = nullptr;   // 6 x N x B(Nt+1)m
-  void* d_pws = nullptr;   // 2 x N x B(Nt+1)m: P1, P2 of the state-side gradient pass (bwd_prestate)
-  size_t pws_bytes = 0;
-  bool grad_gemm = true;
-  bool grad_rr = false;  // fused register-resident order-3 gradient (qoc_grad_rr.hpp)
-  int* d_ps = nullptr;   // k_expm_rr pass-2 counter + list of Paterson-Stockmeyer units
-  double a0norm = 0.0;   // ||A0||_1 of the generators (host-side, at qoc_set_generators)
-  // exponential that runs: expm_alg, except that when every slice has a large norm (||A0||_1 > 4 theta_12,
-  // tunable bus: ||A_k||_1 ~ 30) the default register-resident Taylor hands over to the reference's own Padé-13
-  // + solve (k_expm ALG 0): over 2000 chained slices only the same algorithm holds |ΔJ| <= 1e-12 against the
-  // reference (Paterson-Stockmeyer: 1.6e-12).  QOC_EXPM_PS=1 keeps Paterson-Stockmeyer there (1.8x faster).
-  int expm_run = 1;
-  bool expm_ps = false;
-  int ncu = 256;         // compute units of the device (persistent-grid sizing)
-  // Taylor-action chains (qoc_tchain.hpp): x_{k+1} = exp(A_k) x_k applied to the state, no U_k formed.
-  // chain_mode 1 selects them (QOC_CHAIN=taylor / expm overrides the automatic choice at qoc_set_generators)
-  int chain_mode = 0;            // 0: propagators (k_expm + k_chain_*), 1: Taylor action (k_tchain_*)
-  int chain_req = QOC_CHAIN_AUTO;  // what qoc_set_chain asked for (kept across qoc_set_generators)
-  bool tchain_ok = false;        // the shape fits the Taylor-action kernels
-  void* d_At = nullptr;          // (nu+1) N x N shifted generators Ã_j = A_j - μ_j I
-  TStep* d_steps = nullptr;      // B x Nt (P, s, e^{μ_k})
-  unsigned long long* d_terms = nullptr;  // Σ P s per forward (executed Taylor terms per direction)
-  TChainParams tprm{};
-  bool cheb_ok = false;          // generators skew-Hermitian with imaginary shifts: Chebyshev applies
-  bool cheb = false;             // Chebyshev terms (k_tchain_prep_cheb) instead of Taylor (QOC_TCHAIN_POLY=taylor)
-  bool cheb_ran = false;         // what the last forward pass used (the backward pass reuses its steps)
-  double* d_tcoef = nullptr;     // B x Nt x TCHEB_STRIDE Chebyshev coefficients (allocated on first use)
-  long long props_since_reset = 0;  // forward passes since the last Padé-histogram reset (chain mode 1)
-  // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
-  ncclComm_t comm = nullptr;
-  int world = 1, rank = 0;
-  long long seed_offset = 0;   // global id of this context's seed 0
-  double* d_best = nullptr;    // [2 local | 2 x world gathered | 2 result]
-  // exact (Fréchet) gradient mode workspace, allocated on first use
-  void* d_fws = nullptr;
-  size_t fws_bytes = 0;
-  // packed states (compress_states, src/utils.jl:96-109): two parity sectors share the kernels' columns, so the
-  // chains and the gradient run on m = max(n1, n2) columns instead of the caller's m_user = n1 + n2
-  int m_user = 0;                       // columns of the caller's states (qoc_create's m)
-  bool packed = false;
-  std::vector<unsigned char> h_rsec;    // N row sectors (0 / 1)
-  std::vector<int> pk_cols[2];          // original columns of sector s: packed column i holds pk_cols[s][i]
-  std::vector<int> pk_pos[2];           // m_user: packed column of original column c in sector s, or -1
-  int zmap[4] = {0, 1, 2, 3};           // z-calibrated cost: original column c -> s m + i
-  unsigned char* d_rsec = nullptr;
-  bool grad_rr_any_m = false;           // the fused gradient fits apart from the column count
-  // caller-layout copies, re-packed when the packing changes
-  std::vector<double> h_gen, h_x0, h_Xt;
-  std::vector<int> h_pen_rows, h_pen_cols;
-  bool have_gen = false, have_x0 = false, have_cost = false, have_prop = false;
-  std::string err;
-};
-
-namespace {
 
 int fail(qoc_ctx* ctx, int code, const char* fmt, ...) {
   char buf[512];
@@ -175,110 +24,6 @@ int fail(qoc_ctx* ctx, int code, const char* fmt, ...) {
   g_err = buf;
   if (ctx) ctx->err = buf;
   return code;
-}
-
-#define HIPCHK(ctx, expr)                                                                     \
-  do {                                                                                        \
-    hipError_t e_ = (expr);                                                                   \
-    if (e_ != hipSuccess) return fail(ctx, QOC_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
-  } while (0)
-
-constexpr int kChainMaxN = 64;
-
-bool expm_supported(int N, int prec) {
-  if (N < 1 || N > 48) return false;
-  const int NT = (N + 15) / 16;
-  size_t lds = 0;
-  if (prec == QOC_FP64) {
-    lds = NT == 1 ? Expm<double, 1>::lds_bytes(N) : NT == 2 ? Expm<double, 2>::lds_bytes(N) : Expm<double, 3>::lds_bytes(N);
-  } else {
-    lds = NT == 1 ? Expm<float, 1>::lds_bytes(N) : NT == 2 ? Expm<float, 2>::lds_bytes(N) : Expm<float, 3>::lds_bytes(N);
-  }
-  return lds <= 160 * 1024;
-}
-
-// Two launches: the T12 pass over every unit, then the Paterson-Stockmeyer pass over the units the
-// first one listed (||A_k||_1 > 4 theta_12); ps = {list (>= nunits ints), counter}.
-template <typename T, int NT, int KS>
-hipError_t launch_expm_rr_k(hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
-                            const void* Ain, void* Uout, unsigned long long* hist, unsigned long long* thist,
-                            int* ps, bool mix) {
-  const size_t lds = ExpmRR<T, NT>::lds_bytes(N);
-  if (mix) {  // one pass, T12 or Paterson-Stockmeyer per slice inline
-    hipError_t e =
-        hipFuncSetAttribute((const void*)k_expm_rr_mix<T, NT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_expm_rr_mix<T, NT, KS>), dim3(nunits), dim3(64 * NT), lds, s, N, nu, nunits,
-                       (const cx<T>*)Agen, u, (const cx<T>*)Ain, (cx<T>*)Uout, hist, thist);
-    return hipGetLastError();
-  }
-  hipError_t e =
-      hipFuncSetAttribute((const void*)k_expm_rr<T, NT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_expm_rr_ps<T, NT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  int* list = ps + 1;
-  if ((e = hipMemsetAsync(ps, 0, sizeof(int), s)) != hipSuccess) return e;
-  hipLaunchKernelGGL((k_expm_rr<T, NT, KS>), dim3(nunits), dim3(64 * NT), lds, s, N, nu, nunits, (const cx<T>*)Agen, u,
-                     (const cx<T>*)Ain, (cx<T>*)Uout, hist, thist, list, ps);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  const int grid = nunits;  // pass 2 exits at once past the listed count
-  hipLaunchKernelGGL((k_expm_rr_ps<T, NT, KS>), dim3(grid), dim3(64 * NT), lds, s, N, nu, (const cx<T>*)Agen, u,
-                     (const cx<T>*)Ain, (cx<T>*)Uout, hist, thist, (const int*)list, (const int*)ps);
-  return hipGetLastError();
-}
-
-// k-steps: f64 ceil(N/4) (compile-time, one of the 4 values for this NT), f32 all 4 NT.
-template <typename T, int NT>
-hipError_t launch_expm_rr_t(hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
-                            const void* Ain, void* Uout, unsigned long long* hist, unsigned long long* thist, int* ps,
-                            bool mix) {
-  const int ks = sizeof(T) == 8 ? (N + 3) / 4 : 4 * NT;
-#define QOC_RRK(K) \
-  if (ks == (K)) return launch_expm_rr_k<T, NT, (K)>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, thist, ps, mix)
-  if constexpr (sizeof(T) == 8) {
-    QOC_RRK(4 * NT - 3);
-    QOC_RRK(4 * NT - 2);
-    QOC_RRK(4 * NT - 1);
-  }
-  QOC_RRK(4 * NT);
-#undef QOC_RRK
-  return hipErrorInvalidValue;
-}
-
-template <typename T, int NT, int ALG>
-hipError_t launch_expm_t(hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
-                         const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq,
-                         unsigned long long* thist) {
-  const size_t lds = Expm<T, NT>::lds_bytes(N);
-  hipError_t e =
-      hipFuncSetAttribute((const void*)k_expm<T, NT, ALG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_expm<T, NT, ALG>), dim3(nunits), dim3(256), lds, s, N, nu, nunits, (const cx<T>*)Agen, u,
-                     (const cx<T>*)Ain, (cx<T>*)Uout, hist, deg, sq, thist);
-  return hipGetLastError();
-}
-
-// alg 0: Padé + solve (reference algorithm); alg 1: register-resident Taylor T12; alg 2: LDS Paterson-Stockmeyer.
-hipError_t launch_expm(int prec, hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
-                       const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq, int alg = 0,
-                       unsigned long long* thist = nullptr, int* ps = nullptr, bool mix = false) {
-  const int NT = (N + 15) / 16;
-  // alg 1: the register-resident T12 kernel (qoc_expm_rr.hpp); alg 2: the LDS Paterson-Stockmeyer one.
-  const bool rr = alg == 1 && ps;  // the register-resident kernel needs the pass-2 list (ctx workspace)
-#define QOC_LX(TT, NTT)                                                                                   \
-  return alg ? (rr ? launch_expm_rr_t<TT, NTT>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, thist, ps, mix) \
-                   : launch_expm_t<TT, NTT, 1>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq, thist)) \
-             : launch_expm_t<TT, NTT, 0>(s, N, nu, nunits, Agen, u, Ain, Uout, hist, deg, sq, thist)
-  if (prec == QOC_FP64) {
-    if (NT == 1) QOC_LX(double, 1);
-    if (NT == 2) QOC_LX(double, 2);
-    QOC_LX(double, 3);
-  }
-  if (NT == 1) QOC_LX(float, 1);
-  if (NT == 2) QOC_LX(float, 2);
-  QOC_LX(float, 3);
-#undef QOC_LX
 }
 
 template <typename T>
@@ -417,45 +162,6 @@ bool gens_block_diagonal(const qoc_ctx* c) {
   return true;
 }
 
-size_t chain_lds(const qoc_ctx* c) {
-  const ChainShape sh = chain_shape(c->N, c->m, c->prec == QOC_FP64);
-  // sized for the largest column block either direction may use (chain_dispatch's override: 2 at JT >= 10)
-  const int cb = sh.JT >= 10 ? 2 : sh.CB;
-  return (size_t)(2 * sh.S * sh.JT * chain_mpad(c->m, cb)) * c->esz + 64 * sizeof(double);
-}
-
-// k_chain_fwd / k_chain_bwd instantiated per thread shape (chain_shape): (S, JT, CB) = (4, 4, 1|4),
-// (8, 4, 1|4), (4, 10, 1|2), (4, 12, 1|2), fp32 also (4, 16, 1|2).
-template <typename T, typename F>
-hipError_t chain_dispatch(int N, int m, int cb_override, F&& f) {
-  using std::integral_constant;
-  ChainShape sh = chain_shape(N, m, sizeof(T) == 8);
-  if (cb_override > 0 && sh.JT >= 10) sh.CB = cb_override == 2 ? 2 : 1;  // tuning knob (QOC_CHAIN_CB_*)
-  if (sh.JT == 4) {
-    if (sh.S == 4)
-      return sh.CB == 4 ? f(integral_constant<int, 4>(), integral_constant<int, 4>(), integral_constant<int, 4>())
-                        : f(integral_constant<int, 4>(), integral_constant<int, 4>(), integral_constant<int, 1>());
-    return sh.CB == 4 ? f(integral_constant<int, 8>(), integral_constant<int, 4>(), integral_constant<int, 4>())
-                      : f(integral_constant<int, 8>(), integral_constant<int, 4>(), integral_constant<int, 1>());
-  }
-  if (sh.JT == 10)
-    return sh.CB == 2 ? f(integral_constant<int, 4>(), integral_constant<int, 10>(), integral_constant<int, 2>())
-                      : f(integral_constant<int, 4>(), integral_constant<int, 10>(), integral_constant<int, 1>());
-  if (sh.JT == 12)
-    return sh.CB == 2 ? f(integral_constant<int, 4>(), integral_constant<int, 12>(), integral_constant<int, 2>())
-                      : f(integral_constant<int, 4>(), integral_constant<int, 12>(), integral_constant<int, 1>());
-  if constexpr (sizeof(T) == 4) {
-    if (sh.JT == 16)
-      return sh.CB == 2 ? f(integral_constant<int, 4>(), integral_constant<int, 16>(), integral_constant<int, 2>())
-                        : f(integral_constant<int, 4>(), integral_constant<int, 16>(), integral_constant<int, 1>());
-  }
-  return hipErrorInvalidValue;
-}
-
-size_t grad_lds(const qoc_ctx* c, int order) {
-  return (size_t)(c->N * (c->N + 1) + 2 * order * c->N * c->m) * c->esz + 64 * sizeof(double);
-}
-
 hipEvent_t take_event(qoc_ctx* c) {
   if (!c->event_pool.empty()) {
     hipEvent_t e = c->event_pool.back();
@@ -468,1175 +174,15 @@ hipEvent_t take_event(qoc_ctx* c) {
 }
 
 // RAII-less bracket: mark_begin returns the index of the pending mark, mark_end records its stop event.
-int mark_begin(qoc_ctx* c, int phase, hipStream_t s = nullptr) {
+int mark_begin(qoc_ctx* c, int phase, hipStream_t s) {
   if (!c->profiling) return -1;
   qoc_ctx::Mark m{phase, take_event(c), take_event(c)};
   (void)hipEventRecord(m.a, s ? s : c->stream);
   c->marks.push_back(m);
   return (int)c->marks.size() - 1;
 }
-void mark_end(qoc_ctx* c, int idx, hipStream_t s = nullptr) {
+void mark_end(qoc_ctx* c, int idx, hipStream_t s) {
   if (idx >= 0) (void)hipEventRecord(c->marks[idx].b, s ? s : c->stream);
-}
-
-template <typename T>
-int frechet_grad(qoc_ctx* c, double* d_dJdu);
-template <typename T>
-int grad_gemm_o3(qoc_ctx* c, double* d_dJdu);
-template <typename T>
-int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode = 0);
-
-template <typename T>
-int ode_forward(qoc_ctx* c);
-template <typename T>
-int ode_adjoint(qoc_ctx* c);
-template <typename T>
-int tchain_forward(qoc_ctx* c);
-template <typename T>
-int tchain_backward(qoc_ctx* c, int k_lo = 0, int k_hi = -1);
-template <typename T>
-int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu);
-bool tchain_mf(const qoc_ctx* c);
-
-template <typename T>
-int run_forward(qoc_ctx* c) {
-  if (c->prop_method == QOC_PROP_TSIT5) return ode_forward<T>(c);
-  if (c->chain_mode == 1) return tchain_forward<T>(c);
-  int mk = mark_begin(c, 0);
-  hipError_t e = launch_expm(c->prec, c->stream, c->N, c->nu, c->B * c->Nt, c->d_A, c->d_u, nullptr, c->d_U,
-                             c->d_hist, nullptr, nullptr, c->expm_run, c->d_hist + 5 * 64, c->d_ps,
-                             c->a0norm > 4.0 * kTheta12);
-  mark_end(c, mk);
-  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm launch: %s", hipGetErrorString(e));
-  const size_t lds = chain_lds(c);
-  mk = mark_begin(c, 1);
-  e = chain_dispatch<T>(c->N, c->m, c->chain_cb_fwd, [&](auto S_, auto JT_, auto CB_) {
-    constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value;
-    hipError_t r = hipFuncSetAttribute((const void*)k_chain_fwd<T, S, JT, CB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
-    if (r != hipSuccess) return r;
-    hipLaunchKernelGGL((k_chain_fwd<T, S, JT, CB>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
-                       (const cx<T>*)c->d_U, (const cx<T>*)c->d_x0, c->x0_per_seed, (cx<T>*)c->d_X,
-                       (const cx<T>*)c->d_Xt, c->cost_kind, c->cost_n, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu,
-                       c->d_J, c->d_coef, sectors(c));
-    return hipGetLastError();
-  });
-  mark_end(c, mk);
-  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_chain_fwd launch: %s", hipGetErrorString(e));
-  return QOC_OK;
-}
-
-template <typename T>
-int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
-  size_t lds = chain_lds(c);
-  int mk;
-  if (c->prop_method == QOC_PROP_TSIT5) {
-    int r = ode_adjoint<T>(c);
-    if (r) return r;
-  } else if (c->chain_mode == 1) {
-    if (order == 3 && c->grad_rr && c->bwd_chunks > 1 && c->Nt >= 64 && tchain_mf(c)) return tchain_backward_overlapped<T>(c, d_dJdu);
-    int r = tchain_backward<T>(c);
-    if (r) return r;
-  } else {
-    mk = mark_begin(c, 2);
-    const hipError_t e = chain_dispatch<T>(c->N, c->m, c->chain_cb_bwd, [&](auto S_, auto JT_, auto CB_) {
-      constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value;
-      hipError_t r = hipFuncSetAttribute((const void*)k_chain_bwd<T, S, JT, CB>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (r != hipSuccess) return r;
-      hipLaunchKernelGGL((k_chain_bwd<T, S, JT, CB>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, c->N, c->m, c->Nt,
-                         (const cx<T>*)c->d_U, (const cx<T>*)c->d_X, (cx<T>*)c->d_L, (const cx<T>*)c->d_Xt,
-                         c->cost_kind, (const cx<double>*)c->d_coef, c->mu != 0.0 ? c->d_pmask : nullptr, c->mu,
-                         c->src_on ? (const cx<T>*)c->d_src : nullptr, sectors(c));
-      return hipGetLastError();
-    });
-    mark_end(c, mk);
-    if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_chain_bwd launch: %s", hipGetErrorString(e));
-  }
-  if (order == QOC_DUKDP_EXACT) {
-    mk = mark_begin(c, 3);
-    int r = frechet_grad<T>(c, d_dJdu);
-    mark_end(c, mk);
-    return r;
-  }
-  if (order == 3 && c->grad_rr) {
-    mk = mark_begin(c, 3);
-    int r = grad_rr_o3<T>(c, d_dJdu, c->stream, 0, c->Nt);
-    mark_end(c, mk);
-    return r;
-  }
-  if (order == 3 && c->grad_gemm) {
-    mk = mark_begin(c, 3);
-    int r = grad_gemm_o3<T>(c, d_dJdu);
-    mark_end(c, mk);
-    return r;
-  }
-  lds = grad_lds(c, order);
-  HIPCHK(c, hipFuncSetAttribute((const void*)k_grad<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  mk = mark_begin(c, 3);
-  hipLaunchKernelGGL((k_grad<T>), dim3(c->B * c->Nt), dim3(GRAD_THREADS), lds, c->stream, c->N, c->m, c->nu, c->Nt,
-                     order, (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, d_dJdu);
-  mark_end(c, mk);
-  HIPCHK(c, hipGetLastError());
-  return QOC_OK;
-}
-
-// =============================================================================================
-// Large-N path: chunked batched-GEMM pipeline (N beyond the LDS-resident kernels).
-//   propagate : per chunk of slices  k_form_norm -> Padé products (6 GEMMs for d = 13, fused
-//               lincomb epilogues) -> Newton-Schulz solve of (V-U) X = (V+U) (all GEMM) ->
-//               squarings;  then the forward chain as Nt batched GEMMs over the seeds.
-//   sensitivity: backward chain as Nt batched U^H GEMMs; per chunk P_a = X^a x, Q_b = (X^H)^b λ,
-//               W_a = sum_b Q_b/(a+b+1)!, M' = W P^H (one GEMM, K = order*m), dJdu = Re<A_j, M'>.
-// =============================================================================================
-static const double hPade3[4] = {120.0, 60.0, 12.0, 1.0};
-static const double hPade5[6] = {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0};
-static const double hPade7[8] = {17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0};
-static const double hPade9[10] = {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0,
-                                  2162160.0, 110880.0, 3960.0, 90.0, 1.0};
-static const double hPade13[14] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
-                                   1187353796428800.0, 129060195264000.0, 10559470521600.0,
-                                   670442572800.0, 33522128640.0, 1323241920.0, 40840800.0,
-                                   960960.0, 16380.0, 182.0, 1.0};
-
-size_t big_ws_elems_per_item(int N, int m) {
-  const size_t NN = (size_t)N * N, Nm = (size_t)N * m;
-  return std::max(8 * NN, 2 * NN + 11 * Nm);
-}
-
-Opd mk_opd(const void* base, size_t elem_off, size_t esz, long long inner, int per = 0, long long outer = 0,
-           int u0 = 0) {
-  Opd o;
-  o.p = (const char*)base + elem_off * esz;
-  o.inner = inner;
-  o.per = per;
-  o.outer = outer;
-  o.u0 = u0;
-  return o;
-}
-
-GemmArgs gemm_args(int M, int K, int Ncol, int nitems) {
-  GemmArgs g;
-  std::memset(&g, 0, sizeof(g));
-  g.M = M;
-  g.K = K;
-  g.Ncol = Ncol;
-  g.nitems = nitems;
-  g.alpha1 = 1.0;
-  return g;
-}
-
-template <typename T>
-int big_gemm(qoc_ctx* c, int opa, int opb, GemmArgs g, int mode = 0) {
-  g.tiles_m = (g.M + BG_BM - 1) / BG_BM;
-  g.tiles = g.tiles_m * ((g.Ncol + BG_BN - 1) / BG_BN);
-  const long long total = (long long)g.nitems * g.tiles;
-  if (total <= 0 || total >= (1LL << 31)) return fail(c, QOC_ERR_ARG, "GEMM grid out of range");
-  const dim3 grid((unsigned)total), blk(BG_THREADS);
-  qoc_ctx::GMark gm{nullptr, nullptr, 8.0 * g.M * (double)g.K * g.Ncol * g.nitems};
-  if (c->profiling) {
-    gm.a = take_event(c);
-    gm.b = take_event(c);
-    (void)hipEventRecord(gm.a, c->stream);
-  }
-  if (mode == 1) hipLaunchKernelGGL((k_bgemm<T, 0, 0, true, 1, 2, 1>), grid, blk, 0, c->stream, g);
-  else if (mode == 2) hipLaunchKernelGGL((k_bgemm<T, 0, 0, true, 1, 2, 2>), grid, blk, 0, c->stream, g);
-  else if (opa == 0 && opb == 0) hipLaunchKernelGGL((k_bgemm<T, 0, 0>), grid, blk, 0, c->stream, g);
-  else if (opa == 1 && opb == 0) hipLaunchKernelGGL((k_bgemm<T, 1, 0>), grid, blk, 0, c->stream, g);
-  else if (opa == 0 && opb == 1) hipLaunchKernelGGL((k_bgemm<T, 0, 1>), grid, blk, 0, c->stream, g);
-  else hipLaunchKernelGGL((k_bgemm<T, 1, 1>), grid, blk, 0, c->stream, g);
-  HIPCHK(c, hipGetLastError());
-  if (c->profiling) {
-    (void)hipEventRecord(gm.b, c->stream);
-    c->gmarks.push_back(gm);
-  }
-  return QOC_OK;
-}
-
-template <typename T>
-int big_lincomb(qoc_ctx* c, LinArgs a) {
-  const size_t total = (size_t)a.rows * a.cols * a.nitems;
-  const unsigned blocks = (unsigned)std::min<size_t>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL((k_lincomb<T>), dim3(blocks), dim3(256), 0, c->stream, a);
-  HIPCHK(c, hipGetLastError());
-  return QOC_OK;
-}
-
-// exp(A_k) for units [u0, u0+cnt) -> d_U.  Workspace buffers w(i), i < 8, of cnt x N x N.
-// Paterson-Stockmeyer degree m = 3r + 2 (r = 2..8): the largest ||A||_1 whose Taylor tail sum_{k>m} ||A||^k / k!
-// is <= 2^-53 (fp64) or 2^-24 (fp32, the unit roundoff of the arithmetic the fp32 pipeline runs in)
-static const double hTaylorTheta[7] = {0.069933, 0.247240, 0.553491, 0.978345, 1.504147, 2.113468, 2.791345};
-static const double hTaylorTheta32[7] = {0.648322, 1.31065, 2.099345, 2.969587, 3.894655, 4.858047, 5.849147};
-
-// T12 on the GEMM pipeline: Â = A / 2^s, Â2 = Â², A3 = Â2 Â, B_j = x_j0 I + x_j1 Â + x_j2 Â2 + x_j3 A3,
-// A6 = B3 + B4², T12 = B1 + (B2 + A6) A6, then s squarings.  Each B_j comes out of the A3 product's epilogue
-// (B1, B4, B3: its three outputs); B2 is carried as B2 = β B3 + (x_20 I + (x_21 − β x_31) Â + (x_22 − β x_32) Â2)
-// with β = x_23 / x_33, so that B2 + A6 leaves the B4² product's epilogue next to A6 (three addends).
-// Host copy of kT12 (qoc_expm.hpp).
-static const double hT12[4][4] = {
-    {1.0, 0.99999999999276613715098, -0.13243184210109929356121, -0.050548416421727518977426},
-    {5.5174437753406856228547, 1.3093238729673181077940, 0.0043247187525051520919919, 0.0096586056829351321677927},
-    {0.0, 1.3110895450078318461208e-12, 0.097250029534075019542638, 0.0068219250901116764187357},
-    {0.0, 0.13181061013830184015682, 0.020278555405892590793357, 0.0067595184686308635977856}};
-
-template <typename T>
-int t12_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, const Opd& Asrc, const Opd& dest, int ts,
-                   bool count_hist) {
-  const size_t NN = (size_t)N * N, esz = c->esz;
-  auto w = [&](int i) { return mk_opd(ws, (size_t)i * ws_items * NN, esz, (long long)NN); };
-  if (count_hist) c->big_thist[kT12Row * 64 + std::min(ts, 63)] += cnt;
-  const double sc = std::ldexp(1.0, -ts), (*x)[4] = hT12, beta = x[1][3] / x[2][3];
-  int r;
-  GemmArgs g = gemm_args(N, N, N, cnt);  // Â2 -> w1
-  g.A = Asrc; g.B = Asrc; g.C1 = w(1); g.alpha1 = sc * sc;
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-  g = gemm_args(N, N, N, cnt);  // A3 = sc Â2 A:  B1 -> w2, B4 -> w3, B3 -> w4
-  g.A = w(1); g.B = Asrc;
-  g.nY = 2; g.Y[0] = Asrc; g.Y[1] = w(1);
-  g.C1 = w(2); g.alpha1 = x[0][3] * sc; g.w1[0] = x[0][1] * sc; g.w1[1] = x[0][2]; g.gamma1 = x[0][0];
-  g.C2 = w(3); g.alpha2 = x[3][3] * sc; g.w2[0] = x[3][1] * sc; g.w2[1] = x[3][2]; g.gamma2 = x[3][0];
-  g.C3 = w(4); g.alpha3 = x[2][3] * sc; g.w3[0] = x[2][1] * sc; g.w3[1] = x[2][2]; g.gamma3 = x[2][0];
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-  g = gemm_args(N, N, N, cnt);  // B4²:  A6 = B4² + B3 -> w5,  B2 + A6 -> w6
-  g.A = w(3); g.B = w(3);
-  g.nY = 3; g.Y[0] = w(4); g.Y[1] = Asrc; g.Y[2] = w(1);
-  g.C1 = w(5); g.w1[0] = 1.0;
-  g.C2 = w(6); g.alpha2 = 1.0; g.w2[0] = 1.0 + beta; g.w2[1] = (x[1][1] - beta * x[2][1]) * sc;
-  g.w2[2] = x[1][2] - beta * x[2][2]; g.gamma2 = x[1][0];
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-  g = gemm_args(N, N, N, cnt);  // T12 = (B2 + A6) A6 + B1
-  g.A = w(6); g.B = w(5); g.C1 = ts == 0 ? dest : w(7);
-  g.nY = 1; g.Y[0] = w(2); g.w1[0] = 1.0;
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-  int xb = 7;
-  for (int q = 0; q < ts; ++q) {
-    const int nb = xb == 7 ? 1 : 7;
-    g = gemm_args(N, N, N, cnt);
-    g.A = w(xb); g.B = w(xb); g.C1 = q == ts - 1 ? dest : w(nb);
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-    xb = nb;
-  }
-  return QOC_OK;
-}
-
-// Taylor / Paterson-Stockmeyer exponential on the GEMM pipeline (the large-N analogue of k_expm ALG 1):
-// degree m = 3r + 2 with (r, s) minimising 2 + r + s for the chunk's max norm; every B_i = c I + c' A + c'' A2
-// is added in a GEMM epilogue, so the chunk costs exactly 2 + r + s GEMMs and no element-wise pass.
-template <typename T>
-int taylor_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, const Opd& Asrc, const Opd& dest,
-                      double nA, bool count_hist) {
-  const size_t NN = (size_t)N * N, esz = c->esz;
-  auto w = [&](int i) { return mk_opd(ws, (size_t)i * ws_items * NN, esz, (long long)NN); };
-  int tr = 2, ts = 0, best = 1 << 30;
-  const double* th = sizeof(T) == 4 ? hTaylorTheta32 : hTaylorTheta;
-  for (int rr = 2; rr <= 8; ++rr) {
-    const int ss = nA > th[rr - 2] ? (int)std::ceil(std::log2(nA / th[rr - 2])) : 0;
-    if (2 + rr + ss < best || (2 + rr + ss == best && ss < ts)) {
-      best = 2 + rr + ss;
-      tr = rr;
-      ts = ss;
-    }
-  }
-  // Degree-12 Taylor in 4 products (the T12 scheme of k_expm_rr, coefficients kT12) when it needs fewer GEMMs:
-  // 4 + s12 with θ12 = 1.5622 in fp32 (tail <= 2^-24) / kTheta12 in fp64.  Synthetic slices (||A||_1 in
-  // (3.1, 4.2]): 6 GEMMs instead of Paterson-Stockmeyer's 7.
-  const double th12 = sizeof(T) == 4 ? 1.562211457125874 : kTheta12;
-  const int s12 = nA > th12 ? (int)std::ceil(std::log2(nA / th12)) : 0;
-  if (4 + s12 < best && !getenv("QOC_BIG_NO_T12")) return t12_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, s12, count_hist);
-  if (count_hist) c->big_thist[(tr - 2) * 64 + std::min(ts, 63)] += cnt;
-  static const double f[27] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720, 1.0 / 5040, 1.0 / 40320,
-                               2.755731922398589e-06, 2.755731922398589e-07, 2.505210838544172e-08,
-                               2.08767569878681e-09, 1.6059043836821613e-10, 1.1470745597729725e-11,
-                               7.647163731819816e-13, 4.779477332387385e-14, 2.8114572543455206e-15,
-                               1.5619206968586225e-16, 8.22063524662433e-18, 4.110317623312165e-19,
-                               1.9572941063391263e-20, 8.896791392450574e-22, 3.8681701706306835e-23,
-                               1.6117375710961184e-24, 6.446950284384474e-26, 2.4795962632247976e-27};
-  const double sc = std::ldexp(1.0, -ts);
-  int r;
-  // Â2 = sc^2 A A -> w1
-  GemmArgs g = gemm_args(N, N, N, cnt);
-  g.A = Asrc; g.B = Asrc; g.C1 = w(1); g.alpha1 = sc * sc;
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-  // Â3 = sc Â2 A -> w2, and B_r = c_{3r} I + c_{3r+1} Â + c_{3r+2} Â2 -> w3 from the epilogue
-  g = gemm_args(N, N, N, cnt);
-  g.A = w(1); g.B = Asrc; g.C1 = w(2); g.alpha1 = sc;
-  g.nY = 2; g.Y[0] = Asrc; g.Y[1] = w(1);
-  g.C2 = w(3); g.alpha2 = 0.0; g.w2[0] = f[3 * tr + 1] * sc; g.w2[1] = f[3 * tr + 2]; g.gamma2 = f[3 * tr];
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-  int cur = 3;
-  for (int i = tr - 1; i >= 0; --i) {  // cur <- Â3 cur + B_i  (polynomials in A commute)
-    const int nxt = cur == 3 ? 4 : 3;
-    g = gemm_args(N, N, N, cnt);
-    g.A = w(2); g.B = w(cur);
-    g.C1 = (i == 0) ? (ts == 0 ? dest : w(6)) : w(nxt);
-    g.nY = 2; g.Y[0] = Asrc; g.Y[1] = w(1);
-    g.w1[0] = f[3 * i + 1] * sc; g.w1[1] = f[3 * i + 2]; g.gamma1 = f[3 * i];
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-    cur = nxt;
-  }
-  int xb = 6;
-  for (int q = 0; q < ts; ++q) {
-    const int nb = xb == 6 ? 7 : 6;
-    g = gemm_args(N, N, N, cnt);
-    g.A = w(xb); g.B = w(xb); g.C1 = q == ts - 1 ? dest : w(nb);
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-    xb = nb;
-  }
-  return QOC_OK;
-}
-
-// exp of cnt explicit n x n matrices (operand Asrc, chunk max 1-norm nA) -> dest, all GEMM:
-// Padé (Higham 2005 degree / squarings for nA) + Newton-Schulz solve + squarings.  Workspace:
-// 8 buffers of ws_items x n x n at ws; red >= cnt doubles.
-template <typename T>
-int expm_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, double* red, const Opd& Asrc,
-                    const Opd& dest, double nA, bool count_hist) {
-  const size_t NN = (size_t)N * N, esz = c->esz;
-  auto w = [&](int i) { return mk_opd(ws, (size_t)i * ws_items * NN, esz, (long long)NN); };
-  int r;
-  // Padé degree / squarings: the thresholds of k_expm (Higham 2005), one (d, s) per chunk chosen
-  // from the chunk's largest norm (any degree >= the per-slice choice meets the same bound).  Counted
-  // for the reference-equivalent accounting whichever algorithm runs.
-  int d, sq = 0;
-  if (nA <= 2.1) {
-    d = nA > 0.95 ? 9 : nA > 0.25 ? 7 : nA > 0.015 ? 5 : 3;
-  } else {
-    d = 13;
-    const double sl = std::log2(nA / 5.4);
-    sq = sl > 0 ? (int)std::ceil(sl) : 0;
-  }
-  const int di = d == 3 ? 0 : d == 5 ? 1 : d == 7 ? 2 : d == 9 ? 3 : 4;
-  if (count_hist) c->big_hist[di * 64 + std::min(sq, 63)] += cnt;
-  if (c->expm_alg != 0) return taylor_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, nA, count_hist);
-  const double* C = d == 3 ? hPade3 : d == 5 ? hPade5 : d == 7 ? hPade7 : d == 9 ? hPade9 : hPade13;
-  const double sc = std::ldexp(1.0, -sq);
-  GemmArgs g;
-  // buffers: 0 A, 1 A2, 2 A4, 3 A6, 4 T1/A8, 5 T2, 6 U', 7 V
-  g = gemm_args(N, N, N, cnt);
-  g.A = Asrc; g.B = Asrc; g.C1 = w(1); g.alpha1 = sc * sc;
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // A2
-  if (d == 13) {
-    g = gemm_args(N, N, N, cnt);
-    g.A = w(1); g.B = w(1); g.C1 = w(2);
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // A4
-    // A6 = A2 A4, with T1 = c13 A6 + c11 A4 + c9 A2 and T2 = c12 A6 + c10 A4 + c8 A2 from its epilogue
-    g.A = w(1); g.B = w(2); g.C1 = w(3); g.C2 = w(4); g.C3 = w(5);
-    g.nY = 2; g.Y[0] = w(2); g.Y[1] = w(1);
-    g.alpha2 = C[13]; g.w2[0] = C[11]; g.w2[1] = C[9];
-    g.alpha3 = C[12]; g.w3[0] = C[10]; g.w3[1] = C[8];
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-    g = gemm_args(N, N, N, cnt);
-    g.A = w(3); g.B = w(4); g.C1 = w(6);
-    g.nY = 3; g.Y[0] = w(3); g.Y[1] = w(2); g.Y[2] = w(1);
-    g.w1[0] = C[7]; g.w1[1] = C[5]; g.w1[2] = C[3]; g.gamma1 = C[1];
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // U' = A6 T1 + c7 A6 + c5 A4 + c3 A2 + c1 I
-    g.B = w(5); g.C1 = w(7);
-    g.w1[0] = C[6]; g.w1[1] = C[4]; g.w1[2] = C[2]; g.gamma1 = C[0];
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // V
-  } else {
-    // powers A^{2k} = A^{2k-2} A2 (oracle: P = P @ A2), buffers 1.. ; U', V as lincombs
-    const int npow = d / 2;  // number of even powers beyond I: d=3:1, 5:2, 7:3, 9:4
-    for (int k = 2; k <= npow; ++k) {
-      g = gemm_args(N, N, N, cnt);
-      g.A = w(k - 1); g.B = w(1); g.C1 = w(k);
-      if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-    }
-    LinArgs la;
-    std::memset(&la, 0, sizeof(la));
-    la.rows = N; la.cols = N; la.nitems = cnt; la.nt = npow;
-    for (int k = 1; k <= npow; ++k) la.Y[k - 1] = w(k);
-    la.out = w(6); la.dI = C[1];
-    for (int k = 1; k <= npow; ++k) la.w[k - 1] = C[2 * k + 1];
-    la.out2 = w(7); la.dI2 = C[0];
-    for (int k = 1; k <= npow; ++k) la.w2[k - 1] = C[2 * k];
-    if ((r = big_lincomb<T>(c, la))) return r;  // U', V in one pass
-  }
-  // U = (A/2^s) U';  P = V + U -> w1,  Q = V - U -> w2
-  g = gemm_args(N, N, N, cnt);
-  g.A = Asrc; g.B = w(6); g.C1 = w(1); g.C2 = w(2);
-  g.alpha1 = sc; g.alpha2 = -sc;
-  g.nY = 1; g.Y[0] = w(7); g.w1[0] = 1.0; g.w2[0] = 1.0;
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-  // Newton-Schulz for Q^{-1}:  Y0 = P / c0^2,  R = I - Q Y,  Y <- Y + Y R  (R_{k+1} = R_k^2).
-  // For A = -i H dt, P = conj-adjoint partner of Q and R0 = I - QP/c0^2 is tiny; ||R0||_F (computed
-  // in the GEMM epilogue) fixes the iteration count: smallest k with ||R0||^(2^k) <= tol.
-  const double c0sq = C[0] * C[0];
-  HIPCHK(c, hipMemsetAsync(red, 0, (size_t)cnt * sizeof(double), c->stream));
-  g = gemm_args(N, N, N, cnt);
-  g.A = w(2); g.B = w(1); g.C1 = w(3); g.alpha1 = -1.0 / c0sq; g.gamma1 = 1.0; g.sumsq = red;
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // R0 -> w3
-  std::vector<double> ss(cnt);
-  HIPCHK(c, hipMemcpyAsync(ss.data(), red, (size_t)cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  double e0 = 0.0;
-  for (double v : ss) e0 = std::max(e0, std::sqrt(v));
-  if (!(e0 < 0.9))
-    return fail(c, QOC_ERR_UNSUPPORTED,
-                "large-N solve: Newton-Schulz residual %.3g >= 0.9 (generators not skew-Hermitian?)", e0);
-  // stop once the residual bound is below the GEMMs' own rounding level (fp32 K=256 dot products
-  // carry ~1e-6 relative error; fp64 ~1e-15)
-  const double tol = c->prec == QOC_FP64 ? 1e-16 : 1e-7;
-  int iters = 1;
-  for (double e = e0 * e0; e > tol && iters < 8; e *= e) ++iters;
-  c->ns_iters += iters;
-  // Y1 = (P + P R0)/c0^2 -> w4
-  g = gemm_args(N, N, N, cnt);
-  g.A = w(1); g.B = w(3); g.C1 = w(4); g.alpha1 = 1.0 / c0sq;
-  g.nY = 1; g.Y[0] = w(1); g.w1[0] = 1.0 / c0sq;
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-  int cur = 4;
-  for (int it = 1; it < iters; ++it) {
-    g = gemm_args(N, N, N, cnt);
-    g.A = w(2); g.B = w(cur); g.C1 = w(3); g.alpha1 = -1.0; g.gamma1 = 1.0;
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // R = I - Q Y
-    const int nxt = cur == 4 ? 5 : 4;
-    g = gemm_args(N, N, N, cnt);
-    g.A = w(cur); g.B = w(3); g.C1 = w(nxt);
-    g.nY = 1; g.Y[0] = w(cur); g.w1[0] = 1.0;
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // Y <- Y + Y R
-    cur = nxt;
-  }
-  // X = Y P, then s squarings; the last product lands in d_U
-  g = gemm_args(N, N, N, cnt);
-  g.A = w(cur); g.B = w(1); g.C1 = sq == 0 ? dest : w(6);
-  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-  int xb = 6;
-  for (int q = 0; q < sq; ++q) {
-    const int nb = xb == 6 ? 7 : 6;
-    g = gemm_args(N, N, N, cnt);
-    g.A = w(xb); g.B = w(xb); g.C1 = q == sq - 1 ? dest : w(nb);
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-    xb = nb;
-  }
-  return QOC_OK;
-}
-
-// exp(A_k) for units [u0, u0+cnt) -> d_U (forms A_k from the generators, chunk max norm, then the GEMM expm)
-template <typename T>
-int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
-  const int N = c->N;
-  const size_t NN = (size_t)N * N, esz = c->esz;
-  cx<T>* a0 = (cx<T>*)c->d_ws;
-  HIPCHK(c, hipMemsetAsync(c->d_red, 0, sizeof(double), c->stream));
-  hipLaunchKernelGGL((k_form_norm<T>), dim3(cnt), dim3(256), 0, c->stream, N, c->nu, u0, (const cx<T>*)c->d_A,
-                     (const double*)c->d_u, a0, (unsigned long long*)c->d_red);
-  HIPCHK(c, hipGetLastError());
-  double nA = 0.0;
-  HIPCHK(c, hipMemcpyAsync(&nA, c->d_red, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return expm_gemm_chunk<T>(c, N, cnt, c->d_ws, (size_t)c->chunk, c->d_red, mk_opd(c->d_ws, 0, esz, (long long)NN),
-                            mk_opd(c->d_U, (size_t)u0 * NN, esz, (long long)NN), nA, true);
-}
-
-template <typename T>
-int big_forward(qoc_ctx* c) {
-  const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
-  const size_t NN = (size_t)N * N, Nm = (size_t)N * m, esz = c->esz;
-  const long long units = (long long)B * Nt;
-  int r;
-  int mk = mark_begin(c, 0);
-  for (long long u0 = 0; u0 < units; u0 += c->chunk) {
-    const int cnt = (int)std::min<long long>(c->chunk, units - u0);
-    if ((r = big_expm_chunk<T>(c, u0, cnt))) return r;
-  }
-  mark_end(c, mk);
-  mk = mark_begin(c, 1);
-  // x_0 for every seed
-  LinArgs la;
-  std::memset(&la, 0, sizeof(la));
-  la.rows = N; la.cols = m; la.nitems = B; la.nt = 1; la.w[0] = 1.0;
-  la.Y[0] = mk_opd(c->d_x0, 0, esz, c->x0_per_seed ? (long long)Nm : 0);
-  la.out = mk_opd(c->d_X, 0, esz, (long long)(Nt + 1) * Nm);
-  if ((r = big_lincomb<T>(c, la))) return r;
-  // x_{k+1} = U_k x_k, batched over seeds
-  for (int k = 0; k < Nt; ++k) {
-    GemmArgs g = gemm_args(N, N, m, B);
-    g.A = mk_opd(c->d_U, (size_t)k * NN, esz, (long long)Nt * NN);
-    g.B = mk_opd(c->d_X, (size_t)k * Nm, esz, (long long)(Nt + 1) * Nm);
-    g.C1 = mk_opd(c->d_X, (size_t)(k + 1) * Nm, esz, (long long)(Nt + 1) * Nm);
-    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
-  }
-  // costs
-  const bool pen = c->mu != 0.0;
-  if (pen) {
-    hipLaunchKernelGGL((k_penalty_sum<T>), dim3(B), dim3(256), 0, c->stream, N, m, Nt, (const cx<T>*)c->d_X,
-                       c->d_pmask, c->mu, c->d_J);
-    HIPCHK(c, hipGetLastError());
-  }
-  if (c->cost_kind != QOC_COST_EXTERNAL) {
-    hipLaunchKernelGGL((k_terminal_cost<T>), dim3(B), dim3(256), 0, c->stream, N, m, Nt, (const cx<T>*)c->d_X,
-                       (const cx<T>*)c->d_Xt, c->cost_kind, c->cost_n, pen ? 1 : 0, c->d_J, c->d_coef, sectors(c));
-    HIPCHK(c, hipGetLastError());
-  } else if (!pen) {
-    HIPCHK(c, hipMemsetAsync(c->d_J, 0, (size_t)B * sizeof(double), c->stream));
-  }
-  mark_end(c, mk);
-  return QOC_OK;
-}
-
-template <typename T>
-int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
-  const int N = c->N, m = c->m, Nt = c->Nt, B = c->B, nu = c->nu;
-  const size_t NN = (size_t)N * N, Nm = (size_t)N * m, esz = c->esz;
-  const bool pen = c->mu != 0.0;
-  const unsigned eb = (unsigned)std::min<size_t>((Nm * B + 255) / 256, 8192);
-  int r;
-  int mk = mark_begin(c, 2);
-  if (c->cost_kind != QOC_COST_EXTERNAL) {
-    hipLaunchKernelGGL((k_lambda_final<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, (const cx<T>*)c->d_Xt,
-                       (const cx<double>*)c->d_coef, (cx<T>*)c->d_L, sectors(c));
-    HIPCHK(c, hipGetLastError());
-  }
-  if (pen) {
-    hipLaunchKernelGGL((k_penalty_grad<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, Nt,
-                       (const cx<T>*)c->d_X, c->d_pmask, 2.0 * c->mu, (cx<T>*)c->d_L);
-    HIPCHK(c, hipGetLastError());
-  }
-  if (c->src_on) {
-    hipLaunchKernelGGL((k_add_source<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, Nt, (const cx<T>*)c->d_src,
-                       (cx<T>*)c->d_L);
-    HIPCHK(c, hipGetLastError());
-  }
-  // λ_k = U_k^H λ_{k+1} (+ dL/dx(x_k))
-  for (int k = Nt - 1; k >= 0; --k) {
-    GemmArgs g = gemm_args(N, N, m, B);
-    g.A = mk_opd(c->d_U, (size_t)k * NN, esz, (long long)Nt * NN);
-    g.B = mk_opd(c->d_L, (size_t)(k + 1) * Nm, esz, (long long)(Nt + 1) * Nm);
-    g.C1 = mk_opd(c->d_L, (size_t)k * Nm, esz, (long long)(Nt + 1) * Nm);
-    if ((r = big_gemm<T>(c, 1, 0, g))) return r;
-    if (pen) {
-      hipLaunchKernelGGL((k_penalty_grad<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, k,
-                         (const cx<T>*)c->d_X, c->d_pmask, 2.0 * c->mu, (cx<T>*)c->d_L);
-      HIPCHK(c, hipGetLastError());
-    }
-    if (c->src_on) {
-      hipLaunchKernelGGL((k_add_source<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, k, (const cx<T>*)c->d_src,
-                         (cx<T>*)c->d_L);
-      HIPCHK(c, hipGetLastError());
-    }
-  }
-  mark_end(c, mk);
-  mk = mark_begin(c, 3);
-  if (order == QOC_DUKDP_EXACT) {
-    r = frechet_grad<T>(c, d_dJdu);
-    mark_end(c, mk);
-    return r;
-  }
-  // gradient, per chunk of slice units
-  const long long units = (long long)B * Nt;
-  const int o = order;
-  const size_t C = (size_t)c->chunk;
-  const size_t offX = 0, offP = C * NN, offQ = offP + C * o * Nm, offW = offQ + C * (o > 1 ? o - 1 : 1) * Nm,
-               offM = offW + C * o * Nm;
-  static const double inv_fact[9] = {1.0, 1.0, 1.0 / 2, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720, 1.0 / 5040, 1.0 / 40320};
-  // Order 3 with m close to N: the same M' from the co-state/state outer product G = λ_{k+1} x_k^H,
-  //   M' = G + (Y G + G Y)/2 + (Y^2 G + Y G Y + G Y^2)/6,   Y = X^H,
-  // as five products (G: N^2 m flops; T1 = G Y, S = Y G + T1, R = T1 Y/6 + G + S/2, M' = Y S/6 + R: N^3 each)
-  // instead of seven N^2 m-GEMM equivalents; cheaper when 4 N < 6 m (synthetic: m = N).
-  bool sandwich = o == 3 && 4 * N < 6 * m;
-  if (const char* s = getenv("QOC_GRAD_SANDWICH")) sandwich = o == 3 && atoi(s) != 0;
-  for (long long u0 = 0; u0 < units; u0 += c->chunk) {
-    const int cnt = (int)std::min<long long>(c->chunk, units - u0);
-    hipLaunchKernelGGL((k_form_norm<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)c->d_A,
-                       (const double*)c->d_u, (cx<T>*)((char*)c->d_ws + offX * esz), (unsigned long long*)nullptr);
-    HIPCHK(c, hipGetLastError());
-    const Opd Xk = mk_opd(c->d_ws, offX, esz, (long long)NN);
-    if (sandwich) {  // workspace: X, then three N x N blocks per item (G / R, T1 / M', S) — 4 NN of the 8 NN
-      const size_t offG = C * NN, offT = 2 * C * NN, offS = 3 * C * NN;
-      const Opd Gk = mk_opd(c->d_ws, offG, esz, (long long)NN), Tk = mk_opd(c->d_ws, offT, esz, (long long)NN),
-                Sk = mk_opd(c->d_ws, offS, esz, (long long)NN);
-      GemmArgs g = gemm_args(N, m, N, cnt);  // G = λ x^H
-      g.A = mk_opd(c->d_L, Nm, esz, (long long)Nm, Nt, (long long)(Nt + 1) * Nm, (int)u0);
-      g.B = mk_opd(c->d_X, 0, esz, (long long)Nm, Nt, (long long)(Nt + 1) * Nm, (int)u0);
-      g.C1 = Gk;
-      if ((r = big_gemm<T>(c, 0, 1, g))) return r;
-      g = gemm_args(N, N, N, cnt);  // T1 = G X^H
-      g.A = Gk; g.B = Xk; g.C1 = Tk;
-      if ((r = big_gemm<T>(c, 0, 1, g))) return r;
-      g = gemm_args(N, N, N, cnt);  // S = X^H G + T1
-      g.A = Xk; g.B = Gk; g.C1 = Sk; g.nY = 1; g.Y[0] = Tk; g.w1[0] = 1.0;
-      if ((r = big_gemm<T>(c, 1, 0, g))) return r;
-      g = gemm_args(N, N, N, cnt);  // R = T1 X^H / 6 + G + S / 2   (over G, element-wise in the epilogue)
-      g.A = Tk; g.B = Xk; g.C1 = Gk; g.alpha1 = 1.0 / 6;
-      g.nY = 2; g.Y[0] = Gk; g.w1[0] = 1.0; g.Y[1] = Sk; g.w1[1] = 0.5;
-      if ((r = big_gemm<T>(c, 0, 1, g))) return r;
-      g = gemm_args(N, N, N, cnt);  // M' = X^H S / 6 + R   (over T1)
-      g.A = Xk; g.B = Sk; g.C1 = Tk; g.alpha1 = 1.0 / 6; g.nY = 1; g.Y[0] = Gk; g.w1[0] = 1.0;
-      if ((r = big_gemm<T>(c, 1, 0, g))) return r;
-      hipLaunchKernelGGL((k_gen_contract<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)c->d_A,
-                         (const cx<T>*)((char*)c->d_ws + offT * esz), d_dJdu);
-      HIPCHK(c, hipGetLastError());
-      continue;
-    }
-    auto Pa = [&](int a) { return mk_opd(c->d_ws, offP + a * Nm, esz, (long long)(o * Nm)); };
-    auto Qb = [&](int b) {  // Q_0 = λ_{k+1} in place; Q_b (b >= 1) in the workspace
-      if (b == 0) return mk_opd(c->d_L, Nm, esz, (long long)Nm, Nt, (long long)(Nt + 1) * Nm, (int)u0);
-      return mk_opd(c->d_ws, offQ + (b - 1) * Nm, esz, (long long)((o - 1) * Nm));
-    };
-    auto Wa = [&](int a) { return mk_opd(c->d_ws, offW + a * Nm, esz, (long long)(o * Nm)); };
-    const Opd xk = mk_opd(c->d_X, 0, esz, (long long)Nm, Nt, (long long)(Nt + 1) * Nm, (int)u0);
-    LinArgs la;
-    std::memset(&la, 0, sizeof(la));
-    if (o == 1) {
-      la.rows = N; la.cols = m; la.nitems = cnt; la.nt = 1; la.w[0] = 1.0;
-      la.Y[0] = xk; la.out = Pa(0);
-      if ((r = big_lincomb<T>(c, la))) return r;  // P_0 = x_k
-    }
-    for (int a = 1; a < o; ++a) {
-      GemmArgs g = gemm_args(N, N, m, cnt);
-      g.A = Xk; g.B = a == 1 ? xk : Pa(a - 1); g.C1 = Pa(a);
-      if (a == 1) {  // P_0 = x_k copied into the stacked P from this GEMM's epilogue
-        g.C2 = Pa(0); g.alpha2 = 0.0; g.nY = 1; g.Y[0] = xk; g.w2[0] = 1.0;
-      }
-      if ((r = big_gemm<T>(c, 0, 0, g))) return r;  // P_a = X P_{a-1}
-    }
-    if (o == 3) {
-      // Q_1 = X^H λ  (+ W_2 = λ/6 from the epilogue);  X^H Q_1 -> W_0 = λ + Q_1/2 + Q_2/6, W_1 = λ/2 + Q_1/6
-      GemmArgs g = gemm_args(N, N, m, cnt);
-      g.A = Xk; g.B = Qb(0); g.C1 = Qb(1);
-      g.C2 = Wa(2); g.alpha2 = 0.0; g.nY = 1; g.Y[0] = Qb(0); g.w2[0] = 1.0 / 6;
-      if ((r = big_gemm<T>(c, 1, 0, g))) return r;
-      g = gemm_args(N, N, m, cnt);
-      g.A = Xk; g.B = Qb(1);
-      g.nY = 2; g.Y[0] = Qb(0); g.Y[1] = Qb(1);
-      g.C1 = Wa(0); g.alpha1 = 1.0 / 6; g.w1[0] = 1.0; g.w1[1] = 0.5;
-      g.C2 = Wa(1); g.alpha2 = 0.0; g.w2[0] = 0.5; g.w2[1] = 1.0 / 6;
-      if ((r = big_gemm<T>(c, 1, 0, g))) return r;
-    } else {
-    for (int b = 1; b < o; ++b) {
-      GemmArgs g = gemm_args(N, N, m, cnt);
-      g.A = Xk; g.B = Qb(b - 1); g.C1 = Qb(b);
-      if ((r = big_gemm<T>(c, 1, 0, g))) return r;  // Q_b = X^H Q_{b-1}
-    }
-    for (int a = 0; a < o; a += 2) {  // W_a = sum_b Q_b/(a+b+1)!, two W's per pass
-      std::memset(&la, 0, sizeof(la));
-      la.rows = N; la.cols = m; la.nitems = cnt; la.nt = o - a;
-      for (int b = 0; b < o - a; ++b) {
-        la.Y[b] = Qb(b);
-        la.w[b] = inv_fact[a + b + 1];
-        la.w2[b] = b < o - a - 1 ? inv_fact[a + b + 2] : 0.0;
-      }
-      la.out = Wa(a);
-      if (a + 1 < o) la.out2 = Wa(a + 1);
-      if ((r = big_lincomb<T>(c, la))) return r;
-    }
-    }
-    GemmArgs g = gemm_args(N, o * m, N, cnt);
-    g.A = mk_opd(c->d_ws, offW, esz, (long long)(o * Nm));
-    g.B = mk_opd(c->d_ws, offP, esz, (long long)(o * Nm));
-    g.C1 = mk_opd(c->d_ws, offM, esz, (long long)NN);
-    if ((r = big_gemm<T>(c, 0, 1, g))) return r;  // M' = W P^H
-    hipLaunchKernelGGL((k_gen_contract<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)c->d_A,
-                       (const cx<T>*)((char*)c->d_ws + offM * esz), d_dJdu);
-    HIPCHK(c, hipGetLastError());
-  }
-  mark_end(c, mk);
-  return QOC_OK;
-}
-
-// Order-3 gradient of the LDS-resident path as GEMMs over every (seed, slice) at once.  With the state
-// matrix Xall = [x_0 .. x_Nt] of all seeds (N x B(Nt+1)m, the d_X buffer as is) and
-// X_k v = A0 v + sum_j u_jk A_j v = [A0 | A1 | ...] [v; u_1k v; ...]:
-//   P1 = X Xall, P2 = X P1, Q1 = X^H Lsh (Lsh = λ_{k+1} columns), and from the epilogues
-//   W2 = λ/6, W0 = λ + Q1/2 + Q2/6, W1 = λ/2 + Q1/6 (Q2 = X^H Q1 is never stored);
-//   dJdu[k, j] = sum_a Re<W_a, A_j P_a>  (k_bgemm MODE 2 epilogue, [A1; A2; ...] x P_a).
-// Same contraction as k_grad / the reference's expm_jacobian! order 3, on MFMA with the generators
-// shared by every GEMM.
-template <typename T>
-int grad_gemm_o3(qoc_ctx* c, double* d_dJdu) {
-  const int N = c->N, m = c->m, nu = c->nu, Nt = c->Nt;
-  const size_t Nm = (size_t)N * m, esz = c->esz;
-  const long long cols = (long long)c->B * (Nt + 1) * m - m;  // the last seed's x_Nt column block is unused
-  const size_t bufN = (size_t)N * ((size_t)c->B * (Nt + 1) * m);
-  auto buf = [&](int i) { return mk_opd(c->d_gws, (size_t)i * bufN, esz, 0); };
-  const Opd Xall = mk_opd(c->d_X, 0, esz, 0), Lsh = mk_opd(c->d_L, Nm, esz, 0);
-  const Opd P1 = buf(0), P2 = buf(1), Q1 = buf(2), W0 = buf(3), W1 = buf(4), W2 = buf(5);
-  HIPCHK(c, hipMemsetAsync(d_dJdu, 0, (size_t)c->B * Nt * nu * sizeof(double), c->stream));
-  auto comb = [&](const void* Gmat, const Opd& Bsrc) {
-    GemmArgs g = gemm_args(N, (nu + 1) * N, (int)cols, 1);
-    g.A = mk_opd(Gmat, 0, esz, 0);
-    g.B = Bsrc;
-    g.uc = c->d_u;
-    g.kb = N;
-    g.cm = m;
-    g.sps = Nt + 1;
-    g.cNt = Nt;
-    g.cnu = nu;
-    return g;
-  };
-  int r;
-  GemmArgs g = comb(c->d_A, Xall);
-  g.C1 = P1;
-  if ((r = big_gemm<T>(c, 0, 0, g, 1))) return r;  // P1 = X x
-  g = comb(c->d_A, P1);
-  g.C1 = P2;
-  if ((r = big_gemm<T>(c, 0, 0, g, 1))) return r;  // P2 = X P1
-  g = comb(c->d_AH, Lsh);
-  g.C1 = Q1;
-  g.C2 = W2; g.alpha2 = 0.0; g.nY = 1; g.Y[0] = Lsh; g.w2[0] = 1.0 / 6;
-  if ((r = big_gemm<T>(c, 0, 0, g, 1))) return r;  // Q1 = X^H λ, W2 = λ/6
-  g = comb(c->d_AH, Q1);
-  g.nY = 2; g.Y[0] = Lsh; g.Y[1] = Q1;
-  g.C1 = W0; g.alpha1 = 1.0 / 6; g.w1[0] = 1.0; g.w1[1] = 0.5;
-  g.C2 = W1; g.alpha2 = 0.0; g.w2[0] = 0.5; g.w2[1] = 1.0 / 6;
-  if ((r = big_gemm<T>(c, 0, 0, g, 1))) return r;  // W0, W1 (Q2 consumed in the epilogue)
-  const Opd Pa[3] = {Xall, P1, P2}, Wa[3] = {W0, W1, W2};
-  for (int a = 0; a < 3; ++a) {
-    GemmArgs h = gemm_args(nu * N, N, (int)cols, 1);
-    h.A = mk_opd(c->d_Cst, 0, esz, 0);
-    h.B = Pa[a];
-    h.C1 = Pa[a];  // not written in MODE 2
-    h.kb = N;
-    h.cm = m;
-    h.sps = Nt + 1;
-    h.cNt = Nt;
-    h.cnu = nu;
-    h.dot = d_dJdu;
-    h.Wd = Wa[a];
-    if ((r = big_gemm<T>(c, 0, 0, h, 2))) return r;  // dJdu += Re<W_a, A_j P_a>
-  }
-  return QOC_OK;
-}
-
-// Fused order-3 gradient (qoc_grad_rr.hpp): k_grad_rr_q (co-state side -> W0, W1 in the state layout)
-// then k_grad_rr_p (state side + contraction -> dJdu).  Persistent grids of 4-wave workgroups.
-template <typename T, int NT, int KS, int NU>
-int grad_rr_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode) {
-  using G = GradRR<T, NT>;
-  const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
-  const size_t lds = G::lds_bytes(N, NU);
-  const long long units = (long long)B * nk, ntiles = (units + 16 / m - 1) / (16 / m);
-  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
-  const int grid = (int)std::max<long long>(1, std::min<long long>((ntiles + 3) / 4, (long long)c->ncu * per_cu));
-  const size_t bufN = (size_t)N * ((size_t)B * (Nt + 1) * m);
-  cx<T>* W0 = (cx<T>*)c->d_gws;
-  cx<T>* W1 = W0 + bufN;
-  // mode 0: q + p;  1: state side only (k_grad_rr_s -> P1, P2 in d_pws);  2: q + p reading P1, P2
-  cx<T>* P1 = (cx<T>*)c->d_pws;
-  cx<T>* P2 = P1 ? P1 + bufN : nullptr;
-  if (mode == 1) {
-    HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_s<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((k_grad_rr_s<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
-                       (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, P1, P2);
-    HIPCHK(c, hipGetLastError());
-    return QOC_OK;
-  }
-  HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_q<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((k_grad_rr_q<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
-                     (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_L, W0, W1);
-  HIPCHK(c, hipGetLastError());
-  if (mode == 2) {
-    HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_p<T, NT, KS, NU, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((k_grad_rr_p<T, NT, KS, NU, true>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
-                       (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, (const cx<T>*)W0,
-                       (const cx<T>*)W1, d_dJdu, (const cx<T>*)P1, (const cx<T>*)P2);
-  } else {
-    HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_p<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((k_grad_rr_p<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
-                       (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, (const cx<T>*)W0,
-                       (const cx<T>*)W1, d_dJdu);
-  }
-  HIPCHK(c, hipGetLastError());
-  return QOC_OK;
-}
-
-template <typename T, int NT, int NU>
-int grad_rr_nt(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode) {
-  const int ks = sizeof(T) == 8 ? (c->N + 3) / 4 : 4 * NT;
-  if constexpr (sizeof(T) == 8) {
-    if (ks == 4 * NT - 3) return grad_rr_launch<T, NT, 4 * NT - 3, NU>(c, d_dJdu, st, k0, nk, mode);
-    if (ks == 4 * NT - 2) return grad_rr_launch<T, NT, 4 * NT - 2, NU>(c, d_dJdu, st, k0, nk, mode);
-    if (ks == 4 * NT - 1) return grad_rr_launch<T, NT, 4 * NT - 1, NU>(c, d_dJdu, st, k0, nk, mode);
-  }
-  return grad_rr_launch<T, NT, 4 * NT, NU>(c, d_dJdu, st, k0, nk, mode);
-}
-
-template <typename T>
-int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode) {
-  const int NT = (c->N + 15) / 16;
-  if (c->nu == 1) {
-    if (NT == 1) return grad_rr_nt<T, 1, 1>(c, d_dJdu, st, k0, nk, mode);
-    if (NT == 2) return grad_rr_nt<T, 2, 1>(c, d_dJdu, st, k0, nk, mode);
-    return grad_rr_nt<T, 3, 1>(c, d_dJdu, st, k0, nk, mode);
-  }
-  if (NT == 1) return grad_rr_nt<T, 1, 2>(c, d_dJdu, st, k0, nk, mode);
-  if (NT == 2) return grad_rr_nt<T, 2, 2>(c, d_dJdu, st, k0, nk, mode);
-  return grad_rr_nt<T, 3, 2>(c, d_dJdu, st, k0, nk, mode);
-}
-
-// Exact gradient (QOC_DUKDP_EXACT): one Fréchet derivative per slice from the 2N x 2N block exponential
-// (qoc_frechet.hpp), k_expm when 2N fits the LDS-resident kernel, the GEMM pipeline otherwise.
-template <typename T>
-int frechet_grad(qoc_ctx* c, double* d_dJdu) {
-  const int N = c->N, n2 = 2 * N, nu = c->nu;
-  const size_t NN = (size_t)N * N, BB = (size_t)n2 * n2, esz = c->esz;
-  const long long units = (long long)c->B * c->Nt;
-  const bool small = expm_supported(n2, c->prec);
-  const size_t per_item = (small ? 2 : 10) * BB * esz + 3 * sizeof(double);
-  size_t freeb = 0, totalb = 0;
-  (void)hipMemGetInfo(&freeb, &totalb);
-  const size_t budget = std::min<size_t>(4ull << 30, std::max<size_t>(freeb / 8, per_item));
-  const int fch = (int)std::max<long long>(1, std::min<long long>({(long long)(budget / per_item), units, 16384LL}));
-  const size_t need = (size_t)fch * per_item + nu * NN * esz + 64 * sizeof(double);
-  if (c->fws_bytes < need) {
-    if (c->d_fws) HIPCHK(c, hipFree(c->d_fws));
-    c->d_fws = nullptr;
-    c->fws_bytes = 0;
-    HIPCHK(c, hipMalloc(&c->d_fws, need));
-    c->fws_bytes = need;
-  }
-  char* p = (char*)c->d_fws;
-  cx<T>* blocks = (cx<T>*)p;
-  p += (size_t)fch * BB * esz;
-  cx<T>* E = (cx<T>*)p;
-  p += (size_t)fch * BB * esz;
-  void* ws = nullptr;
-  if (!small) {
-    ws = p;
-    p += 8 * (size_t)fch * BB * esz;
-  }
-  cx<T>* At = (cx<T>*)p;
-  p += nu * NN * esz;
-  double* alpha = (double*)p;
-  p += (size_t)fch * sizeof(double);
-  double* red = (double*)p;  // fch + 8 doubles
-  hipLaunchKernelGGL((k_transpose_gens<T>), dim3(256), dim3(256), 0, c->stream, N, nu, (const cx<T>*)c->d_A, At);
-  HIPCHK(c, hipGetLastError());
-  int r;
-  for (long long u0 = 0; u0 < units; u0 += fch) {
-    const int cnt = (int)std::min<long long>(fch, units - u0);
-    hipLaunchKernelGGL((k_frechet_build<T>), dim3(cnt), dim3(256), 0, c->stream, N, c->m, nu, c->Nt, u0,
-                       (const cx<T>*)c->d_A, (const double*)c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L,
-                       blocks, alpha);
-    HIPCHK(c, hipGetLastError());
-    if (small) {
-      hipError_t e = launch_expm(c->prec, c->stream, n2, 0, cnt, nullptr, nullptr, blocks, E, nullptr, nullptr, nullptr,
-                                 c->expm_alg, nullptr, c->d_ps);
-      if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_expm (Frechet block): %s", hipGetErrorString(e));
-    } else {
-      HIPCHK(c, hipMemsetAsync(red, 0, sizeof(double), c->stream));
-      hipLaunchKernelGGL((k_norm1_max<T>), dim3(cnt), dim3(256), 0, c->stream, n2, (const cx<T>*)blocks,
-                         (unsigned long long*)red);
-      HIPCHK(c, hipGetLastError());
-      double nA = 0.0;
-      HIPCHK(c, hipMemcpyAsync(&nA, red, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      if ((r = expm_gemm_chunk<T>(c, n2, cnt, ws, (size_t)fch, red, mk_opd(blocks, 0, esz, (long long)BB),
-                                  mk_opd(E, 0, esz, (long long)BB), nA, false)))
-        return r;
-    }
-    hipLaunchKernelGGL((k_frechet_contract<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)At,
-                       (const cx<T>*)E, (const double*)alpha, d_dJdu);
-    HIPCHK(c, hipGetLastError());
-  }
-  return QOC_OK;
-}
-
-// ---- ODE path (fixed-step Tsit5, qoc_ode.hpp) ------------------------------------------------
-// k_ode_pwc instantiation by N: register-resident rows up to 48 (fp64) / 64 (fp32), LDS beyond
-template <typename T>
-void launch_ode_pwc(qoc_ctx* c, int adjoint, cx<T>* S, const unsigned char* pmask, double two_mu) {
-  const int N = c->N, W = std::min(c->m, 4);
-  const size_t lds = (((size_t)N * N * c->esz + 15) & ~(size_t)15) + (size_t)W * 64 * c->esz;
-  auto go = [&](auto kern) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(c->B), dim3(64 * W), lds, c->stream, N, c->m, c->nu, c->Nt, c->nsub, adjoint,
-                       (const cx<T>*)c->d_A, (const double*)c->d_u, (const cx<T>*)c->d_x0, c->x0_per_seed, S,
-                       (const cx<T>*)c->d_X, pmask, two_mu);
-  };
-  if (c->ode_kernel == 1) go(k_ode_pwc<T, 0>);
-  else if (N <= 16) go(k_ode_pwc<T, 16>);
-  else if (N <= 32) go(k_ode_pwc<T, 32>);
-  else if (N <= 48) go(k_ode_pwc<T, 48>);
-  else if (sizeof(T) == 4) go(k_ode_pwc<T, 64>);
-  else go(k_ode_pwc<T, 0>);
-}
-
-template <typename T>
-int ode_forward(qoc_ctx* c) {
-  int mk = mark_begin(c, 1);
-  launch_ode_pwc<T>(c, 0, (cx<T>*)c->d_X, nullptr, 0.0);
-  HIPCHK(c, hipGetLastError());
-  const bool pen = c->mu != 0.0;
-  if (pen) {
-    hipLaunchKernelGGL((k_penalty_sum<T>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
-                       (const cx<T>*)c->d_X, c->d_pmask, c->mu, c->d_J);
-    HIPCHK(c, hipGetLastError());
-  }
-  if (c->cost_kind != QOC_COST_EXTERNAL) {
-    hipLaunchKernelGGL((k_terminal_cost<T>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
-                       (const cx<T>*)c->d_X, (const cx<T>*)c->d_Xt, c->cost_kind, c->cost_n, pen ? 1 : 0, c->d_J,
-                       c->d_coef, sectors(c));
-    HIPCHK(c, hipGetLastError());
-  } else if (!pen) {
-    HIPCHK(c, hipMemsetAsync(c->d_J, 0, (size_t)c->B * sizeof(double), c->stream));
-  }
-  mark_end(c, mk);
-  return QOC_OK;
-}
-
-template <typename T>
-int ode_adjoint(qoc_ctx* c) {
-  const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
-  const size_t Nm = (size_t)N * m;
-  const bool pen = c->mu != 0.0;
-  const unsigned eb = (unsigned)std::min<size_t>((Nm * B + 255) / 256, 8192);
-  int mk = mark_begin(c, 2);
-  if (c->cost_kind != QOC_COST_EXTERNAL) {
-    hipLaunchKernelGGL((k_lambda_final<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, (const cx<T>*)c->d_Xt,
-                       (const cx<double>*)c->d_coef, (cx<T>*)c->d_L, sectors(c));
-    HIPCHK(c, hipGetLastError());
-  }
-  if (pen) {
-    hipLaunchKernelGGL((k_penalty_grad<T>), dim3(eb), dim3(256), 0, c->stream, N, m, Nt, B, Nt,
-                       (const cx<T>*)c->d_X, c->d_pmask, 2.0 * c->mu, (cx<T>*)c->d_L);
-    HIPCHK(c, hipGetLastError());
-  }
-  launch_ode_pwc<T>(c, 1, (cx<T>*)c->d_L, pen ? c->d_pmask : nullptr, 2.0 * c->mu);
-  HIPCHK(c, hipGetLastError());
-  mark_end(c, mk);
-  return QOC_OK;
-}
-
-// ---- Taylor-action chains (qoc_tchain.hpp) -----------------------------------------------------
-size_t tchain_lds(const qoc_ctx* c) {
-  const TShape sh = tchain_shape(c->N, c->m, c->prec == QOC_FP64);
-  return (size_t)(c->nu + 1) * c->N * c->N * c->esz + (size_t)2 * sh.S * sh.JT * chain_mpad(c->m, sh.CB) * c->esz +
-         64 * sizeof(double);
-}
-
-// k_tchain_* instantiated per (S, JT) x (CB, NP) in {(1, 1), (2, 1), (2, 2), (2, 4)}.
-template <typename T, typename F>
-hipError_t tchain_dispatch(int N, int m, F&& f) {
-  using std::integral_constant;
-  const TShape sh = tchain_shape(N, m, sizeof(T) == 8);
-  auto cbnp = [&](auto S_, auto JT_) -> hipError_t {
-    if (sh.CB == 1 && sh.NP == 1) return f(S_, JT_, integral_constant<int, 1>(), integral_constant<int, 1>());
-    if (sh.CB == 2 && sh.NP == 1) return f(S_, JT_, integral_constant<int, 2>(), integral_constant<int, 1>());
-    if (sh.CB == 2 && sh.NP == 2) return f(S_, JT_, integral_constant<int, 2>(), integral_constant<int, 2>());
-    if (sh.CB == 2 && sh.NP == 4) return f(S_, JT_, integral_constant<int, 2>(), integral_constant<int, 4>());
-    return hipErrorInvalidValue;
-  };
-  if (sh.JT == 4)
-    return sh.S == 4 ? cbnp(integral_constant<int, 4>(), integral_constant<int, 4>())
-                     : cbnp(integral_constant<int, 8>(), integral_constant<int, 4>());
-  if (sh.JT == 10) return cbnp(integral_constant<int, 4>(), integral_constant<int, 10>());
-  if (sh.JT == 12) return cbnp(integral_constant<int, 4>(), integral_constant<int, 12>());
-  if constexpr (sizeof(T) == 4) {
-    if (sh.JT == 16) return cbnp(integral_constant<int, 4>(), integral_constant<int, 16>());
-  }
-  return hipErrorInvalidValue;
-}
-
-TChainArgs tchain_args(qoc_ctx* c) {
-  TChainArgs g{};
-  g.N = c->N;
-  g.m = c->m;
-  g.nu = c->nu;
-  g.Nt = c->Nt;
-  g.At = c->d_At;
-  g.u = c->d_u;
-  g.steps = c->d_steps;
-  g.x0 = c->d_x0;
-  g.x0_per_seed = c->x0_per_seed;
-  g.X = c->d_X;
-  g.L = c->d_L;
-  g.Xt = c->d_Xt;
-  g.cost_kind = c->cost_kind;
-  g.n_norm = c->cost_n;
-  g.pmask = c->mu != 0.0 ? c->d_pmask : nullptr;
-  g.mu = c->mu;
-  g.J = c->d_J;
-  g.coef = c->d_coef;
-  g.src = c->src_on ? c->d_src : nullptr;
-  g.tcoef = c->d_tcoef;
-  g.sc = sectors(c);
-  g.k_lo = 0;
-  g.k_hi = c->Nt;
-  return g;
-}
-
-// fp64: the MFMA formulation (k_tchain_mf_*), one wave per (16-row block, column pair); fp32: the VALU one.
-bool tchain_mf(const qoc_ctx* c) {
-  return c->prec == QOC_FP64 && tchain_mf_kq(c->N) > 0 && tchain_mf_waves(c->N, c->m) <= 16 &&
-         tchain_mf_lds(c->N, c->m, c->nu) <= 160 * 1024;
-}
-template <typename F>
-hipError_t tchain_mf_dispatch(int N, F&& f) {
-  using std::integral_constant;
-  switch (tchain_mf_kq(N)) {
-    case 3: return f(integral_constant<int, 3>());
-    case 4: return f(integral_constant<int, 4>());
-    case 6: return f(integral_constant<int, 6>());
-    case 8: return f(integral_constant<int, 8>());
-    case 10: return f(integral_constant<int, 10>());
-    case 12: return f(integral_constant<int, 12>());
-  }
-  return hipErrorInvalidValue;
-}
-
-template <typename T>
-int tchain_forward(qoc_ctx* c) {
-  const long long units = (long long)c->B * c->Nt;
-  const bool cheb = c->cheb && tchain_mf(c);
-  if (cheb && !c->d_tcoef) {
-    const size_t bytes = (size_t)units * TCHEB_STRIDE * sizeof(double);
-    HIPCHK(c, hipMalloc((void**)&c->d_tcoef, bytes));
-    c->dev_bytes += bytes;
-  }
-  int mk = mark_begin(c, 0);
-  const unsigned pb = (unsigned)std::min<long long>((units + 255) / 256, 2048);
-  if (cheb)
-    hipLaunchKernelGGL(k_tchain_prep_cheb, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u,
-                       c->tprm, c->d_steps, c->d_tcoef, c->d_terms);
-  else
-    hipLaunchKernelGGL(k_tchain_prep, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u, c->tprm,
-                       c->d_steps, c->d_terms);
-  mark_end(c, mk);
-  HIPCHK(c, hipGetLastError());
-  c->cheb_ran = cheb;
-  const TChainArgs g = tchain_args(c);
-  if (tchain_mf(c)) {
-    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
-    const int threads = 64 * tchain_mf_waves(c->N, c->m);
-    mk = mark_begin(c, 1);
-    hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
-      constexpr int KQ = decltype(KQ_)::value;
-      const int mt = tchain_mf_maxt(c->N, c->m, c->nu);
-      auto kern = mt == 256   ? (cheb ? k_tchain_mf_fwd<KQ, true, 256> : k_tchain_mf_fwd<KQ, false, 256>)
-                  : mt == 512 ? (cheb ? k_tchain_mf_fwd<KQ, true, 512> : k_tchain_mf_fwd<KQ, false, 512>)
-                              : (cheb ? k_tchain_mf_fwd<KQ, true, 1024> : k_tchain_mf_fwd<KQ, false, 1024>);
-      hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (r != hipSuccess) return r;
-      hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);
-      return hipGetLastError();
-    });
-    mark_end(c, mk);
-    if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_mf_fwd launch: %s", hipGetErrorString(e));
-    c->props_since_reset++;
-    return QOC_OK;
-  }
-  const size_t lds = tchain_lds(c);
-  mk = mark_begin(c, 1);
-  hipError_t e = tchain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_, auto NP_) {
-    constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value,
-                  NP = decltype(NP_)::value;
-    hipError_t r = hipFuncSetAttribute((const void*)k_tchain_fwd<T, S, JT, CB, NP>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (r != hipSuccess) return r;
-    hipLaunchKernelGGL((k_tchain_fwd<T, S, JT, CB, NP>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, g);
-    return hipGetLastError();
-  });
-  mark_end(c, mk);
-  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_fwd launch: %s", hipGetErrorString(e));
-  c->props_since_reset++;
-  return QOC_OK;
-}
-
-template <typename T>
-int tchain_backward(qoc_ctx* c, int k_lo, int k_hi) {
-  TChainArgs g = tchain_args(c);
-  if (tchain_mf(c)) {
-    if (k_hi >= 0) {  // a range of slices (tchain_backward_overlapped)
-      g.k_lo = k_lo;
-      g.k_hi = k_hi;
-      g.prio = c->bwd_prio & 1;
-    }
-    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
-    const int threads = 64 * tchain_mf_waves(c->N, c->m);
-    int mk = mark_begin(c, 2);
-    hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
-      constexpr int KQ = decltype(KQ_)::value;
-      // the (P, s, coefficients) of the forward pass are reused: the same polynomial as the states'
-      const int mt = tchain_mf_maxt(c->N, c->m, c->nu);
-      auto kern = mt == 256   ? (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 256> : k_tchain_mf_bwd<KQ, false, 256>)
-                  : mt == 512 ? (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 512> : k_tchain_mf_bwd<KQ, false, 512>)
-                              : (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 1024> : k_tchain_mf_bwd<KQ, false, 1024>);
-      hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (r != hipSuccess) return r;
-      hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);
-      return hipGetLastError();
-    });
-    mark_end(c, mk);
-    if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_mf_bwd launch: %s", hipGetErrorString(e));
-    return QOC_OK;
-  }
-  const size_t lds = tchain_lds(c);
-  int mk = mark_begin(c, 2);
-  hipError_t e = tchain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_, auto NP_) {
-    constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value,
-                  NP = decltype(NP_)::value;
-    hipError_t r = hipFuncSetAttribute((const void*)k_tchain_bwd<T, S, JT, CB, NP>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (r != hipSuccess) return r;
-    hipLaunchKernelGGL((k_tchain_bwd<T, S, JT, CB, NP>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, g);
-    return hipGetLastError();
-  });
-  mark_end(c, mk);
-  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_bwd launch: %s", hipGetErrorString(e));
-  return QOC_OK;
-}
-
-// Backward chain in slice ranges with the gradient of each finished range on a second stream: the order-3
-// gradient of slices [k_lo, k_hi) needs only x_k and λ_{k+1}, so it runs while the chain works on the
-// next range (lower k).  The chain's workgroup (3 waves, ~84 KB LDS, <= 264 VGPRs at N = 40) leaves room on
-// each CU for one gradient workgroup, whose waves take the chain's MFMA idle cycles.  Chunk boundaries are
-// uniform in k except the last (exposed) range, bwd_last_frac of a uniform one.
-template <typename T>
-int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu) {
-  const int Nt = c->Nt, S = std::min(c->bwd_chunks, std::max(1, Nt / 32));  // ranges of >= ~32 slices
-  if (!c->stream2) {
-    int lo = 0, hi = 0;
-    HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIPCHK(c, hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, (c->bwd_prio & 2) ? lo : 0));
-  }
-  while ((int)c->sync_ev.size() < S + 2) {
-    hipEvent_t e;
-    HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    c->sync_ev.push_back(e);
-  }
-  // k boundaries: kb[0] = Nt > kb[1] > ... > kb[S] = 0; the last range is shorter
-  std::vector<int> kb(S + 1);
-  const double last = std::max(0.05, std::min(1.0, c->bwd_last_frac)), w = Nt / (S - 1 + last);
-  for (int i = 0; i <= S; ++i) kb[i] = std::max(0, Nt - (int)std::lround(i * w));
-  kb[S] = 0;
-  // state side first (QOC_BWD_PRESTATE): P1 = X x_k, P2 = X P1 of every slice need only the forward's states, so
-  // they run beside the first range, which otherwise has nothing beside it; each range then runs q + p (PRE).
-  const size_t pws = (size_t)2 * c->N * c->B * (Nt + 1) * c->m * c->esz;
-  // auto: only when a CU keeps room beside its chain waves (<= 3 per CU, or small N whose chain waves are
-  // light); measured: cavity (3 waves/CU) +1.3 %, zz +0.9 %, tunable bus (2 WGs x 2 waves/CU) -2.6 %
-  const long long chain_waves = (long long)((c->B + c->ncu - 1) / c->ncu) * tchain_mf_waves(c->N, c->m);
-  const bool pre = c->bwd_prestate == 1 || (c->bwd_prestate == 2 && (chain_waves <= 3 || c->N <= 16));
-  if (pre && c->pws_bytes < pws) {
-    if (c->d_pws) HIPCHK(c, hipFree(c->d_pws));
-    c->d_pws = nullptr;
-    c->pws_bytes = 0;
-    HIPCHK(c, hipMalloc(&c->d_pws, pws));
-    c->pws_bytes = pws;
-    c->dev_bytes += pws;
-  }
-  HIPCHK(c, hipEventRecord(c->sync_ev[S], c->stream));  // stream2 starts after everything queued so far
-  HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[S], 0));
-  if (pre) {
-    const int mk = mark_begin(c, 3, c->stream2);
-    const int r = grad_rr_o3<T>(c, d_dJdu, c->stream2, 0, Nt, 1);
-    mark_end(c, mk, c->stream2);
-    if (r) return r;
-  }
-  for (int i = 0; i < S; ++i) {
-    if (kb[i + 1] >= kb[i]) continue;
-    int r = tchain_backward<T>(c, kb[i + 1], kb[i]);
-    if (r) return r;
-    HIPCHK(c, hipEventRecord(c->sync_ev[i], c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[i], 0));
-    const int mk = mark_begin(c, 3, c->stream2);
-    r = grad_rr_o3<T>(c, d_dJdu, c->stream2, kb[i + 1], kb[i] - kb[i + 1], pre ? 2 : 0);
-    mark_end(c, mk, c->stream2);
-    if (r) return r;
-  }
-  HIPCHK(c, hipEventRecord(c->sync_ev[S + 1], c->stream2));
-  HIPCHK(c, hipStreamWaitEvent(c->stream, c->sync_ev[S + 1], 0));
-  return QOC_OK;
 }
 
 // Taylor-tail thresholds: θ_P = largest β with Σ_{t>P} β^t / t! <= tol.
@@ -1796,17 +342,14 @@ int check_ready(qoc_ctx* c) {
   return QOC_OK;
 }
 
-}  // namespace
+}  // namespace qoc_host
 
-#ifndef QOC_SOURCE_HASH
-#define QOC_SOURCE_HASH "unknown"
-#endif
+using namespace qoc_host;
+
 
 extern "C" {
 
 const char* qoc_last_error(const qoc_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
-
-const char* qoc_source_hash(void) { return QOC_SOURCE_HASH; }
 
 int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, int precision) {
   if (!out) return fail(nullptr, QOC_ERR_ARG, "out is null");
@@ -1999,16 +542,7 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
     r = upload(c, Aj[j], (char*)c->d_A + (j + 1) * NN * c->esz, NN);
   }
   if (r != QOC_OK) return r;
-  if (c->d_AH) {
-    const unsigned blocks = (unsigned)std::min<size_t>(((c->nu + 1) * NN + 255) / 256, 2048);
-    if (c->prec == QOC_FP64)
-      hipLaunchKernelGGL((k_gen_aux<double>), dim3(blocks), dim3(256), 0, c->stream, c->N, c->nu,
-                         (const cx<double>*)c->d_A, (cx<double>*)c->d_AH, (cx<double>*)c->d_Cst);
-    else
-      hipLaunchKernelGGL((k_gen_aux<float>), dim3(blocks), dim3(256), 0, c->stream, c->N, c->nu,
-                         (const cx<float>*)c->d_A, (cx<float>*)c->d_AH, (cx<float>*)c->d_Cst);
-    HIPCHK(c, hipGetLastError());
-  }
+  if (c->d_AH) HIPCHK(c, launch_gen_aux(c));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   {  // ||A0||_1 (host copy): selects the one-pass k_expm_rr_mix when every slice has large norm anyway
     double nrm = 0.0;
@@ -2546,37 +1080,11 @@ int qoc_propagate_envelope(qoc_ctx* c, int kind, const double* params, int np, d
   const long long nsteps = (long long)std::llround(tgate / dt);
   const size_t env_lds = (size_t)(c->nu + 1) * c->N * c->N * c->esz;
   if (env_lds > 160 * 1024) return fail(c, QOC_ERR_UNSUPPORTED, "generators (%zu B) exceed the 160 KiB LDS", env_lds);
-  if (c->prec == QOC_FP64)
-    HIPCHK(c, hipFuncSetAttribute((const void*)k_ode_envelope<double>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)env_lds));
-  else
-    HIPCHK(c, hipFuncSetAttribute((const void*)k_ode_envelope<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)env_lds));
   double* dP = nullptr;
   HIPCHK(c, hipMalloc((void**)&dP, (size_t)c->B * np * sizeof(double)));
   hipError_t e = hipMemcpy(dP, params, (size_t)c->B * np * sizeof(double), hipMemcpyHostToDevice);
-  if (e == hipSuccess) {
-    const int W = std::min(c->m, 4);
-    const size_t lds = env_lds;
-    if (c->prec == QOC_FP64)
-      hipLaunchKernelGGL((k_ode_envelope<double>), dim3(c->B), dim3(64 * W), lds, c->stream, c->N, c->m, c->nu, c->Nt,
-                         kind, (const double*)dP, np, dt, nsteps, (const cx<double>*)c->d_A,
-                         (const cx<double>*)c->d_x0, c->x0_per_seed, (cx<double>*)c->d_X);
-    else
-      hipLaunchKernelGGL((k_ode_envelope<float>), dim3(c->B), dim3(64 * W), lds, c->stream, c->N, c->m, c->nu, c->Nt,
-                         kind, (const double*)dP, np, dt, nsteps, (const cx<float>*)c->d_A,
-                         (const cx<float>*)c->d_x0, c->x0_per_seed, (cx<float>*)c->d_X);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess && c->cost_kind != QOC_COST_EXTERNAL) {
-    if (c->prec == QOC_FP64)
-      hipLaunchKernelGGL((k_terminal_cost<double>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
-                         (const cx<double>*)c->d_X, (const cx<double>*)c->d_Xt, c->cost_kind, c->cost_n, 0, c->d_J,
-                         c->d_coef, sectors(c));
-    else
-      hipLaunchKernelGGL((k_terminal_cost<float>), dim3(c->B), dim3(256), 0, c->stream, c->N, c->m, c->Nt,
-                         (const cx<float>*)c->d_X, (const cx<float>*)c->d_Xt, c->cost_kind, c->cost_n, 0, c->d_J,
-                         c->d_coef, sectors(c));
-    e = hipGetLastError();
-  }
+  if (e == hipSuccess) e = launch_envelope(c, kind, dP, np, dt, nsteps);
+  if (e == hipSuccess && c->cost_kind != QOC_COST_EXTERNAL) e = launch_terminal_cost(c);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess && J_out && c->cost_kind != QOC_COST_EXTERNAL)
     e = hipMemcpy(J_out, c->d_J, c->B * sizeof(double), hipMemcpyDeviceToHost);
@@ -2728,14 +1236,7 @@ int qoc_pade_histogram(qoc_ctx* c, long long* hist, int reset) {
     if (c->props_since_reset > 0 && c->have_gen) {
       HIPCHK(c, hipMemsetAsync(c->d_hist, 0, 5 * 64 * sizeof(long long), c->stream));
       const long long units = (long long)c->B * c->Nt;
-      const unsigned blocks = (unsigned)std::min<long long>((units + 3) / 4, 8192);
-      if (c->prec == QOC_FP64)
-        hipLaunchKernelGGL((k_pade_units<double>), dim3(blocks), dim3(256), 0, c->stream, c->N, c->nu, units,
-                           (const cx<double>*)c->d_A, (const double*)c->d_u, c->d_hist);
-      else
-        hipLaunchKernelGGL((k_pade_units<float>), dim3(blocks), dim3(256), 0, c->stream, c->N, c->nu, units,
-                           (const cx<float>*)c->d_A, (const double*)c->d_u, c->d_hist);
-      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, launch_pade_units(c, units));
       HIPCHK(c, hipMemcpyAsync(hist, c->d_hist, 5 * 64 * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipMemsetAsync(c->d_hist, 0, 5 * 64 * sizeof(long long), c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -23,7 +23,7 @@ namespace qoc {
 
 // Diagnostic phase stamps (built only with -DQOC_PROBE by tools/; never in the product library).
 #ifdef QOC_PROBE
-__device__ unsigned long long g_probe[64];
+static __device__ unsigned long long g_probe[64];
 #define QOC_STAMP(i)                                                            \
   do {                                                                          \
     __builtin_amdgcn_sched_barrier(0);                                          \
@@ -32,7 +32,7 @@ __device__ unsigned long long g_probe[64];
     __builtin_amdgcn_sched_barrier(0);                                          \
     if (blockIdx.x == 7 && threadIdx.x == 0) g_probe[i] = t_;                   \
   } while (0)
-__device__ unsigned long long g_life[3 * 65536];
+static __device__ unsigned long long g_life[3 * 65536];
 #define QOC_LIFE(slot)                                                                           \
   do {                                                                                           \
     unsigned long long t_;                                                                       \
@@ -89,12 +89,12 @@ __device__ unsigned long long g_life[3 * 65536];
   } while (0)
 #endif
 
-__constant__ double kPade3[4] = {120.0, 60.0, 12.0, 1.0};
-__constant__ double kPade5[6] = {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0};
-__constant__ double kPade7[8] = {17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0};
-__constant__ double kPade9[10] = {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0,
+static __constant__ double kPade3[4] = {120.0, 60.0, 12.0, 1.0};
+static __constant__ double kPade5[6] = {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0};
+static __constant__ double kPade7[8] = {17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0};
+static __constant__ double kPade9[10] = {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0,
                                   2162160.0, 110880.0, 3960.0, 90.0, 1.0};
-__constant__ double kPade13[14] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
+static __constant__ double kPade13[14] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
                                    1187353796428800.0, 129060195264000.0, 10559470521600.0,
                                    670442572800.0, 33522128640.0, 1323241920.0, 40840800.0,
                                    960960.0, 16380.0, 182.0, 1.0};
@@ -102,8 +102,8 @@ __constant__ double kPade13[14] = {64764752532480000.0, 32382376266240000.0, 777
 // Taylor / Paterson-Stockmeyer alternative (ALG = 1): degree m = 3r + 2, r = 2..8, cost 2 + r GEMMs
 // (A2, A3, then r Horner products in A3).  kTaylorTheta[r - 2]: largest ||A||_1 with
 // sum_{k>m} ||A||^k / k! <= 2^-53 (computed with scipy, tools note in DESIGN.md).
-__constant__ double kTaylorTheta[7] = {0.069933, 0.247240, 0.553491, 0.978345, 1.504147, 2.113468, 2.791345};
-__constant__ double kInvFact[27] = {1.0,
+static __constant__ double kTaylorTheta[7] = {0.069933, 0.247240, 0.553491, 0.978345, 1.504147, 2.113468, 2.791345};
+static __constant__ double kInvFact[27] = {1.0,
                                     1.0,
                                     0.5,
                                     0.16666666666666666,
@@ -153,7 +153,7 @@ __device__ __forceinline__ void taylor_select(double nA, int& r, int& s) {
 //   A2 = A A, A3 = A2 A, B_j = x_j0 I + x_j1 A + x_j2 A2 + x_j3 A3,
 //   A6 = B3 + B4 B4,  T12 = B1 + (B2 + A6) A6  ==  sum_{k<=12} A^k / k!  exactly.
 // kTheta12: largest ||A||_1 with sum_{k>12} ||A||^k / k! <= 2^-53.
-__constant__ double kT12[4][4] = {
+static __constant__ double kT12[4][4] = {
     {1.0, 0.99999999999276613715098, -0.13243184210109929356121, -0.050548416421727518977426},
     {5.5174437753406856228547, 1.3093238729673181077940, 0.0043247187525051520919919, 0.0096586056829351321677927},
     {0.0, 1.3110895450078318461208e-12, 0.097250029534075019542638, 0.0068219250901116764187357},

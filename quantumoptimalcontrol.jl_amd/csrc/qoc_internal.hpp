@@ -1,0 +1,230 @@
+// qoc_internal.hpp — host-side internals of libqoc_mi355x.so shared by its translation units.
+//
+// The library is compiled as several translation units in parallel (one per kernel family, __graft_entry__.build):
+//   qoc_engine.hip        the C ABI (include/qoc.h), context setup, host math, RCCL epilogue
+//   qoc_run.hip           run_forward / run_backward: the propagator chains and the per-slice gradient
+//   qoc_run_expm.hip      the exponential kernels (k_expm, k_expm_rr*)
+//   qoc_run_tchain.hip    the Taylor-action chains (k_tchain_*)
+//   qoc_run_grad.hip      the fused order-3 gradient (k_grad_rr_*)
+//   qoc_run_big.hip       the large-N GEMM pipeline, the GEMM-shaped gradient and the Fréchet gradient
+//   qoc_run_ode.hip       the Tsit5 path
+// Each kernel template is launched from one translation unit only; the context (qoc_ctx) and the entry points
+// between the units are declared here.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/qoc.h"
+#include "qoc_chain.hpp"
+#include "qoc_comm.hpp"
+#include "qoc_tchain.hpp"
+
+using namespace qoc;
+
+struct qoc_ctx {
+  int dev = 0, N = 0, m = 0, nu = 0, Nt = 0, B = 0, prec = QOC_FP64;
+  size_t esz = 16;  // bytes per complex element on device
+  hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;        // gradient ranges overlapped with the backward chain
+  std::vector<hipEvent_t> sync_ev;      // cross-stream ordering events (no timing)
+  int bwd_chunks = 4;                   // slice ranges of the overlapped backward chain (1: not overlapped)
+  double bwd_last_frac = 0.5;           // last range's length relative to the others
+  int bwd_prio = 0;                     // bit 0: s_setprio in the chain; bit 1: low-priority gradient stream
+  int bwd_prestate = 2;                 // P1, P2 of every slice beside the first backward range (k_grad_rr_s): 0 off, 1 on, 2 auto
+  void* d_A = nullptr;    // (nu+1) x N*N
+  void* d_x0 = nullptr;   // N*m or B*N*m
+  int x0_per_seed = 0;
+  void* d_Xt = nullptr;   // N*m target
+  int cost_kind = QOC_COST_TRACE;
+  double cost_n = 1.0;
+  unsigned char* d_pmask = nullptr;
+  double mu = 0.0;
+  void* d_src = nullptr;   // B x (Nt+1) x N x m caller's dL/dx(x_k) (qoc_set_costate_source), device precision
+  bool src_on = false;
+  double* d_u = nullptr;     // B*nu*Nt, u of the last propagate
+  void* d_U = nullptr;       // B*Nt*N*N
+  void* d_X = nullptr;       // B*(Nt+1)*N*m
+  void* d_L = nullptr;       // B*(Nt+1)*N*m
+  double* d_J = nullptr;     // B
+  cx<double>* d_coef = nullptr;  // B*m
+  double* d_dJdu = nullptr;  // B*nu*Nt
+  int* d_flag = nullptr;
+  unsigned long long* d_hist = nullptr;  // 5*64 reference (Padé) selection + 8*64 executed Taylor (r, s) / T12 s
+  int chain_cb_fwd = 0, chain_cb_bwd = 0;  // 0: chain_shape's column block; QOC_CHAIN_CB_FWD / _BWD = 1 | 2 (N > 32)
+  int expm_alg = 1;  // 1 Taylor: register-resident T12 (default), 2 LDS Paterson-Stockmeyer (QOC_EXPM_LDS=1), 0 Padé (QOC_EXPM_PADE=1)
+  int prop_method = 0;                   // QOC_PROP_EXPM / QOC_PROP_TSIT5
+  int nsub = 10;                         // Tsit5 steps per slice (reference dt = 0.1 Δt)
+  int ode_kernel = 0;                    // 0 register-resident rows when N fits, 1 LDS rows (QOC_ODE_LDS=1)
+  double* d_stage = nullptr;             // host->device staging (fp64 complex), max(B*N*m, (nu+1)*N*N)*2
+  size_t stage_elems = 0;
+  std::vector<double> h_u;
+  // live per-kernel timing (hipEvents recorded on `stream` around each hot-path launch)
+  bool profiling = false;
+  struct Mark {
+    int phase;
+    hipEvent_t a, b;
+  };
+  std::vector<Mark> marks;
+  std::vector<hipEvent_t> event_pool;
+  double phase_ms[4] = {0, 0, 0, 0};
+  long long phase_n[4] = {0, 0, 0, 0};
+  // large-N path: every k_bgemm launch bracketed while profiling (algorithmic FLOPs per launch)
+  struct GMark {
+    hipEvent_t a, b;
+    double flops;
+  };
+  std::vector<GMark> gmarks;
+  double gemm_ms = 0, gemm_flops = 0;
+  long long gemm_n = 0;
+  // large-N path (N beyond the LDS-resident kernels): chunked batched-GEMM pipeline
+  bool big = false;
+  int chunk = 0;                // slices per chunk
+  void* d_ws = nullptr;         // chunk workspace
+  double* d_red = nullptr;      // per-item reductions (chunk + 8 doubles)
+  long long big_hist[5 * 64] = {};
+  long long big_thist[8 * 64] = {};  // executed Taylor (r, s) on the large-N path
+  long long ns_iters = 0;       // Newton-Schulz iterations executed (all chunks)
+  size_t dev_bytes = 0;
+  // spline parameterisation (examples/ipopt_callbacks_exp.jl:13-14, 28)
+  double* d_Bs = nullptr;  // Nt x ns
+  int ns = 0;
+  double* d_cstage = nullptr;  // host-pointer variants: B x ns x nu coefficients / gradient
+  // GEMM-shaped gradient of the LDS-resident path (order 3, N >= 32: below that the 64-row GEMM tiles
+  // are mostly padding and the per-slice k_grad is faster): generator layouts + P/Q/W workspace
+  void* d_AH = nullptr;    // (nu+1) x N*N: [A0^H | A1^H | ...]
+  void* d_Cst = nullptr;   // nu N x N: [A1; A2; ...]
+  void* d_gws = nullptr;   // 6 x N x B(Nt+1)m
+  void* d_pws = nullptr;   // 2 x N x B(Nt+1)m: P1, P2 of the state-side gradient pass (bwd_prestate)
+  size_t pws_bytes = 0;
+  bool grad_gemm = true;
+  bool grad_rr = false;  // fused register-resident order-3 gradient (qoc_grad_rr.hpp)
+  int* d_ps = nullptr;   // k_expm_rr pass-2 counter + list of Paterson-Stockmeyer units
+  double a0norm = 0.0;   // ||A0||_1 of the generators (host-side, at qoc_set_generators)
+  // exponential that runs: expm_alg, except that when every slice has a large norm (||A0||_1 > 4 theta_12,
+  // tunable bus: ||A_k||_1 ~ 30) the default register-resident Taylor hands over to the reference's own Padé-13
+  // + solve (k_expm ALG 0): over 2000 chained slices only the same algorithm holds |ΔJ| <= 1e-12 against the
+  // reference (Paterson-Stockmeyer: 1.6e-12).  QOC_EXPM_PS=1 keeps Paterson-Stockmeyer there (1.8x faster).
+  int expm_run = 1;
+  bool expm_ps = false;
+  int ncu = 256;         // compute units of the device (persistent-grid sizing)
+  // Taylor-action chains (qoc_tchain.hpp): x_{k+1} = exp(A_k) x_k applied to the state, no U_k formed.
+  // chain_mode 1 selects them (QOC_CHAIN=taylor / expm overrides the automatic choice at qoc_set_generators)
+  int chain_mode = 0;            // 0: propagators (k_expm + k_chain_*), 1: Taylor action (k_tchain_*)
+  int chain_req = QOC_CHAIN_AUTO;  // what qoc_set_chain asked for (kept across qoc_set_generators)
+  bool tchain_ok = false;        // the shape fits the Taylor-action kernels
+  void* d_At = nullptr;          // (nu+1) N x N shifted generators Ã_j = A_j - μ_j I
+  TStep* d_steps = nullptr;      // B x Nt (P, s, e^{μ_k})
+  unsigned long long* d_terms = nullptr;  // Σ P s per forward (executed Taylor terms per direction)
+  TChainParams tprm{};
+  bool cheb_ok = false;          // generators skew-Hermitian with imaginary shifts: Chebyshev applies
+  bool cheb = false;             // Chebyshev terms (k_tchain_prep_cheb) instead of Taylor (QOC_TCHAIN_POLY=taylor)
+  bool cheb_ran = false;         // what the last forward pass used (the backward pass reuses its steps)
+  double* d_tcoef = nullptr;     // B x Nt x TCHEB_STRIDE Chebyshev coefficients (allocated on first use)
+  long long props_since_reset = 0;  // forward passes since the last Padé-histogram reset (chain mode 1)
+  // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
+  ncclComm_t comm = nullptr;
+  int world = 1, rank = 0;
+  long long seed_offset = 0;   // global id of this context's seed 0
+  double* d_best = nullptr;    // [2 local | 2 x world gathered | 2 result]
+  // exact (Fréchet) gradient mode workspace, allocated on first use
+  void* d_fws = nullptr;
+  size_t fws_bytes = 0;
+  // packed states (compress_states, src/utils.jl:96-109): two parity sectors share the kernels' columns, so the
+  // chains and the gradient run on m = max(n1, n2) columns instead of the caller's m_user = n1 + n2
+  int m_user = 0;                       // columns of the caller's states (qoc_create's m)
+  bool packed = false;
+  std::vector<unsigned char> h_rsec;    // N row sectors (0 / 1)
+  std::vector<int> pk_cols[2];          // original columns of sector s: packed column i holds pk_cols[s][i]
+  std::vector<int> pk_pos[2];           // m_user: packed column of original column c in sector s, or -1
+  int zmap[4] = {0, 1, 2, 3};           // z-calibrated cost: original column c -> s m + i
+  unsigned char* d_rsec = nullptr;
+  bool grad_rr_any_m = false;           // the fused gradient fits apart from the column count
+  // caller-layout copies, re-packed when the packing changes
+  std::vector<double> h_gen, h_x0, h_Xt;
+  std::vector<int> h_pen_rows, h_pen_cols;
+  bool have_gen = false, have_x0 = false, have_cost = false, have_prop = false;
+  std::string err;
+};
+
+namespace qoc_host {
+
+extern thread_local std::string g_err;
+int fail(qoc_ctx* ctx, int code, const char* fmt, ...);
+
+#define HIPCHK(ctx, expr)                                                                     \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess) return fail(ctx, QOC_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int kChainMaxN = 64;
+
+// ---- qoc_engine.hip: staging, packed states, timing marks, dispatch ----
+int upload(qoc_ctx* ctx, const double* host, void* dev, size_t nelem);
+int download(qoc_ctx* ctx, const void* dev, double* host, size_t nelem);
+bool grad_rr_cols(int m);
+Sectors sectors(const qoc_ctx* c);
+int upload_states(qoc_ctx* c, const double* host, void* dev, size_t count, const char* what);
+int download_states(qoc_ctx* c, const void* dev, double* host);
+hipEvent_t take_event(qoc_ctx* c);
+int mark_begin(qoc_ctx* c, int phase, hipStream_t s = nullptr);
+void mark_end(qoc_ctx* c, int idx, hipStream_t s = nullptr);
+RcclApi& rccl();
+
+// ---- qoc_run_expm.hip ----
+bool expm_supported(int N, int prec);
+// alg 0: Padé + solve (reference algorithm); alg 1: register-resident Taylor T12; alg 2: LDS Paterson-Stockmeyer.
+hipError_t launch_expm(int prec, hipStream_t s, int N, int nu, int nunits, const void* Agen, const double* u,
+                       const void* Ain, void* Uout, unsigned long long* hist, int* deg, int* sq, int alg = 0,
+                       unsigned long long* thist = nullptr, int* ps = nullptr, bool mix = false);
+
+// ---- qoc_run.hip ----
+template <typename T>
+int run_forward(qoc_ctx* c);
+template <typename T>
+int run_backward(qoc_ctx* c, int order, double* d_dJdu);
+
+// ---- qoc_run_big.hip ----
+size_t big_ws_elems_per_item(int N, int m);
+template <typename T>
+int big_forward(qoc_ctx* c);
+template <typename T>
+int big_backward(qoc_ctx* c, int order, double* d_dJdu);
+template <typename T>
+int grad_gemm_o3(qoc_ctx* c, double* d_dJdu);
+template <typename T>
+int frechet_grad(qoc_ctx* c, double* d_dJdu);
+hipError_t launch_gen_aux(qoc_ctx* c);
+
+// ---- qoc_run_grad.hip ----
+template <typename T>
+int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode = 0);
+
+// ---- qoc_run_ode.hip ----
+template <typename T>
+int ode_forward(qoc_ctx* c);
+template <typename T>
+int ode_adjoint(qoc_ctx* c);
+hipError_t launch_envelope(qoc_ctx* c, int kind, const double* dP, int np, double dt, long long nsteps);
+hipError_t launch_terminal_cost(qoc_ctx* c);
+
+// ---- qoc_run_tchain.hip ----
+bool tchain_mf(const qoc_ctx* c);
+template <typename T>
+int tchain_forward(qoc_ctx* c);
+template <typename T>
+int tchain_backward(qoc_ctx* c, int k_lo = 0, int k_hi = -1);
+template <typename T>
+int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu);
+hipError_t launch_pade_units(qoc_ctx* c, long long units);
+
+}  // namespace qoc_host

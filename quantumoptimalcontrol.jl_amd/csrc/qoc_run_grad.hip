@@ -1,0 +1,76 @@
+// qoc_run_grad.hip — launches of the fused order-3 gradient (qoc_grad_rr.hpp: k_grad_rr_q / _p / _s).
+#include "qoc_grad_rr.hpp"
+#include "qoc_internal.hpp"
+
+namespace qoc_host {
+
+// Fused order-3 gradient (qoc_grad_rr.hpp): k_grad_rr_q (co-state side -> W0, W1 in the state layout)
+// then k_grad_rr_p (state side + contraction -> dJdu).  Persistent grids of 4-wave workgroups.
+template <typename T, int NT, int KS, int NU>
+int grad_rr_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode) {
+  using G = GradRR<T, NT>;
+  const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
+  const size_t lds = G::lds_bytes(N, NU);
+  const long long units = (long long)B * nk, ntiles = (units + 16 / m - 1) / (16 / m);
+  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+  const int grid = (int)std::max<long long>(1, std::min<long long>((ntiles + 3) / 4, (long long)c->ncu * per_cu));
+  const size_t bufN = (size_t)N * ((size_t)B * (Nt + 1) * m);
+  cx<T>* W0 = (cx<T>*)c->d_gws;
+  cx<T>* W1 = W0 + bufN;
+  // mode 0: q + p;  1: state side only (k_grad_rr_s -> P1, P2 in d_pws);  2: q + p reading P1, P2
+  cx<T>* P1 = (cx<T>*)c->d_pws;
+  cx<T>* P2 = P1 ? P1 + bufN : nullptr;
+  if (mode == 1) {
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_s<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_grad_rr_s<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
+                       (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, P1, P2);
+    HIPCHK(c, hipGetLastError());
+    return QOC_OK;
+  }
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_q<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((k_grad_rr_q<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
+                     (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_L, W0, W1);
+  HIPCHK(c, hipGetLastError());
+  if (mode == 2) {
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_p<T, NT, KS, NU, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_grad_rr_p<T, NT, KS, NU, true>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
+                       (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, (const cx<T>*)W0,
+                       (const cx<T>*)W1, d_dJdu, (const cx<T>*)P1, (const cx<T>*)P2);
+  } else {
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_p<T, NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_grad_rr_p<T, NT, KS, NU>), dim3(grid), dim3(256), lds, st, N, m, Nt, B, k0, nk,
+                       (const cx<T>*)c->d_A, c->d_u, (const cx<T>*)c->d_X, (const cx<T>*)c->d_L, (const cx<T>*)W0,
+                       (const cx<T>*)W1, d_dJdu);
+  }
+  HIPCHK(c, hipGetLastError());
+  return QOC_OK;
+}
+
+template <typename T, int NT, int NU>
+int grad_rr_nt(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode) {
+  const int ks = sizeof(T) == 8 ? (c->N + 3) / 4 : 4 * NT;
+  if constexpr (sizeof(T) == 8) {
+    if (ks == 4 * NT - 3) return grad_rr_launch<T, NT, 4 * NT - 3, NU>(c, d_dJdu, st, k0, nk, mode);
+    if (ks == 4 * NT - 2) return grad_rr_launch<T, NT, 4 * NT - 2, NU>(c, d_dJdu, st, k0, nk, mode);
+    if (ks == 4 * NT - 1) return grad_rr_launch<T, NT, 4 * NT - 1, NU>(c, d_dJdu, st, k0, nk, mode);
+  }
+  return grad_rr_launch<T, NT, 4 * NT, NU>(c, d_dJdu, st, k0, nk, mode);
+}
+
+template <typename T>
+int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode) {
+  const int NT = (c->N + 15) / 16;
+  if (c->nu == 1) {
+    if (NT == 1) return grad_rr_nt<T, 1, 1>(c, d_dJdu, st, k0, nk, mode);
+    if (NT == 2) return grad_rr_nt<T, 2, 1>(c, d_dJdu, st, k0, nk, mode);
+    return grad_rr_nt<T, 3, 1>(c, d_dJdu, st, k0, nk, mode);
+  }
+  if (NT == 1) return grad_rr_nt<T, 1, 2>(c, d_dJdu, st, k0, nk, mode);
+  if (NT == 2) return grad_rr_nt<T, 2, 2>(c, d_dJdu, st, k0, nk, mode);
+  return grad_rr_nt<T, 3, 2>(c, d_dJdu, st, k0, nk, mode);
+}
+
+template int grad_rr_o3<double>(qoc_ctx*, double*, hipStream_t, int, int, int);
+template int grad_rr_o3<float>(qoc_ctx*, double*, hipStream_t, int, int, int);
+
+}  // namespace qoc_host

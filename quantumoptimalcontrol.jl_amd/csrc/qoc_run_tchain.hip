@@ -1,0 +1,266 @@
+// qoc_run_tchain.hip — launches of the Taylor-action chains (qoc_tchain.hpp) and the overlapped backward.
+#include "qoc_internal.hpp"
+
+namespace qoc_host {
+
+// ---- Taylor-action chains (qoc_tchain.hpp) -----------------------------------------------------
+size_t tchain_lds(const qoc_ctx* c) {
+  const TShape sh = tchain_shape(c->N, c->m, c->prec == QOC_FP64);
+  return (size_t)(c->nu + 1) * c->N * c->N * c->esz + (size_t)2 * sh.S * sh.JT * chain_mpad(c->m, sh.CB) * c->esz +
+         64 * sizeof(double);
+}
+
+// k_tchain_* instantiated per (S, JT) x (CB, NP) in {(1, 1), (2, 1), (2, 2), (2, 4)}.
+template <typename T, typename F>
+hipError_t tchain_dispatch(int N, int m, F&& f) {
+  using std::integral_constant;
+  const TShape sh = tchain_shape(N, m, sizeof(T) == 8);
+  auto cbnp = [&](auto S_, auto JT_) -> hipError_t {
+    if (sh.CB == 1 && sh.NP == 1) return f(S_, JT_, integral_constant<int, 1>(), integral_constant<int, 1>());
+    if (sh.CB == 2 && sh.NP == 1) return f(S_, JT_, integral_constant<int, 2>(), integral_constant<int, 1>());
+    if (sh.CB == 2 && sh.NP == 2) return f(S_, JT_, integral_constant<int, 2>(), integral_constant<int, 2>());
+    if (sh.CB == 2 && sh.NP == 4) return f(S_, JT_, integral_constant<int, 2>(), integral_constant<int, 4>());
+    return hipErrorInvalidValue;
+  };
+  if (sh.JT == 4)
+    return sh.S == 4 ? cbnp(integral_constant<int, 4>(), integral_constant<int, 4>())
+                     : cbnp(integral_constant<int, 8>(), integral_constant<int, 4>());
+  if (sh.JT == 10) return cbnp(integral_constant<int, 4>(), integral_constant<int, 10>());
+  if (sh.JT == 12) return cbnp(integral_constant<int, 4>(), integral_constant<int, 12>());
+  if constexpr (sizeof(T) == 4) {
+    if (sh.JT == 16) return cbnp(integral_constant<int, 4>(), integral_constant<int, 16>());
+  }
+  return hipErrorInvalidValue;
+}
+
+TChainArgs tchain_args(qoc_ctx* c) {
+  TChainArgs g{};
+  g.N = c->N;
+  g.m = c->m;
+  g.nu = c->nu;
+  g.Nt = c->Nt;
+  g.At = c->d_At;
+  g.u = c->d_u;
+  g.steps = c->d_steps;
+  g.x0 = c->d_x0;
+  g.x0_per_seed = c->x0_per_seed;
+  g.X = c->d_X;
+  g.L = c->d_L;
+  g.Xt = c->d_Xt;
+  g.cost_kind = c->cost_kind;
+  g.n_norm = c->cost_n;
+  g.pmask = c->mu != 0.0 ? c->d_pmask : nullptr;
+  g.mu = c->mu;
+  g.J = c->d_J;
+  g.coef = c->d_coef;
+  g.src = c->src_on ? c->d_src : nullptr;
+  g.tcoef = c->d_tcoef;
+  g.sc = sectors(c);
+  g.k_lo = 0;
+  g.k_hi = c->Nt;
+  return g;
+}
+
+// fp64: the MFMA formulation (k_tchain_mf_*), one wave per (16-row block, column pair); fp32: the VALU one.
+bool tchain_mf(const qoc_ctx* c) {
+  return c->prec == QOC_FP64 && tchain_mf_kq(c->N) > 0 && tchain_mf_waves(c->N, c->m) <= 16 &&
+         tchain_mf_lds(c->N, c->m, c->nu) <= 160 * 1024;
+}
+template <typename F>
+hipError_t tchain_mf_dispatch(int N, F&& f) {
+  using std::integral_constant;
+  switch (tchain_mf_kq(N)) {
+    case 3: return f(integral_constant<int, 3>());
+    case 4: return f(integral_constant<int, 4>());
+    case 6: return f(integral_constant<int, 6>());
+    case 8: return f(integral_constant<int, 8>());
+    case 10: return f(integral_constant<int, 10>());
+    case 12: return f(integral_constant<int, 12>());
+  }
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+int tchain_forward(qoc_ctx* c) {
+  const long long units = (long long)c->B * c->Nt;
+  const bool cheb = c->cheb && tchain_mf(c);
+  if (cheb && !c->d_tcoef) {
+    const size_t bytes = (size_t)units * TCHEB_STRIDE * sizeof(double);
+    HIPCHK(c, hipMalloc((void**)&c->d_tcoef, bytes));
+    c->dev_bytes += bytes;
+  }
+  int mk = mark_begin(c, 0);
+  const unsigned pb = (unsigned)std::min<long long>((units + 255) / 256, 2048);
+  if (cheb)
+    hipLaunchKernelGGL(k_tchain_prep_cheb, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u,
+                       c->tprm, c->d_steps, c->d_tcoef, c->d_terms);
+  else
+    hipLaunchKernelGGL(k_tchain_prep, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u, c->tprm,
+                       c->d_steps, c->d_terms);
+  mark_end(c, mk);
+  HIPCHK(c, hipGetLastError());
+  c->cheb_ran = cheb;
+  const TChainArgs g = tchain_args(c);
+  if (tchain_mf(c)) {
+    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
+    const int threads = 64 * tchain_mf_waves(c->N, c->m);
+    mk = mark_begin(c, 1);
+    hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
+      constexpr int KQ = decltype(KQ_)::value;
+      const int mt = tchain_mf_maxt(c->N, c->m, c->nu);
+      auto kern = mt == 256   ? (cheb ? k_tchain_mf_fwd<KQ, true, 256> : k_tchain_mf_fwd<KQ, false, 256>)
+                  : mt == 512 ? (cheb ? k_tchain_mf_fwd<KQ, true, 512> : k_tchain_mf_fwd<KQ, false, 512>)
+                              : (cheb ? k_tchain_mf_fwd<KQ, true, 1024> : k_tchain_mf_fwd<KQ, false, 1024>);
+      hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (r != hipSuccess) return r;
+      hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);
+      return hipGetLastError();
+    });
+    mark_end(c, mk);
+    if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_mf_fwd launch: %s", hipGetErrorString(e));
+    c->props_since_reset++;
+    return QOC_OK;
+  }
+  const size_t lds = tchain_lds(c);
+  mk = mark_begin(c, 1);
+  hipError_t e = tchain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_, auto NP_) {
+    constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value,
+                  NP = decltype(NP_)::value;
+    hipError_t r = hipFuncSetAttribute((const void*)k_tchain_fwd<T, S, JT, CB, NP>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL((k_tchain_fwd<T, S, JT, CB, NP>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, g);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_fwd launch: %s", hipGetErrorString(e));
+  c->props_since_reset++;
+  return QOC_OK;
+}
+
+template <typename T>
+int tchain_backward(qoc_ctx* c, int k_lo, int k_hi) {
+  TChainArgs g = tchain_args(c);
+  if (tchain_mf(c)) {
+    if (k_hi >= 0) {  // a range of slices (tchain_backward_overlapped)
+      g.k_lo = k_lo;
+      g.k_hi = k_hi;
+      g.prio = c->bwd_prio & 1;
+    }
+    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
+    const int threads = 64 * tchain_mf_waves(c->N, c->m);
+    int mk = mark_begin(c, 2);
+    hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
+      constexpr int KQ = decltype(KQ_)::value;
+      // the (P, s, coefficients) of the forward pass are reused: the same polynomial as the states'
+      const int mt = tchain_mf_maxt(c->N, c->m, c->nu);
+      auto kern = mt == 256   ? (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 256> : k_tchain_mf_bwd<KQ, false, 256>)
+                  : mt == 512 ? (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 512> : k_tchain_mf_bwd<KQ, false, 512>)
+                              : (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 1024> : k_tchain_mf_bwd<KQ, false, 1024>);
+      hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (r != hipSuccess) return r;
+      hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);
+      return hipGetLastError();
+    });
+    mark_end(c, mk);
+    if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_mf_bwd launch: %s", hipGetErrorString(e));
+    return QOC_OK;
+  }
+  const size_t lds = tchain_lds(c);
+  int mk = mark_begin(c, 2);
+  hipError_t e = tchain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_, auto NP_) {
+    constexpr int S = decltype(S_)::value, JT = decltype(JT_)::value, CB = decltype(CB_)::value,
+                  NP = decltype(NP_)::value;
+    hipError_t r = hipFuncSetAttribute((const void*)k_tchain_bwd<T, S, JT, CB, NP>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (r != hipSuccess) return r;
+    hipLaunchKernelGGL((k_tchain_bwd<T, S, JT, CB, NP>), dim3(c->B), dim3(CHAIN_THREADS), lds, c->stream, g);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_bwd launch: %s", hipGetErrorString(e));
+  return QOC_OK;
+}
+
+// Backward chain in slice ranges with the gradient of each finished range on a second stream: the order-3
+// gradient of slices [k_lo, k_hi) needs only x_k and λ_{k+1}, so it runs while the chain works on the
+// next range (lower k).  The chain's workgroup (3 waves, ~84 KB LDS, <= 264 VGPRs at N = 40) leaves room on
+// each CU for one gradient workgroup, whose waves take the chain's MFMA idle cycles.  Chunk boundaries are
+// uniform in k except the last (exposed) range, bwd_last_frac of a uniform one.
+template <typename T>
+int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu) {
+  const int Nt = c->Nt, S = std::min(c->bwd_chunks, std::max(1, Nt / 32));  // ranges of >= ~32 slices
+  if (!c->stream2) {
+    int lo = 0, hi = 0;
+    HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(c, hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, (c->bwd_prio & 2) ? lo : 0));
+  }
+  while ((int)c->sync_ev.size() < S + 2) {
+    hipEvent_t e;
+    HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->sync_ev.push_back(e);
+  }
+  // k boundaries: kb[0] = Nt > kb[1] > ... > kb[S] = 0; the last range is shorter
+  std::vector<int> kb(S + 1);
+  const double last = std::max(0.05, std::min(1.0, c->bwd_last_frac)), w = Nt / (S - 1 + last);
+  for (int i = 0; i <= S; ++i) kb[i] = std::max(0, Nt - (int)std::lround(i * w));
+  kb[S] = 0;
+  // state side first (QOC_BWD_PRESTATE): P1 = X x_k, P2 = X P1 of every slice need only the forward's states, so
+  // they run beside the first range, which otherwise has nothing beside it; each range then runs q + p (PRE).
+  const size_t pws = (size_t)2 * c->N * c->B * (Nt + 1) * c->m * c->esz;
+  // auto: only when a CU keeps room beside its chain waves (<= 3 per CU, or small N whose chain waves are
+  // light); measured: cavity (3 waves/CU) +1.3 %, zz +0.9 %, tunable bus (2 WGs x 2 waves/CU) -2.6 %
+  const long long chain_waves = (long long)((c->B + c->ncu - 1) / c->ncu) * tchain_mf_waves(c->N, c->m);
+  const bool pre = c->bwd_prestate == 1 || (c->bwd_prestate == 2 && (chain_waves <= 3 || c->N <= 16));
+  if (pre && c->pws_bytes < pws) {
+    if (c->d_pws) HIPCHK(c, hipFree(c->d_pws));
+    c->d_pws = nullptr;
+    c->pws_bytes = 0;
+    HIPCHK(c, hipMalloc(&c->d_pws, pws));
+    c->pws_bytes = pws;
+    c->dev_bytes += pws;
+  }
+  HIPCHK(c, hipEventRecord(c->sync_ev[S], c->stream));  // stream2 starts after everything queued so far
+  HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[S], 0));
+  if (pre) {
+    const int mk = mark_begin(c, 3, c->stream2);
+    const int r = grad_rr_o3<T>(c, d_dJdu, c->stream2, 0, Nt, 1);
+    mark_end(c, mk, c->stream2);
+    if (r) return r;
+  }
+  for (int i = 0; i < S; ++i) {
+    if (kb[i + 1] >= kb[i]) continue;
+    int r = tchain_backward<T>(c, kb[i + 1], kb[i]);
+    if (r) return r;
+    HIPCHK(c, hipEventRecord(c->sync_ev[i], c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[i], 0));
+    const int mk = mark_begin(c, 3, c->stream2);
+    r = grad_rr_o3<T>(c, d_dJdu, c->stream2, kb[i + 1], kb[i] - kb[i + 1], pre ? 2 : 0);
+    mark_end(c, mk, c->stream2);
+    if (r) return r;
+  }
+  HIPCHK(c, hipEventRecord(c->sync_ev[S + 1], c->stream2));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->sync_ev[S + 1], 0));
+  return QOC_OK;
+}
+
+// reference-equivalent Padé (d, s) of every unit of the last propagated u -> c->d_hist (k_pade_units)
+hipError_t launch_pade_units(qoc_ctx* c, long long units) {
+  const unsigned blocks = (unsigned)std::min<long long>((units + 3) / 4, 8192);
+  if (c->prec == QOC_FP64)
+    hipLaunchKernelGGL((k_pade_units<double>), dim3(blocks), dim3(256), 0, c->stream, c->N, c->nu, units,
+                       (const cx<double>*)c->d_A, (const double*)c->d_u, c->d_hist);
+  else
+    hipLaunchKernelGGL((k_pade_units<float>), dim3(blocks), dim3(256), 0, c->stream, c->N, c->nu, units,
+                       (const cx<float>*)c->d_A, (const double*)c->d_u, c->d_hist);
+  return hipGetLastError();
+}
+
+template int tchain_forward<double>(qoc_ctx*);
+template int tchain_forward<float>(qoc_ctx*);
+template int tchain_backward<double>(qoc_ctx*, int, int);
+template int tchain_backward<float>(qoc_ctx*, int, int);
+template int tchain_backward_overlapped<double>(qoc_ctx*, double*);
+template int tchain_backward_overlapped<float>(qoc_ctx*, double*);
+
+}  // namespace qoc_host

@@ -12,7 +12,7 @@
 namespace qoc {
 
 // u[b*nu*Nt + k*nu + j] = sum_s Bs[k + Nt s] c[b*ns*nu + s + ns j]
-__global__ void k_spline_u(int B, int Nt, int ns, int nu, const double* __restrict__ Bs, const double* __restrict__ c,
+static __global__ void k_spline_u(int B, int Nt, int ns, int nu, const double* __restrict__ Bs, const double* __restrict__ c,
                            double* __restrict__ u) {
   const long long total = (long long)B * Nt * nu;
   for (long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x; g < total; g += (long long)gridDim.x * blockDim.x) {
@@ -28,7 +28,7 @@ __global__ void k_spline_u(int B, int Nt, int ns, int nu, const double* __restri
 }
 
 // dJdc[b*ns*nu + s + ns j] = sum_k Bs[k + Nt s] dJdu[b*nu*Nt + k*nu + j]   (one wave per output)
-__global__ void k_spline_grad(int B, int Nt, int ns, int nu, const double* __restrict__ Bs,
+static __global__ void k_spline_grad(int B, int Nt, int ns, int nu, const double* __restrict__ Bs,
                               const double* __restrict__ dJdu, double* __restrict__ dJdc) {
   const int lane = threadIdx.x & 63;
   const long long total = (long long)B * ns * nu;
@@ -51,7 +51,7 @@ __global__ void k_spline_grad(int B, int Nt, int ns, int nu, const double* __res
 // gjac[b*2*nc + 0*nc + i] = c_i / g0,  gjac[b*2*nc + nc + (s + ns j)] = (d_s - d_{s+1}) / g1
 // with d_s = c[s, j] - c[s-1, j] for 1 <= s < ns and d_0 = d_ns = 0.  A zero norm has a zero
 // gradient (the subgradient Zygote's norm rrule returns at 0).  One workgroup per seed.
-__global__ void k_spline_constraints(int ns, int nu, const double* __restrict__ c, double* __restrict__ g,
+static __global__ void k_spline_constraints(int ns, int nu, const double* __restrict__ c, double* __restrict__ g,
                                      double* __restrict__ gjac) {
   __shared__ double red[8];
   const int b = blockIdx.x, nc = ns * nu;

@@ -26,7 +26,7 @@ namespace qoc {
 
 // Diagnostic cycle stamps of the term loop (tools/tchain_probe.hip builds with -DQOC_PROBE; empty otherwise).
 #ifdef QOC_PROBE
-__device__ unsigned long long g_tc[16];
+static __device__ unsigned long long g_tc[16];
 #define TC_T(var)                                                                \
   unsigned long long var;                                                        \
   do {                                                                           \
@@ -100,7 +100,7 @@ struct TChainParams {
 };
 
 // (P, s, e^{μ}) per unit, plus Σ P s (executed Taylor terms per direction) for the roofline accounting.
-__global__ void k_tchain_prep(int nu, long long units, const double* __restrict__ u, const TChainParams prm,
+static __global__ void k_tchain_prep(int nu, long long units, const double* __restrict__ u, const TChainParams prm,
                               TStep* __restrict__ steps, unsigned long long* __restrict__ terms) {
   unsigned long long cnt = 0;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < units; e += (long long)gridDim.x * blockDim.x) {
@@ -271,7 +271,7 @@ __device__ int cheb_series(double rho, double tol, double* __restrict__ ce) {
   return P;
 }
 
-__global__ void k_tchain_prep_cheb(int nu, long long units, const double* __restrict__ u, const TChainParams prm,
+static __global__ void k_tchain_prep_cheb(int nu, long long units, const double* __restrict__ u, const TChainParams prm,
                                    TStep* __restrict__ steps, double* __restrict__ coef,
                                    unsigned long long* __restrict__ terms) {
   unsigned long long cnt = 0;
