@@ -186,6 +186,57 @@ def cpu_baseline(prob, u_all, order, nthreads, target_s=12.0):
     }, (J, g, S2)
 
 
+def launch_ranks(n: int) -> int:
+    """Start n ranks of this script (torch.distributed.run, rendezvous on 127.0.0.1) and return their exit
+    code.  Called before anything touches the GPU: the ranks are child processes, this one only waits."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_plumbing(args, rank: int, world: int) -> None:
+    """The multi-rank plumbing without a GPU (gloo): every rank holds B synthetic objectives of its seed shard,
+    the best (J, global seed) is exchanged K times with the barrier / max-over-ranks timing of the GPU run, and
+    rank 0 prints the contract line (data "cpu-plumbing", no evals measured)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from qoc_amd import multi
+    if world > 1:
+        dist.init_process_group("gloo")
+    B = args.seeds or 8
+    J = torch.from_numpy(np.random.default_rng(rank).uniform(0.1, 1.0, B))
+    for _ in range(args.warmup):
+        best = multi.gather_best(J, rank * B)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        best = multi.gather_best(J, rank * B)
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "GRAPE gradient evals/sec (dim N, T slices, B seeds) @ 1/2/4/8 GPU", "value": None,
+                          "unit": "evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": float(el.item()) / max(args.steps, 1) * 1e3, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": None, "data": "cpu-plumbing",
+                          "config": {"workload": "best-(J, seed) exchange only", "seeds_per_rank": B,
+                                     "global_seeds": B * world, "parallelism": f"seed-sharded x{world}"},
+                          "best_over_ranks": {"J": best[0], "seed": best[1], "transport": "torch.distributed (gloo)"}}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -196,11 +247,20 @@ def main():
     ap.add_argument("--seeds", type=int, default=0, help="override seeds per GPU")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-plumbing", action="store_true",
+                    help="no GPU: check the launcher and the best-(J, seed) exchange over gloo (CPU tests)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the ranks (before anything touches the GPU) and report their exit code
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.cpu_plumbing:
+        return cpu_plumbing(args, rank, world)
 
     import numpy as np
     import torch
@@ -228,14 +288,15 @@ def main():
     gathered = torch.empty(2 * world, dtype=torch.float64, device=dev)
     stream = torch.cuda.ExternalStream(eng.stream(), device=dev)
     seed_offset = torch.arange(B, dtype=torch.float64, device=dev) + rank * B
-    # the one exchange: best (J, global seed) over all ranks, RCCL inside libqoc_mi355x.so (qoc_allgather_best);
-    # torch.distributed's all_gather (also RCCL) only if the library cannot load RCCL
+    # the one exchange: best (J, global seed) over all ranks, RCCL inside libqoc_mi355x.so (qoc_allgather_best,
+    # a real communicator also at world 1); torch.distributed's all_gather (also RCCL) only if the library
+    # cannot load RCCL
     from qoc_amd import multi
-    transport = "rccl-libqoc" if multi.init_engine_comm(eng, rank * B) else "torch.distributed"
+    transport = multi.init_engine_comm(eng, rank * B)
 
     def step():
         eng.eval_device(u_d.data_ptr(), args.order, J_d.data_ptr(), g_d.data_ptr())
-        if transport == "rccl-libqoc":
+        if transport in ("rccl-libqoc", "local"):
             eng.allgather_best_device(best_d.data_ptr())  # on the engine stream, after its kernels
         elif world > 1:
             with torch.cuda.stream(stream):  # ordered after the engine's kernels
@@ -390,7 +451,7 @@ def main():
                 "ns_iters_per_chunk": ns_it, "chunk": info1["chunk"]}
     ref_f = ref_eval_flops(N, m, nu, {k: v / B for k, v in hist_launch.items()}, args.order)
 
-    best = best_d.cpu().numpy().tolist() if world > 1 or transport == "rccl-libqoc" else None
+    best = best_d.cpu().numpy().tolist()
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -446,7 +507,8 @@ def main():
                                      "note": "reference-algorithm flops x eval rate; not executed work, may exceed peak"},
             "parity_vs_cpu_port": parity,
             "engine": info1,
-            "best_over_ranks": {"J": best[0], "seed": int(best[1]), "transport": transport} if best else None,
+            "best_over_ranks": {"J": best[0], "seed": int(best[1]), "transport": transport,
+                                "communicator_ranks": eng.comm_ranks()},
         }
         if cpu and cpu.get("value"):
             out["speedup_vs_cpu"] = value / cpu["value"]

@@ -113,6 +113,11 @@ int qoc_set_spline_basis(qoc_ctx* ctx, const double* Bs, int ns);
 int qoc_eval_spline_dev(qoc_ctx* ctx, const double* d_c, int dUkdp_order, double* d_J, double* d_dJdc);
 /* Host-pointer variant (J_out: B, dJdc_out: B x ns x nu). */
 int qoc_eval_spline(qoc_ctx* ctx, const double* c, int dUkdp_order, double* J_out, double* dJdc_out);
+/* f alone (examples/ipopt_callbacks_exp.jl:11-19: spline map, propagate, J; no sensitivity), host pointers; and
+ * f_grad's sensitivity (:21-31) for the coefficients last passed to qoc_propagate_spline (QOC_ERR_STALE for any
+ * other c, the reference's "Cache data from other control signal u"). */
+int qoc_propagate_spline(qoc_ctx* ctx, const double* c, double* J_out);
+int qoc_sensitivity_spline(qoc_ctx* ctx, const double* c, int dUkdp_order, double* dJdc_out);
 /* Constraints g = [norm(c), norm(diff(c, dims=1))] and their Jacobian (examples/ipopt_callbacks_exp.jl:33-51),
  * device pointers: d_g (B x 2), d_gjac (B x 2 x nc, constraint-major = Ipopt's dense triplet order; may be NULL). */
 int qoc_spline_constraints_dev(qoc_ctx* ctx, const double* d_c, double* d_g, double* d_gjac);
@@ -200,12 +205,17 @@ int qoc_chain_terms(qoc_ctx* ctx, long long* terms, int reset);
  * distributes (MPI / Distributed.jl / torch.distributed); every rank then calls qoc_comm_init with its rank
  * and the global id of its seed 0.  qoc_allgather_best returns the best J of the last propagate over all
  * ranks and its global seed (lowest seed on ties); without qoc_comm_init it covers this context alone.
+ * With an id, qoc_comm_init creates a real RCCL communicator for any world size (world = 1 included: a
+ * one-rank ncclAllGather on the same path as the multi-GPU run); with id = NULL (world = 1 only) none is made.
+ * On any error the context is left without a communicator (world 1, seed offset 0).
+ * qoc_comm_ranks returns the communicator's rank count, 0 when the context has none.
  * RCCL is loaded on first use (librccl.so.1); two ranks cannot share one GPU (RCCL rejects duplicate
  * devices).  The _dev variant writes (J_best, seed) as two doubles to device memory on qoc_stream without
  * synchronising. */
 #define QOC_UNIQUE_ID_BYTES 128
 int qoc_comm_unique_id(void* id_out);
 int qoc_comm_init(qoc_ctx* ctx, int world, int rank, const void* id, long long seed_offset);
+int qoc_comm_ranks(qoc_ctx* ctx);
 int qoc_allgather_best(qoc_ctx* ctx, double* J_best, int* seed_best);
 int qoc_allgather_best_dev(qoc_ctx* ctx, double* d_out);
 

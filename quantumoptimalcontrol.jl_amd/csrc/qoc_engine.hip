@@ -771,18 +771,26 @@ int qoc_set_compression(qoc_ctx* c, const int* rows1, int nr1, const int* cols1,
     restore();
     return fail(c, QOC_ERR_ARG, "generators couple the two compress_states row blocks");
   }
+  int old_zmap[4];
+  std::memcpy(old_zmap, c->zmap, sizeof(old_zmap));
   if (on && mu_ == 4)
     for (int oc = 0; oc < 4; ++oc) c->zmap[oc] = pos[0][oc] >= 0 ? pos[0][oc] : c->m + pos[1][oc];
   std::string saved_err = c->err;
   int r = QOC_OK;
-  if (on) HIPCHK(c, hipMemcpy(c->d_rsec, rsec.data(), N, hipMemcpyHostToDevice));
+  // packing on the host (pack_states reads h_rsec), validated before any device state changes
   if (c->have_x0) r = upload_states(c, c->h_x0.data(), c->d_x0, c->x0_per_seed ? (size_t)c->B : 1, "x0");
   if (r == QOC_OK && c->have_cost && !c->h_Xt.empty()) r = upload_states(c, c->h_Xt.data(), c->d_Xt, 1, nullptr);
+  if (r == QOC_OK && on) {
+    const hipError_t e = hipMemcpy(c->d_rsec, rsec.data(), N, hipMemcpyHostToDevice);
+    if (e != hipSuccess) r = fail(c, QOC_ERR_HIP, "row sectors upload: %s", hipGetErrorString(e));
+  }
   if (r != QOC_OK) {
     saved_err = c->err;
     restore();
+    std::memcpy(c->zmap, old_zmap, sizeof(old_zmap));
     if (c->have_x0) upload_states(c, c->h_x0.data(), c->d_x0, c->x0_per_seed ? (size_t)c->B : 1, nullptr);
     if (c->have_cost && !c->h_Xt.empty()) upload_states(c, c->h_Xt.data(), c->d_Xt, 1, nullptr);
+    if (!old_rsec.empty()) (void)hipMemcpy(c->d_rsec, old_rsec.data(), N, hipMemcpyHostToDevice);
     c->err = saved_err;
     return r;
   }
@@ -815,6 +823,7 @@ int qoc_propagate_dev(qoc_ctx* c, const double* d_u, double* d_J) {
     HIPCHK(c, hipMemcpyAsync(d_J, c->d_J, c->B * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
   c->have_prop = true;
   c->h_u.clear();  // host copy unknown for device-side u
+  c->h_coef.clear();
   return QOC_OK;
 }
 
@@ -858,6 +867,7 @@ int qoc_propagate(qoc_ctx* c, const double* u, double* J_out) {
   if (J_out) HIPCHK(c, hipMemcpyAsync(J_out, c->d_J, c->B * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->h_u.assign(u, u + nu_t);
+  c->h_coef.clear();
   c->have_prop = true;
   return QOC_OK;
 }
@@ -1043,6 +1053,53 @@ int qoc_eval_spline(qoc_ctx* c, const double* coef, int order, double* J_out, do
   return QOC_OK;
 }
 
+int qoc_propagate_spline(qoc_ctx* c, const double* coef, double* J_out) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  if (!c->ns) return fail(c, QOC_ERR_STATE, "spline basis not set (qoc_set_spline_basis)");
+  if (!coef) return fail(c, QOC_ERR_ARG, "c is null");
+  HIPCHK(c, hipSetDevice(c->dev));
+  const size_t nc = (size_t)c->B * c->ns * c->nu;
+  HIPCHK(c, hipMemcpyAsync(c->d_cstage, coef, nc * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  const long long nuT = (long long)c->B * c->Nt * c->nu;
+  const unsigned blocks = (unsigned)std::min<long long>((nuT + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_spline_u, dim3(blocks), dim3(256), 0, c->stream, c->B, c->Nt, c->ns, c->nu, c->d_Bs,
+                     c->d_cstage, c->d_u);
+  HIPCHK(c, hipGetLastError());
+  c->h_coef.clear();
+  int r = qoc_propagate_dev(c, c->d_u, nullptr);
+  if (r) return r;
+  if (J_out) HIPCHK(c, hipMemcpyAsync(J_out, c->d_J, c->B * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->h_coef.assign(coef, coef + nc);
+  return QOC_OK;
+}
+
+int qoc_sensitivity_spline(qoc_ctx* c, const double* coef, int order, double* dJdc_out) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  if (!c->ns) return fail(c, QOC_ERR_STATE, "spline basis not set (qoc_set_spline_basis)");
+  if (!coef) return fail(c, QOC_ERR_ARG, "c is null");
+  int r = check_ready(c);
+  if (r) return r;
+  const size_t nc = (size_t)c->B * c->ns * c->nu;
+  if (!c->have_prop || c->h_coef.size() != nc || std::memcmp(coef, c->h_coef.data(), nc * sizeof(double)) != 0)
+    return fail(c, QOC_ERR_STALE, "Cache data from other control signal u");
+  if (order < 0 || order > 4) return fail(c, QOC_ERR_ARG, "dUkdp_order must be 1..4 or QOC_DUKDP_EXACT (got %d)", order);
+  if (c->cost_kind == QOC_COST_EXTERNAL)
+    return fail(c, QOC_ERR_STATE, "qoc_sensitivity_spline needs a device-side cost (TRACE or ZCAL)");
+  r = backward(c, order, c->d_dJdu);
+  if (r) return r;
+  if (dJdc_out) {
+    const long long outs = (long long)c->B * c->ns * c->nu;
+    const unsigned gb = (unsigned)std::min<long long>((outs * 64 + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_spline_grad, dim3(gb), dim3(256), 0, c->stream, c->B, c->Nt, c->ns, c->nu, c->d_Bs,
+                       c->d_dJdu, c->d_cstage + nc);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(dJdc_out, c->d_cstage + nc, nc * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return QOC_OK;
+}
+
 int qoc_spline_constraints_dev(qoc_ctx* c, const double* d_c, double* d_g, double* d_gjac) {
   if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
   if (!c->ns) return fail(c, QOC_ERR_STATE, "spline basis not set (qoc_set_spline_basis)");
@@ -1147,27 +1204,45 @@ int qoc_comm_init(qoc_ctx* c, int world, int rank, const void* id, long long see
   if (world > 1 && !id) return fail(c, QOC_ERR_ARG, "unique id is null");
   HIPCHK(c, hipSetDevice(c->dev));
   RcclApi& r = rccl();
+  // any previous communicator is dropped first; until the new one exists the context covers its own seeds
   if (c->comm) {
     r.commDestroy(c->comm);
     c->comm = nullptr;
   }
   if (c->d_best) HIPCHK(c, hipFree(c->d_best));
   c->d_best = nullptr;
-  HIPCHK(c, hipMalloc((void**)&c->d_best, (size_t)(4 + 2 * world) * sizeof(double)));
-  c->world = world;
-  c->rank = rank;
-  c->seed_offset = seed_offset;
-  if (world > 1) {
-    if (!r.ok) return fail(c, QOC_ERR_UNSUPPORTED, "RCCL (librccl.so.1) not available");
+  c->world = 1;
+  c->rank = 0;
+  c->seed_offset = 0;
+  double* best = nullptr;
+  HIPCHK(c, hipMalloc((void**)&best, (size_t)(4 + 2 * world) * sizeof(double)));
+  // With a unique id a real RCCL communicator is created, also for world = 1 (a one-rank all-gather through the
+  // same code path as the multi-GPU run); without one (world = 1 only) the context covers its own seeds.
+  ncclComm_t comm = nullptr;
+  if (id) {
+    if (!r.ok) {
+      hipFree(best);
+      return fail(c, QOC_ERR_UNSUPPORTED, "RCCL (librccl.so.1) not available");
+    }
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
-    const ncclResult_t e = r.commInitRank(&c->comm, world, uid, rank);
-    if (e != ncclSuccess) {
-      c->comm = nullptr;
+    const ncclResult_t e = r.commInitRank(&comm, world, uid, rank);
+    if (e != ncclSuccess || !comm) {
+      hipFree(best);
       return fail(c, QOC_ERR_HIP, "ncclCommInitRank (rank %d of %d): %s", rank, world, r.getErrorString(e));
     }
   }
+  c->comm = comm;
+  c->d_best = best;
+  c->world = world;
+  c->rank = rank;
+  c->seed_offset = seed_offset;
   return QOC_OK;
+}
+
+int qoc_comm_ranks(qoc_ctx* c) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  return c->comm ? c->world : 0;
 }
 
 int qoc_allgather_best_dev(qoc_ctx* c, double* d_out) {
@@ -1182,7 +1257,7 @@ int qoc_allgather_best_dev(qoc_ctx* c, double* d_out) {
   hipLaunchKernelGGL(k_argmin_seed, dim3(1), dim3(256), 0, c->stream, (const double*)c->d_J, c->B, c->seed_offset,
                      c->d_best);
   HIPCHK(c, hipGetLastError());
-  if (c->world > 1) {
+  if (c->comm && rccl().ok) {
     const ncclResult_t e = rccl().allGather(c->d_best, c->d_best + 2, 2, ncclFloat64, c->comm, c->stream);
     if (e != ncclSuccess) return fail(c, QOC_ERR_HIP, "ncclAllGather: %s", rccl().getErrorString(e));
     hipLaunchKernelGGL(k_pick_best, dim3(1), dim3(64), 0, c->stream, (const double*)(c->d_best + 2), c->world, res);

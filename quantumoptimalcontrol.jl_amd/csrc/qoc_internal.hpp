@@ -67,6 +67,7 @@ struct qoc_ctx {
   double* d_stage = nullptr;             // host->device staging (fp64 complex), max(B*N*m, (nu+1)*N*N)*2
   size_t stage_elems = 0;
   std::vector<double> h_u;
+  std::vector<double> h_coef;  // spline coefficients of the last qoc_propagate_spline
   // live per-kernel timing (hipEvents recorded on `stream` around each hot-path launch)
   bool profiling = false;
   struct Mark {

@@ -211,37 +211,53 @@ int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu) {
   // auto: only when a CU keeps room beside its chain waves (<= 3 per CU, or small N whose chain waves are
   // light); measured: cavity (3 waves/CU) +1.3 %, zz +0.9 %, tunable bus (2 WGs x 2 waves/CU) -2.6 %
   const long long chain_waves = (long long)((c->B + c->ncu - 1) / c->ncu) * tchain_mf_waves(c->N, c->m);
-  const bool pre = c->bwd_prestate == 1 || (c->bwd_prestate == 2 && (chain_waves <= 3 || c->N <= 16));
-  if (pre && c->pws_bytes < pws) {
-    if (c->d_pws) HIPCHK(c, hipFree(c->d_pws));
+  bool pre = c->bwd_prestate == 1 || (c->bwd_prestate == 2 && (chain_waves <= 3 || c->N <= 16));
+  if (pre && c->pws_bytes < pws) {  // grown on first use; without the buffer the ranges run q + p in full
+    if (c->d_pws) {
+      HIPCHK(c, hipStreamSynchronize(c->stream2));
+      HIPCHK(c, hipFree(c->d_pws));
+      c->dev_bytes -= c->pws_bytes;
+    }
     c->d_pws = nullptr;
     c->pws_bytes = 0;
-    HIPCHK(c, hipMalloc(&c->d_pws, pws));
-    c->pws_bytes = pws;
-    c->dev_bytes += pws;
+    if (hipMalloc(&c->d_pws, pws) == hipSuccess) {
+      c->pws_bytes = pws;
+      c->dev_bytes += pws;
+    } else {
+      (void)hipGetLastError();
+      c->d_pws = nullptr;
+      pre = false;
+    }
   }
   HIPCHK(c, hipEventRecord(c->sync_ev[S], c->stream));  // stream2 starts after everything queued so far
   HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[S], 0));
+  // every exit joins stream2 back into the engine stream, so that later work on c->stream (uploads, the next
+  // call's kernels) is ordered after the gradients already queued on stream2
+  auto join = [&](int r) {
+    const hipError_t e1 = hipEventRecord(c->sync_ev[S + 1], c->stream2);
+    const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(c->stream, c->sync_ev[S + 1], 0) : e1;
+    if (r == QOC_OK && e2 != hipSuccess) return fail(c, QOC_ERR_HIP, "stream join: %s", hipGetErrorString(e2));
+    return r;
+  };
   if (pre) {
     const int mk = mark_begin(c, 3, c->stream2);
     const int r = grad_rr_o3<T>(c, d_dJdu, c->stream2, 0, Nt, 1);
     mark_end(c, mk, c->stream2);
-    if (r) return r;
+    if (r) return join(r);
   }
   for (int i = 0; i < S; ++i) {
     if (kb[i + 1] >= kb[i]) continue;
     int r = tchain_backward<T>(c, kb[i + 1], kb[i]);
-    if (r) return r;
-    HIPCHK(c, hipEventRecord(c->sync_ev[i], c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[i], 0));
+    if (r) return join(r);
+    hipError_t e = hipEventRecord(c->sync_ev[i], c->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream2, c->sync_ev[i], 0);
+    if (e != hipSuccess) return join(fail(c, QOC_ERR_HIP, "range event: %s", hipGetErrorString(e)));
     const int mk = mark_begin(c, 3, c->stream2);
     r = grad_rr_o3<T>(c, d_dJdu, c->stream2, kb[i + 1], kb[i] - kb[i + 1], pre ? 2 : 0);
     mark_end(c, mk, c->stream2);
-    if (r) return r;
+    if (r) return join(r);
   }
-  HIPCHK(c, hipEventRecord(c->sync_ev[S + 1], c->stream2));
-  HIPCHK(c, hipStreamWaitEvent(c->stream, c->sync_ev[S + 1], 0));
-  return QOC_OK;
+  return join(QOC_OK);
 }
 
 // reference-equivalent Padé (d, s) of every unit of the last propagated u -> c->d_hist (k_pade_units)

@@ -13,6 +13,7 @@
 module QOCMI355X
 
 import QuantumOptimalControl
+using LinearAlgebra: tr
 const QOC = QuantumOptimalControl
 
 const libqoc = get(ENV, "QOC_MI355X_LIB", joinpath(@__DIR__, "..", "qoc_amd", "libqoc_mi355x.so"))
@@ -218,13 +219,28 @@ function setup_state_penalty(inds_penalty, inds_css, μ)
     return L, PenaltyGrad(collect(inds_penalty), collect(inds_css), Float64(μ))
 end
 
+# x_target / n given with untagged closures: they must be the trace infidelity of x_target (the reference's
+# setup_infidelity(x_target, n), src/penalty_fcns.jl:15-24), checked on a probe state.
+function check_trace_closures(Jfinal, dJfinal_dx, Xt, nn)
+    xp = Xt .+ 0.1 .* cis.(reshape(1:length(Xt), size(Xt)))
+    Ω = tr(Xt' * xp)
+    Jw, dJw = 1 - abs2(Ω) / nn^2, -2Ω / nn^2 .* Xt
+    ok = isapprox(Jfinal(xp), Jw; rtol=1e-12, atol=1e-14) &&
+         isapprox(dJfinal_dx(xp), dJw; rtol=1e-12, atol=1e-14)
+    ok || error("x_target given but (Jfinal, dJfinal_dx) are not setup_infidelity(x_target, n): pass the " *
+                "closures without x_target (host-evaluated cost) or use QOCMI355X.setup_infidelity")
+    return nothing
+end
+
 """
     setup_ipopt_callbacks(A0Δt, A1Δt, A2Δt, x0, u_prototype, (Jfinal, dJfinal_dx), (L, dL_dx), B; x_target, n)
 
 GPU version of examples/ipopt_callbacks_exp.jl:1-54: f = Jfinal(x[end]) + sum(L, x) and f_grad = B' dJdu'.
+As in the reference, f only propagates (Ipopt's line-search evaluations pay no gradient) and f_grad runs the
+sensitivity of the coefficients f last saw, re-propagating first if Ipopt asks for the gradient of new ones.
 With the tagged costs of this module (setup_infidelity / setup_infidelity_zcalibrated) and penalty
-(setup_state_penalty, or the reference's disabled Returns(0) pair) the spline map, the propagation, the cost
-and the sensitivity run in one `qoc_eval_spline` call on the device.  Any other cost closure is evaluated on
+(setup_state_penalty, or the reference's disabled Returns(0) pair) both run on the device
+(`qoc_propagate_spline`, `qoc_sensitivity_spline`).  Any other cost closure is evaluated on
 the host at x[end] and handed over as λ_{Nt+1} (QOC_COST_EXTERNAL), exactly as the reference's f / f_grad do;
 any other penalty pair is evaluated on the host too: sum(L, x) in f, and dL_dx(x[k]) for every slice added to
 the co-states on the device (qoc_set_costate_source).  g / g_jac are the reference's norm constraints.
@@ -248,11 +264,13 @@ function setup_ipopt_callbacks(A0Δt, A1Δt, A2Δt, x0, u_prototype, (Jfinal, dJ
     # other (L, dL_dx) takes the host path below (sum(L, x) on the host, dL_dx through the co-state source)
     device_penalty = dL_dx isa PenaltyGrad || no_penalty(L)
     set_penalty!(cache, dL_dx isa PenaltyGrad ? dL_dx : nothing)
-    # cost: on the device when tagged, else the caller's closures on the host (x_target / n keywords: the
-    # trace infidelity, for callers that pass plain closures built from them)
+    # cost: on the device when tagged, else the caller's closures on the host.  The x_target / n keywords name the
+    # trace infidelity for callers that pass the reference's own (untagged) setup_infidelity(x_target, n)
+    # closures; closures that are not that cost are an error rather than silently replaced by it.
     if Jfinal isa TraceJ || (x_target !== nothing && !(Jfinal isa ZCalJ))
         Xt = Jfinal isa TraceJ ? Jfinal.Xt : Matrix{ComplexF64}(x_target)
         nn = Jfinal isa TraceJ ? Jfinal.n : (n === nothing ? size(Xt, 2) : n)
+        Jfinal isa TraceJ || check_trace_closures(Jfinal, dJfinal_dx, Xt, nn)
         kind = QOC_COST_TRACE
     elseif Jfinal isa ZCalJ
         Xt, nn, kind = Jfinal.Xt, 4.0, QOC_COST_ZCAL
@@ -267,24 +285,35 @@ function setup_ipopt_callbacks(A0Δt, A1Δt, A2Δt, x0, u_prototype, (Jfinal, dJ
     c_prev = fill(NaN, nc)
     J = Ref{Cdouble}(0.0)
     dJdc = zeros(nc)
-    evaluate!(c) = if kind != QOC_COST_EXTERNAL && device_penalty
-        check(ccall((:qoc_eval_spline, libqoc), Cint,
-                    (Ptr{Cvoid}, Ptr{Float64}, Cint, Ref{Cdouble}, Ptr{Float64}),
-                    cache.ctx, c, 3, J, dJdc), cache.ctx)
-    else  # examples/ipopt_callbacks_exp.jl:14-18, 27-28 with the caller's closures
+    on_device = kind != QOC_COST_EXTERNAL && device_penalty
+    # f: examples/ipopt_callbacks_exp.jl:11-19 — spline map, propagate, cost; no sensitivity
+    propagate!(c) = if on_device
+        check(ccall((:qoc_propagate_spline, libqoc), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ref{Cdouble}),
+                    cache.ctx, c, J), cache.ctx)
+    else
         u = Matrix(transpose(Bm * reshape(c, nsplines, nu)))
         x = QOC.propagate(A0Δt, A, u, x0, cache)
         J[] = Jfinal(x[end]) + (no_penalty(L) ? 0.0 : sum(L, x))
+    end
+    # f_grad: :21-31 — the sensitivity of the last propagated c, mapped to the coefficients (B' dJdu')
+    sensitivity!(c) = if on_device
+        check(ccall((:qoc_sensitivity_spline, libqoc), Cint, (Ptr{Cvoid}, Ptr{Float64}, Cint, Ptr{Float64}),
+                    cache.ctx, c, 3, dJdc), cache.ctx)
+    else
         dJdu = QOC.grape_sensitivity(A0Δt, A, dJfinal_dx, cache.u, x0, cache; dUkdp_order=3, dL_dx=dL_dx)
         dJdc .= (Bm' * transpose(dJdu))[:]
     end
     f = function (c::Vector{Float64})
         c_prev .= c
-        evaluate!(c)
+        propagate!(c)
         J[]
     end
     f_grad = function (c, f_grad_out)
-        c_prev == c || evaluate!(c)
+        if c_prev != c  # Ipopt asked for the gradient first (:22-25)
+            c_prev .= c
+            propagate!(c)
+        end
+        sensitivity!(c)
         f_grad_out .= dJdc
     end
     g_oop = function (c)

@@ -64,12 +64,15 @@ SIGNATURES = {
     "qoc_set_chain": (C.c_int, [_vp, C.c_int]),
     "qoc_comm_unique_id": (C.c_int, [_vp]),
     "qoc_comm_init": (C.c_int, [_vp, C.c_int, C.c_int, _vp, C.c_longlong]),
+    "qoc_comm_ranks": (C.c_int, [_vp]),
     "qoc_allgather_best": (C.c_int, [_vp, _dp, _ip]),
     "qoc_allgather_best_dev": (C.c_int, [_vp, _vp]),
     "qoc_chain_terms": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_set_spline_basis": (C.c_int, [_vp, _dp, C.c_int]),
     "qoc_eval_spline_dev": (C.c_int, [_vp, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "qoc_eval_spline": (C.c_int, [_vp, _dp, C.c_int, _dp, _dp]),
+    "qoc_propagate_spline": (C.c_int, [_vp, _dp, _dp]),
+    "qoc_sensitivity_spline": (C.c_int, [_vp, _dp, C.c_int, _dp]),
     "qoc_spline_constraints_dev": (C.c_int, [_vp, C.c_void_p, C.c_void_p, C.c_void_p]),
     "qoc_gemm_stats": (C.c_int, [_vp, _dp, C.POINTER(C.c_longlong), _dp, C.c_int]),
     "qoc_expm_batched": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _ip, _ip]),

@@ -227,7 +227,12 @@ def propagate(A0, A, u, x0, cache: MI355XCache | None = None):
     A cache last used by propagate_pwc (Tsit5) is switched back to the exponential."""
     u = np.asarray(u, dtype=np.float64)
     if cache is None:
-        cache = setup_grape_cache(A0, x0, u.shape[-2:], B=1 if u.ndim == 2 else u.shape[0])
+        # the reference converts x0 to complex before building its cache (src/gradient_computations.jl:4-8), so
+        # a real N-row x0 is a complex state; only a 2N-row real x0 is the complex2real layout
+        x0c = np.asarray(x0)
+        if not np.iscomplexobj(x0c) and x0c.shape[0] != 2 * np.shape(A0)[0]:
+            x0c = x0c.astype(np.complex128)
+        cache = setup_grape_cache(A0, x0c, u.shape[-2:], B=1 if u.ndim == 2 else u.shape[0])
     if getattr(cache.engine, "prop_method", "expm") != "expm":
         cache.engine.set_propagation("expm")
     return _propagate(A0, A, u, x0, cache)

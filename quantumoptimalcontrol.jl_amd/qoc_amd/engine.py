@@ -248,6 +248,22 @@ class GrapeEngine:
         self._chk(self._lib.qoc_eval_spline(self._h, _ptr(cf), _order(order), _ptr(J), _ptr(g)))
         return J, np.transpose(g, (0, 2, 1)).copy()
 
+    def propagate_spline(self, c):
+        """Ipopt's f alone (examples/ipopt_callbacks_exp.jl:11-19): spline map + propagate + J, no sensitivity."""
+        c = np.asarray(c, dtype=np.float64).reshape(self.B, self.ns, self.nu)
+        cf = np.ascontiguousarray(np.transpose(c, (0, 2, 1)))
+        J = np.zeros(self.B)
+        self._chk(self._lib.qoc_propagate_spline(self._h, _ptr(cf), _ptr(J)))
+        return J
+
+    def sensitivity_spline(self, c, order: int = 3):
+        """Ipopt's f_grad sensitivity (:21-31) for the coefficients of the last propagate_spline -> dJdc."""
+        c = np.asarray(c, dtype=np.float64).reshape(self.B, self.ns, self.nu)
+        cf = np.ascontiguousarray(np.transpose(c, (0, 2, 1)))
+        g = np.zeros_like(cf)
+        self._chk(self._lib.qoc_sensitivity_spline(self._h, _ptr(cf), _order(order), _ptr(g)))
+        return np.transpose(g, (0, 2, 1)).copy()
+
     def eval_spline_device(self, d_c: int, order: int, d_J: int, d_dJdc: int):
         """Device pointers: c and dJdc are B x nu x ns doubles (column-major ns x nu per seed)."""
         self._chk(self._lib.qoc_eval_spline_dev(self._h, C.c_void_p(d_c), _order(order), C.c_void_p(d_J),
@@ -310,9 +326,16 @@ class GrapeEngine:
     # ---- multi-GPU epilogue (include/qoc.h qoc_comm_* / qoc_allgather_best) -------------
     def comm_init(self, world: int, rank: int, unique_id: bytes | None, seed_offset: int):
         """Join the RCCL communicator of `world` ranks (unique_id: the QOC_UNIQUE_ID_BYTES bytes one rank made
-        with comm_unique_id(); None for world = 1).  seed_offset: global id of this context's seed 0."""
+        with comm_unique_id(); with world = 1 it makes a one-rank communicator, None makes none).
+        seed_offset: global id of this context's seed 0."""
         buf = C.create_string_buffer(bytes(unique_id), 128) if unique_id is not None else None
         self._chk(self._lib.qoc_comm_init(self._h, int(world), int(rank), buf, int(seed_offset)))
+
+    def comm_ranks(self) -> int:
+        """Ranks of the engine's RCCL communicator (0: none; the epilogue then covers this engine alone)."""
+        r = self._lib.qoc_comm_ranks(self._h)
+        self._chk(min(r, 0))
+        return int(r)
 
     def allgather_best(self):
         """(J_best, global seed) of the last propagate over every rank of the communicator."""

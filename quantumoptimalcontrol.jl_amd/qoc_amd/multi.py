@@ -40,9 +40,11 @@ def gather_best(J_local, seed_offset: int, out=None):
     return float(allv[r, 0]), int(allv[r, 1])
 
 
-def init_engine_comm(engine, seed_offset: int) -> bool:
+def init_engine_comm(engine, seed_offset: int) -> str:
     """Join the engine's RCCL communicator over the default process group: rank 0 makes the unique id and
-    torch.distributed broadcasts it.  Returns False (and leaves the engine on its own) when RCCL is missing."""
+    torch.distributed broadcasts it (a one-rank communicator at world 1, through the same ncclAllGather path).
+    Returns the transport of the epilogue: "rccl-libqoc" when every rank joined a communicator of `world`
+    ranks, else "torch.distributed" (world > 1, RCCL missing) or "local" (world 1 without RCCL)."""
     import torch.distributed as dist
 
     from . import _lib
@@ -50,17 +52,33 @@ def init_engine_comm(engine, seed_offset: int) -> bool:
 
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
-    if world == 1:
-        engine.comm_init(1, 0, None, seed_offset)
-        return True
     box = [None]
     if rank == 0:
         try:
             box[0] = comm_unique_id()
         except _lib.QOCError:
             box[0] = b""
-    dist.broadcast_object_list(box, src=0)
-    if not box[0]:
-        return False
-    engine.comm_init(world, rank, box[0], seed_offset)
-    return True
+    if world > 1:
+        dist.broadcast_object_list(box, src=0)
+    ok = bool(box[0])
+    if ok:
+        try:
+            engine.comm_init(world, rank, box[0], seed_offset)
+        except _lib.QOCError:
+            ok = False
+    ok = ok and engine.comm_ranks() == world
+    if world > 1:  # every rank must take the same transport
+        import torch
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        if dist.get_backend() == "nccl":
+            flag = flag.cuda()
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = bool(flag.item())
+        if not ok:
+            engine.comm_init(1, 0, None, seed_offset)  # drop any communicator; gather over torch.distributed
+            return "torch.distributed"
+        return "rccl-libqoc"
+    if not ok:
+        engine.comm_init(1, 0, None, seed_offset)
+        return "local"
+    return "rccl-libqoc"

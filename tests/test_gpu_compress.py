@@ -184,3 +184,28 @@ def test_errors(built_lib):
     with pytest.raises(QOCError, match="couple"):
         e.set_generators(A0, prob.A)
     e.close()
+
+
+@pytest.mark.parametrize("zcal", [False, True])
+def test_failed_repack_leaves_the_packing_intact(built_lib, zcal):
+    """A re-pack that x0 fails (entries outside the new blocks) leaves the previous packing fully in place: the host
+    layout, the device row sectors and the z-calibrated column map; J and dJ/du still match the oracle."""
+    from qoc_amd import QOCError
+    prob, v, u = _block_problem(seed=21)
+    e = _engine(prob, v, u.shape[0], chain="taylor", zcal=zcal)
+    (r1, c1), (r2, c2) = v
+    with pytest.raises(QOCError, match="outside the compress_states blocks"):
+        e.set_compression(((r1, c2), (r2, c1)))  # x0's columns c1 live on r1: outside the swapped blocks
+    assert e.info()["kernel_m"] == 2
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    cost = O.setup_infidelity_zcalibrated(prob.x_target) if zcal else None
+    for b in range(u.shape[0]):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3, cost=cost)
+        assert abs(J[b] - Jr) <= 1e-12, (b, J[b], Jr)
+        if zcal:
+            res, dth = O.zcal_gradient_match(g[b], prob.A0, prob.A, u[b], prob.x0, prob.x_target, order=3)
+            assert res <= 1e-10 and abs(dth) <= 1e-6, (b, res, dth)
+        else:
+            assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
+    e.close()

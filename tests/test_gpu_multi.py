@@ -1,7 +1,8 @@
 """Multi-GPU epilogue on the one-GPU box.
 
-* qoc_allgather_best through the C ABI (RCCL communicator of one rank): the best (J, global seed) of the last
-  propagate equals the argmin over the engine's J.
+* qoc_allgather_best through the C ABI: without a communicator, and with a real one-rank RCCL communicator
+  (qoc_comm_unique_id -> ncclCommInitRank(nranks = 1) -> ncclAllGather) created next to torch's own "nccl"
+  process group in the same process; the best (J, global seed) of the last propagate equals the argmin.
 * Two ranks sharing the one device, each propagating its contiguous shard of the seeds through its own engine:
   the gathered best equals the single-process argmin over the full batch.  RCCL rejects two ranks on one GPU
   ("Duplicate GPU detected"), so these two ranks exchange over gloo (qoc_amd.multi.gather_best); the RCCL
@@ -36,6 +37,57 @@ def test_allgather_best_world1_c_abi(built_lib):
     Jb, sb = e.allgather_best()
     assert Jb == J.min() and sb == 1000 + int(np.argmin(J))
     e.close()
+
+
+def _rccl_world1(port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "quantumoptimalcontrol.jl_amd"))
+    import torch
+    import torch.distributed as dist
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+        t = torch.ones(4, device="cuda")
+        dist.all_reduce(t)  # torch's RCCL communicator is up
+        from qoc_amd import GrapeEngine, multi
+        prob, u = _problem()
+        e = GrapeEngine(prob.A0, prob.A, prob.x0, NT, B=B_TOTAL)
+        e.set_cost_trace(prob.x_target, prob.n)
+        J = e.propagate(u)
+        transport = multi.init_engine_comm(e, 1000)  # libqoc's own one-rank RCCL communicator
+        ranks = e.comm_ranks()
+        Jb, sb = e.allgather_best()  # ncclAllGather inside libqoc_mi355x.so
+        d = torch.empty(2, dtype=torch.float64, device="cuda")
+        e.allgather_best_device(d.data_ptr())
+        e.synchronize()
+        dev = d.cpu().tolist()
+        dist.all_reduce(t)  # torch's communicator still works next to libqoc's
+        torch.cuda.synchronize()
+        ok_t = float(t[0].item()) == 1.0
+        e.close()
+        dist.destroy_process_group()
+        q.put(("ok", transport, ranks, (Jb, sb), dev, J.min(), int(np.argmin(J)), ok_t))
+    except Exception as ex:  # reported to the parent
+        q.put(("error", repr(ex)))
+
+
+def test_rccl_world1_communicator_next_to_torch_nccl(built_lib):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_world1, args=(_port(), q))
+    p.start()
+    res = q.get(timeout=100)
+    p.join(timeout=60)
+    assert res[0] == "ok", res
+    _, transport, ranks, (Jb, sb), dev, Jmin, amin, ok_t = res
+    assert transport == "rccl-libqoc" and ranks == 1
+    assert Jb == Jmin and sb == 1000 + amin
+    assert dev == [Jmin, float(1000 + amin)]
+    assert ok_t
+    assert p.exitcode == 0
 
 
 def _port():

@@ -225,6 +225,22 @@ def test_reference_shaped_api(built_lib):
     assert np.linalg.norm(g2 - gr2) / np.linalg.norm(gr2) < 1e-10
 
 
+def test_propagate_without_cache_real_x0(built_lib):
+    """propagate(A0, A, u, x0) with no cache and a real N x m x0 (np.eye(N)[:, :m]): the reference converts x0 to
+    complex before building the cache (src/gradient_computations.jl:4-8), so it is a complex state, not the
+    2N-row complex2real layout."""
+    import qoc_amd as Q
+    from qoc_amd import systems
+    prob = systems.zz_problem(20, tgate=2.0)
+    u = systems.zz_controls(1, 20, 2.0, seed=6)[0]
+    x0 = np.eye(prob.N)[:, :4]
+    x = Q.propagate(prob.A0, prob.A, u, x0)
+    c = O.setup_grape_cache(prob.A0, x0.astype(complex), u.shape)
+    xr = O.propagate(prob.A0, prob.A, u, x0.astype(complex), c)
+    assert len(x) == 21
+    assert np.abs(x[20] - xr[20]).max() < 1e-13
+
+
 @pytest.mark.parametrize("chain", CHAINS)
 def test_fp32_small(built_lib, chain):
     from qoc_amd import systems
@@ -577,6 +593,8 @@ def test_overlapped_backward_ranges_are_bit_identical(built_lib, monkeypatch, ra
         g = e.grape_sensitivity(u, 3)
         launches = e.phase_times()["k_chain_bwd"][1]
         lam = [e.costate(k, seed=b) for b in range(3) for k in range(prob.Nt + 1)]
+        g2 = e.grape_sensitivity(u, 3)  # a second call on the same propagate: the same result
+        assert np.array_equal(g, g2)
         e.close()
         out.append((J, g, np.array(lam), launches))
     assert out[0][3] == 1 and out[1][3] == int(ranges[0])
@@ -586,3 +604,34 @@ def test_overlapped_backward_ranges_are_bit_identical(built_lib, monkeypatch, ra
         Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3, penalty=pen)
         assert abs(out[1][0][b] - Jr) <= 1e-12
         assert np.linalg.norm(out[1][1][b] - gr) / np.linalg.norm(gr) <= 1e-10
+
+
+def test_overlapped_backward_with_costate_source_repeated(built_lib, monkeypatch):
+    """The overlapped backward (ranges + gradient on the second stream) with the caller's co-state source, twice in a
+    row on one engine and once more after a new propagate: every call matches the single-launch backward bitwise
+    and the oracle's gradient with the same dL/dx closure."""
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=10, Nt=96)
+    u = systems.cavity_controls(2, prob.Nt, seed=23)
+    Lo, dLo = O.setup_state_penalty([1, 4], [0, 1], 0.15)
+    res = []
+    for chunks in ("1", "4"):
+        monkeypatch.setenv("QOC_BWD_CHUNKS", chunks)
+        e = _engine(prob, 2, chain="taylor")
+        out = []
+        for uu in (u, u, u * 0.9):
+            e.propagate(uu)
+            src = np.stack([np.stack([dLo(e.state(k, seed=b)) for k in range(prob.Nt + 1)]) for b in range(2)])
+            e.set_costate_source(src)
+            out.append(e.grape_sensitivity(uu, 3))
+        e.close()
+        res.append(out)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
+    for i, uu in enumerate((u, u, u * 0.9)):
+        for b in range(2):
+            c = O.setup_grape_cache(prob.A0, prob.x0, uu[b].shape)
+            O.propagate(prob.A0, prob.A, uu[b], prob.x0, c)
+            gr = O.grape_sensitivity(prob.A0, prob.A, O.setup_infidelity(prob.x_target, prob.n)[1], c.u, prob.x0, c,
+                                     dUkdp_order=3, dL_dx=dLo)
+            assert np.linalg.norm(res[1][i][b] - gr) / np.linalg.norm(gr) <= 1e-10

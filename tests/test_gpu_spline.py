@@ -52,6 +52,30 @@ def test_eval_spline_matches_oracle(built_lib):
     e.close()
 
 
+def test_f_alone_then_f_grad_like_the_reference_callbacks(built_lib):
+    """Ipopt's f only propagates (examples/ipopt_callbacks_exp.jl:11-19) and f_grad runs the sensitivity for the
+    coefficients f last saw (:21-31): qoc_propagate_spline + qoc_sensitivity_spline give the fused eval's J and
+    dJdc bitwise; the sensitivity refuses other coefficients (the reference's stale-u error)."""
+    from qoc_amd import GrapeEngine, StaleCacheError
+    prob, Bs = _zz()
+    ns = Bs.shape[1]
+    rng = np.random.default_rng(3)
+    c = (0.2 * rng.standard_normal((2, ns * 2))).reshape(2, 2, ns).transpose(0, 2, 1)
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2)
+    e.set_cost_trace(prob.x_target, prob.n)
+    e.set_spline_basis(Bs)
+    J0, g0 = e.eval_spline(c)
+    J1 = e.propagate_spline(c)
+    assert np.array_equal(J0, J1)
+    g1 = e.sensitivity_spline(c)
+    assert np.array_equal(g0, g1)
+    with pytest.raises(StaleCacheError, match="Cache data from other control signal u"):
+        e.sensitivity_spline(c * 1.001)
+    e.propagate_spline(c * 1.001)  # a line-search f: no sensitivity
+    e.sensitivity_spline(c * 1.001)
+    e.close()
+
+
 def test_multistart_optimiser_parity_with_oracle_driven_run(built_lib):
     from qoc_amd import GrapeEngine
     from qoc_amd.optimize import SplineGrape, minimize_batched, spline_constraints_torch

@@ -53,3 +53,36 @@ def test_gather_best_gloo_world2():
         assert p.exitcode == 0
     for rank, (J, seed) in out:
         assert J == pytest.approx(0.01) and seed == 10 + 3
+
+
+def test_bench_launcher_starts_two_ranks_cpu():
+    """`python bench.py --gpus 2` with no WORLD_SIZE starts its own two ranks (torch.distributed.run) and rank 0
+    reports n_gpus 2; --cpu-plumbing runs the ranks' best-(J, seed) exchange over gloo without a GPU."""
+    import json
+    import subprocess
+    import sys
+
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--cpu-plumbing",
+                          "--steps", "3", "--warmup", "1", "--seeds", "8"], capture_output=True, text=True,
+                         timeout=240, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 only
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["config"]["global_seeds"] == 16
+    J = np.concatenate([np.random.default_rng(r).uniform(0.1, 1.0, 8) for r in range(2)])
+    assert rec["best_over_ranks"]["seed"] == int(np.argmin(J))
+    assert rec["best_over_ranks"]["J"] == J.min()
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--cpu-plumbing"],
+                         capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
