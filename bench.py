@@ -63,13 +63,14 @@ def ref_eval_flops(N, m, nu, hist_per_eval, order=3):
     return f
 
 
-def grad_flops(N, m, nu, Nt, B, order):
-    """Executed algorithmic FLOPs of the gradient phase.  Order 3 (the Ipopt path) runs as GEMMs over all
-    slices: 4 generator-combine GEMMs (N x (nu+1)N per state column: P1, P2, Q1, Q2) and 3 contraction
-    GEMMs (nu N x N: A_j P_a).  Other orders: k_grad's (order-1) X and X^H matvecs + nu*order A_j matvecs."""
+def grad_flops(N, m, nu, Nt, B, order, captured=False):
+    """Executed algorithmic FLOPs of the gradient phase.  Order 3 (the Ipopt path): 4 generator-combine products
+    (N x (nu+1)N per state column: P1, P2, Q1, Q2) and 3 nu contraction products (A_j P_a), 8 N^2 m each per slice;
+    with the chains' captured products (k_grad_rr_c) P1, P2, Q1, Q2 come from the chains and only the 3 nu
+    contractions run.  Other orders: k_grad's (order-1) X and X^H matvecs + nu*order A_j matvecs."""
     mv = 8.0 * N * N * m
     if order == 3:
-        return B * Nt * mv * (4 * (nu + 1) + 3 * nu)
+        return B * Nt * mv * ((0 if captured else 4 * (nu + 1)) + 3 * nu)
     return B * Nt * (2 * (order - 1) * mv + nu * order * mv)
 
 
@@ -369,7 +370,8 @@ def main():
         tl = terms / K
         models = {
             "k_expm": ("mfma", 0.0, "TFLOP/s", peak),  # k_tchain_prep: (P, s, e^mu) per slice, no flops counted
-            "k_grad": ("mfma", grad_flops(N, m, nu, Nt, B, args.order) / 1e12, "TFLOP/s", peak),
+            "k_grad": ("mfma", grad_flops(N, m, nu, Nt, B, args.order,
+                                          info1.get("backward") in ("captured", "concurrent")) / 1e12, "TFLOP/s", peak),
             "k_chain_fwd": ("mfma", 8.0 * N * N * m * tl / 1e12, "TFLOP/s", peak),
             "k_chain_bwd": ("mfma", 8.0 * N * N * m * tl / 1e12, "TFLOP/s", peak),
         }
@@ -410,7 +412,8 @@ def main():
     if taylor:
         mf = prob.precision == "fp64"
         names = {"k_expm": "k_tchain_prep", "k_chain_fwd": "k_tchain_mf_fwd" if mf else "k_tchain_fwd",
-                 "k_chain_bwd": "k_tchain_mf_bwd" if mf else "k_tchain_bwd", "k_grad": "k_grad_rr"}
+                 "k_chain_bwd": "k_tchain_mf_bwd" if mf else "k_tchain_bwd",
+                 "k_grad": "k_grad_rr_c" if info1.get("backward") in ("captured", "concurrent") else "k_grad_rr"}
         for k in ("k_chain_fwd", "k_chain_bwd"):
             # serial Taylor terms of one seed per launch and the time each takes (the chains' critical path)
             kern[k]["kernel"] = names[k]
@@ -423,6 +426,8 @@ def main():
                 "launches_per_step": lps[dom],
                 "note": ("latency-bound serial recurrence (one workgroup per seed, Taylor terms in sequence): "
                          "achieved = executed matvec flops / launch time"
+                         + ("; the backward (μ) recurrence runs beside the forward chain on a second stream, the "
+                            "contraction after both" if info1.get("backward") == "concurrent" else "")
                          + ("; the backward chain runs in slice ranges, each range's gradient overlapped with "
                             "the next range" if lps.get("k_chain_bwd", 1) > 1 else ""))}
     elif not large:

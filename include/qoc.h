@@ -178,9 +178,11 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
  * info[3] = device bytes allocated by the context, info[4] = chain mode (QOC_CHAIN_PROPAGATORS /
  * QOC_CHAIN_TAYLOR), info[5] = exponential the propagators run (0 the reference's Padé + solve, 1 register-
  * resident Taylor / Paterson-Stockmeyer, 2 LDS Paterson-Stockmeyer), info[6] = 1 when the Taylor-action chains
- * use Chebyshev terms (skew-Hermitian generators, fp64; QOC_TCHAIN_POLY=taylor keeps Taylor), info[7] = state columns the kernels run on (m, or max(nc1, nc2) with qoc_set_compression).  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
+ * use Chebyshev terms (skew-Hermitian generators, fp64; QOC_TCHAIN_POLY=taylor keeps Taylor), info[7] = state columns the kernels run on (m, or max(nc1, nc2) with qoc_set_compression), info[8] = how the
+ * last backward ran (0 generic, 1 from the chains' captured products, 2 concurrent μ recurrence of qoc_eval_dev),
+ * info[9] = 1 when the last forward chain wrote its captured products.  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
  * selects the large-N path for any size (testing). */
-int qoc_get_info(qoc_ctx* ctx, long long* info /*[8]*/);
+int qoc_get_info(qoc_ctx* ctx, long long* info /*[10]*/);
 
 /* How the chains x_{k+1} = U_k x_k (src/gradient_computations.jl:27-29) and λ_k = U_k^H λ_{k+1} (:52-58)
  * apply the slice exponentials:

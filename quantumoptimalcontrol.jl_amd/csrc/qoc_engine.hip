@@ -326,6 +326,8 @@ int forward(qoc_ctx* c) {
   return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
 }
 int backward(qoc_ctx* c, int order, double* d_dJdu) {
+  c->L_is_mu = false;  // every backward path below writes λ itself
+  c->last_eval_mode = 0;
   if (c->src_on && c->prop_method == QOC_PROP_TSIT5)
     return fail(c, QOC_ERR_UNSUPPORTED, "a co-state source (dL_dx) is not part of the Tsit5 path (compute_pwc_gradient)");
   if (c->big)
@@ -477,6 +479,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   if (getenv("QOC_BWD_LAST")) c->bwd_last_frac = atof(getenv("QOC_BWD_LAST"));
   if (getenv("QOC_BWD_PRIO")) c->bwd_prio = atoi(getenv("QOC_BWD_PRIO"));
   if (getenv("QOC_BWD_PRESTATE")) c->bwd_prestate = atoi(getenv("QOC_BWD_PRESTATE"));
+  if (getenv("QOC_CONCURRENT")) c->concurrent = atoi(getenv("QOC_CONCURRENT")) != 0;
   hipMemset(c->d_L, 0, (size_t)B * (Nt + 1) * Nm * c->esz);
   *out = c;
   return QOC_OK;
@@ -489,6 +492,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->comm && rccl().commDestroy) rccl().commDestroy(c->comm);
   if (c->d_best) hipFree(c->d_best);
   if (c->d_tcoef) hipFree(c->d_tcoef);
+  if (c->d_coef_mu) hipFree(c->d_coef_mu);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
                   c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_pws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec};
   for (void* p : ptrs)
@@ -556,6 +560,9 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
   }
   if (c->tchain_ok) {  // shifted generators Ã_j = A_j - μ_j I and their norms for the Taylor-action chains
     tchain_thresholds(c->tprm, c->prec);
+    const char* capenv = getenv("QOC_CAPTURE");
+    c->cap_ok = c->prec == QOC_FP64 && !(capenv && atoi(capenv) == 0);
+    c->tprm.pmin = c->cap_ok ? 2 : 1;  // the captured products are the first two of every slice
     // Chebyshev needs every Ã_j skew-Hermitian (A_j^H = -A_j, Schrödinger generators -i H Δt), so that
     // Ã_k = -i H̃_k has its spectrum on the imaginary axis within the bound ρ_k
     bool skew = true;
@@ -850,6 +857,25 @@ int qoc_grape_sensitivity_dev(qoc_ctx* c, const double* d_u, int order, double* 
 int qoc_eval_dev(qoc_ctx* c, const double* d_u, int order, double* d_J, double* d_dJdu) {
   if (c && c->cost_kind == QOC_COST_EXTERNAL)
     return fail(c, QOC_ERR_STATE, "qoc_eval_dev needs a device-side cost (TRACE or ZCAL)");
+  if (c && c->have_gen && tchain_concurrent_ok(c, order)) {
+    // forward chain and the μ recurrence side by side (tchain_eval_concurrent)
+    int r = check_ready(c);
+    if (r) return r;
+    if (!d_u) return fail(c, QOC_ERR_ARG, "d_u is null");
+    const size_t nu_t = (size_t)c->B * c->nu * c->Nt;
+    if (d_u != c->d_u) HIPCHK(c, hipMemcpyAsync(c->d_u, d_u, nu_t * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    c->have_prop = false;
+    r = c->prec == QOC_FP64 ? tchain_eval_concurrent<double>(c, d_dJdu ? d_dJdu : c->d_dJdu)
+                            : tchain_eval_concurrent<float>(c, d_dJdu ? d_dJdu : c->d_dJdu);
+    if (r) return r;
+    c->props_since_reset++;
+    if (d_J && d_J != c->d_J)
+      HIPCHK(c, hipMemcpyAsync(d_J, c->d_J, c->B * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    c->have_prop = true;
+    c->h_u.clear();
+    c->h_coef.clear();
+    return QOC_OK;
+  }
   int r = qoc_propagate_dev(c, d_u, d_J);
   if (r) return r;
   if (order < 0 || order > 4) return fail(c, QOC_ERR_ARG, "dUkdp_order must be 1..4 or QOC_DUKDP_EXACT (got %d)", order);
@@ -926,7 +952,29 @@ int qoc_get_costates(qoc_ctx* c, int seed, int k, double* lam_out) {
   if (seed < 0 || seed >= c->B || k < 0 || k > c->Nt) return fail(c, QOC_ERR_ARG, "index out of range");
   HIPCHK(c, hipSetDevice(c->dev));
   const size_t Nm = (size_t)c->N * c->m;
-  return download_states(c, (char*)c->d_L + ((size_t)seed * (c->Nt + 1) + k) * Nm * c->esz, lam_out);
+  const void* src = (char*)c->d_L + ((size_t)seed * (c->Nt + 1) + k) * Nm * c->esz;
+  if (!c->L_is_mu) return download_states(c, src, lam_out);
+  // the concurrent eval left μ_k: λ_k = coef ⊙ μ_k (per row sector and packed column, lam_coef)
+  std::vector<double> mu(2 * Nm), cf(4 * (size_t)c->m);
+  int r = download(c, src, mu.data(), Nm);
+  if (r) return r;
+  HIPCHK(c, hipMemcpy(cf.data(), c->d_coef_mu + (size_t)seed * 2 * c->m, 2 * (size_t)c->m * sizeof(cx<double>),
+                      hipMemcpyDeviceToHost));
+  for (int col = 0; col < c->m; ++col)
+    for (int row = 0; row < c->N; ++row) {
+      const int sct = c->packed ? c->h_rsec[row] : 0;
+      const double fr = cf[2 * (sct * c->m + col)], fi = cf[2 * (sct * c->m + col) + 1];
+      double* v = mu.data() + 2 * (row + (size_t)c->N * col);
+      const double vr = v[0], vi = v[1];
+      v[0] = fr * vr - fi * vi;
+      v[1] = fr * vi + fi * vr;
+    }
+  if (!c->packed) {
+    std::memcpy(lam_out, mu.data(), 2 * Nm * sizeof(double));
+    return QOC_OK;
+  }
+  unpack_states(c, mu.data(), lam_out);
+  return QOC_OK;
 }
 
 int qoc_get_propagator(qoc_ctx* c, int seed, int k, double* U_out) {
@@ -1168,6 +1216,8 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[5] = c->big ? c->expm_alg : c->expm_run;  // the large-N pipeline keeps its own (Taylor / Padé) choice
   info[6] = c->chain_mode == 1 && c->cheb && tchain_mf(c) ? 1 : 0;  // Taylor-action chains: Chebyshev terms
   info[7] = c->m;  // state columns the kernels run on (< the caller's m when compress_states packing is on)
+  info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 concurrent μ recurrence
+  info[9] = c->fwd_captured ? 1 : 0;
   return QOC_OK;
 }
 

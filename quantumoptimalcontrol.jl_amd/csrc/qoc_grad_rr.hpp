@@ -388,4 +388,149 @@ __global__ __launch_bounds__(256, 2) void k_grad_rr_s(int N, int m, int Nt, int 
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Contraction from the chains' captured products (k_grad_rr_c).  The register-resident MFMA chains write, per slice,
+// their first two products D1 = Â v, D2 = Â y_1 with Â = scale · Ã_k (Ã_k = A_k − μ_k I, the exact scalar shift) and
+// y_1 = D1 / κ' (κ' = 2 Chebyshev, 1 Taylor): Ã v = r D1 and Ã² v = κ r² D2 with r = 1 / scale, κ = κ'.  So, with
+// A_k = Ã_k + μ_k I (src/gradient_computations.jl:18-22) and the products of the reference's order-3 Jacobian
+// (:177-213, contracted as in k_grad_rr_q / _p):
+//   P1 = A x = μ x + r F1,   P2 = A² x = μ² x + 2 μ r F1 + κ r² F2            (F: forward captures, v = x_k)
+//   Q1 = A^H λ = μ̄ λ + r G1, Q2 = μ̄² λ + 2 μ̄ r G1 + κ r² G2                  (G: backward captures, v = λ_{k+1})
+//   W0 = λ + Q1/2 + Q2/6,    W1 = λ/2 + Q1/6
+//   dJdu[k, j] = Re[<W0, A_j x> + <W1, A_j P1> + <λ/6, A_j P2>]
+// i.e. only the 3 nu contractions are generator products.  μ mode (coef != nullptr): the backward chain ran from
+// X_target (μ_k = U_k^H .. U_{Nt-1}^H X_target) and λ = coef ⊙ μ element-wise (lam_coef: per row sector and column),
+// which commutes with every product above, so W0, W1 and λ are scaled by the coefficient on load.
+struct GradCapArgs {
+  int N, m, Nt, B, k0, nk;
+  const void* Agen;          // generators A_j (unshifted), column-major
+  const double* u;           // B x Nt x nu
+  const void* X;             // states (B x (Nt+1) x N x m)
+  const void* L;             // co-states λ, or μ in μ mode
+  const void* F1;            // forward captures D1, D2 at slice k
+  const void* F2;
+  const void* G1;            // backward captures D1, D2 at slice k
+  const void* G2;
+  const double* steps;       // TStep records, 4 doubles each (scale at [3])
+  double mur[3], mui[3];     // shifts μ_j: μ_k = μ_0 + Σ_j u_jk μ_j
+  double kappa;              // 2 Chebyshev, 1 Taylor
+  const cx<double>* coef;    // μ mode: λ_N coefficients (B x 2m, chain_costs); nullptr: L holds λ
+  unsigned long long rsec_mask;  // packed states: bit r = row sector of row r (N <= 64), else 0
+  double* dJdu;
+};
+
+template <int NT, int KS, int NU>
+__global__ __launch_bounds__(256, 2) void k_grad_rr_c(const GradCapArgs a) {
+  using G = GradRR<double, NT>;
+  using Own = typename G::Own;
+  using M = MF<double>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int N = a.N, m = a.m, Nt = a.Nt;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6;
+  double* Gr = reinterpret_cast<double*>(smem);
+  double* Gi = Gr + (size_t)(NU + 1) * N * G::ldp(N);
+  grad_gens_to_lds<double, NT>(N, NU, (const cx<double>*)a.Agen, Gr, Gi);
+  const long long units = (long long)a.B * a.nk, ntiles = (units + 16 / m - 1) / (16 / m);
+  const int col = (lane & 15) % m;
+  // V = c * src (ACC: V += c * src) over this lane's entries; rows >= N read the last row (masked later)
+  // the lane index is made opaque per call: otherwise every row offset / mask of every call is hoisted out of the
+  // tile loop (loop-invariant) and spilled
+  auto ld = [&](Own& V, const void* srcv, size_t base, cx<double> c, bool accum) __attribute__((always_inline)) {
+    const cx<double>* src = (const cx<double>*)srcv + base;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const cx<double> x = src[min(16 * t + M::drow(ln, e), N - 1)];
+        const double vr = c.r * x.r - c.i * x.i, vi = c.r * x.i + c.i * x.r;
+        V.r[t][e] = accum ? V.r[t][e] + vr : vr;
+        V.i[t][e] = accum ? V.i[t][e] + vi : vi;
+      }
+    asm volatile("" ::: "memory");  // one source at a time
+  };
+  // rows >= N (and tiles past the last unit) -> 0; μ mode: × λ_N coefficient of (row sector, column)
+  auto fin = [&](Own& V, bool ok, bool scl, cx<double> f0, cx<double> f1) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = 16 * t + M::drow(ln, e);
+        const bool in = ok && row < N;
+        double vr = V.r[t][e], vi = V.i[t][e];
+        if (scl) {
+          const cx<double> f = ((a.rsec_mask >> min(row, 63)) & 1ull) ? f1 : f0;
+          const double wr = f.r * vr - f.i * vi;
+          vi = f.r * vi + f.i * vr;
+          vr = wr;
+        }
+        V.r[t][e] = in ? vr : 0.0;
+        V.i[t][e] = in ? vi : 0.0;
+      }
+  };
+  for (long long tile = (long long)blockIdx.x * nw + wave; tile < ntiles; tile += (long long)gridDim.x * nw) {
+    const GradTile g = grad_tile(tile, lane, N, m, Nt, a.k0, a.nk, units);
+    double sj[NU], s2[NU];
+    double mr = a.mur[0], mi = a.mui[0];
+#pragma unroll
+    for (int j = 0; j < NU; ++j) {
+      const double uj = a.u[g.unit * NU + j];
+      mr += uj * a.mur[j + 1];
+      mi += uj * a.mui[j + 1];
+      sj[j] = 0.0;
+      s2[j] = 0.0;
+    }
+    const double r = 1.0 / a.steps[4 * g.unit + 3], kr2 = a.kappa * r * r;
+    const bool scl = a.coef != nullptr;
+    cx<double> f0 = {1.0, 0.0}, f1 = {1.0, 0.0};
+    if (scl) {
+      const cx<double>* cb = a.coef + (size_t)(g.unit / Nt) * 2 * m;
+      f0 = cb[col];
+      f1 = cb[m + col];
+    }
+    const double br = mr, bi = -mi;                                  // conj(μ_k)
+    const double b2r = mr * mr - mi * mi, b2i = -2.0 * mr * mi;      // conj(μ_k)^2
+    Own V, W;
+    // <W0, A_j x>,  W0 = (1 + μ̄/2 + μ̄²/6) λ + r (1/2 + μ̄/3) G1 + κ r²/6 G2
+    ld(W, a.L, g.bl, cx<double>{1.0 + br / 2 + b2r / 6, bi / 2 + b2i / 6}, false);
+    ld(W, a.G1, g.bx, cx<double>{r * (0.5 + br / 3), r * bi / 3}, true);
+    ld(W, a.G2, g.bx, cx<double>{kr2 / 6, 0.0}, true);
+    fin(W, g.ok, scl, f0, f1);
+    ld(V, a.X, g.bx, cx<double>{1.0, 0.0}, false);
+    fin(V, g.ok, false, f0, f1);
+    G::template contract<KS, NU>(N, Gr, Gi, V, W, sj, lane);
+    asm volatile("" ::: "memory");
+    // <W1, A_j P1>,  P1 = μ x + r F1,  W1 = (1/2 + μ̄/6) λ + r/6 G1
+    ld(V, a.X, g.bx, cx<double>{mr, mi}, false);
+    ld(V, a.F1, g.bx, cx<double>{r, 0.0}, true);
+    fin(V, g.ok, false, f0, f1);
+    ld(W, a.L, g.bl, cx<double>{0.5 + br / 6, bi / 6}, false);
+    ld(W, a.G1, g.bx, cx<double>{r / 6, 0.0}, true);
+    fin(W, g.ok, scl, f0, f1);
+    G::template contract<KS, NU>(N, Gr, Gi, V, W, sj, lane);
+    asm volatile("" ::: "memory");
+    // <λ, A_j P2> / 6,  P2 = μ² x + 2 μ r F1 + κ r² F2
+    ld(V, a.X, g.bx, cx<double>{b2r, -b2i}, false);
+    ld(V, a.F1, g.bx, cx<double>{2.0 * r * mr, 2.0 * r * mi}, true);
+    ld(V, a.F2, g.bx, cx<double>{kr2, 0.0}, true);
+    fin(V, g.ok, false, f0, f1);
+    ld(W, a.L, g.bl, cx<double>{1.0, 0.0}, false);
+    fin(W, g.ok, scl, f0, f1);
+    G::template contract<KS, NU>(N, Gr, Gi, V, W, s2, lane);
+    const int c = lane & 15;
+#pragma unroll
+    for (int j = 0; j < NU; ++j) {
+      double v = sj[j] + s2[j] * (1.0 / 6.0);
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      for (int o = 1; o < m; o <<= 1) v += __shfl_xor(v, o);
+      if (g.ok && lane < 16 && c % m == 0) a.dJdu[g.unit * NU + j] = v;
+    }
+  }
+}
+
 }  // namespace qoc

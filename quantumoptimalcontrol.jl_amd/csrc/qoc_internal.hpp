@@ -131,6 +131,16 @@ struct qoc_ctx {
   bool cheb_ran = false;         // what the last forward pass used (the backward pass reuses its steps)
   double* d_tcoef = nullptr;     // B x Nt x TCHEB_STRIDE Chebyshev coefficients (allocated on first use)
   long long props_since_reset = 0;  // forward passes since the last Padé-histogram reset (chain mode 1)
+  // Captured products (register-resident MFMA chains, order-3 fused gradient): the chains write their first two
+  // products per slice (forward -> d_pws, backward -> d_gws) and the gradient is k_grad_rr_c, contractions only.
+  bool cap_ok = false;           // the shape takes it (qoc_set_generators; QOC_CAPTURE=0 turns it off)
+  bool fwd_captured = false;     // the last forward pass wrote its captures
+  // qoc_eval_dev with a built-in cost and no penalty / co-state source: the backward recurrence runs from X_target
+  // (μ_k, λ_k = coef ⊙ μ_k) beside the forward chain on stream2 (QOC_CONCURRENT=0 turns it off)
+  bool concurrent = true;
+  bool L_is_mu = false;          // d_L holds μ_k (qoc_get_costates applies the coefficients d_coef_mu)
+  cx<double>* d_coef_mu = nullptr;  // B x 2m: the λ_N coefficients of the eval that left μ in d_L
+  int last_eval_mode = 0;        // 0 other, 1 captured sequential backward, 2 concurrent μ mode (qoc_get_info)
   // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
@@ -209,6 +219,8 @@ hipError_t launch_gen_aux(qoc_ctx* c);
 // ---- qoc_run_grad.hip ----
 template <typename T>
 int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode = 0);
+// k_grad_rr_c: the order-3 contraction from the chains' captures (mu_mode: L holds μ, λ = coef ⊙ μ)
+int grad_rr_cap(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode);
 
 // ---- qoc_run_ode.hip ----
 template <typename T>
@@ -222,8 +234,16 @@ hipError_t launch_terminal_cost(qoc_ctx* c);
 bool tchain_mf(const qoc_ctx* c);
 template <typename T>
 int tchain_forward(qoc_ctx* c);
+// flags: TB_CAPTURE (write the backward captures), TB_MU (start from X_target: μ mode); st: nullptr = c->stream
+enum { TB_CAPTURE = 1, TB_MU = 2 };
 template <typename T>
-int tchain_backward(qoc_ctx* c, int k_lo = 0, int k_hi = -1);
+int tchain_backward(qoc_ctx* c, int k_lo = 0, int k_hi = -1, hipStream_t st = nullptr, int flags = 0);
+template <typename T>
+int tchain_backward_captured(qoc_ctx* c, double* d_dJdu);
+template <typename T>
+int tchain_eval_concurrent(qoc_ctx* c, double* d_dJdu);
+bool tchain_concurrent_ok(const qoc_ctx* c, int order);
+int ensure_pws(qoc_ctx* c);
 template <typename T>
 int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu);
 hipError_t launch_pade_units(qoc_ctx* c, long long units);

@@ -80,6 +80,7 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
     int r = ode_adjoint<T>(c);
     if (r) return r;
   } else if (c->chain_mode == 1) {
+    if (order == 3 && c->grad_rr && c->fwd_captured) return tchain_backward_captured<T>(c, d_dJdu);
     if (order == 3 && c->grad_rr && c->bwd_chunks > 1 && c->Nt >= 64 && tchain_mf(c)) return tchain_backward_overlapped<T>(c, d_dJdu);
     int r = tchain_backward<T>(c);
     if (r) return r;

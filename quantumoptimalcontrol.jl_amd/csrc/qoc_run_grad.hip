@@ -70,6 +70,70 @@ int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int m
   return grad_rr_nt<T, 3, 2>(c, d_dJdu, st, k0, nk, mode);
 }
 
+// k_grad_rr_c over the units of slices [k0, k0 + nk) (fp64: the captures come from the MFMA chains)
+template <int NT, int KS, int NU>
+int grad_cap_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode) {
+  using G = GradRR<double, NT>;
+  const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
+  const size_t lds = G::lds_bytes(N, NU);
+  const long long units = (long long)B * nk, ntiles = (units + 16 / m - 1) / (16 / m);
+  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+  const int grid = (int)std::max<long long>(1, std::min<long long>((ntiles + 3) / 4, (long long)c->ncu * per_cu));
+  const size_t bufN = (size_t)N * ((size_t)B * (Nt + 1) * m);
+  GradCapArgs a{};
+  a.N = N;
+  a.m = m;
+  a.Nt = Nt;
+  a.B = B;
+  a.k0 = k0;
+  a.nk = nk;
+  a.Agen = c->d_A;
+  a.u = c->d_u;
+  a.X = c->d_X;
+  a.L = c->d_L;
+  a.F1 = c->d_pws;
+  a.F2 = (const cx<double>*)c->d_pws + bufN;
+  a.G1 = c->d_gws;
+  a.G2 = (const cx<double>*)c->d_gws + bufN;
+  a.steps = (const double*)c->d_steps;
+  for (int j = 0; j < 3; ++j) {
+    a.mur[j] = j <= c->nu ? c->tprm.mur[j] : 0.0;
+    a.mui[j] = j <= c->nu ? c->tprm.mui[j] : 0.0;
+  }
+  a.kappa = c->cheb_ran ? 2.0 : 1.0;
+  a.coef = mu_mode ? c->d_coef : nullptr;
+  a.rsec_mask = 0;
+  if (c->packed)
+    for (int r = 0; r < N && r < 64; ++r) a.rsec_mask |= (unsigned long long)(c->h_rsec[r] & 1) << r;
+  a.dJdu = d_dJdu;
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_c<NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((k_grad_rr_c<NT, KS, NU>), dim3(grid), dim3(256), lds, st, a);
+  HIPCHK(c, hipGetLastError());
+  return QOC_OK;
+}
+
+template <int NT, int NU>
+int grad_cap_nt(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode) {
+  const int ks = (c->N + 3) / 4;
+  if (ks == 4 * NT - 3) return grad_cap_launch<NT, 4 * NT - 3, NU>(c, d_dJdu, st, k0, nk, mu_mode);
+  if (ks == 4 * NT - 2) return grad_cap_launch<NT, 4 * NT - 2, NU>(c, d_dJdu, st, k0, nk, mu_mode);
+  if (ks == 4 * NT - 1) return grad_cap_launch<NT, 4 * NT - 1, NU>(c, d_dJdu, st, k0, nk, mu_mode);
+  return grad_cap_launch<NT, 4 * NT, NU>(c, d_dJdu, st, k0, nk, mu_mode);
+}
+
+int grad_rr_cap(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode) {
+  if (c->prec != QOC_FP64 || !c->d_pws || !c->d_gws) return fail(c, QOC_ERR_STATE, "captured gradient: no captures");
+  const int NT = (c->N + 15) / 16;
+  if (c->nu == 1) {
+    if (NT == 1) return grad_cap_nt<1, 1>(c, d_dJdu, st, k0, nk, mu_mode);
+    if (NT == 2) return grad_cap_nt<2, 1>(c, d_dJdu, st, k0, nk, mu_mode);
+    return grad_cap_nt<3, 1>(c, d_dJdu, st, k0, nk, mu_mode);
+  }
+  if (NT == 1) return grad_cap_nt<1, 2>(c, d_dJdu, st, k0, nk, mu_mode);
+  if (NT == 2) return grad_cap_nt<2, 2>(c, d_dJdu, st, k0, nk, mu_mode);
+  return grad_cap_nt<3, 2>(c, d_dJdu, st, k0, nk, mu_mode);
+}
+
 template int grad_rr_o3<double>(qoc_ctx*, double*, hipStream_t, int, int, int);
 template int grad_rr_o3<float>(qoc_ctx*, double*, hipStream_t, int, int, int);
 

@@ -80,8 +80,10 @@ hipError_t tchain_mf_dispatch(int N, F&& f) {
   return hipErrorInvalidValue;
 }
 
-template <typename T>
-int tchain_forward(qoc_ctx* c) {
+bool tchain_cap_ok(const qoc_ctx* c);
+
+// the step records of every (seed, slice): β_k, (P, s), e^{μ_k} and the Chebyshev coefficients
+int tchain_prep(qoc_ctx* c) {
   const long long units = (long long)c->B * c->Nt;
   const bool cheb = c->cheb && tchain_mf(c);
   if (cheb && !c->d_tcoef) {
@@ -100,7 +102,31 @@ int tchain_forward(qoc_ctx* c) {
   mark_end(c, mk);
   HIPCHK(c, hipGetLastError());
   c->cheb_ran = cheb;
-  const TChainArgs g = tchain_args(c);
+  return QOC_OK;
+}
+
+template <typename T>
+int tchain_forward_chain(qoc_ctx* c);
+
+template <typename T>
+int tchain_forward(qoc_ctx* c) {
+  const int r = tchain_prep(c);
+  return r ? r : tchain_forward_chain<T>(c);
+}
+
+// the forward chain over the step records tchain_prep wrote (with its captures when the shape takes them)
+template <typename T>
+int tchain_forward_chain(qoc_ctx* c) {
+  const bool cheb = c->cheb_ran;
+  int mk;
+  TChainArgs g = tchain_args(c);
+  c->fwd_captured = false;
+  if (tchain_cap_ok(c) && ensure_pws(c) == QOC_OK) {  // P1 / P2 of the gradient as by-products
+    const size_t bufN = (size_t)c->N * ((size_t)c->B * (c->Nt + 1) * c->m);
+    g.cap1 = c->d_pws;
+    g.cap2 = (cx<double>*)c->d_pws + bufN;
+    c->fwd_captured = true;
+  }
   if (tchain_mf(c)) {
     const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
     const int threads = 64 * tchain_mf_waves(c->N, c->m);
@@ -139,17 +165,24 @@ int tchain_forward(qoc_ctx* c) {
 }
 
 template <typename T>
-int tchain_backward(qoc_ctx* c, int k_lo, int k_hi) {
+int tchain_backward(qoc_ctx* c, int k_lo, int k_hi, hipStream_t st, int flags) {
   TChainArgs g = tchain_args(c);
+  if (!st) st = c->stream;
   if (tchain_mf(c)) {
     if (k_hi >= 0) {  // a range of slices (tchain_backward_overlapped)
       g.k_lo = k_lo;
       g.k_hi = k_hi;
       g.prio = c->bwd_prio & 1;
     }
+    if (flags & TB_CAPTURE) {  // Q1 / Q2 of the gradient as by-products (d_gws: the W0 / W1 buffers)
+      const size_t bufN = (size_t)c->N * ((size_t)c->B * (c->Nt + 1) * c->m);
+      g.cap1 = c->d_gws;
+      g.cap2 = (cx<double>*)c->d_gws + bufN;
+    }
+    g.mu_mode = (flags & TB_MU) ? 1 : 0;
     const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
     const int threads = 64 * tchain_mf_waves(c->N, c->m);
-    int mk = mark_begin(c, 2);
+    int mk = mark_begin(c, 2, st);
     hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
       // the (P, s, coefficients) of the forward pass are reused: the same polynomial as the states'
@@ -159,13 +192,14 @@ int tchain_backward(qoc_ctx* c, int k_lo, int k_hi) {
                               : (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 1024> : k_tchain_mf_bwd<KQ, false, 1024>);
       hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (r != hipSuccess) return r;
-      hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);
+      hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, st, g);
       return hipGetLastError();
     });
-    mark_end(c, mk);
+    mark_end(c, mk, st);
     if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_mf_bwd launch: %s", hipGetErrorString(e));
     return QOC_OK;
   }
+  if (flags) return fail(c, QOC_ERR_UNSUPPORTED, "captured / μ-mode backward needs the MFMA chains");
   const size_t lds = tchain_lds(c);
   int mk = mark_begin(c, 2);
   hipError_t e = tchain_dispatch<T>(c->N, c->m, [&](auto S_, auto JT_, auto CB_, auto NP_) {
@@ -272,11 +306,137 @@ hipError_t launch_pade_units(qoc_ctx* c, long long units) {
   return hipGetLastError();
 }
 
+// The register-resident MFMA chains (MAXT = 256) can write their first two products per slice; with the fused
+// order-3 gradient they then replace its generator products (k_grad_rr_c).
+bool tchain_cap_ok(const qoc_ctx* c) {
+  return c->cap_ok && tchain_mf(c) && tchain_mf_maxt(c->N, c->m, c->nu) == 256 && c->grad_rr && c->nu <= 2;
+}
+
+// d_pws: the forward captures (two state-shaped buffers), grown on first use; QOC_ERR_HIP if it cannot be had
+int ensure_pws(qoc_ctx* c) {
+  const size_t pws = (size_t)2 * c->N * c->B * (c->Nt + 1) * c->m * c->esz;
+  if (c->d_pws && c->pws_bytes >= pws) return QOC_OK;
+  if (c->d_pws) {
+    if (c->stream2) HIPCHK(c, hipStreamSynchronize(c->stream2));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(c->d_pws));
+    c->dev_bytes -= c->pws_bytes;
+  }
+  c->d_pws = nullptr;
+  c->pws_bytes = 0;
+  if (hipMalloc(&c->d_pws, pws) != hipSuccess) {
+    (void)hipGetLastError();
+    c->d_pws = nullptr;
+    return fail(c, QOC_ERR_HIP, "capture buffers (%zu bytes) not available", pws);
+  }
+  c->pws_bytes = pws;
+  c->dev_bytes += pws;
+  return QOC_OK;
+}
+
+int ensure_stream2(qoc_ctx* c, int nev) {
+  if (!c->stream2) {
+    int lo = 0, hi = 0;
+    HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(c, hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, (c->bwd_prio & 2) ? lo : 0));
+  }
+  while ((int)c->sync_ev.size() < nev) {
+    hipEvent_t e;
+    HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->sync_ev.push_back(e);
+  }
+  return QOC_OK;
+}
+
+// grape_sensitivity after a captured forward: the backward chain writes its captures, range by range (as
+// tchain_backward_overlapped), and each finished range's contraction (k_grad_rr_c) runs on the second stream.
+template <typename T>
+int tchain_backward_captured(qoc_ctx* c, double* d_dJdu) {
+  const int Nt = c->Nt;
+  const int S = c->bwd_chunks > 1 && Nt >= 64 ? std::min(c->bwd_chunks, std::max(1, Nt / 32)) : 1;
+  int r = ensure_stream2(c, S + 2);
+  if (r) return r;
+  std::vector<int> kb(S + 1);
+  const double last = std::max(0.05, std::min(1.0, c->bwd_last_frac)), w = Nt / (S - 1 + last);
+  for (int i = 0; i <= S; ++i) kb[i] = std::max(0, Nt - (int)std::lround(i * w));
+  kb[S] = 0;
+  kb[0] = Nt;
+  HIPCHK(c, hipEventRecord(c->sync_ev[S], c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[S], 0));
+  auto join = [&](int rc) {
+    const hipError_t e1 = hipEventRecord(c->sync_ev[S + 1], c->stream2);
+    const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(c->stream, c->sync_ev[S + 1], 0) : e1;
+    if (rc == QOC_OK && e2 != hipSuccess) return fail(c, QOC_ERR_HIP, "stream join: %s", hipGetErrorString(e2));
+    return rc;
+  };
+  for (int i = 0; i < S; ++i) {
+    if (kb[i + 1] >= kb[i]) continue;
+    r = tchain_backward<T>(c, kb[i + 1], kb[i], c->stream, TB_CAPTURE);
+    if (r) return join(r);
+    hipError_t e = hipEventRecord(c->sync_ev[i], c->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream2, c->sync_ev[i], 0);
+    if (e != hipSuccess) return join(fail(c, QOC_ERR_HIP, "range event: %s", hipGetErrorString(e)));
+    const int mk = mark_begin(c, 3, c->stream2);
+    r = grad_rr_cap(c, d_dJdu, c->stream2, kb[i + 1], kb[i] - kb[i + 1], false);
+    mark_end(c, mk, c->stream2);
+    if (r) return join(r);
+  }
+  c->last_eval_mode = 1;
+  return join(QOC_OK);
+}
+
+// One eval (propagate + order-3 sensitivity) with a built-in cost and no penalty / co-state source: for those costs
+// λ_{Nt} = coef ⊙ X_target (src/penalty_fcns.jl:19-22, 35-40), and every later λ_k = U_k^H λ_{k+1} is linear, so
+// λ_k = coef ⊙ μ_k with μ_k = U_k^H .. U_{Nt-1}^H X_target, which needs only the step records.  The μ recurrence
+// (k_tchain_mf_bwd in μ mode) therefore runs on the second stream beside the forward chain, whose coefficients are
+// not known until its end; the contraction (k_grad_rr_c) then applies coef on load.  d_L holds μ afterwards.
+bool tchain_concurrent_ok(const qoc_ctx* c, int order) {
+  return c->concurrent && order == 3 && tchain_cap_ok(c) && c->chain_mode == 1 && c->prop_method == QOC_PROP_EXPM &&
+         !c->big && (c->cost_kind == QOC_COST_TRACE || c->cost_kind == QOC_COST_ZCAL) && c->mu == 0.0 && !c->src_on;
+}
+
+template <typename T>
+int tchain_eval_concurrent(qoc_ctx* c, double* d_dJdu) {
+  int r = ensure_stream2(c, 4);
+  if (r) return r;
+  if ((r = ensure_pws(c))) return r;
+  if (!c->d_coef_mu) {
+    HIPCHK(c, hipMalloc((void**)&c->d_coef_mu, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
+    c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
+  }
+  // the step records first (both chains read them)
+  if ((r = tchain_prep(c))) return r;
+  HIPCHK(c, hipEventRecord(c->sync_ev[0], c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[0], 0));
+  // μ recurrence beside the forward chain
+  r = tchain_backward<T>(c, 0, c->Nt, c->stream2, TB_CAPTURE | TB_MU);
+  if (r == QOC_OK) r = tchain_forward_chain<T>(c);
+  if (r == QOC_OK && !c->fwd_captured) r = fail(c, QOC_ERR_STATE, "concurrent eval: forward captures missing");
+  const hipError_t e1 = hipEventRecord(c->sync_ev[1], c->stream2);
+  const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(c->stream, c->sync_ev[1], 0) : e1;
+  if (r) return r;
+  if (e2 != hipSuccess) return fail(c, QOC_ERR_HIP, "stream join: %s", hipGetErrorString(e2));
+  const int mk = mark_begin(c, 3);
+  r = grad_rr_cap(c, d_dJdu, c->stream, 0, c->Nt, true);
+  mark_end(c, mk);
+  if (r) return r;
+  // the coefficients that turn μ into λ, kept for qoc_get_costates (a later forward rewrites d_coef)
+  HIPCHK(c, hipMemcpyAsync(c->d_coef_mu, c->d_coef, (size_t)c->B * 2 * c->m * sizeof(cx<double>),
+                           hipMemcpyDeviceToDevice, c->stream));
+  c->L_is_mu = true;
+  c->last_eval_mode = 2;
+  return QOC_OK;
+}
+
 template int tchain_forward<double>(qoc_ctx*);
 template int tchain_forward<float>(qoc_ctx*);
-template int tchain_backward<double>(qoc_ctx*, int, int);
-template int tchain_backward<float>(qoc_ctx*, int, int);
+template int tchain_backward<double>(qoc_ctx*, int, int, hipStream_t, int);
+template int tchain_backward<float>(qoc_ctx*, int, int, hipStream_t, int);
 template int tchain_backward_overlapped<double>(qoc_ctx*, double*);
 template int tchain_backward_overlapped<float>(qoc_ctx*, double*);
+template int tchain_backward_captured<double>(qoc_ctx*, double*);
+template int tchain_backward_captured<float>(qoc_ctx*, double*);
+template int tchain_eval_concurrent<double>(qoc_ctx*, double*);
+template int tchain_eval_concurrent<float>(qoc_ctx*, double*);
 
 }  // namespace qoc_host

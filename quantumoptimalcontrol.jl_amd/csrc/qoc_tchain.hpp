@@ -65,15 +65,20 @@ constexpr int TCHAIN_NUMAX = 8;  // controls per slice the Taylor-action chains 
 // Per-step inputs of the chains (TStep + u_k), fetched one step ahead through VECTOR loads: scalar loads would
 // miss the scalar cache on every new step (an L2 / HBM round trip on the critical path), and an outstanding
 // scalar load shares lgkmcnt with the LDS traffic of the Taylor terms, forcing lgkmcnt(0) drains there.
-struct TPre {
+// NUR: control registers (TCHAIN_NUMAX; 2 in the register-resident MFMA chains, which take nu <= 2 — six fewer
+// live doubles per copy in a kernel that has to stay within 256 VGPRs).
+template <int NUR>
+struct TPreN {
   double pr, pi;
   int P, s;
   double scale;
   double cl;  // Chebyshev: c_t of this lane's t = lane (v_readlane'd by the term loop)
-  double u[TCHAIN_NUMAX];
+  double u[NUR];
 };
-__device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const double* __restrict__ uk, int nu, TPre& d,
-                                          const double* __restrict__ ce = nullptr) {
+using TPre = TPreN<TCHAIN_NUMAX>;
+template <int NUR>
+__device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const double* __restrict__ uk, int nu,
+                                          TPreN<NUR>& d, const double* __restrict__ ce = nullptr) {
   int z;
   asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // per-lane (VGPR) address: global_load, not s_load
   const double4 v = *reinterpret_cast<const double4*>(reinterpret_cast<const double*>(st) + z);
@@ -85,7 +90,7 @@ __device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const do
   d.scale = v.w;
   d.cl = ce ? ce[threadIdx.x & 63] : 0.0;
 #pragma unroll
-  for (int j = 0; j < TCHAIN_NUMAX; ++j) {  // clamped, unconditional loads: no branches around them
+  for (int j = 0; j < NUR; ++j) {  // clamped, unconditional loads: no branches around them
     const double v = uk[min(j, nu - 1) + z];
     d.u[j] = j < nu ? v : 0.0;
   }
@@ -97,6 +102,8 @@ struct TChainParams {
   double mur[9], mui[9];      // shifts μ_j
   double theta[TCHAIN_PMAX + 1];  // θ_P: largest β whose degree-P Taylor tail is within tolerance (θ_0 unused)
   double theta_max;           // substep bound (β / s <= theta_max)
+  int pmin;                   // fewest terms per substep (2: the chains' first two products are the gradient's
+                              // A_k x and A_k^2 x, captured by the register-resident MFMA chains)
 };
 
 // (P, s, e^{μ}) per unit, plus Σ P s (executed Taylor terms per direction) for the roofline accounting.
@@ -116,7 +123,7 @@ static __global__ void k_tchain_prep(int nu, long long units, const double* __re
       s = (int)ceil(beta / prm.theta_max);
       beta /= s;
     }
-    int P = 1;
+    int P = prm.pmin > 1 ? prm.pmin : 1;
     while (P < TCHAIN_PMAX && prm.theta[P] < beta) ++P;
     const double er = exp(mr);
     steps[e] = TStep{er * cos(mi), er * sin(mi), P, s, 1.0 / s};
@@ -243,7 +250,7 @@ __device__ double bessel_series_k(double h, int k) {
   return sum;
 }
 
-__device__ int cheb_series(double rho, double tol, double* __restrict__ ce) {
+__device__ int cheb_series(double rho, double tol, double* __restrict__ ce, int pmin) {
   constexpr int K = TCHEB_PMAX + 1;
   const double h = 0.5 * rho;
   int kz = K + 1;  // J_k = 0 for k >= kz (bessel_j stops once (ρ/2)^k / k! < 1e-40)
@@ -264,6 +271,7 @@ __device__ int cheb_series(double rho, double tol, double* __restrict__ ce) {
       break;
     }
   }
+  if (P < pmin) P = pmin;  // more terms than the tail needs: the extra coefficients are just as exact
   for (int k = 0; k <= P; ++k) {
     const double v = bessel_series_k(h, k);
     ce[k] = k ? 2.0 * v : v;
@@ -291,9 +299,10 @@ static __global__ void k_tchain_prep_cheb(int nu, long long units, const double*
     double* ce = coef + (size_t)e * TCHEB_STRIDE;
     int P = 0;
     if (rho <= 2.0) {
-      P = cheb_series(rho, tol, ce);
+      P = cheb_series(rho, tol, ce, prm.pmin);
     } else {
-      P = cheb_miller(rho, tol, ce);
+      P = cheb_miller(rho, tol, ce);  // every coefficient 0..TCHEB_PMAX written
+      if (P < prm.pmin) P = prm.pmin;
     }
     const double er = exp(mr);
     steps[e] = TStep{er * cos(mi), er * sin(mi), P, s, 2.0 / beta};
@@ -324,6 +333,14 @@ struct TChainArgs {
   const double* tcoef;     // B x Nt x TCHEB_STRIDE Chebyshev coefficients (Chebyshev variant)
   int k_lo, k_hi;          // backward MFMA chain: slices k_hi-1 .. k_lo (k_hi < Nt: λ_{k_hi} read from L)
   int prio;                // raise the chain waves' issue priority (gradient waves share the SIMDs)
+  // Register-resident MFMA chains: the first two products of every slice, D1 = Â v and D2 = Â y_1 (v = x_k forward,
+  // λ_{k+1} backward, Â the scaled shifted generator), written in the state layout at slice k (nullptr: not kept).
+  // They are the order-3 gradient's A_k x_k, A_k^2 x_k and A_k^H λ, (A_k^H)^2 λ up to the exact shift / scale
+  // (k_grad_rr_c), so the gradient runs no generator products of its own except the contractions.
+  void* cap1;
+  void* cap2;
+  int mu_mode;             // backward: μ_k = U_k^H .. U_{Nt-1}^H X_target (λ_k = coef ⊙ μ_k for the built-in costs),
+                           // started from X_target alone: it needs no forward result and can run beside it
 };
 
 // Thread layout of the Taylor-action chains.  Waves split the rows into G blocks of R = 64 / S rows and the
@@ -721,10 +738,14 @@ __host__ __device__ inline int tchain_mf_maxt(int N, int m, int nu) {
   const int w = tchain_mf_waves(N, m);
   return w <= 4 && nu <= 2 ? 256 : w <= 8 ? 512 : 1024;
 }
+// LDS of the MFMA chains: the generators (the register-resident variant, MAXT = 256, keeps only Ã_2 there and reads
+// its register operands from HBM once), 2 x (y, y') state buffers, 16 reduction doubles + 48 for 1/t + 64 per wave
+// (coefficients).  So two chain workgroups fit one CU's 160 KB (forward and backward side by side).
 __host__ inline size_t tchain_mf_lds(int N, int m, int nu) {
   const int KQ = tchain_mf_kq(N), CP = (m + 1) / 2;
-  // generators, 2 x (y, y') state buffers, then 16 reduction doubles + 48 for 1/t + 64 per wave (coefficients)
-  return (size_t)(nu + 1) * N * N * 16 + (size_t)2 * 2 * CP * 4 * KQ * 4 * 8 + (64 + 64 * tchain_mf_waves(N, m)) * 8;
+  // register-resident variant: Ã_0, Ã_1 in registers, Ã_2 (nu = 2) in LDS
+  const size_t gen = (size_t)(tchain_mf_maxt(N, m, nu) == 256 ? (nu >= 2 ? 1 : 0) : nu + 1) * N * N * 16;
+  return gen + (size_t)2 * 2 * CP * 4 * KQ * 4 * 8 + (64 + 64 * tchain_mf_waves(N, m)) * 8;
 }
 
 template <int KQ>
@@ -755,7 +776,8 @@ struct TChainMF {
     return yb + (size_t)((buf * 2 + prime) * CP) * RP * 4;
   }
   // a = Ã_k (or its conjugate transpose, whichever the LDS generators hold) at A-operand positions
-  __device__ __forceinline__ void form(int N, int nu, const cx<double>* __restrict__ gen, const double (&uk)[TCHAIN_NUMAX],
+  template <int NUR>
+  __device__ __forceinline__ void form(int N, int nu, const cx<double>* __restrict__ gen, const double (&uk)[NUR],
                                        double scale, double (&ar)[KQ], double (&ai)[KQ]) const {
     const int NN = N * N, rc = min(rowA, N - 1);
 #pragma unroll
@@ -768,7 +790,7 @@ struct TChainMF {
     // register pair reused per element the compiler waited for every read in turn (lgkmcnt(0) after each
     // ds_read_b128, ~KQ LDS latencies per generator and slice)
 #pragma unroll
-    for (int j = 0; j < TCHAIN_NUMAX; ++j) {
+    for (int j = 0; j < NUR; ++j) {
       if (j >= nu) break;
       const double uj = uk[j];
       const cx<double>* Gj = gen + (size_t)(j + 1) * NN;
@@ -789,29 +811,48 @@ struct TChainMF {
       ai[q] = ok ? ai[q] * scale : 0.0;
     }
   }
-  // Register-resident generators (nu <= 2, 256-thread launch bound: one wave per SIMD, 512 VGPRs): this lane's
-  // A-operand elements of Ã_0..Ã_nu, read from LDS once; form_regs then builds a slice's rows with no LDS traffic.
-  __device__ __forceinline__ void load_gen(int N, int nu, const cx<double>* __restrict__ gen, double (&gr)[3][KQ],
-                                           double (&gi)[3][KQ]) const {
+  // Register-resident generators (nu <= 2, 256-thread launch bound): this lane's A-operand elements of Ã_0 and Ã_1
+  // (HERM: of Ã_j^H, the backward chain's), read from HBM once (At: column-major Ã_j, L2-resident); Ã_2 stays in
+  // LDS (a third register copy would take the kernel past the 256 VGPRs that let two chain waves share a SIMD).
+  // form_regs then builds a slice's rows with KQ LDS reads at most.
+  template <bool HERM>
+  __device__ __forceinline__ void load_gen(int N, int nu, const cx<double>* __restrict__ At, double (&gr)[2][KQ],
+                                           double (&gi)[2][KQ]) const {
     const int NN = N * N, rc = min(rowA, N - 1);
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < KQ; ++q) {
         const bool ok = j <= nu && rowA < N && 4 * q + kl < N;
-        const cx<double> v = gen[(size_t)min(j, nu) * NN + rc + N * min(4 * q + kl, N - 1)];
+        const int cc = min(4 * q + kl, N - 1);
+        const cx<double> v = At[(size_t)min(j, nu) * NN + (HERM ? cc + N * rc : rc + N * cc)];
         gr[j][q] = ok ? v.r : 0.0;
-        gi[j][q] = ok ? v.i : 0.0;
+        gi[j][q] = ok ? (HERM ? -v.i : v.i) : 0.0;
       }
   }
-  __device__ __forceinline__ void form_regs(const double (&gr)[3][KQ], const double (&gi)[3][KQ],
-                                            const double (&uk)[TCHAIN_NUMAX], double scale, double (&ar)[KQ],
-                                            double (&ai)[KQ]) const {
+  // g2: LDS image of Ã_2 (or Ã_2^H), column-major, used when nu == 2
+  template <int NUR>
+  __device__ __forceinline__ void form_regs(int N, int nu, const double (&gr)[2][KQ], const double (&gi)[2][KQ],
+                                            const cx<double>* __restrict__ g2, const double (&uk)[NUR], double scale,
+                                            double (&ar)[KQ], double (&ai)[KQ]) const {
+    static_assert(NUR >= 2, "form_regs reads u_1, u_2");
     const double u1 = uk[0] * scale, u2 = uk[1] * scale;  // uk[j >= nu] = 0
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
-      ar[q] = fma(u2, gr[2][q], fma(u1, gr[1][q], scale * gr[0][q]));
-      ai[q] = fma(u2, gi[2][q], fma(u1, gi[1][q], scale * gi[0][q]));
+      ar[q] = fma(u1, gr[1][q], scale * gr[0][q]);
+      ai[q] = fma(u1, gi[1][q], scale * gi[0][q]);
+    }
+    if (nu >= 2) {
+      const int rc = min(rowA, N - 1);
+      cx<double> v[KQ];
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) v[q] = g2[rc + N * min(4 * q + kl, N - 1)];
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        const bool ok = rowA < N && 4 * q + kl < N;
+        ar[q] = fma(ok ? u2 : 0.0, v[q].r, ar[q]);
+        ai[q] = fma(ok ? u2 : 0.0, v[q].i, ai[q]);
+      }
     }
   }
   // D = A y for this wave's rows and column pair (y from buffer `buf`)
@@ -887,10 +928,12 @@ struct TChainMF {
 
   // One slice (see TChain::step); acc = this lane's D element of the state.  CHEB: the Chebyshev recurrence
   // with this lane's coefficient register cl (lane t holds c_t); else Taylor (1/t from the LDS table invt).
-  template <bool CHEB>
+  // CAP: the first substep's first two products D1 = Â y_0 and D2 = Â y_1 go to cd1, cd2 (P >= 2: prm.pmin).
+  template <bool CHEB, bool CAP = false>
   __device__ __forceinline__ void step(int N, const double (&ar)[KQ], const double (&ai)[KQ], double* yb,
                                        const double* __restrict__ invt, int& cur, int P, int s, cx<double> ph,
-                                       double& acc, double cl, double* __restrict__ cw) const {
+                                       double& acc, double cl, double* __restrict__ cw, double& cd1,
+                                       double& cd2) const {
     if constexpr (CHEB) {  // this step's coefficients -> the wave's own LDS slot (in-order LDS: no barrier)
       cw[threadIdx.x & 63] = cl;
       __builtin_amdgcn_wave_barrier();
@@ -906,6 +949,12 @@ struct TChainMF {
         const double ct = CHEB ? cw[t] : invt[t];
         __builtin_amdgcn_sched_barrier(0);
         const double D = matvec(ar, ai, ybuf(yb, CP, cur, 0), ybuf(yb, CP, cur, 1));
+        if constexpr (CAP) {
+          if (sub == 0 && t <= 2) {
+            if (t == 1) cd1 = D;
+            else cd2 = D;
+          }
+        }
         double z;
         if constexpr (CHEB) {
           z = t == 1 ? 0.5 * D : D + ym2;
@@ -940,15 +989,20 @@ struct TChainMF {
   }
 };
 
+// Register-resident variant (MAXT = 256, nu <= 2): the generators live in registers, not in LDS, and the first two
+// products of every slice are written to g.cap1 / g.cap2 when those are set (TChainArgs); the writes of slice k
+// are issued at the start of slice k + 1, next to the state's, ahead of the step-data prefetch.
 template <int KQ, bool CHEB, int MAXT>
 __global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
   using C = TChainMF<KQ>;
   constexpr int RP = C::RP;
+  constexpr bool REGS = MAXT == 256;  // generators in registers (the dispatch picks MAXT = 256 only for nu <= 2)
+  constexpr int NUR = REGS ? 2 : TCHAIN_NUMAX;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
   const int NN = N * N, Nm = N * m, CP = (m + 1) / 2;
-  cx<double>* gen = reinterpret_cast<cx<double>*>(smem);
-  double* yb = reinterpret_cast<double*>(gen + (size_t)(nu + 1) * NN);
+  cx<double>* gen = reinterpret_cast<cx<double>*>(smem);  // REGS: Ã_2 only
+  double* yb = reinterpret_cast<double*>(gen + (size_t)(REGS ? (nu >= 2 ? 1 : 0) : nu + 1) * NN);
   double* red = yb + (size_t)2 * 2 * CP * RP * 4;
   double* invt = red + 16;
   double* cw = invt + 48 + 64 * (tid >> 6);  // per-wave Chebyshev coefficient slot
@@ -960,7 +1014,11 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
   const TStep* stb = g.steps + (size_t)b * Nt;
   C rg;
   rg.setup(N, m);
-  for (int e = tid; e < (nu + 1) * NN; e += nthr) gen[e] = At[e];
+  if constexpr (!REGS) {
+    for (int e = tid; e < (nu + 1) * NN; e += nthr) gen[e] = At[e];
+  } else if (nu >= 2) {
+    for (int e = tid; e < NN; e += nthr) gen[e] = At[2 * (size_t)NN + e];
+  }
   const int YB = 2 * 2 * CP * RP * 4;
   for (int e = tid; e < YB; e += nthr) yb[e] = 0.0;
   __syncthreads();
@@ -974,39 +1032,52 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
   }
   const bool pen_m = rg.actD && g.pmask && g.pmask[rg.rowD + N * rg.colD];
   double pen = 0.0;
+  const size_t own = (size_t)rg.rowD + (size_t)N * rg.colD;
   auto store = [&](double v, int k_) __attribute__((always_inline)) {
     if (rg.actD) {
-      reinterpret_cast<double*>(Xb + (size_t)k_ * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = v;
+      reinterpret_cast<double*>(Xb + (size_t)k_ * Nm + own)[rg.n & 1] = v;
       if (pen_m) pen += v * v;
     }
   };
+  const bool cap = REGS && g.cap1 != nullptr;
+  double* c1b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm + own) : nullptr;
+  double* c2b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm + own) : nullptr;
+  auto cap_store = [&](double d1, double d2, int k_) __attribute__((always_inline)) {
+    if (cap && rg.actD) {
+      c1b[2 * (size_t)k_ * Nm + (rg.n & 1)] = d1;
+      c2b[2 * (size_t)k_ * Nm + (rg.n & 1)] = d2;
+    }
+  };
   __syncthreads();
-  constexpr bool REGS = MAXT == 256;  // generators in registers (the dispatch picks MAXT = 256 only for nu <= 2)
-  double gr[3][KQ], gi[3][KQ];
-  if constexpr (REGS) rg.load_gen(N, nu, gen, gr, gi);
+  double gr[2][KQ], gi[2][KQ];
+  if constexpr (REGS) rg.template load_gen<false>(N, nu, At, gr, gi);
   double acc = rg.actD ? yb[(rg.cp * RP + rg.rowD) * 4 + rg.n] : 0.0;
   store(acc, 0);
 #ifdef QOC_PROBE
   const unsigned long long c0_ = __builtin_amdgcn_s_memtime(), r0_ = __builtin_amdgcn_s_memrealtime();
 #endif
   int cur = 0;
+  double cd1 = 0.0, cd2 = 0.0;
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
-  TPre nx;
+  TPreN<NUR> nx;
   tpre_load(stb, ub, nu, nx, ceb);
   for (int k = 0; k < Nt; ++k) {
     TC_T(s0);
     // x_k (the previous slice's result) goes to HBM here, ahead of this slice's prefetch: the wait for the
     // prefetch at the end of the slice (vmcnt, in issue order) then never waits for a just-issued store
-    if (k > 0) store(acc, k);
-    const TPre st = nx;
+    if (k > 0) {
+      store(acc, k);
+      cap_store(cd1, cd2, k - 1);
+    }
+    const TPreN<NUR> st = nx;
     const int kn = min(k + 1, Nt - 1);
     tpre_load(stb + kn, ub + (size_t)kn * nu, nu, nx, CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     double ar[KQ], ai[KQ];
-    if constexpr (REGS) rg.form_regs(gr, gi, st.u, st.scale, ar, ai);
+    if constexpr (REGS) rg.form_regs(N, nu, gr, gi, gen, st.u, st.scale, ar, ai);
     else rg.form(N, nu, gen, st.u, st.scale, ar, ai);
     TC_T(s1);
-    rg.template step<CHEB>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, st.pi}, acc, st.cl, cw);
+    rg.template step<CHEB, REGS>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, st.pi}, acc, st.cl, cw, cd1, cd2);
     TC_T(s2);
     TC_T(s3);
     TC_ADD(10, s1 - s0);
@@ -1015,6 +1086,7 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
     TC_ADD(13, 1);
   }
   store(acc, Nt);
+  cap_store(cd1, cd2, Nt - 1);
   __syncthreads();
 #ifdef QOC_PROBE
   if (blockIdx.x == 7 && threadIdx.x == 0) {
@@ -1035,11 +1107,13 @@ template <int KQ, bool CHEB, int MAXT>
 __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
   using C = TChainMF<KQ>;
   constexpr int RP = C::RP;
+  constexpr bool REGS = MAXT == 256;  // see k_tchain_mf_fwd
+  constexpr int NUR = REGS ? 2 : TCHAIN_NUMAX;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
   const int NN = N * N, Nm = N * m, CP = (m + 1) / 2;
-  cx<double>* gen = reinterpret_cast<cx<double>*>(smem);
-  double* yb = reinterpret_cast<double*>(gen + (size_t)(nu + 1) * NN);
+  cx<double>* gen = reinterpret_cast<cx<double>*>(smem);  // REGS: Ã_2^H only
+  double* yb = reinterpret_cast<double*>(gen + (size_t)(REGS ? (nu >= 2 ? 1 : 0) : nu + 1) * NN);
   double* invt = yb + (size_t)2 * 2 * CP * RP * 4 + 16;
   double* cw = invt + 48 + 64 * (tid >> 6);  // per-wave Chebyshev coefficient slot
   for (int e = tid; e <= TCHAIN_PMAX; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
@@ -1050,26 +1124,30 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
   const double* ub = g.u + (size_t)b * Nt * nu;
   const TStep* stb = g.steps + (size_t)b * Nt;
   const double tmu = 2.0 * g.mu;
-  const cx<double>* srcb = g.src ? (const cx<double>*)g.src + (size_t)b * (Nt + 1) * Nm : nullptr;
+  // μ mode: no penalty and no co-state source (the host selects it only without them)
+  const unsigned char* pmask = g.mu_mode ? nullptr : g.pmask;
+  const cx<double>* srcb = (g.src && !g.mu_mode) ? (const cx<double>*)g.src + (size_t)b * (Nt + 1) * Nm : nullptr;
   if (g.prio) __builtin_amdgcn_s_setprio(3);
   C rg;
   rg.setup(N, m);
-  for (int e = tid; e < (nu + 1) * NN; e += nthr) {
-    const int j = e / NN, rc = e - j * NN, r = rc % N, c = rc / N;
+  for (int e = tid; e < (REGS ? (nu >= 2 ? NN : 0) : (nu + 1) * NN); e += nthr) {
+    const int j = (REGS ? 2 : 0) + e / NN, rc = e % NN, r = rc % N, c = rc / N;
     const cx<double> v = At[(size_t)j * NN + c + N * r];  // (Ã_j^H)[r, c] = conj(Ã_j[c, r])
     gen[e] = cx<double>{v.r, -v.i};
   }
   const int YB = 2 * 2 * CP * RP * 4;
   for (int e = tid; e < YB; e += nthr) yb[e] = 0.0;
   __syncthreads();
-  // λ_{Nt} = dJfinal/dx(x_N) (+ dL/dx(x_N)) -> buffer 0 and HBM; a later range of slices starts from the
-  // λ_{k_hi} the previous range stored
+  // λ_{Nt} = dJfinal/dx(x_N) (+ dL/dx(x_N)) -> buffer 0 and HBM (μ mode: μ_{Nt} = X_target); a later range of
+  // slices starts from the λ_{k_hi} the previous range stored
   const int k_lo = g.k_lo, k_hi = g.k_hi;
   for (int o = tid; o < Nm; o += nthr) {
     const int r = o % N, col = o / N;
     cx<double> v;
     if (k_hi < Nt) {
       v = Lb[(size_t)k_hi * Nm + o];
+    } else if (g.mu_mode) {
+      v = Xt[o];
     } else if (g.cost_kind == COST_EXTERNAL) {
       v = Lb[(size_t)Nt * Nm + o];
     } else {
@@ -1077,7 +1155,7 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
       v = cx<double>{cf.r * t.r - cf.i * t.i, cf.r * t.i + cf.i * t.r};
     }
     if (k_hi == Nt) {
-      if (g.pmask && g.pmask[o]) {
+      if (pmask && pmask[o]) {
         const cx<double> xv = Xb[(size_t)Nt * Nm + o];
         v.r += tmu * xv.r;
         v.i += tmu * xv.i;
@@ -1094,38 +1172,51 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
     yb[CP * RP * 4 + q + 1] = v.r;
     yb[CP * RP * 4 + q] = -v.i;
   }
-  const bool pen_m = rg.actD && g.pmask && g.pmask[rg.rowD + N * rg.colD];
+  const bool pen_m = rg.actD && pmask && pmask[rg.rowD + N * rg.colD];
+  const size_t own = (size_t)rg.rowD + (size_t)N * rg.colD;
+  const bool cap = REGS && g.cap1 != nullptr;
+  double* c1b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm + own) : nullptr;
+  double* c2b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm + own) : nullptr;
+  auto cap_store = [&](double d1, double d2, int k_) __attribute__((always_inline)) {
+    if (cap && rg.actD) {
+      c1b[2 * (size_t)k_ * Nm + (rg.n & 1)] = d1;
+      c2b[2 * (size_t)k_ * Nm + (rg.n & 1)] = d2;
+    }
+  };
   __syncthreads();
-  constexpr bool REGS = MAXT == 256;  // see k_tchain_mf_fwd
-  double gr[3][KQ], gi[3][KQ];
-  if constexpr (REGS) rg.load_gen(N, nu, gen, gr, gi);
+  double gr[2][KQ], gi[2][KQ];
+  if constexpr (REGS) rg.template load_gen<true>(N, nu, At, gr, gi);
   int cur = 0;
-  double acc = 0.0;
+  double acc = 0.0, cd1 = 0.0, cd2 = 0.0;
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
-  TPre nx;
+  TPreN<NUR> nx;
   tpre_load(stb + k_hi - 1, ub + (size_t)(k_hi - 1) * nu, nu, nx,
             CHEB ? ceb + (size_t)(k_hi - 1) * TCHEB_STRIDE : nullptr);
   for (int k = k_hi - 1; k >= k_lo; --k) {
     // λ_{k+1} (the previous slice's result) to HBM ahead of this slice's loads (see k_tchain_mf_fwd)
-    if (k < k_hi - 1 && rg.actD) reinterpret_cast<double*>(Lb + (size_t)(k + 1) * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = acc;
-    const TPre st = nx;
+    if (k < k_hi - 1) {
+      if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)(k + 1) * Nm + own)[rg.n & 1] = acc;
+      cap_store(cd1, cd2, k + 1);
+    }
+    const TPreN<NUR> st = nx;
     const int kp = max(k - 1, 0);
     tpre_load(stb + kp, ub + (size_t)kp * nu, nu, nx, CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
-    const size_t ok_ = (size_t)k * Nm + rg.rowD + N * rg.colD;
+    const size_t ok_ = (size_t)k * Nm + own;
     double xk = pen_m ? tmu * reinterpret_cast<const double*>(Xb + ok_)[rg.n & 1] : 0.0;
     if (srcb && rg.actD) xk += reinterpret_cast<const double*>(srcb + ok_)[rg.n & 1];
     double ar[KQ], ai[KQ];
-    if constexpr (REGS) rg.form_regs(gr, gi, st.u, st.scale, ar, ai);
+    if constexpr (REGS) rg.form_regs(N, nu, gr, gi, gen, st.u, st.scale, ar, ai);
     else rg.form(N, nu, gen, st.u, st.scale, ar, ai);
-    rg.template step<CHEB>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, -st.pi}, acc, st.cl, cw);
+    rg.template step<CHEB, REGS>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, -st.pi}, acc, st.cl, cw, cd1, cd2);
     if (pen_m || (srcb && rg.actD)) {
       acc += xk;
       rg.put(C::ybuf(yb, rg.CP, cur, 0), C::ybuf(yb, rg.CP, cur, 1), acc);
     }
-    if (g.pmask || srcb) rg.sync();  // the penalised entries changed after the step's last barrier
+    if (pmask || srcb) rg.sync();  // the penalised entries changed after the step's last barrier
   }
-  if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)k_lo * Nm + rg.rowD + N * rg.colD)[rg.n & 1] = acc;  // λ_{k_lo}
+  if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)k_lo * Nm + own)[rg.n & 1] = acc;  // λ_{k_lo}
+  cap_store(cd1, cd2, k_lo);
 }
 
 // Reference-equivalent accounting (the Taylor-action path forms no A_k norm of its own): the Padé (d, s) that

@@ -75,7 +75,7 @@ def test_tunable_bus_full_size(built_lib, chain):
     assert info["chain"] == ("taylor" if chain == "auto" else "propagators")
 
 
-def test_synthetic_full_size_fp32(built_lib):
+def test_synthetic_full_size_fp32(built_lib, golden_dir):
     """config 5: synthetic GUE N=256, m=256 (x0 = I), nu=2, Nt=1000, B=128, fp32 on the large-N pipeline."""
     import qoc_oracle as O
     from qoc_amd import GrapeEngine, systems
@@ -94,6 +94,15 @@ def test_synthetic_full_size_fp32(built_lib):
         assert np.abs(xN.conj().T @ xN - np.eye(prob.N)).max() < 5e-3
         Jr = 1 - abs(np.trace(prob.x_target.conj().T @ xN)) ** 2 / prob.n ** 2
         assert abs(J[b] - Jr) < 1e-4
+    # all 1000 slices against the fp64 oracle's committed fixture (tests/golden/make_fullsize.py): seeds 0 and 127,
+    # J, dJdu and x_N of seed 0, at the fp32 bar
+    fx = np.load(golden_dir / "synthetic_full.npz")
+    for i, b in enumerate(fx["seeds"]):
+        assert abs(J[b] - fx["J"][i]) <= 1e-4, (b, J[b], fx["J"][i])
+        rel = np.linalg.norm(g[b] - fx["dJdu"][i]) / np.linalg.norm(fx["dJdu"][i])
+        assert rel <= 1e-3, (b, rel)
+    xN0 = e.state(prob.Nt, seed=0)
+    assert np.abs(xN0 - fx["x_final_seed0"]).max() <= 2e-4
     e.close()
     # bounded prefix of seed 0 against the fp64 numpy oracle
     n2 = 12
@@ -129,3 +138,24 @@ def test_cavity_known_answer_on_gpu(built_lib, golden_dir, chain):
     tgt = np.kron([1.0, 0.0], np.exp(1j * theta))
     tgt = tgt / np.linalg.norm(tgt)
     assert abs(abs(np.vdot(tgt, xN)) - 0.999979) < 1e-6
+
+
+@pytest.mark.parametrize("chain", ["auto", "propagators"])
+def test_zz_measured_pulse_fixture(built_lib, golden_dir, chain):
+    """examples/zz_coupling_simulation.jl:3-13: the reference's measured zz pulse (CSV x 1e-9, 500 slices,
+    Δt = 20/500, x0 = Q_css) propagated on the GPU; x_501 against the fp64 oracle's fixture at 1e-13, and the
+    NOT-gate cost / order-3 gradient of that pulse at the fp64 bar."""
+    from qoc_amd import GrapeEngine, systems
+    fx = np.load(golden_dir / "zz_pulse_fixture.npz")
+    prob = systems.zz_problem(500)
+    u = fx["u"][None]
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, 500, B=1)
+    if chain != "auto":
+        e.set_chain(chain)
+    e.set_cost_trace(prob.x_target, prob.n)
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    assert np.abs(e.state(500) - fx["x_final"]).max() <= 1e-13
+    assert abs(J[0] - fx["J"]) <= 1e-12
+    assert np.linalg.norm(g[0] - fx["dJdu"]) / np.linalg.norm(fx["dJdu"]) <= 1e-10
+    e.close()

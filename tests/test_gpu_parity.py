@@ -185,7 +185,10 @@ def test_device_pointer_eval_matches_host_path(built_lib):
     e.eval_device(ud.data_ptr(), 3, Jd.data_ptr(), gd.data_ptr())
     e.synchronize()
     assert np.array_equal(Jd.cpu().numpy(), Jh)
-    assert np.array_equal(np.transpose(gd.cpu().numpy(), (0, 2, 1)), gh)
+    # the device eval runs the μ recurrence beside the forward chain (λ = coef ⊙ μ): the same gradient to rounding
+    gdh = np.transpose(gd.cpu().numpy(), (0, 2, 1))
+    for b in range(4):
+        assert np.linalg.norm(gdh[b] - gh[b]) / np.linalg.norm(gh[b]) <= 1e-12
     # stale check on the device path
     e.propagate_device(ud.data_ptr(), Jd.data_ptr())
     u2 = ud.clone()

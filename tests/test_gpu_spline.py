@@ -54,8 +54,8 @@ def test_eval_spline_matches_oracle(built_lib):
 
 def test_f_alone_then_f_grad_like_the_reference_callbacks(built_lib):
     """Ipopt's f only propagates (examples/ipopt_callbacks_exp.jl:11-19) and f_grad runs the sensitivity for the
-    coefficients f last saw (:21-31): qoc_propagate_spline + qoc_sensitivity_spline give the fused eval's J and
-    dJdc bitwise; the sensitivity refuses other coefficients (the reference's stale-u error)."""
+    coefficients f last saw (:21-31): qoc_propagate_spline + qoc_sensitivity_spline give the fused eval's J (bitwise)
+    and dJdc; the sensitivity refuses other coefficients (the reference's stale-u error)."""
     from qoc_amd import GrapeEngine, StaleCacheError
     prob, Bs = _zz()
     ns = Bs.shape[1]
@@ -68,7 +68,10 @@ def test_f_alone_then_f_grad_like_the_reference_callbacks(built_lib):
     J1 = e.propagate_spline(c)
     assert np.array_equal(J0, J1)
     g1 = e.sensitivity_spline(c)
-    assert np.array_equal(g0, g1)
+    # the fused eval runs the co-state recurrence beside the forward chain (λ = coef ⊙ μ), the split calls after it:
+    # the same gradient to rounding
+    for b in range(2):
+        assert np.linalg.norm(g1[b] - g0[b]) / np.linalg.norm(g0[b]) <= 1e-12
     with pytest.raises(StaleCacheError, match="Cache data from other control signal u"):
         e.sensitivity_spline(c * 1.001)
     e.propagate_spline(c * 1.001)  # a line-search f: no sensitivity

@@ -373,3 +373,16 @@ def test_zcal_gradient_match_recovers_a_phase_shift():
     g0 = O.grape_eval(prob.A0, prob.A, u, prob.x0, prob.x_target, order=3,
                       cost=O.setup_infidelity_zcalibrated(prob.x_target))[1]
     assert np.linalg.norm(g - g0) / np.linalg.norm(g0) > 1e-10  # the shift is visible at the 1e-10 bar
+
+
+def test_oracle_reproduces_zz_pulse_fixture(golden_dir):
+    """tests/golden/zz_pulse_fixture.npz (examples/zz_coupling_simulation.jl's forward run) is the oracle's output."""
+    from qoc_amd import systems
+    fx = np.load(golden_dir / "zz_pulse_fixture.npz")
+    prob = systems.zz_problem(500)
+    iq = np.load(golden_dir / "zz_coupling_pulse_tahereh210823.npy") * 1e-9
+    assert np.array_equal(np.ascontiguousarray(iq.T), fx["u"])
+    xs = O.propagate(prob.A0, prob.A, fx["u"], prob.x0)
+    assert np.abs(xs[-1] - fx["x_final"]).max() <= 1e-14
+    # unitary propagation of an orthonormal x0
+    assert np.abs(fx["x_final"].conj().T @ fx["x_final"] - np.eye(4)).max() <= 1e-13
