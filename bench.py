@@ -43,15 +43,20 @@ def expm_flops(N, hist):
     return sum(cnt * (8.0 * N ** 3 * (GEMMS_PER_DEGREE[d] + s) + (40.0 / 3.0) * N ** 3) for (d, s), cnt in hist.items())
 
 
-def taylor_gemms(m):
+def taylor_gemms(m, large=False):
     """Complex GEMMs of one executed Taylor polynomial: m = 12 is the 4-product scheme (A2, A3, B4^2,
-    (B2 + A6) A6); m = 3r+2 is Paterson-Stockmeyer (A2, A3, r Horner products in A3)."""
-    return 4 if m == 12 else 2 + (m - 2) // 3
+    (B2 + A6) A6); on the large-N path m = 8 is the 3-product scheme (A2, A2 P, L R); otherwise m = 3r+2 is
+    Paterson-Stockmeyer (A2, A3, r Horner products in A3)."""
+    if m == 12:
+        return 4
+    if m == 8 and large:
+        return 3
+    return 2 + (m - 2) // 3
 
 
-def taylor_flops(N, thist):
+def taylor_flops(N, thist, large=False):
     """Algorithmic FLOPs of the executed Taylor exponentials: taylor_gemms(m) + s squarings, 8 N^3 each."""
-    return sum(cnt * 8.0 * N ** 3 * (taylor_gemms(m) + s) for (m, s), cnt in thist.items())
+    return sum(cnt * 8.0 * N ** 3 * (taylor_gemms(m, large) + s) for (m, s), cnt in thist.items())
 
 
 def ref_eval_flops(N, m, nu, hist_per_eval, order=3):
@@ -293,7 +298,16 @@ def main():
     # a real communicator also at world 1); torch.distributed's all_gather (also RCCL) only if the library
     # cannot load RCCL
     from qoc_amd import multi
-    transport = multi.init_engine_comm(eng, rank * B)
+    # RCCL prints its version banner on stdout when a communicator comes up: keep stdout for the one JSON line
+    sys.stdout.flush()
+    saved_fd = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        transport = multi.init_engine_comm(eng, rank * B)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved_fd, 1)
+        os.close(saved_fd)
 
     def step():
         eng.eval_device(u_d.data_ptr(), args.order, J_d.data_ptr(), g_d.data_ptr())
@@ -364,10 +378,12 @@ def main():
         except Exception:
             traffic_all = {}
     taylor = info1.get("chain") == "taylor" and not large
+    dual = info1.get("concurrent_launch") == "dual"
     if taylor:
         # Taylor-action chains (csrc/qoc_tchain.hpp): no exponential kernel; the chains carry the Taylor terms,
-        # each an N x N by N x m complex matvec (8 N^2 m flops) on v_mfma_f64_4x4x4 (fp64) / VALU (fp32)
-        tl = terms / K
+        # each an N x N by N x m complex matvec (8 N^2 m flops) on v_mfma_f64_4x4x4 (fp64) / VALU (fp32); the dual
+        # launch (k_tchain_mf_dual) carries both directions' terms
+        tl = terms / K * (2 if dual else 1)
         models = {
             "k_expm": ("mfma", 0.0, "TFLOP/s", peak),  # k_tchain_prep: (P, s, e^mu) per slice, no flops counted
             "k_grad": ("mfma", grad_flops(N, m, nu, Nt, B, args.order,
@@ -389,13 +405,21 @@ def main():
         nchunks = math.ceil(B * Nt / info1["chunk"])
         ns_it = (info1["ns_iters"] - info0["ns_iters"]) / max(nchunks * K, 1)
         if thist:
-            f_expm = taylor_flops(N, {k: v / K for k, v in thist.items()})
+            f_expm = taylor_flops(N, {k: v / K for k, v in thist.items()}, large=True)
         else:
             g_expm = sum(c * (GEMMS_PER_DEGREE[d] + s) for (d, s), c in hist_launch.items())
             slices = sum(hist_launch.values())
             f_expm = 8.0 * N ** 3 * (g_expm + slices * (2 * ns_it + 1))
         f_chain = 8.0 * N * N * m * B * Nt
-        f_grad = 8.0 * N * N * m * B * Nt * (2 * (args.order - 1) + args.order)
+        # order 3 with m > 2N/3 (synthetic: m = N): five products of G = λ x^H (one N^2 m, four N^3; big_backward),
+        # else 2(o-1) + o N^2 m-GEMM equivalents (P_a, Q_b, M' = W P^H)
+        sandwich = args.order == 3 and 4 * N < 6 * m
+        if os.environ.get("QOC_GRAD_SANDWICH") is not None:
+            sandwich = args.order == 3 and int(os.environ["QOC_GRAD_SANDWICH"]) != 0
+        if sandwich:
+            f_grad = 8.0 * B * Nt * (N * N * m + 4.0 * N ** 3)
+        else:
+            f_grad = 8.0 * N * N * m * B * Nt * (2 * (args.order - 1) + args.order)
         models = {
             "k_expm": ("mfma", f_expm / 1e12, "TFLOP/s", peak),
             "k_chain_fwd": ("mfma", f_chain / 1e12, "TFLOP/s", peak),
@@ -411,23 +435,28 @@ def main():
     names = {"k_expm": "k_expm_rr", "k_chain_fwd": "k_chain_fwd", "k_chain_bwd": "k_chain_bwd", "k_grad": "k_grad_rr"}
     if taylor:
         mf = prob.precision == "fp64"
-        names = {"k_expm": "k_tchain_prep", "k_chain_fwd": "k_tchain_mf_fwd" if mf else "k_tchain_fwd",
+        names = {"k_expm": "k_tchain_prep",
+                 "k_chain_fwd": "k_tchain_mf_dual" if dual else "k_tchain_mf_fwd" if mf else "k_tchain_fwd",
                  "k_chain_bwd": "k_tchain_mf_bwd" if mf else "k_tchain_bwd",
                  "k_grad": "k_grad_rr_c" if info1.get("backward") in ("captured", "concurrent") else "k_grad_rr"}
         for k in ("k_chain_fwd", "k_chain_bwd"):
             # serial Taylor terms of one seed per launch and the time each takes (the chains' critical path)
             kern[k]["kernel"] = names[k]
-            kern[k]["terms_per_seed"] = terms / K / B
+            kern[k]["terms_per_seed"] = terms / K / B  # per direction
             kern[k]["ns_per_serial_term"] = per_step[k] * 1e6 / max(terms / K / B, 1e-9)
         dom = max(("k_chain_fwd", "k_chain_bwd", "k_grad"), key=lambda k: per_step[k])
+        if dual:
+            kern["k_chain_fwd"]["note"] = "k_tchain_mf_dual: forward chain and mu recurrence of every seed in one launch"
         roof = {"kernel": names[dom], "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
                 "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
                 "traffic": traffic_all.get(names[dom]), "ms_per_launch": kern[dom]["ms_per_launch"],
                 "launches_per_step": lps[dom],
                 "note": ("latency-bound serial recurrence (one workgroup per seed, Taylor terms in sequence): "
                          "achieved = executed matvec flops / launch time"
-                         + ("; the backward (μ) recurrence runs beside the forward chain on a second stream, the "
-                            "contraction after both" if info1.get("backward") == "concurrent" else "")
+                         + ("; the backward (μ) recurrence runs beside the forward chain (k_tchain_mf_dual: one "
+                            "launch of 2B workgroups; flops of both directions), the contraction after both"
+                            if dual else "; the backward (μ) recurrence runs beside the forward chain on a second "
+                            "stream, the contraction after both" if info1.get("backward") == "concurrent" else "")
                          + ("; the backward chain runs in slice ranges, each range's gradient overlapped with "
                             "the next range" if lps.get("k_chain_bwd", 1) > 1 else ""))}
     elif not large:

@@ -179,7 +179,8 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
  * QOC_CHAIN_TAYLOR), info[5] = exponential the propagators run (0 the reference's Padé + solve, 1 register-
  * resident Taylor / Paterson-Stockmeyer, 2 LDS Paterson-Stockmeyer), info[6] = 1 when the Taylor-action chains
  * use Chebyshev terms (skew-Hermitian generators, fp64; QOC_TCHAIN_POLY=taylor keeps Taylor), info[7] = state columns the kernels run on (m, or max(nc1, nc2) with qoc_set_compression), info[8] = how the
- * last backward ran (0 generic, 1 from the chains' captured products, 2 concurrent μ recurrence of qoc_eval_dev),
+ * last backward ran (0 generic, 1 from the chains' captured products, 2 concurrent μ recurrence of qoc_eval_dev on
+ * a second stream, 3 the same in one launch with the forward chain),
  * info[9] = 1 when the last forward chain wrote its captured products.  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
  * selects the large-N path for any size (testing). */
 int qoc_get_info(qoc_ctx* ctx, long long* info /*[10]*/);

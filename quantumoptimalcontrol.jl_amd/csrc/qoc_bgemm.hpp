@@ -399,6 +399,23 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
   }
 }
 
+// 2-norm bound of every A_k of a chunk for skew-Hermitian generators: ||A_k||_2 <= Σ_j |c_jk| ρ_j with c_0 = 1,
+// c_j = u_jk, ρ_j = ||A_j||_2 (the spectral radius, A_j normal) -> atomic max in bmax (one thread per unit).
+struct SpecBound {
+  double rho[9];
+};
+static __global__ void k_spec_bound(int nu, long long unit0, int cnt, const double* __restrict__ u, const SpecBound sb,
+                             unsigned long long* __restrict__ bmax) {
+  double best = 0.0;
+  for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < cnt; it += gridDim.x * blockDim.x) {
+    double b = sb.rho[0];
+    for (int j = 0; j < nu; ++j) b += fabs(u[(unit0 + it) * nu + j]) * sb.rho[j + 1];
+    best = fmax(best, b);
+  }
+  for (int off = 32; off > 0; off >>= 1) best = fmax(best, __shfl_xor(best, off));
+  if ((threadIdx.x & 63) == 0) atomicMax(bmax, (unsigned long long)__double_as_longlong(best));
+}
+
 // ---------------------------------------------------------------------------------------------
 // Element-wise kernels
 // ---------------------------------------------------------------------------------------------

@@ -479,7 +479,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   if (getenv("QOC_BWD_LAST")) c->bwd_last_frac = atof(getenv("QOC_BWD_LAST"));
   if (getenv("QOC_BWD_PRIO")) c->bwd_prio = atoi(getenv("QOC_BWD_PRIO"));
   if (getenv("QOC_BWD_PRESTATE")) c->bwd_prestate = atoi(getenv("QOC_BWD_PRESTATE"));
-  if (getenv("QOC_CONCURRENT")) c->concurrent = atoi(getenv("QOC_CONCURRENT")) != 0;
+  if (getenv("QOC_CONCURRENT")) c->concurrent = std::max(0, std::min(2, atoi(getenv("QOC_CONCURRENT"))));
   hipMemset(c->d_L, 0, (size_t)B * (Nt + 1) * Nm * c->esz);
   *out = c;
   return QOC_OK;
@@ -557,6 +557,31 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
     }
     c->a0norm = nrm;
     c->expm_run = (c->expm_alg == 1 && nrm > 4.0 * kTheta12 && !c->expm_ps) ? 0 : c->expm_alg;
+  }
+  c->big_rho_ok = false;
+  if (c->big && !(getenv("QOC_BIG_NORM1") && atoi(getenv("QOC_BIG_NORM1")) != 0)) {
+    // large-N path: 2-norm bounds of skew-Hermitian generators (ρ_j = ||A_j||_2) for the Taylor degree choice
+    bool skew = true;
+    for (int j = 0; j <= c->nu && skew; ++j) {
+      const double* G = j == 0 ? A0 : Aj[j - 1];
+      double amax = 0.0, dev = 0.0;
+      for (int col = 0; col < c->N; ++col)
+        for (int row = 0; row < c->N; ++row) {
+          const size_t a = 2 * (row + (size_t)c->N * col), b = 2 * (col + (size_t)c->N * row);
+          amax = std::max(amax, std::hypot(G[a], G[a + 1]));
+          dev = std::max(dev, std::hypot(G[a] + G[b], G[a + 1] - G[b + 1]));
+        }
+      skew = dev <= 1e-13 * std::max(amax, 1e-300);
+    }
+    if (skew && c->nu < 9) {
+      for (int j = 0; j <= c->nu; ++j) {
+        double lmin, lmax;
+        herm_extremes(j == 0 ? A0 : Aj[j - 1], c->N, lmin, lmax);
+        const double rho = std::max(std::fabs(lmin), std::fabs(lmax));
+        c->big_rho[j] = rho * (1.0 + 1e-12) + 4.0 * c->N * 2.3e-16 * rho + 1e-300;  // backward-error margin
+      }
+      c->big_rho_ok = true;
+    }
   }
   if (c->tchain_ok) {  // shifted generators Ã_j = A_j - μ_j I and their norms for the Taylor-action chains
     tchain_thresholds(c->tprm, c->prec);
@@ -1216,7 +1241,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[5] = c->big ? c->expm_alg : c->expm_run;  // the large-N pipeline keeps its own (Taylor / Padé) choice
   info[6] = c->chain_mode == 1 && c->cheb && tchain_mf(c) ? 1 : 0;  // Taylor-action chains: Chebyshev terms
   info[7] = c->m;  // state columns the kernels run on (< the caller's m when compress_states packing is on)
-  info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 concurrent μ recurrence
+  info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 / 3 concurrent μ recurrence
   info[9] = c->fwd_captured ? 1 : 0;
   return QOC_OK;
 }

@@ -94,6 +94,10 @@ struct qoc_ctx {
   long long big_hist[5 * 64] = {};
   long long big_thist[8 * 64] = {};  // executed Taylor (r, s) on the large-N path
   long long ns_iters = 0;       // Newton-Schulz iterations executed (all chunks)
+  // skew-Hermitian generators: ρ_j = ||A_j||_2 (host tridiagonalisation + bisection at qoc_set_generators); the
+  // chunk's Taylor degree / squarings then follow the 2-norm bound Σ_j |c_jk| ρ_j instead of the 1-norm
+  double big_rho[9] = {};
+  bool big_rho_ok = false;
   size_t dev_bytes = 0;
   // spline parameterisation (examples/ipopt_callbacks_exp.jl:13-14, 28)
   double* d_Bs = nullptr;  // Nt x ns
@@ -136,11 +140,13 @@ struct qoc_ctx {
   bool cap_ok = false;           // the shape takes it (qoc_set_generators; QOC_CAPTURE=0 turns it off)
   bool fwd_captured = false;     // the last forward pass wrote its captures
   // qoc_eval_dev with a built-in cost and no penalty / co-state source: the backward recurrence runs from X_target
-  // (μ_k, λ_k = coef ⊙ μ_k) beside the forward chain on stream2 (QOC_CONCURRENT=0 turns it off)
-  bool concurrent = true;
+  // (μ_k, λ_k = coef ⊙ μ_k) beside the forward chain: 1 (default) both in one launch (k_tchain_mf_dual), 2 two
+  // launches on two streams, 0 off (QOC_CONCURRENT)
+  int concurrent = 1;
   bool L_is_mu = false;          // d_L holds μ_k (qoc_get_costates applies the coefficients d_coef_mu)
   cx<double>* d_coef_mu = nullptr;  // B x 2m: the λ_N coefficients of the eval that left μ in d_L
-  int last_eval_mode = 0;        // 0 other, 1 captured sequential backward, 2 concurrent μ mode (qoc_get_info)
+  int last_eval_mode = 0;        // 0 other, 1 captured sequential backward, 2 / 3 concurrent μ mode: two streams /
+                                 // one dual launch (qoc_get_info)
   // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
@@ -206,6 +212,9 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu);
 
 // ---- qoc_run_big.hip ----
 size_t big_ws_elems_per_item(int N, int m);
+// extreme eigenvalues of the Hermitian H = i A of a skew-Hermitian generator (column-major interleaved N x N):
+// Householder tridiagonalisation + Sturm bisection, O(N^3), any N
+void herm_extremes(const double* A, int N, double& lmin, double& lmax);
 template <typename T>
 int big_forward(qoc_ctx* c);
 template <typename T>

@@ -4,6 +4,8 @@
 #include "qoc_frechet.hpp"
 #include "qoc_internal.hpp"
 
+#include <complex>
+
 namespace qoc_host {
 
 // =============================================================================================
@@ -104,6 +106,50 @@ static const double hT12[4][4] = {
     {0.0, 1.3110895450078318461208e-12, 0.097250029534075019542638, 0.0068219250901116764187357},
     {0.0, 0.13181061013830184015682, 0.020278555405892590793357, 0.0067595184686308635977856}};
 
+// Degree-8 Taylor polynomial in 3 products (the m = 8 scheme of Bader, Blanes & Casas 2019; coefficients re-derived
+// by tools/derive_t8.py, exact to 60 digits):  A2 = Â², A4 = A2 (x1 Â + x2 A2),
+// A8 = (x3 A2 + A4)(x4 I + x5 Â + x6 A2 + x7 A4),  T8 = I + Â + y2 A2 + A8 = Σ_{k<=8} Â^k / k!.
+static const double hT8x[7] = {0.01992047682223989399948029, 0.004980119205559973499870072, 0.1225521150112074730916119,
+                               2.974307204847626663750796,  0.8765009801785553359771326,  0.07665265321119146690319094,
+                               1.0};
+static const double hT8y2 = 0.1354923613528506316624289;
+// largest ||A|| whose degree-8 Taylor tail Σ_{k>8} ||A||^k / k! is <= 2^-24 (fp32) / 2^-53 (fp64): PS r = 2's
+static const double kTheta8_32 = 0.648322, kTheta8_64 = 0.069933;
+
+template <typename T>
+int t8_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, const Opd& Asrc, const Opd& dest, int ts,
+                  bool count_hist) {
+  const size_t NN = (size_t)N * N, esz = c->esz;
+  auto w = [&](int i) { return mk_opd(ws, (size_t)i * ws_items * NN, esz, (long long)NN); };
+  if (count_hist) c->big_thist[0 * 64 + std::min(ts, 63)] += cnt;  // row 0 (m = 8) on the large-N path: T8
+  const double sc = std::ldexp(1.0, -ts);
+  const double* x = hT8x;
+  int r;
+  GemmArgs g = gemm_args(N, N, N, cnt);  // A2 = sc² A A -> w1;  P = x1 Â + x2 A2 -> w2
+  g.A = Asrc; g.B = Asrc; g.C1 = w(1); g.alpha1 = sc * sc;
+  g.C2 = w(2); g.alpha2 = x[1] * sc * sc; g.nY = 1; g.Y[0] = Asrc; g.w2[0] = x[0] * sc;
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  g = gemm_args(N, N, N, cnt);  // A4 = A2 P:  L = x3 A2 + A4 -> w3,  R = x7 A4 + x6 A2 + x5 Â + x4 I -> w4
+  g.A = w(1); g.B = w(2);
+  g.nY = 2; g.Y[0] = w(1); g.Y[1] = Asrc;
+  g.C1 = w(3); g.alpha1 = 1.0; g.w1[0] = x[2];
+  g.C2 = w(4); g.alpha2 = x[6]; g.w2[0] = x[5]; g.w2[1] = x[4] * sc; g.gamma2 = x[3];
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  g = gemm_args(N, N, N, cnt);  // T8 = L R + y2 A2 + Â + I
+  g.A = w(3); g.B = w(4); g.C1 = ts == 0 ? dest : w(7);
+  g.nY = 2; g.Y[0] = w(1); g.w1[0] = hT8y2; g.Y[1] = Asrc; g.w1[1] = sc; g.gamma1 = 1.0;
+  if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+  int xb = 7;
+  for (int q = 0; q < ts; ++q) {
+    const int nb = xb == 7 ? 1 : 7;
+    g = gemm_args(N, N, N, cnt);
+    g.A = w(xb); g.B = w(xb); g.C1 = q == ts - 1 ? dest : w(nb);
+    if ((r = big_gemm<T>(c, 0, 0, g))) return r;
+    xb = nb;
+  }
+  return QOC_OK;
+}
+
 template <typename T>
 int t12_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, const Opd& Asrc, const Opd& dest, int ts,
                    bool count_hist) {
@@ -167,7 +213,14 @@ int taylor_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, con
   // (3.1, 4.2]): 6 GEMMs instead of Paterson-Stockmeyer's 7.
   const double th12 = sizeof(T) == 4 ? 1.562211457125874 : kTheta12;
   const int s12 = nA > th12 ? (int)std::ceil(std::log2(nA / th12)) : 0;
-  if (4 + s12 < best && !getenv("QOC_BIG_NO_T12")) return t12_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, s12, count_hist);
+  // degree 8 in 3 products (T8) when 3 + s8 GEMMs beat both: synthetic slices (2-norm bound 0.58 <= θ8 = 0.648 in
+  // fp32) need no squaring
+  const double th8 = sizeof(T) == 4 ? kTheta8_32 : kTheta8_64;
+  const int s8 = nA > th8 ? (int)std::ceil(std::log2(nA / th8)) : 0;
+  const bool t12ok = !getenv("QOC_BIG_NO_T12");
+  if (3 + s8 < best && (!t12ok || 3 + s8 <= 4 + s12) && !getenv("QOC_BIG_NO_T8"))
+    return t8_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, s8, count_hist);
+  if (4 + s12 < best && t12ok) return t12_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, s12, count_hist);
   if (count_hist) c->big_thist[(tr - 2) * 64 + std::min(ts, 63)] += cnt;
   static const double f[27] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720, 1.0 / 5040, 1.0 / 40320,
                                2.755731922398589e-06, 2.755731922398589e-07, 2.505210838544172e-08,
@@ -215,7 +268,7 @@ int taylor_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, con
 // 8 buffers of ws_items x n x n at ws; red >= cnt doubles.
 template <typename T>
 int expm_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, double* red, const Opd& Asrc,
-                    const Opd& dest, double nA, bool count_hist) {
+                    const Opd& dest, double nA, bool count_hist, double nA_exec = -1.0) {
   const size_t NN = (size_t)N * N, esz = c->esz;
   auto w = [&](int i) { return mk_opd(ws, (size_t)i * ws_items * NN, esz, (long long)NN); };
   int r;
@@ -232,7 +285,11 @@ int expm_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, doubl
   }
   const int di = d == 3 ? 0 : d == 5 ? 1 : d == 7 ? 2 : d == 9 ? 3 : 4;
   if (count_hist) c->big_hist[di * 64 + std::min(sq, 63)] += cnt;
-  if (c->expm_alg != 0) return taylor_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, nA, count_hist);
+  // the executed Taylor scheme may use a tighter norm bound (nA_exec: the 2-norm bound of skew-Hermitian slices);
+  // the Padé (d, s) above is the reference's 1-norm choice, kept for the reference-equivalent accounting
+  if (c->expm_alg != 0)
+    return taylor_gemm_chunk<T>(c, N, cnt, ws, ws_items, Asrc, dest, nA_exec >= 0.0 ? std::min(nA, nA_exec) : nA,
+                                count_hist);
   const double* C = d == 3 ? hPade3 : d == 5 ? hPade5 : d == 7 ? hPade7 : d == 9 ? hPade9 : hPade13;
   const double sc = std::ldexp(1.0, -sq);
   GemmArgs g;
@@ -342,15 +399,24 @@ int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
   const int N = c->N;
   const size_t NN = (size_t)N * N, esz = c->esz;
   cx<T>* a0 = (cx<T>*)c->d_ws;
-  HIPCHK(c, hipMemsetAsync(c->d_red, 0, sizeof(double), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_red, 0, 2 * sizeof(double), c->stream));
   hipLaunchKernelGGL((k_form_norm<T>), dim3(cnt), dim3(256), 0, c->stream, N, c->nu, u0, (const cx<T>*)c->d_A,
                      (const double*)c->d_u, a0, (unsigned long long*)c->d_red);
   HIPCHK(c, hipGetLastError());
-  double nA = 0.0;
-  HIPCHK(c, hipMemcpyAsync(&nA, c->d_red, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (c->big_rho_ok) {
+    SpecBound sb{};
+    for (int j = 0; j <= c->nu && j < 9; ++j) sb.rho[j] = c->big_rho[j];
+    const unsigned blocks = (unsigned)std::min<long long>((cnt + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_spec_bound, dim3(blocks), dim3(256), 0, c->stream, c->nu, u0, cnt, (const double*)c->d_u, sb,
+                       (unsigned long long*)(c->d_red + 1));
+    HIPCHK(c, hipGetLastError());
+  }
+  double nA[2] = {0.0, 0.0};
+  HIPCHK(c, hipMemcpyAsync(nA, c->d_red, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return expm_gemm_chunk<T>(c, N, cnt, c->d_ws, (size_t)c->chunk, c->d_red, mk_opd(c->d_ws, 0, esz, (long long)NN),
-                            mk_opd(c->d_U, (size_t)u0 * NN, esz, (long long)NN), nA, true);
+                            mk_opd(c->d_U, (size_t)u0 * NN, esz, (long long)NN), nA[0], true,
+                            c->big_rho_ok ? nA[1] : -1.0);
 }
 
 template <typename T>
@@ -689,6 +755,86 @@ int frechet_grad(qoc_ctx* c, double* d_dJdu) {
     HIPCHK(c, hipGetLastError());
   }
   return QOC_OK;
+}
+
+// Extreme eigenvalues of H = i A (A skew-Hermitian, column-major interleaved N x N): Householder reduction of H to a
+// Hermitian tridiagonal T (its off-diagonal moduli give a real symmetric tridiagonal with the same spectrum), then
+// Sturm-count bisection for the smallest and the largest eigenvalue.  Backward stable: the interval is exact up to
+// ~N eps ||H||, which the caller adds as a margin.
+void herm_extremes(const double* A, int N, double& lmin, double& lmax) {
+  using C = std::complex<double>;
+  std::vector<C> H((size_t)N * N);
+  auto h = [&](int r, int c) -> C& { return H[r + (size_t)N * c]; };
+  for (int c = 0; c < N; ++c)
+    for (int r = 0; r < N; ++r) {
+      const C a(A[2 * (r + (size_t)N * c)], A[2 * (r + (size_t)N * c) + 1]);
+      h(r, c) = C(0.0, 1.0) * a;  // H = i A
+    }
+  for (int c = 0; c < N; ++c)  // exact Hermitian symmetry
+    for (int r = c; r < N; ++r) {
+      const C v = 0.5 * (h(r, c) + std::conj(h(c, r)));
+      h(r, c) = v;
+      h(c, r) = std::conj(v);
+    }
+  std::vector<C> v(N), p(N), q(N);
+  for (int k = 0; k + 2 < N; ++k) {
+    double nx = 0.0;
+    for (int i = k + 1; i < N; ++i) nx += std::norm(h(i, k));
+    nx = std::sqrt(nx);
+    if (nx == 0.0) continue;
+    const C x0 = h(k + 1, k);
+    const C alpha = -(std::abs(x0) > 0 ? x0 / std::abs(x0) : C(1.0)) * nx;
+    for (int i = 0; i < N; ++i) v[i] = 0.0;
+    for (int i = k + 1; i < N; ++i) v[i] = h(i, k);
+    v[k + 1] -= alpha;
+    double nv = 0.0;
+    for (int i = k + 1; i < N; ++i) nv += std::norm(v[i]);
+    nv = std::sqrt(nv);
+    if (nv == 0.0) continue;
+    for (int i = k + 1; i < N; ++i) v[i] /= nv;
+    // H <- (I - 2 v v^H) H (I - 2 v v^H) = H - 2 v w^H - 2 w v^H, w = p - (v^H p) v, p = H v
+    for (int i = k; i < N; ++i) {
+      C s = 0.0;
+      for (int j = k + 1; j < N; ++j) s += h(i, j) * v[j];
+      p[i] = s;
+    }
+    C K = 0.0;
+    for (int i = k + 1; i < N; ++i) K += std::conj(v[i]) * p[i];
+    for (int i = k; i < N; ++i) q[i] = p[i] - K * v[i];
+    for (int j = k; j < N; ++j)
+      for (int i = k; i < N; ++i) h(i, j) -= 2.0 * (v[i] * std::conj(q[j]) + q[i] * std::conj(v[j]));
+  }
+  std::vector<double> d(N), e(N, 0.0);
+  double gl = 1e300, gu = -1e300;
+  for (int i = 0; i < N; ++i) {
+    d[i] = h(i, i).real();
+    if (i + 1 < N) e[i] = std::abs(h(i + 1, i));
+  }
+  for (int i = 0; i < N; ++i) {  // Gershgorin interval of T
+    const double r = (i > 0 ? e[i - 1] : 0.0) + (i + 1 < N ? e[i] : 0.0);
+    gl = std::min(gl, d[i] - r);
+    gu = std::max(gu, d[i] + r);
+  }
+  auto count_below = [&](double x) {  // eigenvalues of T below x (Sturm: negative pivots of T - x I = L D L^T)
+    int cnt = 0;
+    double piv = 1.0;
+    for (int i = 0; i < N; ++i) {
+      piv = d[i] - x - (i > 0 ? e[i - 1] * e[i - 1] / piv : 0.0);
+      if (piv == 0.0) piv = -1e-300;
+      if (piv < 0.0) ++cnt;
+    }
+    return cnt;
+  };
+  auto bisect = [&](int target) {  // smallest x with count_below(x) > target: the (target+1)-th eigenvalue
+    double lo = gl, hi = gu;
+    for (int it = 0; it < 200 && hi - lo > 1e-15 * std::max(std::fabs(lo), std::fabs(hi)) + 1e-300; ++it) {
+      const double mid = 0.5 * (lo + hi);
+      (count_below(mid) > target ? hi : lo) = mid;
+    }
+    return 0.5 * (lo + hi);
+  };
+  lmin = bisect(0);
+  lmax = bisect(N - 1);
 }
 
 // generator layouts of the GEMM-shaped gradient: [A0^H | A1^H | ...] and [A1; A2; ...]

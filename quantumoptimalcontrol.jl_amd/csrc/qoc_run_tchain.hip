@@ -408,14 +408,40 @@ int tchain_eval_concurrent(qoc_ctx* c, double* d_dJdu) {
   if ((r = tchain_prep(c))) return r;
   HIPCHK(c, hipEventRecord(c->sync_ev[0], c->stream));
   HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[0], 0));
-  // μ recurrence beside the forward chain
-  r = tchain_backward<T>(c, 0, c->Nt, c->stream2, TB_CAPTURE | TB_MU);
-  if (r == QOC_OK) r = tchain_forward_chain<T>(c);
-  if (r == QOC_OK && !c->fwd_captured) r = fail(c, QOC_ERR_STATE, "concurrent eval: forward captures missing");
-  const hipError_t e1 = hipEventRecord(c->sync_ev[1], c->stream2);
-  const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(c->stream, c->sync_ev[1], 0) : e1;
-  if (r) return r;
-  if (e2 != hipSuccess) return fail(c, QOC_ERR_HIP, "stream join: %s", hipGetErrorString(e2));
+  if (c->concurrent == 2) {
+    // μ recurrence beside the forward chain: two launches on two streams
+    r = tchain_backward<T>(c, 0, c->Nt, c->stream2, TB_CAPTURE | TB_MU);
+    if (r == QOC_OK) r = tchain_forward_chain<T>(c);
+    if (r == QOC_OK && !c->fwd_captured) r = fail(c, QOC_ERR_STATE, "concurrent eval: forward captures missing");
+    const hipError_t e1 = hipEventRecord(c->sync_ev[1], c->stream2);
+    const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(c->stream, c->sync_ev[1], 0) : e1;
+    if (r) return r;
+    if (e2 != hipSuccess) return fail(c, QOC_ERR_HIP, "stream join: %s", hipGetErrorString(e2));
+  } else {
+    // one launch of 2B workgroups: k_tchain_mf_dual (forward chain and μ recurrence of every seed)
+    const size_t bufN = (size_t)c->N * ((size_t)c->B * (c->Nt + 1) * c->m);
+    TChainArgs gf = tchain_args(c), gb = tchain_args(c);
+    gf.cap1 = c->d_pws;
+    gf.cap2 = (cx<double>*)c->d_pws + bufN;
+    gb.cap1 = c->d_gws;
+    gb.cap2 = (cx<double>*)c->d_gws + bufN;
+    gb.mu_mode = 1;
+    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
+    const int threads = 64 * tchain_mf_waves(c->N, c->m);
+    const int mk = mark_begin(c, 1);
+    hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
+      constexpr int KQ = decltype(KQ_)::value;
+      auto kern = c->cheb_ran ? k_tchain_mf_dual<KQ, true, 256> : k_tchain_mf_dual<KQ, false, 256>;
+      hipError_t q = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (q != hipSuccess) return q;
+      hipLaunchKernelGGL(kern, dim3(2 * c->B), dim3(threads), lds, c->stream, gf, gb);
+      return hipGetLastError();
+    });
+    mark_end(c, mk);
+    if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_tchain_mf_dual launch: %s", hipGetErrorString(e));
+    c->fwd_captured = true;
+    c->props_since_reset++;
+  }
   const int mk = mark_begin(c, 3);
   r = grad_rr_cap(c, d_dJdu, c->stream, 0, c->Nt, true);
   mark_end(c, mk);
@@ -424,7 +450,7 @@ int tchain_eval_concurrent(qoc_ctx* c, double* d_dJdu) {
   HIPCHK(c, hipMemcpyAsync(c->d_coef_mu, c->d_coef, (size_t)c->B * 2 * c->m * sizeof(cx<double>),
                            hipMemcpyDeviceToDevice, c->stream));
   c->L_is_mu = true;
-  c->last_eval_mode = 2;
+  c->last_eval_mode = c->concurrent == 2 ? 2 : 3;
   return QOC_OK;
 }
 

@@ -993,13 +993,13 @@ struct TChainMF {
 // products of every slice are written to g.cap1 / g.cap2 when those are set (TChainArgs); the writes of slice k
 // are issued at the start of slice k + 1, next to the state's, ahead of the step-data prefetch.
 template <int KQ, bool CHEB, int MAXT>
-__global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
+__device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const int b) {
   using C = TChainMF<KQ>;
   constexpr int RP = C::RP;
   constexpr bool REGS = MAXT == 256;  // generators in registers (the dispatch picks MAXT = 256 only for nu <= 2)
   constexpr int NUR = REGS ? 2 : TCHAIN_NUMAX;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, tid = threadIdx.x, nthr = blockDim.x;
   const int NN = N * N, Nm = N * m, CP = (m + 1) / 2;
   cx<double>* gen = reinterpret_cast<cx<double>*>(smem);  // REGS: Ã_2 only
   double* yb = reinterpret_cast<double*>(gen + (size_t)(REGS ? (nu >= 2 ? 1 : 0) : nu + 1) * NN);
@@ -1104,13 +1104,13 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
 }
 
 template <int KQ, bool CHEB, int MAXT>
-__global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
+__device__ __forceinline__ void tchain_mf_bwd_body(const TChainArgs& g, const int b) {
   using C = TChainMF<KQ>;
   constexpr int RP = C::RP;
   constexpr bool REGS = MAXT == 256;  // see k_tchain_mf_fwd
   constexpr int NUR = REGS ? 2 : TCHAIN_NUMAX;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, b = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
+  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, tid = threadIdx.x, nthr = blockDim.x;
   const int NN = N * N, Nm = N * m, CP = (m + 1) / 2;
   cx<double>* gen = reinterpret_cast<cx<double>*>(smem);  // REGS: Ã_2^H only
   double* yb = reinterpret_cast<double*>(gen + (size_t)(REGS ? (nu >= 2 ? 1 : 0) : nu + 1) * NN);
@@ -1217,6 +1217,30 @@ __global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
   }
   if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)k_lo * Nm + own)[rg.n & 1] = acc;  // λ_{k_lo}
   cap_store(cd1, cd2, k_lo);
+}
+
+template <int KQ, bool CHEB, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_tchain_mf_fwd(const TChainArgs g) {
+  tchain_mf_fwd_body<KQ, CHEB, MAXT>(g, blockIdx.x);
+}
+template <int KQ, bool CHEB, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_tchain_mf_bwd(const TChainArgs g) {
+  tchain_mf_bwd_body<KQ, CHEB, MAXT>(g, blockIdx.x);
+}
+
+// Forward chain and μ recurrence of every seed in ONE launch of 2B workgroups (the concurrent eval): every workgroup
+// is resident from the start, so each CU carries both directions' chains side by side.  Two launches on two
+// streams leave the placement to the dispatcher, which can stack one direction's workgroups on some CUs while
+// others idle.  The direction alternates every 8 workgroups, so that each XCD (workgroups round-robin over the
+// 8 XCDs) takes both.
+template <int KQ, bool CHEB, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_tchain_mf_dual(const TChainArgs gf, const TChainArgs gb) {
+  const int i = blockIdx.x, B = gridDim.x >> 1;
+  const bool by8 = (B & 7) == 0;
+  const int dir = by8 ? (i >> 3) & 1 : i & 1;
+  const int seed = by8 ? ((i >> 4) << 3) | (i & 7) : i >> 1;
+  if (dir == 0) tchain_mf_fwd_body<KQ, CHEB, MAXT>(gf, seed);
+  else tchain_mf_bwd_body<KQ, CHEB, MAXT>(gb, seed);
 }
 
 // Reference-equivalent accounting (the Taylor-action path forms no A_k norm of its own): the Padé (d, s) that

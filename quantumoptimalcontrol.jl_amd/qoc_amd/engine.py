@@ -316,7 +316,8 @@ class GrapeEngine:
                 "device_bytes": int(v[3]), "chain": "taylor" if v[4] == 1 else "propagators",
                 "expm": {0: "pade", 1: "taylor_rr", 2: "ps_lds"}.get(int(v[5]), "?"),
                 "chain_poly": "chebyshev" if v[6] else "taylor", "kernel_m": int(v[7]),
-                "backward": {0: "generic", 1: "captured", 2: "concurrent"}.get(int(v[8]), "?"),
+                "backward": {0: "generic", 1: "captured", 2: "concurrent", 3: "concurrent"}.get(int(v[8]), "?"),
+                "concurrent_launch": {2: "two_streams", 3: "dual"}.get(int(v[8])),
                 "fwd_captured": bool(v[9])}
 
     def set_chain(self, mode: str = "auto"):
