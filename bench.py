@@ -49,7 +49,7 @@ def taylor_gemms(m, large=False):
     Paterson-Stockmeyer (A2, A3, r Horner products in A3)."""
     if m == 12:
         return 4
-    if m == 8 and large:
+    if m == "8t":
         return 3
     return 2 + (m - 2) // 3
 
@@ -533,7 +533,7 @@ def main():
             "cpu_baseline": cpu,
             "kernels": kern,
             "pade_hist_per_step": {f"d{d}s{s}": v / K for (d, s), v in sorted(hist.items())},
-            "taylor_hist_per_step": {f"m{mm}s{s}": v / K for (mm, s), v in sorted(thist.items())},
+            "taylor_hist_per_step": {f"m{mm}s{s}": v / K for (mm, s), v in sorted(thist.items(), key=str)},
             # the reference algorithm's flops per eval (SURVEY §8d F_eval, Padé (d, s) counted on the device)
             # times this engine's eval rate: a reference-equivalent RATE, not a utilisation figure (the engine
             # executes far fewer flops than that formula; see "roofline" for the executed work)

@@ -137,10 +137,12 @@ int qoc_pade_histogram(qoc_ctx* ctx, long long* hist, int reset);
  *   hist[(r-2)*64 + s], r = 2..8: degree m = 3r+2 Taylor by Paterson-Stockmeyer (2 + r GEMMs) with s
  *     squarings (large-N pipeline; LDS kernel with QOC_EXPM_LDS=1);
  *   hist[7*64 + s]: degree-12 Taylor in 4 GEMMs (Bader-Blanes-Casas form) with s squarings (the
- *     default register-resident kernel).
+ *     default register-resident kernel);
+ *   hist[8*64 + s]: degree-8 Taylor in 3 GEMMs (Bader-Blanes-Casas form) with s squarings (large-N pipeline).
+ * hist holds 9*64 entries.
  * The truncation tail is <= 2^-53 in every case.  qoc_pade_histogram keeps reporting the Padé (d, s)
  * the reference would select. */
-int qoc_taylor_histogram(qoc_ctx* ctx, long long* hist, int reset);
+int qoc_taylor_histogram(qoc_ctx* ctx, long long* hist /*[9*64]*/, int reset);
 
 /* Live per-kernel timing: when enabled, hipEvents are recorded on qoc_stream around each hot-path
  * kernel (phase 0 k_expm, 1 k_chain_fwd, 2 k_chain_bwd, 3 k_grad).  qoc_phase_times synchronises the

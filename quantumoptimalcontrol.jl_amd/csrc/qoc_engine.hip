@@ -1372,7 +1372,8 @@ int qoc_taylor_histogram(qoc_ctx* c, long long* hist, int reset) {
   HIPCHK(c, hipMemcpyAsync(hist, c->d_hist + 5 * 64, 8 * 64 * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
   if (reset) HIPCHK(c, hipMemsetAsync(c->d_hist + 5 * 64, 0, 8 * 64 * sizeof(long long), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  for (int i = 0; i < 8 * 64; ++i) hist[i] += c->big_thist[i];
+  for (int i = 8 * 64; i < 9 * 64; ++i) hist[i] = 0;
+  for (int i = 0; i < 9 * 64; ++i) hist[i] += c->big_thist[i];
   if (reset) std::memset(c->big_thist, 0, sizeof(c->big_thist));
   return QOC_OK;
 }

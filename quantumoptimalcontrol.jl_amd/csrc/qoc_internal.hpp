@@ -92,7 +92,7 @@ struct qoc_ctx {
   void* d_ws = nullptr;         // chunk workspace
   double* d_red = nullptr;      // per-item reductions (chunk + 8 doubles)
   long long big_hist[5 * 64] = {};
-  long long big_thist[8 * 64] = {};  // executed Taylor (r, s) on the large-N path
+  long long big_thist[9 * 64] = {};  // executed Taylor (r, s) on the large-N path; row 8: T8
   long long ns_iters = 0;       // Newton-Schulz iterations executed (all chunks)
   // skew-Hermitian generators: ρ_j = ||A_j||_2 (host tridiagonalisation + bisection at qoc_set_generators); the
   // chunk's Taylor degree / squarings then follow the 2-norm bound Σ_j |c_jk| ρ_j instead of the 1-norm

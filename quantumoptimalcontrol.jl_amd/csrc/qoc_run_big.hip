@@ -121,7 +121,7 @@ int t8_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, const O
                   bool count_hist) {
   const size_t NN = (size_t)N * N, esz = c->esz;
   auto w = [&](int i) { return mk_opd(ws, (size_t)i * ws_items * NN, esz, (long long)NN); };
-  if (count_hist) c->big_thist[0 * 64 + std::min(ts, 63)] += cnt;  // row 0 (m = 8) on the large-N path: T8
+  if (count_hist) c->big_thist[8 * 64 + std::min(ts, 63)] += cnt;  // row 8: T8
   const double sc = std::ldexp(1.0, -ts);
   const double* x = hT8x;
   int r;

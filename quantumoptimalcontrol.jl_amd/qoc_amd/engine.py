@@ -365,11 +365,15 @@ class GrapeEngine:
         return {"ms": ms.value, "launches": n.value, "flops": fl.value}
 
     def taylor_histogram(self, reset: bool = False) -> dict:
-        """Executed Taylor counts {(m, s): count}: degree m = 3r+2 by Paterson-Stockmeyer (2 + r GEMMs) or
-        m = 12 by the 4-GEMM scheme, with s squarings (include/qoc.h: qoc_taylor_histogram)."""
-        h = np.zeros(8 * 64, dtype=np.int64)
+        """Executed Taylor counts {(m, s): count}: degree m = 3r+2 by Paterson-Stockmeyer (2 + r GEMMs),
+        m = 12 by the 4-GEMM scheme, m = "8t" by the 3-GEMM degree-8 scheme (large-N path), with s squarings
+        (include/qoc.h: qoc_taylor_histogram)."""
+        h = np.zeros(9 * 64, dtype=np.int64)
         self._chk(self._lib.qoc_taylor_histogram(self._h, h.ctypes.data_as(C.POINTER(C.c_longlong)), int(reset)))
-        return {(12 if i // 64 == 7 else 3 * (i // 64 + 2) + 2, i % 64): int(v) for i, v in enumerate(h) if v}
+        # row 8: the 3-product degree-8 scheme (large-N path), reported as m = "8t" to keep it apart from
+        # Paterson-Stockmeyer's degree 8 (row 0, 4 GEMMs)
+        return {("8t" if i // 64 == 8 else 12 if i // 64 == 7 else 3 * (i // 64 + 2) + 2, i % 64): int(v)
+                for i, v in enumerate(h) if v}
 
     def pade_histogram(self, reset: bool = False) -> dict:
         h = np.zeros(5 * 64, dtype=np.int64)

@@ -179,6 +179,8 @@ def test_large_n_t12_and_paterson_stockmeyer(built_lib, monkeypatch, precision):
     oracle (fp64 bar, or the fp32 tolerance) on norms that need squarings."""
     from qoc_amd import GrapeEngine
     monkeypatch.setenv("QOC_CHUNK", "4")
+    monkeypatch.setenv("QOC_BIG_NORM1", "1")  # the 1-norm choice without the 3-product T8 (next test)
+    monkeypatch.setenv("QOC_BIG_NO_T8", "1")
     rng = np.random.default_rng(31)
     prob = _gue_problem(72, 4, 6, norm0=2.4, normj=0.6, seed=32)
     u = rng.uniform(-1, 1, size=(2, 2, prob.Nt))
@@ -197,3 +199,41 @@ def test_large_n_t12_and_paterson_stockmeyer(built_lib, monkeypatch, precision):
         _compare(prob, u, J, g, tol=tol)
     assert hists["0"] and all(m == 12 for (m, _) in hists["0"]), hists
     assert hists["1"] and all(m != 12 for (m, _) in hists["1"]), hists
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_large_n_t8_with_spectral_bound(built_lib, monkeypatch, precision):
+    """Skew-Hermitian generators: the chunk's Taylor choice follows the 2-norm bound Σ_j |c_jk| ρ_j (ρ_j = ||A_j||_2
+    from the host tridiagonalisation), and degrees <= 8 run in 3 products (T8, histogram row m = 8; fp32: no
+    squaring at the GUE norms, fp64 with squarings).  QOC_BIG_NO_T8=1 falls back to T12 / Paterson-Stockmeyer and
+    QOC_BIG_NORM1=1 to the 1-norm choice; every variant matches the oracle."""
+    from qoc_amd import GrapeEngine
+    monkeypatch.setenv("QOC_CHUNK", "4")
+    rng = np.random.default_rng(33)
+    # 1-norms; the spectral radii of these GUE generators are ~0.3 of them (fp32: bound ~0.5 <= θ8 = 0.648; fp64:
+    # bound ~0.04 <= θ8 = 0.0699)
+    norms = (1.2, 0.3) if precision == "fp32" else (0.1, 0.03)
+    prob = _gue_problem(72, 4, 6, norm0=norms[0], normj=norms[1], seed=34)
+    u = rng.uniform(-1, 1, size=(2, 2, prob.Nt))
+    tol = (1e-12, 1e-10) if precision == "fp64" else (1e-4, 1e-3)
+    hists = {}
+    for mode in ("t8", "no_t8", "norm1"):
+        if mode == "no_t8":
+            monkeypatch.setenv("QOC_BIG_NO_T8", "1")
+        if mode == "norm1":
+            monkeypatch.delenv("QOC_BIG_NO_T8")
+            monkeypatch.setenv("QOC_BIG_NORM1", "1")
+        e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2, precision=precision)
+        e.set_cost_trace(prob.x_target, prob.n)
+        J = e.propagate(u)
+        g = e.grape_sensitivity(u, 3)
+        hists[mode] = e.taylor_histogram()
+        e.close()
+        _compare(prob, u, J, g, tol=tol)
+    assert hists["t8"] and all(m == "8t" and s == 0 for (m, s) in hists["t8"]), hists
+    assert all(m != "8t" for (m, _) in hists["no_t8"]), hists
+
+    def gemms(h):  # T8 3 + s, T12 4 + s, Paterson-Stockmeyer m = 3r + 2: 2 + r + s
+        return sum(c * ((3 if m == "8t" else 4 if m == 12 else 2 + (m - 2) // 3) + s) for (m, s), c in h.items())
+    assert gemms(hists["no_t8"]) > gemms(hists["t8"]), hists
+    assert gemms(hists["norm1"]) > gemms(hists["t8"]), hists  # the 1-norm bound costs products

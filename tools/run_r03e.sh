@@ -5,6 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 T=${1:-r03e}
 export TMPDIR=/tmp
+timeout -k 10 60 tools/mfma4_lat > gpurun_out/${T}_mfma4_lat.txt 2>&1 || exit 1
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_concurrent.py tests/test_gpu_spline.py tests/test_gpu_large_n.py > gpurun_out/${T}_focus.log 2>&1 || exit 1
 for c in cavity tunable_bus zz_batch; do
   for mode in 0 2 1; do
