@@ -327,6 +327,25 @@ def zcal_gradient_match(g, A0, A, u, x0, x_target, order=3, nsub=None, h=1e-6):
     return float(np.linalg.norm(r - t * d) / np.linalg.norm(g0)), t
 
 
+def zcal_dtheta_bound(x_target, xN, theta_tol=1e-9):
+    """How far apart two correct golden-section searches (src/fidelities.jl:81-137) may stop, from the curvature of
+    the calibration objective J(δ) = sqrt(a1 + b1 cos(δ+Δ)) + sqrt(a2 + b2 cos(δ-Δ)) at its maximum: a comparison
+    of f values is decided by rounding once c·w^2 < 2 eps J with c = |J''|/2, so each search stops within
+    w = sqrt(4 eps J / |J''|) (+ its bracket θ_tol) of the optimum and the two within twice that.  A factor 2 margin
+    covers the rounding of the bracket updates themselves."""
+    X = np.asarray(x_target, dtype=np.complex128)
+    m = [complex(v) for v in np.diag(X.conj().T @ np.asarray(xN, dtype=np.complex128))]
+    F, th = optimal_calibration(m, theta_tol)
+
+    def Jt(t):  # the objective in θ1 directly (θ1 = ϕ_mean + α δ)
+        return abs(m[0] + m[1] * _cis(t)) + abs(m[2] + m[3] * _cis(t))
+    hh = 1e-3
+    J2 = abs(Jt(th[0] + hh) - 2 * Jt(th[0]) + Jt(th[0] - hh)) / hh ** 2
+    eps = np.finfo(np.float64).eps
+    w = math.sqrt(4 * eps * max(F, 1e-300) / max(J2, 1e-300))
+    return 2 * (2 * w + 2 * theta_tol)
+
+
 # ---------------------------------------------------------------------------
 # Phase-calibrated fidelities (src/fidelities.jl)
 # ---------------------------------------------------------------------------

@@ -18,9 +18,6 @@ import qoc_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-ZCAL_MAX_DTHETA = 1e-6  # see test_gpu_parity.test_zcalibrated_cost
-
-
 def _problems():
     from qoc_amd import systems
     out = {}
@@ -114,7 +111,8 @@ def test_concurrent_eval_zcalibrated(built_lib):
         xN = O.propagate(prob.A0, prob.A, u[b], prob.x0)[-1]
         assert abs(J[b] - Jz(xN)) <= 1e-12
         res, dth = O.zcal_gradient_match(g[b], prob.A0, prob.A, u[b], prob.x0, prob.x_target, order=3)
-        assert res <= 1e-10 and abs(dth) <= ZCAL_MAX_DTHETA, (b, res, dth)
+        bound = O.zcal_dtheta_bound(prob.x_target, xN)  # see test_gpu_parity.test_zcalibrated_cost
+        assert res <= 1e-10 and abs(dth) <= bound, (b, res, dth, bound)
     e.close()
 
 
@@ -159,7 +157,8 @@ def test_concurrent_eval_packed_states(built_lib):
             assert abs(J[b] - Jr) <= 1e-12
             if zcal:
                 res, dth = O.zcal_gradient_match(g[b], prob.A0, prob.A, u[b], prob.x0, prob.x_target, order=3)
-                assert res <= 1e-10 and abs(dth) <= ZCAL_MAX_DTHETA, (b, res, dth)
+                bound = O.zcal_dtheta_bound(prob.x_target, O.propagate(prob.A0, prob.A, u[b], prob.x0)[-1])
+                assert res <= 1e-10 and abs(dth) <= bound, (b, res, dth, bound)
             else:
                 assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
                 scale = np.abs(cr.lam[prob.Nt]).max()

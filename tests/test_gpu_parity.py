@@ -119,8 +119,8 @@ def test_state_penalty(built_lib, chain):
 # the optimum, so θ is fixed only to ~sqrt(eps) and two correct implementations (GPU, oracle) stop at phases a
 # few 1e-9..1e-8 apart.  J is stationary in θ (held to the 1e-12 bar); the gradient carries e^{iθ} linearly, so
 # it is compared with the oracle's gradient family g(Δθ) (qoc_oracle.zcal_gradient_match): the GPU gradient
-# must equal g(Δθ) for some |Δθ| <= 1e-6 to the 1e-10 bar.
-ZCAL_MAX_DTHETA = 1e-6
+# must equal g(Δθ) to the 1e-10 bar for some |Δθ| within the per-seed bound qoc_oracle.zcal_dtheta_bound derives
+# from the curvature of the calibration objective at its maximum (≈ 2.5e-7 for these cases).
 
 
 @pytest.mark.parametrize("path", ["propagators", "taylor", "large_n", "tsit5"])
@@ -148,7 +148,9 @@ def test_zcalibrated_cost(built_lib, path, monkeypatch):
               O.propagate(prob.A0, prob.A, u[b], prob.x0))[-1]
         assert abs(J[b] - Jz(xN)) <= 1e-12, (b, J[b] - Jz(xN))
         res, dth = O.zcal_gradient_match(g[b], prob.A0, prob.A, u[b], prob.x0, prob.x_target, order=3, nsub=nsub)
-        assert res <= 1e-10 and abs(dth) <= ZCAL_MAX_DTHETA, (b, res, dth)
+        bound = O.zcal_dtheta_bound(prob.x_target, xN)
+        print(f"zcal {path} seed {b}: |dtheta| = {abs(dth):.3e} (bound {bound:.3e}), residual {res:.2e}")
+        assert res <= 1e-10 and abs(dth) <= bound, (b, res, dth, bound)
     e.close()
 
 

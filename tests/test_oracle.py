@@ -375,6 +375,32 @@ def test_zcal_gradient_match_recovers_a_phase_shift():
     assert np.linalg.norm(g - g0) / np.linalg.norm(g0) > 1e-10  # the shift is visible at the 1e-10 bar
 
 
+def test_zcal_dtheta_bound_covers_the_golden_section():
+    """qoc_oracle.zcal_dtheta_bound (the z-cal GPU tests' |Δθ| bar): the golden-section phase lies within half the
+    bound of the true maximiser (Newton on the analytic dJ/dθ), on random overlaps and on the zz test cases."""
+    rng = np.random.default_rng(5)
+    cases = [rng.standard_normal(4) + 1j * rng.standard_normal(4) for _ in range(200)]
+    cases = [c / np.abs(c).max() for c in cases]
+    for m in cases:
+        F, th = O.optimal_calibration(m)
+        t = th[0]
+
+        def d(t, k):  # k-th derivative of |m0 + m1 e^{it}| + |m2 + m3 e^{it}| by central differences of dJ
+            def J1(t):
+                s = 0.0
+                for a, b in ((m[0], m[1]), (m[2], m[3])):
+                    v = a + b * np.exp(1j * t)
+                    s += (np.conj(v) * 1j * b * np.exp(1j * t)).real / abs(v)
+                return s
+            return J1(t) if k == 1 else (J1(t + 1e-6) - J1(t - 1e-6)) / 2e-6
+        for _ in range(6):
+            t -= d(t, 1) / d(t, 2)
+        X = np.eye(4, dtype=complex)
+        bound = O.zcal_dtheta_bound(X, np.diag(m))
+        dd = abs((th[0] - t + np.pi) % (2 * np.pi) - np.pi)
+        assert dd <= bound / 2, (m, dd, bound)
+
+
 def test_oracle_reproduces_zz_pulse_fixture(golden_dir):
     """tests/golden/zz_pulse_fixture.npz (examples/zz_coupling_simulation.jl's forward run) is the oracle's output."""
     from qoc_amd import systems
