@@ -183,9 +183,11 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
  * use Chebyshev terms (skew-Hermitian generators, fp64; QOC_TCHAIN_POLY=taylor keeps Taylor), info[7] = state columns the kernels run on (m, or max(nc1, nc2) with qoc_set_compression), info[8] = how the
  * last backward ran (0 generic, 1 from the chains' captured products, 2 concurrent μ recurrence of qoc_eval_dev on
  * a second stream, 3 the same in one launch with the forward chain),
- * info[9] = 1 when the last forward chain wrote its captured products.  QOC_FORCE_LARGE_N=1 in the environment at qoc_create
- * selects the large-N path for any size (testing). */
-int qoc_get_info(qoc_ctx* ctx, long long* info /*[10]*/);
+ * info[9] = 1 when the last forward chain wrote its captured products, info[10] = the Taylor-action chain kernels
+ * (0 none / the fp32 VALU ones, 1 MFMA with the state in LDS, 2 MFMA with the state in registers: N <= 16, nu <= 2,
+ * QOC_TCHAIN_ROT=0 keeps 1).  QOC_FORCE_LARGE_N=1 in the environment at qoc_create selects the large-N path for
+ * any size (testing). */
+int qoc_get_info(qoc_ctx* ctx, long long* info /*[11]*/);
 
 /* How the chains x_{k+1} = U_k x_k (src/gradient_computations.jl:27-29) and λ_k = U_k^H λ_{k+1} (:52-58)
  * apply the slice exponentials:

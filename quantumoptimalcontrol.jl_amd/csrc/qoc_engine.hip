@@ -480,6 +480,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   if (getenv("QOC_BWD_PRIO")) c->bwd_prio = atoi(getenv("QOC_BWD_PRIO"));
   if (getenv("QOC_BWD_PRESTATE")) c->bwd_prestate = atoi(getenv("QOC_BWD_PRESTATE"));
   if (getenv("QOC_CONCURRENT")) c->concurrent = std::max(0, std::min(2, atoi(getenv("QOC_CONCURRENT"))));
+  if (getenv("QOC_TCHAIN_ROT")) c->tchain_rot = atoi(getenv("QOC_TCHAIN_ROT")) != 0;
   hipMemset(c->d_L, 0, (size_t)B * (Nt + 1) * Nm * c->esz);
   *out = c;
   return QOC_OK;
@@ -1243,6 +1244,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[7] = c->m;  // state columns the kernels run on (< the caller's m when compress_states packing is on)
   info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 / 3 concurrent μ recurrence
   info[9] = c->fwd_captured ? 1 : 0;
+  info[10] = c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
   return QOC_OK;
 }
 

@@ -143,6 +143,8 @@ struct qoc_ctx {
   // (μ_k, λ_k = coef ⊙ μ_k) beside the forward chain: 1 (default) both in one launch (k_tchain_mf_dual), 2 two
   // launches on two streams, 0 off (QOC_CONCURRENT)
   int concurrent = 1;
+  // N <= 16 with nu <= 2: the LDS-free MFMA chains (TChainRot, state in registers); QOC_TCHAIN_ROT=0 keeps TChainMF
+  bool tchain_rot = true;
   bool L_is_mu = false;          // d_L holds μ_k (qoc_get_costates applies the coefficients d_coef_mu)
   cx<double>* d_coef_mu = nullptr;  // B x 2m: the λ_N coefficients of the eval that left μ in d_L
   int last_eval_mode = 0;        // 0 other, 1 captured sequential backward, 2 / 3 concurrent μ mode: two streams /
@@ -241,6 +243,7 @@ hipError_t launch_terminal_cost(qoc_ctx* c);
 
 // ---- qoc_run_tchain.hip ----
 bool tchain_mf(const qoc_ctx* c);
+bool tchain_mf_rot(const qoc_ctx* c);
 template <typename T>
 int tchain_forward(qoc_ctx* c);
 // flags: TB_CAPTURE (write the backward captures), TB_MU (start from X_target: μ mode); st: nullptr = c->stream

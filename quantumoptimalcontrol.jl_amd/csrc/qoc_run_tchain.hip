@@ -66,10 +66,15 @@ bool tchain_mf(const qoc_ctx* c) {
   return c->prec == QOC_FP64 && tchain_mf_kq(c->N) > 0 && tchain_mf_waves(c->N, c->m) <= 16 &&
          tchain_mf_lds(c->N, c->m, c->nu) <= 160 * 1024;
 }
+// N <= 16 on the register-resident variant (nu <= 2): TChainRot (KQ = -4 selects it), no LDS round trip per term
+bool tchain_mf_rot(const qoc_ctx* c) {
+  return c->tchain_rot && c->N <= 16 && tchain_mf_maxt(c->N, c->m, c->nu) == 256;
+}
 template <typename F>
-hipError_t tchain_mf_dispatch(int N, F&& f) {
+hipError_t tchain_mf_dispatch(const qoc_ctx* c, F&& f) {
   using std::integral_constant;
-  switch (tchain_mf_kq(N)) {
+  if (tchain_mf_rot(c)) return f(integral_constant<int, -4>());
+  switch (tchain_mf_kq(c->N)) {
     case 3: return f(integral_constant<int, 3>());
     case 4: return f(integral_constant<int, 4>());
     case 6: return f(integral_constant<int, 6>());
@@ -78,6 +83,27 @@ hipError_t tchain_mf_dispatch(int N, F&& f) {
     case 12: return f(integral_constant<int, 12>());
   }
   return hipErrorInvalidValue;
+}
+// the chain kernels of one KQ for a launch bound (TChainRot: 256 only)
+template <int KQ>
+void (*mf_fwd_kernel(int mt, bool cheb))(TChainArgs) {
+  if constexpr (KQ < 0) {
+    return cheb ? k_tchain_mf_fwd<KQ, true, 256> : k_tchain_mf_fwd<KQ, false, 256>;
+  } else {
+    return mt == 256   ? (cheb ? k_tchain_mf_fwd<KQ, true, 256> : k_tchain_mf_fwd<KQ, false, 256>)
+           : mt == 512 ? (cheb ? k_tchain_mf_fwd<KQ, true, 512> : k_tchain_mf_fwd<KQ, false, 512>)
+                       : (cheb ? k_tchain_mf_fwd<KQ, true, 1024> : k_tchain_mf_fwd<KQ, false, 1024>);
+  }
+}
+template <int KQ>
+void (*mf_bwd_kernel(int mt, bool cheb))(TChainArgs) {
+  if constexpr (KQ < 0) {
+    return cheb ? k_tchain_mf_bwd<KQ, true, 256> : k_tchain_mf_bwd<KQ, false, 256>;
+  } else {
+    return mt == 256   ? (cheb ? k_tchain_mf_bwd<KQ, true, 256> : k_tchain_mf_bwd<KQ, false, 256>)
+           : mt == 512 ? (cheb ? k_tchain_mf_bwd<KQ, true, 512> : k_tchain_mf_bwd<KQ, false, 512>)
+                       : (cheb ? k_tchain_mf_bwd<KQ, true, 1024> : k_tchain_mf_bwd<KQ, false, 1024>);
+  }
 }
 
 bool tchain_cap_ok(const qoc_ctx* c);
@@ -131,12 +157,9 @@ int tchain_forward_chain(qoc_ctx* c) {
     const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
     const int threads = 64 * tchain_mf_waves(c->N, c->m);
     mk = mark_begin(c, 1);
-    hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
+    hipError_t e = tchain_mf_dispatch(c, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
-      const int mt = tchain_mf_maxt(c->N, c->m, c->nu);
-      auto kern = mt == 256   ? (cheb ? k_tchain_mf_fwd<KQ, true, 256> : k_tchain_mf_fwd<KQ, false, 256>)
-                  : mt == 512 ? (cheb ? k_tchain_mf_fwd<KQ, true, 512> : k_tchain_mf_fwd<KQ, false, 512>)
-                              : (cheb ? k_tchain_mf_fwd<KQ, true, 1024> : k_tchain_mf_fwd<KQ, false, 1024>);
+      auto kern = mf_fwd_kernel<KQ>(tchain_mf_maxt(c->N, c->m, c->nu), cheb);
       hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (r != hipSuccess) return r;
       hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, c->stream, g);
@@ -183,13 +206,10 @@ int tchain_backward(qoc_ctx* c, int k_lo, int k_hi, hipStream_t st, int flags) {
     const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
     const int threads = 64 * tchain_mf_waves(c->N, c->m);
     int mk = mark_begin(c, 2, st);
-    hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
+    hipError_t e = tchain_mf_dispatch(c, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
       // the (P, s, coefficients) of the forward pass are reused: the same polynomial as the states'
-      const int mt = tchain_mf_maxt(c->N, c->m, c->nu);
-      auto kern = mt == 256   ? (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 256> : k_tchain_mf_bwd<KQ, false, 256>)
-                  : mt == 512 ? (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 512> : k_tchain_mf_bwd<KQ, false, 512>)
-                              : (c->cheb_ran ? k_tchain_mf_bwd<KQ, true, 1024> : k_tchain_mf_bwd<KQ, false, 1024>);
+      auto kern = mf_bwd_kernel<KQ>(tchain_mf_maxt(c->N, c->m, c->nu), c->cheb_ran);
       hipError_t r = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (r != hipSuccess) return r;
       hipLaunchKernelGGL(kern, dim3(c->B), dim3(threads), lds, st, g);
@@ -429,7 +449,7 @@ int tchain_eval_concurrent(qoc_ctx* c, double* d_dJdu) {
     const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
     const int threads = 64 * tchain_mf_waves(c->N, c->m);
     const int mk = mark_begin(c, 1);
-    hipError_t e = tchain_mf_dispatch(c->N, [&](auto KQ_) {
+    hipError_t e = tchain_mf_dispatch(c, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
       auto kern = c->cheb_ran ? k_tchain_mf_dual<KQ, true, 256> : k_tchain_mf_dual<KQ, false, 256>;
       hipError_t q = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -742,7 +742,7 @@ __host__ __device__ inline int tchain_mf_maxt(int N, int m, int nu) {
 // its register operands from HBM once), 2 x (y, y') state buffers, 16 reduction doubles + 48 for 1/t + 64 per wave
 // (coefficients).  So two chain workgroups fit one CU's 160 KB (forward and backward side by side).
 __host__ inline size_t tchain_mf_lds(int N, int m, int nu) {
-  const int KQ = tchain_mf_kq(N), CP = (m + 1) / 2;
+  const int KQ = N <= 16 ? 4 : tchain_mf_kq(N), CP = (m + 1) / 2;  // N <= 16: room for TChainRot's 16-row state
   // register-resident variant: Ã_0, Ã_1 in registers, Ã_2 (nu = 2) in LDS
   const size_t gen = (size_t)(tchain_mf_maxt(N, m, nu) == 256 ? (nu >= 2 ? 1 : 0) : nu + 1) * N * N * 16;
   return gen + (size_t)2 * 2 * CP * 4 * KQ * 4 * 8 + (64 + 64 * tchain_mf_waves(N, m)) * 8;
@@ -989,14 +989,160 @@ struct TChainMF {
   }
 };
 
+// ---------------------------------------------------------------------------------------------------------
+// N <= 16 (one row block, the zz system): the products without LDS.  In the 4x4x4_4b layout a lane's D element
+// (row 4b + hi, column lo; hi = l >> 4, lo = l & 3) sits in the lane where block b's B operand holds k = hi of a
+// k-quad.  Rotating the state by 4j lanes inside each 16-lane DPP row (row_ror) hands block b the k-quad
+// q_j(b) = the bank that rotation brings in, and instruction j's A operand holds the matching columns 4 q_j(b) + hi
+// (arranged once per slice).  Four instructions per part (Ar, Ai) cover K = 16, so the state stays in registers
+// from one Taylor term to the next: no LDS write / read round trip and no barrier per term, the TChainMF term's
+// critical path (~750 cycles at N = 9; ~300 here).  The Ai products accumulate on their own chain and enter
+// through the n <-> n^1 swap with the column sign (y' = [-yi, yr] on the output side).  The LDS state buffers
+// still receive each substep's result (the cost epilogue and the penalty update read them).
+// KQ = 4 always (k-quads past N carry zero A columns); the launch bound and register-resident generators of
+// MAXT = 256 (nu <= 2) are required.
+// ---------------------------------------------------------------------------------------------------------
+struct TChainRot : TChainMF<4> {
+  using Base = TChainMF<4>;
+  // full-row DPP move with bound_ctrl (every lane has a source, so no old value is materialised first)
+  template <int CTRL>
+  static __device__ __forceinline__ double mv(double v) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)u, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  }
+  int qj[4];  // the k-quad rotation j brings to this lane's block
+  __device__ __forceinline__ void setup(int N, int m) {
+    Base::setup(N, m);
+    const int b = (threadIdx.x >> 2) & 3;
+    qj[0] = b;
+    qj[1] = __builtin_amdgcn_update_dpp(0, b, 0x124, 0xf, 0xf, false);  // row_ror:4
+    qj[2] = __builtin_amdgcn_update_dpp(0, b, 0x128, 0xf, 0xf, false);  // row_ror:8
+    qj[3] = __builtin_amdgcn_update_dpp(0, b, 0x12C, 0xf, 0xf, false);  // row_ror:12
+  }
+  __device__ __forceinline__ int colA(int j) const { return 4 * qj[j] + kl; }
+  template <bool HERM>
+  __device__ __forceinline__ void load_gen(int N, int nu, const cx<double>* __restrict__ At, double (&gr)[2][4],
+                                           double (&gi)[2][4]) const {
+    const int NN = N * N, rc = min(rowA, N - 1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = colA(q), cc = min(col, N - 1);
+        const bool ok = j <= nu && rowA < N && col < N;
+        const cx<double> v = At[(size_t)min(j, nu) * NN + (HERM ? cc + N * rc : rc + N * cc)];
+        gr[j][q] = ok ? v.r : 0.0;
+        gi[j][q] = ok ? (HERM ? -v.i : v.i) : 0.0;
+      }
+  }
+  template <int NUR>
+  __device__ __forceinline__ void form_regs(int N, int nu, const double (&gr)[2][4], const double (&gi)[2][4],
+                                            const cx<double>* __restrict__ g2, const double (&uk)[NUR], double scale,
+                                            double (&ar)[4], double (&ai)[4]) const {
+    static_assert(NUR >= 2, "form_regs reads u_1, u_2");
+    const double u1 = uk[0] * scale, u2 = uk[1] * scale;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ar[q] = fma(u1, gr[1][q], scale * gr[0][q]);
+      ai[q] = fma(u1, gi[1][q], scale * gi[0][q]);
+    }
+    if (nu >= 2) {
+      const int rc = min(rowA, N - 1);
+      cx<double> v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = g2[rc + N * min(colA(q), N - 1)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = rowA < N && colA(q) < N;
+        ar[q] = fma(ok ? u2 : 0.0, v[q].r, ar[q]);
+        ai[q] = fma(ok ? u2 : 0.0, v[q].i, ai[q]);
+      }
+    }
+  }
+  // D = A y with y this wave's state in the D layout (one element per lane)
+  __device__ __forceinline__ double matvec(const double (&ar)[4], const double (&ai)[4], double y) const {
+    double bv[4];
+    bv[0] = y;
+    bv[1] = mv<0x124>(y);  // row_ror:4
+    bv[2] = mv<0x128>(y);  // row_ror:8
+    bv[3] = mv<0x12C>(y);  // row_ror:12
+    double d0 = 0.0, d1 = 0.0;  // Ar and Ai products, alternating: consecutive MFMAs never depend on each other
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      d0 = MF<double>::mma4(ar[q], bv[q], d0);
+      d1 = MF<double>::mma4(ai[q], bv[q], d1);
+    }
+    const double o = mv<0xB1>(d1);  // quad_perm [1,0,3,2]: (Ai y)[n ^ 1]
+    return (n & 1) ? d0 + o : d0 - o;
+  }
+  // One slice (see TChainMF::step); the slice's start state is acc (this lane's D element).
+  template <bool CHEB, bool CAP = false>
+  __device__ __forceinline__ void step(int N, const double (&ar)[4], const double (&ai)[4], double* yb,
+                                       const double* __restrict__ invt, int& cur, int P, int s, cx<double> ph,
+                                       double& acc, double cl, double* __restrict__ cw, double& cd1,
+                                       double& cd2) const {
+    if constexpr (CHEB) {
+      cw[threadIdx.x & 63] = cl;
+      __builtin_amdgcn_wave_barrier();
+    }
+    for (int sub = 0; sub < s; ++sub) {
+      double y = actD ? acc : 0.0;
+      double ym2 = 0.0;  // y_{t-2} (Chebyshev)
+      acc = CHEB ? cw[0] * y : y;
+      for (int t = 1; t <= P; ++t) {
+        const double ct = CHEB ? cw[t] : invt[t];
+        __builtin_amdgcn_sched_barrier(0);
+        const double D = matvec(ar, ai, y);
+        if constexpr (CAP) {
+          if (sub == 0 && t <= 2) {
+            if (t == 1) cd1 = D;
+            else cd2 = D;
+          }
+        }
+        double z;
+        if constexpr (CHEB) {
+          z = t == 1 ? 0.5 * D : D + ym2;
+          ym2 = y;
+          acc += ct * z;
+        } else {
+          z = D * ct;
+          acc += z;
+        }
+        y = z;
+      }
+      if (sub == s - 1) {
+        const double o = dpp_mov<0xB1>(acc);
+        acc = (n & 1) ? ph.r * acc + ph.i * o : ph.r * acc - ph.i * o;
+      }
+      if (actD) put(ybuf(yb, CP, cur ^ 1, 0), ybuf(yb, CP, cur ^ 1, 1), acc);
+      sync();
+      cur ^= 1;
+    }
+  }
+};
+
+// the chain struct of a body instantiation: KQ < 0 selects the LDS-free TChainRot (|KQ| = 4)
+template <int KQ>
+struct TChainSel {
+  using type = TChainMF<KQ>;
+};
+template <>
+struct TChainSel<-4> {
+  using type = TChainRot;
+};
+
 // Register-resident variant (MAXT = 256, nu <= 2): the generators live in registers, not in LDS, and the first two
 // products of every slice are written to g.cap1 / g.cap2 when those are set (TChainArgs); the writes of slice k
 // are issued at the start of slice k + 1, next to the state's, ahead of the step-data prefetch.
 template <int KQ, bool CHEB, int MAXT>
 __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const int b) {
-  using C = TChainMF<KQ>;
+  using C = typename TChainSel<KQ>::type;
+  constexpr int KA = KQ < 0 ? -KQ : KQ;
   constexpr int RP = C::RP;
   constexpr bool REGS = MAXT == 256;  // generators in registers (the dispatch picks MAXT = 256 only for nu <= 2)
+  static_assert(KQ > 0 || REGS, "TChainRot needs the register-resident generators");
   constexpr int NUR = REGS ? 2 : TCHAIN_NUMAX;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, tid = threadIdx.x, nthr = blockDim.x;
@@ -1049,7 +1195,7 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
     }
   };
   __syncthreads();
-  double gr[2][KQ], gi[2][KQ];
+  double gr[2][KA], gi[2][KA];
   if constexpr (REGS) rg.template load_gen<false>(N, nu, At, gr, gi);
   double acc = rg.actD ? yb[(rg.cp * RP + rg.rowD) * 4 + rg.n] : 0.0;
   store(acc, 0);
@@ -1059,9 +1205,20 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
   int cur = 0;
   double cd1 = 0.0, cd2 = 0.0;
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
-  TPreN<NUR> nx;
-  tpre_load(stb, ub, nu, nx, ceb);
-  for (int k = 0; k < Nt; ++k) {
+  // step data of PD slices in flight: TChainRot's slices (~7 terms at N = 9, ~1 us) are shorter than a loaded HBM
+  // round trip, so one slice of prefetch left each slice waiting for the next one's records
+  constexpr int PD = KQ < 0 ? 3 : 1;
+  TPreN<NUR> nx[PD];
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int ki = min(i, Nt - 1);
+    tpre_load(stb + ki, ub + (size_t)ki * nu, nu, nx[i], CHEB ? ceb + (size_t)ki * TCHEB_STRIDE : nullptr);
+  }
+  for (int k0 = 0; k0 < Nt; k0 += PD)
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int k = k0 + i;
+    if (k >= Nt) break;
     TC_T(s0);
     // x_k (the previous slice's result) goes to HBM here, ahead of this slice's prefetch: the wait for the
     // prefetch at the end of the slice (vmcnt, in issue order) then never waits for a just-issued store
@@ -1069,11 +1226,11 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
       store(acc, k);
       cap_store(cd1, cd2, k - 1);
     }
-    const TPreN<NUR> st = nx;
-    const int kn = min(k + 1, Nt - 1);
-    tpre_load(stb + kn, ub + (size_t)kn * nu, nu, nx, CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
+    const TPreN<NUR> st = nx[i];
+    const int kn = min(k + PD, Nt - 1);
+    tpre_load(stb + kn, ub + (size_t)kn * nu, nu, nx[i], CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
-    double ar[KQ], ai[KQ];
+    double ar[KA], ai[KA];
     if constexpr (REGS) rg.form_regs(N, nu, gr, gi, gen, st.u, st.scale, ar, ai);
     else rg.form(N, nu, gen, st.u, st.scale, ar, ai);
     TC_T(s1);
@@ -1105,9 +1262,11 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
 
 template <int KQ, bool CHEB, int MAXT>
 __device__ __forceinline__ void tchain_mf_bwd_body(const TChainArgs& g, const int b) {
-  using C = TChainMF<KQ>;
+  using C = typename TChainSel<KQ>::type;
+  constexpr int KA = KQ < 0 ? -KQ : KQ;
   constexpr int RP = C::RP;
   constexpr bool REGS = MAXT == 256;  // see k_tchain_mf_fwd
+  static_assert(KQ > 0 || REGS, "TChainRot needs the register-resident generators");
   constexpr int NUR = REGS ? 2 : TCHAIN_NUMAX;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, tid = threadIdx.x, nthr = blockDim.x;
@@ -1184,28 +1343,37 @@ __device__ __forceinline__ void tchain_mf_bwd_body(const TChainArgs& g, const in
     }
   };
   __syncthreads();
-  double gr[2][KQ], gi[2][KQ];
+  double gr[2][KA], gi[2][KA];
   if constexpr (REGS) rg.template load_gen<true>(N, nu, At, gr, gi);
   int cur = 0;
-  double acc = 0.0, cd1 = 0.0, cd2 = 0.0;
+  double acc = rg.actD ? yb[(rg.cp * RP + rg.rowD) * 4 + rg.n] : 0.0;  // λ at k_hi (TChainRot starts from acc)
+  double cd1 = 0.0, cd2 = 0.0;
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
-  TPreN<NUR> nx;
-  tpre_load(stb + k_hi - 1, ub + (size_t)(k_hi - 1) * nu, nu, nx,
-            CHEB ? ceb + (size_t)(k_hi - 1) * TCHEB_STRIDE : nullptr);
-  for (int k = k_hi - 1; k >= k_lo; --k) {
+  constexpr int PD = KQ < 0 ? 3 : 1;  // slices of step data in flight (see tchain_mf_fwd_body)
+  TPreN<NUR> nx[PD];
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int ki = max(k_hi - 1 - i, 0);
+    tpre_load(stb + ki, ub + (size_t)ki * nu, nu, nx[i], CHEB ? ceb + (size_t)ki * TCHEB_STRIDE : nullptr);
+  }
+  for (int k0 = k_hi - 1; k0 >= k_lo; k0 -= PD)
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int k = k0 - i;
+    if (k < k_lo) break;
     // λ_{k+1} (the previous slice's result) to HBM ahead of this slice's loads (see k_tchain_mf_fwd)
     if (k < k_hi - 1) {
       if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)(k + 1) * Nm + own)[rg.n & 1] = acc;
       cap_store(cd1, cd2, k + 1);
     }
-    const TPreN<NUR> st = nx;
-    const int kp = max(k - 1, 0);
-    tpre_load(stb + kp, ub + (size_t)kp * nu, nu, nx, CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
+    const TPreN<NUR> st = nx[i];
+    const int kp = max(k - PD, 0);
+    tpre_load(stb + kp, ub + (size_t)kp * nu, nu, nx[i], CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     const size_t ok_ = (size_t)k * Nm + own;
     double xk = pen_m ? tmu * reinterpret_cast<const double*>(Xb + ok_)[rg.n & 1] : 0.0;
     if (srcb && rg.actD) xk += reinterpret_cast<const double*>(srcb + ok_)[rg.n & 1];
-    double ar[KQ], ai[KQ];
+    double ar[KA], ai[KA];
     if constexpr (REGS) rg.form_regs(N, nu, gr, gi, gen, st.u, st.scale, ar, ai);
     else rg.form(N, nu, gen, st.u, st.scale, ar, ai);
     rg.template step<CHEB, REGS>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, -st.pi}, acc, st.cl, cw, cd1, cd2);

@@ -310,7 +310,7 @@ class GrapeEngine:
 
     def info(self) -> dict:
         """Which pipeline the context runs (qoc_get_info): 'lds' kernels or the 'large_n' GEMM path."""
-        v = np.zeros(10, dtype=np.int64)
+        v = np.zeros(11, dtype=np.int64)
         self._chk(self._lib.qoc_get_info(self._h, v.ctypes.data_as(C.POINTER(C.c_longlong))))
         return {"path": "large_n" if v[0] else "lds", "chunk": int(v[1]), "ns_iters": int(v[2]),
                 "device_bytes": int(v[3]), "chain": "taylor" if v[4] == 1 else "propagators",
@@ -318,7 +318,8 @@ class GrapeEngine:
                 "chain_poly": "chebyshev" if v[6] else "taylor", "kernel_m": int(v[7]),
                 "backward": {0: "generic", 1: "captured", 2: "concurrent", 3: "concurrent"}.get(int(v[8]), "?"),
                 "concurrent_launch": {2: "two_streams", 3: "dual"}.get(int(v[8])),
-                "fwd_captured": bool(v[9])}
+                "fwd_captured": bool(v[9]),
+                "chain_kernel": {0: None, 1: "mfma_lds", 2: "mfma_regs"}.get(int(v[10]))}
 
     def set_chain(self, mode: str = "auto"):
         """How the chains apply exp(A_k) (include/qoc.h qoc_set_chain): 'propagators' forms every U_k (the

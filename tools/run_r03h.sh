@@ -1,0 +1,9 @@
+#!/bin/bash
+# Register-resident chains (TChainRot): parity tests, then zz / tunable-bus benches.
+set -o pipefail
+mkdir -p gpurun_out
+T=${1:-r03h}
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_rot.py tests/test_gpu_concurrent.py > gpurun_out/${T}_test.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --config zz_batch --no-cpu > gpurun_out/${T}_zz.json 2>gpurun_out/${T}_zz.err || exit 1
+QOC_TCHAIN_ROT=0 timeout -k 10 300 python bench.py --config zz_batch --no-cpu > gpurun_out/${T}_zz_lds.json 2>/dev/null || exit 1
+echo done
