@@ -403,6 +403,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
       {(void**)&c->d_dJdu, (size_t)B * nu * Nt * sizeof(double)},
       {(void**)&c->d_flag, sizeof(int)},
       {(void**)&c->d_hist, 13 * 64 * sizeof(unsigned long long)},
+      {(void**)&c->d_sink, TCHAIN_SINK * sizeof(double)},
       {(void**)&c->d_ps, ((size_t)std::max<long long>((long long)B * Nt, 16384) + 1) * sizeof(int)},
   };
   for (auto& a : allocs) {
@@ -480,7 +481,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
   if (getenv("QOC_BWD_PRIO")) c->bwd_prio = atoi(getenv("QOC_BWD_PRIO"));
   if (getenv("QOC_BWD_PRESTATE")) c->bwd_prestate = atoi(getenv("QOC_BWD_PRESTATE"));
   if (getenv("QOC_CONCURRENT")) c->concurrent = std::max(0, std::min(2, atoi(getenv("QOC_CONCURRENT"))));
-  if (getenv("QOC_TCHAIN_ROT")) c->tchain_rot = atoi(getenv("QOC_TCHAIN_ROT")) != 0;
+  if (getenv("QOC_TCHAIN_ROT")) c->tchain_rot = atoi(getenv("QOC_TCHAIN_ROT"));
   hipMemset(c->d_L, 0, (size_t)B * (Nt + 1) * Nm * c->esz);
   *out = c;
   return QOC_OK;
@@ -495,7 +496,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->d_tcoef) hipFree(c->d_tcoef);
   if (c->d_coef_mu) hipFree(c->d_coef_mu);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
-                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_pws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec};
+                  c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_pws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec, c->d_sink};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (auto& m : c->marks) {

@@ -58,6 +58,7 @@ struct qoc_ctx {
   cx<double>* d_coef = nullptr;  // B*m
   double* d_dJdu = nullptr;  // B*nu*Nt
   int* d_flag = nullptr;
+  double* d_sink = nullptr;  // TCHAIN_SINK doubles: the MFMA chains' branch-free stores of lanes without an element
   unsigned long long* d_hist = nullptr;  // 5*64 reference (Padé) selection + 8*64 executed Taylor (r, s) / T12 s
   int chain_cb_fwd = 0, chain_cb_bwd = 0;  // 0: chain_shape's column block; QOC_CHAIN_CB_FWD / _BWD = 1 | 2 (N > 32)
   int expm_alg = 1;  // 1 Taylor: register-resident T12 (default), 2 LDS Paterson-Stockmeyer (QOC_EXPM_LDS=1), 0 Padé (QOC_EXPM_PADE=1)
@@ -143,8 +144,9 @@ struct qoc_ctx {
   // (μ_k, λ_k = coef ⊙ μ_k) beside the forward chain: 1 (default) both in one launch (k_tchain_mf_dual), 2 two
   // launches on two streams, 0 off (QOC_CONCURRENT)
   int concurrent = 1;
-  // N <= 16 with nu <= 2: the LDS-free MFMA chains (TChainRot, state in registers); QOC_TCHAIN_ROT=0 keeps TChainMF
-  bool tchain_rot = true;
+  // the MFMA chains with the state in registers (TChainRot): 1 (default) for N <= 32 with nu <= 2, 3 also for
+  // N <= 48 (generators in LDS), 0 off: TChainMF everywhere (QOC_TCHAIN_ROT)
+  int tchain_rot = 1;
   bool L_is_mu = false;          // d_L holds μ_k (qoc_get_costates applies the coefficients d_coef_mu)
   cx<double>* d_coef_mu = nullptr;  // B x 2m: the λ_N coefficients of the eval that left μ in d_L
   int last_eval_mode = 0;        // 0 other, 1 captured sequential backward, 2 / 3 concurrent μ mode: two streams /

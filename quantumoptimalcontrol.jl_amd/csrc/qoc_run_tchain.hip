@@ -44,6 +44,7 @@ TChainArgs tchain_args(qoc_ctx* c) {
   g.steps = c->d_steps;
   g.x0 = c->d_x0;
   g.x0_per_seed = c->x0_per_seed;
+  g.sink = c->d_sink;
   g.X = c->d_X;
   g.L = c->d_L;
   g.Xt = c->d_Xt;
@@ -66,14 +67,24 @@ bool tchain_mf(const qoc_ctx* c) {
   return c->prec == QOC_FP64 && tchain_mf_kq(c->N) > 0 && tchain_mf_waves(c->N, c->m) <= 16 &&
          tchain_mf_lds(c->N, c->m, c->nu) <= 160 * 1024;
 }
-// N <= 16 on the register-resident variant (nu <= 2): TChainRot (KQ = -4 selects it), no LDS round trip per term
+// TChainRot<G> (KQ = -4 / -8 / -12 select G = 1 / 2 / 3): one wave per column pair with the state in registers, no
+// LDS round trip per term.  m <= 8; G <= 2 (N <= 32) with nu <= 2 by default (generators in registers); G = 3
+// (N <= 48, generators in LDS) with QOC_TCHAIN_ROT=3
 bool tchain_mf_rot(const qoc_ctx* c) {
-  return c->tchain_rot && c->N <= 16 && tchain_mf_maxt(c->N, c->m, c->nu) == 256;
+  if (!c->tchain_rot || !tchain_mf(c) || (c->m + 1) / 2 > 4) return false;
+  if (c->N <= 32) return c->nu <= 2;
+  return c->tchain_rot >= 3 && c->N <= 48 && tchain_mf_lds(c->N, c->m, c->nu, true) <= 160 * 1024;
+}
+int tchain_mf_threads(const qoc_ctx* c) {
+  return 64 * (tchain_mf_rot(c) ? (c->m + 1) / 2 : tchain_mf_waves(c->N, c->m));
 }
 template <typename F>
 hipError_t tchain_mf_dispatch(const qoc_ctx* c, F&& f) {
   using std::integral_constant;
-  if (tchain_mf_rot(c)) return f(integral_constant<int, -4>());
+  if (tchain_mf_rot(c))
+    return c->N <= 16 ? f(integral_constant<int, -4>())
+           : c->N <= 32 ? f(integral_constant<int, -8>())
+                        : f(integral_constant<int, -12>());
   switch (tchain_mf_kq(c->N)) {
     case 3: return f(integral_constant<int, 3>());
     case 4: return f(integral_constant<int, 4>());
@@ -154,8 +165,8 @@ int tchain_forward_chain(qoc_ctx* c) {
     c->fwd_captured = true;
   }
   if (tchain_mf(c)) {
-    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
-    const int threads = 64 * tchain_mf_waves(c->N, c->m);
+    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu, tchain_mf_rot(c));
+    const int threads = tchain_mf_threads(c);
     mk = mark_begin(c, 1);
     hipError_t e = tchain_mf_dispatch(c, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
@@ -203,8 +214,8 @@ int tchain_backward(qoc_ctx* c, int k_lo, int k_hi, hipStream_t st, int flags) {
       g.cap2 = (cx<double>*)c->d_gws + bufN;
     }
     g.mu_mode = (flags & TB_MU) ? 1 : 0;
-    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
-    const int threads = 64 * tchain_mf_waves(c->N, c->m);
+    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu, tchain_mf_rot(c));
+    const int threads = tchain_mf_threads(c);
     int mk = mark_begin(c, 2, st);
     hipError_t e = tchain_mf_dispatch(c, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;
@@ -329,7 +340,8 @@ hipError_t launch_pade_units(qoc_ctx* c, long long units) {
 // The register-resident MFMA chains (MAXT = 256) can write their first two products per slice; with the fused
 // order-3 gradient they then replace its generator products (k_grad_rr_c).
 bool tchain_cap_ok(const qoc_ctx* c) {
-  return c->cap_ok && tchain_mf(c) && tchain_mf_maxt(c->N, c->m, c->nu) == 256 && c->grad_rr && c->nu <= 2;
+  return c->cap_ok && tchain_mf(c) && (tchain_mf_rot(c) || tchain_mf_maxt(c->N, c->m, c->nu) == 256) && c->grad_rr &&
+         c->nu <= 2;
 }
 
 // d_pws: the forward captures (two state-shaped buffers), grown on first use; QOC_ERR_HIP if it cannot be had
@@ -446,8 +458,8 @@ int tchain_eval_concurrent(qoc_ctx* c, double* d_dJdu) {
     gb.cap1 = c->d_gws;
     gb.cap2 = (cx<double>*)c->d_gws + bufN;
     gb.mu_mode = 1;
-    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu);
-    const int threads = 64 * tchain_mf_waves(c->N, c->m);
+    const size_t lds = tchain_mf_lds(c->N, c->m, c->nu, tchain_mf_rot(c));
+    const int threads = tchain_mf_threads(c);
     const int mk = mark_begin(c, 1);
     hipError_t e = tchain_mf_dispatch(c, [&](auto KQ_) {
       constexpr int KQ = decltype(KQ_)::value;

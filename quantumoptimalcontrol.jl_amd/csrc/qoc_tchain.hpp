@@ -76,7 +76,12 @@ struct TPreN {
   double u[NUR];
 };
 using TPre = TPreN<TCHAIN_NUMAX>;
-template <int NUR>
+// CL: load the Chebyshev coefficient (ce valid) — a compile-time choice, so that the loads are the same on every
+// path (a load skipped at run time leaves the waitcnt pass unsure of the count in flight; see TChainArgs::sink)
+// ZERO: u[j >= nu] = 0 (the VALU chains read every slot).  The MFMA chains never read u[j >= nu] and pass false:
+// the select needs the loaded value, and the compiler put it (with its vmcnt wait for the just-issued prefetch)
+// at the loop latch.
+template <int NUR, bool CL = false, bool ZERO = true>
 __device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const double* __restrict__ uk, int nu,
                                           TPreN<NUR>& d, const double* __restrict__ ce = nullptr) {
   int z;
@@ -88,11 +93,12 @@ __device__ __forceinline__ void tpre_load(const TStep* __restrict__ st, const do
   d.P = (int)(ps & 0xffffffff);
   d.s = (int)(ps >> 32);
   d.scale = v.w;
-  d.cl = ce ? ce[threadIdx.x & 63] : 0.0;
+  if constexpr (CL) d.cl = ce[(threadIdx.x & 63) + z];
+  else d.cl = ce ? ce[threadIdx.x & 63] : 0.0;
 #pragma unroll
   for (int j = 0; j < NUR; ++j) {  // clamped, unconditional loads: no branches around them
     const double v = uk[min(j, nu - 1) + z];
-    d.u[j] = j < nu ? v : 0.0;
+    d.u[j] = !ZERO || j < nu ? v : 0.0;
   }
 }
 
@@ -341,7 +347,16 @@ struct TChainArgs {
   void* cap2;
   int mu_mode;             // backward: μ_k = U_k^H .. U_{Nt-1}^H X_target (λ_k = coef ⊙ μ_k for the built-in costs),
                            // started from X_target alone: it needs no forward result and can run beside it
+  // TCHAIN_SINK doubles that the MFMA chains' lanes without a state element store to, so that the per-slice stores
+  // need no branch: with a skipped store on one path the waitcnt pass no longer knows how many memory operations
+  // are in flight and waits for all of them (the just-issued stores and prefetches included) before the next use
+  // of the step data, an HBM round trip per slice (measured: 550 cycles at N = 9, 1650 at N = 27)
+  double* sink;
 };
+constexpr int TCHAIN_SINK = 1 << 16;
+__device__ __forceinline__ double* tchain_sink(const TChainArgs& g) {
+  return g.sink + 2 * (((size_t)blockIdx.x * blockDim.x + threadIdx.x) & (TCHAIN_SINK / 2 - 1));
+}
 
 // Thread layout of the Taylor-action chains.  Waves split the rows into G blocks of R = 64 / S rows and the
 // columns into CGN groups (G = 1: 4 groups, G = 2: 2, else 1); each computing wave walks its columns in
@@ -741,16 +756,25 @@ __host__ __device__ inline int tchain_mf_maxt(int N, int m, int nu) {
 // LDS of the MFMA chains: the generators (the register-resident variant, MAXT = 256, keeps only Ã_2 there and reads
 // its register operands from HBM once), 2 x (y, y') state buffers, 16 reduction doubles + 48 for 1/t + 64 per wave
 // (coefficients).  So two chain workgroups fit one CU's 160 KB (forward and backward side by side).
-__host__ inline size_t tchain_mf_lds(int N, int m, int nu) {
-  const int KQ = N <= 16 ? 4 : tchain_mf_kq(N), CP = (m + 1) / 2;  // N <= 16: room for TChainRot's 16-row state
+// rot: the TChainRot kernels (16 G-row state, one wave per column pair; G = 3 keeps every generator in LDS).
+__host__ inline size_t tchain_mf_lds(int N, int m, int nu, bool rot = false) {
+  const int G = (N + 15) / 16, CP = (m + 1) / 2;
+  const int KQ = rot ? 4 * G : tchain_mf_kq(N);
+  const bool regs = rot ? G <= 2 : tchain_mf_maxt(N, m, nu) == 256;
   // register-resident variant: Ã_0, Ã_1 in registers, Ã_2 (nu = 2) in LDS
-  const size_t gen = (size_t)(tchain_mf_maxt(N, m, nu) == 256 ? (nu >= 2 ? 1 : 0) : nu + 1) * N * N * 16;
-  return gen + (size_t)2 * 2 * CP * 4 * KQ * 4 * 8 + (64 + 64 * tchain_mf_waves(N, m)) * 8;
+  const size_t gen = (size_t)(regs ? (nu >= 2 ? 1 : 0) : nu + 1) * N * N * 16;
+  return gen + (size_t)2 * 2 * CP * 4 * KQ * 4 * 8 + (64 + 64 * (rot ? CP : tchain_mf_waves(N, m))) * 8;
 }
 
 template <int KQ>
 struct TChainMF {
   static constexpr int RP = 4 * KQ;  // padded rows of the LDS state
+  static constexpr int E = 1;        // D elements per lane (TChainRot<2>: 2)
+  static constexpr int KA = KQ;      // A-operand registers per generator part
+  static constexpr int PD = KQ <= 10 ? 2 : 1;  // slices of step data in flight (tchain_mf_fwd_body; KQ = 12 would
+                                              // pass 256 VGPRs with a second record)
+  static constexpr bool REGS_OK = true;
+  static constexpr int NG = 2;  // generators with register-resident A operands (Ã_0, Ã_1; Ã_2 from LDS)
   int rowA, rowD, n, kl, cp, G, CP;
   bool solo;  // one row block (N <= 16): each wave owns its column pair outright, no workgroup barriers
   bool actD;  // this lane's D element is a real state entry (row < N, column < m)
@@ -770,6 +794,11 @@ struct TChainMF {
     n = l & 3;
     colD = 2 * cp + (n >> 1);
     actD = rowD < N && colD < m;
+  }
+  __device__ __forceinline__ int rowE(int) const { return rowD; }
+  __device__ __forceinline__ bool actE(int) const { return actD; }
+  __device__ __forceinline__ void put_e(double* yb, int buf, int, double v) const {
+    put(ybuf(yb, CP, buf, 0), ybuf(yb, CP, buf, 1), v);
   }
   // LDS state: [buf][y | y'][cp][RP rows][4]
   static __device__ __forceinline__ double* ybuf(double* yb, int CP, int buf, int prime) {
@@ -932,8 +961,9 @@ struct TChainMF {
   template <bool CHEB, bool CAP = false>
   __device__ __forceinline__ void step(int N, const double (&ar)[KQ], const double (&ai)[KQ], double* yb,
                                        const double* __restrict__ invt, int& cur, int P, int s, cx<double> ph,
-                                       double& acc, double cl, double* __restrict__ cw, double& cd1,
-                                       double& cd2) const {
+                                       double (&acc_)[1], double cl, double* __restrict__ cw, double (&cd1_)[1],
+                                       double (&cd2_)[1]) const {
+    double &acc = acc_[0], &cd1 = cd1_[0], &cd2 = cd2_[0];
     if constexpr (CHEB) {  // this step's coefficients -> the wave's own LDS slot (in-order LDS: no barrier)
       cw[threadIdx.x & 63] = cl;
       __builtin_amdgcn_wave_barrier();
@@ -990,147 +1020,368 @@ struct TChainMF {
 };
 
 // ---------------------------------------------------------------------------------------------------------
-// N <= 16 (one row block, the zz system): the products without LDS.  In the 4x4x4_4b layout a lane's D element
-// (row 4b + hi, column lo; hi = l >> 4, lo = l & 3) sits in the lane where block b's B operand holds k = hi of a
+// N <= 32 (G = 1 or 2 row groups of 16, the zz and tunable-bus systems): the products without LDS.  One wave per
+// column pair owns the whole state, G elements per lane.  In the 4x4x4_4b layout a lane's D element (row
+// 16g + 4b + hi, column lo; hi = l >> 4, lo = l & 3) sits in the lane where block b's B operand holds k = hi of a
 // k-quad.  Rotating the state by 4j lanes inside each 16-lane DPP row (row_ror) hands block b the k-quad
-// q_j(b) = the bank that rotation brings in, and instruction j's A operand holds the matching columns 4 q_j(b) + hi
-// (arranged once per slice).  Four instructions per part (Ar, Ai) cover K = 16, so the state stays in registers
-// from one Taylor term to the next: no LDS write / read round trip and no barrier per term, the TChainMF term's
-// critical path (~750 cycles at N = 9; ~300 here).  The Ai products accumulate on their own chain and enter
-// through the n <-> n^1 swap with the column sign (y' = [-yi, yr] on the output side).  The LDS state buffers
-// still receive each substep's result (the cost epilogue and the penalty update read them).
-// KQ = 4 always (k-quads past N carry zero A columns); the launch bound and register-resident generators of
-// MAXT = 256 (nu <= 2) are required.
+// q_j(b) = the bank that rotation brings in, and instruction (g_out, g_in, j)'s A operand holds the matching
+// entries Ã[16 g_out + 4b + lo][16 g_in + 4 q_j(b) + hi] (arranged once per slice).  4 G^2 instructions per part
+// (Ar, Ai) cover K = 16 G, so the state stays in registers from one Taylor term to the next: no LDS write / read
+// round trip and no barrier per term (the TChainMF term's critical path: ~750 cycles at N = 9), and for G = 2 one
+// wave instead of two per column pair (no cross-wave exchange).  The Ai products accumulate on their own chains
+// and enter through the n <-> n^1 swap with the column sign (y' = [-yi, yr] on the output side).  The LDS state
+// buffers still receive each substep's result (the cost epilogue and the penalty update read them).  Needs the
+// register-resident generators of MAXT = 256 (nu <= 2): 2 x 4G^2 complex A-operand registers per generator.
 // ---------------------------------------------------------------------------------------------------------
-struct TChainRot : TChainMF<4> {
-  using Base = TChainMF<4>;
-  // full-row DPP move with bound_ctrl (every lane has a source, so no old value is materialised first)
-  template <int CTRL>
-  static __device__ __forceinline__ double mv(double v) {
-    const long long u = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)u, CTRL, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xf, 0xf, true);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-  }
+template <int G>
+struct TChainRot {
+  static constexpr int RP = 16 * G;     // padded rows of the LDS state
+  static constexpr int E = G;           // D elements per lane
+  static constexpr int KA = 4 * G * G;  // A-operand registers per generator part: [g_out][g_in][j]
+  static constexpr int PD = G == 1 ? 3 : 2;  // step records in flight (PD - 1 slices of latency hidden): G = 1
+                                             // slices (~7 terms at N = 9, ~1 us) are shorter than a loaded HBM
+                                             // round trip
+  // G <= 2: the generators' A-operand entries live in registers (MAXT = 256, nu <= 2); G = 3 (N <= 48): 2 x 36
+  // complex per generator would not fit beside the 36 formed ones, so all nu + 1 generators stay in LDS and
+  // form() reads each slice's entries there
+  static constexpr bool REGS_OK = G <= 2;
+  static constexpr int NG = G == 1 ? 3 : 2;  // register-resident generators: G = 1 keeps Ã_2 there too (4 entries)
+  int n, kl, cp, CP, b4, lo, colD;
+  bool solo = true;
   int qj[4];  // the k-quad rotation j brings to this lane's block
+  bool act[G];
   __device__ __forceinline__ void setup(int N, int m) {
-    Base::setup(N, m);
-    const int b = (threadIdx.x >> 2) & 3;
+    const int l = threadIdx.x & 63;
+    cp = threadIdx.x >> 6;
+    CP = (m + 1) / 2;
+    const int b = (l >> 2) & 3;
+    b4 = 4 * b;
+    kl = l >> 4;
+    lo = l & 3;
+    n = lo;
+    colD = 2 * cp + (n >> 1);
+#pragma unroll
+    for (int e = 0; e < G; ++e) act[e] = rowE(e) < N && colD < m;
     qj[0] = b;
     qj[1] = __builtin_amdgcn_update_dpp(0, b, 0x124, 0xf, 0xf, false);  // row_ror:4
     qj[2] = __builtin_amdgcn_update_dpp(0, b, 0x128, 0xf, 0xf, false);  // row_ror:8
     qj[3] = __builtin_amdgcn_update_dpp(0, b, 0x12C, 0xf, 0xf, false);  // row_ror:12
   }
-  __device__ __forceinline__ int colA(int j) const { return 4 * qj[j] + kl; }
+  __device__ __forceinline__ int rowE(int e) const { return 16 * e + b4 + kl; }  // D element e's row
+  __device__ __forceinline__ bool actE(int e) const { return act[e]; }
+  __device__ __forceinline__ int rowA(int go) const { return 16 * go + b4 + lo; }
+  __device__ __forceinline__ int colA(int gi, int j) const { return 16 * gi + 4 * qj[j] + kl; }
+  static __device__ __forceinline__ double* ybuf(double* yb, int CP, int buf, int prime) {
+    return yb + (size_t)((buf * 2 + prime) * CP) * RP * 4;
+  }
+  // full-row DPP move with bound_ctrl (every lane has a source, so no old value is materialised first)
+  template <int CTRL>
+  static __device__ __forceinline__ double mv(double v) {
+    const long long u = __double_as_longlong(v);
+    const int lo_ = __builtin_amdgcn_update_dpp(0, (int)u, CTRL, 0xf, 0xf, true);
+    const int hi_ = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi_ << 32) | (unsigned)lo_);
+  }
   template <bool HERM>
-  __device__ __forceinline__ void load_gen(int N, int nu, const cx<double>* __restrict__ At, double (&gr)[2][4],
-                                           double (&gi)[2][4]) const {
-    const int NN = N * N, rc = min(rowA, N - 1);
+  __device__ __forceinline__ void load_gen(int N, int nu, const cx<double>* __restrict__ At, double (&gr)[NG][KA],
+                                           double (&gi)[NG][KA]) const {
+    const int NN = N * N;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NG; ++j)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int col = colA(q), cc = min(col, N - 1);
-        const bool ok = j <= nu && rowA < N && col < N;
+      for (int x = 0; x < KA; ++x) {
+        const int row = rowA(x / (4 * G)), col = colA((x / 4) % G, x % 4);
+        const int rc = min(row, N - 1), cc = min(col, N - 1);
+        const bool ok = j <= nu && row < N && col < N;
         const cx<double> v = At[(size_t)min(j, nu) * NN + (HERM ? cc + N * rc : rc + N * cc)];
-        gr[j][q] = ok ? v.r : 0.0;
-        gi[j][q] = ok ? (HERM ? -v.i : v.i) : 0.0;
+        gr[j][x] = ok ? v.r : 0.0;
+        gi[j][x] = ok ? (HERM ? -v.i : v.i) : 0.0;
       }
   }
   template <int NUR>
-  __device__ __forceinline__ void form_regs(int N, int nu, const double (&gr)[2][4], const double (&gi)[2][4],
+  __device__ __forceinline__ void form_regs(int N, int nu, const double (&gr)[NG][KA], const double (&gi)[NG][KA],
                                             const cx<double>* __restrict__ g2, const double (&uk)[NUR], double scale,
-                                            double (&ar)[4], double (&ai)[4]) const {
+                                            double (&ar)[KA], double (&ai)[KA]) const {
     static_assert(NUR >= 2, "form_regs reads u_1, u_2");
-    const double u1 = uk[0] * scale, u2 = uk[1] * scale;
+    const double u1 = uk[0] * scale, u2 = nu >= 2 ? uk[1] * scale : 0.0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      ar[q] = fma(u1, gr[1][q], scale * gr[0][q]);
-      ai[q] = fma(u1, gi[1][q], scale * gi[0][q]);
+    for (int x = 0; x < KA; ++x) {
+      ar[x] = fma(u1, gr[1][x], scale * gr[0][x]);
+      ai[x] = fma(u1, gi[1][x], scale * gi[0][x]);
     }
-    if (nu >= 2) {
-      const int rc = min(rowA, N - 1);
-      cx<double> v[4];
+    if constexpr (NG == 3) {  // Ã_2 in registers too (zero when nu < 2)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = g2[rc + N * min(colA(q), N - 1)];
+      for (int x = 0; x < KA; ++x) {
+        ar[x] = fma(u2, gr[2][x], ar[x]);
+        ai[x] = fma(u2, gi[2][x], ai[x]);
+      }
+    } else if (nu >= 2) {
+      cx<double> v[KA];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool ok = rowA < N && colA(q) < N;
-        ar[q] = fma(ok ? u2 : 0.0, v[q].r, ar[q]);
-        ai[q] = fma(ok ? u2 : 0.0, v[q].i, ai[q]);
+      for (int x = 0; x < KA; ++x) {
+        const int row = rowA(x / (4 * G)), col = colA((x / 4) % G, x % 4);
+        v[x] = g2[min(row, N - 1) + N * min(col, N - 1)];
+      }
+#pragma unroll
+      for (int x = 0; x < KA; ++x) {
+        const int row = rowA(x / (4 * G)), col = colA((x / 4) % G, x % 4);
+        const bool ok = row < N && col < N;
+        ar[x] = fma(ok ? u2 : 0.0, v[x].r, ar[x]);
+        ai[x] = fma(ok ? u2 : 0.0, v[x].i, ai[x]);
       }
     }
   }
-  // D = A y with y this wave's state in the D layout (one element per lane)
-  __device__ __forceinline__ double matvec(const double (&ar)[4], const double (&ai)[4], double y) const {
-    double bv[4];
-    bv[0] = y;
-    bv[1] = mv<0x124>(y);  // row_ror:4
-    bv[2] = mv<0x128>(y);  // row_ror:8
-    bv[3] = mv<0x12C>(y);  // row_ror:12
-    double d0 = 0.0, d1 = 0.0;  // Ar and Ai products, alternating: consecutive MFMAs never depend on each other
+  // from the LDS generators (column-major; the backward kernels keep the conjugate transposes there)
+  template <int NUR>
+  __device__ __forceinline__ void form(int N, int nu, const cx<double>* __restrict__ gen, const double (&uk)[NUR],
+                                       double scale, double (&ar)[KA], double (&ai)[KA]) const {
+    const int NN = N * N;
+    // the lane roles from an opaque lane index: left loop-invariant, the compiler hoists every entry's LDS offset
+    // and validity out of the slice loop and runs out of registers (G = 3: 512 VGPRs and scratch)
+    int l = threadIdx.x & 63;
+    asm volatile("" : "+v"(l));
+    const int bq = (l >> 2) & 3, lq = l & 3, kq = l >> 4;
+    const int q[4] = {bq, __builtin_amdgcn_update_dpp(0, bq, 0x124, 0xf, 0xf, false),
+                      __builtin_amdgcn_update_dpp(0, bq, 0x128, 0xf, 0xf, false),
+                      __builtin_amdgcn_update_dpp(0, bq, 0x12C, 0xf, 0xf, false)};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      d0 = MF<double>::mma4(ar[q], bv[q], d0);
-      d1 = MF<double>::mma4(ai[q], bv[q], d1);
-    }
-    const double o = mv<0xB1>(d1);  // quad_perm [1,0,3,2]: (Ai y)[n ^ 1]
-    return (n & 1) ? d0 + o : d0 - o;
-  }
-  // One slice (see TChainMF::step); the slice's start state is acc (this lane's D element).
-  template <bool CHEB, bool CAP = false>
-  __device__ __forceinline__ void step(int N, const double (&ar)[4], const double (&ai)[4], double* yb,
-                                       const double* __restrict__ invt, int& cur, int P, int s, cx<double> ph,
-                                       double& acc, double cl, double* __restrict__ cw, double& cd1,
-                                       double& cd2) const {
-    if constexpr (CHEB) {
-      cw[threadIdx.x & 63] = cl;
-      __builtin_amdgcn_wave_barrier();
-    }
-    for (int sub = 0; sub < s; ++sub) {
-      double y = actD ? acc : 0.0;
-      double ym2 = 0.0;  // y_{t-2} (Chebyshev)
-      acc = CHEB ? cw[0] * y : y;
-      for (int t = 1; t <= P; ++t) {
-        const double ct = CHEB ? cw[t] : invt[t];
+    for (int go = 0; go < G; ++go) {  // one output group (4G entries) at a time: bounded transient registers
+      constexpr int W = 4 * G;
+      const int row = 16 * go + 4 * bq + lq, rc = min(row, N - 1);
+      int off[W];
+      bool ok[W];
+#pragma unroll
+      for (int y = 0; y < W; ++y) {
+        const int col = 16 * (y / 4) + 4 * q[y % 4] + kq;
+        off[y] = rc + N * min(col, N - 1);
+        ok[y] = row < N && col < N;
+      }
+      cx<double> v[W];
+#pragma unroll
+      for (int y = 0; y < W; ++y) v[y] = gen[off[y]];
+#pragma unroll
+      for (int y = 0; y < W; ++y) {
+        ar[go * W + y] = v[y].r;
+        ai[go * W + y] = v[y].i;
+      }
+#pragma unroll
+      for (int j = 0; j < NUR; ++j) {
+        if (j >= nu) break;
+        const double uj = uk[j];
+        const cx<double>* Gj = gen + (size_t)(j + 1) * NN;
+#pragma unroll
+        for (int y = 0; y < W; ++y) v[y] = Gj[off[y]];
         __builtin_amdgcn_sched_barrier(0);
-        const double D = matvec(ar, ai, y);
+#pragma unroll
+        for (int y = 0; y < W; ++y) {
+          ar[go * W + y] = fma(uj, v[y].r, ar[go * W + y]);
+          ai[go * W + y] = fma(uj, v[y].i, ai[go * W + y]);
+        }
+      }
+#pragma unroll
+      for (int y = 0; y < W; ++y) {
+        ar[go * W + y] = ok[y] ? ar[go * W + y] * scale : 0.0;
+        ai[go * W + y] = ok[y] ? ai[go * W + y] * scale : 0.0;
+      }
+    }
+  }
+  // D = A y with y this wave's state in the D layout (G elements per lane)
+  __device__ __forceinline__ void matvec(const double (&ar)[KA], const double (&ai)[KA], const double (&y)[G],
+                                         double (&D)[G]) const {
+    double bv[G][4];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      bv[g][0] = y[g];
+      bv[g][1] = mv<0x124>(y[g]);  // row_ror:4
+      bv[g][2] = mv<0x128>(y[g]);  // row_ror:8
+      bv[g][3] = mv<0x12C>(y[g]);  // row_ror:12
+    }
+    double d0[G], d1[G];  // Ar and Ai products of each output group: 2G chains, interleaved
+#pragma unroll
+    for (int g = 0; g < G; ++g) d0[g] = d1[g] = 0.0;
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int go = 0; go < G; ++go) {
+          const int x = (go * G + gi) * 4 + j;
+          d0[go] = MF<double>::mma4(ar[x], bv[gi][j], d0[go]);
+          d1[go] = MF<double>::mma4(ai[x], bv[gi][j], d1[go]);
+        }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const double o = mv<0xB1>(d1[g]);  // quad_perm [1,0,3,2]: (Ai y)[n ^ 1]
+      D[g] = (n & 1) ? d0[g] + o : d0[g] - o;
+    }
+  }
+  // this lane's element of row `row` into y and its rotated copy into y' (see TChainMF::put)
+  __device__ __forceinline__ void put_row(double* y, double* yp, int row, double v) const {
+    const int o = (cp * RP + row) * 4;
+    y[o + n] = v;
+    yp[o + (n ^ 1)] = (n & 1) ? -v : v;
+  }
+  __device__ __forceinline__ void put_e(double* yb, int buf, int e, double v) const {
+    put_row(ybuf(yb, CP, buf, 0), ybuf(yb, CP, buf, 1), rowE(e), v);
+  }
+  __device__ __forceinline__ void sync() const {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+  __device__ __forceinline__ void put_all(double* yb, int buf, const double (&v)[G]) const {
+#pragma unroll
+    for (int e = 0; e < G; ++e)
+      if (act[e]) put_row(ybuf(yb, CP, buf, 0), ybuf(yb, CP, buf, 1), rowE(e), v[e]);
+  }
+  // One slice (see TChainMF::step); the slice's start state is acc (this lane's D elements).
+  template <bool CHEB, bool CAP = false>
+  __device__ __forceinline__ void step(int N, const double (&ar)[KA], const double (&ai)[KA], double* yb,
+                                       const double* __restrict__ invt, int& cur, int P, int s, cx<double> ph,
+                                       double (&acc)[G], double cl, double* __restrict__ cw, double (&cd1)[G],
+                                       double (&cd2)[G]) const {
+    // the term coefficients: Chebyshev c_t from lane t of cl (v_readlane, no LDS round trip; they only enter the
+    // sum, off the recurrence's critical path), Taylor 1/t from the LDS table
+    auto coef = [&](int t) __attribute__((always_inline)) {
+      if constexpr (CHEB) {
+        const long long u = __double_as_longlong(cl);
+        const int lo_ = __builtin_amdgcn_readlane((int)u, t), hi_ = __builtin_amdgcn_readlane((int)(u >> 32), t);
+        return __longlong_as_double(((long long)hi_ << 32) | (unsigned)lo_);
+      } else {
+        return invt[t];
+      }
+    };
+    (void)cw;
+    for (int sub = 0; sub < s; ++sub) {
+      double y[G], ym2[G];  // y_{t-1}, y_{t-2} (Chebyshev)
+      const double c0 = CHEB ? coef(0) : 1.0;
+#pragma unroll
+      for (int e = 0; e < G; ++e) {
+        y[e] = act[e] ? acc[e] : 0.0;
+        ym2[e] = 0.0;
+        acc[e] = c0 * y[e];
+      }
+      // group e's product D of term t -> the recurrence (captures, z_t, the sum) and its next B operands
+      double bv[G][4];
+      auto rot = [&](int e) __attribute__((always_inline)) {
+        bv[e][0] = y[e];
+        bv[e][1] = mv<0x124>(y[e]);  // row_ror:4
+        bv[e][2] = mv<0x128>(y[e]);  // row_ror:8
+        bv[e][3] = mv<0x12C>(y[e]);  // row_ror:12
+      };
+      auto fin = [&](int e, double D, int t, double ct) __attribute__((always_inline)) {
         if constexpr (CAP) {
           if (sub == 0 && t <= 2) {
-            if (t == 1) cd1 = D;
-            else cd2 = D;
+            if (t == 1) cd1[e] = D;
+            else cd2[e] = D;
           }
         }
         double z;
         if constexpr (CHEB) {
-          z = t == 1 ? 0.5 * D : D + ym2;
-          ym2 = y;
-          acc += ct * z;
+          z = t == 1 ? 0.5 * D : D + ym2[e];
+          ym2[e] = y[e];
+          acc[e] += ct * z;
         } else {
           z = D * ct;
-          acc += z;
+          acc[e] += z;
         }
-        y = z;
+        y[e] = z;
+        rot(e);
+      };
+      auto dsum = [&](double d0, double d1) __attribute__((always_inline)) {
+        const double o = mv<0xB1>(d1);  // quad_perm [1,0,3,2]: (Ai y)[n ^ 1]
+        return (n & 1) ? d0 + o : d0 - o;
+      };
+#pragma unroll
+      for (int e = 0; e < G; ++e) rot(e);
+      if constexpr (G == 1) {
+        for (int t = 1; t <= P; ++t) {
+          const double ct = coef(t);
+          __builtin_amdgcn_sched_barrier(0);
+          double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            d0 = MF<double>::mma4(ar[j], bv[0][j], d0);
+            d1 = MF<double>::mma4(ai[j], bv[0][j], d1);
+          }
+          fin(0, dsum(d0, d1), t, ct);
+        }
+      } else {
+        // Software-pipelined across terms: the products of input group 0 go first, and the previous term's last
+        // output group is finished behind them; the last input group runs output-group-major, so groups
+        // 0..G-2 complete early and their recurrence runs behind the remaining products.  The MFMA pipe then
+        // never waits for a term's tail (DPP swap, recurrence, rotations) before the next term's products.
+        double pd0 = 0.0, pd1 = 0.0, pct = 0.0;  // the previous term's pending group G - 1
+        for (int t = 1; t <= P; ++t) {
+          const double ct = coef(t);
+          double d0[G], d1[G];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int go = 0; go < G; ++go) {
+              const int x = go * G * 4 + j;
+              d0[go] = MF<double>::mma4(ar[x], bv[0][j], j ? d0[go] : 0.0);
+              d1[go] = MF<double>::mma4(ai[x], bv[0][j], j ? d1[go] : 0.0);
+            }
+          __builtin_amdgcn_sched_barrier(0);
+          if (t > 1) fin(G - 1, dsum(pd0, pd1), t - 1, pct);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int gi = 1; gi < G - 1; ++gi)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int go = 0; go < G; ++go) {
+                const int x = (go * G + gi) * 4 + j;
+                d0[go] = MF<double>::mma4(ar[x], bv[gi][j], d0[go]);
+                d1[go] = MF<double>::mma4(ai[x], bv[gi][j], d1[go]);
+              }
+#pragma unroll
+          for (int go = 0; go < G; ++go)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int x = (go * G + G - 1) * 4 + j;
+              d0[go] = MF<double>::mma4(ar[x], bv[G - 1][j], d0[go]);
+              d1[go] = MF<double>::mma4(ai[x], bv[G - 1][j], d1[go]);
+            }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int e = 0; e < G - 1; ++e) fin(e, dsum(d0[e], d1[e]), t, ct);
+          pd0 = d0[G - 1];
+          pd1 = d1[G - 1];
+          pct = ct;
+        }
+        fin(G - 1, dsum(pd0, pd1), P, pct);
       }
       if (sub == s - 1) {
-        const double o = dpp_mov<0xB1>(acc);
-        acc = (n & 1) ? ph.r * acc + ph.i * o : ph.r * acc - ph.i * o;
+#pragma unroll
+        for (int e = 0; e < G; ++e) {
+          const double o = mv<0xB1>(acc[e]);
+          acc[e] = (n & 1) ? ph.r * acc[e] + ph.i * o : ph.r * acc[e] - ph.i * o;
+        }
       }
-      if (actD) put(ybuf(yb, CP, cur ^ 1, 0), ybuf(yb, CP, cur ^ 1, 1), acc);
+      put_all(yb, cur ^ 1, acc);
       sync();
       cur ^= 1;
     }
   }
 };
 
-// the chain struct of a body instantiation: KQ < 0 selects the LDS-free TChainRot (|KQ| = 4)
+// the chain struct of a body instantiation: KQ < 0 selects the LDS-free TChainRot<-KQ / 4>
 template <int KQ>
 struct TChainSel {
   using type = TChainMF<KQ>;
 };
 template <>
 struct TChainSel<-4> {
-  using type = TChainRot;
+  using type = TChainRot<1>;
+};
+template <>
+struct TChainSel<-8> {
+  using type = TChainRot<2>;
+};
+template <>
+struct TChainSel<-12> {
+  using type = TChainRot<3>;
 };
 
 // Register-resident variant (MAXT = 256, nu <= 2): the generators live in registers, not in LDS, and the first two
@@ -1139,10 +1390,10 @@ struct TChainSel<-4> {
 template <int KQ, bool CHEB, int MAXT>
 __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const int b) {
   using C = typename TChainSel<KQ>::type;
-  constexpr int KA = KQ < 0 ? -KQ : KQ;
+  constexpr int KA = C::KA, E = C::E;
   constexpr int RP = C::RP;
-  constexpr bool REGS = MAXT == 256;  // generators in registers (the dispatch picks MAXT = 256 only for nu <= 2)
-  static_assert(KQ > 0 || REGS, "TChainRot needs the register-resident generators");
+  constexpr bool REGS = MAXT == 256 && C::REGS_OK;  // generators in registers (the dispatch picks MAXT = 256 only for nu <= 2)
+  constexpr bool CAPS = REGS || KQ < 0;  // chains that write the gradient's captured products
   constexpr int NUR = REGS ? 2 : TCHAIN_NUMAX;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, tid = threadIdx.x, nthr = blockDim.x;
@@ -1176,43 +1427,62 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
       yb[CP * RP * 4 + (c2 * RP + r) * 4 + (nn ^ 1)] = (nn & 1) ? -v.i : v.r;
     }
   }
-  const bool pen_m = rg.actD && g.pmask && g.pmask[rg.rowD + N * rg.colD];
+  // this lane's E state elements: rows rg.rowE(e) of column rg.colD (re or im by rg.n)
+  bool pen_m[E];
+  size_t own[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    own[e] = (size_t)rg.rowE(e) + (size_t)N * rg.colD;
+    pen_m[e] = rg.actE(e) && g.pmask && g.pmask[own[e]];
+  }
   double pen = 0.0;
-  const size_t own = (size_t)rg.rowD + (size_t)N * rg.colD;
-  auto store = [&](double v, int k_) __attribute__((always_inline)) {
-    if (rg.actD) {
-      reinterpret_cast<double*>(Xb + (size_t)k_ * Nm + own)[rg.n & 1] = v;
-      if (pen_m) pen += v * v;
+  double* const sink = tchain_sink(g);
+  // stores without branches (TChainArgs::sink): lanes without an element write to the sink
+  auto store = [&](const double (&v)[E], int k_) __attribute__((always_inline)) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      double* p = rg.actE(e) ? reinterpret_cast<double*>(Xb + (size_t)k_ * Nm + own[e]) + (rg.n & 1) : sink;
+      *p = v[e];
+      pen += pen_m[e] ? v[e] * v[e] : 0.0;
     }
   };
-  const bool cap = REGS && g.cap1 != nullptr;
-  double* c1b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm + own) : nullptr;
-  double* c2b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm + own) : nullptr;
-  auto cap_store = [&](double d1, double d2, int k_) __attribute__((always_inline)) {
-    if (cap && rg.actD) {
-      c1b[2 * (size_t)k_ * Nm + (rg.n & 1)] = d1;
-      c2b[2 * (size_t)k_ * Nm + (rg.n & 1)] = d2;
+  const bool cap = CAPS && g.cap1 != nullptr;
+  double* c1b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm) : nullptr;
+  double* c2b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm) : nullptr;
+  // real = false: the same stores, all to the sink (the loops' first iteration has no previous slice to store)
+  auto cap_store = [&](const double (&d1)[E], const double (&d2)[E], int k_, bool real) __attribute__((always_inline)) {
+    if constexpr (!CAPS) return;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {  // without captures (cap1 = nullptr) every lane writes to the sink
+      const bool to = cap && real && rg.actE(e);
+      const size_t o = 2 * ((size_t)k_ * Nm + own[e]) + (rg.n & 1);
+      double* p1 = to ? c1b + o : sink;
+      double* p2 = to ? c2b + o : sink + 1;
+      *p1 = d1[e];
+      *p2 = d2[e];
     }
   };
   __syncthreads();
-  double gr[2][KA], gi[2][KA];
+  double gr[C::NG][KA], gi[C::NG][KA];
   if constexpr (REGS) rg.template load_gen<false>(N, nu, At, gr, gi);
-  double acc = rg.actD ? yb[(rg.cp * RP + rg.rowD) * 4 + rg.n] : 0.0;
+  double acc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[e] = rg.actE(e) ? yb[(rg.cp * RP + rg.rowE(e)) * 4 + rg.n] : 0.0;
   store(acc, 0);
 #ifdef QOC_PROBE
   const unsigned long long c0_ = __builtin_amdgcn_s_memtime(), r0_ = __builtin_amdgcn_s_memrealtime();
 #endif
   int cur = 0;
-  double cd1 = 0.0, cd2 = 0.0;
+  double cd1[E] = {}, cd2[E] = {};
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
-  // step data of PD slices in flight: TChainRot's slices (~7 terms at N = 9, ~1 us) are shorter than a loaded HBM
-  // round trip, so one slice of prefetch left each slice waiting for the next one's records
-  constexpr int PD = KQ < 0 ? 3 : 1;
+  // step data of PD slices in flight (TChainRot<1>: its slices, ~7 terms at N = 9, ~1 us, are shorter than a
+  // loaded HBM round trip, so one slice of prefetch left each slice waiting for the next one's records)
+  constexpr int PD = C::PD;
   TPreN<NUR> nx[PD];
 #pragma unroll
   for (int i = 0; i < PD; ++i) {
     const int ki = min(i, Nt - 1);
-    tpre_load(stb + ki, ub + (size_t)ki * nu, nu, nx[i], CHEB ? ceb + (size_t)ki * TCHEB_STRIDE : nullptr);
+    tpre_load<NUR, CHEB, false>(stb + ki, ub + (size_t)ki * nu, nu, nx[i], CHEB ? ceb + (size_t)ki * TCHEB_STRIDE : nullptr);
   }
   for (int k0 = 0; k0 < Nt; k0 += PD)
 #pragma unroll
@@ -1220,21 +1490,32 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
     const int k = k0 + i;
     if (k >= Nt) break;
     TC_T(s0);
-    // x_k (the previous slice's result) goes to HBM here, ahead of this slice's prefetch: the wait for the
-    // prefetch at the end of the slice (vmcnt, in issue order) then never waits for a just-issued store
-    if (k > 0) {
-      store(acc, k);
-      cap_store(cd1, cd2, k - 1);
-    }
-    const TPreN<NUR> st = nx[i];
+    // x_k (the previous slice's result) goes to HBM here, ahead of this slice's prefetch.  The same stores in every
+    // iteration (k = 0 rewrites x_0, its captures go to the sink): a store skipped on some path leaves the waitcnt
+    // pass unsure how many memory operations are in flight, and the next use of the prefetched step data then
+    // waited for the just-issued stores as well (an HBM round trip per slice)
+    store(acc, k);
+    cap_store(cd1, cd2, max(k - 1, 0), k > 0);
+    // PD = 1: copy the record, then prefetch the next into its registers.  PD > 1: use the record in place and
+    // prefetch into its registers after the slice (PD - 1 slices of latency hidden): no copy, which the compiler
+    // otherwise made at the loop latch from the just-issued loads, waiting for them there
     const int kn = min(k + PD, Nt - 1);
-    tpre_load(stb + kn, ub + (size_t)kn * nu, nu, nx[i], CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
+    TPreN<NUR> st_;
+    if constexpr (PD == 1) {
+      st_ = nx[i];
+      tpre_load<NUR, CHEB, false>(stb + kn, ub + (size_t)kn * nu, nu, nx[i],
+                                  CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
+    }
+    const TPreN<NUR>& st = PD == 1 ? st_ : nx[i];
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
     double ar[KA], ai[KA];
     if constexpr (REGS) rg.form_regs(N, nu, gr, gi, gen, st.u, st.scale, ar, ai);
     else rg.form(N, nu, gen, st.u, st.scale, ar, ai);
     TC_T(s1);
-    rg.template step<CHEB, REGS>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, st.pi}, acc, st.cl, cw, cd1, cd2);
+    rg.template step<CHEB, CAPS>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, st.pi}, acc, st.cl, cw, cd1, cd2);
+    if constexpr (PD > 1)
+      tpre_load<NUR, CHEB, false>(stb + kn, ub + (size_t)kn * nu, nu, nx[i],
+                                  CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
     TC_T(s2);
     TC_T(s3);
     TC_ADD(10, s1 - s0);
@@ -1243,7 +1524,7 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
     TC_ADD(13, 1);
   }
   store(acc, Nt);
-  cap_store(cd1, cd2, Nt - 1);
+  cap_store(cd1, cd2, Nt - 1, true);
   __syncthreads();
 #ifdef QOC_PROBE
   if (blockIdx.x == 7 && threadIdx.x == 0) {
@@ -1263,10 +1544,10 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
 template <int KQ, bool CHEB, int MAXT>
 __device__ __forceinline__ void tchain_mf_bwd_body(const TChainArgs& g, const int b) {
   using C = typename TChainSel<KQ>::type;
-  constexpr int KA = KQ < 0 ? -KQ : KQ;
+  constexpr int KA = C::KA, E = C::E;
   constexpr int RP = C::RP;
-  constexpr bool REGS = MAXT == 256;  // see k_tchain_mf_fwd
-  static_assert(KQ > 0 || REGS, "TChainRot needs the register-resident generators");
+  constexpr bool REGS = MAXT == 256 && C::REGS_OK;  // see k_tchain_mf_fwd
+  constexpr bool CAPS = REGS || KQ < 0;  // chains that write the gradient's captured products
   constexpr int NUR = REGS ? 2 : TCHAIN_NUMAX;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, tid = threadIdx.x, nthr = blockDim.x;
@@ -1331,60 +1612,95 @@ __device__ __forceinline__ void tchain_mf_bwd_body(const TChainArgs& g, const in
     yb[CP * RP * 4 + q + 1] = v.r;
     yb[CP * RP * 4 + q] = -v.i;
   }
-  const bool pen_m = rg.actD && pmask && pmask[rg.rowD + N * rg.colD];
-  const size_t own = (size_t)rg.rowD + (size_t)N * rg.colD;
-  const bool cap = REGS && g.cap1 != nullptr;
-  double* c1b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm + own) : nullptr;
-  double* c2b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm + own) : nullptr;
-  auto cap_store = [&](double d1, double d2, int k_) __attribute__((always_inline)) {
-    if (cap && rg.actD) {
-      c1b[2 * (size_t)k_ * Nm + (rg.n & 1)] = d1;
-      c2b[2 * (size_t)k_ * Nm + (rg.n & 1)] = d2;
+  bool pen_m[E];
+  size_t own[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    own[e] = (size_t)rg.rowE(e) + (size_t)N * rg.colD;
+    pen_m[e] = rg.actE(e) && pmask && pmask[own[e]];
+  }
+  const bool cap = CAPS && g.cap1 != nullptr;
+  double* c1b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm) : nullptr;
+  double* c2b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm) : nullptr;
+  double* const sink = tchain_sink(g);  // stores without branches (see the forward body)
+  // real = false: the same stores, all to the sink (the loops' first iteration has no previous slice to store)
+  auto cap_store = [&](const double (&d1)[E], const double (&d2)[E], int k_, bool real) __attribute__((always_inline)) {
+    if constexpr (!CAPS) return;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {  // without captures (cap1 = nullptr) every lane writes to the sink
+      const bool to = cap && real && rg.actE(e);
+      const size_t o = 2 * ((size_t)k_ * Nm + own[e]) + (rg.n & 1);
+      double* p1 = to ? c1b + o : sink;
+      double* p2 = to ? c2b + o : sink + 1;
+      *p1 = d1[e];
+      *p2 = d2[e];
+    }
+  };
+  auto store_lam = [&](const double (&v)[E], int k_) __attribute__((always_inline)) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      double* p = rg.actE(e) ? reinterpret_cast<double*>(Lb + (size_t)k_ * Nm + own[e]) + (rg.n & 1) : sink;
+      *p = v[e];
     }
   };
   __syncthreads();
-  double gr[2][KA], gi[2][KA];
+  double gr[C::NG][KA], gi[C::NG][KA];
   if constexpr (REGS) rg.template load_gen<true>(N, nu, At, gr, gi);
   int cur = 0;
-  double acc = rg.actD ? yb[(rg.cp * RP + rg.rowD) * 4 + rg.n] : 0.0;  // λ at k_hi (TChainRot starts from acc)
-  double cd1 = 0.0, cd2 = 0.0;
+  double acc[E];  // λ at k_hi (TChainRot starts from acc)
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[e] = rg.actE(e) ? yb[(rg.cp * RP + rg.rowE(e)) * 4 + rg.n] : 0.0;
+  double cd1[E] = {}, cd2[E] = {};
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
-  constexpr int PD = KQ < 0 ? 3 : 1;  // slices of step data in flight (see tchain_mf_fwd_body)
+  constexpr int PD = C::PD;  // slices of step data in flight (see tchain_mf_fwd_body)
   TPreN<NUR> nx[PD];
 #pragma unroll
   for (int i = 0; i < PD; ++i) {
     const int ki = max(k_hi - 1 - i, 0);
-    tpre_load(stb + ki, ub + (size_t)ki * nu, nu, nx[i], CHEB ? ceb + (size_t)ki * TCHEB_STRIDE : nullptr);
+    tpre_load<NUR, CHEB, false>(stb + ki, ub + (size_t)ki * nu, nu, nx[i], CHEB ? ceb + (size_t)ki * TCHEB_STRIDE : nullptr);
   }
   for (int k0 = k_hi - 1; k0 >= k_lo; k0 -= PD)
 #pragma unroll
   for (int i = 0; i < PD; ++i) {
     const int k = k0 - i;
     if (k < k_lo) break;
-    // λ_{k+1} (the previous slice's result) to HBM ahead of this slice's loads (see k_tchain_mf_fwd)
-    if (k < k_hi - 1) {
-      if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)(k + 1) * Nm + own)[rg.n & 1] = acc;
-      cap_store(cd1, cd2, k + 1);
-    }
-    const TPreN<NUR> st = nx[i];
+    // λ_{k+1} (the previous slice's result) to HBM ahead of this slice's loads, the same stores in every iteration
+    // (see tchain_mf_fwd_body; the first rewrites λ_{k_hi}, its captures go to the sink)
+    store_lam(acc, k + 1);
+    cap_store(cd1, cd2, k + 1, k < k_hi - 1);
     const int kp = max(k - PD, 0);
-    tpre_load(stb + kp, ub + (size_t)kp * nu, nu, nx[i], CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
+    TPreN<NUR> st_;  // see tchain_mf_fwd_body
+    if constexpr (PD == 1) {
+      st_ = nx[i];
+      tpre_load<NUR, CHEB, false>(stb + kp, ub + (size_t)kp * nu, nu, nx[i],
+                                  CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
+    }
+    const TPreN<NUR>& st = PD == 1 ? st_ : nx[i];
     const int P = __builtin_amdgcn_readfirstlane(st.P), ns = __builtin_amdgcn_readfirstlane(st.s);
-    const size_t ok_ = (size_t)k * Nm + own;
-    double xk = pen_m ? tmu * reinterpret_cast<const double*>(Xb + ok_)[rg.n & 1] : 0.0;
-    if (srcb && rg.actD) xk += reinterpret_cast<const double*>(srcb + ok_)[rg.n & 1];
+    double xk[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const size_t ok_ = (size_t)k * Nm + own[e];
+      xk[e] = pen_m[e] ? tmu * reinterpret_cast<const double*>(Xb + ok_)[rg.n & 1] : 0.0;
+      if (srcb && rg.actE(e)) xk[e] += reinterpret_cast<const double*>(srcb + ok_)[rg.n & 1];
+    }
     double ar[KA], ai[KA];
     if constexpr (REGS) rg.form_regs(N, nu, gr, gi, gen, st.u, st.scale, ar, ai);
     else rg.form(N, nu, gen, st.u, st.scale, ar, ai);
-    rg.template step<CHEB, REGS>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, -st.pi}, acc, st.cl, cw, cd1, cd2);
-    if (pen_m || (srcb && rg.actD)) {
-      acc += xk;
-      rg.put(C::ybuf(yb, rg.CP, cur, 0), C::ybuf(yb, rg.CP, cur, 1), acc);
-    }
+    rg.template step<CHEB, CAPS>(N, ar, ai, yb, invt, cur, P, ns, cx<double>{st.pr, -st.pi}, acc, st.cl, cw, cd1, cd2);
+    if constexpr (PD > 1)
+      tpre_load<NUR, CHEB, false>(stb + kp, ub + (size_t)kp * nu, nu, nx[i],
+                                  CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (pen_m[e] || (srcb && rg.actE(e))) {
+        acc[e] += xk[e];
+        rg.put_e(yb, cur, e, acc[e]);
+      }
     if (pmask || srcb) rg.sync();  // the penalised entries changed after the step's last barrier
   }
-  if (rg.actD) reinterpret_cast<double*>(Lb + (size_t)k_lo * Nm + own)[rg.n & 1] = acc;  // λ_{k_lo}
-  cap_store(cd1, cd2, k_lo);
+  store_lam(acc, k_lo);  // λ_{k_lo}
+  cap_store(cd1, cd2, k_lo, true);
 }
 
 template <int KQ, bool CHEB, int MAXT>

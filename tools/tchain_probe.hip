@@ -92,7 +92,9 @@ void run_mf(int N, int m, int Nt, int B, int P) {
   TChainArgs g{};
   g.N = N; g.m = m; g.nu = nu; g.Nt = Nt; g.At = dA; g.u = du; g.steps = dst; g.x0 = dx0; g.X = dX; g.L = dX;
   g.Xt = dx0; g.cost_kind = 2; g.n_norm = 1.0; g.J = dJ; g.coef = (cx<double>*)dcoef; g.tcoef = dtc;
-  const size_t lds = tchain_mf_lds(N, m, nu);
+  (void)hipMalloc(&g.sink, TCHAIN_SINK * sizeof(double));
+  const size_t lds = tchain_mf_lds(N, m, nu, KQ < 0);
+  const int threads = KQ < 0 ? 64 * ((m + 1) / 2) : 64 * tchain_mf_waves(N, m);
   (void)hipFuncSetAttribute((const void*)k_tchain_mf_fwd<KQ, CHEB, MAXT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
@@ -104,7 +106,7 @@ void run_mf(int N, int m, int Nt, int B, int P) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tc), z, sizeof(z));
 #endif
     (void)hipEventRecord(a);
-    hipLaunchKernelGGL((k_tchain_mf_fwd<KQ, CHEB, MAXT>), dim3(B), dim3(64 * tchain_mf_waves(N, m)), lds, 0, g);
+    hipLaunchKernelGGL((k_tchain_mf_fwd<KQ, CHEB, MAXT>), dim3(B), dim3(threads), lds, 0, g);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     (void)hipEventElapsedTime(&ms, a, b);
@@ -128,12 +130,17 @@ void run_mf(int N, int m, int Nt, int B, int P) {
 }
 
 int main() {
-  run_mf<10, false>(40, 2, 1000, 256, 11);
-  run_mf<10, true>(40, 2, 1000, 256, 9);
-  run_mf<10, true>(40, 2, 1000, 256, 6);
-  run_mf<10, true>(40, 2, 1000, 256, 3);
+  // KQ < 0: the register-state chains (TChainRot<-KQ / 4>); B = 2x the bench's seeds mimics the dual launch's waves
   run_mf<3, true>(9, 4, 500, 512, 8);
-  run_mf<3, true>(9, 4, 500, 512, 4);
-  run_mf<8, false>(27, 1, 2000, 512, 20);
+  run_mf<-4, true>(9, 4, 500, 512, 8);
+  run_mf<-4, true>(9, 4, 500, 512, 4);
+  run_mf<-4, true>(9, 4, 500, 512, 2);
+  run_mf<-4, true>(9, 4, 500, 1024, 8);
+  run_mf<8, true>(27, 1, 500, 512, 40);
+  run_mf<-8, true>(27, 1, 500, 512, 40);
+  run_mf<-8, true>(27, 1, 500, 512, 20);
+  run_mf<-8, true>(27, 1, 500, 1024, 40);
+  run_mf<10, true>(40, 2, 500, 256, 9);
+  run_mf<-12, true>(40, 2, 250, 256, 9);
   return 0;
 }
