@@ -77,7 +77,18 @@ int grad_cap_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, 
   const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
   const size_t lds = G::lds_bytes(N, NU);
   const long long units = (long long)B * nk, ntiles = (units + 16 / m - 1) / (16 / m);
-  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+  // as many resident workgroups as the kernel's registers and LDS allow (N <= 16: 3 per CU; the loads of a tile
+  // are waited for before its contractions, so resident waves are the memory-level parallelism)
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_c<NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  static int occ = 0;  // per instantiation (lds depends on N, fixed by the instantiation up to 3 rows)
+  int per_cu = occ;
+  if (per_cu < 1) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_grad_rr_c<NT, KS, NU>, 256, lds) !=
+            hipSuccess ||
+        per_cu < 1)
+      per_cu = lds <= 80 * 1024 ? 2 : 1;
+    occ = per_cu;
+  }
   const int grid = (int)std::max<long long>(1, std::min<long long>((ntiles + 3) / 4, (long long)c->ncu * per_cu));
   const size_t bufN = (size_t)N * ((size_t)B * (Nt + 1) * m);
   GradCapArgs a{};
@@ -106,7 +117,6 @@ int grad_cap_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, 
   if (c->packed)
     for (int r = 0; r < N && r < 64; ++r) a.rsec_mask |= (unsigned long long)(c->h_rsec[r] & 1) << r;
   a.dJdu = d_dJdu;
-  HIPCHK(c, hipFuncSetAttribute((const void*)k_grad_rr_c<NT, KS, NU>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL((k_grad_rr_c<NT, KS, NU>), dim3(grid), dim3(256), lds, st, a);
   HIPCHK(c, hipGetLastError());
   return QOC_OK;

@@ -1438,12 +1438,13 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
   double pen = 0.0;
   double* const sink = tchain_sink(g);
   // stores without branches (TChainArgs::sink): lanes without an element write to the sink
-  auto store = [&](const double (&v)[E], int k_) __attribute__((always_inline)) {
+  // count: the state enters the penalty sum (false for the loop's k = 0 rewrite of x_0)
+  auto store = [&](const double (&v)[E], int k_, bool count) __attribute__((always_inline)) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       double* p = rg.actE(e) ? reinterpret_cast<double*>(Xb + (size_t)k_ * Nm + own[e]) + (rg.n & 1) : sink;
       *p = v[e];
-      pen += pen_m[e] ? v[e] * v[e] : 0.0;
+      pen += pen_m[e] && count ? v[e] * v[e] : 0.0;
     }
   };
   const bool cap = CAPS && g.cap1 != nullptr;
@@ -1468,7 +1469,7 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
   double acc[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) acc[e] = rg.actE(e) ? yb[(rg.cp * RP + rg.rowE(e)) * 4 + rg.n] : 0.0;
-  store(acc, 0);
+  store(acc, 0, true);
 #ifdef QOC_PROBE
   const unsigned long long c0_ = __builtin_amdgcn_s_memtime(), r0_ = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1494,7 +1495,7 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
     // iteration (k = 0 rewrites x_0, its captures go to the sink): a store skipped on some path leaves the waitcnt
     // pass unsure how many memory operations are in flight, and the next use of the prefetched step data then
     // waited for the just-issued stores as well (an HBM round trip per slice)
-    store(acc, k);
+    store(acc, k, k > 0);
     cap_store(cd1, cd2, max(k - 1, 0), k > 0);
     // PD = 1: copy the record, then prefetch the next into its registers.  PD > 1: use the record in place and
     // prefetch into its registers after the slice (PD - 1 slices of latency hidden): no copy, which the compiler
@@ -1523,7 +1524,7 @@ __device__ __forceinline__ void tchain_mf_fwd_body(const TChainArgs& g, const in
     TC_ADD(12, s3 - s2);
     TC_ADD(13, 1);
   }
-  store(acc, Nt);
+  store(acc, Nt, true);
   cap_store(cd1, cd2, Nt - 1, true);
   __syncthreads();
 #ifdef QOC_PROBE

@@ -2,8 +2,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 T=${1:-r03q}
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -DQOC_PROBE -o /tmp/tchain_probe tools/tchain_probe.hip || exit 1
-timeout -k 10 200 /tmp/tchain_probe > gpurun_out/${T}_probe.log 2>&1 || exit 1
+true
+true
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_rot.py tests/test_gpu_concurrent.py tests/test_gpu_parity.py > gpurun_out/${T}_test.log 2>&1 || exit 1
 for c in zz_batch tunable_bus cavity; do
   timeout -k 10 300 python bench.py --config $c --no-cpu > gpurun_out/${T}_$c.json 2>gpurun_out/${T}_$c.err || exit 1
