@@ -79,6 +79,18 @@ def grad_flops(N, m, nu, Nt, B, order, captured=False):
     return B * Nt * (2 * (order - 1) * mv + nu * order * mv)
 
 
+def block_sizes(prob):
+    """Row counts of the generators' invariant blocks (connected components of the union sparsity pattern of
+    A_0..A_nu), as the engine's qoc_set_generators finds them for the block chains (csrc/qoc_blk.hpp)."""
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import connected_components
+    M = np.abs(np.asarray(prob.A0)) > 0
+    for a in prob.A:
+        M |= np.abs(np.asarray(a)) > 0
+    _, lab = connected_components(csr_matrix(M), directed=False)
+    return np.bincount(lab)
+
+
 def chain_bytes(N, m, Nt, B, esz):
     """Compulsory HBM bytes of one chain launch: read all U_k once, write the N x m state per slice."""
     return B * Nt * N * N * esz + B * (Nt + 1) * N * m * esz
@@ -379,7 +391,27 @@ def main():
             traffic_all = {}
     taylor = info1.get("chain") == "taylor" and not large
     dual = info1.get("concurrent_launch") == "dual"
-    if taylor:
+    blocks = taylor and info1.get("chain_kernel") == "blocks"
+    if blocks:
+        # block chains (csrc/qoc_blk.hpp): one lane per (block, column), each term an n_b x n_b complex matvec in
+        # VALU registers; the launch's algorithmic bytes are the states it writes (x_k, and μ_k in the dual launch)
+        # plus the step records it reads (32 B record + P+1 Chebyshev coefficients + u_k per slice); the gradient
+        # reads x_k and λ_{k+1} once and writes dJdu
+        nb2 = float(np.sum(block_sizes(prob).astype(np.float64) ** 2))
+        dirs = 2 if dual else 1
+        tl = terms / K * dirs
+        p_avg = terms / K / max(B * Nt, 1)
+        rec = B * Nt * (32 + 8 * (p_avg + 1) + 8 * nu)
+        st = B * (Nt + 1) * N * m * esz
+        models = {
+            "k_expm": ("hbm", (B * Nt * (8 * nu + 32 + 8 * (p_avg + 1))) / 1e9, "GB/s", PEAK_HBM_GBS),
+            "k_chain_fwd": ("hbm", dirs * (st + rec) / 1e9, "GB/s", PEAK_HBM_GBS),
+            "k_chain_bwd": ("hbm", (st + rec) / 1e9, "GB/s", PEAK_HBM_GBS),
+            "k_grad": ("hbm", (2 * B * Nt * N * m * esz + 16 * nu * B * Nt) / 1e9, "GB/s", PEAK_HBM_GBS),
+        }
+        block_flops = {"k_chain_fwd": 8.0 * nb2 * m * tl, "k_chain_bwd": 8.0 * nb2 * m * terms / K,
+                       "k_grad": 8.0 * nb2 * m * B * Nt * (2 * (args.order - 1) + nu * args.order)}
+    elif taylor:
         # Taylor-action chains (csrc/qoc_tchain.hpp): no exponential kernel; the chains carry the Taylor terms,
         # each an N x N by N x m complex matvec (8 N^2 m flops) on v_mfma_f64_4x4x4 (fp64) / VALU (fp32); the dual
         # launch (k_tchain_mf_dual) carries both directions' terms
@@ -433,7 +465,27 @@ def main():
         kern[k] = {"ms_per_launch": per_launch[k], "launches_per_step": lps[k], "bound": bound, "achieved": ach,
                    "unit": unit, "peak": pk, "frac": ach / pk}
     names = {"k_expm": "k_expm_rr", "k_chain_fwd": "k_chain_fwd", "k_chain_bwd": "k_chain_bwd", "k_grad": "k_grad_rr"}
-    if taylor:
+    if blocks:
+        names = {"k_expm": "k_tchain_prep", "k_chain_fwd": "k_blk_dual" if dual else "k_blk_fwd",
+                 "k_chain_bwd": "k_blk_bwd", "k_grad": "k_blk_grad"}
+        for k in ("k_chain_fwd", "k_chain_bwd", "k_grad"):
+            kern[k]["kernel"] = names[k]
+            t = per_step[k] / 1e3
+            kern[k]["executed_tflops"] = block_flops[k] / 1e12 / t if t > 0 else 0.0
+        for k in ("k_chain_fwd", "k_chain_bwd"):
+            kern[k]["terms_per_seed"] = terms / K / B
+            kern[k]["ns_per_serial_term"] = per_step[k] * 1e6 / max(terms / K / B, 1e-9)
+        dom = max(("k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad"), key=lambda k: per_step[k])
+        roof = {"kernel": names[dom], "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
+                "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
+                "traffic": traffic_all.get(names[dom]), "ms_per_launch": kern[dom]["ms_per_launch"],
+                "launches_per_step": lps[dom],
+                "blocks": [int(x) for x in block_sizes(prob)],
+                "note": ("block chains (generators with invariant blocks): achieved = algorithmic HBM bytes per launch "
+                         "(states written, step records read; the gradient: x_k and λ_{k+1} read) / launch time"
+                         + ("; the forward chain and the μ recurrence of every seed in one launch (k_blk_dual)" if dual
+                            else ""))}
+    elif taylor:
         mf = prob.precision == "fp64"
         names = {"k_expm": "k_tchain_prep",
                  "k_chain_fwd": "k_tchain_mf_dual" if dual else "k_tchain_mf_fwd" if mf else "k_tchain_fwd",

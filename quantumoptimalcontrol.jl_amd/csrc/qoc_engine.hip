@@ -322,6 +322,7 @@ RcclApi& rccl() {
 }
 
 int forward(qoc_ctx* c) {
+  if (blk_active(c)) return blk_forward(c);
   if (c->big) return c->prec == QOC_FP64 ? big_forward<double>(c) : big_forward<float>(c);
   return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
 }
@@ -330,6 +331,7 @@ int backward(qoc_ctx* c, int order, double* d_dJdu) {
   c->last_eval_mode = 0;
   if (c->src_on && c->prop_method == QOC_PROP_TSIT5)
     return fail(c, QOC_ERR_UNSUPPORTED, "a co-state source (dL_dx) is not part of the Tsit5 path (compute_pwc_gradient)");
+  if (blk_active(c)) return blk_backward(c, order, d_dJdu);
   if (c->big)
     return c->prec == QOC_FP64 ? big_backward<double>(c, order, d_dJdu) : big_backward<float>(c, order, d_dJdu);
   return c->prec == QOC_FP64 ? run_backward<double>(c, order, d_dJdu) : run_backward<float>(c, order, d_dJdu);
@@ -495,6 +497,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->d_best) hipFree(c->d_best);
   if (c->d_tcoef) hipFree(c->d_tcoef);
   if (c->d_coef_mu) hipFree(c->d_coef_mu);
+  if (c->d_brow) hipFree(c->d_brow);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
                   c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_pws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec, c->d_sink};
   for (void* p : ptrs)
@@ -659,6 +662,12 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
     else c->chain_mode = (cheb_run ? c->tprm.rad[0] <= 25.0 : c->tprm.nrm[0] <= 1.0) ? 1 : 0;
   } else {
     c->chain_mode = 0;
+  }
+  if (c->tchain_ok) {  // invariant blocks of the generators (qoc_blk.hpp)
+    r = blk_detect(c);
+    if (r) return r;
+  } else {
+    c->blk_nb = 0;
   }
   c->have_gen = true;
   c->have_prop = false;
@@ -884,7 +893,7 @@ int qoc_grape_sensitivity_dev(qoc_ctx* c, const double* d_u, int order, double* 
 int qoc_eval_dev(qoc_ctx* c, const double* d_u, int order, double* d_J, double* d_dJdu) {
   if (c && c->cost_kind == QOC_COST_EXTERNAL)
     return fail(c, QOC_ERR_STATE, "qoc_eval_dev needs a device-side cost (TRACE or ZCAL)");
-  if (c && c->have_gen && tchain_concurrent_ok(c, order)) {
+  if (c && c->have_gen && (blk_concurrent_ok(c, order) || tchain_concurrent_ok(c, order))) {
     // forward chain and the μ recurrence side by side (tchain_eval_concurrent)
     int r = check_ready(c);
     if (r) return r;
@@ -892,8 +901,9 @@ int qoc_eval_dev(qoc_ctx* c, const double* d_u, int order, double* d_J, double* 
     const size_t nu_t = (size_t)c->B * c->nu * c->Nt;
     if (d_u != c->d_u) HIPCHK(c, hipMemcpyAsync(c->d_u, d_u, nu_t * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     c->have_prop = false;
-    r = c->prec == QOC_FP64 ? tchain_eval_concurrent<double>(c, d_dJdu ? d_dJdu : c->d_dJdu)
-                            : tchain_eval_concurrent<float>(c, d_dJdu ? d_dJdu : c->d_dJdu);
+    r = blk_concurrent_ok(c, order)  ? blk_eval_concurrent(c, order, d_dJdu ? d_dJdu : c->d_dJdu)
+        : c->prec == QOC_FP64 ? tchain_eval_concurrent<double>(c, d_dJdu ? d_dJdu : c->d_dJdu)
+                              : tchain_eval_concurrent<float>(c, d_dJdu ? d_dJdu : c->d_dJdu);
     if (r) return r;
     c->props_since_reset++;
     if (d_J && d_J != c->d_J)
@@ -1245,7 +1255,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[7] = c->m;  // state columns the kernels run on (< the caller's m when compress_states packing is on)
   info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 / 3 concurrent μ recurrence
   info[9] = c->fwd_captured ? 1 : 0;
-  info[10] = c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
+  info[10] = blk_active(c) ? 3 : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
   return QOC_OK;
 }
 

@@ -8,6 +8,7 @@
 //   qoc_run_grad.hip      the fused order-3 gradient (k_grad_rr_*)
 //   qoc_run_big.hip       the large-N GEMM pipeline, the GEMM-shaped gradient and the Fréchet gradient
 //   qoc_run_ode.hip       the Tsit5 path
+//   qoc_run_blk.hip       the block chains and block gradient (generators with small invariant blocks)
 // Each kernel template is launched from one translation unit only; the context (qoc_ctx) and the entry points
 // between the units are declared here.
 #pragma once
@@ -150,7 +151,12 @@ struct qoc_ctx {
   bool L_is_mu = false;          // d_L holds μ_k (qoc_get_costates applies the coefficients d_coef_mu)
   cx<double>* d_coef_mu = nullptr;  // B x 2m: the λ_N coefficients of the eval that left μ in d_L
   int last_eval_mode = 0;        // 0 other, 1 captured sequential backward, 2 / 3 concurrent μ mode: two streams /
-                                 // one dual launch (qoc_get_info)
+                                 // one dual launch, 4 block chains' concurrent eval (qoc_get_info)
+  // generators with small invariant blocks (qoc_blk.hpp, detected at qoc_set_generators; QOC_BLOCKS=0 off): the
+  // chains and the gradient run per block
+  int blk_nb = 0;                // padded block size 2 / 3 / 4 (0: no block path)
+  int nblk = 0;                  // blocks
+  int* d_brow = nullptr;         // nblk x blk_nb rows of each block (-1 padding)
   // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
@@ -261,5 +267,15 @@ int ensure_pws(qoc_ctx* c);
 template <typename T>
 int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu);
 hipError_t launch_pade_units(qoc_ctx* c, long long units);
+TChainArgs tchain_args(qoc_ctx* c);
+int tchain_prep(qoc_ctx* c);
+
+// ---- qoc_run_blk.hip ----
+int blk_detect(qoc_ctx* c);
+bool blk_active(const qoc_ctx* c);
+int blk_forward(qoc_ctx* c);
+int blk_backward(qoc_ctx* c, int order, double* d_dJdu);
+bool blk_concurrent_ok(const qoc_ctx* c, int order);
+int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu);
 
 }  // namespace qoc_host

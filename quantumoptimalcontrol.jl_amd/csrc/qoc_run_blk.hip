@@ -1,0 +1,201 @@
+// qoc_run_blk.hip — the block chains and block gradient (qoc_blk.hpp): detection of the generators' invariant
+// blocks, and the launches of one propagate / grape_sensitivity / concurrent eval on them.
+#include <numeric>
+
+#include "qoc_blk.hpp"
+#include "qoc_internal.hpp"
+
+namespace qoc_host {
+
+// Connected components of the union sparsity pattern of A_0..A_nu (host copy, c->h_gen): rows i and k share a block
+// whenever some A_j[i, k] or A_j[k, i] is nonzero.  Blocks of at most BLK_NBMAX rows turn the block path on
+// (QOC_BLOCKS=0 keeps the dense chains); d_brow lists each block's rows in increasing order, blocks ordered by
+// their first row, padded with -1 to NB = 2, 3 or 4.
+int blk_detect(qoc_ctx* c) {
+  c->blk_nb = 0;
+  c->nblk = 0;
+  const char* env = getenv("QOC_BLOCKS");
+  if (env && atoi(env) == 0) return QOC_OK;
+  const int N = c->N;
+  const size_t NN = (size_t)N * N;
+  std::vector<int> par(N);
+  std::iota(par.begin(), par.end(), 0);
+  auto find = [&](int x) {
+    while (par[x] != x) x = par[x] = par[par[x]];
+    return x;
+  };
+  for (int j = 0; j <= c->nu; ++j)
+    for (int col = 0; col < N; ++col)
+      for (int row = 0; row < N; ++row) {
+        const double* v = c->h_gen.data() + 2 * (j * NN + row + (size_t)N * col);
+        if (row != col && (v[0] != 0.0 || v[1] != 0.0)) {
+          const int a = find(row), b = find(col);
+          if (a != b) par[std::max(a, b)] = std::min(a, b);
+        }
+      }
+  std::vector<std::vector<int>> blocks;
+  std::vector<int> id(N, -1);
+  for (int row = 0; row < N; ++row) {
+    const int root = find(row);
+    if (id[root] < 0) {
+      id[root] = (int)blocks.size();
+      blocks.emplace_back();
+    }
+    blocks[id[root]].push_back(row);
+  }
+  size_t mx = 0;
+  for (const auto& bl : blocks) mx = std::max(mx, bl.size());
+  if (mx > (size_t)BLK_NBMAX) return QOC_OK;
+  const int NB = mx <= 2 ? 2 : mx <= 3 ? 3 : 4;
+  const int nblk = (int)blocks.size();
+  std::vector<int> brow((size_t)nblk * NB, -1);
+  for (int b = 0; b < nblk; ++b)
+    for (size_t i = 0; i < blocks[b].size(); ++i) brow[(size_t)b * NB + i] = blocks[b][i];
+  if (c->d_brow) {
+    HIPCHK(c, hipFree(c->d_brow));
+    c->d_brow = nullptr;
+  }
+  HIPCHK(c, hipMalloc((void**)&c->d_brow, brow.size() * sizeof(int)));
+  HIPCHK(c, hipMemcpy(c->d_brow, brow.data(), brow.size() * sizeof(int), hipMemcpyHostToDevice));
+  c->blk_nb = NB;
+  c->nblk = nblk;
+  return QOC_OK;
+}
+
+// The block path runs the Taylor-action chains' fp64 scheme (step records, shifted generators) on unpacked states
+bool blk_active(const qoc_ctx* c) {
+  return c->blk_nb > 0 && c->prec == QOC_FP64 && c->chain_mode == 1 && c->prop_method == QOC_PROP_EXPM && !c->big &&
+         !c->packed && c->nu <= 2 && c->nblk * c->m <= BLK_MAXT && c->nblk <= 256;
+}
+
+static BlkArgs blk_args(const qoc_ctx* c) {
+  BlkArgs bk{};
+  bk.brow = c->d_brow;
+  bk.A = c->d_A;
+  bk.nblk = c->nblk;
+  return bk;
+}
+
+static int blk_threads(const qoc_ctx* c) { return 64 * ((c->nblk * c->m + 63) / 64); }
+
+template <typename F>
+static hipError_t blk_dispatch(const qoc_ctx* c, F&& f) {
+  using std::integral_constant;
+  switch (c->blk_nb) {
+    case 2: return c->cheb_ran ? f(integral_constant<int, 2>(), std::true_type()) : f(integral_constant<int, 2>(), std::false_type());
+    case 3: return c->cheb_ran ? f(integral_constant<int, 3>(), std::true_type()) : f(integral_constant<int, 3>(), std::false_type());
+    case 4: return c->cheb_ran ? f(integral_constant<int, 4>(), std::true_type()) : f(integral_constant<int, 4>(), std::false_type());
+  }
+  return hipErrorInvalidValue;
+}
+
+int blk_forward(qoc_ctx* c) {
+  int r = tchain_prep(c);
+  if (r) return r;
+  const TChainArgs g = tchain_args(c);
+  const BlkArgs bk = blk_args(c);
+  const size_t lds = blk_lds(c->N, c->m);
+  const int mk = mark_begin(c, 1);
+  const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
+    constexpr int NB = decltype(NB_)::value;
+    constexpr bool CH = decltype(CH_)::value;
+    hipLaunchKernelGGL((k_blk_fwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blk_fwd launch: %s", hipGetErrorString(e));
+  c->fwd_captured = false;
+  c->props_since_reset++;
+  return QOC_OK;
+}
+
+// the order-o gradient from d_X and d_L (mu_mode: d_L holds μ, λ = coef ⊙ μ with the coefficients in d_coef)
+static int blk_grad(qoc_ctx* c, int order, bool mu_mode, double* d_dJdu) {
+  const TChainArgs g = tchain_args(c);
+  const BlkArgs bk = blk_args(c);
+  const long long units = (long long)c->B * c->Nt;
+  const int upw = 256 / c->nblk;
+  const unsigned blocks = (unsigned)((units + upw - 1) / upw);
+  const int mk = mark_begin(c, 3);
+  hipError_t e = hipSuccess;
+  auto launch = [&](auto NB_) {
+    constexpr int NB = decltype(NB_)::value;
+    switch (order) {
+      case 1: hipLaunchKernelGGL((k_blk_grad<NB, 1>), dim3(blocks), dim3(256), 0, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
+      case 2: hipLaunchKernelGGL((k_blk_grad<NB, 2>), dim3(blocks), dim3(256), 0, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
+      case 3: hipLaunchKernelGGL((k_blk_grad<NB, 3>), dim3(blocks), dim3(256), 0, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
+      default: hipLaunchKernelGGL((k_blk_grad<NB, 4>), dim3(blocks), dim3(256), 0, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
+    }
+    return hipGetLastError();
+  };
+  if (c->blk_nb == 2) e = launch(std::integral_constant<int, 2>());
+  else if (c->blk_nb == 3) e = launch(std::integral_constant<int, 3>());
+  else e = launch(std::integral_constant<int, 4>());
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blk_grad launch: %s", hipGetErrorString(e));
+  return QOC_OK;
+}
+
+// grape_sensitivity: λ by the block backward chain (penalty, co-state source and an external λ_N included), then the
+// block gradient for orders 1..4; the exact (Fréchet) gradient runs its own dense kernel on the same λ.
+int blk_backward(qoc_ctx* c, int order, double* d_dJdu) {
+  const TChainArgs g = tchain_args(c);
+  const BlkArgs bk = blk_args(c);
+  const size_t lds = blk_lds(c->N, c->m);
+  int mk = mark_begin(c, 2);
+  const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
+    constexpr int NB = decltype(NB_)::value;
+    constexpr bool CH = decltype(CH_)::value;
+    hipLaunchKernelGGL((k_blk_bwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blk_bwd launch: %s", hipGetErrorString(e));
+  if (order == QOC_DUKDP_EXACT) {
+    mk = mark_begin(c, 3);
+    const int r = frechet_grad<double>(c, d_dJdu);
+    mark_end(c, mk);
+    return r;
+  }
+  return blk_grad(c, order, false, d_dJdu);
+}
+
+// qoc_eval_dev with a built-in cost, no penalty and no co-state source: the forward chain and the μ recurrence
+// (λ_k = coef ⊙ μ_k, src/penalty_fcns.jl:19-22, 35-40) in one launch, then the gradient with the coefficients.
+bool blk_concurrent_ok(const qoc_ctx* c, int order) {
+  return blk_active(c) && c->concurrent && order >= 1 && order <= BLK_ORDMAX &&
+         (c->cost_kind == QOC_COST_TRACE || c->cost_kind == QOC_COST_ZCAL) && c->mu == 0.0 && !c->src_on;
+}
+
+int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
+  if (!c->d_coef_mu) {
+    HIPCHK(c, hipMalloc((void**)&c->d_coef_mu, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
+    c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
+  }
+  int r = tchain_prep(c);
+  if (r) return r;
+  const TChainArgs gf = tchain_args(c);
+  TChainArgs gb = tchain_args(c);
+  gb.mu_mode = 1;
+  const BlkArgs bk = blk_args(c);
+  const size_t lds = blk_lds(c->N, c->m);
+  const int mk = mark_begin(c, 1);
+  const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
+    constexpr int NB = decltype(NB_)::value;
+    constexpr bool CH = decltype(CH_)::value;
+    hipLaunchKernelGGL((k_blk_dual<NB, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blk_dual launch: %s", hipGetErrorString(e));
+  c->fwd_captured = false;
+  c->props_since_reset++;
+  if ((r = blk_grad(c, order, true, d_dJdu))) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_coef_mu, c->d_coef, (size_t)c->B * 2 * c->m * sizeof(cx<double>),
+                           hipMemcpyDeviceToDevice, c->stream));
+  c->L_is_mu = true;
+  c->last_eval_mode = 4;
+  return QOC_OK;
+}
+
+}  // namespace qoc_host

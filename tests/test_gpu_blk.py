@@ -1,0 +1,223 @@
+"""The block path (csrc/qoc_blk.hpp): generators whose union sparsity pattern splits into small invariant blocks
+(cavity-qubit: 2 x 2 blocks, zz coupling: 3 x 3) run the chains and the gradient block by block.  Checked through
+the C ABI against the oracle (the reference's dense algorithm: src/gradient_computations.jl:17-29 forward, :52-58
+co-states, :65-74 + :177-223 the gradient) and against the dense Taylor-action kernels (QOC_BLOCKS=0), at the
+fp64 bar of SURVEY.md §8c: |ΔJ| <= 1e-12, ||ΔdJdu|| / ||dJdu|| <= 1e-10 per seed, states and co-states 1e-12
+relative to their largest entry.
+"""
+import numpy as np
+import pytest
+
+import qoc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases():
+    from qoc_amd import systems
+    out = {}
+    p = systems.zz_problem(60, tgate=6.0)  # N = 9, 3 blocks of 3, m = 4, nu = 2
+    out["zz"] = (p, systems.zz_controls(3, 60, 6.0, seed=61))
+    p = systems.cavity_problem(N_cavity=10, Nt=50)  # N = 20, 10 blocks of 2, m = 2
+    out["cavity20"] = (p, systems.cavity_controls(3, p.Nt, seed=62))
+    p = systems.cavity_problem(N_cavity=20, Nt=40)  # N = 40 (the BASELINE system), 20 blocks of 2
+    out["cavity40"] = (p, systems.cavity_controls(2, p.Nt, seed=63))
+    return out
+
+
+def _block_problem(NB=4, nblk=5, nu=2, m=3, Nt=30, seed=0):
+    """Random skew-Hermitian generators with nblk blocks of NB rows under a random permutation (a block of
+    NB - 1 rows too, so that padding is exercised)."""
+    from qoc_amd import systems
+    rng = np.random.default_rng(seed)
+    sizes = [NB] * (nblk - 1) + [NB - 1]
+    N = sum(sizes)
+    perm = rng.permutation(N)
+    gens = []
+    for j in range(nu + 1):
+        H = np.zeros((N, N), complex)
+        o = 0
+        for s in sizes:
+            G = rng.standard_normal((s, s)) + 1j * rng.standard_normal((s, s))
+            H[o:o + s, o:o + s] = (G + G.conj().T) / 2
+            o += s
+        H = H[np.ix_(perm, perm)]
+        gens.append(-1j * H * (0.08 if j == 0 else 0.05))
+    x0 = np.linalg.qr(rng.standard_normal((N, m)) + 1j * rng.standard_normal((N, m)))[0]
+    xt = np.linalg.qr(rng.standard_normal((N, m)) + 1j * rng.standard_normal((N, m)))[0]
+    prob = systems.Problem("blocks", gens[0], gens[1:], x0, xt, float(m), Nt, "fp64")
+    u = rng.uniform(-1, 1, size=(2, nu, Nt))
+    return prob, u
+
+
+def _engine(prob, B, blocks, monkeypatch, penalty=None, chain="taylor"):
+    from qoc_amd import GrapeEngine
+    monkeypatch.setenv("QOC_BLOCKS", "1" if blocks else "0")
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
+    e.set_cost_trace(prob.x_target, prob.n)
+    e.set_chain(chain)
+    if penalty is not None:
+        e.set_state_penalty(*penalty)
+    return e
+
+
+def _eval(e, u, device, order=3):
+    if not device:
+        J = e.propagate(u)
+        return J, e.grape_sensitivity(u, order)
+    import torch
+    B, nu, Nt = u.shape
+    ud = torch.from_numpy(np.ascontiguousarray(np.transpose(u, (0, 2, 1)))).cuda()
+    Jd = torch.empty(B, dtype=torch.float64, device="cuda")
+    gd = torch.empty(B, Nt, nu, dtype=torch.float64, device="cuda")
+    e.eval_device(ud.data_ptr(), order, Jd.data_ptr(), gd.data_ptr())
+    e.synchronize()
+    return Jd.cpu().numpy(), np.transpose(gd.cpu().numpy(), (0, 2, 1))
+
+
+def _assert_seed(J, g, Jr, gr, tag):
+    assert abs(J - Jr) <= 1e-12, (tag, J - Jr)
+    rel = np.linalg.norm(g - gr) / np.linalg.norm(gr)
+    assert rel <= 1e-10, (tag, rel)
+
+
+@pytest.mark.parametrize("name", ["zz", "cavity20", "cavity40"])
+@pytest.mark.parametrize("device", [False, True])
+def test_blocks_match_oracle_and_dense_chains(built_lib, monkeypatch, name, device):
+    prob, u = _cases()[name]
+    B = u.shape[0]
+    e = _engine(prob, B, True, monkeypatch)
+    J, g = _eval(e, u, device)
+    info = e.info()
+    assert info["chain_kernel"] == "blocks", info
+    assert info["backward"] == ("blocks" if device else "generic"), info
+    xs = [e.state(k, seed=0) for k in (1, prob.Nt // 2, prob.Nt)]
+    lams = [e.costate(k, seed=0) for k in (0, prob.Nt // 2, prob.Nt)]
+    e.close()
+    ed = _engine(prob, B, False, monkeypatch)
+    Jd, gd = _eval(ed, u, device)
+    assert ed.info()["chain_kernel"] in ("mfma_regs", "mfma_lds")
+    ed.close()
+    for b in range(B):
+        J0, g0, c0 = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, (name, b))
+        _assert_seed(J[b], g[b], Jd[b], gd[b], (name, b, "dense"))
+        if b == 0:
+            xsc = max(np.abs(x).max() for x in c0.x)
+            for x, k in zip(xs, (1, prob.Nt // 2, prob.Nt)):
+                assert np.abs(x - c0.x[k]).max() <= 1e-12 * xsc, ("x", k)
+            lsc = max(np.abs(lam).max() for lam in c0.lam)
+            for lam, k in zip(lams, (0, prob.Nt // 2, prob.Nt)):
+                assert np.abs(lam - c0.lam[k]).max() <= 1e-12 * lsc, ("lambda", k)
+
+
+@pytest.mark.parametrize("order", [1, 2, 3, 4, "exact"])
+@pytest.mark.parametrize("device", [False, True])
+def test_blocks_gradient_orders(built_lib, monkeypatch, order, device):
+    """expm_jacobian! orders 1..4 (src/gradient_computations.jl:177-213) in the block gradient; the exact Fréchet
+    gradient (opt-in) runs its dense kernel on the block chains' states and co-states."""
+    from qoc_amd import systems
+    prob = systems.zz_problem(50, tgate=5.0)
+    u = systems.zz_controls(2, 50, 5.0, seed=64)
+    e = _engine(prob, 2, True, monkeypatch)
+    J, g = _eval(e, u, device and order != "exact", order)
+    assert e.info()["chain_kernel"] == "blocks"
+    e.close()
+    for b in range(2):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=order)
+        _assert_seed(J[b], g[b], J0, g0, (order, b))
+
+
+@pytest.mark.parametrize("poly", ["taylor", "chebyshev"])
+def test_blocks_penalty_and_costate_source(built_lib, monkeypatch, poly):
+    """The state penalty (src/penalty_fcns.jl:1-11: L in the forward, 2 mu x_k added to λ_k in the backward) and a
+    caller's dL/dx closure (qoc_set_costate_source) on the block chains, Taylor and Chebyshev terms."""
+    from qoc_amd import systems
+    monkeypatch.setenv("QOC_TCHAIN_POLY", poly)
+    prob = systems.zz_problem(40, tgate=4.0)
+    u = systems.zz_controls(2, 40, 4.0, seed=65)
+    qb = systems.QuantumBasis([3, 3])
+    pen = (qb(["20", "21", "22"]), [0, 1, 2, 3], 0.37)
+    e = _engine(prob, 2, True, monkeypatch, penalty=pen)
+    J = e.propagate(u)
+    g = e.grape_sensitivity(u, 3)
+    info = e.info()
+    assert info["chain_kernel"] == "blocks" and info["chain_poly"] == poly
+    e.close()
+    for b in range(2):
+        Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3, penalty=pen)
+        _assert_seed(J[b], g[b], Jr, gr, ("penalty", b))
+    # the same penalty as a co-state source: dL/dx(x_k) from the oracle's states, the cost's L added by hand
+    Lf, dLf = O.setup_state_penalty(*pen)
+    e = _engine(prob, 2, True, monkeypatch)
+    J = e.propagate(u)
+    src = np.stack([np.stack([dLf(e.state(k, seed=b)) for k in range(prob.Nt + 1)]) for b in range(2)])
+    e.set_costate_source(src)
+    g = e.grape_sensitivity(u, 3)
+    e.close()
+    for b in range(2):
+        Jr, gr, c = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3, penalty=pen)
+        assert abs(J[b] + sum(Lf(x) for x in c.x) - Jr) <= 1e-12
+        assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
+
+
+@pytest.mark.parametrize("NB,nu,m", [(4, 2, 3), (4, 1, 1), (3, 2, 2), (2, 1, 5)])
+@pytest.mark.parametrize("poly", ["taylor", "chebyshev"])
+def test_blocks_random_permuted_blocks(built_lib, monkeypatch, NB, nu, m, poly):
+    """Random block-diagonal skew-Hermitian generators hidden by a permutation (the detection works on the pattern,
+    not on contiguous rows), a short last block (padding lanes), one or two controls, odd column counts."""
+    monkeypatch.setenv("QOC_TCHAIN_POLY", poly)
+    prob, u = _block_problem(NB=NB, nblk=5, nu=nu, m=m, seed=NB * 10 + nu + m)
+    for device in (False, True):
+        e = _engine(prob, 2, True, monkeypatch)
+        J, g = _eval(e, u, device)
+        assert e.info()["chain_kernel"] == "blocks"
+        e.close()
+        for b in range(2):
+            J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+            _assert_seed(J[b], g[b], J0, g0, (NB, nu, m, device, b))
+
+
+def test_blocks_external_cost_and_zcalibrated(built_lib, monkeypatch):
+    """An external λ_N (qoc_grape_sensitivity's lambda_final: the caller's dJfinal_dx closure) and the z-calibrated
+    cost (src/penalty_fcns.jl:27-42) on the block path; the z-calibrated gradient is held to the oracle's gradient
+    family g(Δθ) within the per-seed calibration-phase bound (see tests/test_gpu_parity.py)."""
+    from qoc_amd import GrapeEngine, systems
+    monkeypatch.setenv("QOC_BLOCKS", "1")
+    prob = systems.zz_problem(40, tgate=4.0)
+    u = systems.zz_controls(2, 40, 4.0, seed=66)
+    Jf, dJf = O.setup_infidelity(prob.x_target, prob.n)
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2)
+    e.set_cost_external()
+    e.set_chain("taylor")
+    e.propagate(u)
+    lam = np.stack([dJf(e.state(prob.Nt, seed=b)) for b in range(2)])
+    g = e.grape_sensitivity(u, 3, lambda_final=lam)
+    assert e.info()["chain_kernel"] == "blocks"
+    e.close()
+    for b in range(2):
+        _, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        assert np.linalg.norm(g[b] - g0) / np.linalg.norm(g0) <= 1e-10
+    Jz, _ = O.setup_infidelity_zcalibrated(prob.x_target)
+    for device in (False, True):
+        e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2)
+        e.set_cost_zcalibrated(prob.x_target)
+        e.set_chain("taylor")
+        J, g = _eval(e, u, device)
+        assert e.info()["chain_kernel"] == "blocks"
+        e.close()
+        for b in range(2):
+            xN = O.propagate(prob.A0, prob.A, u[b], prob.x0)[-1]
+            assert abs(J[b] - Jz(xN)) <= 1e-12
+            res, dth = O.zcal_gradient_match(g[b], prob.A0, prob.A, u[b], prob.x0, prob.x_target, order=3)
+            assert res <= 1e-10 and abs(dth) <= O.zcal_dtheta_bound(prob.x_target, xN), (device, b, res, dth)
+
+
+def test_blocks_off_for_dense_generators(built_lib, monkeypatch):
+    """A coupling between every pair of blocks (the tunable bus: two parity blocks of 14 and 13 rows) keeps the dense
+    chains: blocks above 4 rows take no block lanes."""
+    from qoc_amd import systems
+    prob = systems.tunable_bus_problem(Nt=32, tgate=350.0 * 32 / 2000)
+    e = _engine(prob, 1, True, monkeypatch)
+    assert e.info()["chain_kernel"] != "blocks"
+    e.close()

@@ -14,16 +14,34 @@ import qoc_oracle as O
 pytestmark = pytest.mark.gpu
 
 
-CHAINS = ["propagators", "taylor"]
+# "taylor" takes the block chains where the generators have small invariant blocks (zz, cavity: qoc_blk.hpp);
+# "taylor_dense" keeps the dense Taylor-action kernels there (QOC_BLOCKS=0 at qoc_set_generators)
+CHAINS = ["propagators", "taylor", "taylor_dense"]
 
 
-def _engine(prob, B, precision="fp64", chain=None):
+def _engine(prob, B, precision="fp64", chain=None, cost=True):
+    import os
     from qoc_amd import GrapeEngine
-    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B, precision=precision)
-    e.set_cost_trace(prob.x_target, prob.n)
+    dense = chain == "taylor_dense"
+    old = os.environ.get("QOC_BLOCKS")
+    if dense:
+        os.environ["QOC_BLOCKS"] = "0"
+    try:
+        e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B, precision=precision)
+    finally:
+        if dense:
+            if old is None:
+                os.environ.pop("QOC_BLOCKS")
+            else:
+                os.environ["QOC_BLOCKS"] = old
+    if cost:
+        e.set_cost_trace(prob.x_target, prob.n)
     if chain is not None:
+        chain = "taylor" if dense else chain
         e.set_chain(chain)
         assert e.info()["chain"] == chain
+        if dense:
+            assert e.info()["chain_kernel"] != "blocks"
     return e
 
 
@@ -260,8 +278,7 @@ def test_per_seed_x0(built_lib, chain):
     u = systems.zz_controls(2, 20, 2.0, seed=2)
     rng = np.random.default_rng(5)
     x0s = np.stack([np.linalg.qr(rng.standard_normal((9, 4)) + 1j * rng.standard_normal((9, 4)))[0] for _ in range(2)])
-    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2)
-    e.set_chain(chain)
+    e = _engine(prob, 2, chain=chain, cost=False)
     e.set_x0(x0s, per_seed=True)
     e.set_cost_trace(prob.x_target, 4)
     J = e.propagate(u)
@@ -461,9 +478,7 @@ def test_external_cost_and_costates(built_lib, chain):
     from qoc_amd import systems
     prob = systems.cavity_problem(N_cavity=8, Nt=25)
     u = systems.cavity_controls(2, prob.Nt, seed=31)
-    from qoc_amd import GrapeEngine
-    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=2)
-    e.set_chain(chain)
+    e = _engine(prob, 2, chain=chain, cost=False)
     e.set_cost_external()
     e.propagate(u)
     rng = np.random.default_rng(3)
@@ -583,6 +598,7 @@ def test_overlapped_backward_ranges_are_bit_identical(built_lib, monkeypatch, ra
     (QOC_BWD_CHUNKS=1), with a state penalty and a ragged Nt, and matches the oracle.  QOC_BWD_PRESTATE=1: the
     state side (P1, P2) of every slice first, beside the first range (k_grad_rr_s), then q + p reading them."""
     monkeypatch.setenv("QOC_BWD_PRESTATE", ranges[2])
+    monkeypatch.setenv("QOC_BLOCKS", "0")  # the dense chains' ranges (the block chains run one backward launch)
     from qoc_amd import systems
     prob = systems.cavity_problem(N_cavity=10, Nt=131)
     u = systems.cavity_controls(3, prob.Nt, seed=17)
@@ -616,6 +632,7 @@ def test_overlapped_backward_with_costate_source_repeated(built_lib, monkeypatch
     row on one engine and once more after a new propagate: every call matches the single-launch backward bitwise
     and the oracle's gradient with the same dL/dx closure."""
     from qoc_amd import systems
+    monkeypatch.setenv("QOC_BLOCKS", "0")  # the dense chains' ranges
     prob = systems.cavity_problem(N_cavity=10, Nt=96)
     u = systems.cavity_controls(2, prob.Nt, seed=23)
     Lo, dLo = O.setup_state_penalty([1, 4], [0, 1], 0.15)

@@ -12,6 +12,12 @@ import qoc_oracle as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _dense_chains(monkeypatch):
+    """These kernels are the dense Taylor-action chains: the block path (qoc_blk.hpp) stays off."""
+    monkeypatch.setenv("QOC_BLOCKS", "0")
+
+
 def _cases():
     from qoc_amd import systems
     out = {}
