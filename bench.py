@@ -82,6 +82,7 @@ def grad_flops(N, m, nu, Nt, B, order, captured=False):
 def block_sizes(prob):
     """Row counts of the generators' invariant blocks (connected components of the union sparsity pattern of
     A_0..A_nu), as the engine's qoc_set_generators finds them for the block chains (csrc/qoc_blk.hpp)."""
+    import numpy as np
     from scipy.sparse import csr_matrix
     from scipy.sparse.csgraph import connected_components
     M = np.abs(np.asarray(prob.A0)) > 0

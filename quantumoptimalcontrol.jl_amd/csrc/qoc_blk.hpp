@@ -364,6 +364,271 @@ __global__ __launch_bounds__(BLK_MAXT) void k_blk_dual(const TChainArgs gf, cons
   else blk_bwd_body<NB, CHEB>(gb, bk, seed);
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Blocks of 5..16 rows (the tunable bus: two parity blocks of 14 and 13 rows at N = 27): one wave per (block,
+// state column pair) runs TChainRot<1>'s MFMA term (qoc_tchain.hpp) on the block's 16-row state.  In the
+// v_mfma_f64_4x4x4_4b layout a lane's D element (local row 4b + hi, column lo) is block b's B operand for k = hi of
+// a k-quad, and a DPP row_ror by 4j hands block b the k-quad q_j(b) of the state; the A operands hold
+// Ã[r(4b + lo)][r(4 q_j(b) + hi)] with r() the block's row list (brow, 16 entries per block, -1 padding), so the
+// dense G = 2 chain's 32 MFMAs per term become 8 per block wave with no cross-wave exchange.  The gradient stays the
+// dense fused kernels: with captures (D1 = Â v, D2 = Â y_1 of each slice, the layout TChainArgs::cap1 / cap2
+// documents) the concurrent eval's contraction k_grad_rr_c, else k_grad_rr_q / p from the stored states.
+// ---------------------------------------------------------------------------------------------------------
+struct BlkRotLane {
+  int n, cp, beta;
+  int rowE;     // global row of this lane's D element (-1: padding, or no block)
+  int colD;     // state column of the D element
+  bool act;     // rowE >= 0 && colD < m
+  int rowA;     // global row of the lane's A-operand entries
+  int colA[4];  // global column of the A-operand entry of rotation j
+  __device__ __forceinline__ void setup(const BlkArgs& bk, int m) {
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int b = (l >> 2) & 3, kl = l >> 4, lo = l & 3;
+    const bool wok = w < bk.nblk * ((m + 1) / 2);
+    beta = wok ? w % bk.nblk : 0;
+    cp = wok ? w / bk.nblk : 0;
+    n = lo;
+    colD = 2 * cp + (n >> 1);
+    const int* rb = bk.brow + beta * 16;
+    rowE = wok ? rb[4 * b + kl] : -1;
+    act = rowE >= 0 && colD < m;
+    rowA = wok ? rb[4 * b + lo] : -1;
+    const int q[4] = {b, __builtin_amdgcn_update_dpp(0, b, 0x124, 0xf, 0xf, false),   // row_ror:4
+                      __builtin_amdgcn_update_dpp(0, b, 0x128, 0xf, 0xf, false),      // row_ror:8
+                      __builtin_amdgcn_update_dpp(0, b, 0x12C, 0xf, 0xf, false)};     // row_ror:12
+#pragma unroll
+    for (int j = 0; j < 4; ++j) colA[j] = wok ? rb[4 * q[j] + kl] : -1;
+  }
+  // the A-operand entries of Ã_0..Ã_2 (HERM: of Ã_j^H), zero outside the block and for j > nu
+  template <bool HERM>
+  __device__ __forceinline__ void load_gen(const cx<double>* __restrict__ At, int N, int nu, double (&gr)[3][4],
+                                           double (&gi)[3][4]) const {
+    const size_t NN = (size_t)N * N;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const bool ok = j <= nu && rowA >= 0 && colA[x] >= 0;
+        const int rr = max(rowA, 0), cc = max(colA[x], 0);
+        const cx<double> v = At[(size_t)min(j, nu) * NN + (HERM ? cc + (size_t)N * rr : rr + (size_t)N * cc)];
+        gr[j][x] = ok ? v.r : 0.0;
+        gi[j][x] = ok ? (HERM ? -v.i : v.i) : 0.0;
+      }
+  }
+};
+
+// one slice on the wave's 16-row block state (one element per lane, TChainRot<1>::step without the LDS mirror);
+// CAP: D1, D2 of the first substep
+template <bool CHEB>
+__device__ __forceinline__ void blkrot_slice(const double (&ar)[4], const double (&ai)[4], double& acc, bool act,
+                                             int n, int P, int s, double phr, double phi, double cl,
+                                             const double* __restrict__ invt, double& cd1, double& cd2) {
+  using R = TChainRot<1>;
+  for (int sub = 0; sub < s; ++sub) {
+    double y = act ? acc : 0.0, ym2 = 0.0;
+    acc = (CHEB ? bcast(cl, 0) : 1.0) * y;
+    double bv[4] = {y, R::mv<0x124>(y), R::mv<0x128>(y), R::mv<0x12C>(y)};
+    for (int t = 1; t <= P; ++t) {
+      const double ct = CHEB ? bcast(cl, t) : invt[t];
+      __builtin_amdgcn_sched_barrier(0);
+      double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        d0 = MF<double>::mma4(ar[j], bv[j], d0);
+        d1 = MF<double>::mma4(ai[j], bv[j], d1);
+      }
+      const double o = R::mv<0xB1>(d1);  // quad_perm [1,0,3,2]: (Ai y)[n ^ 1]
+      const double D = (n & 1) ? d0 + o : d0 - o;
+      if (sub == 0 && t == 1) cd1 = D;
+      if (sub == 0 && t == 2) cd2 = D;
+      double z;
+      if constexpr (CHEB) {
+        z = t == 1 ? 0.5 * D : D + ym2;
+        ym2 = y;
+        acc = fma(ct, z, acc);
+      } else {
+        z = D * ct;
+        acc += z;
+      }
+      y = z;
+      bv[0] = y;
+      bv[1] = R::mv<0x124>(y);
+      bv[2] = R::mv<0x128>(y);
+      bv[3] = R::mv<0x12C>(y);
+    }
+    if (sub == s - 1) {
+      const double o = R::mv<0xB1>(acc);
+      acc = (n & 1) ? phr * acc + phi * o : phr * acc - phi * o;
+    }
+  }
+}
+
+__device__ __forceinline__ void blkrot_form(const double (&gr)[3][4], const double (&gi)[3][4], const double (&u)[2],
+                                            double scale, double (&ar)[4], double (&ai)[4]) {
+  const double u1 = u[0] * scale, u2 = u[1] * scale;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    ar[x] = fma(u2, gr[2][x], fma(u1, gr[1][x], scale * gr[0][x]));
+    ai[x] = fma(u2, gi[2][x], fma(u1, gi[1][x], scale * gi[0][x]));
+  }
+}
+
+template <bool CHEB>
+__device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkArgs& bk, const int b) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* invt = reinterpret_cast<double*>(smem);
+  double* red = invt + 64;
+  double* xN = red + 16;
+  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, tid = threadIdx.x, nthr = blockDim.x;
+  const size_t Nm = (size_t)N * m;
+  for (int e = tid; e < 64; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
+  BlkRotLane ln;
+  ln.setup(bk, m);
+  double gr[3][4], gi[3][4];
+  ln.load_gen<false>((const cx<double>*)g.At, N, nu, gr, gi);
+  const cx<double>* x0b = (const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0);
+  double* Xb = reinterpret_cast<double*>((cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm);
+  double* const sink = tchain_sink(g);
+  const size_t o = (size_t)ln.colD * N + max(ln.rowE, 0), oe = 2 * o + (ln.n & 1);
+  double acc = 0.0;
+  if (ln.act) {
+    const cx<double> v = x0b[o];
+    acc = (ln.n & 1) ? v.i : v.r;
+  }
+  const bool pm = ln.act && g.pmask && g.pmask[o];
+  const bool cap = g.cap1 != nullptr;
+  double* c1b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm) : nullptr;
+  double* c2b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm) : nullptr;
+  double pen = 0.0;
+  __syncthreads();
+  *(ln.act ? Xb + oe : sink) = acc;
+  pen += pm ? acc * acc : 0.0;
+  const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
+  const TStep* stb = g.steps + (size_t)b * Nt;
+  const double* ub = g.u + (size_t)b * Nt * nu;
+  constexpr int PD = 2;
+  TPreN<2> nx[PD];
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int ki = min(i, Nt - 1);
+    tpre_load<2, CHEB, false>(stb + ki, ub + (size_t)ki * nu, nu, nx[i], CHEB ? ceb + (size_t)ki * TCHEB_STRIDE : nullptr);
+  }
+  for (int k0 = 0; k0 < Nt; k0 += PD)
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+      const int k = k0 + i;
+      if (k >= Nt) break;
+      const TPreN<2>& st = nx[i];
+      const int P = __builtin_amdgcn_readfirstlane(st.P), s = __builtin_amdgcn_readfirstlane(st.s);
+      double ar[4], ai[4], cd1 = 0.0, cd2 = 0.0;
+      blkrot_form(gr, gi, st.u, st.scale, ar, ai);
+      blkrot_slice<CHEB>(ar, ai, acc, ln.act, ln.n, P, s, st.pr, st.pi, st.cl, invt, cd1, cd2);
+      const int kn = min(k + PD, Nt - 1);
+      tpre_load<2, CHEB, false>(stb + kn, ub + (size_t)kn * nu, nu, nx[i], CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
+      *(ln.act ? Xb + (size_t)(k + 1) * 2 * Nm + oe : sink) = acc;
+      pen += pm ? acc * acc : 0.0;
+      const bool to = cap && ln.act;
+      *(to ? c1b + (size_t)k * 2 * Nm + oe : sink) = cd1;
+      *(to ? c2b + (size_t)k * 2 * Nm + oe : sink + 1) = cd2;
+    }
+  if (ln.act) xN[oe] = acc;
+  __syncthreads();
+  chain_costs<double>(N, m, (const cx<double>*)g.Xt, [&](int q) { return cx<double>{xN[2 * q], xN[2 * q + 1]}; },
+                      g.cost_kind, g.n_norm, block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * 2 * m, g.sc);
+}
+
+template <bool CHEB>
+__device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkArgs& bk, const int b) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* invt = reinterpret_cast<double*>(smem);
+  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, tid = threadIdx.x, nthr = blockDim.x;
+  const size_t Nm = (size_t)N * m;
+  for (int e = tid; e < 64; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
+  BlkRotLane ln;
+  ln.setup(bk, m);
+  double gr[3][4], gi[3][4];
+  ln.load_gen<true>((const cx<double>*)g.At, N, nu, gr, gi);
+  const double* Xb = reinterpret_cast<const double*>((const cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm);
+  double* Lb = reinterpret_cast<double*>((cx<double>*)g.L + (size_t)b * (Nt + 1) * Nm);
+  const double* srcb =
+      (g.src && !g.mu_mode) ? reinterpret_cast<const double*>((const cx<double>*)g.src + (size_t)b * (Nt + 1) * Nm) : nullptr;
+  const unsigned char* pmask = g.mu_mode ? nullptr : g.pmask;
+  const double tmu = 2.0 * g.mu;
+  double* const sink = tchain_sink(g);
+  const size_t o = (size_t)ln.colD * N + max(ln.rowE, 0), oe = 2 * o + (ln.n & 1);
+  const bool pm = ln.act && pmask && pmask[o];
+  const bool srcl = ln.act && srcb;
+  double acc = 0.0;
+  if (ln.act) {
+    cx<double> v;
+    if (g.mu_mode) {
+      v = ((const cx<double>*)g.Xt)[o];
+    } else if (g.cost_kind == COST_EXTERNAL) {
+      v = reinterpret_cast<const cx<double>*>(Lb)[(size_t)Nt * Nm + o];
+    } else {
+      const cx<double> cf = g.coef[(size_t)b * 2 * m + ln.colD], t = ((const cx<double>*)g.Xt)[o];
+      v = cx<double>{cf.r * t.r - cf.i * t.i, cf.r * t.i + cf.i * t.r};
+    }
+    acc = (ln.n & 1) ? v.i : v.r;
+    if (pm) acc += tmu * Xb[(size_t)Nt * 2 * Nm + oe];
+    if (srcl) acc += srcb[(size_t)Nt * 2 * Nm + oe];
+  }
+  const bool cap = g.cap1 != nullptr;
+  double* c1b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm) : nullptr;
+  double* c2b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm) : nullptr;
+  __syncthreads();
+  *(ln.act ? Lb + (size_t)Nt * 2 * Nm + oe : sink) = acc;
+  const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
+  const TStep* stb = g.steps + (size_t)b * Nt;
+  const double* ub = g.u + (size_t)b * Nt * nu;
+  constexpr int PD = 2;
+  TPreN<2> nx[PD];
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int ki = max(Nt - 1 - i, 0);
+    tpre_load<2, CHEB, false>(stb + ki, ub + (size_t)ki * nu, nu, nx[i], CHEB ? ceb + (size_t)ki * TCHEB_STRIDE : nullptr);
+  }
+  for (int k0 = Nt - 1; k0 >= 0; k0 -= PD)
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+      const int k = k0 - i;
+      if (k < 0) break;
+      const TPreN<2>& st = nx[i];
+      const int P = __builtin_amdgcn_readfirstlane(st.P), s = __builtin_amdgcn_readfirstlane(st.s);
+      const size_t ok_ = (size_t)k * 2 * Nm + oe;
+      double xa = pm ? tmu * Xb[ok_] : 0.0;  // 2μ x_k on the mask + the caller's dL/dx(x_k), after the slice
+      if (srcl) xa += srcb[ok_];
+      double ar[4], ai[4], cd1 = 0.0, cd2 = 0.0;
+      blkrot_form(gr, gi, st.u, st.scale, ar, ai);
+      blkrot_slice<CHEB>(ar, ai, acc, ln.act, ln.n, P, s, st.pr, -st.pi, st.cl, invt, cd1, cd2);
+      const int kp = max(k - PD, 0);
+      tpre_load<2, CHEB, false>(stb + kp, ub + (size_t)kp * nu, nu, nx[i], CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
+      acc += xa;
+      *(ln.act ? Lb + ok_ : sink) = acc;
+      const bool to = cap && ln.act;
+      *(to ? c1b + ok_ : sink) = cd1;
+      *(to ? c2b + ok_ : sink + 1) = cd2;
+    }
+}
+
+template <bool CHEB>
+__global__ __launch_bounds__(1024) void k_blkrot_fwd(const TChainArgs g, const BlkArgs bk) {
+  blkrot_fwd_body<CHEB>(g, bk, blockIdx.x);
+}
+template <bool CHEB>
+__global__ __launch_bounds__(1024) void k_blkrot_bwd(const TChainArgs g, const BlkArgs bk) {
+  blkrot_bwd_body<CHEB>(g, bk, blockIdx.x);
+}
+template <bool CHEB>
+__global__ __launch_bounds__(1024) void k_blkrot_dual(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk) {
+  const int i = blockIdx.x, B = gridDim.x >> 1;
+  const bool by8 = (B & 7) == 0;
+  const int dir = by8 ? (i >> 3) & 1 : i & 1;
+  const int seed = by8 ? ((i >> 4) << 3) | (i & 7) : i >> 1;
+  if (dir == 0) blkrot_fwd_body<CHEB>(gf, bk, seed);
+  else blkrot_bwd_body<CHEB>(gb, bk, seed);
+}
+
 // The order-ORD gradient per block (expm_jacobian! + _compute_u_sensitivity, src/gradient_computations.jl:177-223):
 // with X = A_k on the block, P_b = X^b x_k and Q_a = (X^H)^a λ_{k+1},
 //   λ^H dU_j x = Σ_{a+b < ORD} <Q_a, A_j P_b> / (a+b+1)! = Σ_b <W_b, A_j P_b>,  W_b = Σ_{a < ORD-b} Q_a / (a+b+1)!

@@ -1255,7 +1255,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[7] = c->m;  // state columns the kernels run on (< the caller's m when compress_states packing is on)
   info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 / 3 concurrent μ recurrence
   info[9] = c->fwd_captured ? 1 : 0;
-  info[10] = blk_active(c) ? 3 : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
+  info[10] = blk_active(c) ? (blk_rot(c) ? 4 : 3) : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
   return QOC_OK;
 }
 

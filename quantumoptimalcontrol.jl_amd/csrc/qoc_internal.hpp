@@ -154,7 +154,7 @@ struct qoc_ctx {
                                  // one dual launch, 4 block chains' concurrent eval (qoc_get_info)
   // generators with small invariant blocks (qoc_blk.hpp, detected at qoc_set_generators; QOC_BLOCKS=0 off): the
   // chains and the gradient run per block
-  int blk_nb = 0;                // padded block size 2 / 3 / 4 (0: no block path)
+  int blk_nb = 0;                // padded block size 2 / 3 / 4 (VALU lanes), 16 (MFMA block waves), 0: no block path
   int nblk = 0;                  // blocks
   int* d_brow = nullptr;         // nblk x blk_nb rows of each block (-1 padding)
   // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
@@ -219,6 +219,8 @@ template <typename T>
 int run_forward(qoc_ctx* c);
 template <typename T>
 int run_backward(qoc_ctx* c, int order, double* d_dJdu);
+template <typename T>
+int dense_gradient(qoc_ctx* c, int order, double* d_dJdu);
 
 // ---- qoc_run_big.hip ----
 size_t big_ws_elems_per_item(int N, int m);
@@ -263,7 +265,9 @@ int tchain_backward_captured(qoc_ctx* c, double* d_dJdu);
 template <typename T>
 int tchain_eval_concurrent(qoc_ctx* c, double* d_dJdu);
 bool tchain_concurrent_ok(const qoc_ctx* c, int order);
+bool tchain_cap_ok(const qoc_ctx* c);
 int ensure_pws(qoc_ctx* c);
+int ensure_stream2(qoc_ctx* c, int nev);
 template <typename T>
 int tchain_backward_overlapped(qoc_ctx* c, double* d_dJdu);
 hipError_t launch_pade_units(qoc_ctx* c, long long units);
@@ -273,6 +277,7 @@ int tchain_prep(qoc_ctx* c);
 // ---- qoc_run_blk.hip ----
 int blk_detect(qoc_ctx* c);
 bool blk_active(const qoc_ctx* c);
+bool blk_rot(const qoc_ctx* c);
 int blk_forward(qoc_ctx* c);
 int blk_backward(qoc_ctx* c, int order, double* d_dJdu);
 bool blk_concurrent_ok(const qoc_ctx* c, int order);

@@ -100,6 +100,15 @@ int run_backward(qoc_ctx* c, int order, double* d_dJdu) {
     mark_end(c, mk);
     if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_chain_bwd launch: %s", hipGetErrorString(e));
   }
+  return dense_gradient<T>(c, order, d_dJdu);
+}
+
+// the gradient from the stored x_k and λ_k (every chain kind): the exact Fréchet kernel, the fused order-3
+// kernels, the GEMM-shaped order-3 path or the per-slice k_grad
+template <typename T>
+int dense_gradient(qoc_ctx* c, int order, double* d_dJdu) {
+  int mk;
+  size_t lds;
   if (order == QOC_DUKDP_EXACT) {
     mk = mark_begin(c, 3);
     int r = frechet_grad<T>(c, d_dJdu);
@@ -132,5 +141,7 @@ template int run_forward<double>(qoc_ctx*);
 template int run_forward<float>(qoc_ctx*);
 template int run_backward<double>(qoc_ctx*, int, double*);
 template int run_backward<float>(qoc_ctx*, int, double*);
+template int dense_gradient<double>(qoc_ctx*, int, double*);
+template int dense_gradient<float>(qoc_ctx*, int, double*);
 
 }  // namespace qoc_host

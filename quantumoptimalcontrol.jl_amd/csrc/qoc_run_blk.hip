@@ -45,8 +45,10 @@ int blk_detect(qoc_ctx* c) {
   }
   size_t mx = 0;
   for (const auto& bl : blocks) mx = std::max(mx, bl.size());
-  if (mx > (size_t)BLK_NBMAX) return QOC_OK;
-  const int NB = mx <= 2 ? 2 : mx <= 3 ? 3 : 4;
+  // blocks of <= 4 rows: the VALU lanes; 5..16 rows: one MFMA wave per block (only when the dense state needs more
+  // than one 16-row group, N > 16: at N <= 16 the dense register chain already runs one wave per column pair)
+  if (mx > 16 || (mx > (size_t)BLK_NBMAX && N <= 16)) return QOC_OK;
+  const int NB = mx <= 2 ? 2 : mx <= 3 ? 3 : mx <= 4 ? 4 : 16;
   const int nblk = (int)blocks.size();
   std::vector<int> brow((size_t)nblk * NB, -1);
   for (int b = 0; b < nblk; ++b)
@@ -64,9 +66,13 @@ int blk_detect(qoc_ctx* c) {
 
 // The block path runs the Taylor-action chains' fp64 scheme (step records, shifted generators) on unpacked states
 bool blk_active(const qoc_ctx* c) {
-  return c->blk_nb > 0 && c->prec == QOC_FP64 && c->chain_mode == 1 && c->prop_method == QOC_PROP_EXPM && !c->big &&
-         !c->packed && c->nu <= 2 && c->nblk * c->m <= BLK_MAXT && c->nblk <= 256;
+  if (c->blk_nb <= 0 || c->prec != QOC_FP64 || c->chain_mode != 1 || c->prop_method != QOC_PROP_EXPM || c->big ||
+      c->packed || c->nu > 2)
+    return false;
+  if (c->blk_nb == 16) return tchain_mf(c) && c->nblk * ((c->m + 1) / 2) <= 16;  // one wave per (block, column pair)
+  return c->nblk * c->m <= BLK_MAXT && c->nblk <= 256;
 }
+bool blk_rot(const qoc_ctx* c) { return c->blk_nb == 16; }
 
 static BlkArgs blk_args(const qoc_ctx* c) {
   BlkArgs bk{};
@@ -76,12 +82,15 @@ static BlkArgs blk_args(const qoc_ctx* c) {
   return bk;
 }
 
-static int blk_threads(const qoc_ctx* c) { return 64 * ((c->nblk * c->m + 63) / 64); }
+static int blk_threads(const qoc_ctx* c) {
+  return blk_rot(c) ? 64 * c->nblk * ((c->m + 1) / 2) : 64 * ((c->nblk * c->m + 63) / 64);
+}
 
 template <typename F>
 static hipError_t blk_dispatch(const qoc_ctx* c, F&& f) {
   using std::integral_constant;
   switch (c->blk_nb) {
+    case 16: return c->cheb_ran ? f(integral_constant<int, 16>(), std::true_type()) : f(integral_constant<int, 16>(), std::false_type());
     case 2: return c->cheb_ran ? f(integral_constant<int, 2>(), std::true_type()) : f(integral_constant<int, 2>(), std::false_type());
     case 3: return c->cheb_ran ? f(integral_constant<int, 3>(), std::true_type()) : f(integral_constant<int, 3>(), std::false_type());
     case 4: return c->cheb_ran ? f(integral_constant<int, 4>(), std::true_type()) : f(integral_constant<int, 4>(), std::false_type());
@@ -99,7 +108,8 @@ int blk_forward(qoc_ctx* c) {
   const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
     constexpr int NB = decltype(NB_)::value;
     constexpr bool CH = decltype(CH_)::value;
-    hipLaunchKernelGGL((k_blk_fwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    if constexpr (NB == 16) hipLaunchKernelGGL((k_blkrot_fwd<CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    else hipLaunchKernelGGL((k_blk_fwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
     return hipGetLastError();
   });
   mark_end(c, mk);
@@ -146,23 +156,21 @@ int blk_backward(qoc_ctx* c, int order, double* d_dJdu) {
   const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
     constexpr int NB = decltype(NB_)::value;
     constexpr bool CH = decltype(CH_)::value;
-    hipLaunchKernelGGL((k_blk_bwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    if constexpr (NB == 16) hipLaunchKernelGGL((k_blkrot_bwd<CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    else hipLaunchKernelGGL((k_blk_bwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
     return hipGetLastError();
   });
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blk_bwd launch: %s", hipGetErrorString(e));
-  if (order == QOC_DUKDP_EXACT) {
-    mk = mark_begin(c, 3);
-    const int r = frechet_grad<double>(c, d_dJdu);
-    mark_end(c, mk);
-    return r;
-  }
+  if (order == QOC_DUKDP_EXACT || blk_rot(c)) return dense_gradient<double>(c, order, d_dJdu);
   return blk_grad(c, order, false, d_dJdu);
 }
 
 // qoc_eval_dev with a built-in cost, no penalty and no co-state source: the forward chain and the μ recurrence
 // (λ_k = coef ⊙ μ_k, src/penalty_fcns.jl:19-22, 35-40) in one launch, then the gradient with the coefficients.
 bool blk_concurrent_ok(const qoc_ctx* c, int order) {
+  // MFMA block waves: the contraction from the chains' captures (k_grad_rr_c, order 3)
+  if (blk_rot(c) && !(order == 3 && tchain_cap_ok(c))) return false;
   return blk_active(c) && c->concurrent && order >= 1 && order <= BLK_ORDMAX &&
          (c->cost_kind == QOC_COST_TRACE || c->cost_kind == QOC_COST_ZCAL) && c->mu == 0.0 && !c->src_on;
 }
@@ -172,25 +180,41 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
     HIPCHK(c, hipMalloc((void**)&c->d_coef_mu, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
     c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
   }
-  int r = tchain_prep(c);
+  int r = blk_rot(c) ? ensure_pws(c) : QOC_OK;
   if (r) return r;
-  const TChainArgs gf = tchain_args(c);
+  if ((r = tchain_prep(c))) return r;
+  TChainArgs gf = tchain_args(c);
   TChainArgs gb = tchain_args(c);
   gb.mu_mode = 1;
+  if (blk_rot(c)) {  // the first two products of every slice for k_grad_rr_c (forward -> d_pws, μ -> d_gws)
+    const size_t bufN = (size_t)c->N * ((size_t)c->B * (c->Nt + 1) * c->m);
+    gf.cap1 = c->d_pws;
+    gf.cap2 = (cx<double>*)c->d_pws + bufN;
+    gb.cap1 = c->d_gws;
+    gb.cap2 = (cx<double>*)c->d_gws + bufN;
+  }
   const BlkArgs bk = blk_args(c);
   const size_t lds = blk_lds(c->N, c->m);
   const int mk = mark_begin(c, 1);
   const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
     constexpr int NB = decltype(NB_)::value;
     constexpr bool CH = decltype(CH_)::value;
-    hipLaunchKernelGGL((k_blk_dual<NB, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
+    if constexpr (NB == 16) hipLaunchKernelGGL((k_blkrot_dual<CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
+    else hipLaunchKernelGGL((k_blk_dual<NB, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
     return hipGetLastError();
   });
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blk_dual launch: %s", hipGetErrorString(e));
-  c->fwd_captured = false;
+  c->fwd_captured = false;  // the block backward recomputes its own products
   c->props_since_reset++;
-  if ((r = blk_grad(c, order, true, d_dJdu))) return r;
+  if (blk_rot(c)) {
+    const int mg = mark_begin(c, 3);
+    r = grad_rr_cap(c, d_dJdu, c->stream, 0, c->Nt, true);
+    mark_end(c, mg);
+  } else {
+    r = blk_grad(c, order, true, d_dJdu);
+  }
+  if (r) return r;
   HIPCHK(c, hipMemcpyAsync(c->d_coef_mu, c->d_coef, (size_t)c->B * 2 * c->m * sizeof(cx<double>),
                            hipMemcpyDeviceToDevice, c->stream));
   c->L_is_mu = true;

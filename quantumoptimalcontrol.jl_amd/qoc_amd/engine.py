@@ -319,7 +319,7 @@ class GrapeEngine:
                 "backward": {0: "generic", 1: "captured", 2: "concurrent", 3: "concurrent", 4: "blocks"}.get(int(v[8]), "?"),
                 "concurrent_launch": {2: "two_streams", 3: "dual", 4: "dual"}.get(int(v[8])),
                 "fwd_captured": bool(v[9]),
-                "chain_kernel": {0: None, 1: "mfma_lds", 2: "mfma_regs", 3: "blocks"}.get(int(v[10]))}
+                "chain_kernel": {0: None, 1: "mfma_lds", 2: "mfma_regs", 3: "blocks", 4: "blocks_mfma"}.get(int(v[10]))}
 
     def set_chain(self, mode: str = "auto"):
         """How the chains apply exp(A_k) (include/qoc.h qoc_set_chain): 'propagators' forms every U_k (the

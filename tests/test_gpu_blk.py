@@ -214,10 +214,79 @@ def test_blocks_external_cost_and_zcalibrated(built_lib, monkeypatch):
 
 
 def test_blocks_off_for_dense_generators(built_lib, monkeypatch):
-    """A coupling between every pair of blocks (the tunable bus: two parity blocks of 14 and 13 rows) keeps the dense
-    chains: blocks above 4 rows take no block lanes."""
+    """Generators coupling every row (one block of 20 rows) keep the dense chains; so do blocks of 5..16 rows at
+    N <= 16, where the dense register chain already runs one wave per column pair."""
+    prob, _ = _block_problem(NB=4, nblk=2, nu=2, m=2, seed=3)
+    import dataclasses
     from qoc_amd import systems
-    prob = systems.tunable_bus_problem(Nt=32, tgate=350.0 * 32 / 2000)
-    e = _engine(prob, 1, True, monkeypatch)
-    assert e.info()["chain_kernel"] != "blocks"
+    rng = np.random.default_rng(7)
+    H = systems._gue(rng, 20)
+    dense = dataclasses.replace(prob, A0=-0.05j * H, A=[-0.03j * systems._gue(rng, 20), -0.02j * systems._gue(rng, 20)],
+                                x0=np.eye(20, 2, dtype=complex), x_target=np.eye(20, 2, dtype=complex))
+    e = _engine(dense, 1, True, monkeypatch)
+    assert e.info()["chain_kernel"] not in ("blocks", "blocks_mfma")
     e.close()
+    p16, _ = _block_problem(NB=8, nblk=2, nu=1, m=1, seed=4)  # N = 15
+    e = _engine(p16, 1, True, monkeypatch)
+    assert e.info()["chain_kernel"] not in ("blocks", "blocks_mfma")
+    e.close()
+
+
+@pytest.mark.parametrize("which", ["tunable_bus", "tunable_bus_cz"])
+@pytest.mark.parametrize("device", [False, True])
+def test_blocks_mfma_tunable_bus(built_lib, monkeypatch, which, device):
+    """The tunable bus (two parity blocks of 14 and 13 rows at N = 27): one MFMA wave per (block, column pair)
+    instead of the dense two-group register chain; against the oracle and the dense chains.  The CZ variant
+    (m = 4: two column pairs, x0 columns in both blocks)."""
+    from qoc_amd import systems
+    Nt = 48
+    mk = systems.tunable_bus_problem if which == "tunable_bus" else systems.tunable_bus_cz_problem
+    prob = mk(Nt=Nt, tgate=350.0 * Nt / 2000)
+    u = systems.tunable_bus_controls(2, Nt, seed=67)
+    e = _engine(prob, 2, True, monkeypatch)
+    J, g = _eval(e, u, device)
+    info = e.info()
+    assert info["chain_kernel"] == "blocks_mfma", info
+    lams = [e.costate(k, seed=1) for k in (0, Nt // 2, Nt)]
+    xs = [e.state(k, seed=1) for k in (1, Nt // 2, Nt)]
+    e.close()
+    ed = _engine(prob, 2, False, monkeypatch)
+    Jd, gd = _eval(ed, u, device)
+    assert ed.info()["chain_kernel"] == "mfma_regs"
+    ed.close()
+    for b in range(2):
+        J0, g0, c0 = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, (which, b))
+        _assert_seed(J[b], g[b], Jd[b], gd[b], (which, b, "dense"))
+    xsc = max(np.abs(x).max() for x in c0.x)
+    for x, k in zip(xs, (1, Nt // 2, Nt)):
+        assert np.abs(x - c0.x[k]).max() <= 1e-12 * xsc, ("x", k)
+    lsc = max(np.abs(lam).max() for lam in c0.lam)
+    for lam, k in zip(lams, (0, Nt // 2, Nt)):
+        assert np.abs(lam - c0.lam[k]).max() <= 1e-12 * lsc, ("lambda", k)
+
+
+@pytest.mark.parametrize("NB,nblk,nu,m", [(10, 3, 2, 3), (16, 2, 1, 1), (7, 4, 2, 2), (12, 3, 1, 5)])
+@pytest.mark.parametrize("poly", ["taylor", "chebyshev"])
+def test_blocks_mfma_random_permuted_blocks(built_lib, monkeypatch, NB, nblk, nu, m, poly):
+    """Random permuted blocks of 5..16 rows (a short last block for padding lanes), both polynomials, host and device
+    evals, a state penalty and the orders 1, 2, 4 (the dense gradient kernels on the block chains' states)."""
+    monkeypatch.setenv("QOC_TCHAIN_POLY", poly)
+    prob, u = _block_problem(NB=NB, nblk=nblk, nu=nu, m=m, seed=NB * 10 + nblk + nu + m)
+    for device in (False, True):
+        e = _engine(prob, 2, True, monkeypatch)
+        J, g = _eval(e, u, device)
+        assert e.info()["chain_kernel"] == "blocks_mfma"
+        e.close()
+        for b in range(2):
+            J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+            _assert_seed(J[b], g[b], J0, g0, (NB, nu, m, device, b))
+    pen = ([0, 3, 5], [0], 0.3)
+    e = _engine(prob, 2, True, monkeypatch, penalty=pen)
+    J = e.propagate(u)
+    gs = {o: e.grape_sensitivity(u, o) for o in (1, 2, 4)}
+    e.close()
+    for b in range(2):
+        for o, g in gs.items():
+            J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=o, penalty=pen)
+            _assert_seed(J[b], g[b], J0, g0, ("penalty", o, b))

@@ -36,8 +36,11 @@ def _gpu(prob, u, chain=None):
     return J, g, info
 
 
-def _check_config(name, seeds, chain=None):
+def _check_config(name, seeds, chain=None, monkeypatch=None):
     from qoc_amd import systems
+    if chain == "dense":  # the dense Taylor-action kernels (no block chains; qoc_blk.hpp)
+        monkeypatch.setenv("QOC_BLOCKS", "0")
+        chain = None
     mk_prob, mk_u, B = systems.CONFIGS[name]
     prob = mk_prob()
     u = mk_u(B, 0)
@@ -52,27 +55,30 @@ def _check_config(name, seeds, chain=None):
     return info
 
 
-@pytest.mark.parametrize("chain", ["auto", "propagators"])
-def test_zz_batch_full_size(built_lib, chain):
+@pytest.mark.parametrize("chain", ["auto", "dense", "propagators"])
+def test_zz_batch_full_size(built_lib, chain, monkeypatch):
     """config 2: zz_coupling N=9, m=4, Nt=500, B=512 (first and last seeds of the batch checked)."""
     seeds = list(range(CHECK_SEEDS // 2)) + list(range(512 - CHECK_SEEDS // 2, 512))
-    _check_config("zz_batch", seeds, None if chain == "auto" else chain)
+    info = _check_config("zz_batch", seeds, None if chain == "auto" else chain, monkeypatch)
+    assert (info["chain_kernel"] == "blocks") == (chain == "auto")
 
 
-@pytest.mark.parametrize("chain", ["auto", "propagators"])
-def test_cavity_full_size(built_lib, chain):
+@pytest.mark.parametrize("chain", ["auto", "dense", "propagators"])
+def test_cavity_full_size(built_lib, chain, monkeypatch):
     """config 3: cavity(20) x qubit N=40, m=2, Nt=1000, B=256."""
     seeds = list(range(0, 256, 256 // CHECK_SEEDS))
-    _check_config("cavity", seeds, None if chain == "auto" else chain)
+    info = _check_config("cavity", seeds, None if chain == "auto" else chain, monkeypatch)
+    assert (info["chain_kernel"] == "blocks") == (chain == "auto")
 
 
-@pytest.mark.parametrize("chain", ["auto", "propagators"])
-def test_tunable_bus_full_size(built_lib, chain):
+@pytest.mark.parametrize("chain", ["auto", "dense", "propagators"])
+def test_tunable_bus_full_size(built_lib, chain, monkeypatch):
     """config 4: two_qubit_tunable_bus N=27, m=1, Nt=2000, B=512 per GPU, ||A_k||_1 ~ 30: every seed against
     the C port, over 2000 chained slices: the default Chebyshev Taylor-action chains (spectral radius ~14 per
     slice) and the propagators (the reference's Padé-13)."""
-    info = _check_config("tunable_bus", list(range(512)), None if chain == "auto" else chain)
-    assert info["chain"] == ("taylor" if chain == "auto" else "propagators")
+    info = _check_config("tunable_bus", list(range(512)), None if chain == "auto" else chain, monkeypatch)
+    assert info["chain"] == ("propagators" if chain == "propagators" else "taylor")
+    assert (info["chain_kernel"] == "blocks_mfma") == (chain == "auto")
 
 
 def test_synthetic_full_size_fp32(built_lib, golden_dir):
