@@ -393,6 +393,7 @@ def main():
     taylor = info1.get("chain") == "taylor" and not large
     dual = info1.get("concurrent_launch") == "dual"
     blocks = taylor and info1.get("chain_kernel") == "blocks"
+    rot_blocks = taylor and info1.get("chain_kernel") == "blocks_mfma"
     if blocks:
         # block chains (csrc/qoc_blk.hpp): one lane per (block, column), each term an n_b x n_b complex matvec in
         # VALU registers; the launch's algorithmic bytes are the states it writes (x_k, and μ_k in the dual launch)
@@ -415,14 +416,19 @@ def main():
     elif taylor:
         # Taylor-action chains (csrc/qoc_tchain.hpp): no exponential kernel; the chains carry the Taylor terms,
         # each an N x N by N x m complex matvec (8 N^2 m flops) on v_mfma_f64_4x4x4 (fp64) / VALU (fp32); the dual
-        # launch (k_tchain_mf_dual) carries both directions' terms
+        # launch (k_tchain_mf_dual) carries both directions' terms.  MFMA block waves (k_blkrot_*, qoc_blk.hpp):
+        # per term 8 v_mfma_f64_4x4x4_4b (4 x 128 flops each) per (block, column pair) wave
         tl = terms / K * (2 if dual else 1)
+        mv_flops = 8.0 * N * N * m
+        if rot_blocks:
+            mv_flops = 8 * 4 * 128.0 * len(block_sizes(prob)) * ((m + 1) // 2)
         models = {
             "k_expm": ("mfma", 0.0, "TFLOP/s", peak),  # k_tchain_prep: (P, s, e^mu) per slice, no flops counted
             "k_grad": ("mfma", grad_flops(N, m, nu, Nt, B, args.order,
-                                          info1.get("backward") in ("captured", "concurrent")) / 1e12, "TFLOP/s", peak),
-            "k_chain_fwd": ("mfma", 8.0 * N * N * m * tl / 1e12, "TFLOP/s", peak),
-            "k_chain_bwd": ("mfma", 8.0 * N * N * m * tl / 1e12, "TFLOP/s", peak),
+                                          info1.get("backward") in ("captured", "concurrent", "blocks")) / 1e12,
+                       "TFLOP/s", peak),
+            "k_chain_fwd": ("mfma", mv_flops * tl / 1e12, "TFLOP/s", peak),
+            "k_chain_bwd": ("mfma", mv_flops * tl / 1e12, "TFLOP/s", peak),
         }
     elif not large:
         models = {
@@ -491,7 +497,9 @@ def main():
         names = {"k_expm": "k_tchain_prep",
                  "k_chain_fwd": "k_tchain_mf_dual" if dual else "k_tchain_mf_fwd" if mf else "k_tchain_fwd",
                  "k_chain_bwd": "k_tchain_mf_bwd" if mf else "k_tchain_bwd",
-                 "k_grad": "k_grad_rr_c" if info1.get("backward") in ("captured", "concurrent") else "k_grad_rr"}
+                 "k_grad": "k_grad_rr_c" if info1.get("backward") in ("captured", "concurrent", "blocks") else "k_grad_rr"}
+        if rot_blocks:
+            names.update({"k_chain_fwd": "k_blkrot_dual" if dual else "k_blkrot_fwd", "k_chain_bwd": "k_blkrot_bwd"})
         for k in ("k_chain_fwd", "k_chain_bwd"):
             # serial Taylor terms of one seed per launch and the time each takes (the chains' critical path)
             kern[k]["kernel"] = names[k]
@@ -499,15 +507,15 @@ def main():
             kern[k]["ns_per_serial_term"] = per_step[k] * 1e6 / max(terms / K / B, 1e-9)
         dom = max(("k_chain_fwd", "k_chain_bwd", "k_grad"), key=lambda k: per_step[k])
         if dual:
-            kern["k_chain_fwd"]["note"] = "k_tchain_mf_dual: forward chain and mu recurrence of every seed in one launch"
+            kern["k_chain_fwd"]["note"] = names["k_chain_fwd"] + ": forward chain and mu recurrence of every seed in one launch"
         roof = {"kernel": names[dom], "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
                 "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
                 "traffic": traffic_all.get(names[dom]), "ms_per_launch": kern[dom]["ms_per_launch"],
                 "launches_per_step": lps[dom],
                 "note": ("latency-bound serial recurrence (one workgroup per seed, Taylor terms in sequence): "
                          "achieved = executed matvec flops / launch time"
-                         + ("; the backward (μ) recurrence runs beside the forward chain (k_tchain_mf_dual: one "
-                            "launch of 2B workgroups; flops of both directions), the contraction after both"
+                         + ("; the backward (μ) recurrence runs beside the forward chain (" + names["k_chain_fwd"] +
+                            ": one launch of 2B workgroups; flops of both directions), the contraction after both"
                             if dual else "; the backward (μ) recurrence runs beside the forward chain on a second "
                             "stream, the contraction after both" if info1.get("backward") == "concurrent" else "")
                          + ("; the backward chain runs in slice ranges, each range's gradient overlapped with "
