@@ -392,8 +392,11 @@ def main():
             traffic_all = {}
     taylor = info1.get("chain") == "taylor" and not large
     dual = info1.get("concurrent_launch") == "dual"
-    blocks = taylor and info1.get("chain_kernel") == "blocks"
-    rot_blocks = taylor and info1.get("chain_kernel") == "blocks_mfma"
+    bsz = block_sizes(prob) if taylor and info1.get("chain_kernel") in ("blocks", "blocks_mfma") else None
+    # blocks of <= 4 rows (VALU lanes or packed MFMA block waves) with the block gradient; 5..16 rows: MFMA block
+    # waves with the dense gradient
+    blocks = bsz is not None and bsz.max() <= 4
+    rot_blocks = bsz is not None and bsz.max() > 4
     if blocks:
         # block chains (csrc/qoc_blk.hpp): one lane per (block, column), each term an n_b x n_b complex matvec in
         # VALU registers; the launch's algorithmic bytes are the states it writes (x_k, and μ_k in the dual launch)
@@ -473,8 +476,9 @@ def main():
                    "unit": unit, "peak": pk, "frac": ach / pk}
     names = {"k_expm": "k_expm_rr", "k_chain_fwd": "k_chain_fwd", "k_chain_bwd": "k_chain_bwd", "k_grad": "k_grad_rr"}
     if blocks:
-        names = {"k_expm": "k_tchain_prep", "k_chain_fwd": "k_blk_dual" if dual else "k_blk_fwd",
-                 "k_chain_bwd": "k_blk_bwd", "k_grad": "k_blk_grad"}
+        kb = "k_blkrot" if info1.get("chain_kernel") == "blocks_mfma" else "k_blk"
+        names = {"k_expm": "k_tchain_prep", "k_chain_fwd": kb + ("_dual" if dual else "_fwd"),
+                 "k_chain_bwd": kb + "_bwd", "k_grad": "k_blk_grad"}
         for k in ("k_chain_fwd", "k_chain_bwd", "k_grad"):
             kern[k]["kernel"] = names[k]
             t = per_step[k] / 1e3

@@ -34,6 +34,8 @@ struct BlkArgs {
   const int* brow;         // nblk x NB: rows (= columns) of each block in increasing order, -1 padding
   const void* A;           // (nu+1) x N x N unshifted generators (the gradient's A_k and A_j)
   int nblk;
+  const int* wrow;         // MFMA block waves: nwb x 16 rows of each wave's state (-1 padding)
+  int nwb;
 };
 
 // This lane's (block, column) pair: lane l < nblk m owns block l % nblk of column l / nblk, so that the lanes of
@@ -365,15 +367,18 @@ __global__ __launch_bounds__(BLK_MAXT) void k_blk_dual(const TChainArgs gf, cons
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// Blocks of 5..16 rows (the tunable bus: two parity blocks of 14 and 13 rows at N = 27): one wave per (block,
-// state column pair) runs TChainRot<1>'s MFMA term (qoc_tchain.hpp) on the block's 16-row state.  In the
-// v_mfma_f64_4x4x4_4b layout a lane's D element (local row 4b + hi, column lo) is block b's B operand for k = hi of
-// a k-quad, and a DPP row_ror by 4j hands block b the k-quad q_j(b) of the state; the A operands hold
-// Ã[r(4b + lo)][r(4 q_j(b) + hi)] with r() the block's row list (brow, 16 entries per block, -1 padding), so the
-// dense G = 2 chain's 32 MFMAs per term become 8 per block wave with no cross-wave exchange.  The gradient stays the
-// dense fused kernels: with captures (D1 = Â v, D2 = Â y_1 of each slice, the layout TChainArgs::cap1 / cap2
-// documents) the concurrent eval's contraction k_grad_rr_c, else k_grad_rr_q / p from the stored states.
-// ---------------------------------------------------------------------------------------------------------
+// MFMA block waves: each wave owns a 16-row state ("wave block", wrow: 16 global rows, -1 padding) and one state
+// column pair, and runs TChainRot<1>'s v_mfma_f64_4x4x4_4b term (qoc_tchain.hpp) on it.  In the 4x4x4_4b layout a
+// lane's D element (local row 4b + hi, column lo) is block b's B operand for k = hi of a k-quad, and a DPP row_ror by
+// 4j hands block b the k-quad q_j(b) of the state; the A operands hold Ã[r(4b + lo)][r(4 q_j(b) + hi)].
+//  * JR = 4: one invariant block of 5..16 rows per wave (the tunable bus: two parity blocks of 14 and 13 rows at
+//    N = 27): 8 MFMAs per term per block wave instead of the dense two-group chain's 32 in one wave.
+//  * JR = 1: invariant blocks of <= 4 rows packed into the wave's four aligned 4-row slots (cavity: two 2-row blocks
+//    per slot, zz: one 3-row block per slot).  No block couples two slots, so only the unrotated k-quad (j = 0)
+//    carries entries: a term is 2 MFMAs (Ar, Ai) on the state as it sits in the D layout (D = B layout at K = 4),
+//    no rotation, and 4 slots x 2 columns of blocks per instruction.
+// No cross-wave exchange per term.  With captures (D1 = Â v, D2 = Â y_1 of each slice, the layout TChainArgs::cap1 /
+// cap2 documents) the concurrent eval's contraction is k_grad_rr_c; the blocks of <= 4 rows use k_blk_grad instead.
 struct BlkRotLane {
   int n, cp, beta;
   int rowE;     // global row of this lane's D element (-1: padding, or no block)
@@ -384,12 +389,12 @@ struct BlkRotLane {
   __device__ __forceinline__ void setup(const BlkArgs& bk, int m) {
     const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int b = (l >> 2) & 3, kl = l >> 4, lo = l & 3;
-    const bool wok = w < bk.nblk * ((m + 1) / 2);
-    beta = wok ? w % bk.nblk : 0;
-    cp = wok ? w / bk.nblk : 0;
+    const bool wok = w < bk.nwb * ((m + 1) / 2);
+    beta = wok ? w % bk.nwb : 0;
+    cp = wok ? w / bk.nwb : 0;
     n = lo;
     colD = 2 * cp + (n >> 1);
-    const int* rb = bk.brow + beta * 16;
+    const int* rb = bk.wrow + beta * 16;
     rowE = wok ? rb[4 * b + kl] : -1;
     act = rowE >= 0 && colD < m;
     rowA = wok ? rb[4 * b + lo] : -1;
@@ -400,14 +405,14 @@ struct BlkRotLane {
     for (int j = 0; j < 4; ++j) colA[j] = wok ? rb[4 * q[j] + kl] : -1;
   }
   // the A-operand entries of Ã_0..Ã_2 (HERM: of Ã_j^H), zero outside the block and for j > nu
-  template <bool HERM>
-  __device__ __forceinline__ void load_gen(const cx<double>* __restrict__ At, int N, int nu, double (&gr)[3][4],
-                                           double (&gi)[3][4]) const {
+  template <bool HERM, int JR>
+  __device__ __forceinline__ void load_gen(const cx<double>* __restrict__ At, int N, int nu, double (&gr)[3][JR],
+                                           double (&gi)[3][JR]) const {
     const size_t NN = (size_t)N * N;
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
+      for (int x = 0; x < JR; ++x) {
         const bool ok = j <= nu && rowA >= 0 && colA[x] >= 0;
         const int rr = max(rowA, 0), cc = max(colA[x], 0);
         const cx<double> v = At[(size_t)min(j, nu) * NN + (HERM ? cc + (size_t)N * rr : rr + (size_t)N * cc)];
@@ -419,21 +424,30 @@ struct BlkRotLane {
 
 // one slice on the wave's 16-row block state (one element per lane, TChainRot<1>::step without the LDS mirror);
 // CAP: D1, D2 of the first substep
-template <bool CHEB>
-__device__ __forceinline__ void blkrot_slice(const double (&ar)[4], const double (&ai)[4], double& acc, bool act,
+template <int JR, bool CHEB>
+__device__ __forceinline__ void blkrot_slice(const double (&ar)[JR], const double (&ai)[JR], double& acc, bool act,
                                              int n, int P, int s, double phr, double phi, double cl,
                                              const double* __restrict__ invt, double& cd1, double& cd2) {
   using R = TChainRot<1>;
+  auto rot = [](double v, double (&bv)[4]) __attribute__((always_inline)) {
+    bv[0] = v;
+    if constexpr (JR > 1) {
+      bv[1] = R::mv<0x124>(v);  // row_ror:4
+      bv[2] = R::mv<0x128>(v);  // row_ror:8
+      bv[3] = R::mv<0x12C>(v);  // row_ror:12
+    }
+  };
   for (int sub = 0; sub < s; ++sub) {
     double y = act ? acc : 0.0, ym2 = 0.0;
     acc = (CHEB ? bcast(cl, 0) : 1.0) * y;
-    double bv[4] = {y, R::mv<0x124>(y), R::mv<0x128>(y), R::mv<0x12C>(y)};
+    double bv[4];
+    rot(y, bv);
     for (int t = 1; t <= P; ++t) {
       const double ct = CHEB ? bcast(cl, t) : invt[t];
       __builtin_amdgcn_sched_barrier(0);
       double d0 = 0.0, d1 = 0.0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < JR; ++j) {
         d0 = MF<double>::mma4(ar[j], bv[j], d0);
         d1 = MF<double>::mma4(ai[j], bv[j], d1);
       }
@@ -451,10 +465,7 @@ __device__ __forceinline__ void blkrot_slice(const double (&ar)[4], const double
         acc += z;
       }
       y = z;
-      bv[0] = y;
-      bv[1] = R::mv<0x124>(y);
-      bv[2] = R::mv<0x128>(y);
-      bv[3] = R::mv<0x12C>(y);
+      rot(y, bv);
     }
     if (sub == s - 1) {
       const double o = R::mv<0xB1>(acc);
@@ -463,17 +474,18 @@ __device__ __forceinline__ void blkrot_slice(const double (&ar)[4], const double
   }
 }
 
-__device__ __forceinline__ void blkrot_form(const double (&gr)[3][4], const double (&gi)[3][4], const double (&u)[2],
-                                            double scale, double (&ar)[4], double (&ai)[4]) {
+template <int JR>
+__device__ __forceinline__ void blkrot_form(const double (&gr)[3][JR], const double (&gi)[3][JR], const double (&u)[2],
+                                            double scale, double (&ar)[JR], double (&ai)[JR]) {
   const double u1 = u[0] * scale, u2 = u[1] * scale;
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {
+  for (int x = 0; x < JR; ++x) {
     ar[x] = fma(u2, gr[2][x], fma(u1, gr[1][x], scale * gr[0][x]));
     ai[x] = fma(u2, gi[2][x], fma(u1, gi[1][x], scale * gi[0][x]));
   }
 }
 
-template <bool CHEB>
+template <int JR, bool CHEB>
 __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkArgs& bk, const int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* invt = reinterpret_cast<double*>(smem);
@@ -484,8 +496,8 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
   for (int e = tid; e < 64; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
   BlkRotLane ln;
   ln.setup(bk, m);
-  double gr[3][4], gi[3][4];
-  ln.load_gen<false>((const cx<double>*)g.At, N, nu, gr, gi);
+  double gr[3][JR], gi[3][JR];
+  ln.load_gen<false, JR>((const cx<double>*)g.At, N, nu, gr, gi);
   const cx<double>* x0b = (const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0);
   double* Xb = reinterpret_cast<double*>((cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm);
   double* const sink = tchain_sink(g);
@@ -520,9 +532,9 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
       if (k >= Nt) break;
       const TPreN<2>& st = nx[i];
       const int P = __builtin_amdgcn_readfirstlane(st.P), s = __builtin_amdgcn_readfirstlane(st.s);
-      double ar[4], ai[4], cd1 = 0.0, cd2 = 0.0;
-      blkrot_form(gr, gi, st.u, st.scale, ar, ai);
-      blkrot_slice<CHEB>(ar, ai, acc, ln.act, ln.n, P, s, st.pr, st.pi, st.cl, invt, cd1, cd2);
+      double ar[JR], ai[JR], cd1 = 0.0, cd2 = 0.0;
+      blkrot_form<JR>(gr, gi, st.u, st.scale, ar, ai);
+      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, ln.n, P, s, st.pr, st.pi, st.cl, invt, cd1, cd2);
       const int kn = min(k + PD, Nt - 1);
       tpre_load<2, CHEB, false>(stb + kn, ub + (size_t)kn * nu, nu, nx[i], CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
       *(ln.act ? Xb + (size_t)(k + 1) * 2 * Nm + oe : sink) = acc;
@@ -537,7 +549,7 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
                       g.cost_kind, g.n_norm, block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * 2 * m, g.sc);
 }
 
-template <bool CHEB>
+template <int JR, bool CHEB>
 __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkArgs& bk, const int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* invt = reinterpret_cast<double*>(smem);
@@ -546,8 +558,8 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
   for (int e = tid; e < 64; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
   BlkRotLane ln;
   ln.setup(bk, m);
-  double gr[3][4], gi[3][4];
-  ln.load_gen<true>((const cx<double>*)g.At, N, nu, gr, gi);
+  double gr[3][JR], gi[3][JR];
+  ln.load_gen<true, JR>((const cx<double>*)g.At, N, nu, gr, gi);
   const double* Xb = reinterpret_cast<const double*>((const cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm);
   double* Lb = reinterpret_cast<double*>((cx<double>*)g.L + (size_t)b * (Nt + 1) * Nm);
   const double* srcb =
@@ -598,9 +610,9 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
       const size_t ok_ = (size_t)k * 2 * Nm + oe;
       double xa = pm ? tmu * Xb[ok_] : 0.0;  // 2μ x_k on the mask + the caller's dL/dx(x_k), after the slice
       if (srcl) xa += srcb[ok_];
-      double ar[4], ai[4], cd1 = 0.0, cd2 = 0.0;
-      blkrot_form(gr, gi, st.u, st.scale, ar, ai);
-      blkrot_slice<CHEB>(ar, ai, acc, ln.act, ln.n, P, s, st.pr, -st.pi, st.cl, invt, cd1, cd2);
+      double ar[JR], ai[JR], cd1 = 0.0, cd2 = 0.0;
+      blkrot_form<JR>(gr, gi, st.u, st.scale, ar, ai);
+      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, ln.n, P, s, st.pr, -st.pi, st.cl, invt, cd1, cd2);
       const int kp = max(k - PD, 0);
       tpre_load<2, CHEB, false>(stb + kp, ub + (size_t)kp * nu, nu, nx[i], CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
       acc += xa;
@@ -611,22 +623,22 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
     }
 }
 
-template <bool CHEB>
+template <int JR, bool CHEB>
 __global__ __launch_bounds__(1024) void k_blkrot_fwd(const TChainArgs g, const BlkArgs bk) {
-  blkrot_fwd_body<CHEB>(g, bk, blockIdx.x);
+  blkrot_fwd_body<JR, CHEB>(g, bk, blockIdx.x);
 }
-template <bool CHEB>
+template <int JR, bool CHEB>
 __global__ __launch_bounds__(1024) void k_blkrot_bwd(const TChainArgs g, const BlkArgs bk) {
-  blkrot_bwd_body<CHEB>(g, bk, blockIdx.x);
+  blkrot_bwd_body<JR, CHEB>(g, bk, blockIdx.x);
 }
-template <bool CHEB>
+template <int JR, bool CHEB>
 __global__ __launch_bounds__(1024) void k_blkrot_dual(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk) {
   const int i = blockIdx.x, B = gridDim.x >> 1;
   const bool by8 = (B & 7) == 0;
   const int dir = by8 ? (i >> 3) & 1 : i & 1;
   const int seed = by8 ? ((i >> 4) << 3) | (i & 7) : i >> 1;
-  if (dir == 0) blkrot_fwd_body<CHEB>(gf, bk, seed);
-  else blkrot_bwd_body<CHEB>(gb, bk, seed);
+  if (dir == 0) blkrot_fwd_body<JR, CHEB>(gf, bk, seed);
+  else blkrot_bwd_body<JR, CHEB>(gb, bk, seed);
 }
 
 // The order-ORD gradient per block (expm_jacobian! + _compute_u_sensitivity, src/gradient_computations.jl:177-223):

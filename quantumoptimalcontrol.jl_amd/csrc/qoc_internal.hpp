@@ -157,6 +157,9 @@ struct qoc_ctx {
   int blk_nb = 0;                // padded block size 2 / 3 / 4 (VALU lanes), 16 (MFMA block waves), 0: no block path
   int nblk = 0;                  // blocks
   int* d_brow = nullptr;         // nblk x blk_nb rows of each block (-1 padding)
+  int blk_jr = 0;                // chain kernels: 0 VALU lanes (k_blk_*), 1 / 4 MFMA block waves (k_blkrot_*<JR>)
+  int nwb = 0;                   // MFMA block waves per column pair
+  int* d_wrow = nullptr;         // nwb x 16 rows of each wave's state (-1 padding)
   // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;

@@ -1,5 +1,6 @@
 // qoc_run_blk.hip — the block chains and block gradient (qoc_blk.hpp): detection of the generators' invariant
 // blocks, and the launches of one propagate / grape_sensitivity / concurrent eval on them.
+#include <cstring>
 #include <numeric>
 
 #include "qoc_blk.hpp"
@@ -14,8 +15,11 @@ namespace qoc_host {
 int blk_detect(qoc_ctx* c) {
   c->blk_nb = 0;
   c->nblk = 0;
+  c->blk_jr = 0;
+  c->nwb = 0;
   const char* env = getenv("QOC_BLOCKS");
-  if (env && atoi(env) == 0) return QOC_OK;
+  if (env && !std::strcmp(env, "0")) return QOC_OK;
+  const bool valu = env && !std::strcmp(env, "valu");  // blocks of <= 4 rows on the VALU lanes (k_blk_*)
   const int N = c->N;
   const size_t NN = (size_t)N * N;
   std::vector<int> par(N);
@@ -45,22 +49,53 @@ int blk_detect(qoc_ctx* c) {
   }
   size_t mx = 0;
   for (const auto& bl : blocks) mx = std::max(mx, bl.size());
-  // blocks of <= 4 rows: the VALU lanes; 5..16 rows: one MFMA wave per block (only when the dense state needs more
-  // than one 16-row group, N > 16: at N <= 16 the dense register chain already runs one wave per column pair)
+  // blocks of <= 4 rows: packed into the aligned 4-row slots of MFMA block waves (JR = 1), or one VALU lane per
+  // (block, column) with QOC_BLOCKS=valu; 5..16 rows: one MFMA wave per block (JR = 4), only when the dense state
+  // needs more than one 16-row group (N > 16: at N <= 16 the dense register chain already runs one wave per column
+  // pair)
   if (mx > 16 || (mx > (size_t)BLK_NBMAX && N <= 16)) return QOC_OK;
   const int NB = mx <= 2 ? 2 : mx <= 3 ? 3 : mx <= 4 ? 4 : 16;
   const int nblk = (int)blocks.size();
   std::vector<int> brow((size_t)nblk * NB, -1);
   for (int b = 0; b < nblk; ++b)
     for (size_t i = 0; i < blocks[b].size(); ++i) brow[(size_t)b * NB + i] = blocks[b][i];
-  if (c->d_brow) {
-    HIPCHK(c, hipFree(c->d_brow));
-    c->d_brow = nullptr;
+  // the MFMA waves' 16-row states
+  std::vector<int> wrow;
+  int jr = 0;
+  if (NB == 16) {
+    jr = 4;
+    wrow = brow;
+  } else if (!valu) {
+    jr = 1;
+    std::vector<int> slot;  // rows of the 4-row slots, in order (a block never straddles two slots)
+    int fill = 0;
+    for (const auto& bl : blocks) {
+      if (fill + (int)bl.size() > 4) {
+        for (; fill < 4; ++fill) slot.push_back(-1);
+        fill = 0;
+      }
+      for (int r : bl) slot.push_back(r);
+      fill += (int)bl.size();
+      if (fill == 4) fill = 0;
+    }
+    while (slot.size() % 16) slot.push_back(-1);
+    wrow = slot;
   }
+  for (int** p : {&c->d_brow, &c->d_wrow})
+    if (*p) {
+      HIPCHK(c, hipFree(*p));
+      *p = nullptr;
+    }
   HIPCHK(c, hipMalloc((void**)&c->d_brow, brow.size() * sizeof(int)));
   HIPCHK(c, hipMemcpy(c->d_brow, brow.data(), brow.size() * sizeof(int), hipMemcpyHostToDevice));
+  if (jr) {
+    HIPCHK(c, hipMalloc((void**)&c->d_wrow, wrow.size() * sizeof(int)));
+    HIPCHK(c, hipMemcpy(c->d_wrow, wrow.data(), wrow.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
   c->blk_nb = NB;
   c->nblk = nblk;
+  c->blk_jr = jr;
+  c->nwb = (int)(wrow.size() / 16);
   return QOC_OK;
 }
 
@@ -69,31 +104,38 @@ bool blk_active(const qoc_ctx* c) {
   if (c->blk_nb <= 0 || c->prec != QOC_FP64 || c->chain_mode != 1 || c->prop_method != QOC_PROP_EXPM || c->big ||
       c->packed || c->nu > 2)
     return false;
-  if (c->blk_nb == 16) return tchain_mf(c) && c->nblk * ((c->m + 1) / 2) <= 16;  // one wave per (block, column pair)
+  if (c->blk_jr) return c->nwb * ((c->m + 1) / 2) <= 16 && (c->blk_nb < 16 || tchain_mf(c));  // MFMA block waves
   return c->nblk * c->m <= BLK_MAXT && c->nblk <= 256;
 }
-bool blk_rot(const qoc_ctx* c) { return c->blk_nb == 16; }
+// MFMA block waves (k_blkrot_*): the chain kernels; blocks of 16 rows also take the dense gradient kernels
+bool blk_rot(const qoc_ctx* c) { return c->blk_jr > 0; }
+static bool blk_big(const qoc_ctx* c) { return c->blk_nb == 16; }
 
 static BlkArgs blk_args(const qoc_ctx* c) {
   BlkArgs bk{};
   bk.brow = c->d_brow;
   bk.A = c->d_A;
   bk.nblk = c->nblk;
+  bk.wrow = c->d_wrow;
+  bk.nwb = c->nwb;
   return bk;
 }
 
 static int blk_threads(const qoc_ctx* c) {
-  return blk_rot(c) ? 64 * c->nblk * ((c->m + 1) / 2) : 64 * ((c->nblk * c->m + 63) / 64);
+  return blk_rot(c) ? 64 * c->nwb * ((c->m + 1) / 2) : 64 * ((c->nblk * c->m + 63) / 64);
 }
 
+// f(kernel-selector, Chebyshev): selector 1 / 4 = k_blkrot_*<JR>, 2 / 3 / 4 + 100 = k_blk_*<NB> (VALU lanes)
 template <typename F>
 static hipError_t blk_dispatch(const qoc_ctx* c, F&& f) {
   using std::integral_constant;
+  auto ch = [&](auto K_) { return c->cheb_ran ? f(K_, std::true_type()) : f(K_, std::false_type()); };
+  if (c->blk_jr == 1) return ch(integral_constant<int, 1>());
+  if (c->blk_jr == 4) return ch(integral_constant<int, 4>());
   switch (c->blk_nb) {
-    case 16: return c->cheb_ran ? f(integral_constant<int, 16>(), std::true_type()) : f(integral_constant<int, 16>(), std::false_type());
-    case 2: return c->cheb_ran ? f(integral_constant<int, 2>(), std::true_type()) : f(integral_constant<int, 2>(), std::false_type());
-    case 3: return c->cheb_ran ? f(integral_constant<int, 3>(), std::true_type()) : f(integral_constant<int, 3>(), std::false_type());
-    case 4: return c->cheb_ran ? f(integral_constant<int, 4>(), std::true_type()) : f(integral_constant<int, 4>(), std::false_type());
+    case 2: return ch(integral_constant<int, 102>());
+    case 3: return ch(integral_constant<int, 103>());
+    case 4: return ch(integral_constant<int, 104>());
   }
   return hipErrorInvalidValue;
 }
@@ -108,8 +150,8 @@ int blk_forward(qoc_ctx* c) {
   const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
     constexpr int NB = decltype(NB_)::value;
     constexpr bool CH = decltype(CH_)::value;
-    if constexpr (NB == 16) hipLaunchKernelGGL((k_blkrot_fwd<CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
-    else hipLaunchKernelGGL((k_blk_fwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    if constexpr (NB < 100) hipLaunchKernelGGL((k_blkrot_fwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    else hipLaunchKernelGGL((k_blk_fwd<NB - 100, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
     return hipGetLastError();
   });
   mark_end(c, mk);
@@ -156,13 +198,13 @@ int blk_backward(qoc_ctx* c, int order, double* d_dJdu) {
   const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
     constexpr int NB = decltype(NB_)::value;
     constexpr bool CH = decltype(CH_)::value;
-    if constexpr (NB == 16) hipLaunchKernelGGL((k_blkrot_bwd<CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
-    else hipLaunchKernelGGL((k_blk_bwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    if constexpr (NB < 100) hipLaunchKernelGGL((k_blkrot_bwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    else hipLaunchKernelGGL((k_blk_bwd<NB - 100, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
     return hipGetLastError();
   });
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blk_bwd launch: %s", hipGetErrorString(e));
-  if (order == QOC_DUKDP_EXACT || blk_rot(c)) return dense_gradient<double>(c, order, d_dJdu);
+  if (order == QOC_DUKDP_EXACT || blk_big(c)) return dense_gradient<double>(c, order, d_dJdu);
   return blk_grad(c, order, false, d_dJdu);
 }
 
@@ -170,7 +212,7 @@ int blk_backward(qoc_ctx* c, int order, double* d_dJdu) {
 // (λ_k = coef ⊙ μ_k, src/penalty_fcns.jl:19-22, 35-40) in one launch, then the gradient with the coefficients.
 bool blk_concurrent_ok(const qoc_ctx* c, int order) {
   // MFMA block waves: the contraction from the chains' captures (k_grad_rr_c, order 3)
-  if (blk_rot(c) && !(order == 3 && tchain_cap_ok(c))) return false;
+  if (blk_big(c) && !(order == 3 && tchain_cap_ok(c))) return false;
   return blk_active(c) && c->concurrent && order >= 1 && order <= BLK_ORDMAX &&
          (c->cost_kind == QOC_COST_TRACE || c->cost_kind == QOC_COST_ZCAL) && c->mu == 0.0 && !c->src_on;
 }
@@ -180,13 +222,13 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
     HIPCHK(c, hipMalloc((void**)&c->d_coef_mu, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
     c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
   }
-  int r = blk_rot(c) ? ensure_pws(c) : QOC_OK;
+  int r = blk_big(c) ? ensure_pws(c) : QOC_OK;
   if (r) return r;
   if ((r = tchain_prep(c))) return r;
   TChainArgs gf = tchain_args(c);
   TChainArgs gb = tchain_args(c);
   gb.mu_mode = 1;
-  if (blk_rot(c)) {  // the first two products of every slice for k_grad_rr_c (forward -> d_pws, μ -> d_gws)
+  if (blk_big(c)) {  // the first two products of every slice for k_grad_rr_c (forward -> d_pws, μ -> d_gws)
     const size_t bufN = (size_t)c->N * ((size_t)c->B * (c->Nt + 1) * c->m);
     gf.cap1 = c->d_pws;
     gf.cap2 = (cx<double>*)c->d_pws + bufN;
@@ -199,15 +241,15 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
   const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
     constexpr int NB = decltype(NB_)::value;
     constexpr bool CH = decltype(CH_)::value;
-    if constexpr (NB == 16) hipLaunchKernelGGL((k_blkrot_dual<CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
-    else hipLaunchKernelGGL((k_blk_dual<NB, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
+    if constexpr (NB < 100) hipLaunchKernelGGL((k_blkrot_dual<NB, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
+    else hipLaunchKernelGGL((k_blk_dual<NB - 100, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
     return hipGetLastError();
   });
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blk_dual launch: %s", hipGetErrorString(e));
   c->fwd_captured = false;  // the block backward recomputes its own products
   c->props_since_reset++;
-  if (blk_rot(c)) {
+  if (blk_big(c)) {
     const int mg = mark_begin(c, 3);
     r = grad_rr_cap(c, d_dJdu, c->stream, 0, c->Nt, true);
     mark_end(c, mg);

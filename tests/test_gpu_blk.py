@@ -50,9 +50,13 @@ def _block_problem(NB=4, nblk=5, nu=2, m=3, Nt=30, seed=0):
     return prob, u
 
 
+BLK = ("blocks", "blocks_mfma")
+
+
 def _engine(prob, B, blocks, monkeypatch, penalty=None, chain="taylor"):
+    """blocks: True (default kernels: MFMA block waves), "valu" (blocks of <= 4 rows on VALU lanes), False (dense)."""
     from qoc_amd import GrapeEngine
-    monkeypatch.setenv("QOC_BLOCKS", "1" if blocks else "0")
+    monkeypatch.setenv("QOC_BLOCKS", "valu" if blocks == "valu" else "1" if blocks else "0")
     e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
     e.set_cost_trace(prob.x_target, prob.n)
     e.set_chain(chain)
@@ -83,13 +87,16 @@ def _assert_seed(J, g, Jr, gr, tag):
 
 @pytest.mark.parametrize("name", ["zz", "cavity20", "cavity40"])
 @pytest.mark.parametrize("device", [False, True])
-def test_blocks_match_oracle_and_dense_chains(built_lib, monkeypatch, name, device):
+@pytest.mark.parametrize("kind", ["mfma", "valu"])
+def test_blocks_match_oracle_and_dense_chains(built_lib, monkeypatch, name, device, kind):
+    """Blocks of <= 4 rows: packed into the 4-row slots of MFMA block waves (default) or one VALU lane per (block,
+    column) (QOC_BLOCKS=valu); the block gradient either way."""
     prob, u = _cases()[name]
     B = u.shape[0]
-    e = _engine(prob, B, True, monkeypatch)
+    e = _engine(prob, B, True if kind == "mfma" else "valu", monkeypatch)
     J, g = _eval(e, u, device)
     info = e.info()
-    assert info["chain_kernel"] == "blocks", info
+    assert info["chain_kernel"] == ("blocks_mfma" if kind == "mfma" else "blocks"), info
     assert info["backward"] == ("blocks" if device else "generic"), info
     xs = [e.state(k, seed=0) for k in (1, prob.Nt // 2, prob.Nt)]
     lams = [e.costate(k, seed=0) for k in (0, prob.Nt // 2, prob.Nt)]
@@ -121,7 +128,7 @@ def test_blocks_gradient_orders(built_lib, monkeypatch, order, device):
     u = systems.zz_controls(2, 50, 5.0, seed=64)
     e = _engine(prob, 2, True, monkeypatch)
     J, g = _eval(e, u, device and order != "exact", order)
-    assert e.info()["chain_kernel"] == "blocks"
+    assert e.info()["chain_kernel"] in BLK
     e.close()
     for b in range(2):
         J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=order)
@@ -142,7 +149,7 @@ def test_blocks_penalty_and_costate_source(built_lib, monkeypatch, poly):
     J = e.propagate(u)
     g = e.grape_sensitivity(u, 3)
     info = e.info()
-    assert info["chain_kernel"] == "blocks" and info["chain_poly"] == poly
+    assert info["chain_kernel"] in BLK and info["chain_poly"] == poly
     e.close()
     for b in range(2):
         Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3, penalty=pen)
@@ -163,15 +170,16 @@ def test_blocks_penalty_and_costate_source(built_lib, monkeypatch, poly):
 
 @pytest.mark.parametrize("NB,nu,m", [(4, 2, 3), (4, 1, 1), (3, 2, 2), (2, 1, 5)])
 @pytest.mark.parametrize("poly", ["taylor", "chebyshev"])
-def test_blocks_random_permuted_blocks(built_lib, monkeypatch, NB, nu, m, poly):
+@pytest.mark.parametrize("kind", ["mfma", "valu"])
+def test_blocks_random_permuted_blocks(built_lib, monkeypatch, NB, nu, m, poly, kind):
     """Random block-diagonal skew-Hermitian generators hidden by a permutation (the detection works on the pattern,
     not on contiguous rows), a short last block (padding lanes), one or two controls, odd column counts."""
     monkeypatch.setenv("QOC_TCHAIN_POLY", poly)
     prob, u = _block_problem(NB=NB, nblk=5, nu=nu, m=m, seed=NB * 10 + nu + m)
     for device in (False, True):
-        e = _engine(prob, 2, True, monkeypatch)
+        e = _engine(prob, 2, True if kind == "mfma" else "valu", monkeypatch)
         J, g = _eval(e, u, device)
-        assert e.info()["chain_kernel"] == "blocks"
+        assert e.info()["chain_kernel"] == ("blocks_mfma" if kind == "mfma" else "blocks")
         e.close()
         for b in range(2):
             J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
@@ -193,7 +201,7 @@ def test_blocks_external_cost_and_zcalibrated(built_lib, monkeypatch):
     e.propagate(u)
     lam = np.stack([dJf(e.state(prob.Nt, seed=b)) for b in range(2)])
     g = e.grape_sensitivity(u, 3, lambda_final=lam)
-    assert e.info()["chain_kernel"] == "blocks"
+    assert e.info()["chain_kernel"] in BLK
     e.close()
     for b in range(2):
         _, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
@@ -204,7 +212,7 @@ def test_blocks_external_cost_and_zcalibrated(built_lib, monkeypatch):
         e.set_cost_zcalibrated(prob.x_target)
         e.set_chain("taylor")
         J, g = _eval(e, u, device)
-        assert e.info()["chain_kernel"] == "blocks"
+        assert e.info()["chain_kernel"] in BLK
         e.close()
         for b in range(2):
             xN = O.propagate(prob.A0, prob.A, u[b], prob.x0)[-1]
@@ -224,11 +232,11 @@ def test_blocks_off_for_dense_generators(built_lib, monkeypatch):
     dense = dataclasses.replace(prob, A0=-0.05j * H, A=[-0.03j * systems._gue(rng, 20), -0.02j * systems._gue(rng, 20)],
                                 x0=np.eye(20, 2, dtype=complex), x_target=np.eye(20, 2, dtype=complex))
     e = _engine(dense, 1, True, monkeypatch)
-    assert e.info()["chain_kernel"] not in ("blocks", "blocks_mfma")
+    assert e.info()["chain_kernel"] not in BLK
     e.close()
     p16, _ = _block_problem(NB=8, nblk=2, nu=1, m=1, seed=4)  # N = 15
     e = _engine(p16, 1, True, monkeypatch)
-    assert e.info()["chain_kernel"] not in ("blocks", "blocks_mfma")
+    assert e.info()["chain_kernel"] not in BLK
     e.close()
 
 

@@ -60,7 +60,7 @@ def test_zz_batch_full_size(built_lib, chain, monkeypatch):
     """config 2: zz_coupling N=9, m=4, Nt=500, B=512 (first and last seeds of the batch checked)."""
     seeds = list(range(CHECK_SEEDS // 2)) + list(range(512 - CHECK_SEEDS // 2, 512))
     info = _check_config("zz_batch", seeds, None if chain == "auto" else chain, monkeypatch)
-    assert (info["chain_kernel"] == "blocks") == (chain == "auto")
+    assert (info["chain_kernel"] == "blocks_mfma") == (chain == "auto")
 
 
 @pytest.mark.parametrize("chain", ["auto", "dense", "propagators"])
@@ -68,7 +68,7 @@ def test_cavity_full_size(built_lib, chain, monkeypatch):
     """config 3: cavity(20) x qubit N=40, m=2, Nt=1000, B=256."""
     seeds = list(range(0, 256, 256 // CHECK_SEEDS))
     info = _check_config("cavity", seeds, None if chain == "auto" else chain, monkeypatch)
-    assert (info["chain_kernel"] == "blocks") == (chain == "auto")
+    assert (info["chain_kernel"] == "blocks_mfma") == (chain == "auto")
 
 
 @pytest.mark.parametrize("chain", ["auto", "dense", "propagators"])
