@@ -423,54 +423,74 @@ struct BlkRotLane {
 };
 
 // one slice on the wave's 16-row block state (one element per lane, TChainRot<1>::step without the LDS mirror);
-// CAP: D1, D2 of the first substep
+// D1, D2 of the first substep go to cd1, cd2 (the captures).  sg = +1 on imaginary lanes, -1 on real ones: the Ai
+// products enter through the n <-> n^1 swap with that sign, as one FMA.  Chebyshev terms carry y_{t-2} in the Ar
+// MFMA's accumulator input (y_t = Â y_{t-1} + y_{t-2} in one chain), and the term loop runs two terms per
+// iteration with the roles of the two state registers swapped, so no register copies are left in it.
 template <int JR, bool CHEB>
 __device__ __forceinline__ void blkrot_slice(const double (&ar)[JR], const double (&ai)[JR], double& acc, bool act,
-                                             int n, int P, int s, double phr, double phi, double cl,
+                                             double sg, int P, int s, double phr, double phi, double cl,
                                              const double* __restrict__ invt, double& cd1, double& cd2) {
   using R = TChainRot<1>;
-  auto rot = [](double v, double (&bv)[4]) __attribute__((always_inline)) {
-    bv[0] = v;
+  // Ar y + c + sg (Ai y)[n ^ 1]
+  auto prod = [&](double y, double c) __attribute__((always_inline)) {
+    double bv[4];
+    bv[0] = y;
     if constexpr (JR > 1) {
-      bv[1] = R::mv<0x124>(v);  // row_ror:4
-      bv[2] = R::mv<0x128>(v);  // row_ror:8
-      bv[3] = R::mv<0x12C>(v);  // row_ror:12
+      bv[1] = R::mv<0x124>(y);  // row_ror:4
+      bv[2] = R::mv<0x128>(y);  // row_ror:8
+      bv[3] = R::mv<0x12C>(y);  // row_ror:12
     }
+    double d1 = 0.0, d0 = c;
+#pragma unroll
+    for (int j = 0; j < JR; ++j) d1 = MF<double>::mma4(ai[j], bv[j], d1);
+#pragma unroll
+    for (int j = 0; j < JR; ++j) d0 = MF<double>::mma4(ar[j], bv[j], d0);
+    return fma(sg, R::mv<0xB1>(d1), d0);  // quad_perm [1,0,3,2]
   };
   for (int sub = 0; sub < s; ++sub) {
-    double y = act ? acc : 0.0, ym2 = 0.0;
-    acc = (CHEB ? bcast(cl, 0) : 1.0) * y;
-    double bv[4];
-    rot(y, bv);
-    for (int t = 1; t <= P; ++t) {
-      const double ct = CHEB ? bcast(cl, t) : invt[t];
-      __builtin_amdgcn_sched_barrier(0);
-      double d0 = 0.0, d1 = 0.0;
-#pragma unroll
-      for (int j = 0; j < JR; ++j) {
-        d0 = MF<double>::mma4(ar[j], bv[j], d0);
-        d1 = MF<double>::mma4(ai[j], bv[j], d1);
+    const double y0 = act ? acc : 0.0;
+    if constexpr (CHEB) {
+      acc = bcast(cl, 0) * y0;
+      double a = y0, b;
+      {  // t = 1: y_1 = Â y_0 / 2
+        const double D = prod(y0, 0.0);
+        if (sub == 0) cd1 = D;
+        b = 0.5 * D;
+        acc = fma(bcast(cl, 1), b, acc);
       }
-      const double o = R::mv<0xB1>(d1);  // quad_perm [1,0,3,2]: (Ai y)[n ^ 1]
-      const double D = (n & 1) ? d0 + o : d0 - o;
-      if (sub == 0 && t == 1) cd1 = D;
-      if (sub == 0 && t == 2) cd2 = D;
-      double z;
-      if constexpr (CHEB) {
-        z = t == 1 ? 0.5 * D : D + ym2;
-        ym2 = y;
-        acc = fma(ct, z, acc);
+      if (P >= 2) {  // t = 2: the plain product is the second capture
+        const double D = prod(b, 0.0);
+        if (sub == 0) cd2 = D;
+        a = D + a;
+        acc = fma(bcast(cl, 2), a, acc);
       } else {
-        z = D * ct;
+        a = b;  // y_{t-1} in a for the (empty) loop below
+      }
+      // here a = y_{t-1}, b = y_{t-2} for t = 3
+      int t = 3;
+      for (; t + 1 <= P; t += 2) {
+        b = prod(a, b);
+        acc = fma(bcast(cl, t), b, acc);
+        a = prod(b, a);
+        acc = fma(bcast(cl, t + 1), a, acc);
+      }
+      if (t <= P) {
+        b = prod(a, b);
+        acc = fma(bcast(cl, t), b, acc);
+      }
+    } else {
+      acc = y0;
+      double z = y0;
+      for (int t = 1; t <= P; ++t) {
+        const double D = prod(z, 0.0);
+        if (sub == 0 && t == 1) cd1 = D;
+        if (sub == 0 && t == 2) cd2 = D;
+        z = D * invt[t];
         acc += z;
       }
-      y = z;
-      rot(y, bv);
     }
-    if (sub == s - 1) {
-      const double o = R::mv<0xB1>(acc);
-      acc = (n & 1) ? phr * acc + phi * o : phr * acc - phi * o;
-    }
+    if (sub == s - 1) acc = fma(sg * phi, R::mv<0xB1>(acc), phr * acc);
   }
 }
 
@@ -496,6 +516,7 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
   for (int e = tid; e < 64; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
   BlkRotLane ln;
   ln.setup(bk, m);
+  const double sg = (ln.n & 1) ? 1.0 : -1.0;
   double gr[3][JR], gi[3][JR];
   ln.load_gen<false, JR>((const cx<double>*)g.At, N, nu, gr, gi);
   const cx<double>* x0b = (const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0);
@@ -518,7 +539,7 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
   const TStep* stb = g.steps + (size_t)b * Nt;
   const double* ub = g.u + (size_t)b * Nt * nu;
-  constexpr int PD = 2;
+  constexpr int PD = JR == 1 ? 4 : 2;  // step records in flight (packed blocks: short slices)
   TPreN<2> nx[PD];
 #pragma unroll
   for (int i = 0; i < PD; ++i) {
@@ -534,14 +555,16 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
       const int P = __builtin_amdgcn_readfirstlane(st.P), s = __builtin_amdgcn_readfirstlane(st.s);
       double ar[JR], ai[JR], cd1 = 0.0, cd2 = 0.0;
       blkrot_form<JR>(gr, gi, st.u, st.scale, ar, ai);
-      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, ln.n, P, s, st.pr, st.pi, st.cl, invt, cd1, cd2);
+      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, P, s, st.pr, st.pi, st.cl, invt, cd1, cd2);
       const int kn = min(k + PD, Nt - 1);
       tpre_load<2, CHEB, false>(stb + kn, ub + (size_t)kn * nu, nu, nx[i], CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
       *(ln.act ? Xb + (size_t)(k + 1) * 2 * Nm + oe : sink) = acc;
       pen += pm ? acc * acc : 0.0;
-      const bool to = cap && ln.act;
-      *(to ? c1b + (size_t)k * 2 * Nm + oe : sink) = cd1;
-      *(to ? c2b + (size_t)k * 2 * Nm + oe : sink + 1) = cd2;
+      if constexpr (JR > 1) {  // packed blocks (JR = 1) feed k_blk_grad, which forms its own products
+        const bool to = cap && ln.act;
+        *(to ? c1b + (size_t)k * 2 * Nm + oe : sink) = cd1;
+        *(to ? c2b + (size_t)k * 2 * Nm + oe : sink + 1) = cd2;
+      }
     }
   if (ln.act) xN[oe] = acc;
   __syncthreads();
@@ -558,6 +581,7 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
   for (int e = tid; e < 64; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
   BlkRotLane ln;
   ln.setup(bk, m);
+  const double sg = (ln.n & 1) ? 1.0 : -1.0;
   double gr[3][JR], gi[3][JR];
   ln.load_gen<true, JR>((const cx<double>*)g.At, N, nu, gr, gi);
   const double* Xb = reinterpret_cast<const double*>((const cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm);
@@ -593,7 +617,7 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
   const TStep* stb = g.steps + (size_t)b * Nt;
   const double* ub = g.u + (size_t)b * Nt * nu;
-  constexpr int PD = 2;
+  constexpr int PD = JR == 1 ? 4 : 2;  // step records in flight (packed blocks: short slices)
   TPreN<2> nx[PD];
 #pragma unroll
   for (int i = 0; i < PD; ++i) {
@@ -612,14 +636,16 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
       if (srcl) xa += srcb[ok_];
       double ar[JR], ai[JR], cd1 = 0.0, cd2 = 0.0;
       blkrot_form<JR>(gr, gi, st.u, st.scale, ar, ai);
-      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, ln.n, P, s, st.pr, -st.pi, st.cl, invt, cd1, cd2);
+      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, P, s, st.pr, -st.pi, st.cl, invt, cd1, cd2);
       const int kp = max(k - PD, 0);
       tpre_load<2, CHEB, false>(stb + kp, ub + (size_t)kp * nu, nu, nx[i], CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
       acc += xa;
       *(ln.act ? Lb + ok_ : sink) = acc;
-      const bool to = cap && ln.act;
-      *(to ? c1b + ok_ : sink) = cd1;
-      *(to ? c2b + ok_ : sink + 1) = cd2;
+      if constexpr (JR > 1) {
+        const bool to = cap && ln.act;
+        *(to ? c1b + ok_ : sink) = cd1;
+        *(to ? c2b + ok_ : sink + 1) = cd2;
+      }
     }
 }
 

@@ -10,7 +10,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("k_blk_dual", "k_blk_grad", "k_blk_fwd", "k_blk_bwd", "k_tchain_mf_dual", "k_grad_rr_c", "k_spec_bound", "k_tchain_mf_fwd", "k_tchain_mf_bwd", "k_tchain_prep", "k_tchain_fwd", "k_tchain_bwd", "k_pade_units",
+KERNELS = ("k_blkrot_dual", "k_blkrot_fwd", "k_blkrot_bwd", "k_blk_dual", "k_blk_grad", "k_blk_fwd", "k_blk_bwd", "k_tchain_mf_dual", "k_grad_rr_c", "k_spec_bound", "k_tchain_mf_fwd", "k_tchain_mf_bwd", "k_tchain_prep", "k_tchain_fwd", "k_tchain_bwd", "k_pade_units",
            "k_argmin_seed", "k_expm_rr_ps", "k_expm_rr_mix", "k_expm_rr", "k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad_rr_q", "k_grad_rr_p", "k_grad_rr_s", "k_grad", "k_bgemm", "k_form_norm", "k_lincomb", "k_gen_contract")
 
 
@@ -47,6 +47,8 @@ def main(out_dir, cfg, tag, repo="."):
     fetch = pmc(os.path.join(out_dir, "pmc_fetch"))
     write = pmc(os.path.join(out_dir, "pmc_write"))
     sq = pmc(os.path.join(out_dir, "pmc_sq"))
+    for k, v in pmc(os.path.join(out_dir, "pmc_sq2")).items():  # second SQ pass (wait / busy cycles)
+        sq.setdefault(k, {}).update(v)
     lines = [f"# rocprofv3 summary — {tag}, config `{cfg}`", "",
              f"Source: `{src}` (kernel-trace --stats of `bench.py --config {cfg} --warmup 1 --no-cpu` (tools/profile*.sh)).", "",
              "| kernel | calls | avg ms | total ms | % |", "|---|---|---|---|---|"]
