@@ -505,6 +505,91 @@ __device__ __forceinline__ void blkrot_form(const double (&gr)[3][JR], const dou
   }
 }
 
+// Step records of the MFMA block waves, staged through a per-wave LDS slot in chunks of BLK_CH slices.  A slice
+// of packed blocks is short (~9 terms of a few dozen cycles), shorter than an HBM round trip; with per-slice
+// register prefetches the compiler's vmcnt waits at the loop head also covered the newest prefetches, so every
+// slice waited for memory (~0.75 us per slice measured).  Here the loads of chunk c + 1 are issued at the start of
+// chunk c into registers and written to LDS at the start of chunk c + 1 (one wait per chunk); the slices read
+// their record (broadcast) and this lane's Chebyshev coefficient from LDS.
+constexpr int BLK_CH = 8;
+constexpr int BLK_STAGE = BLK_CH * (8 + 64);  // doubles per wave: [CH][8] records + [CH][64] coefficients
+struct BlkStage {
+  double* rec;  // this wave's [CH][8]: pr, pi, (P | s << 32), scale, u_1, u_2
+  double* cof;  // this wave's [CH][64]
+  double4 t4;
+  double u0, u1;
+  double rc[BLK_CH];
+};
+// loads of the chunk whose slice j is k = kfirst + dir j (clamped: the same loads on every path)
+template <bool CHEB>
+__device__ __forceinline__ void blk_stage_issue(BlkStage& S, const TStep* __restrict__ stb, const double* __restrict__ ub,
+                                                const double* __restrict__ ceb, int nu, int Nt, int kfirst, int dir) {
+  const int l = threadIdx.x & 63;
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // per-lane (VGPR) address: vector loads, not s_load (see tpre_load)
+  const int kl = min(max(kfirst + dir * (l & (BLK_CH - 1)), 0), Nt - 1);
+  S.t4 = *reinterpret_cast<const double4*>(reinterpret_cast<const double*>(stb + kl) + z);
+  S.u0 = ub[(size_t)kl * nu + z];
+  S.u1 = ub[(size_t)kl * nu + min(1, nu - 1) + z];
+  if constexpr (CHEB) {
+#pragma unroll
+    for (int j = 0; j < BLK_CH; ++j) {
+      const int kj = min(max(kfirst + dir * j, 0), Nt - 1);
+      S.rc[j] = ceb[(size_t)kj * TCHEB_STRIDE + l + z];
+    }
+  }
+}
+template <bool CHEB>
+__device__ __forceinline__ void blk_stage_commit(BlkStage& S) {
+  const int l = threadIdx.x & 63;
+  if (l < BLK_CH) {
+    double* r = S.rec + 8 * l;
+    r[0] = S.t4.x;
+    r[1] = S.t4.y;
+    r[2] = S.t4.z;
+    r[3] = S.t4.w;
+    r[4] = S.u0;
+    r[5] = S.u1;
+  }
+  if constexpr (CHEB) {
+#pragma unroll
+    for (int j = 0; j < BLK_CH; ++j) S.cof[64 * j + l] = S.rc[j];
+  }
+}
+// slice j of the staged chunk
+struct BlkRec {
+  double pr, pi, scale, u[2], cl;
+  int P, s;
+};
+template <bool CHEB>
+__device__ __forceinline__ BlkRec blk_stage_read(const BlkStage& S, int j) {
+  const double* r = S.rec + 8 * j;
+  BlkRec q;
+  q.pr = r[0];
+  q.pi = r[1];
+  const long long ps = __double_as_longlong(r[2]);
+  q.P = __builtin_amdgcn_readfirstlane((int)(ps & 0xffffffff));
+  q.s = __builtin_amdgcn_readfirstlane((int)(ps >> 32));
+  q.scale = r[3];
+  q.u[0] = r[4];
+  q.u[1] = r[5];
+  q.cl = CHEB ? S.cof[64 * j + (threadIdx.x & 63)] : 0.0;
+  return q;
+}
+// LDS of the MFMA block waves: blk_lds + one staging slot per wave
+__host__ __device__ inline size_t blkrot_lds(int N, int m, int waves) {
+  return blk_lds(N, m) + (size_t)waves * BLK_STAGE * sizeof(double);
+}
+// after_xN: 80 + 2 N m doubles into the dynamic LDS, 16-byte aligned.  No integer round trip on the pointer: the
+// compiler must still see an LDS address (a generic one becomes flat_load, whose waitcnt drains vmcnt as well)
+__device__ __forceinline__ BlkStage blk_stage_slot(double* after_xN) {
+  double* base = after_xN;
+  BlkStage S;
+  S.rec = base + (size_t)(threadIdx.x >> 6) * BLK_STAGE;
+  S.cof = S.rec + 8 * BLK_CH;
+  return S;
+}
+
 template <int JR, bool CHEB>
 __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkArgs& bk, const int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -539,25 +624,18 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
   const TStep* stb = g.steps + (size_t)b * Nt;
   const double* ub = g.u + (size_t)b * Nt * nu;
-  constexpr int PD = JR == 1 ? 4 : 2;  // step records in flight (packed blocks: short slices)
-  TPreN<2> nx[PD];
-#pragma unroll
-  for (int i = 0; i < PD; ++i) {
-    const int ki = min(i, Nt - 1);
-    tpre_load<2, CHEB, false>(stb + ki, ub + (size_t)ki * nu, nu, nx[i], CHEB ? ceb + (size_t)ki * TCHEB_STRIDE : nullptr);
-  }
-  for (int k0 = 0; k0 < Nt; k0 += PD)
-#pragma unroll
-    for (int i = 0; i < PD; ++i) {
-      const int k = k0 + i;
+  BlkStage S = blk_stage_slot(xN + 2 * Nm);
+  blk_stage_issue<CHEB>(S, stb, ub, ceb, nu, Nt, 0, 1);
+  for (int c0 = 0; c0 < Nt; c0 += BLK_CH) {
+    blk_stage_commit<CHEB>(S);
+    if (c0 + BLK_CH < Nt) blk_stage_issue<CHEB>(S, stb, ub, ceb, nu, Nt, c0 + BLK_CH, 1);
+    for (int j = 0; j < BLK_CH; ++j) {
+      const int k = c0 + j;
       if (k >= Nt) break;
-      const TPreN<2>& st = nx[i];
-      const int P = __builtin_amdgcn_readfirstlane(st.P), s = __builtin_amdgcn_readfirstlane(st.s);
+      const BlkRec st = blk_stage_read<CHEB>(S, j);
       double ar[JR], ai[JR], cd1 = 0.0, cd2 = 0.0;
       blkrot_form<JR>(gr, gi, st.u, st.scale, ar, ai);
-      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, P, s, st.pr, st.pi, st.cl, invt, cd1, cd2);
-      const int kn = min(k + PD, Nt - 1);
-      tpre_load<2, CHEB, false>(stb + kn, ub + (size_t)kn * nu, nu, nx[i], CHEB ? ceb + (size_t)kn * TCHEB_STRIDE : nullptr);
+      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, st.P, st.s, st.pr, st.pi, st.cl, invt, cd1, cd2);
       *(ln.act ? Xb + (size_t)(k + 1) * 2 * Nm + oe : sink) = acc;
       pen += pm ? acc * acc : 0.0;
       if constexpr (JR > 1) {  // packed blocks (JR = 1) feed k_blk_grad, which forms its own products
@@ -566,6 +644,7 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
         *(to ? c2b + (size_t)k * 2 * Nm + oe : sink + 1) = cd2;
       }
     }
+  }
   if (ln.act) xN[oe] = acc;
   __syncthreads();
   chain_costs<double>(N, m, (const cx<double>*)g.Xt, [&](int q) { return cx<double>{xN[2 * q], xN[2 * q + 1]}; },
@@ -617,28 +696,21 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
   const double* ceb = CHEB ? g.tcoef + (size_t)b * Nt * TCHEB_STRIDE : nullptr;
   const TStep* stb = g.steps + (size_t)b * Nt;
   const double* ub = g.u + (size_t)b * Nt * nu;
-  constexpr int PD = JR == 1 ? 4 : 2;  // step records in flight (packed blocks: short slices)
-  TPreN<2> nx[PD];
-#pragma unroll
-  for (int i = 0; i < PD; ++i) {
-    const int ki = max(Nt - 1 - i, 0);
-    tpre_load<2, CHEB, false>(stb + ki, ub + (size_t)ki * nu, nu, nx[i], CHEB ? ceb + (size_t)ki * TCHEB_STRIDE : nullptr);
-  }
-  for (int k0 = Nt - 1; k0 >= 0; k0 -= PD)
-#pragma unroll
-    for (int i = 0; i < PD; ++i) {
-      const int k = k0 - i;
+  BlkStage S = blk_stage_slot(reinterpret_cast<double*>(smem) + 80 + 2 * Nm);
+  blk_stage_issue<CHEB>(S, stb, ub, ceb, nu, Nt, Nt - 1, -1);
+  for (int c0 = 0; c0 < Nt; c0 += BLK_CH) {
+    blk_stage_commit<CHEB>(S);
+    if (c0 + BLK_CH < Nt) blk_stage_issue<CHEB>(S, stb, ub, ceb, nu, Nt, Nt - 1 - (c0 + BLK_CH), -1);
+    for (int j = 0; j < BLK_CH; ++j) {
+      const int k = Nt - 1 - (c0 + j);
       if (k < 0) break;
-      const TPreN<2>& st = nx[i];
-      const int P = __builtin_amdgcn_readfirstlane(st.P), s = __builtin_amdgcn_readfirstlane(st.s);
+      const BlkRec st = blk_stage_read<CHEB>(S, j);
       const size_t ok_ = (size_t)k * 2 * Nm + oe;
       double xa = pm ? tmu * Xb[ok_] : 0.0;  // 2μ x_k on the mask + the caller's dL/dx(x_k), after the slice
       if (srcl) xa += srcb[ok_];
       double ar[JR], ai[JR], cd1 = 0.0, cd2 = 0.0;
       blkrot_form<JR>(gr, gi, st.u, st.scale, ar, ai);
-      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, P, s, st.pr, -st.pi, st.cl, invt, cd1, cd2);
-      const int kp = max(k - PD, 0);
-      tpre_load<2, CHEB, false>(stb + kp, ub + (size_t)kp * nu, nu, nx[i], CHEB ? ceb + (size_t)kp * TCHEB_STRIDE : nullptr);
+      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, st.P, st.s, st.pr, -st.pi, st.cl, invt, cd1, cd2);
       acc += xa;
       *(ln.act ? Lb + ok_ : sink) = acc;
       if constexpr (JR > 1) {
@@ -647,18 +719,19 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
         *(to ? c2b + ok_ : sink + 1) = cd2;
       }
     }
+  }
 }
 
 template <int JR, bool CHEB>
-__global__ __launch_bounds__(1024) void k_blkrot_fwd(const TChainArgs g, const BlkArgs bk) {
+__global__ __launch_bounds__(512) void k_blkrot_fwd(const TChainArgs g, const BlkArgs bk) {
   blkrot_fwd_body<JR, CHEB>(g, bk, blockIdx.x);
 }
 template <int JR, bool CHEB>
-__global__ __launch_bounds__(1024) void k_blkrot_bwd(const TChainArgs g, const BlkArgs bk) {
+__global__ __launch_bounds__(512) void k_blkrot_bwd(const TChainArgs g, const BlkArgs bk) {
   blkrot_bwd_body<JR, CHEB>(g, bk, blockIdx.x);
 }
 template <int JR, bool CHEB>
-__global__ __launch_bounds__(1024) void k_blkrot_dual(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk) {
+__global__ __launch_bounds__(512) void k_blkrot_dual(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk) {
   const int i = blockIdx.x, B = gridDim.x >> 1;
   const bool by8 = (B & 7) == 0;
   const int dir = by8 ? (i >> 3) & 1 : i & 1;

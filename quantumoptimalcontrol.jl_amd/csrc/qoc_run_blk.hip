@@ -104,7 +104,8 @@ bool blk_active(const qoc_ctx* c) {
   if (c->blk_nb <= 0 || c->prec != QOC_FP64 || c->chain_mode != 1 || c->prop_method != QOC_PROP_EXPM || c->big ||
       c->packed || c->nu > 2)
     return false;
-  if (c->blk_jr) return c->nwb * ((c->m + 1) / 2) <= 16 && (c->blk_nb < 16 || tchain_mf(c));  // MFMA block waves
+  // MFMA block waves: <= 8 per workgroup (the 512-thread launch bound keeps 256 VGPRs per wave)
+  if (c->blk_jr) return c->nwb * ((c->m + 1) / 2) <= 8 && (c->blk_nb < 16 || tchain_mf(c));
   return c->nblk * c->m <= BLK_MAXT && c->nblk <= 256;
 }
 // MFMA block waves (k_blkrot_*): the chain kernels; blocks of 16 rows also take the dense gradient kernels
@@ -123,6 +124,15 @@ static BlkArgs blk_args(const qoc_ctx* c) {
 
 static int blk_threads(const qoc_ctx* c) {
   return blk_rot(c) ? 64 * c->nwb * ((c->m + 1) / 2) : 64 * ((c->nblk * c->m + 63) / 64);
+}
+static size_t blk_lds_of(const qoc_ctx* c) {
+  return blk_rot(c) ? blkrot_lds(c->N, c->m, blk_threads(c) / 64) : blk_lds(c->N, c->m);
+}
+// dynamic LDS above the 64 KiB default (up to 16 MFMA block waves of staging)
+template <typename K>
+static hipError_t blk_lds_attr(K kern, size_t lds) {
+  return lds > 65536 ? hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)
+                     : hipSuccess;
 }
 
 // f(kernel-selector, Chebyshev): selector 1 / 4 = k_blkrot_*<JR>, 2 / 3 / 4 + 100 = k_blk_*<NB> (VALU lanes)
@@ -145,12 +155,16 @@ int blk_forward(qoc_ctx* c) {
   if (r) return r;
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
-  const size_t lds = blk_lds(c->N, c->m);
+  const size_t lds = blk_lds_of(c);
   const int mk = mark_begin(c, 1);
   const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
     constexpr int NB = decltype(NB_)::value;
     constexpr bool CH = decltype(CH_)::value;
-    if constexpr (NB < 100) hipLaunchKernelGGL((k_blkrot_fwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    if constexpr (NB < 100) {
+      const hipError_t q = blk_lds_attr(k_blkrot_fwd<NB, CH>, lds);
+      if (q != hipSuccess) return q;
+      hipLaunchKernelGGL((k_blkrot_fwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    }
     else hipLaunchKernelGGL((k_blk_fwd<NB - 100, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
     return hipGetLastError();
   });
@@ -193,12 +207,16 @@ static int blk_grad(qoc_ctx* c, int order, bool mu_mode, double* d_dJdu) {
 int blk_backward(qoc_ctx* c, int order, double* d_dJdu) {
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
-  const size_t lds = blk_lds(c->N, c->m);
+  const size_t lds = blk_lds_of(c);
   int mk = mark_begin(c, 2);
   const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
     constexpr int NB = decltype(NB_)::value;
     constexpr bool CH = decltype(CH_)::value;
-    if constexpr (NB < 100) hipLaunchKernelGGL((k_blkrot_bwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    if constexpr (NB < 100) {
+      const hipError_t q = blk_lds_attr(k_blkrot_bwd<NB, CH>, lds);
+      if (q != hipSuccess) return q;
+      hipLaunchKernelGGL((k_blkrot_bwd<NB, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
+    }
     else hipLaunchKernelGGL((k_blk_bwd<NB - 100, CH>), dim3(c->B), dim3(blk_threads(c)), lds, c->stream, g, bk);
     return hipGetLastError();
   });
@@ -236,12 +254,16 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
     gb.cap2 = (cx<double>*)c->d_gws + bufN;
   }
   const BlkArgs bk = blk_args(c);
-  const size_t lds = blk_lds(c->N, c->m);
+  const size_t lds = blk_lds_of(c);
   const int mk = mark_begin(c, 1);
   const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
     constexpr int NB = decltype(NB_)::value;
     constexpr bool CH = decltype(CH_)::value;
-    if constexpr (NB < 100) hipLaunchKernelGGL((k_blkrot_dual<NB, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
+    if constexpr (NB < 100) {
+      const hipError_t q = blk_lds_attr(k_blkrot_dual<NB, CH>, lds);
+      if (q != hipSuccess) return q;
+      hipLaunchKernelGGL((k_blkrot_dual<NB, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
+    }
     else hipLaunchKernelGGL((k_blk_dual<NB - 100, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
     return hipGetLastError();
   });
