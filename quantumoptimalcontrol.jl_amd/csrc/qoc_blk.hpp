@@ -427,10 +427,13 @@ struct BlkRotLane {
 // products enter through the n <-> n^1 swap with that sign, as one FMA.  Chebyshev terms carry y_{t-2} in the Ar
 // MFMA's accumulator input (y_t = Â y_{t-1} + y_{t-2} in one chain), and the term loop runs two terms per
 // iteration with the roles of the two state registers swapped, so no register copies are left in it.
+// cof: the slice's staged Chebyshev coefficients in LDS (c_t at cof[t], read as broadcasts: one ds_read2 per two
+// terms instead of two v_readlane per term on the VALU)
 template <int JR, bool CHEB>
 __device__ __forceinline__ void blkrot_slice(const double (&ar)[JR], const double (&ai)[JR], double& acc, bool act,
-                                             double sg, int P, int s, double phr, double phi, double cl,
-                                             const double* __restrict__ invt, double& cd1, double& cd2) {
+                                             double sg, int P, int s, double phr, double phi,
+                                             const double* __restrict__ cof, const double* __restrict__ invt,
+                                             double& cd1, double& cd2) {
   using R = TChainRot<1>;
   // Ar y + c + sg (Ai y)[n ^ 1]
   auto prod = [&](double y, double c) __attribute__((always_inline)) {
@@ -451,33 +454,36 @@ __device__ __forceinline__ void blkrot_slice(const double (&ar)[JR], const doubl
   for (int sub = 0; sub < s; ++sub) {
     const double y0 = act ? acc : 0.0;
     if constexpr (CHEB) {
-      acc = bcast(cl, 0) * y0;
+      const double c0 = cof[0], c1 = cof[1], c2 = cof[2];
+      acc = c0 * y0;
       double a = y0, b;
       {  // t = 1: y_1 = Â y_0 / 2
         const double D = prod(y0, 0.0);
         if (sub == 0) cd1 = D;
         b = 0.5 * D;
-        acc = fma(bcast(cl, 1), b, acc);
+        acc = fma(c1, b, acc);
       }
       if (P >= 2) {  // t = 2: the plain product is the second capture
         const double D = prod(b, 0.0);
         if (sub == 0) cd2 = D;
         a = D + a;
-        acc = fma(bcast(cl, 2), a, acc);
+        acc = fma(c2, a, acc);
       } else {
         a = b;  // y_{t-1} in a for the (empty) loop below
       }
       // here a = y_{t-1}, b = y_{t-2} for t = 3
       int t = 3;
       for (; t + 1 <= P; t += 2) {
+        const double ca = cof[t], cb = cof[t + 1];
         b = prod(a, b);
-        acc = fma(bcast(cl, t), b, acc);
+        acc = fma(ca, b, acc);
         a = prod(b, a);
-        acc = fma(bcast(cl, t + 1), a, acc);
+        acc = fma(cb, a, acc);
       }
       if (t <= P) {
+        const double ca = cof[t];
         b = prod(a, b);
-        acc = fma(bcast(cl, t), b, acc);
+        acc = fma(ca, b, acc);
       }
     } else {
       acc = y0;
@@ -573,7 +579,7 @@ __device__ __forceinline__ BlkRec blk_stage_read(const BlkStage& S, int j) {
   q.scale = r[3];
   q.u[0] = r[4];
   q.u[1] = r[5];
-  q.cl = CHEB ? S.cof[64 * j + (threadIdx.x & 63)] : 0.0;
+  q.cl = 0.0;
   return q;
 }
 // LDS of the MFMA block waves: blk_lds + one staging slot per wave
@@ -635,7 +641,7 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
       const BlkRec st = blk_stage_read<CHEB>(S, j);
       double ar[JR], ai[JR], cd1 = 0.0, cd2 = 0.0;
       blkrot_form<JR>(gr, gi, st.u, st.scale, ar, ai);
-      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, st.P, st.s, st.pr, st.pi, st.cl, invt, cd1, cd2);
+      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, st.P, st.s, st.pr, st.pi, S.cof + 64 * j, invt, cd1, cd2);
       *(ln.act ? Xb + (size_t)(k + 1) * 2 * Nm + oe : sink) = acc;
       pen += pm ? acc * acc : 0.0;
       if constexpr (JR > 1) {  // packed blocks (JR = 1) feed k_blk_grad, which forms its own products
@@ -710,7 +716,7 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
       if (srcl) xa += srcb[ok_];
       double ar[JR], ai[JR], cd1 = 0.0, cd2 = 0.0;
       blkrot_form<JR>(gr, gi, st.u, st.scale, ar, ai);
-      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, st.P, st.s, st.pr, -st.pi, st.cl, invt, cd1, cd2);
+      blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, st.P, st.s, st.pr, -st.pi, S.cof + 64 * j, invt, cd1, cd2);
       acc += xa;
       *(ln.act ? Lb + ok_ : sink) = acc;
       if constexpr (JR > 1) {
