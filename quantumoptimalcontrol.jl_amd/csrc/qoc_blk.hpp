@@ -382,42 +382,67 @@ __global__ __launch_bounds__(BLK_MAXT) void k_blk_dual(const TChainArgs gf, cons
 struct BlkRotLane {
   int n, cp, beta;
   int rowE;     // global row of this lane's D element (-1: padding, or no block)
+  int pe;       // the D element's part: 0 real, 1 imaginary
   int colD;     // state column of the D element
   bool act;     // rowE >= 0 && colD < m
-  int rowA;     // global row of the lane's A-operand entries
-  int colA[4];  // global column of the A-operand entry of rotation j
+  int rowA;     // global row of the lane's A-operand entries (JR = 0: row * 2 + part)
+  int colA[4];  // global column of the A-operand entry of rotation j (JR = 0: column * 2 + part)
+  // JR = 0 (real embedding): wrow entries are row * 2 + part, a wave holds 4 complex state columns (n)
+  template <int JR>
   __device__ __forceinline__ void setup(const BlkArgs& bk, int m) {
     const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int b = (l >> 2) & 3, kl = l >> 4, lo = l & 3;
-    const bool wok = w < bk.nwb * ((m + 1) / 2);
+    const int CPW = JR == 0 ? (m + 3) / 4 : (m + 1) / 2;
+    const bool wok = w < bk.nwb * CPW;
     beta = wok ? w % bk.nwb : 0;
     cp = wok ? w / bk.nwb : 0;
     n = lo;
-    colD = 2 * cp + (n >> 1);
     const int* rb = bk.wrow + beta * 16;
-    rowE = wok ? rb[4 * b + kl] : -1;
-    act = rowE >= 0 && colD < m;
-    rowA = wok ? rb[4 * b + lo] : -1;
-    const int q[4] = {b, __builtin_amdgcn_update_dpp(0, b, 0x124, 0xf, 0xf, false),   // row_ror:4
-                      __builtin_amdgcn_update_dpp(0, b, 0x128, 0xf, 0xf, false),      // row_ror:8
-                      __builtin_amdgcn_update_dpp(0, b, 0x12C, 0xf, 0xf, false)};     // row_ror:12
+    const int e = wok ? rb[4 * b + kl] : -1;
+    if constexpr (JR == 0) {
+      colD = 4 * cp + n;
+      rowE = e >= 0 ? e >> 1 : -1;
+      pe = e >= 0 ? e & 1 : 0;
+      rowA = wok ? rb[4 * b + lo] : -1;
+      colA[0] = e;
+      colA[1] = colA[2] = colA[3] = -1;
+    } else {
+      colD = 2 * cp + (n >> 1);
+      rowE = e;
+      pe = n & 1;
+      rowA = wok ? rb[4 * b + lo] : -1;
+      const int q[4] = {b, __builtin_amdgcn_update_dpp(0, b, 0x124, 0xf, 0xf, false),   // row_ror:4
+                        __builtin_amdgcn_update_dpp(0, b, 0x128, 0xf, 0xf, false),      // row_ror:8
+                        __builtin_amdgcn_update_dpp(0, b, 0x12C, 0xf, 0xf, false)};     // row_ror:12
 #pragma unroll
-    for (int j = 0; j < 4; ++j) colA[j] = wok ? rb[4 * q[j] + kl] : -1;
+      for (int j = 0; j < 4; ++j) colA[j] = wok ? rb[4 * q[j] + kl] : -1;
+    }
+    act = rowE >= 0 && colD < m;
   }
-  // the A-operand entries of Ã_0..Ã_2 (HERM: of Ã_j^H), zero outside the block and for j > nu
-  template <bool HERM, int JR>
-  __device__ __forceinline__ void load_gen(const cx<double>* __restrict__ At, int N, int nu, double (&gr)[3][JR],
-                                           double (&gi)[3][JR]) const {
+  // the A-operand entries of Ã_0..Ã_2 (HERM: of Ã_j^H), zero outside the block and for j > nu.  JR = 0: the real
+  // embedding [[Re, -Im], [Im, Re]] of the complex entry (rows / columns carry their part), in gr (gi unused)
+  template <bool HERM, int JR, int JA>
+  __device__ __forceinline__ void load_gen(const cx<double>* __restrict__ At, int N, int nu, double (&gr)[3][JA],
+                                           double (&gi)[3][JA]) const {
     const size_t NN = (size_t)N * N;
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
-      for (int x = 0; x < JR; ++x) {
-        const bool ok = j <= nu && rowA >= 0 && colA[x] >= 0;
-        const int rr = max(rowA, 0), cc = max(colA[x], 0);
-        const cx<double> v = At[(size_t)min(j, nu) * NN + (HERM ? cc + (size_t)N * rr : rr + (size_t)N * cc)];
-        gr[j][x] = ok ? v.r : 0.0;
-        gi[j][x] = ok ? (HERM ? -v.i : v.i) : 0.0;
+      for (int x = 0; x < JA; ++x) {
+        if constexpr (JR == 0) {
+          const bool ok = j <= nu && rowA >= 0 && colA[0] >= 0;
+          const int rr = max(rowA, 0) >> 1, cc = max(colA[0], 0) >> 1, p1 = rowA & 1, p2 = colA[0] & 1;
+          const cx<double> v = At[(size_t)min(j, nu) * NN + (HERM ? cc + (size_t)N * rr : rr + (size_t)N * cc)];
+          const double a = v.r, bi = HERM ? -v.i : v.i;
+          gr[j][x] = ok ? (p1 == p2 ? a : (p1 == 0 ? -bi : bi)) : 0.0;
+          gi[j][x] = 0.0;
+        } else {
+          const bool ok = j <= nu && rowA >= 0 && colA[x] >= 0;
+          const int rr = max(rowA, 0), cc = max(colA[x], 0);
+          const cx<double> v = At[(size_t)min(j, nu) * NN + (HERM ? cc + (size_t)N * rr : rr + (size_t)N * cc)];
+          gr[j][x] = ok ? v.r : 0.0;
+          gi[j][x] = ok ? (HERM ? -v.i : v.i) : 0.0;
+        }
       }
   }
 };
@@ -429,14 +454,15 @@ struct BlkRotLane {
 // iteration with the roles of the two state registers swapped, so no register copies are left in it.
 // cof: the slice's staged Chebyshev coefficients in LDS (c_t at cof[t], read as broadcasts: one ds_read2 per two
 // terms instead of two v_readlane per term on the VALU)
-template <int JR, bool CHEB>
-__device__ __forceinline__ void blkrot_slice(const double (&ar)[JR], const double (&ai)[JR], double& acc, bool act,
+template <int JR, bool CHEB, int JA = (JR ? JR : 1)>
+__device__ __forceinline__ void blkrot_slice(const double (&ar)[JA], const double (&ai)[JA], double& acc, bool act,
                                              double sg, int P, int s, double phr, double phi,
                                              const double* __restrict__ cof, const double* __restrict__ invt,
                                              double& cd1, double& cd2) {
   using R = TChainRot<1>;
   // Ar y + c + sg (Ai y)[n ^ 1]
   auto prod = [&](double y, double c) __attribute__((always_inline)) {
+    if constexpr (JR == 0) return MF<double>::mma4(ar[0], y, c);  // real embedding: one real 4x4 per slot
     double bv[4];
     bv[0] = y;
     if constexpr (JR > 1) {
@@ -496,16 +522,19 @@ __device__ __forceinline__ void blkrot_slice(const double (&ar)[JR], const doubl
         acc += z;
       }
     }
-    if (sub == s - 1) acc = fma(sg * phi, R::mv<0xB1>(acc), phr * acc);
+    if (sub == s - 1) {  // e^{μ}: the partner part of the element is lane n ^ 1 (complex slots) or l ^ 32 (real)
+      const double o = JR == 0 ? __shfl_xor(acc, 32) : R::mv<0xB1>(acc);
+      acc = fma(sg * phi, o, phr * acc);
+    }
   }
 }
 
-template <int JR>
-__device__ __forceinline__ void blkrot_form(const double (&gr)[3][JR], const double (&gi)[3][JR], const double (&u)[2],
-                                            double scale, double (&ar)[JR], double (&ai)[JR]) {
+template <int JA>
+__device__ __forceinline__ void blkrot_form(const double (&gr)[3][JA], const double (&gi)[3][JA], const double (&u)[2],
+                                            double scale, double (&ar)[JA], double (&ai)[JA]) {
   const double u1 = u[0] * scale, u2 = u[1] * scale;
 #pragma unroll
-  for (int x = 0; x < JR; ++x) {
+  for (int x = 0; x < JA; ++x) {
     ar[x] = fma(u2, gr[2][x], fma(u1, gr[1][x], scale * gr[0][x]));
     ai[x] = fma(u2, gi[2][x], fma(u1, gi[1][x], scale * gi[0][x]));
   }
@@ -605,19 +634,20 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
   const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, tid = threadIdx.x, nthr = blockDim.x;
   const size_t Nm = (size_t)N * m;
   for (int e = tid; e < 64; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
+  constexpr int JA = JR ? JR : 1;
   BlkRotLane ln;
-  ln.setup(bk, m);
-  const double sg = (ln.n & 1) ? 1.0 : -1.0;
-  double gr[3][JR], gi[3][JR];
-  ln.load_gen<false, JR>((const cx<double>*)g.At, N, nu, gr, gi);
+  ln.setup<JR>(bk, m);
+  const double sg = ln.pe ? 1.0 : -1.0;
+  double gr[3][JA], gi[3][JA];
+  ln.load_gen<false, JR, JA>((const cx<double>*)g.At, N, nu, gr, gi);
   const cx<double>* x0b = (const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0);
   double* Xb = reinterpret_cast<double*>((cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm);
   double* const sink = tchain_sink(g);
-  const size_t o = (size_t)ln.colD * N + max(ln.rowE, 0), oe = 2 * o + (ln.n & 1);
+  const size_t o = (size_t)ln.colD * N + max(ln.rowE, 0), oe = 2 * o + ln.pe;
   double acc = 0.0;
   if (ln.act) {
     const cx<double> v = x0b[o];
-    acc = (ln.n & 1) ? v.i : v.r;
+    acc = ln.pe ? v.i : v.r;
   }
   const bool pm = ln.act && g.pmask && g.pmask[o];
   const bool cap = g.cap1 != nullptr;
@@ -639,8 +669,8 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
       const int k = c0 + j;
       if (k >= Nt) break;
       const BlkRec st = blk_stage_read<CHEB>(S, j);
-      double ar[JR], ai[JR], cd1 = 0.0, cd2 = 0.0;
-      blkrot_form<JR>(gr, gi, st.u, st.scale, ar, ai);
+      double ar[JA], ai[JA], cd1 = 0.0, cd2 = 0.0;
+      blkrot_form<JA>(gr, gi, st.u, st.scale, ar, ai);
       blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, st.P, st.s, st.pr, st.pi, S.cof + 64 * j, invt, cd1, cd2);
       *(ln.act ? Xb + (size_t)(k + 1) * 2 * Nm + oe : sink) = acc;
       pen += pm ? acc * acc : 0.0;
@@ -664,11 +694,12 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
   const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, tid = threadIdx.x, nthr = blockDim.x;
   const size_t Nm = (size_t)N * m;
   for (int e = tid; e < 64; e += nthr) invt[e] = e ? 1.0 / e : 0.0;
+  constexpr int JA = JR ? JR : 1;
   BlkRotLane ln;
-  ln.setup(bk, m);
-  const double sg = (ln.n & 1) ? 1.0 : -1.0;
-  double gr[3][JR], gi[3][JR];
-  ln.load_gen<true, JR>((const cx<double>*)g.At, N, nu, gr, gi);
+  ln.setup<JR>(bk, m);
+  const double sg = ln.pe ? 1.0 : -1.0;
+  double gr[3][JA], gi[3][JA];
+  ln.load_gen<true, JR, JA>((const cx<double>*)g.At, N, nu, gr, gi);
   const double* Xb = reinterpret_cast<const double*>((const cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm);
   double* Lb = reinterpret_cast<double*>((cx<double>*)g.L + (size_t)b * (Nt + 1) * Nm);
   const double* srcb =
@@ -676,7 +707,7 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
   const unsigned char* pmask = g.mu_mode ? nullptr : g.pmask;
   const double tmu = 2.0 * g.mu;
   double* const sink = tchain_sink(g);
-  const size_t o = (size_t)ln.colD * N + max(ln.rowE, 0), oe = 2 * o + (ln.n & 1);
+  const size_t o = (size_t)ln.colD * N + max(ln.rowE, 0), oe = 2 * o + ln.pe;
   const bool pm = ln.act && pmask && pmask[o];
   const bool srcl = ln.act && srcb;
   double acc = 0.0;
@@ -690,7 +721,7 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
       const cx<double> cf = g.coef[(size_t)b * 2 * m + ln.colD], t = ((const cx<double>*)g.Xt)[o];
       v = cx<double>{cf.r * t.r - cf.i * t.i, cf.r * t.i + cf.i * t.r};
     }
-    acc = (ln.n & 1) ? v.i : v.r;
+    acc = ln.pe ? v.i : v.r;
     if (pm) acc += tmu * Xb[(size_t)Nt * 2 * Nm + oe];
     if (srcl) acc += srcb[(size_t)Nt * 2 * Nm + oe];
   }
@@ -714,8 +745,8 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
       const size_t ok_ = (size_t)k * 2 * Nm + oe;
       double xa = pm ? tmu * Xb[ok_] : 0.0;  // 2μ x_k on the mask + the caller's dL/dx(x_k), after the slice
       if (srcl) xa += srcb[ok_];
-      double ar[JR], ai[JR], cd1 = 0.0, cd2 = 0.0;
-      blkrot_form<JR>(gr, gi, st.u, st.scale, ar, ai);
+      double ar[JA], ai[JA], cd1 = 0.0, cd2 = 0.0;
+      blkrot_form<JA>(gr, gi, st.u, st.scale, ar, ai);
       blkrot_slice<JR, CHEB>(ar, ai, acc, ln.act, sg, st.P, st.s, st.pr, -st.pi, S.cof + 64 * j, invt, cd1, cd2);
       acc += xa;
       *(ln.act ? Lb + ok_ : sink) = acc;

@@ -158,6 +158,7 @@ struct qoc_ctx {
   int nblk = 0;                  // blocks
   int* d_brow = nullptr;         // nblk x blk_nb rows of each block (-1 padding)
   int blk_jr = 0;                // chain kernels: 0 VALU lanes (k_blk_*), 1 / 4 MFMA block waves (k_blkrot_*<JR>)
+  bool blk_real = false;         // MFMA block waves on the real embedding of blocks of <= 2 rows (k_blkrot_*<0>)
   int nwb = 0;                   // MFMA block waves per column pair
   int* d_wrow = nullptr;         // nwb x 16 rows of each wave's state (-1 padding)
   // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts

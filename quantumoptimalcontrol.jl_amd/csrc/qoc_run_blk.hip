@@ -16,10 +16,15 @@ int blk_detect(qoc_ctx* c) {
   c->blk_nb = 0;
   c->nblk = 0;
   c->blk_jr = 0;
+  c->blk_real = false;
   c->nwb = 0;
   const char* env = getenv("QOC_BLOCKS");
   if (env && !std::strcmp(env, "0")) return QOC_OK;
   const bool valu = env && !std::strcmp(env, "valu");  // blocks of <= 4 rows on the VALU lanes (k_blk_*)
+  // blocks of <= 2 rows on their real embedding (JR = 0, QOC_BLOCKS=real): one MFMA per term and no DPP swap, but
+  // 4 columns per wave and 5 waves per cavity seed instead of 3; measured the same as the complex slots (cavity
+  // chain 0.79 vs 0.78 ms), so the complex slots stay the default
+  const bool real_req = env && !std::strcmp(env, "real");
   const int N = c->N;
   const size_t NN = (size_t)N * N;
   std::vector<int> par(N);
@@ -62,9 +67,28 @@ int blk_detect(qoc_ctx* c) {
   // the MFMA waves' 16-row states
   std::vector<int> wrow;
   int jr = 0;
+  bool real = false;
   if (NB == 16) {
     jr = 4;
     wrow = brow;
+  } else if (real_req && mx <= 2) {
+    // real embedding: a block of <= 2 complex rows is one 4-row slot [Re r0, Re r1, Im r0, Im r1] (two 1-row blocks
+    // share a slot); entries row * 2 + part, so that each element's partner part sits 32 lanes away
+    real = true;
+    std::vector<int> rows;  // complex rows in slot order, 2 per slot (-1 padding)
+    for (const auto& bl : blocks) {
+      if (bl.size() == 2 && rows.size() % 2) rows.push_back(-1);  // a 2-row block starts a slot
+      for (int r : bl) rows.push_back(r);
+    }
+    if (rows.size() % 2) rows.push_back(-1);
+    for (size_t q = 0; q < rows.size(); q += 2) {
+      const int r0 = rows[q], r1 = rows[q + 1];
+      wrow.push_back(r0 >= 0 ? 2 * r0 : -1);
+      wrow.push_back(r1 >= 0 ? 2 * r1 : -1);
+      wrow.push_back(r0 >= 0 ? 2 * r0 + 1 : -1);
+      wrow.push_back(r1 >= 0 ? 2 * r1 + 1 : -1);
+    }
+    while (wrow.size() % 16) wrow.push_back(-1);
   } else if (!valu) {
     jr = 1;
     std::vector<int> slot;  // rows of the 4-row slots, in order (a block never straddles two slots)
@@ -88,13 +112,14 @@ int blk_detect(qoc_ctx* c) {
     }
   HIPCHK(c, hipMalloc((void**)&c->d_brow, brow.size() * sizeof(int)));
   HIPCHK(c, hipMemcpy(c->d_brow, brow.data(), brow.size() * sizeof(int), hipMemcpyHostToDevice));
-  if (jr) {
+  if (jr || real) {
     HIPCHK(c, hipMalloc((void**)&c->d_wrow, wrow.size() * sizeof(int)));
     HIPCHK(c, hipMemcpy(c->d_wrow, wrow.data(), wrow.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   c->blk_nb = NB;
   c->nblk = nblk;
   c->blk_jr = jr;
+  c->blk_real = real;
   c->nwb = (int)(wrow.size() / 16);
   return QOC_OK;
 }
@@ -105,11 +130,12 @@ bool blk_active(const qoc_ctx* c) {
       c->packed || c->nu > 2)
     return false;
   // MFMA block waves: <= 8 per workgroup (the 512-thread launch bound keeps 256 VGPRs per wave)
+  if (c->blk_real) return c->nwb * ((c->m + 3) / 4) <= 8;
   if (c->blk_jr) return c->nwb * ((c->m + 1) / 2) <= 8 && (c->blk_nb < 16 || tchain_mf(c));
   return c->nblk * c->m <= BLK_MAXT && c->nblk <= 256;
 }
 // MFMA block waves (k_blkrot_*): the chain kernels; blocks of 16 rows also take the dense gradient kernels
-bool blk_rot(const qoc_ctx* c) { return c->blk_jr > 0; }
+bool blk_rot(const qoc_ctx* c) { return c->blk_jr > 0 || c->blk_real; }
 static bool blk_big(const qoc_ctx* c) { return c->blk_nb == 16; }
 
 static BlkArgs blk_args(const qoc_ctx* c) {
@@ -123,6 +149,7 @@ static BlkArgs blk_args(const qoc_ctx* c) {
 }
 
 static int blk_threads(const qoc_ctx* c) {
+  if (c->blk_real) return 64 * c->nwb * ((c->m + 3) / 4);  // 4 state columns per real-embedded wave
   return blk_rot(c) ? 64 * c->nwb * ((c->m + 1) / 2) : 64 * ((c->nblk * c->m + 63) / 64);
 }
 static size_t blk_lds_of(const qoc_ctx* c) {
@@ -140,6 +167,7 @@ template <typename F>
 static hipError_t blk_dispatch(const qoc_ctx* c, F&& f) {
   using std::integral_constant;
   auto ch = [&](auto K_) { return c->cheb_ran ? f(K_, std::true_type()) : f(K_, std::false_type()); };
+  if (c->blk_real) return ch(integral_constant<int, 0>());
   if (c->blk_jr == 1) return ch(integral_constant<int, 1>());
   if (c->blk_jr == 4) return ch(integral_constant<int, 4>());
   switch (c->blk_nb) {

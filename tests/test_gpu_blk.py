@@ -54,9 +54,10 @@ BLK = ("blocks", "blocks_mfma")
 
 
 def _engine(prob, B, blocks, monkeypatch, penalty=None, chain="taylor"):
-    """blocks: True (default kernels: MFMA block waves), "valu" (blocks of <= 4 rows on VALU lanes), False (dense)."""
+    """blocks: True (default kernels: MFMA block waves, complex slots), "real" (blocks of <= 2 rows on their real
+    embedding), "valu" (blocks of <= 4 rows on VALU lanes), False (dense)."""
     from qoc_amd import GrapeEngine
-    monkeypatch.setenv("QOC_BLOCKS", "valu" if blocks == "valu" else "1" if blocks else "0")
+    monkeypatch.setenv("QOC_BLOCKS", blocks if blocks in ("valu", "real") else "1" if blocks else "0")
     e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
     e.set_cost_trace(prob.x_target, prob.n)
     e.set_chain(chain)
@@ -87,16 +88,16 @@ def _assert_seed(J, g, Jr, gr, tag):
 
 @pytest.mark.parametrize("name", ["zz", "cavity20", "cavity40"])
 @pytest.mark.parametrize("device", [False, True])
-@pytest.mark.parametrize("kind", ["mfma", "valu"])
+@pytest.mark.parametrize("kind", ["mfma", "real", "valu"])
 def test_blocks_match_oracle_and_dense_chains(built_lib, monkeypatch, name, device, kind):
     """Blocks of <= 4 rows: packed into the 4-row slots of MFMA block waves (default) or one VALU lane per (block,
     column) (QOC_BLOCKS=valu); the block gradient either way."""
     prob, u = _cases()[name]
     B = u.shape[0]
-    e = _engine(prob, B, True if kind == "mfma" else "valu", monkeypatch)
+    e = _engine(prob, B, True if kind == "mfma" else kind, monkeypatch)
     J, g = _eval(e, u, device)
     info = e.info()
-    assert info["chain_kernel"] == ("blocks_mfma" if kind == "mfma" else "blocks"), info
+    assert info["chain_kernel"] == ("blocks" if kind == "valu" else "blocks_mfma"), info
     assert info["backward"] == ("blocks" if device else "generic"), info
     xs = [e.state(k, seed=0) for k in (1, prob.Nt // 2, prob.Nt)]
     lams = [e.costate(k, seed=0) for k in (0, prob.Nt // 2, prob.Nt)]
@@ -168,18 +169,18 @@ def test_blocks_penalty_and_costate_source(built_lib, monkeypatch, poly):
         assert np.linalg.norm(g[b] - gr) / np.linalg.norm(gr) <= 1e-10
 
 
-@pytest.mark.parametrize("NB,nu,m", [(4, 2, 3), (4, 1, 1), (3, 2, 2), (2, 1, 5)])
+@pytest.mark.parametrize("NB,nu,m", [(4, 2, 3), (4, 1, 1), (3, 2, 2), (2, 1, 5), (2, 2, 8)])
 @pytest.mark.parametrize("poly", ["taylor", "chebyshev"])
-@pytest.mark.parametrize("kind", ["mfma", "valu"])
+@pytest.mark.parametrize("kind", ["mfma", "real", "valu"])
 def test_blocks_random_permuted_blocks(built_lib, monkeypatch, NB, nu, m, poly, kind):
     """Random block-diagonal skew-Hermitian generators hidden by a permutation (the detection works on the pattern,
     not on contiguous rows), a short last block (padding lanes), one or two controls, odd column counts."""
     monkeypatch.setenv("QOC_TCHAIN_POLY", poly)
     prob, u = _block_problem(NB=NB, nblk=5, nu=nu, m=m, seed=NB * 10 + nu + m)
     for device in (False, True):
-        e = _engine(prob, 2, True if kind == "mfma" else "valu", monkeypatch)
+        e = _engine(prob, 2, True if kind == "mfma" else kind, monkeypatch)
         J, g = _eval(e, u, device)
-        assert e.info()["chain_kernel"] == ("blocks_mfma" if kind == "mfma" else "blocks")
+        assert e.info()["chain_kernel"] == ("blocks" if kind == "valu" else "blocks_mfma")
         e.close()
         for b in range(2):
             J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
