@@ -392,7 +392,8 @@ def main():
             traffic_all = {}
     taylor = info1.get("chain") == "taylor" and not large
     dual = info1.get("concurrent_launch") == "dual"
-    bsz = block_sizes(prob) if taylor and info1.get("chain_kernel") in ("blocks", "blocks_mfma") else None
+    bsz = block_sizes(prob) if taylor and info1.get("chain_kernel") in ("blocks", "blocks_mfma", "blocks_prop") else None
+    bprop = info1.get("chain_kernel") == "blocks_prop"
     # blocks of <= 4 rows (VALU lanes or packed MFMA block waves) with the block gradient; 5..16 rows: MFMA block
     # waves with the dense gradient
     blocks = bsz is not None and bsz.max() <= 4
@@ -407,6 +408,8 @@ def main():
         tl = terms / K * dirs
         p_avg = terms / K / max(B * Nt, 1)
         rec = B * Nt * (32 + 8 * (p_avg + 1) + 8 * nu)
+        if bprop:  # block propagators: each direction reads u_k and forms its step records in the kernel
+            rec = B * Nt * 8 * nu
         st = B * (Nt + 1) * N * m * esz
         models = {
             "k_expm": ("hbm", (B * Nt * (8 * nu + 32 + 8 * (p_avg + 1))) / 1e9, "GB/s", PEAK_HBM_GBS),
@@ -476,9 +479,9 @@ def main():
                    "unit": unit, "peak": pk, "frac": ach / pk}
     names = {"k_expm": "k_expm_rr", "k_chain_fwd": "k_chain_fwd", "k_chain_bwd": "k_chain_bwd", "k_grad": "k_grad_rr"}
     if blocks:
-        kb = "k_blkrot" if info1.get("chain_kernel") == "blocks_mfma" else "k_blk"
+        kb = {"blocks_mfma": "k_blkrot", "blocks_prop": "k_blku"}.get(info1.get("chain_kernel"), "k_blk")
         names = {"k_expm": "k_tchain_prep", "k_chain_fwd": kb + ("_dual" if dual else "_fwd"),
-                 "k_chain_bwd": kb + "_bwd", "k_grad": "k_blk_grad"}
+                 "k_chain_bwd": kb + "_bwd", "k_grad": "k_blku_grad" if bprop else "k_blk_grad"}
         for k in ("k_chain_fwd", "k_chain_bwd", "k_grad"):
             kern[k]["kernel"] = names[k]
             t = per_step[k] / 1e3

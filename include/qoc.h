@@ -133,16 +133,18 @@ int qoc_get_propagator(qoc_ctx* ctx, int seed, int k, double* U_out);   /* Uk_ve
 int qoc_pade_histogram(qoc_ctx* ctx, long long* hist, int reset);
 
 /* Exponential algorithm actually executed (no linear solve; same result as the reference's Padé to
- * fp rounding; QOC_EXPM_PADE=1 at qoc_create selects the Padé + solve algorithm).  8*64 entries:
+ * fp rounding; QOC_EXPM_PADE=1 at qoc_create selects the Padé + solve algorithm).  QOC_TAYLOR_HIST_ENTRIES = 9*64 entries:
  *   hist[(r-2)*64 + s], r = 2..8: degree m = 3r+2 Taylor by Paterson-Stockmeyer (2 + r GEMMs) with s
  *     squarings (large-N pipeline; LDS kernel with QOC_EXPM_LDS=1);
  *   hist[7*64 + s]: degree-12 Taylor in 4 GEMMs (Bader-Blanes-Casas form) with s squarings (the
  *     default register-resident kernel);
  *   hist[8*64 + s]: degree-8 Taylor in 3 GEMMs (Bader-Blanes-Casas form) with s squarings (large-N pipeline).
- * hist holds 9*64 entries.
  * The truncation tail is <= 2^-53 in every case.  qoc_pade_histogram keeps reporting the Padé (d, s)
- * the reference would select. */
-int qoc_taylor_histogram(qoc_ctx* ctx, long long* hist /*[9*64]*/, int reset);
+ * the reference would select.  qoc_taylor_histogram_n takes the capacity of hist and fails (QOC_ERR_ARG) when it
+ * is below QOC_TAYLOR_HIST_ENTRIES; qoc_taylor_histogram (no capacity) writes QOC_TAYLOR_HIST_ENTRIES entries. */
+#define QOC_TAYLOR_HIST_ENTRIES (9 * 64)
+int qoc_taylor_histogram(qoc_ctx* ctx, long long* hist /*[QOC_TAYLOR_HIST_ENTRIES]*/, int reset);
+int qoc_taylor_histogram_n(qoc_ctx* ctx, long long* hist, int n, int reset);
 
 /* Live per-kernel timing: when enabled, hipEvents are recorded on qoc_stream around each hot-path
  * kernel (phase 0 k_expm, 1 k_chain_fwd, 2 k_chain_bwd, 3 k_grad).  qoc_phase_times synchronises the
@@ -186,10 +188,15 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
  * info[9] = 1 when the last forward chain wrote its captured products, info[10] = the Taylor-action chain kernels
  * (0 none / the fp32 VALU ones, 1 MFMA with the state in LDS, 2 MFMA with the state in registers: N <= 32, nu <= 2,
  * QOC_TCHAIN_ROT=0 keeps 1; 3 block chains: the generators split into invariant blocks of <= 4 rows, one VALU lane
- * per (block, column); 4 block chains with one MFMA wave per (block of 5..16 rows, column pair); QOC_BLOCKS=0 at
- * qoc_set_generators keeps the dense kernels).  QOC_FORCE_LARGE_N=1 in the environment at qoc_create selects the large-N path for
- * any size (testing). */
-int qoc_get_info(qoc_ctx* ctx, long long* info /*[11]*/);
+ * per (block, column); 4 block chains with one MFMA wave per (block of 5..16 rows, column pair), or blocks of <= 4 rows
+ * packed into MFMA slots (QOC_BLKU=0); 5 block propagators: blocks of <= 4 rows, U_k formed per (slice, block) apart
+ * from the serial chain, one block matvec per slice (the default for blocks of <= 4 rows); QOC_BLOCKS=0 at
+ * qoc_set_generators keeps the dense kernels).  QOC_FORCE_LARGE_N=1 in the environment at qoc_create selects the
+ * large-N path for any size (testing).  qoc_get_info_n takes the capacity of info and fails (QOC_ERR_ARG) when it is
+ * below QOC_INFO_ENTRIES; qoc_get_info (no capacity) writes QOC_INFO_ENTRIES entries. */
+#define QOC_INFO_ENTRIES 11
+int qoc_get_info(qoc_ctx* ctx, long long* info /*[QOC_INFO_ENTRIES]*/);
+int qoc_get_info_n(qoc_ctx* ctx, long long* info, int n);
 
 /* How the chains x_{k+1} = U_k x_k (src/gradient_computations.jl:27-29) and λ_k = U_k^H λ_{k+1} (:52-58)
  * apply the slice exponentials:

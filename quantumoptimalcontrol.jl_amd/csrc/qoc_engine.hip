@@ -1098,6 +1098,9 @@ int qoc_set_spline_basis(qoc_ctx* c, const double* Bs, int ns) {
   HIPCHK(c, hipMalloc((void**)&c->d_cstage, (size_t)2 * c->B * ns * c->nu * sizeof(double)));
   HIPCHK(c, hipMemcpy(c->d_Bs, Bs, (size_t)c->Nt * ns * sizeof(double), hipMemcpyHostToDevice));
   c->ns = ns;
+  // states and co-states of a spline propagate belong to the old basis' u: qoc_sensitivity_spline must now see
+  // them as stale (QOC_ERR_STALE), even for the same coefficients
+  c->h_coef.clear();
   return QOC_OK;
 }
 
@@ -1244,6 +1247,12 @@ int qoc_propagate_envelope(qoc_ctx* c, int kind, const double* params, int np, d
   return QOC_OK;
 }
 
+int qoc_get_info_n(qoc_ctx* c, long long* info, int n) {
+  if (n < QOC_INFO_ENTRIES)
+    return fail(c, QOC_ERR_ARG, "info buffer holds %d entries, QOC_INFO_ENTRIES = %d", n, QOC_INFO_ENTRIES);
+  return qoc_get_info(c, info);
+}
+
 int qoc_get_info(qoc_ctx* c, long long* info) {
   if (!c || !info) return fail(c, QOC_ERR_ARG, "null argument");
   info[0] = c->big ? 1 : 0;
@@ -1256,7 +1265,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[7] = c->m;  // state columns the kernels run on (< the caller's m when compress_states packing is on)
   info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 / 3 concurrent μ recurrence
   info[9] = c->fwd_captured ? 1 : 0;
-  info[10] = blk_active(c) ? (blk_rot(c) ? 4 : 3) : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
+  info[10] = blk_active(c) ? (blku_on(c) ? 5 : blk_rot(c) ? 4 : 3) : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
   return QOC_OK;
 }
 
@@ -1378,6 +1387,13 @@ int qoc_chain_terms(qoc_ctx* c, long long* terms, int reset) {
   if (reset) HIPCHK(c, hipMemsetAsync(c->d_terms, 0, sizeof(long long), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return QOC_OK;
+}
+
+int qoc_taylor_histogram_n(qoc_ctx* c, long long* hist, int n, int reset) {
+  if (n < QOC_TAYLOR_HIST_ENTRIES)
+    return fail(c, QOC_ERR_ARG, "histogram buffer holds %d entries, QOC_TAYLOR_HIST_ENTRIES = %d", n,
+                QOC_TAYLOR_HIST_ENTRIES);
+  return qoc_taylor_histogram(c, hist, reset);
 }
 
 int qoc_taylor_histogram(qoc_ctx* c, long long* hist, int reset) {

@@ -161,6 +161,7 @@ struct qoc_ctx {
   bool blk_real = false;         // MFMA block waves on the real embedding of blocks of <= 2 rows (k_blkrot_*<0>)
   int nwb = 0;                   // MFMA block waves per column pair
   int* d_wrow = nullptr;         // nwb x 16 rows of each wave's state (-1 padding)
+  size_t blk_dev_bytes = 0;      // d_brow + d_wrow (counted in dev_bytes)
   // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
@@ -282,6 +283,7 @@ int tchain_prep(qoc_ctx* c);
 int blk_detect(qoc_ctx* c);
 bool blk_active(const qoc_ctx* c);
 bool blk_rot(const qoc_ctx* c);
+bool blku_on(const qoc_ctx* c);
 int blk_forward(qoc_ctx* c);
 int blk_backward(qoc_ctx* c, int order, double* d_dJdu);
 bool blk_concurrent_ok(const qoc_ctx* c, int order);

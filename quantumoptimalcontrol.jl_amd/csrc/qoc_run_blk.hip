@@ -4,9 +4,14 @@
 #include <numeric>
 
 #include "qoc_blk.hpp"
+#include "qoc_blku.hpp"
 #include "qoc_internal.hpp"
 
 namespace qoc_host {
+
+static int blku_forward(qoc_ctx* c);
+static int blku_backward(qoc_ctx* c, int order, double* d_dJdu);
+static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu);
 
 // Connected components of the union sparsity pattern of A_0..A_nu (host copy, c->h_gen): rows i and k share a block
 // whenever some A_j[i, k] or A_j[k, i] is nonzero.  Blocks of at most BLK_NBMAX rows turn the block path on
@@ -110,12 +115,17 @@ int blk_detect(qoc_ctx* c) {
       HIPCHK(c, hipFree(*p));
       *p = nullptr;
     }
+  c->dev_bytes -= c->blk_dev_bytes;  // the row lists of a previous qoc_set_generators
+  c->blk_dev_bytes = 0;
   HIPCHK(c, hipMalloc((void**)&c->d_brow, brow.size() * sizeof(int)));
   HIPCHK(c, hipMemcpy(c->d_brow, brow.data(), brow.size() * sizeof(int), hipMemcpyHostToDevice));
+  c->blk_dev_bytes += brow.size() * sizeof(int);
   if (jr || real) {
     HIPCHK(c, hipMalloc((void**)&c->d_wrow, wrow.size() * sizeof(int)));
     HIPCHK(c, hipMemcpy(c->d_wrow, wrow.data(), wrow.size() * sizeof(int), hipMemcpyHostToDevice));
+    c->blk_dev_bytes += wrow.size() * sizeof(int);
   }
+  c->dev_bytes += c->blk_dev_bytes;
   c->blk_nb = NB;
   c->nblk = nblk;
   c->blk_jr = jr;
@@ -137,6 +147,60 @@ bool blk_active(const qoc_ctx* c) {
 // MFMA block waves (k_blkrot_*): the chain kernels; blocks of 16 rows also take the dense gradient kernels
 bool blk_rot(const qoc_ctx* c) { return c->blk_jr > 0 || c->blk_real; }
 static bool blk_big(const qoc_ctx* c) { return c->blk_nb == 16; }
+
+// Block propagators (qoc_blku.hpp), the default for blocks of <= 4 rows: formed per (slice, block) apart from the
+// serial chain, which then runs one NB x NB matvec per slice.  QOC_BLKU=0 keeps the polynomial-in-the-chain kernels
+// (k_blkrot_* / k_blk_*).  The gradient packs 64 / nblk slices per wave (nblk <= 32); the chain lanes take
+// nblk m <= 256 (block, column) pairs.
+bool blku_on(const qoc_ctx* c) {
+  // QOC_BLOCKS=valu / real ask for those kernel variants explicitly (blk_jr != 1): they keep them
+  if (!blk_active(c) || c->blk_jr != 1 || c->blk_nb > BLK_NBMAX || c->nu < 1 || c->nu > 2 || c->nblk > 32 ||
+      c->nblk * c->m > 256)
+    return false;
+  const char* env = getenv("QOC_BLKU");
+  return !(env && !std::strcmp(env, "0"));
+}
+
+struct BlkuShape {
+  int C, CW, W;
+  size_t lds;
+};
+// Waves per workgroup: CW chain waves (one lane per (block, column)) and FW formation waves, sized so that forming
+// a chunk (C nblk propagators, ~190 / 450 / 2600 VALU operations each for NB = 2 / 3 / 4) takes about as long as the
+// chain waves' C matvecs (4 NB^2 FMAs + ~20 per slice); QOC_BLKU_FW overrides FW.  C: the most slices per chunk
+// (<= 64, <= the formation lanes, which compute one step record each) whose double-buffered propagators keep the
+// workgroup within 52 KB of LDS (three workgroups per CU).
+static BlkuShape blku_shape(const qoc_ctx* c) {
+  BlkuShape s{};
+  const int NB = c->blk_nb, E = NB * NB;
+  s.CW = (c->nblk * c->m + 63) / 64;
+  const double costU = NB == 2 ? 190.0 : NB == 3 ? 450.0 : 2600.0, costC = 4.0 * E + 20.0;
+  int fw = (int)std::ceil(c->nblk * costU / (64.0 * costC));
+  if (const char* env = getenv("QOC_BLKU_FW")) fw = atoi(env);
+  fw = std::max(1, std::min(fw, 8 - s.CW));
+  s.W = s.CW + fw;
+  s.C = std::min(64, 64 * fw);
+  while (s.C > 4 && blku_lds(c->N, c->m, NB, c->nblk, s.C) > 52 * 1024) s.C >>= 1;
+  if (const char* env = getenv("QOC_BLKU_C")) s.C = std::max(1, std::min(atoi(env), 64 * fw));
+  s.lds = blku_lds(c->N, c->m, NB, c->nblk, s.C);
+  return s;
+}
+
+static BlkuParams blku_params(const qoc_ctx* c, const BlkuShape& s) {
+  BlkuParams p{};
+  for (int j = 0; j < 3; ++j) {
+    const bool on = j <= c->nu;
+    // skew-Hermitian generators: spectral half-widths (the 2-norm bound of Ã_k); otherwise the shifted 1-norms
+    p.rad[j] = on ? (c->cheb_ok ? c->tprm.rad[j] : c->tprm.nrm[j]) : 0.0;
+    p.mur[j] = on ? c->tprm.mur[j] : 0.0;
+    p.mui[j] = on ? c->tprm.mui[j] : 0.0;
+  }
+  p.theta_cap = c->tprm.theta[17];
+  p.C = s.C;
+  p.CW = s.CW;
+  p.terms = c->d_terms;
+  return p;
+}
 
 static BlkArgs blk_args(const qoc_ctx* c) {
   BlkArgs bk{};
@@ -179,6 +243,7 @@ static hipError_t blk_dispatch(const qoc_ctx* c, F&& f) {
 }
 
 int blk_forward(qoc_ctx* c) {
+  if (blku_on(c)) return blku_forward(c);
   int r = tchain_prep(c);
   if (r) return r;
   const TChainArgs g = tchain_args(c);
@@ -209,6 +274,7 @@ static int blk_grad(qoc_ctx* c, int order, bool mu_mode, double* d_dJdu) {
   const BlkArgs bk = blk_args(c);
   const long long units = (long long)c->B * c->Nt;
   const int upw = 256 / c->nblk;
+  if (upw < 1) return fail(c, QOC_ERR_UNSUPPORTED, "block gradient: %d blocks exceed one workgroup", c->nblk);
   const unsigned blocks = (unsigned)((units + upw - 1) / upw);
   const int mk = mark_begin(c, 3);
   hipError_t e = hipSuccess;
@@ -233,6 +299,7 @@ static int blk_grad(qoc_ctx* c, int order, bool mu_mode, double* d_dJdu) {
 // grape_sensitivity: λ by the block backward chain (penalty, co-state source and an external λ_N included), then the
 // block gradient for orders 1..4; the exact (Fréchet) gradient runs its own dense kernel on the same λ.
 int blk_backward(qoc_ctx* c, int order, double* d_dJdu) {
+  if (blku_on(c)) return blku_backward(c, order, d_dJdu);
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
   const size_t lds = blk_lds_of(c);
@@ -264,6 +331,7 @@ bool blk_concurrent_ok(const qoc_ctx* c, int order) {
 }
 
 int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
+  if (blku_on(c)) return blku_eval_concurrent(c, order, d_dJdu);
   if (!c->d_coef_mu) {
     HIPCHK(c, hipMalloc((void**)&c->d_coef_mu, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
     c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
@@ -306,6 +374,117 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
   } else {
     r = blk_grad(c, order, true, d_dJdu);
   }
+  if (r) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_coef_mu, c->d_coef, (size_t)c->B * 2 * c->m * sizeof(cx<double>),
+                           hipMemcpyDeviceToDevice, c->stream));
+  c->L_is_mu = true;
+  c->last_eval_mode = 4;
+  return QOC_OK;
+}
+
+// ---- block propagators (qoc_blku.hpp) ----------------------------------------------------------------------------
+template <typename F>
+static hipError_t blku_dispatch(const qoc_ctx* c, F&& f) {
+  using std::integral_constant;
+  switch (c->blk_nb) {
+    case 2: return f(integral_constant<int, 2>());
+    case 3: return f(integral_constant<int, 3>());
+    case 4: return f(integral_constant<int, 4>());
+  }
+  return hipErrorInvalidValue;
+}
+
+static int blku_forward(qoc_ctx* c) {
+  const TChainArgs g = tchain_args(c);
+  const BlkArgs bk = blk_args(c);
+  const BlkuShape s = blku_shape(c);
+  const BlkuParams bp = blku_params(c, s);
+  const int mk = mark_begin(c, 1);
+  const hipError_t e = blku_dispatch(c, [&](auto NB_) {
+    constexpr int NB = decltype(NB_)::value;
+    const hipError_t q = blk_lds_attr(k_blku_fwd<NB>, s.lds);
+    if (q != hipSuccess) return q;
+    hipLaunchKernelGGL((k_blku_fwd<NB>), dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, bp);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_fwd launch: %s", hipGetErrorString(e));
+  c->fwd_captured = false;
+  c->props_since_reset++;
+  return QOC_OK;
+}
+
+// the order-o gradient from d_X and d_L (mu_mode: d_L holds μ, λ = coef ⊙ μ with the coefficients in d_coef)
+static int blku_grad(qoc_ctx* c, int order, bool mu_mode, double* d_dJdu) {
+  const TChainArgs g = tchain_args(c);
+  const BlkArgs bk = blk_args(c);
+  const long long units = (long long)c->B * c->Nt;
+  const int upw = 64 / c->nblk;
+  if (upw < 1) return fail(c, QOC_ERR_UNSUPPORTED, "block gradient: %d blocks exceed one wave", c->nblk);
+  const long long waves = (units + upw - 1) / upw;
+  const unsigned blocks = (unsigned)std::max<long long>(1, std::min<long long>((waves + 3) / 4, (long long)c->ncu * 8));
+  const size_t glds = blku_grad_lds(c->blk_nb, c->nblk);
+  const int mk = mark_begin(c, 3);
+  const hipError_t e = blku_dispatch(c, [&](auto NB_) {
+    constexpr int NB = decltype(NB_)::value;
+    switch (order) {
+      case 1: hipLaunchKernelGGL((k_blku_grad<NB, 1>), dim3(blocks), dim3(256), glds, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
+      case 2: hipLaunchKernelGGL((k_blku_grad<NB, 2>), dim3(blocks), dim3(256), glds, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
+      case 3: hipLaunchKernelGGL((k_blku_grad<NB, 3>), dim3(blocks), dim3(256), glds, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
+      default: hipLaunchKernelGGL((k_blku_grad<NB, 4>), dim3(blocks), dim3(256), glds, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
+    }
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_grad launch: %s", hipGetErrorString(e));
+  return QOC_OK;
+}
+
+// grape_sensitivity: λ by the block-propagator backward chain (penalty, co-state source and an external λ_N
+// included), then the block gradient for orders 1..4; the exact (Fréchet) gradient runs its dense kernel on λ.
+static int blku_backward(qoc_ctx* c, int order, double* d_dJdu) {
+  const TChainArgs g = tchain_args(c);
+  const BlkArgs bk = blk_args(c);
+  const BlkuShape s = blku_shape(c);
+  BlkuParams bp = blku_params(c, s);
+  bp.terms = nullptr;
+  const int mk = mark_begin(c, 2);
+  const hipError_t e = blku_dispatch(c, [&](auto NB_) {
+    constexpr int NB = decltype(NB_)::value;
+    const hipError_t q = blk_lds_attr(k_blku_bwd<NB>, s.lds);
+    if (q != hipSuccess) return q;
+    hipLaunchKernelGGL((k_blku_bwd<NB>), dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, bp);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_bwd launch: %s", hipGetErrorString(e));
+  if (order == QOC_DUKDP_EXACT) return dense_gradient<double>(c, order, d_dJdu);
+  return blku_grad(c, order, false, d_dJdu);
+}
+
+// qoc_eval_dev: the forward chain and the μ recurrence in one launch of 2B workgroups, then the gradient
+static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
+  if (!c->d_coef_mu) {
+    HIPCHK(c, hipMalloc((void**)&c->d_coef_mu, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
+    c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
+  }
+  const TChainArgs g = tchain_args(c);
+  const BlkArgs bk = blk_args(c);
+  const BlkuShape s = blku_shape(c);
+  const BlkuParams bp = blku_params(c, s);
+  const int mk = mark_begin(c, 1);
+  const hipError_t e = blku_dispatch(c, [&](auto NB_) {
+    constexpr int NB = decltype(NB_)::value;
+    const hipError_t q = blk_lds_attr(k_blku_dual<NB>, s.lds);
+    if (q != hipSuccess) return q;
+    hipLaunchKernelGGL((k_blku_dual<NB>), dim3(2 * c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, bp);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_dual launch: %s", hipGetErrorString(e));
+  c->fwd_captured = false;
+  c->props_since_reset++;
+  const int r = blku_grad(c, order, true, d_dJdu);
   if (r) return r;
   HIPCHK(c, hipMemcpyAsync(c->d_coef_mu, c->d_coef, (size_t)c->B * 2 * c->m * sizeof(cx<double>),
                            hipMemcpyDeviceToDevice, c->stream));

@@ -58,9 +58,11 @@ SIGNATURES = {
     "qoc_phase_times": (C.c_int, [_vp, _dp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_pade_histogram": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_taylor_histogram": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
+    "qoc_taylor_histogram_n": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int, C.c_int]),
     "qoc_set_propagation": (C.c_int, [_vp, C.c_int, C.c_int]),
     "qoc_propagate_envelope": (C.c_int, [_vp, C.c_int, _dp, C.c_int, C.c_double, C.c_double, _dp, _dp]),
     "qoc_get_info": (C.c_int, [_vp, C.POINTER(C.c_longlong)]),
+    "qoc_get_info_n": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_set_chain": (C.c_int, [_vp, C.c_int]),
     "qoc_comm_unique_id": (C.c_int, [_vp]),
     "qoc_comm_init": (C.c_int, [_vp, C.c_int, C.c_int, _vp, C.c_longlong]),

@@ -311,7 +311,7 @@ class GrapeEngine:
     def info(self) -> dict:
         """Which pipeline the context runs (qoc_get_info): 'lds' kernels or the 'large_n' GEMM path."""
         v = np.zeros(11, dtype=np.int64)
-        self._chk(self._lib.qoc_get_info(self._h, v.ctypes.data_as(C.POINTER(C.c_longlong))))
+        self._chk(self._lib.qoc_get_info_n(self._h, v.ctypes.data_as(C.POINTER(C.c_longlong)), v.size))
         return {"path": "large_n" if v[0] else "lds", "chunk": int(v[1]), "ns_iters": int(v[2]),
                 "device_bytes": int(v[3]), "chain": "taylor" if v[4] == 1 else "propagators",
                 "expm": {0: "pade", 1: "taylor_rr", 2: "ps_lds"}.get(int(v[5]), "?"),
@@ -319,7 +319,7 @@ class GrapeEngine:
                 "backward": {0: "generic", 1: "captured", 2: "concurrent", 3: "concurrent", 4: "blocks"}.get(int(v[8]), "?"),
                 "concurrent_launch": {2: "two_streams", 3: "dual", 4: "dual"}.get(int(v[8])),
                 "fwd_captured": bool(v[9]),
-                "chain_kernel": {0: None, 1: "mfma_lds", 2: "mfma_regs", 3: "blocks", 4: "blocks_mfma"}.get(int(v[10]))}
+                "chain_kernel": {0: None, 1: "mfma_lds", 2: "mfma_regs", 3: "blocks", 4: "blocks_mfma", 5: "blocks_prop"}.get(int(v[10]))}
 
     def set_chain(self, mode: str = "auto"):
         """How the chains apply exp(A_k) (include/qoc.h qoc_set_chain): 'propagators' forms every U_k (the
@@ -370,7 +370,8 @@ class GrapeEngine:
         m = 12 by the 4-GEMM scheme, m = "8t" by the 3-GEMM degree-8 scheme (large-N path), with s squarings
         (include/qoc.h: qoc_taylor_histogram)."""
         h = np.zeros(9 * 64, dtype=np.int64)
-        self._chk(self._lib.qoc_taylor_histogram(self._h, h.ctypes.data_as(C.POINTER(C.c_longlong)), int(reset)))
+        self._chk(self._lib.qoc_taylor_histogram_n(self._h, h.ctypes.data_as(C.POINTER(C.c_longlong)), h.size,
+                                                   int(reset)))
         # row 8: the 3-product degree-8 scheme (large-N path), reported as m = "8t" to keep it apart from
         # Paterson-Stockmeyer's degree 8 (row 0, 4 GEMMs)
         return {("8t" if i // 64 == 8 else 12 if i // 64 == 7 else 3 * (i // 64 + 2) + 2, i % 64): int(v)

@@ -44,7 +44,11 @@ def init_engine_comm(engine, seed_offset: int) -> str:
     """Join the engine's RCCL communicator over the default process group: rank 0 makes the unique id and
     torch.distributed broadcasts it (a one-rank communicator at world 1, through the same ncclAllGather path).
     Returns the transport of the epilogue: "rccl-libqoc" when every rank joined a communicator of `world`
-    ranks, else "torch.distributed" (world > 1, RCCL missing) or "local" (world 1 without RCCL)."""
+    ranks, else "torch.distributed" (world > 1, RCCL missing on some rank) or "local" (world 1 without RCCL).
+
+    ncclCommInitRank is collective: a rank that fails inside it leaves the others blocked there.  So the ranks
+    first agree that every one of them can load RCCL (each makes a unique id of its own, which needs only the
+    library), and only then join; a failure of the join itself is an error on every rank, not a fallback."""
     import torch.distributed as dist
 
     from . import _lib
@@ -52,21 +56,11 @@ def init_engine_comm(engine, seed_offset: int) -> str:
 
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
-    box = [None]
-    if rank == 0:
-        try:
-            box[0] = comm_unique_id()
-        except _lib.QOCError:
-            box[0] = b""
-    if world > 1:
-        dist.broadcast_object_list(box, src=0)
-    ok = bool(box[0])
-    if ok:
-        try:
-            engine.comm_init(world, rank, box[0], seed_offset)
-        except _lib.QOCError:
-            ok = False
-    ok = ok and engine.comm_ranks() == world
+    try:
+        own_id = comm_unique_id()
+    except _lib.QOCError:
+        own_id = b""
+    ok = bool(own_id)
     if world > 1:  # every rank must take the same transport
         import torch
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
@@ -74,11 +68,13 @@ def init_engine_comm(engine, seed_offset: int) -> str:
             flag = flag.cuda()
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         ok = bool(flag.item())
-        if not ok:
-            engine.comm_init(1, 0, None, seed_offset)  # drop any communicator; gather over torch.distributed
-            return "torch.distributed"
-        return "rccl-libqoc"
     if not ok:
-        engine.comm_init(1, 0, None, seed_offset)
-        return "local"
+        engine.comm_init(1, 0, None, seed_offset)  # no communicator: the epilogue covers this engine alone
+        return "torch.distributed" if world > 1 else "local"
+    box = [own_id if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(box, src=0)
+    engine.comm_init(world, rank, box[0], seed_offset)  # collective; raises on failure
+    if engine.comm_ranks() != world:
+        raise _lib.QOCError(_lib.QOC_ERR_STATE, f"RCCL communicator has {engine.comm_ranks()} ranks, expected {world}")
     return "rccl-libqoc"

@@ -50,14 +50,19 @@ def _block_problem(NB=4, nblk=5, nu=2, m=3, Nt=30, seed=0):
     return prob, u
 
 
-BLK = ("blocks", "blocks_mfma")
+BLK = ("blocks", "blocks_mfma", "blocks_prop")
+# chain kernel of each block variant: block propagators formed apart from the chain (qoc_blku.hpp, the default for
+# blocks of <= 4 rows), the polynomial inside the recurrence on MFMA block waves (QOC_BLKU=0), on the real embedding
+# (QOC_BLOCKS=real), on VALU lanes (QOC_BLOCKS=valu)
+KIND_KERNEL = {"prop": "blocks_prop", "mfma": "blocks_mfma", "real": "blocks_mfma", "valu": "blocks"}
 
 
 def _engine(prob, B, blocks, monkeypatch, penalty=None, chain="taylor"):
-    """blocks: True (default kernels: MFMA block waves, complex slots), "real" (blocks of <= 2 rows on their real
-    embedding), "valu" (blocks of <= 4 rows on VALU lanes), False (dense)."""
+    """blocks: True / "prop" (default kernels), "mfma" (MFMA block waves, complex slots), "real" (blocks of <= 2 rows
+    on their real embedding), "valu" (blocks of <= 4 rows on VALU lanes), False (dense)."""
     from qoc_amd import GrapeEngine
     monkeypatch.setenv("QOC_BLOCKS", blocks if blocks in ("valu", "real") else "1" if blocks else "0")
+    monkeypatch.setenv("QOC_BLKU", "0" if blocks == "mfma" else "1")
     e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
     e.set_cost_trace(prob.x_target, prob.n)
     e.set_chain(chain)
@@ -88,16 +93,17 @@ def _assert_seed(J, g, Jr, gr, tag):
 
 @pytest.mark.parametrize("name", ["zz", "cavity20", "cavity40"])
 @pytest.mark.parametrize("device", [False, True])
-@pytest.mark.parametrize("kind", ["mfma", "real", "valu"])
+@pytest.mark.parametrize("kind", ["prop", "mfma", "real", "valu"])
 def test_blocks_match_oracle_and_dense_chains(built_lib, monkeypatch, name, device, kind):
-    """Blocks of <= 4 rows: packed into the 4-row slots of MFMA block waves (default) or one VALU lane per (block,
-    column) (QOC_BLOCKS=valu); the block gradient either way."""
+    """Blocks of <= 4 rows: block propagators formed apart from the chain (default), or the polynomial inside the
+    recurrence: packed into the 4-row slots of MFMA block waves, or one VALU lane per (block, column)
+    (QOC_BLOCKS=valu); the block gradient either way."""
     prob, u = _cases()[name]
     B = u.shape[0]
-    e = _engine(prob, B, True if kind == "mfma" else kind, monkeypatch)
+    e = _engine(prob, B, kind, monkeypatch)
     J, g = _eval(e, u, device)
     info = e.info()
-    assert info["chain_kernel"] == ("blocks" if kind == "valu" else "blocks_mfma"), info
+    assert info["chain_kernel"] == KIND_KERNEL[kind], info
     assert info["backward"] == ("blocks" if device else "generic"), info
     xs = [e.state(k, seed=0) for k in (1, prob.Nt // 2, prob.Nt)]
     lams = [e.costate(k, seed=0) for k in (0, prob.Nt // 2, prob.Nt)]
@@ -121,15 +127,16 @@ def test_blocks_match_oracle_and_dense_chains(built_lib, monkeypatch, name, devi
 
 @pytest.mark.parametrize("order", [1, 2, 3, 4, "exact"])
 @pytest.mark.parametrize("device", [False, True])
-def test_blocks_gradient_orders(built_lib, monkeypatch, order, device):
+@pytest.mark.parametrize("kind", ["prop", "mfma"])
+def test_blocks_gradient_orders(built_lib, monkeypatch, order, device, kind):
     """expm_jacobian! orders 1..4 (src/gradient_computations.jl:177-213) in the block gradient; the exact Fréchet
     gradient (opt-in) runs its dense kernel on the block chains' states and co-states."""
     from qoc_amd import systems
     prob = systems.zz_problem(50, tgate=5.0)
     u = systems.zz_controls(2, 50, 5.0, seed=64)
-    e = _engine(prob, 2, True, monkeypatch)
+    e = _engine(prob, 2, kind, monkeypatch)
     J, g = _eval(e, u, device and order != "exact", order)
-    assert e.info()["chain_kernel"] in BLK
+    assert e.info()["chain_kernel"] == KIND_KERNEL[kind]
     e.close()
     for b in range(2):
         J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=order)
@@ -137,7 +144,8 @@ def test_blocks_gradient_orders(built_lib, monkeypatch, order, device):
 
 
 @pytest.mark.parametrize("poly", ["taylor", "chebyshev"])
-def test_blocks_penalty_and_costate_source(built_lib, monkeypatch, poly):
+@pytest.mark.parametrize("kind", ["prop", "mfma"])
+def test_blocks_penalty_and_costate_source(built_lib, monkeypatch, poly, kind):
     """The state penalty (src/penalty_fcns.jl:1-11: L in the forward, 2 mu x_k added to λ_k in the backward) and a
     caller's dL/dx closure (qoc_set_costate_source) on the block chains, Taylor and Chebyshev terms."""
     from qoc_amd import systems
@@ -146,18 +154,18 @@ def test_blocks_penalty_and_costate_source(built_lib, monkeypatch, poly):
     u = systems.zz_controls(2, 40, 4.0, seed=65)
     qb = systems.QuantumBasis([3, 3])
     pen = (qb(["20", "21", "22"]), [0, 1, 2, 3], 0.37)
-    e = _engine(prob, 2, True, monkeypatch, penalty=pen)
+    e = _engine(prob, 2, kind, monkeypatch, penalty=pen)
     J = e.propagate(u)
     g = e.grape_sensitivity(u, 3)
     info = e.info()
-    assert info["chain_kernel"] in BLK and info["chain_poly"] == poly
+    assert info["chain_kernel"] == KIND_KERNEL[kind] and info["chain_poly"] == poly
     e.close()
     for b in range(2):
         Jr, gr, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3, penalty=pen)
         _assert_seed(J[b], g[b], Jr, gr, ("penalty", b))
     # the same penalty as a co-state source: dL/dx(x_k) from the oracle's states, the cost's L added by hand
     Lf, dLf = O.setup_state_penalty(*pen)
-    e = _engine(prob, 2, True, monkeypatch)
+    e = _engine(prob, 2, kind, monkeypatch)
     J = e.propagate(u)
     src = np.stack([np.stack([dLf(e.state(k, seed=b)) for k in range(prob.Nt + 1)]) for b in range(2)])
     e.set_costate_source(src)
@@ -171,16 +179,16 @@ def test_blocks_penalty_and_costate_source(built_lib, monkeypatch, poly):
 
 @pytest.mark.parametrize("NB,nu,m", [(4, 2, 3), (4, 1, 1), (3, 2, 2), (2, 1, 5), (2, 2, 8)])
 @pytest.mark.parametrize("poly", ["taylor", "chebyshev"])
-@pytest.mark.parametrize("kind", ["mfma", "real", "valu"])
+@pytest.mark.parametrize("kind", ["prop", "mfma", "real", "valu"])
 def test_blocks_random_permuted_blocks(built_lib, monkeypatch, NB, nu, m, poly, kind):
     """Random block-diagonal skew-Hermitian generators hidden by a permutation (the detection works on the pattern,
     not on contiguous rows), a short last block (padding lanes), one or two controls, odd column counts."""
     monkeypatch.setenv("QOC_TCHAIN_POLY", poly)
     prob, u = _block_problem(NB=NB, nblk=5, nu=nu, m=m, seed=NB * 10 + nu + m)
     for device in (False, True):
-        e = _engine(prob, 2, True if kind == "mfma" else kind, monkeypatch)
+        e = _engine(prob, 2, kind, monkeypatch)
         J, g = _eval(e, u, device)
-        assert e.info()["chain_kernel"] == ("blocks" if kind == "valu" else "blocks_mfma")
+        assert e.info()["chain_kernel"] == KIND_KERNEL[kind]
         e.close()
         for b in range(2):
             J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)

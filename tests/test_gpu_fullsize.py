@@ -41,6 +41,9 @@ def _check_config(name, seeds, chain=None, monkeypatch=None):
     if chain == "dense":  # the dense Taylor-action kernels (no block chains; qoc_blk.hpp)
         monkeypatch.setenv("QOC_BLOCKS", "0")
         chain = None
+    if chain == "blkpoly":  # the block chains with the polynomial inside the recurrence (QOC_BLKU=0)
+        monkeypatch.setenv("QOC_BLKU", "0")
+        chain = None
     mk_prob, mk_u, B = systems.CONFIGS[name]
     prob = mk_prob()
     u = mk_u(B, 0)
@@ -55,20 +58,27 @@ def _check_config(name, seeds, chain=None, monkeypatch=None):
     return info
 
 
-@pytest.mark.parametrize("chain", ["auto", "dense", "propagators"])
+# the chain kernels each variant must select: block propagators (qoc_blku.hpp, the default), the block chains with
+# the polynomial inside the recurrence (qoc_blk.hpp), the dense Taylor-action chains, the reference's propagators
+BLOCK_KERNEL = {"auto": "blocks_prop", "blkpoly": "blocks_mfma"}
+
+
+@pytest.mark.parametrize("chain", ["auto", "blkpoly", "dense", "propagators"])
 def test_zz_batch_full_size(built_lib, chain, monkeypatch):
     """config 2: zz_coupling N=9, m=4, Nt=500, B=512 (first and last seeds of the batch checked)."""
     seeds = list(range(CHECK_SEEDS // 2)) + list(range(512 - CHECK_SEEDS // 2, 512))
     info = _check_config("zz_batch", seeds, None if chain == "auto" else chain, monkeypatch)
-    assert (info["chain_kernel"] == "blocks_mfma") == (chain == "auto")
+    assert info["chain_kernel"] == BLOCK_KERNEL.get(chain, info["chain_kernel"]), info
+    assert (info["chain_kernel"] in BLOCK_KERNEL.values()) == (chain in BLOCK_KERNEL), info
 
 
-@pytest.mark.parametrize("chain", ["auto", "dense", "propagators"])
+@pytest.mark.parametrize("chain", ["auto", "blkpoly", "dense", "propagators"])
 def test_cavity_full_size(built_lib, chain, monkeypatch):
     """config 3: cavity(20) x qubit N=40, m=2, Nt=1000, B=256."""
     seeds = list(range(0, 256, 256 // CHECK_SEEDS))
     info = _check_config("cavity", seeds, None if chain == "auto" else chain, monkeypatch)
-    assert (info["chain_kernel"] == "blocks_mfma") == (chain == "auto")
+    assert info["chain_kernel"] == BLOCK_KERNEL.get(chain, info["chain_kernel"]), info
+    assert (info["chain_kernel"] in BLOCK_KERNEL.values()) == (chain in BLOCK_KERNEL), info
 
 
 @pytest.mark.parametrize("chain", ["auto", "dense", "propagators"])

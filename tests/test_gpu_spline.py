@@ -76,6 +76,12 @@ def test_f_alone_then_f_grad_like_the_reference_callbacks(built_lib):
         e.sensitivity_spline(c * 1.001)
     e.propagate_spline(c * 1.001)  # a line-search f: no sensitivity
     e.sensitivity_spline(c * 1.001)
+    # a new basis with the same number of splines: the states belong to the old basis' u, so the sensitivity for the
+    # same coefficients is stale too
+    e.propagate_spline(c)
+    e.set_spline_basis(Bs * 0.5)
+    with pytest.raises(StaleCacheError, match="Cache data from other control signal u"):
+        e.sensitivity_spline(c)
     e.close()
 
 
