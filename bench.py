@@ -30,6 +30,8 @@ GEMMS_PER_DEGREE = {3: 2, 5: 3, 7: 4, 9: 5, 13: 6}
 
 WORKLOADS = {
     "cavity": "cavity_qubit: cavity(20) x qubit(2) dim N=40, m=2, nu=2, Nt=1000, B=256 seeds/GPU, order-3 gradient",
+    "cavity_dense": ("cavity_qubit with the drive also displacing the cavity (Tc = b^dag x I + I x a^dag: no invariant "
+                     "blocks, dense chains): dim N=40, m=2, nu=2, Nt=1000, B=256 seeds/GPU, order-3 gradient"),
     "zz_batch": "zz_coupling: dim N=9, m=4, nu=2, Nt=500, B=512 seeds/GPU, order-3 gradient",
     "tunable_bus": "two_qubit_tunable_bus: dim N=27, m=1, nu=1, Nt=2000, B=512 seeds/GPU, order-3 gradient",
     "zz_plumbing": "zz_coupling Ipopt plumbing: dim N=9, m=4, nu=2, Nt=100, B=1, order-3 gradient",
@@ -374,20 +376,26 @@ def main():
     value = B * world * K / elapsed
 
     # ---- roofline of each kernel, dominant one reported ----
-    per_launch = {k: (ms / max(n, 1)) for k, (ms, n) in phases.items()}
+    per_launch = {k: (ms / n if n else 0.0) for k, (ms, n) in phases.items()}
     # launches per step: the overlapped backward runs the chain and the gradient in slice ranges (several
-    # launches per step); per-launch work = per-step work / launches per step
-    lps = {k: max(n, 1) / K for k, (ms, n) in phases.items()}
-    per_step = {k: per_launch[k] * lps[k] for k in per_launch}
+    # launches per step); per-launch work = per-step work / launches per step.  A kernel that never launched
+    # reports 0 launches and 0 ms
+    lps = {k: n / K for k, (ms, n) in phases.items()}
+    per_step = {k: ms / K for k, (ms, n) in phases.items()}
     hist_launch = {k: v / K for k, v in hist.items()}
     peak = PEAK_TFLOPS[prob.precision]
     info1 = eng.info()
     large = info1["path"] == "large_n"
     traffic_file = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    traffic_all = {}
+    traffic_all, traffic_src = {}, None
     if os.path.exists(traffic_file):
         try:
-            traffic_all = json.load(open(traffic_file))
+            tj = json.load(open(traffic_file))
+            # {"source": profile summary, "run": run id, "kernels": {kernel: HBM bytes per launch}} (older files:
+            # the kernel map alone)
+            traffic_all = tj.get("kernels", tj) if isinstance(tj, dict) else {}
+            traffic_src = {"file": os.path.relpath(traffic_file, ROOT), "source": tj.get("source"),
+                           "run": tj.get("run"), "counters": tj.get("counters")}
         except Exception:
             traffic_all = {}
     taylor = info1.get("chain") == "taylor" and not large
@@ -399,26 +407,38 @@ def main():
     blocks = bsz is not None and bsz.max() <= 4
     rot_blocks = bsz is not None and bsz.max() > 4
     if blocks:
-        # block chains (csrc/qoc_blk.hpp): one lane per (block, column), each term an n_b x n_b complex matvec in
-        # VALU registers; the launch's algorithmic bytes are the states it writes (x_k, and μ_k in the dual launch)
-        # plus the step records it reads (32 B record + P+1 Chebyshev coefficients + u_k per slice); the gradient
-        # reads x_k and λ_{k+1} once and writes dJdu
+        # block chains (csrc/qoc_blk.hpp, qoc_blku.hpp); the launch's algorithmic bytes are the states it writes (x_k,
+        # and μ_k in the dual launch) plus what it reads per slice: the step records of k_tchain_prep (32 B record +
+        # P+1 Chebyshev coefficients + u_k) for the polynomial-in-the-chain kernels, u_k alone for the block
+        # propagators (their step records are formed in the kernel); the gradient reads x_k and λ_{k+1} once and
+        # writes dJdu
         nb2 = float(np.sum(block_sizes(prob).astype(np.float64) ** 2))
         dirs = 2 if dual else 1
         tl = terms / K * dirs
         p_avg = terms / K / max(B * Nt, 1)
-        rec = B * Nt * (32 + 8 * (p_avg + 1) + 8 * nu)
-        if bprop:  # block propagators: each direction reads u_k and forms its step records in the kernel
-            rec = B * Nt * 8 * nu
+        rec = B * Nt * 8 * nu if bprop else B * Nt * (32 + 8 * (p_avg + 1) + 8 * nu)
         st = B * (Nt + 1) * N * m * esz
         models = {
-            "k_expm": ("hbm", (B * Nt * (8 * nu + 32 + 8 * (p_avg + 1))) / 1e9, "GB/s", PEAK_HBM_GBS),
+            "k_expm": ("hbm", 0.0 if bprop else (B * Nt * (8 * nu + 32 + 8 * (p_avg + 1))) / 1e9, "GB/s",
+                       PEAK_HBM_GBS),
             "k_chain_fwd": ("hbm", dirs * (st + rec) / 1e9, "GB/s", PEAK_HBM_GBS),
             "k_chain_bwd": ("hbm", (st + rec) / 1e9, "GB/s", PEAK_HBM_GBS),
             "k_grad": ("hbm", (2 * B * Nt * N * m * esz + 16 * nu * B * Nt) / 1e9, "GB/s", PEAK_HBM_GBS),
         }
-        block_flops = {"k_chain_fwd": 8.0 * nb2 * m * tl, "k_chain_bwd": 8.0 * nb2 * m * terms / K,
-                       "k_grad": 8.0 * nb2 * m * B * Nt * (2 * (args.order - 1) + nu * args.order)}
+        if bprop:
+            # executed fp64 VALU work: per (slice, block) the propagator's Taylor terms in the Cayley-Hamilton basis
+            # (n_b complex multiply-adds per term) plus forming A_k and U_k (~130 flops at n_b = 2), per slice one
+            # n_b x n_b complex matvec per column; the gradient: K (m n_b^2 CMAC), 2(o-1) products of n_b x n_b
+            # blocks and nu traces (8 flops per CMAC)
+            nbk = block_sizes(prob).astype(np.float64)
+            form = float(np.sum(8.0 * nbk * p_avg + 16.0 * nbk ** 3 + 40.0 * nbk ** 2)) * B * Nt
+            block_flops = {"k_chain_fwd": dirs * (form + 8.0 * nb2 * m * B * Nt),
+                           "k_chain_bwd": form + 8.0 * nb2 * m * B * Nt,
+                           "k_grad": 8.0 * B * Nt * float(np.sum(m * nbk ** 2 + 2 * (args.order - 1) * nbk ** 3
+                                                                 + nu * nbk ** 2))}
+        else:
+            block_flops = {"k_chain_fwd": 8.0 * nb2 * m * tl, "k_chain_bwd": 8.0 * nb2 * m * terms / K,
+                           "k_grad": 8.0 * nb2 * m * B * Nt * (2 * (args.order - 1) + nu * args.order)}
     elif taylor:
         # Taylor-action chains (csrc/qoc_tchain.hpp): no exponential kernel; the chains carry the Taylor terms,
         # each an N x N by N x m complex matvec (8 N^2 m flops) on v_mfma_f64_4x4x4 (fp64) / VALU (fp32); the dual
@@ -427,7 +447,9 @@ def main():
         tl = terms / K * (2 if dual else 1)
         mv_flops = 8.0 * N * N * m
         if rot_blocks:
-            mv_flops = 8 * 4 * 128.0 * len(block_sizes(prob)) * ((m + 1) // 2)
+            # algorithmic block work: one n_b x n_b complex matvec per block and column (8 n_b^2 m flops), not the
+            # executed MFMA flops of the 16-row padded waves (8 v_mfma_f64_4x4x4_4b of 4 x 128 flops per column pair)
+            mv_flops = 8.0 * float(np.sum(block_sizes(prob).astype(np.float64) ** 2)) * m
         models = {
             "k_expm": ("mfma", 0.0, "TFLOP/s", peak),  # k_tchain_prep: (P, s, e^mu) per slice, no flops counted
             "k_grad": ("mfma", grad_flops(N, m, nu, Nt, B, args.order,
@@ -487,18 +509,29 @@ def main():
             t = per_step[k] / 1e3
             kern[k]["executed_tflops"] = block_flops[k] / 1e12 / t if t > 0 else 0.0
         for k in ("k_chain_fwd", "k_chain_bwd"):
+            if not lps[k]:
+                continue
             kern[k]["terms_per_seed"] = terms / K / B
-            kern[k]["ns_per_serial_term"] = per_step[k] * 1e6 / max(terms / K / B, 1e-9)
+            if bprop:
+                # serial steps: Nt block matvecs per seed and direction (the propagators are formed beside them);
+                # model: the n_b x n_b complex matvec, 4 n_b^2 dependent-free fp64 FMAs issued at 4 cycles each +
+                # n_b 16-byte stores, at 2.1 GHz
+                nbm = int(block_sizes(prob).max())
+                kern[k]["serial_steps_per_seed"] = Nt
+                kern[k]["ns_per_serial_step"] = per_launch[k] * 1e6 / Nt
+                kern[k]["serial_step_model_ns"] = (16.0 * nbm * nbm + 8.0 * nbm) / 2.1
+            else:
+                kern[k]["ns_per_serial_term"] = per_launch[k] * 1e6 / max(terms / K / B, 1e-9)
         dom = max(("k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad"), key=lambda k: per_step[k])
         roof = {"kernel": names[dom], "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
                 "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
-                "traffic": traffic_all.get(names[dom]), "ms_per_launch": kern[dom]["ms_per_launch"],
-                "launches_per_step": lps[dom],
+                "traffic": traffic_all.get(names[dom]), "traffic_source": traffic_src,
+                "ms_per_launch": kern[dom]["ms_per_launch"], "launches_per_step": lps[dom],
                 "blocks": [int(x) for x in block_sizes(prob)],
                 "note": ("block chains (generators with invariant blocks): achieved = algorithmic HBM bytes per launch "
-                         "(states written, step records read; the gradient: x_k and λ_{k+1} read) / launch time"
-                         + ("; the forward chain and the μ recurrence of every seed in one launch (k_blk_dual)" if dual
-                            else ""))}
+                         "(states written, step records / u_k read; the gradient: x_k and λ_{k+1} read) / launch time"
+                         + ("; the forward chain and the μ recurrence of every seed in one launch (" +
+                            names["k_chain_fwd"] + ")" if dual else ""))}
     elif taylor:
         mf = prob.precision == "fp64"
         names = {"k_expm": "k_tchain_prep",
@@ -511,14 +544,14 @@ def main():
             # serial Taylor terms of one seed per launch and the time each takes (the chains' critical path)
             kern[k]["kernel"] = names[k]
             kern[k]["terms_per_seed"] = terms / K / B  # per direction
-            kern[k]["ns_per_serial_term"] = per_step[k] * 1e6 / max(terms / K / B, 1e-9)
+            kern[k]["ns_per_serial_term"] = per_launch[k] * 1e6 / max(terms / K / B, 1e-9)
         dom = max(("k_chain_fwd", "k_chain_bwd", "k_grad"), key=lambda k: per_step[k])
         if dual:
             kern["k_chain_fwd"]["note"] = names["k_chain_fwd"] + ": forward chain and mu recurrence of every seed in one launch"
         roof = {"kernel": names[dom], "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
                 "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
-                "traffic": traffic_all.get(names[dom]), "ms_per_launch": kern[dom]["ms_per_launch"],
-                "launches_per_step": lps[dom],
+                "traffic": traffic_all.get(names[dom]), "traffic_source": traffic_src,
+                "ms_per_launch": kern[dom]["ms_per_launch"], "launches_per_step": lps[dom],
                 "note": ("latency-bound serial recurrence (one workgroup per seed, Taylor terms in sequence): "
                          "achieved = executed matvec flops / launch time"
                          + ("; the backward (μ) recurrence runs beside the forward chain (" + names["k_chain_fwd"] +
@@ -539,14 +572,15 @@ def main():
             kname = "k_expm_rr_mix" if "k_expm_rr_mix" in traffic_all and "k_expm_rr" not in traffic_all else "k_expm_rr"
         roof = {"kernel": kname, "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
                 "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
-                "traffic": traffic_all.get(kname, traffic_all.get(dom)), "ms_per_launch": kern[dom]["ms_per_launch"]}
+                "traffic": traffic_all.get(kname, traffic_all.get(dom)), "traffic_source": traffic_src,
+                "ms_per_launch": kern[dom]["ms_per_launch"]}
     else:
         # dominant kernel = the batched complex GEMM (every phase is mostly k_bgemm launches)
         gs = eng.gemm_stats()
         ach = gs["flops"] / 1e12 / (gs["ms"] / 1e3) if gs["ms"] > 0 else 0.0
         kern["phases_note"] = "large-N path: k_expm/k_chain_*/k_grad entries are phase totals per step"
         roof = {"kernel": "k_bgemm", "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
-                "frac": ach / peak, "traffic": traffic_all.get("k_bgemm"),
+                "frac": ach / peak, "traffic": traffic_all.get("k_bgemm"), "traffic_source": traffic_src,
                 "ms_per_launch": gs["ms"] / max(gs["launches"], 1),
                 "launches_per_step": gs["launches"] / K,
                 "gflop_per_launch": gs["flops"] / max(gs["launches"], 1) / 1e9,

@@ -5,12 +5,14 @@
 // λ_k = U_k^H λ_{k+1} (:52-58) are serial.  When the generators have small invariant blocks (qoc_blk.hpp: cavity 20
 // blocks of 2 rows, zz 3 blocks of 3), U_k is block-diagonal with the same blocks, and one block of it is an NB x NB
 // matrix that costs about as much to form as the exponential's action on the m state columns — but it does not
-// depend on the state.  These kernels therefore keep the reference's split inside one workgroup per (seed,
-// direction):
-//   * formation waves form the block propagators U_k^β of the next chunk of C slices, parallel over (slice, block),
-//     into LDS (double-buffered), and the step records of the chunk after that (ρ_k, P_k, e^{μ_k});
-//   * chain waves advance the state with ONE NB x NB complex matvec per slice and block from LDS, and store x_{k+1}
-//     (μ_k / λ_k backward) in the caller's layout.
+// depend on the state.  So the work is split the reference's way:
+//   * k_blku_rec: one thread per (seed, slice) forms the step record (ρ_k, the Taylor degree P and halvings J,
+//     e^{μ_k}, the scaled controls), in parallel over every slice of the batch;
+//   * k_blku_fwd / _bwd / _dual: one workgroup per (seed, direction).  Formation waves form the block propagators
+//     U_k^β of the next chunk of C slices, parallel over (slice, block), into LDS (double-buffered); chain waves
+//     advance the state with ONE NB x NB complex matvec per slice and block from LDS, and store x_{k+1} (μ_k / λ_k
+//     backward) in the caller's layout.  The two roles run separate loops with one workgroup barrier per chunk, so
+//     the chain's loop issues no global load (its stores are never waited on).
 // The serial depth per seed drops from Σ_k P_k dependent polynomial terms (cavity 9 000) to Nt matvecs.
 //
 // The block exponential: exp(A_k) = e^{μ_k} exp(Ã_k) with the shifted generators Ã_j = A_j - μ_j I of
@@ -19,11 +21,13 @@
 // generators: r_j = half the width of H_j's spectral interval, Weyl) or ||Ã_k||_1 (other generators: r_j the
 // shifted 1-norms); J is the fewest halvings with ρ_k / 2^J <= θ_cap, and P the smallest degree whose tail
 // Σ_{t>P} (ρ_k / 2^J)^t / t! is <= 2^-53 — the backward-error level of the reference's Padé choice
-// (ExpMethodHigham2005), so U_k agrees with the reference's to rounding.  For NB = 2 and 3 the polynomial is
-// evaluated in the basis {I, Â, Â²} (Cayley-Hamilton: Â^NB is a combination of the lower powers with the
-// characteristic polynomial's coefficients), so that a term costs NB complex multiply-adds instead of NB³;
-// NB = 4 runs the plain matrix recurrence.  θ_cap = θ_17 ≈ 0.98 keeps the basis' rounding at the level of the
-// direct recurrence (numpy: ≤ 8e-16 against mpmath up to norm 1).
+// (ExpMethodHigham2005), so U_k agrees with the reference's to rounding.  Slices are grouped in aligned blocks of 64
+// that share the largest (J, P) among them (more terms than a slice needs only shrink its truncation error), so
+// every propagator of a chunk runs the same term loop.  For NB = 2 and 3 the polynomial is evaluated by Horner's
+// rule in the basis {I, Â, Â²} (Cayley-Hamilton: Â^NB is a combination of the lower powers with the characteristic
+// polynomial's coefficients), a term costing NB complex multiply-adds instead of NB³; NB = 4 runs the plain matrix
+// recurrence.  θ_cap = θ_17 ≈ 0.98 keeps the basis' rounding at the level of the direct recurrence (numpy: ≤ 8e-16
+// against mpmath up to norm 1).
 #pragma once
 #include "qoc_blk.hpp"
 
@@ -33,13 +37,56 @@ struct BlkuParams {
   double rad[3];                   // ρ_k = rad[0] + Σ_j |u_jk| rad[j]
   double mur[3], mui[3];           // shifts μ_j (e^{μ_k} = exp(μ_0 + Σ_j u_jk μ_j))
   double theta_cap;                // ρ_k / 2^J <= theta_cap (< 1)
-  int C;                           // slices per chunk
+  int C;                           // slices per chunk (divides 64)
   int CW;                          // chain waves (waves >= CW form propagators)
-  unsigned long long* terms;       // Σ_k P_k 2^J_k per forward pass (nullptr: not counted)
+  int Ntp;                         // slices per seed in the record array: Nt rounded up to 64
+  const double* rec;               // B x Ntp x BLKU_REC step records (k_blku_rec)
+  unsigned long long* terms;       // Σ_k P_k 2^J_k per forward pass (k_blku_rec; nullptr: not counted)
+  int probe_mode;                  // QOC_PROBE builds only: 1 skip the formation, 2 skip the chain
 };
+
+// Diagnostic cycle stamps (tools/blku_probe.hip builds with -DQOC_PROBE; empty otherwise): per-role segment times of
+// workgroup 7, summed over its lane-0 threads.
+#ifdef QOC_PROBE
+static __device__ unsigned long long g_bk[16];
+#define BK_T(var) TC_T(var)
+#define BK_ADD(slot, v)                                                          \
+  do {                                                                           \
+    if (blockIdx.x == 7 && (threadIdx.x & 63) == 0) atomicAdd(&g_bk[slot], (v)); \
+  } while (0)
+#else
+#define BK_T(var) \
+  do {            \
+  } while (0)
+#define BK_ADD(slot, v) \
+  do {                  \
+  } while (0)
+#endif
+
+// Propagators formed per lane at a time (independent recurrences interleaved): 2 for blocks of 2 rows; blocks of 3
+// and 4 rows take one (two would exceed 256 VGPRs).  Probe builds may override it.
+#ifndef QOC_BLKU_NU
+#define QOC_BLKU_NU(NB) ((NB) == 2 ? 2 : 1)
+#endif
 
 constexpr int BLKU_REC = 8;   // doubles per step record: e^{μ} (2), scale, scale u_1, scale u_2, P, J, -
 constexpr int BLKU_INVT = 32; // 1/t table
+constexpr int BLKU_RECBLK = 64;  // slices sharing one (J, P)
+// Taylor degrees of the block propagators: ρ_k / 2^J <= θ_cap ≈ 0.98 needs P <= 18; the term loops are unrolled to
+// BLKU_TMAX with the coefficients 1/t! as compile-time constants
+constexpr int BLKU_TMAX = 20;
+struct BlkuCoef {
+  double inv[BLKU_TMAX + 2];   // 1/t
+  double fact[BLKU_TMAX + 1];  // 1/t!
+};
+constexpr BlkuCoef blku_coef() {
+  BlkuCoef c{};
+  c.inv[0] = 0.0;
+  for (int t = 1; t <= BLKU_TMAX + 1; ++t) c.inv[t] = 1.0 / t;
+  c.fact[0] = 1.0;
+  for (int t = 1; t <= BLKU_TMAX; ++t) c.fact[t] = c.fact[t - 1] / t;
+  return c;
+}
 
 // LDS of one workgroup, in doubles: 1/t | generator blocks [3][NB^2][nblk] complex | step records [3][C][REC] |
 // block propagators [2][C][NB^2][nblk] complex | x_N (2 N m) | reduction (16)
@@ -55,38 +102,61 @@ __host__ __device__ inline size_t blku_lds(int N, int m, int NB, int nblk, int C
   return (blku_off_xN(NB, nblk, C) + 2 * (size_t)N * m + 16) * sizeof(double);
 }
 
-// Step record of slice k from u_k (one lane per slice).  cnt += P 2^J (executed Taylor terms).  P is the smallest
-// degree whose tail bound b^{P+1} / (P+1)! / (1 - b / (P+2)) >= Σ_{t>P} b^t / t! is <= 2^-53 (b = ρ_k / 2^J < 1).
-__device__ __forceinline__ void blku_record(const BlkuParams& bp, double u1, double u2, const double* __restrict__ invt,
-                                            double* __restrict__ rec, unsigned long long& cnt) {
-  const double rho = fma(fabs(u2), bp.rad[2], fma(fabs(u1), bp.rad[1], bp.rad[0]));
-  const double mr = fma(u2, bp.mur[2], fma(u1, bp.mur[1], bp.mur[0]));
-  const double mi = fma(u2, bp.mui[2], fma(u1, bp.mui[1], bp.mui[0]));
-  int J = 0;
-  double sc = 1.0;
-  while (rho * sc > bp.theta_cap && J < 60) {
-    sc *= 0.5;
-    ++J;
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Step records, one thread per (seed, slice) over B x Ntp (a wave = 64 aligned slices of one seed, which share the
+// largest J and P among them).  J: the fewest halvings with ρ_k / 2^J <= θ_cap; P: the smallest degree whose tail
+// bound b^{P+1} / (P+1)! / (1 - b / (P+2)) >= Σ_{t>P} b^t / t! is <= 2^-53 (b = ρ_k / 2^J < 1).
+// rec = [Re e^{μ_k}, Im e^{μ_k}, 2^-J, 2^-J u_1k, 2^-J u_2k, P, J, 0]; terms += Σ P 2^J (executed Taylor terms).
+__global__ __launch_bounds__(256) void k_blku_rec(const BlkuParams bp, const double* __restrict__ u, int nu, int Nt,
+                                                  long long total, double* __restrict__ rec) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long tt = t < total ? t : 0;
+  const int b = (int)(tt / bp.Ntp), k = (int)(tt - (long long)b * bp.Ntp);
+  const bool valid = t < total && k < Nt;
+  const double* uk = u + ((size_t)b * Nt + min(k, Nt - 1)) * nu;
+  const double u1 = valid && nu > 0 ? uk[0] : 0.0, u2 = valid && nu > 1 ? uk[1] : 0.0;
+  const double rho = valid ? fma(fabs(u2), bp.rad[2], fma(fabs(u1), bp.rad[1], bp.rad[0])) : 0.0;
+  int Jo = 0;
+  double so = 1.0;
+  while (rho * so > bp.theta_cap && Jo < 60) {
+    so *= 0.5;
+    ++Jo;
   }
-  const double b = rho * sc, tol = 1.1102230246251565e-16;
-  double term = b;  // b^{P+1} / (P+1)!
-  int P = 0;
-  while (P < TCHAIN_PMAX && term > tol * fma(-b, invt[P + 2], 1.0)) {
-    ++P;
-    term *= b * invt[P + 1];
+  const int J = wave_max(Jo);
+  const double sc = ldexp(1.0, -J);
+  const double bb = rho * sc, tol = 1.1102230246251565e-16;
+  constexpr BlkuCoef K = blku_coef();
+  double term = bb;  // b^{P+1} / (P+1)!
+  int Po = 0;
+#pragma unroll
+  for (int q = 0; q < BLKU_TMAX; ++q) {  // Po == q in iteration q: the 1/t are constants
+    if (!(term > tol * fma(-bb, K.inv[q + 2], 1.0))) break;
+    Po = q + 1;
+    term *= bb * K.inv[q + 2];
   }
-  const double er = exp(mr);
-  double sn, cs;
-  sincos(mi, &sn, &cs);
-  rec[0] = er * cs;
-  rec[1] = er * sn;
-  rec[2] = sc;
-  rec[3] = sc * u1;
-  rec[4] = sc * u2;
-  rec[5] = (double)P;
-  rec[6] = (double)J;
-  rec[7] = 0.0;
-  cnt += (unsigned long long)P << J;
+  const int P = wave_max(Po);
+  unsigned long long cnt = valid ? (unsigned long long)P << J : 0ull;
+  if (valid) {
+    const double mr = fma(u2, bp.mur[2], fma(u1, bp.mur[1], bp.mur[0]));
+    const double mi = fma(u2, bp.mui[2], fma(u1, bp.mui[1], bp.mui[0]));
+    const double er = exp(mr);
+    double sn, cs;
+    sincos(mi, &sn, &cs);
+    double2* r = reinterpret_cast<double2*>(rec + (size_t)tt * BLKU_REC);
+    r[0] = make_double2(er * cs, er * sn);
+    r[1] = make_double2(sc, sc * u1);
+    r[2] = make_double2(sc * u2, (double)P);
+    r[3] = make_double2((double)J, 0.0);
+  }
+  if (bp.terms) {
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(bp.terms, cnt);
+  }
 }
 
 // u <- u u (NB x NB complex, row-major e = i NB + k)
@@ -115,155 +185,209 @@ __device__ __forceinline__ void blku_square(double (&ur)[NB * NB], double (&ui)[
   }
 }
 
-// Σ_{t<=P} Â^t / t! on the block (Â = ar + i ai, row-major).  invt[t] = 1/t.
-template <int NB>
-__device__ __forceinline__ void blku_taylor(const double (&ar)[NB * NB], const double (&ai)[NB * NB], int P,
-                                            const double* __restrict__ invt, double (&ur)[NB * NB],
-                                            double (&ui)[NB * NB]) {
+// e^{μ} Σ_{t<=P} Â^t / t! for NU independent blocks at once (Â_u = ar[u] + i ai[u], row-major; P uniform over the
+// wave, e^{μ} = (pr[u], pi[u])): the NU recurrences interleave instruction by instruction, so that a lane keeps NU
+// dependency chains in flight.  NB = 2, 3: Horner's rule h <- Â h + c_t I from t = P down to 0 with c_t = 1/t!
+// (compile-time constants) in the Cayley-Hamilton basis, started from h = e^{μ} c_P so that the phase rides along;
+// NB = 4: the matrix recurrence (invt[t] = 1/t).
+template <int NB, int NU>
+__device__ __forceinline__ void blku_taylor(const double (&ar)[NU][NB * NB], const double (&ai)[NU][NB * NB], int P,
+                                            const double (&pr)[NU], const double (&pi)[NU],
+                                            const double* __restrict__ invt, double (&ur)[NU][NB * NB],
+                                            double (&ui)[NU][NB * NB]) {
+  constexpr BlkuCoef K = blku_coef();
   if constexpr (NB == 2) {
-    // Â² = τ Â - δ I: z_t = α_t I + β_t Â with (α, β) <- (-δ β, α + τ β)
-    const double tr = ar[0] + ar[3], ti = ai[0] + ai[3];
-    const double nr = (ar[1] * ar[2] - ai[1] * ai[2]) - (ar[0] * ar[3] - ai[0] * ai[3]);  // -δ
-    const double ni = (ar[1] * ai[2] + ai[1] * ar[2]) - (ar[0] * ai[3] + ai[0] * ar[3]);
-    double zar = 1.0, zai = 0.0, zbr = 0.0, zbi = 0.0;
-    double aar = 1.0, aai = 0.0, abr = 0.0, abi = 0.0, f = 1.0;
-    for (int t = 1; t <= P; ++t) {
-      const double yar = fma(nr, zbr, -ni * zbi), yai = fma(nr, zbi, ni * zbr);
-      const double ybr = fma(tr, zbr, fma(-ti, zbi, zar)), ybi = fma(tr, zbi, fma(ti, zbr, zai));
-      zar = yar;
-      zai = yai;
-      zbr = ybr;
-      zbi = ybi;
-      f *= invt[t];
-      aar = fma(f, zar, aar);
-      aai = fma(f, zai, aai);
-      abr = fma(f, zbr, abr);
-      abi = fma(f, zbi, abi);
+    // Â² = τ Â - δ I: Â (α I + β Â) = (-δ β) I + (α + τ β) Â
+    double tr[NU], ti[NU], nr[NU], ni[NU], hr[NU][2], hi[NU][2];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      tr[u] = ar[u][0] + ar[u][3];
+      ti[u] = ai[u][0] + ai[u][3];
+      nr[u] = (ar[u][1] * ar[u][2] - ai[u][1] * ai[u][2]) - (ar[u][0] * ar[u][3] - ai[u][0] * ai[u][3]);  // -δ
+      ni[u] = (ar[u][1] * ai[u][2] + ai[u][1] * ar[u][2]) - (ar[u][0] * ai[u][3] + ai[u][0] * ar[u][3]);
+      hr[u][0] = hi[u][0] = hr[u][1] = hi[u][1] = 0.0;
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      ur[e] = abr * ar[e] - abi * ai[e] + (e == 0 || e == 3 ? aar : 0.0);
-      ui[e] = abr * ai[e] + abi * ar[e] + (e == 0 || e == 3 ? aai : 0.0);
+    for (int t = BLKU_TMAX; t >= 0; --t) {
+      if (t > P) continue;  // uniform
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const double cr = K.fact[t] * pr[u], ci = K.fact[t] * pi[u];  // e^{μ} c_t
+        const double a_r = fma(nr[u], hr[u][1], fma(-ni[u], hi[u][1], cr));
+        const double a_i = fma(nr[u], hi[u][1], fma(ni[u], hr[u][1], ci));
+        const double b_r = fma(tr[u], hr[u][1], fma(-ti[u], hi[u][1], hr[u][0]));
+        const double b_i = fma(tr[u], hi[u][1], fma(ti[u], hr[u][1], hi[u][0]));
+        hr[u][0] = a_r;
+        hi[u][0] = a_i;
+        hr[u][1] = b_r;
+        hi[u][1] = b_i;
+      }
     }
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ur[u][e] = hr[u][1] * ar[u][e] - hi[u][1] * ai[u][e] + (e == 0 || e == 3 ? hr[u][0] : 0.0);
+        ui[u][e] = hr[u][1] * ai[u][e] + hi[u][1] * ar[u][e] + (e == 0 || e == 3 ? hi[u][0] : 0.0);
+      }
   } else if constexpr (NB == 3) {
     // Â³ = c2 Â² + c1 Â + c0 I (c2 = tr, c1 = -(sum of the principal 2x2 minors), c0 = det):
-    // z_t = α I + β Â + γ Â² with (α, β, γ) <- (γ c0, α + γ c1, β + γ c2)
-    auto mr = [&](int a, int b) { return ar[a] * ar[b] - ai[a] * ai[b]; };
-    auto mi = [&](int a, int b) { return ar[a] * ai[b] + ai[a] * ar[b]; };
-    // principal minors m01 = a00 a11 - a01 a10, m02 = a00 a22 - a02 a20, m12 = a11 a22 - a12 a21
-    const double m01r = mr(0, 4) - mr(1, 3), m01i = mi(0, 4) - mi(1, 3);
-    const double m02r = mr(0, 8) - mr(2, 6), m02i = mi(0, 8) - mi(2, 6);
-    const double m12r = mr(4, 8) - mr(5, 7), m12i = mi(4, 8) - mi(5, 7);
-    const double c2r = ar[0] + ar[4] + ar[8], c2i = ai[0] + ai[4] + ai[8];
-    const double c1r = -(m01r + m02r + m12r), c1i = -(m01i + m02i + m12i);
-    // det = a00 m12 - a01 (a10 a22 - a12 a20) + a02 (a10 a21 - a11 a20)
-    const double q1r = mr(3, 8) - mr(5, 6), q1i = mi(3, 8) - mi(5, 6);
-    const double q2r = mr(3, 7) - mr(4, 6), q2i = mi(3, 7) - mi(4, 6);
-    const double c0r = (ar[0] * m12r - ai[0] * m12i) - (ar[1] * q1r - ai[1] * q1i) + (ar[2] * q2r - ai[2] * q2i);
-    const double c0i = (ar[0] * m12i + ai[0] * m12r) - (ar[1] * q1i + ai[1] * q1r) + (ar[2] * q2i + ai[2] * q2r);
-    double zr[3] = {1.0, 0.0, 0.0}, zi[3] = {0.0, 0.0, 0.0};
-    double sr[3] = {1.0, 0.0, 0.0}, si[3] = {0.0, 0.0, 0.0}, f = 1.0;
-    for (int t = 1; t <= P; ++t) {
-      const double gr = zr[2], gi = zi[2];
-      const double n0r = fma(gr, c0r, -gi * c0i), n0i = fma(gr, c0i, gi * c0r);
-      const double n1r = fma(gr, c1r, fma(-gi, c1i, zr[0])), n1i = fma(gr, c1i, fma(gi, c1r, zi[0]));
-      const double n2r = fma(gr, c2r, fma(-gi, c2i, zr[1])), n2i = fma(gr, c2i, fma(gi, c2r, zi[1]));
-      zr[0] = n0r;
-      zi[0] = n0i;
-      zr[1] = n1r;
-      zi[1] = n1i;
-      zr[2] = n2r;
-      zi[2] = n2i;
-      f *= invt[t];
+    // Â (α I + β Â + γ Â²) = γ c0 I + (α + γ c1) Â + (β + γ c2) Â²
+    double c0r[NU], c0i[NU], c1r[NU], c1i[NU], c2r[NU], c2i[NU], hr[NU][3], hi[NU][3];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        sr[q] = fma(f, zr[q], sr[q]);
-        si[q] = fma(f, zi[q], si[q]);
+    for (int u = 0; u < NU; ++u) {
+      auto mr = [&](int a, int b) { return ar[u][a] * ar[u][b] - ai[u][a] * ai[u][b]; };
+      auto mi = [&](int a, int b) { return ar[u][a] * ai[u][b] + ai[u][a] * ar[u][b]; };
+      // principal minors m01 = a00 a11 - a01 a10, m02 = a00 a22 - a02 a20, m12 = a11 a22 - a12 a21
+      const double m01r = mr(0, 4) - mr(1, 3), m01i = mi(0, 4) - mi(1, 3);
+      const double m02r = mr(0, 8) - mr(2, 6), m02i = mi(0, 8) - mi(2, 6);
+      const double m12r = mr(4, 8) - mr(5, 7), m12i = mi(4, 8) - mi(5, 7);
+      c2r[u] = ar[u][0] + ar[u][4] + ar[u][8];
+      c2i[u] = ai[u][0] + ai[u][4] + ai[u][8];
+      c1r[u] = -(m01r + m02r + m12r);
+      c1i[u] = -(m01i + m02i + m12i);
+      // det = a00 m12 - a01 (a10 a22 - a12 a20) + a02 (a10 a21 - a11 a20)
+      const double q1r = mr(3, 8) - mr(5, 6), q1i = mi(3, 8) - mi(5, 6);
+      const double q2r = mr(3, 7) - mr(4, 6), q2i = mi(3, 7) - mi(4, 6);
+      c0r[u] = (ar[u][0] * m12r - ai[u][0] * m12i) - (ar[u][1] * q1r - ai[u][1] * q1i) + (ar[u][2] * q2r - ai[u][2] * q2i);
+      c0i[u] = (ar[u][0] * m12i + ai[u][0] * m12r) - (ar[u][1] * q1i + ai[u][1] * q1r) + (ar[u][2] * q2i + ai[u][2] * q2r);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) hr[u][q] = hi[u][q] = 0.0;
+    }
+#pragma unroll
+    for (int t = BLKU_TMAX; t >= 0; --t) {
+      if (t > P) continue;  // uniform
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const double gr = hr[u][2], gi = hi[u][2];
+        const double cr = K.fact[t] * pr[u], ci = K.fact[t] * pi[u];
+        const double n0r = fma(gr, c0r[u], fma(-gi, c0i[u], cr)), n0i = fma(gr, c0i[u], fma(gi, c0r[u], ci));
+        const double n1r = fma(gr, c1r[u], fma(-gi, c1i[u], hr[u][0])), n1i = fma(gr, c1i[u], fma(gi, c1r[u], hi[u][0]));
+        const double n2r = fma(gr, c2r[u], fma(-gi, c2i[u], hr[u][1])), n2i = fma(gr, c2i[u], fma(gi, c2r[u], hi[u][1]));
+        hr[u][0] = n0r;
+        hi[u][0] = n0i;
+        hr[u][1] = n1r;
+        hi[u][1] = n1i;
+        hr[u][2] = n2r;
+        hi[u][2] = n2i;
       }
     }
     // U = α I + Â (β I + γ Â)
-    double hr[9], hi[9];
 #pragma unroll
-    for (int e = 0; e < 9; ++e) {
-      hr[e] = sr[2] * ar[e] - si[2] * ai[e] + (e % 4 == 0 ? sr[1] : 0.0);
-      hi[e] = sr[2] * ai[e] + si[2] * ar[e] + (e % 4 == 0 ? si[1] : 0.0);
-    }
+    for (int u = 0; u < NU; ++u) {
+      double wr[9], wi[9];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        double pr = i == k ? sr[0] : 0.0, pi = i == k ? si[0] : 0.0;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          pr = fma(ar[i * 3 + q], hr[q * 3 + k], pr);
-          pr = fma(-ai[i * 3 + q], hi[q * 3 + k], pr);
-          pi = fma(ar[i * 3 + q], hi[q * 3 + k], pi);
-          pi = fma(ai[i * 3 + q], hr[q * 3 + k], pi);
-        }
-        ur[i * 3 + k] = pr;
-        ui[i * 3 + k] = pi;
+      for (int e = 0; e < 9; ++e) {
+        wr[e] = hr[u][2] * ar[u][e] - hi[u][2] * ai[u][e] + (e % 4 == 0 ? hr[u][1] : 0.0);
+        wi[e] = hr[u][2] * ai[u][e] + hi[u][2] * ar[u][e] + (e % 4 == 0 ? hi[u][1] : 0.0);
       }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          double sr = i == k ? hr[u][0] : 0.0, si = i == k ? hi[u][0] : 0.0;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            sr = fma(ar[u][i * 3 + q], wr[q * 3 + k], sr);
+            sr = fma(-ai[u][i * 3 + q], wi[q * 3 + k], sr);
+            si = fma(ar[u][i * 3 + q], wi[q * 3 + k], si);
+            si = fma(ai[u][i * 3 + q], wr[q * 3 + k], si);
+          }
+          ur[u][i * 3 + k] = sr;
+          ui[u][i * 3 + k] = si;
+        }
+    }
   } else {
-    // plain matrix recurrence Y_t = Â Y_{t-1}
-    double yr[NB * NB], yi[NB * NB];
+    // plain matrix recurrence Y_t = Â Y_{t-1}, NU = 1 (NB = 4: 64 CMAC per term); the phase multiplies at the end
+    static_assert(NU == 1, "NB = 4 forms one block per lane at a time");
+    double yr[NB * NB], yi[NB * NB], sr[NB * NB], si[NB * NB];
 #pragma unroll
     for (int e = 0; e < NB * NB; ++e) {
-      yr[e] = ur[e] = (e % (NB + 1) == 0) ? 1.0 : 0.0;
-      yi[e] = ui[e] = 0.0;
+      yr[e] = sr[e] = (e % (NB + 1) == 0) ? 1.0 : 0.0;
+      yi[e] = si[e] = 0.0;
     }
     double f = 1.0;
-    for (int t = 1; t <= P; ++t) {
+    for (int t = 1; t <= P; ++t) {  // not unrolled; the 1/t read is off the critical path
       double vr[NB * NB], vi[NB * NB];
 #pragma unroll
       for (int i = 0; i < NB; ++i)
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
-          double pr = 0.0, pi = 0.0;
+          double qr = 0.0, qi = 0.0;
 #pragma unroll
           for (int q = 0; q < NB; ++q) {
-            pr = fma(ar[i * NB + q], yr[q * NB + k], pr);
-            pr = fma(-ai[i * NB + q], yi[q * NB + k], pr);
-            pi = fma(ar[i * NB + q], yi[q * NB + k], pi);
-            pi = fma(ai[i * NB + q], yr[q * NB + k], pi);
+            qr = fma(ar[0][i * NB + q], yr[q * NB + k], qr);
+            qr = fma(-ai[0][i * NB + q], yi[q * NB + k], qr);
+            qi = fma(ar[0][i * NB + q], yi[q * NB + k], qi);
+            qi = fma(ai[0][i * NB + q], yr[q * NB + k], qi);
           }
-          vr[i * NB + k] = pr;
-          vi[i * NB + k] = pi;
+          vr[i * NB + k] = qr;
+          vi[i * NB + k] = qi;
         }
       f *= invt[t];
 #pragma unroll
       for (int e = 0; e < NB * NB; ++e) {
         yr[e] = vr[e];
         yi[e] = vi[e];
-        ur[e] = fma(f, vr[e], ur[e]);
-        ui[e] = fma(f, vi[e], ui[e]);
+        sr[e] = fma(f, vr[e], sr[e]);
+        si[e] = fma(f, vi[e], si[e]);
       }
+    }
+#pragma unroll
+    for (int e = 0; e < NB * NB; ++e) {
+      ur[0][e] = pr[0] * sr[e] - pi[0] * si[e];
+      ui[0][e] = pr[0] * si[e] + pi[0] * sr[e];
     }
   }
 }
 
-// One block propagator U_k^β = e^{μ_k} (p(Ã_k / 2^J))^{2^J} from the step record rec; gb: generator blocks
-// [3][NB^2][nblk] complex (entries of Ã_j at the block's rows), out: U at entry stride nblk.
-template <int NB>
-__device__ __forceinline__ void blku_form(const double2* __restrict__ gb, int nblk, int beta,
-                                          const double* __restrict__ rec, const double* __restrict__ invt,
-                                          double2* __restrict__ out) {
+// NU block propagators U_k^β = e^{μ_k} (p(Ã_k / 2^J))^{2^J} at once (units u: block beta[u] of the slice whose step
+// record is rec[u]; the chunk's P and J are uniform); gb: generator blocks [3][NB^2][nblk] complex (entries of Ã_j at
+// the block's rows), out[u]: U at entry stride nblk, written when st[u].  With J > 0 the phase is applied before the
+// squarings as e^{μ / 2^J}, i.e. it is taken from the record only when J = 0 (J > 0: the squarings of the
+// phase-free polynomial, then e^{μ}).
+template <int NB, int NU>
+__device__ __forceinline__ void blku_form(const double2* __restrict__ gb, int nblk, const int (&beta)[NU],
+                                          const double* const (&rec)[NU], const double* __restrict__ invt,
+                                          double2* const (&out)[NU], const bool (&st)[NU]) {
   constexpr int E = NB * NB;
-  const double s0 = rec[2], s1 = rec[3], s2 = rec[4];
-  const int P = (int)rec[5], J = (int)rec[6];
-  double ar[E], ai[E];
+  const int P = __builtin_amdgcn_readfirstlane((int)rec[0][5]), J = __builtin_amdgcn_readfirstlane((int)rec[0][6]);
+  double ar[NU][E], ai[NU][E], pr[NU], pi[NU];
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const double2 g0 = gb[(0 * E + e) * nblk + beta], g1 = gb[(1 * E + e) * nblk + beta],
-                  g2 = gb[(2 * E + e) * nblk + beta];
-    ar[e] = fma(s2, g2.x, fma(s1, g1.x, s0 * g0.x));
-    ai[e] = fma(s2, g2.y, fma(s1, g1.y, s0 * g0.y));
+  for (int u = 0; u < NU; ++u) {
+    const double s0 = rec[u][2], s1 = rec[u][3], s2 = rec[u][4];
+    pr[u] = J ? 1.0 : rec[u][0];
+    pi[u] = J ? 0.0 : rec[u][1];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const double2 g0 = gb[(0 * E + e) * nblk + beta[u]], g1 = gb[(1 * E + e) * nblk + beta[u]],
+                    g2 = gb[(2 * E + e) * nblk + beta[u]];
+      ar[u][e] = fma(s2, g2.x, fma(s1, g1.x, s0 * g0.x));
+      ai[u][e] = fma(s2, g2.y, fma(s1, g1.y, s0 * g0.y));
+    }
   }
-  double ur[E], ui[E];
-  blku_taylor<NB>(ar, ai, P, invt, ur, ui);
-  for (int q = 0; q < J; ++q) blku_square<NB>(ur, ui);
-  const double pr = rec[0], pi = rec[1];
+  double ur[NU][E], ui[NU][E];
+  blku_taylor<NB, NU>(ar, ai, P, pr, pi, invt, ur, ui);
+  if (J) {
+    for (int q = 0; q < J; ++q)
 #pragma unroll
-  for (int e = 0; e < E; ++e) out[e * nblk] = make_double2(pr * ur[e] - pi * ui[e], pr * ui[e] + pi * ur[e]);
+      for (int u = 0; u < NU; ++u) blku_square<NB>(ur[u], ui[u]);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const double qr = rec[u][0], qi = rec[u][1];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const double vr = ur[u][e], vi = ui[u][e];
+        ur[u][e] = qr * vr - qi * vi;
+        ui[u][e] = qr * vi + qi * vr;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+    if (st[u])
+#pragma unroll
+      for (int e = 0; e < E; ++e) out[u][e * nblk] = make_double2(ur[u][e], ui[u][e]);
 }
 
 // y = U x (FWD) or U^H x on one block (U row-major complex from LDS, entries at stride nblk)
@@ -288,7 +412,11 @@ __device__ __forceinline__ void blku_apply(const double2 (&U)[NB * NB], const do
 }
 
 // One workgroup per (seed, direction): FWD x_0 -> x_Nt (+ costs), else λ_Nt -> λ_0 (μ mode: X_target -> μ_0).
-template <int NB, bool FWD>
+// ADD (backward, non-μ): 2μ x_k on the penalty mask and the caller's dL/dx(x_k) are added to λ_k after each slice
+// (the only variant whose chain loop reads global memory).  Chunks lie on the absolute slice grid [aC, aC + C), the
+// forward pass taking a = 0, 1, .., the backward pass a = nC - 1, .., 0 (its first chunk may be partial), so that a
+// chunk never straddles two of k_blku_rec's 64-slice (J, P) groups.
+template <int NB, bool FWD, bool ADD>
 __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk, const BlkuParams& bp, const int b,
                                           const int mu_mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -317,37 +445,51 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
     }
   }
   const int nC = (Nt + C - 1) / C;
-  const double* ub = g.u + (size_t)b * Nt * nu;
+  auto chunk_of = [&](int c) { return FWD ? c : nC - 1 - c; };  // absolute chunk of sequence position c
   const bool chain = w < bp.CW;
   const int fl = tid - 64 * bp.CW, FL = nthr - 64 * bp.CW;  // formation lanes
-  unsigned long long cnt = 0;
-  // slice of chunk position p (clamped into [0, Nt-1]: the tail of the last chunk repeats slice Nt-1, unused)
-  auto slice_of = [&](int p) { return FWD ? min(p, Nt - 1) : max(Nt - 1 - p, 0); };
-  // step records of chunk c: one lane per slice, u prefetched one chunk ahead
-  double pu1 = 0.0, pu2 = 0.0;
-  auto uload = [&](int c) {
-    if (!chain && fl < C) {
-      const int k = slice_of(c * C + fl);
-      pu1 = nu > 0 ? ub[(size_t)k * nu] : 0.0;
-      pu2 = nu > 1 ? ub[(size_t)k * nu + 1] : 0.0;
+  // step records of sequence chunk c: C x REC doubles from k_blku_rec (the tail of a partial chunk: clamped reads,
+  // never used), through registers into the LDS ring slot c % 3
+  constexpr int RMAX = 8;  // loads per lane: 64 x REC doubles / 64 lanes at most
+  double rr[RMAX];
+  const double* recb = bp.rec + (size_t)b * bp.Ntp * BLKU_REC;
+  auto rec_load = [&](int c) {
+    const size_t base = (size_t)chunk_of(c) * C * BLKU_REC;
+#pragma unroll
+    for (int i = 0; i < RMAX; ++i) {
+      const int e = fl + i * FL;
+      rr[i] = e < C * BLKU_REC ? recb[base + e] : 0.0;
     }
   };
-  auto records = [&](int c, double u1, double u2) {
-    if (!chain && fl < C) {
-      unsigned long long dummy = 0;
-      const bool real = c * C + fl < Nt;
-      blku_record(bp, u1, u2, invt, recs + ((size_t)(c % 3) * C + fl) * BLKU_REC, FWD && real ? cnt : dummy);
+  auto rec_store = [&](int c) {
+    double* dst = recs + (size_t)(c % 3) * C * BLKU_REC;
+#pragma unroll
+    for (int i = 0; i < RMAX; ++i) {
+      const int e = fl + i * FL;
+      if (e < C * BLKU_REC) dst[e] = rr[i];
     }
   };
+  // the chunk's C nblk propagators, NU per lane at a time (units q, q + FL, ..: independent recurrences interleaved)
+  constexpr int NU = QOC_BLKU_NU(NB);
   auto form = [&](int c) {
-    if (!chain) {
-      const int units = C * nblk;
-      const double* rc = recs + (size_t)(c % 3) * C * BLKU_REC;
-      double2* Uc = Ub + (size_t)(c & 1) * C * E * nblk;
-      for (int q = fl; q < units; q += FL) {
-        const int jj = q / nblk, beta = q - jj * nblk;
-        blku_form<NB>(gb, nblk, beta, rc + (size_t)jj * BLKU_REC, invt, Uc + (size_t)jj * E * nblk + beta);
+    const int a = chunk_of(c), jn = min(C, Nt - a * C), units = jn * nblk;
+    const double* rc = recs + (size_t)(c % 3) * C * BLKU_REC;
+    double2* Uc = Ub + (size_t)(c & 1) * C * E * nblk;
+    for (int q = fl; q < units; q += NU * FL) {
+      int be[NU];
+      const double* rp[NU];
+      double2* op[NU];
+      bool st[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int qu = q + u * FL;
+        st[u] = qu < units;
+        const int qq = st[u] ? qu : q, jj = qq / nblk;
+        be[u] = qq - jj * nblk;
+        rp[u] = rc + (size_t)jj * BLKU_REC;
+        op[u] = Uc + (size_t)jj * E * nblk + be[u];
       }
+      blku_form<NB, NU>(gb, nblk, be, rp, invt, op, st);
     }
   };
   // chain lanes: lane l < nblk m owns block l % nblk of column l / nblk
@@ -362,11 +504,10 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   double* Sb = reinterpret_cast<double*>((cx<double>*)(FWD ? g.X : g.L) + (size_t)b * (Nt + 1) * Nm);
   const double* Xb = reinterpret_cast<const double*>((const cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm);
   const double* srcb =
-      (!FWD && g.src && !mu_mode) ? reinterpret_cast<const double*>((const cx<double>*)g.src + (size_t)b * (Nt + 1) * Nm)
-                                    : nullptr;
+      (ADD && g.src) ? reinterpret_cast<const double*>((const cx<double>*)g.src + (size_t)b * (Nt + 1) * Nm) : nullptr;
   const unsigned char* pmask = (FWD || !mu_mode) ? g.pmask : nullptr;
   const double tmu = 2.0 * g.mu;
-  const bool add = !FWD && (pmask || srcb);
+  const bool penon = pmask != nullptr;
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const bool ok = ln.r[i] >= 0;
@@ -399,75 +540,117 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
     xr[i] = v.r;
     xi[i] = v.i;
   }
-  // the state of slice position k to HBM (padding elements go to the sink: no branch around the stores)
-  auto store = [&](int k) __attribute__((always_inline)) {
+  if (chain) {  // the first state (x_0 / λ_Nt)
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      double* p = ln.r[i] >= 0 ? Sb + (size_t)k * 2 * Nm + off[i] : sink;
+      double* p = ln.r[i] >= 0 ? Sb + (size_t)(FWD ? 0 : Nt) * 2 * Nm + off[i] : sink;
       *reinterpret_cast<double2*>(p) = make_double2(xr[i], xi[i]);
-      if (FWD) pen += pm[i] ? xr[i] * xr[i] + xi[i] * xi[i] : 0.0;
+      if (FWD && penon) pen += pm[i] ? xr[i] * xr[i] + xi[i] * xi[i] : 0.0;
     }
-  };
-  if (chain) store(FWD ? 0 : Nt);
-  // prologue: records of chunks 0 and 1, propagators of chunk 0
-  uload(0);
-  records(0, pu1, pu2);
-  if (nC > 1) {
-    uload(1);
-    records(1, pu1, pu2);
   }
-  if (nC > 2) uload(2);
+  // prologue: records of sequence chunks 0 and 1 in LDS, chunk 2's in flight, propagators of chunk 0
+  if (!chain) {
+    rec_load(0);
+    rec_store(0);
+    if (nC > 1) {
+      rec_load(1);
+      rec_store(1);
+    }
+    if (nC > 2) rec_load(2);
+  }
   lds_barrier();
-  form(0);
+  if (!chain) form(0);
   lds_barrier();
-  for (int c = 0; c < nC; ++c) {
-    if (chain) {
-      const double2* Uc = Ub + (size_t)(c & 1) * C * E * nblk + beta;
-      double2 U0[E], U1[E];
+  if (chain) {
+    // state of each row: a running pointer (padding rows go to the sink with stride 0: no branch around the stores)
+    double* sp[NB];
+    long long sst[NB];
 #pragma unroll
-      for (int e = 0; e < E; ++e) U0[e] = Uc[e * nblk];
-      const int jn = min(C, Nt - c * C);
-      for (int jj = 0; jj < jn; ++jj) {
-        const int k = FWD ? c * C + jj : Nt - 1 - (c * C + jj);
-        const int jp = min(jj + 1, C - 1);
+    for (int i = 0; i < NB; ++i) {
+      const bool ok = ln.r[i] >= 0;
+      sp[i] = ok ? Sb + (FWD ? 2 * Nm : (size_t)(Nt - 1) * 2 * Nm) + off[i] : sink;
+      sst[i] = ok ? (FWD ? 2 * (long long)Nm : -2 * (long long)Nm) : 0;
+    }
+    for (int c = 0; c < nC; ++c) {
+      BK_T(t0);
+#ifdef QOC_PROBE
+      if (bp.probe_mode != 2) {
+#else
+      {
+#endif
+        const int a = chunk_of(c), jn = min(C, Nt - a * C);
+        const double2* Uc = Ub + (size_t)(c & 1) * C * E * nblk + beta;
+        // one slice (chunk position jj): y = U x (U^H backward), the additions of the non-μ backward, the store
+        auto slice = [&](const double2(&U)[E], int jj) __attribute__((always_inline)) {
+          double ar_[NB], ai_[NB];
+          if constexpr (ADD) {  // 2μ x_k on the mask + the caller's dL/dx(x_k), added after the slice
+            const int k = a * C + jj;
 #pragma unroll
-        for (int e = 0; e < E; ++e) U1[e] = Uc[(size_t)jp * E * nblk + e * nblk];
-        double ar_[NB], ai_[NB];
-        if (add) {  // 2μ x_k on the mask + the caller's dL/dx(x_k), added after the slice
-#pragma unroll
-          for (int i = 0; i < NB; ++i) {
-            const size_t o = (size_t)k * 2 * Nm + off[i];
-            ar_[i] = pm[i] ? tmu * Xb[o] : 0.0;
-            ai_[i] = pm[i] ? tmu * Xb[o + 1] : 0.0;
-            if (srcb && ln.r[i] >= 0) {
-              ar_[i] += srcb[o];
-              ai_[i] += srcb[o + 1];
+            for (int i = 0; i < NB; ++i) {
+              const size_t o = (size_t)k * 2 * Nm + off[i];
+              ar_[i] = pm[i] ? tmu * Xb[o] : 0.0;
+              ai_[i] = pm[i] ? tmu * Xb[o + 1] : 0.0;
+              if (srcb && ln.r[i] >= 0) {
+                ar_[i] += srcb[o];
+                ai_[i] += srcb[o + 1];
+              }
             }
           }
-        }
-        double yr[NB], yi[NB];
-        blku_apply<NB, FWD>(U0, xr, xi, yr, yi);
+          double yr[NB], yi[NB];
+          blku_apply<NB, FWD>(U, xr, xi, yr, yi);  // padding rows stay 0: U is diagonal there and x is 0
 #pragma unroll
-        for (int i = 0; i < NB; ++i) {
-          const bool ok = ln.r[i] >= 0;
-          xr[i] = ok ? yr[i] : 0.0;
-          xi[i] = ok ? yi[i] : 0.0;
-          if (add) {
-            xr[i] += ar_[i];
-            xi[i] += ai_[i];
+          for (int i = 0; i < NB; ++i) {
+            xr[i] = yr[i];
+            xi[i] = yi[i];
+            if constexpr (ADD) {
+              xr[i] += ar_[i];
+              xi[i] += ai_[i];
+            }
+            *reinterpret_cast<double2*>(sp[i]) = make_double2(xr[i], xi[i]);
+            sp[i] += sst[i];
+            if (FWD && penon) pen += pm[i] ? xr[i] * xr[i] + xi[i] * xi[i] : 0.0;  // uniform branch
           }
-        }
-        store(FWD ? k + 1 : k);
+        };
+        // two slices per iteration with the roles of the two U register sets swapped (no register copies); the next
+        // slice's U is read from LDS before this slice's matvec.  Forward: jj = 0 .. jn-1; backward: jn-1 .. 0
+        auto pos = [&](int s) { return FWD ? s : jn - 1 - s; };
+        double2 U0[E], U1[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) U0[e] = U1[e];
+        for (int e = 0; e < E; ++e) U0[e] = Uc[(size_t)pos(0) * E * nblk + e * nblk];
+        for (int s = 0; s < jn; s += 2) {
+          const size_t o1 = (size_t)pos(min(s + 1, jn - 1)) * E * nblk;
+#pragma unroll
+          for (int e = 0; e < E; ++e) U1[e] = Uc[o1 + e * nblk];
+          slice(U0, pos(s));
+          if (s + 1 >= jn) break;
+          const size_t o2 = (size_t)pos(min(s + 2, jn - 1)) * E * nblk;
+#pragma unroll
+          for (int e = 0; e < E; ++e) U0[e] = Uc[o2 + e * nblk];
+          slice(U1, pos(s + 1));
+        }
       }
-    } else {
-      const double u1 = pu1, u2 = pu2;
-      if (c + 3 < nC) uload(c + 3);
-      if (c + 1 < nC) form(c + 1);
-      if (c + 2 < nC) records(c + 2, u1, u2);
+      BK_T(t1);
+      lds_barrier();
+      BK_T(t2);
+      BK_ADD(0, t1 - t0);
+      BK_ADD(1, t2 - t1);
     }
-    lds_barrier();
+  } else {
+    for (int c = 0; c < nC; ++c) {
+      BK_T(t0);
+      if (c + 2 < nC) rec_store(c + 2);  // loaded one iteration ago
+      if (c + 3 < nC) rec_load(c + 3);
+#ifdef QOC_PROBE
+      if (c + 1 < nC && bp.probe_mode != 1) form(c + 1);
+#else
+      if (c + 1 < nC) form(c + 1);
+#endif
+      BK_T(t1);
+      lds_barrier();
+      BK_T(t2);
+      BK_ADD(3, t1 - t0);
+      BK_ADD(4, t2 - t1);
+    }
   }
   if (FWD) {
     if (chain) {
@@ -478,10 +661,6 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
           xN[off[i] + 1] = xi[i];
         }
     }
-    if (bp.terms) {
-      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-      if ((tid & 63) == 0 && cnt) atomicAdd(bp.terms, cnt);
-    }
     __syncthreads();
     chain_costs<double>(N, m, (const cx<double>*)g.Xt, [&](int q) { return cx<double>{xN[2 * q], xN[2 * q + 1]}; },
                         g.cost_kind, g.n_norm, block_sum(pen, red) * g.mu, red, g.J + b, g.coef + (size_t)b * 2 * m,
@@ -491,11 +670,12 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
 
 template <int NB>
 __global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_fwd(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
-  blku_body<NB, true>(g, bk, bp, blockIdx.x, 0);
+  blku_body<NB, true, false>(g, bk, bp, blockIdx.x, 0);
 }
-template <int NB>
+// backward: ADD = the state penalty or the caller's co-state source (not in μ mode)
+template <int NB, bool ADD>
 __global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_bwd(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
-  blku_body<NB, false>(g, bk, bp, blockIdx.x, g.mu_mode);
+  blku_body<NB, false, ADD>(g, bk, bp, blockIdx.x, g.mu_mode);
 }
 // the forward chain and the μ recurrence (mu_mode) of every seed in one launch of 2B workgroups (the direction
 // alternating every 8 workgroups, so that each XCD takes both)
@@ -505,8 +685,8 @@ __global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_dual(const TChainA
   const bool by8 = (B & 7) == 0;
   const int dir = by8 ? (i >> 3) & 1 : i & 1;
   const int seed = by8 ? ((i >> 4) << 3) | (i & 7) : i >> 1;
-  if (dir == 0) blku_body<NB, true>(g, bk, bp, seed, 0);
-  else blku_body<NB, false>(g, bk, bp, seed, 1);
+  if (dir == 0) blku_body<NB, true, false>(g, bk, bp, seed, 0);
+  else blku_body<NB, false, false>(g, bk, bp, seed, 1);
 }
 
 // The order-ORD gradient per block (expm_jacobian! + _compute_u_sensitivity, src/gradient_computations.jl:177-223)

@@ -162,6 +162,7 @@ struct qoc_ctx {
   int nwb = 0;                   // MFMA block waves per column pair
   int* d_wrow = nullptr;         // nwb x 16 rows of each wave's state (-1 padding)
   size_t blk_dev_bytes = 0;      // d_brow + d_wrow (counted in dev_bytes)
+  double* d_blkrec = nullptr;    // block propagators: B x Ntp x BLKU_REC step records (k_blku_rec, allocated on first use)
   // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;

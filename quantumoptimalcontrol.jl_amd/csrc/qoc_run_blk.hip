@@ -179,12 +179,18 @@ static BlkuShape blku_shape(const qoc_ctx* c) {
   if (const char* env = getenv("QOC_BLKU_FW")) fw = atoi(env);
   fw = std::max(1, std::min(fw, 8 - s.CW));
   s.W = s.CW + fw;
-  s.C = std::min(64, 64 * fw);
+  s.C = 64;  // a power of two: chunks never straddle k_blku_rec's 64-slice (J, P) groups
   while (s.C > 4 && blku_lds(c->N, c->m, NB, c->nblk, s.C) > 52 * 1024) s.C >>= 1;
-  if (const char* env = getenv("QOC_BLKU_C")) s.C = std::max(1, std::min(atoi(env), 64 * fw));
+  if (const char* env = getenv("QOC_BLKU_C")) {
+    int q = 1;
+    while (q * 2 <= std::min(atoi(env), 64)) q *= 2;
+    s.C = q;
+  }
   s.lds = blku_lds(c->N, c->m, NB, c->nblk, s.C);
   return s;
 }
+
+static int blku_ntp(const qoc_ctx* c) { return (c->Nt + BLKU_RECBLK - 1) / BLKU_RECBLK * BLKU_RECBLK; }
 
 static BlkuParams blku_params(const qoc_ctx* c, const BlkuShape& s) {
   BlkuParams p{};
@@ -198,8 +204,29 @@ static BlkuParams blku_params(const qoc_ctx* c, const BlkuShape& s) {
   p.theta_cap = c->tprm.theta[17];
   p.C = s.C;
   p.CW = s.CW;
+  p.Ntp = blku_ntp(c);
+  p.rec = c->d_blkrec;
   p.terms = c->d_terms;
   return p;
+}
+
+// the step records of every (seed, slice) of the current u (k_blku_rec); count: add Σ P 2^J to the terms counter
+static int blku_records(qoc_ctx* c, BlkuParams& bp, bool count) {
+  const long long total = (long long)c->B * blku_ntp(c);
+  if (!c->d_blkrec) {
+    const size_t bytes = (size_t)total * BLKU_REC * sizeof(double);
+    HIPCHK(c, hipMalloc((void**)&c->d_blkrec, bytes));
+    c->dev_bytes += bytes;
+  }
+  bp.rec = c->d_blkrec;
+  BlkuParams rp = bp;
+  rp.terms = count ? c->d_terms : nullptr;
+  const int mk = mark_begin(c, 0);
+  hipLaunchKernelGGL(k_blku_rec, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, c->stream, rp,
+                     (const double*)c->d_u, c->nu, c->Nt, total, c->d_blkrec);
+  mark_end(c, mk);
+  HIPCHK(c, hipGetLastError());
+  return QOC_OK;
 }
 
 static BlkArgs blk_args(const qoc_ctx* c) {
@@ -398,7 +425,9 @@ static int blku_forward(qoc_ctx* c) {
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
   const BlkuShape s = blku_shape(c);
-  const BlkuParams bp = blku_params(c, s);
+  BlkuParams bp = blku_params(c, s);
+  int r = blku_records(c, bp, true);
+  if (r) return r;
   const int mk = mark_begin(c, 1);
   const hipError_t e = blku_dispatch(c, [&](auto NB_) {
     constexpr int NB = decltype(NB_)::value;
@@ -447,14 +476,19 @@ static int blku_backward(qoc_ctx* c, int order, double* d_dJdu) {
   const BlkArgs bk = blk_args(c);
   const BlkuShape s = blku_shape(c);
   BlkuParams bp = blku_params(c, s);
-  bp.terms = nullptr;
+  int r = blku_records(c, bp, false);  // the u of the last propagate (stale-checked by the caller)
+  if (r) return r;
+  const bool add = g.pmask || g.src;
   const int mk = mark_begin(c, 2);
   const hipError_t e = blku_dispatch(c, [&](auto NB_) {
     constexpr int NB = decltype(NB_)::value;
-    const hipError_t q = blk_lds_attr(k_blku_bwd<NB>, s.lds);
-    if (q != hipSuccess) return q;
-    hipLaunchKernelGGL((k_blku_bwd<NB>), dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, bp);
-    return hipGetLastError();
+    auto launch = [&](auto kern) {
+      const hipError_t q = blk_lds_attr(kern, s.lds);
+      if (q != hipSuccess) return q;
+      hipLaunchKernelGGL(kern, dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, bp);
+      return hipGetLastError();
+    };
+    return add ? launch(k_blku_bwd<NB, true>) : launch(k_blku_bwd<NB, false>);
   });
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_bwd launch: %s", hipGetErrorString(e));
@@ -471,7 +505,9 @@ static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
   const BlkuShape s = blku_shape(c);
-  const BlkuParams bp = blku_params(c, s);
+  BlkuParams bp = blku_params(c, s);
+  int r0 = blku_records(c, bp, true);
+  if (r0) return r0;
   const int mk = mark_begin(c, 1);
   const hipError_t e = blku_dispatch(c, [&](auto NB_) {
     constexpr int NB = decltype(NB_)::value;

@@ -266,6 +266,19 @@ def cavity_problem(N_cavity=20, Nt=1000, dt=1.0) -> Problem:
                    xt.astype(np.complex128), 2.0, Nt, "fp64")
 
 
+def cavity_dense_problem(N_cavity=20, Nt=1000, dt=1.0) -> Problem:
+    """Config 3 with a drive that also displaces the cavity: Tc = b^dag (x) I + I (x) a^dag (one drive line coupled to
+    both modes), so that the generators no longer split into the 2 x 2 invariant blocks of the qubit-only drive
+    (examples/models/cavity_qubit.jl:27, Tc = kron(b', I)) and the dense Taylor-action chains and fused gradient
+    run.  Same H0, x0, target and controls as cavity_problem."""
+    H0, Tc, theta = cavity_model(N_cavity)
+    a = annihilation_op(N_cavity)
+    Tc = Tc + np.kron(np.eye(2), a.T)
+    A0, A1, A2 = setup_bilinear_matrices(H0, Tc / 2, dt)
+    base = cavity_problem(N_cavity, Nt, dt)
+    return Problem("cavity_qubit_dense", A0, [A1, A2], base.x0, base.x_target, base.n, Nt, "fp64")
+
+
 def cavity_controls(B, Nt, seed=0, umax=0.05) -> np.ndarray:
     rng = np.random.default_rng(seed)
     return rng.uniform(-umax, umax, size=(B, 2, Nt))
@@ -349,6 +362,7 @@ CONFIGS = {
     "zz_plumbing": (lambda: zz_problem(100), lambda B, s=0: zz_controls(B, 100, 10.0, s), 1),
     "zz_batch": (lambda: zz_problem(500), lambda B, s=0: zz_controls(B, 500, 20.0, s), 512),
     "cavity": (lambda: cavity_problem(20, 1000), lambda B, s=0: cavity_controls(B, 1000, s), 256),
+    "cavity_dense": (lambda: cavity_dense_problem(20, 1000), lambda B, s=0: cavity_controls(B, 1000, s), 256),
     "tunable_bus": (lambda: tunable_bus_problem(2000), lambda B, s=0: tunable_bus_controls(B, 2000, s), 512),
     "synthetic": (lambda: synthetic_problem(256, 1000), lambda B, s=0: synthetic_controls(B, 1000, 2, s), 128),
 }

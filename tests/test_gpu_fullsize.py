@@ -81,6 +81,17 @@ def test_cavity_full_size(built_lib, chain, monkeypatch):
     assert (info["chain_kernel"] in BLOCK_KERNEL.values()) == (chain in BLOCK_KERNEL), info
 
 
+@pytest.mark.parametrize("chain", ["auto", "propagators"])
+def test_cavity_dense_full_size(built_lib, chain, monkeypatch):
+    """config 3 with a drive that also displaces the cavity (systems.cavity_dense_problem: no invariant blocks): the
+    dense Taylor-action chains on v_mfma_f64_4x4x4 and the fused order-3 gradient, N=40, Nt=1000, B=256, against
+    the C port."""
+    seeds = list(range(0, 256, 256 // CHECK_SEEDS))
+    info = _check_config("cavity_dense", seeds, None if chain == "auto" else chain, monkeypatch)
+    assert info["chain_kernel"] not in BLOCK_KERNEL.values() and info["chain_kernel"] != "blocks", info
+    assert info["chain"] == ("propagators" if chain == "propagators" else "taylor"), info
+
+
 @pytest.mark.parametrize("chain", ["auto", "dense", "propagators"])
 def test_tunable_bus_full_size(built_lib, chain, monkeypatch):
     """config 4: two_qubit_tunable_bus N=27, m=1, Nt=2000, B=512 per GPU, ||A_k||_1 ~ 30: every seed against

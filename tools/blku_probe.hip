@@ -1,0 +1,116 @@
+// Segment cycle breakdown of the block-propagator dual launch (diagnostic; built with -DQOC_PROBE):
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DQOC_PROBE -o tools/blku_probe tools/blku_probe.hip
+// A cavity-shaped problem (N = 2 n blocks of 2 rows {b, b + n}, m = 2, nu = 2) with synthetic skew-Hermitian
+// generators of the cavity's norms; prints the launch time per formation-wave count and chunk size, and for
+// workgroup 7 the cycles per chunk of: chain compute, chain barrier wait, formation, formation + records,
+// formation barrier wait; probe modes 1 (no formation) and 2 (no chain) give the floors of each role.
+// Usage: blku_probe [NB=2|3] [B] [Nt]
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../quantumoptimalcontrol.jl_amd/csrc/qoc_blku.hpp"
+using namespace qoc;
+
+template <int NB>
+void run(int B, int Nt, int nblk, int m, int W, int C, int mode) {
+  const int nu = 2, N = NB * nblk;
+  const size_t NN = (size_t)N * N;
+  std::vector<cx<double>> A((nu + 1) * NN, cx<double>{0, 0});
+  std::vector<int> brow((size_t)nblk * NB);
+  for (int b = 0; b < nblk; ++b)
+    for (int i = 0; i < NB; ++i) brow[b * NB + i] = b + i * nblk;
+  for (int b = 0; b < nblk; ++b)
+    for (int i = 0; i < NB; ++i)
+      for (int k = 0; k < NB; ++k) {
+        const int r = brow[b * NB + i], c = brow[b * NB + k];
+        if (i == k) A[r + (size_t)N * c] = {0.0, -0.016 * (i * b) + 0.15};  // -i (H0 - centre)
+        if (i != k) {
+          A[NN + r + (size_t)N * c] = {0.0, -0.5};                     // -i (T + T^H) / 2
+          A[2 * NN + r + (size_t)N * c] = {i < k ? 0.5 : -0.5, 0.0};  // -i i (T - T^H) / 2
+        }
+      }
+  std::vector<double> u((size_t)B * Nt * nu);
+  for (size_t e = 0; e < u.size(); ++e) u[e] = 0.05 * (((e * 7919) % 1000) / 500.0 - 1.0);
+  std::vector<cx<double>> x0((size_t)N * m, cx<double>{0, 0});
+  for (int c = 0; c < m; ++c)
+    for (int r = 0; r < N; ++r) x0[r + (size_t)N * c] = {(r % 2 == c % 2) ? 1.0 / std::sqrt(N / 2.0) : 0.0, 0.0};
+  cx<double>*dA, *dx0, *dX, *dL, *dcoef;
+  double *dJ, *du, *dsink;
+  int* dbrow;
+  unsigned long long* dterms;
+  (void)hipMalloc(&dA, A.size() * 16);
+  (void)hipMalloc(&du, u.size() * 8);
+  (void)hipMalloc(&dx0, x0.size() * 16);
+  (void)hipMalloc(&dX, (size_t)B * (Nt + 1) * N * m * 16);
+  (void)hipMalloc(&dL, (size_t)B * (Nt + 1) * N * m * 16);
+  (void)hipMalloc(&dcoef, (size_t)B * 2 * m * 16);
+  (void)hipMalloc(&dJ, B * 8);
+  (void)hipMalloc(&dsink, TCHAIN_SINK * 8);
+  (void)hipMalloc(&dbrow, brow.size() * 4);
+  (void)hipMalloc(&dterms, 8);
+  (void)hipMemcpy(dA, A.data(), A.size() * 16, hipMemcpyHostToDevice);
+  (void)hipMemcpy(du, u.data(), u.size() * 8, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dx0, x0.data(), x0.size() * 16, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dbrow, brow.data(), brow.size() * 4, hipMemcpyHostToDevice);
+  TChainArgs g{};
+  g.N = N; g.m = m; g.nu = nu; g.Nt = Nt; g.At = dA; g.u = du; g.x0 = dx0; g.X = dX; g.L = dL;
+  g.Xt = dx0; g.cost_kind = COST_TRACE; g.n_norm = m; g.J = dJ; g.coef = dcoef; g.sink = dsink;
+  BlkArgs bk{};
+  bk.brow = dbrow; bk.A = dA; bk.nblk = nblk;
+  BlkuParams bp{};
+  bp.rad[0] = 0.154; bp.rad[1] = bp.rad[2] = 0.5;
+  bp.theta_cap = 0.978;
+  bp.C = C;
+  bp.CW = (nblk * m + 63) / 64;
+  bp.Ntp = (Nt + 63) / 64 * 64;
+  bp.terms = dterms;
+  bp.probe_mode = mode;
+  double* drec;
+  const long long total = (long long)B * bp.Ntp;
+  (void)hipMalloc(&drec, total * BLKU_REC * 8);
+  bp.rec = drec;
+  hipLaunchKernelGGL(k_blku_rec, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, 0, bp, du, nu, Nt, total, drec);
+  (void)hipDeviceSynchronize();
+  const size_t lds = blku_lds(N, m, NB, nblk, C);
+  (void)hipFuncSetAttribute((const void*)k_blku_dual<NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  float ms = 0;
+  unsigned long long z[16] = {};
+  for (int it = 0; it < 3; ++it) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bk), z, sizeof(z));
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL((k_blku_dual<NB>), dim3(2 * B), dim3(64 * W), lds, 0, g, bk, bp);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    (void)hipEventElapsedTime(&ms, a, b);
+  }
+  if (hipGetLastError() != hipSuccess) {
+    printf("launch failed\n");
+    exit(1);
+  }
+  unsigned long long tc[16];
+  (void)hipMemcpyFromSymbol(tc, HIP_SYMBOL(g_bk), sizeof(tc));
+  const int nC = (Nt + C - 1) / C, fw = W - bp.CW;
+  printf("NB=%d nblk=%d m=%d B=%d Nt=%d W=%d C=%2d mode=%d lds=%zu: %.4f ms  per chunk (cycles): chain %6.0f  wait %6.0f"
+         " | form %6.0f  form+rec %6.0f  wait %6.0f\n",
+         NB, nblk, m, B, Nt, W, C, mode, lds, ms, tc[0] / (double)nC / bp.CW, tc[1] / (double)nC / bp.CW,
+         tc[2] / (double)nC / fw, tc[3] / (double)nC / fw, tc[4] / (double)nC / fw);
+  (void)hipFree(dA); (void)hipFree(du); (void)hipFree(dx0); (void)hipFree(dX); (void)hipFree(dL); (void)hipFree(dcoef);
+  (void)hipFree(dJ); (void)hipFree(dsink); (void)hipFree(dbrow); (void)hipFree(dterms); (void)hipFree(drec);
+}
+
+int main(int argc, char** argv) {
+  const int NB = argc > 1 ? atoi(argv[1]) : 2;
+  const int B = argc > 2 ? atoi(argv[2]) : (NB == 2 ? 256 : 512);
+  const int Nt = argc > 3 ? atoi(argv[3]) : (NB == 2 ? 1000 : 500);
+  const int nblk = NB == 2 ? 20 : 3, m = NB == 2 ? 2 : 4;
+  for (int mode = 0; mode < 3; ++mode)
+    for (int W : {2, 3, 4, 5})
+      for (int C : {8, 16, 32, 64}) {
+        if (NB == 2) run<2>(B, Nt, nblk, m, W, C, mode);
+        else run<3>(B, Nt, nblk, m, W, C, mode);
+      }
+  return 0;
+}
