@@ -42,7 +42,9 @@ struct BlkuParams {
   int Ntp;                         // slices per seed in the record array: Nt rounded up to 64
   const double* rec;               // B x Ntp x BLKU_REC step records (k_blku_rec)
   unsigned long long* terms;       // Σ_k P_k 2^J_k per forward pass (k_blku_rec; nullptr: not counted)
-  int probe_mode;                  // QOC_PROBE builds only: 1 skip the formation, 2 skip the chain
+  double* dJdu;                    // B x Nt x nu: the fused backward's gradient (k_blku_bwdg)
+  int probe_mode;                  // QOC_PROBE builds only: 1 skip the formation, 2 the chain, 3 the chain's stores,
+                                   // 4 the chain's LDS reads
 };
 
 // Diagnostic cycle stamps (tools/blku_probe.hip builds with -DQOC_PROBE; empty otherwise): per-role segment times of
@@ -88,18 +90,43 @@ constexpr BlkuCoef blku_coef() {
   return c;
 }
 
-// LDS of one workgroup, in doubles: 1/t | generator blocks [3][NB^2][nblk] complex | step records [3][C][REC] |
+// LDS of one workgroup, in doubles: 1/t | generator blocks [3][NB^2][nblk] complex | step records [4][C][REC] |
 // block propagators [2][C][NB^2][nblk] complex | x_N (2 N m) | reduction (16)
 __host__ __device__ inline size_t blku_off_gb() { return BLKU_INVT; }
 __host__ __device__ inline size_t blku_off_rec(int NB, int nblk) { return blku_off_gb() + (size_t)6 * NB * NB * nblk; }
 __host__ __device__ inline size_t blku_off_U(int NB, int nblk, int C) {
-  return blku_off_rec(NB, nblk) + (size_t)3 * BLKU_REC * C;
+  return blku_off_rec(NB, nblk) + (size_t)4 * BLKU_REC * C;
 }
 __host__ __device__ inline size_t blku_off_xN(int NB, int nblk, int C) {
   return blku_off_U(NB, nblk, C) + (size_t)4 * C * NB * NB * nblk;
 }
-__host__ __device__ inline size_t blku_lds(int N, int m, int NB, int nblk, int C) {
-  return (blku_off_xN(NB, nblk, C) + 2 * (size_t)N * m + 16) * sizeof(double);
+// the fused backward (k_blku_bwdg) adds: the co-state ring [2][C][N m] complex (λ_{k+1} of each slice of the last
+// two chunks, written by the chain waves) | unshifted generator blocks [3][NB^2][nblk] complex
+__host__ __device__ inline size_t blku_off_lam(int N, int m, int NB, int nblk, int C) {
+  return blku_off_xN(NB, nblk, C) + 2 * (size_t)N * m + 16;
+}
+__host__ __device__ inline size_t blku_off_ga(int N, int m, int NB, int nblk, int C) {
+  return blku_off_lam(N, m, NB, nblk, C) + (size_t)4 * C * N * m;
+}
+__host__ __device__ inline size_t blku_off_xs(int N, int m, int NB, int nblk, int C) {
+  return blku_off_ga(N, m, NB, nblk, C) + (size_t)6 * NB * NB * nblk;
+}
+// | x_k of the last two chunks [2][CNp] complex (CNp = C N m rounded up to 64: whole wave-instructions of LDS-DMA)
+__host__ __device__ inline int blku_cnp(int N, int m, int C) { return (C * N * m + 63) / 64 * 64; }
+// bytes; gw: worker waves of the fused backward (0: the kernels without the gradient)
+__host__ __device__ inline size_t blku_lds(int N, int m, int NB, int nblk, int C, int gw = 0) {
+  if (gw > 0) return (blku_off_xs(N, m, NB, nblk, C) + (size_t)4 * blku_cnp(N, m, C)) * sizeof(double);
+  return blku_off_lam(N, m, NB, nblk, C) * sizeof(double);
+}
+
+// DPP move of a double whose every source lane is valid (quad permutations), or whose invalid-source lanes are never
+// read (row shifts in blku_scan): no old value to preserve, so no zero-initialised destination
+template <int CTRL>
+__device__ __forceinline__ double dpp_any(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)u, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 __device__ __forceinline__ int wave_max(int v) {
@@ -153,9 +180,15 @@ __global__ __launch_bounds__(256) void k_blku_rec(const BlkuParams bp, const dou
     r[2] = make_double2(sc * u2, (double)P);
     r[3] = make_double2((double)J, 0.0);
   }
-  if (bp.terms) {
+  if (bp.terms) {  // one atomic per workgroup (one per wave serialises thousands of them on one address)
+    __shared__ unsigned long long part[4];
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(bp.terms, cnt);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long tot = part[0] + part[1] + part[2] + part[3];
+      if (tot) atomicAdd(bp.terms, tot);
+    }
   }
 }
 
@@ -341,15 +374,14 @@ __device__ __forceinline__ void blku_taylor(const double (&ar)[NU][NB * NB], con
   }
 }
 
-// NU block propagators U_k^β = e^{μ_k} (p(Ã_k / 2^J))^{2^J} at once (units u: block beta[u] of the slice whose step
-// record is rec[u]; the chunk's P and J are uniform); gb: generator blocks [3][NB^2][nblk] complex (entries of Ã_j at
-// the block's rows), out[u]: U at entry stride nblk, written when st[u].  With J > 0 the phase is applied before the
-// squarings as e^{μ / 2^J}, i.e. it is taken from the record only when J = 0 (J > 0: the squarings of the
-// phase-free polynomial, then e^{μ}).
+// NU block propagators U_k^β = e^{μ_k} (p(Ã_k / 2^J))^{2^J} at once into registers (unit u: block beta[u] of the
+// slice whose step record is rec[u]; the chunk's P and J are uniform); gb: generator blocks [3][NB^2][nblk] complex
+// (entries of Ã_j at the block's rows).  With J > 0 the squarings run on the phase-free polynomial and e^{μ} multiplies
+// after them.
 template <int NB, int NU>
 __device__ __forceinline__ void blku_form(const double2* __restrict__ gb, int nblk, const int (&beta)[NU],
                                           const double* const (&rec)[NU], const double* __restrict__ invt,
-                                          double2* const (&out)[NU], const bool (&st)[NU]) {
+                                          double (&ur)[NU][NB * NB], double (&ui)[NU][NB * NB]) {
   constexpr int E = NB * NB;
   const int P = __builtin_amdgcn_readfirstlane((int)rec[0][5]), J = __builtin_amdgcn_readfirstlane((int)rec[0][6]);
   double ar[NU][E], ai[NU][E], pr[NU], pi[NU];
@@ -366,7 +398,6 @@ __device__ __forceinline__ void blku_form(const double2* __restrict__ gb, int nb
       ai[u][e] = fma(s2, g2.y, fma(s1, g1.y, s0 * g0.y));
     }
   }
-  double ur[NU][E], ui[NU][E];
   blku_taylor<NB, NU>(ar, ai, P, pr, pi, invt, ur, ui);
   if (J) {
     for (int q = 0; q < J; ++q)
@@ -383,11 +414,50 @@ __device__ __forceinline__ void blku_form(const double2* __restrict__ gb, int nb
       }
     }
   }
+}
+
+// c = a b (NB x NB complex, row-major)
+template <int NB>
+__device__ __forceinline__ void blku_mm(const double (&ar)[NB * NB], const double (&ai)[NB * NB],
+                                        const double (&br)[NB * NB], const double (&bi)[NB * NB], double (&cr)[NB * NB],
+                                        double (&ci)[NB * NB]) {
 #pragma unroll
-  for (int u = 0; u < NU; ++u)
-    if (st[u])
+  for (int i = 0; i < NB; ++i)
 #pragma unroll
-      for (int e = 0; e < E; ++e) out[u][e * nblk] = make_double2(ur[u][e], ui[u][e]);
+    for (int k = 0; k < NB; ++k) {
+      double sr = 0.0, si = 0.0;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        sr = fma(ar[i * NB + q], br[q * NB + k], fma(-ai[i * NB + q], bi[q * NB + k], sr));
+        si = fma(ar[i * NB + q], bi[q * NB + k], fma(ai[i * NB + q], br[q * NB + k], si));
+      }
+      cr[i * NB + k] = sr;
+      ci[i * NB + k] = si;
+    }
+}
+
+// Inclusive prefix products over the S lanes of a group (lane jl of the group holds T_jl on entry, Q_jl after):
+// forward Q_j = T_j Q_{j-1}, backward Q_j = Q_{j-1} T_j.  Lane jl takes lane jl - d's product by a DPP row shift.
+template <int NB, int S, bool FWD, int D = 1>
+__device__ __forceinline__ void blku_scan(double (&ur)[NB * NB], double (&ui)[NB * NB], int jl) {
+  if constexpr (D < S) {
+    constexpr int E = NB * NB;
+    double vr[E], vi[E], cr[E], ci[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      vr[e] = dpp_any<0x110 + D>(ur[e]);  // row_shr:D
+      vi[e] = dpp_any<0x110 + D>(ui[e]);
+    }
+    if (FWD) blku_mm<NB>(ur, ui, vr, vi, cr, ci);
+    else blku_mm<NB>(vr, vi, ur, ui, cr, ci);
+    const bool take = jl >= D;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      ur[e] = take ? cr[e] : ur[e];
+      ui[e] = take ? ci[e] : ui[e];
+    }
+    blku_scan<NB, S, FWD, 2 * D>(ur, ui, jl);
+  }
 }
 
 // y = U x (FWD) or U^H x on one block (U row-major complex from LDS, entries at stride nblk)
@@ -411,12 +481,126 @@ __device__ __forceinline__ void blku_apply(const double2 (&U)[NB * NB], const do
   }
 }
 
+// nblk rounded up to a power of two: a gradient unit's blocks sit on NBP adjacent lanes (lanes >= nblk of the group
+// idle), so the sum over blocks is a butterfly within the group
+__host__ __device__ inline int blku_nbp(int nblk) {
+  int p = 1;
+  while (p < nblk) p <<= 1;
+  return p;
+}
+__device__ __forceinline__ double blku_group_sum(double v, int nbp) {
+  for (int o = nbp >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Gradient of one (slice, block) unit (expm_jacobian! + _compute_u_sensitivity, src/gradient_computations.jl:177-223)
+// as one trace per generator: with X = A_k on the block and K = Σ_cols x_k λ_{k+1}^H (NB x NB),
+//   Σ_cols λ^H dU_j x = tr(dU_j K) = tr(A_j M),  M = Σ_{a+b<ORD} X^b K X^a / (a+b+1)! = Σ_n L_n / (n+1)!,
+//   L_0 = R_0 = K, L_n = X L_{n-1} + R_n, R_n = R_{n-1} X
+// (dU_j = Σ_{a+b<ORD} X^a A_j X^b / (a+b+1)!, the reference's Taylor terms).
+// K += x λ^H from one column's rows (K[p][q] = Σ_c x_c[p] conj(λ_c[q]))
+template <int NB>
+__device__ __forceinline__ void blku_kacc(double (&kr)[NB * NB], double (&ki)[NB * NB], const double2 (&xv)[NB],
+                                          const double2 (&lv)[NB]) {
+#pragma unroll
+  for (int p = 0; p < NB; ++p)
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {  // x_p conj(λ_q)
+      kr[p * NB + q] = fma(xv[p].x, lv[q].x, fma(xv[p].y, lv[q].y, kr[p * NB + q]));
+      ki[p * NB + q] = fma(xv[p].y, lv[q].x, fma(-xv[p].x, lv[q].y, ki[p * NB + q]));
+    }
+}
+// Re tr(A_j M) for j = 1, 2 from K and u_k; G0..G2: the unit's block of the unshifted generators A_0..A_2
+// (row-major entries at stride nblk)
+template <int NB, int ORD>
+__device__ __forceinline__ void blku_contract(const double2* G0, const double2* G1, const double2* G2, int nblk,
+                                              const double (&kr)[NB * NB], const double (&ki)[NB * NB], double u1,
+                                              double u2, double& acc1, double& acc2) {
+  constexpr int E = NB * NB;
+  constexpr double invf[6] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120};
+  // X = A_0 + u_1 A_1 + u_2 A_2
+  double xr_[E], xi_[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const double2 a0 = G0[e * nblk], a1 = G1[e * nblk], a2 = G2[e * nblk];
+    xr_[e] = fma(u2, a2.x, fma(u1, a1.x, a0.x));
+    xi_[e] = fma(u2, a2.y, fma(u1, a1.y, a0.y));
+  }
+  // M = K + Σ_{n>=1} L_n / (n+1)!,  L_n = X L_{n-1} + R_n,  R_n = R_{n-1} X  (L_0 = R_0 = K)
+  double Mr[E], Mi[E], Lr[E], Li[E], Rr[E], Ri[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    Mr[e] = Lr[e] = Rr[e] = kr[e];
+    Mi[e] = Li[e] = Ri[e] = ki[e];
+  }
+  // in place: row i of R X needs only row i of R, column k of X L + R only column k of L (the same sums, in the
+  // same order, as with separate product matrices: a third fewer live registers)
+#pragma unroll
+  for (int n = 1; n < ORD; ++n) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {  // R_n = R_{n-1} X
+      double tr[NB], ti[NB];
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk) {
+        double sr = 0.0, si = 0.0;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          sr = fma(Rr[i * NB + q], xr_[q * NB + kk], fma(-Ri[i * NB + q], xi_[q * NB + kk], sr));
+          si = fma(Rr[i * NB + q], xi_[q * NB + kk], fma(Ri[i * NB + q], xr_[q * NB + kk], si));
+        }
+        tr[kk] = sr;
+        ti[kk] = si;
+      }
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk) {
+        Rr[i * NB + kk] = tr[kk];
+        Ri[i * NB + kk] = ti[kk];
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < NB; ++kk) {  // L_n = X L_{n-1} + R_n
+      double tr[NB], ti[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        double sr = Rr[i * NB + kk], si = Ri[i * NB + kk];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          sr = fma(xr_[i * NB + q], Lr[q * NB + kk], fma(-xi_[i * NB + q], Li[q * NB + kk], sr));
+          si = fma(xr_[i * NB + q], Li[q * NB + kk], fma(xi_[i * NB + q], Lr[q * NB + kk], si));
+        }
+        tr[i] = sr;
+        ti[i] = si;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        Lr[i * NB + kk] = tr[i];
+        Li[i * NB + kk] = ti[i];
+        Mr[i * NB + kk] = fma(invf[n + 1], tr[i], Mr[i * NB + kk]);
+        Mi[i * NB + kk] = fma(invf[n + 1], ti[i], Mi[i * NB + kk]);
+      }
+    }
+  }
+  // Re tr(A_j M) = Re Σ_{i,q} A_j[i][q] M[q][i]
+  acc1 = acc2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const double2 a1 = G1[(i * NB + q) * nblk], a2 = G2[(i * NB + q) * nblk];
+      acc1 = fma(a1.x, Mr[q * NB + i], fma(-a1.y, Mi[q * NB + i], acc1));
+      acc2 = fma(a2.x, Mr[q * NB + i], fma(-a2.y, Mi[q * NB + i], acc2));
+    }
+}
+
 // One workgroup per (seed, direction): FWD x_0 -> x_Nt (+ costs), else λ_Nt -> λ_0 (μ mode: X_target -> μ_0).
 // ADD (backward, non-μ): 2μ x_k on the penalty mask and the caller's dL/dx(x_k) are added to λ_k after each slice
 // (the only variant whose chain loop reads global memory).  Chunks lie on the absolute slice grid [aC, aC + C), the
 // forward pass taking a = 0, 1, .., the backward pass a = nC - 1, .., 0 (its first chunk may be partial), so that a
 // chunk never straddles two of k_blku_rec's 64-slice (J, P) groups.
-template <int NB, bool FWD, bool ADD>
+// GORD > 0 (backward, non-μ, no additions): the fused gradient of order GORD.  The chain writes λ_{k+1} of every slice
+// into an LDS ring instead of HBM, and the worker waves, besides forming the next chunk's propagators, contract the
+// previous chunk's slices with x_k from HBM (blku_contract): the co-states never leave the workgroup.
+template <int NB, int S, bool FWD, bool ADD, int GORD = 0>
 __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk, const BlkuParams& bp, const int b,
                                           const int mu_mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -444,12 +628,26 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       gb[q] = make_double2(v.r, v.i);
     }
   }
+  static_assert(GORD == 0 || (!FWD && !ADD), "the fused gradient runs on the plain backward chain");
+  double2* const lam = reinterpret_cast<double2*>(lds + blku_off_lam(N, m, NB, nblk, C));
+  double2* const ga = reinterpret_cast<double2*>(lds + blku_off_ga(N, m, NB, nblk, C));
+  if constexpr (GORD > 0) {  // the unshifted generator blocks A_j for the gradient
+    const cx<double>* A = (const cx<double>*)bk.A;
+    const size_t NN = (size_t)N * N;
+    for (int q = tid; q < 3 * E * nblk; q += nthr) {
+      const int j = q / (E * nblk), r = q - j * E * nblk, e = r / nblk, beta = r - e * nblk;
+      const int ri = bk.brow[beta * NB + e / NB], rk = bk.brow[beta * NB + e % NB];
+      cx<double> v = {0.0, 0.0};
+      if (j <= nu && ri >= 0 && rk >= 0) v = A[(size_t)j * NN + ri + (size_t)N * rk];
+      ga[q] = make_double2(v.r, v.i);
+    }
+  }
   const int nC = (Nt + C - 1) / C;
   auto chunk_of = [&](int c) { return FWD ? c : nC - 1 - c; };  // absolute chunk of sequence position c
   const bool chain = w < bp.CW;
   const int fl = tid - 64 * bp.CW, FL = nthr - 64 * bp.CW;  // formation lanes
   // step records of sequence chunk c: C x REC doubles from k_blku_rec (the tail of a partial chunk: clamped reads,
-  // never used), through registers into the LDS ring slot c % 3
+  // never used), through registers into the LDS ring slot c & 3
   constexpr int RMAX = 8;  // loads per lane: 64 x REC doubles / 64 lanes at most
   double rr[RMAX];
   const double* recb = bp.rec + (size_t)b * bp.Ntp * BLKU_REC;
@@ -462,44 +660,132 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
     }
   };
   auto rec_store = [&](int c) {
-    double* dst = recs + (size_t)(c % 3) * C * BLKU_REC;
+    double* dst = recs + (size_t)(c & 3) * C * BLKU_REC;
 #pragma unroll
     for (int i = 0; i < RMAX; ++i) {
       const int e = fl + i * FL;
       if (e < C * BLKU_REC) dst[e] = rr[i];
     }
   };
-  // the chunk's C nblk propagators, NU per lane at a time (units q, q + FL, ..: independent recurrences interleaved)
+  // sequence position s_ (0 .. jn-1, the chain's order) -> chunk position: forward s_, backward jn - 1 - s_
+  auto posn = [&](int s_, int jn) { return FWD ? s_ : jn - 1 - s_; };
+  // the chunk's propagators, folded into prefix products over groups of S consecutive sequence positions:
+  // position lo + j of a group holds Q_j = T_{lo+j} .. T_lo (T = U forward; backward Q_j^H = U_{lo+j}^H .. U_lo^H, so
+  // Q_j = U_lo .. U_{lo+j}), and the chain applies Q_j to the group's incoming state for every j: S independent
+  // matvecs per group instead of S dependent ones.  A unit is one (position, block); the S units of a group sit on S
+  // adjacent lanes (S | 16: one DPP row) and scan by row shifts (Hillis-Steele, log2 S block products).  NU units per
+  // lane at a time, at stride FL (independent recurrences interleaved).
   constexpr int NU = QOC_BLKU_NU(NB);
   auto form = [&](int c) {
-    const int a = chunk_of(c), jn = min(C, Nt - a * C), units = jn * nblk;
-    const double* rc = recs + (size_t)(c % 3) * C * BLKU_REC;
+    const int a = chunk_of(c), jn = min(C, Nt - a * C), units = (jn + S - 1) / S * S * nblk;
+    const double* rc = recs + (size_t)(c & 3) * C * BLKU_REC;
     double2* Uc = Ub + (size_t)(c & 1) * C * E * nblk;
     for (int q = fl; q < units; q += NU * FL) {
-      int be[NU];
+      int be[NU], pp[NU], jl[NU];
       const double* rp[NU];
-      double2* op[NU];
       bool st[NU];
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const int qu = q + u * FL;
-        st[u] = qu < units;
-        const int qq = st[u] ? qu : q, jj = qq / nblk;
-        be[u] = qq - jj * nblk;
-        rp[u] = rc + (size_t)jj * BLKU_REC;
-        op[u] = Uc + (size_t)jj * E * nblk + be[u];
+        const int qq = qu < units ? qu : q, t = qq / S, gq = t / nblk;
+        jl[u] = qq - t * S;
+        be[u] = t - gq * nblk;
+        const int s_ = gq * S + jl[u];
+        st[u] = qu < units && s_ < jn;
+        pp[u] = posn(min(s_, jn - 1), jn);
+        rp[u] = rc + (size_t)pp[u] * BLKU_REC;
       }
-      blku_form<NB, NU>(gb, nblk, be, rp, invt, op, st);
+      double ur[NU][E], ui[NU][E];
+      blku_form<NB, NU>(gb, nblk, be, rp, invt, ur, ui);
+      if constexpr (S > 1) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) blku_scan<NB, S, FWD>(ur[u], ui[u], jl[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        if (st[u]) {
+          double2* o = Uc + (size_t)pp[u] * E * nblk + be[u];
+#pragma unroll
+          for (int e = 0; e < E; ++e) o[e * nblk] = make_double2(ur[u][e], ui[u][e]);
+        }
     }
   };
-  // chain lanes: lane l < nblk m owns block l % nblk of column l / nblk
-  BlkLane<NB> ln;
-  ln.setup(bk, m, chain ? tid : 1 << 30);
-  const int beta = chain && tid < nblk * m ? tid % nblk : 0;
+  // x_k of sequence chunk cq (GORD > 0) into the x ring slot cq & 1 by LDS-DMA (global_load_lds_dwordx4, 16 bytes a
+  // lane): the chunk's jn N m complex are contiguous in HBM; lanes past them reload element 0 into the slot's tail
+  const int CNp = blku_cnp(N, m, C);
+  double2* const xring = reinterpret_cast<double2*>(lds + blku_off_xs(N, m, NB, nblk, C));
+  auto xs_issue = [&](int cq) {
+    if constexpr (GORD > 0) {
+      const int a = chunk_of(cq), n = min(C, Nt - a * C) * (int)Nm;
+      const double2* src = reinterpret_cast<const double2*>((const cx<double>*)g.X + ((size_t)b * (Nt + 1) + (size_t)a * C) * Nm);
+      double2* dst = xring + (size_t)(cq & 1) * CNp;
+      for (int e0 = (w - bp.CW) * 64; e0 < n; e0 += FL) {
+        const int e = e0 + (tid & 63);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + (e < n ? e : 0)),
+                                         (__attribute__((address_space(3))) void*)(dst + e0), 16, 0, 0);
+      }
+    }
+  };
+  // the fused gradient of sequence chunk cq (GORD > 0): the worker waves take 64 / nblk slices per wave-iteration, a
+  // lane per (slice, block); K = Σ_c x_k λ_{k+1}^H from x_k in HBM and λ_{k+1} in the ring slot cq & 1, then
+  // Re tr(A_j M) reduced over the blocks through the wave's LDS slot in a fixed order
+  auto grad = [&](int cq) {
+    if constexpr (GORD > 0) {
+      const int a = chunk_of(cq), jn = min(C, Nt - a * C), gw = w - bp.CW, GW = (nthr >> 6) - bp.CW;
+      const int l = tid & 63, NBP = blku_nbp(nblk), UPW = 64 / NBP, ul = l / NBP, be = l - ul * NBP;
+      const int bc = min(be, nblk - 1);
+      const double2* lr = lam + (size_t)(cq & 1) * C * Nm;
+      const double2* xq = xring + (size_t)(cq & 1) * CNp;
+      const double* rq = recs + (size_t)(cq & 3) * C * BLKU_REC;
+      int r[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) r[i] = be < nblk ? bk.brow[be * NB + i] : -1;
+      for (int it = gw; it * UPW < jn; it += GW) {
+        const int jj = it * UPW + ul;
+        const bool act = be < nblk && jj < jn;
+        const int jc = jj < jn ? jj : 0;
+        // u_k from the step record (2^-J u_j scaled back by 2^J: exact), x_k from the x ring, λ_{k+1} from the λ ring
+        const double* rk = rq + (size_t)jc * BLKU_REC;
+        const int Jk = (int)rk[6];
+        const double u1 = ldexp(rk[3], Jk), u2 = ldexp(rk[4], Jk);
+        const double2* xs = xq + (size_t)jc * Nm;
+        const double2* ls = lr + (size_t)jc * Nm;
+        double kr[E], ki[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) kr[e] = ki[e] = 0.0;
+        for (int c = 0; c < m; ++c) {
+          double2 xv[NB], lv[NB];
+#pragma unroll
+          for (int i = 0; i < NB; ++i) {
+            const int o = c * N + max(r[i], 0);
+            xv[i] = r[i] >= 0 ? xs[o] : make_double2(0.0, 0.0);
+            lv[i] = r[i] >= 0 ? ls[o] : make_double2(0.0, 0.0);
+          }
+          blku_kacc<NB>(kr, ki, xv, lv);
+        }
+        double acc1, acc2;
+        blku_contract<NB, GORD>(ga + bc, ga + E * nblk + bc, ga + 2 * E * nblk + bc, nblk, kr, ki, u1, u2, acc1, acc2);
+        acc1 = blku_group_sum(act ? acc1 : 0.0, NBP);
+        acc2 = blku_group_sum(act ? acc2 : 0.0, NBP);
+        if (be == 0 && jj < jn) {
+          double* o = bp.dJdu + ((size_t)b * Nt + a * C + jj) * nu;
+          o[0] = acc1;
+          if (nu > 1) o[1] = acc2;
+        }
+      }
+    }
+  };
+  // chain lanes, one state element each: the SL lanes of group p = l / SL own rows i = l % SL < NB of block p % nblk
+  // in column p / nblk (SL = 2 for blocks of 2 rows, else 4: a DPP quad; lanes i >= NB idle).  Each slice a lane
+  // gathers its block's column from the group by DPP broadcasts and forms its row of U x (U^H x backward).
+  constexpr int SL = NB == 2 ? 2 : 4;
+  const int pq = tid / SL, ri = tid - pq * SL;
+  const bool cact = chain && pq < nblk * m && ri < NB;
+  const int beta = cact ? pq % nblk : 0, col = cact ? pq / nblk : 0, rr_ = min(ri, NB - 1);
+  const int row = cact ? bk.brow[beta * NB + ri] : -1;
+  const bool ok = row >= 0;
   double* const sink = tchain_sink(g);
-  double xr[NB], xi[NB];
-  size_t off[NB];
-  bool pm[NB];
+  const size_t off = 2 * ((size_t)col * N + max(row, 0));
   double pen = 0.0;
   double* Sb = reinterpret_cast<double*>((cx<double>*)(FWD ? g.X : g.L) + (size_t)b * (Nt + 1) * Nm);
   const double* Xb = reinterpret_cast<const double*>((const cx<double>*)g.X + (size_t)b * (Nt + 1) * Nm);
@@ -508,45 +794,38 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   const unsigned char* pmask = (FWD || !mu_mode) ? g.pmask : nullptr;
   const double tmu = 2.0 * g.mu;
   const bool penon = pmask != nullptr;
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const bool ok = ln.r[i] >= 0;
-    const size_t o = (size_t)ln.c * N + max(ln.r[i], 0);
-    off[i] = 2 * o;
-    pm[i] = ok && pmask && pmask[o];
-    cx<double> v = {0.0, 0.0};
-    if (ok) {
-      if (FWD) {
-        v = ((const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0))[o];
-      } else if (mu_mode) {
-        v = ((const cx<double>*)g.Xt)[o];
+  const bool pm = ok && pmask && pmask[off / 2];
+  double xr = 0.0, xi = 0.0;
+  if (ok) {
+    const size_t o = off / 2;
+    cx<double> v;
+    if (FWD) {
+      v = ((const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0))[o];
+    } else if (mu_mode) {
+      v = ((const cx<double>*)g.Xt)[o];
+    } else {
+      if (g.cost_kind == COST_EXTERNAL) {
+        v = reinterpret_cast<const cx<double>*>(Sb)[(size_t)Nt * Nm + o];
       } else {
-        if (g.cost_kind == COST_EXTERNAL) {
-          v = reinterpret_cast<const cx<double>*>(Sb)[(size_t)Nt * Nm + o];
-        } else {
-          const cx<double> cf = g.coef[(size_t)b * 2 * m + ln.c], t = ((const cx<double>*)g.Xt)[o];
-          v = cx<double>{cf.r * t.r - cf.i * t.i, cf.r * t.i + cf.i * t.r};
-        }
-        if (pm[i]) {
-          v.r += tmu * Xb[(size_t)Nt * 2 * Nm + 2 * o];
-          v.i += tmu * Xb[(size_t)Nt * 2 * Nm + 2 * o + 1];
-        }
-        if (srcb) {
-          v.r += srcb[(size_t)Nt * 2 * Nm + 2 * o];
-          v.i += srcb[(size_t)Nt * 2 * Nm + 2 * o + 1];
-        }
+        const cx<double> cf = g.coef[(size_t)b * 2 * m + col], t = ((const cx<double>*)g.Xt)[o];
+        v = cx<double>{cf.r * t.r - cf.i * t.i, cf.r * t.i + cf.i * t.r};
+      }
+      if (pm) {
+        v.r += tmu * Xb[(size_t)Nt * 2 * Nm + off];
+        v.i += tmu * Xb[(size_t)Nt * 2 * Nm + off + 1];
+      }
+      if (srcb) {
+        v.r += srcb[(size_t)Nt * 2 * Nm + off];
+        v.i += srcb[(size_t)Nt * 2 * Nm + off + 1];
       }
     }
-    xr[i] = v.r;
-    xi[i] = v.i;
+    xr = v.r;
+    xi = v.i;
   }
-  if (chain) {  // the first state (x_0 / λ_Nt)
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      double* p = ln.r[i] >= 0 ? Sb + (size_t)(FWD ? 0 : Nt) * 2 * Nm + off[i] : sink;
-      *reinterpret_cast<double2*>(p) = make_double2(xr[i], xi[i]);
-      if (FWD && penon) pen += pm[i] ? xr[i] * xr[i] + xi[i] * xi[i] : 0.0;
-    }
+  if (chain && GORD == 0) {  // the first state (x_0 / λ_Nt)
+    double* p = ok ? Sb + (size_t)(FWD ? 0 : Nt) * 2 * Nm + off : sink;
+    *reinterpret_cast<double2*>(p) = make_double2(xr, xi);
+    if (FWD && penon) pen += pm ? xr * xr + xi * xi : 0.0;
   }
   // prologue: records of sequence chunks 0 and 1 in LDS, chunk 2's in flight, propagators of chunk 0
   if (!chain) {
@@ -562,15 +841,13 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   if (!chain) form(0);
   lds_barrier();
   if (chain) {
-    // state of each row: a running pointer (padding rows go to the sink with stride 0: no branch around the stores)
-    double* sp[NB];
-    long long sst[NB];
+    // the state element's running pointer (lanes without one go to the sink with stride 0: no branch around stores)
+    double* sp = ok ? Sb + (FWD ? 2 * Nm : (size_t)(Nt - 1) * 2 * Nm) + off : sink;
+    const long long sst = ok ? (FWD ? 2 * (long long)Nm : -2 * (long long)Nm) : 0;
+    // this lane's row of U (U^H backward: the conjugated column) at entry stride nblk
+    int eo[NB];
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const bool ok = ln.r[i] >= 0;
-      sp[i] = ok ? Sb + (FWD ? 2 * Nm : (size_t)(Nt - 1) * 2 * Nm) + off[i] : sink;
-      sst[i] = ok ? (FWD ? 2 * (long long)Nm : -2 * (long long)Nm) : 0;
-    }
+    for (int q = 0; q < NB; ++q) eo[q] = (FWD ? rr_ * NB + q : q * NB + rr_) * nblk;
     for (int c = 0; c < nC; ++c) {
       BK_T(t0);
 #ifdef QOC_PROBE
@@ -578,55 +855,106 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
 #else
       {
 #endif
-        const int a = chunk_of(c), jn = min(C, Nt - a * C);
+        const int a = chunk_of(c), jn = min(C, Nt - a * C), ng = (jn + S - 1) / S;
         const double2* Uc = Ub + (size_t)(c & 1) * C * E * nblk + beta;
-        // one slice (chunk position jj): y = U x (U^H backward), the additions of the non-μ backward, the store
-        auto slice = [&](const double2(&U)[E], int jj) __attribute__((always_inline)) {
-          double ar_[NB], ai_[NB];
-          if constexpr (ADD) {  // 2μ x_k on the mask + the caller's dL/dx(x_k), added after the slice
-            const int k = a * C + jj;
+        double2* const lr = lam + (size_t)(c & 1) * C * Nm + (off >> 1);  // GORD: this element's ring entries
+        // this lane's rows of the group's S prefix products (clamped past the chunk's end: never used)
+        auto ldq = [&](double2(&Q)[S][NB], int gq) __attribute__((always_inline)) {
 #pragma unroll
-            for (int i = 0; i < NB; ++i) {
-              const size_t o = (size_t)k * 2 * Nm + off[i];
-              ar_[i] = pm[i] ? tmu * Xb[o] : 0.0;
-              ai_[i] = pm[i] ? tmu * Xb[o + 1] : 0.0;
-              if (srcb && ln.r[i] >= 0) {
-                ar_[i] += srcb[o];
-                ai_[i] += srcb[o + 1];
-              }
-            }
-          }
-          double yr[NB], yi[NB];
-          blku_apply<NB, FWD>(U, xr, xi, yr, yi);  // padding rows stay 0: U is diagonal there and x is 0
+          for (int j = 0; j < S; ++j) {
+            const size_t o = (size_t)posn(min(gq * S + j, jn - 1), jn) * E * nblk;
 #pragma unroll
-          for (int i = 0; i < NB; ++i) {
-            xr[i] = yr[i];
-            xi[i] = yi[i];
-            if constexpr (ADD) {
-              xr[i] += ar_[i];
-              xi[i] += ai_[i];
-            }
-            *reinterpret_cast<double2*>(sp[i]) = make_double2(xr[i], xi[i]);
-            sp[i] += sst[i];
-            if (FWD && penon) pen += pm[i] ? xr[i] * xr[i] + xi[i] * xi[i] : 0.0;  // uniform branch
+            for (int q = 0; q < NB; ++q) Q[j][q] = Uc[o + eo[q]];
           }
         };
-        // two slices per iteration with the roles of the two U register sets swapped (no register copies); the next
-        // slice's U is read from LDS before this slice's matvec.  Forward: jj = 0 .. jn-1; backward: jn-1 .. 0
-        auto pos = [&](int s) { return FWD ? s : jn - 1 - s; };
-        double2 U0[E], U1[E];
+        // one group (ns <= S positions): gather the block's column of the incoming state, y_j = Q_j x for every j
+        // (independent), the additions of the non-μ backward (S = 1), the stores; the state carries on as y_{ns-1}
+        auto group = [&](const double2(&Q)[S][NB], int gq) __attribute__((always_inline)) {
+          const int ns = min(S, jn - gq * S);
+          double ar_ = 0.0, ai_ = 0.0;
+          if constexpr (ADD) {  // 2μ x_k on the mask + the caller's dL/dx(x_k), added after the slice
+            const size_t o = (size_t)(a * C + posn(gq, jn)) * 2 * Nm + off;
+            ar_ = pm ? tmu * Xb[o] : 0.0;
+            ai_ = pm ? tmu * Xb[o + 1] : 0.0;
+            if (srcb && ok) {
+              ar_ += srcb[o];
+              ai_ += srcb[o + 1];
+            }
+          }
+          double gr[NB], gi[NB];
+          if constexpr (SL == 2) {
+            gr[0] = dpp_any<0xA0>(xr);  // quad_perm [0,0,2,2]: row 0 of the pair
+            gi[0] = dpp_any<0xA0>(xi);
+            gr[1] = dpp_any<0xF5>(xr);  // quad_perm [1,1,3,3]: row 1
+            gi[1] = dpp_any<0xF5>(xi);
+          } else {
+            gr[0] = dpp_any<0x00>(xr);  // quad_perm [q,q,q,q]
+            gi[0] = dpp_any<0x00>(xi);
+            gr[1] = dpp_any<0x55>(xr);
+            gi[1] = dpp_any<0x55>(xi);
+            gr[2] = dpp_any<0xAA>(xr);
+            gi[2] = dpp_any<0xAA>(xi);
+            if constexpr (NB == 4) {
+              gr[3] = dpp_any<0xFF>(xr);
+              gi[3] = dpp_any<0xFF>(xi);
+            }
+          }
+          double yr[S], yi[S];
 #pragma unroll
-        for (int e = 0; e < E; ++e) U0[e] = Uc[(size_t)pos(0) * E * nblk + e * nblk];
-        for (int s = 0; s < jn; s += 2) {
-          const size_t o1 = (size_t)pos(min(s + 1, jn - 1)) * E * nblk;
+          for (int j = 0; j < S; ++j) {
+            double sr = 0.0, si = 0.0;
 #pragma unroll
-          for (int e = 0; e < E; ++e) U1[e] = Uc[o1 + e * nblk];
-          slice(U0, pos(s));
-          if (s + 1 >= jn) break;
-          const size_t o2 = (size_t)pos(min(s + 2, jn - 1)) * E * nblk;
+            for (int q = 0; q < NB; ++q) {
+              const double uim = FWD ? Q[j][q].y : -Q[j][q].y;  // conj for Q^H
+              sr = fma(Q[j][q].x, gr[q], sr);
+              sr = fma(-uim, gi[q], sr);
+              si = fma(Q[j][q].x, gi[q], si);
+              si = fma(uim, gr[q], si);
+            }
+            yr[j] = sr;  // padding rows stay 0: Q is diagonal there and x is 0
+            yi[j] = si;
+          }
+          if constexpr (ADD) {
+            yr[0] += ar_;
+            yi[0] += ai_;
+          }
+          if constexpr (GORD > 0) {  // λ_{k+1} of each slice k of the group into the ring (the group's incoming state
+                                     // for its first slice)
 #pragma unroll
-          for (int e = 0; e < E; ++e) U0[e] = Uc[o2 + e * nblk];
-          slice(U1, pos(s + 1));
+            for (int j = 0; j < S; ++j)
+              if (j < ns && ok) lr[(size_t)posn(gq * S + j, jn) * Nm] = j ? make_double2(yr[j - 1], yi[j - 1])
+                                                                           : make_double2(xr, xi);
+          } else {
+#pragma unroll
+            for (int j = 0; j < S; ++j)
+              if (j < ns) {  // uniform
+#ifdef QOC_PROBE
+                if (bp.probe_mode != 3)
+#endif
+                  *reinterpret_cast<double2*>(sp) = make_double2(yr[j], yi[j]);
+                sp += sst;
+                if (FWD && penon) pen += pm ? yr[j] * yr[j] + yi[j] * yi[j] : 0.0;  // uniform branch
+              }
+          }
+          xr = yr[S - 1];
+          xi = yi[S - 1];
+#pragma unroll
+          for (int j = 0; j + 1 < S; ++j)
+            if (j == ns - 1) {
+              xr = yr[j];
+              xi = yi[j];
+            }
+        };
+        // two groups per iteration with the roles of the two Q register sets swapped (no register copies); the next
+        // group's rows are read from LDS before this group's matvecs
+        double2 Q0[S][NB], Q1[S][NB];
+        ldq(Q0, 0);
+        for (int gq = 0; gq < ng; gq += 2) {
+          ldq(Q1, min(gq + 1, ng - 1));
+          group(Q0, gq);
+          if (gq + 1 >= ng) break;
+          ldq(Q0, min(gq + 2, ng - 1));
+          group(Q1, gq + 1);
         }
       }
       BK_T(t1);
@@ -640,26 +968,32 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       BK_T(t0);
       if (c + 2 < nC) rec_store(c + 2);  // loaded one iteration ago
       if (c + 3 < nC) rec_load(c + 3);
+      xs_issue(c);  // GORD: read by grad(c) in the next iteration
 #ifdef QOC_PROBE
       if (c + 1 < nC && bp.probe_mode != 1) form(c + 1);
 #else
       if (c + 1 < nC) form(c + 1);
 #endif
+      BK_T(tg);
+#ifdef QOC_PROBE
+      if (GORD > 0 && c > 0 && bp.probe_mode != 5) grad(c - 1);
+#else
+      if (GORD > 0 && c > 0) grad(c - 1);
+#endif
+      if constexpr (GORD > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c's x landed before the barrier
       BK_T(t1);
+      BK_ADD(5, t1 - tg);
       lds_barrier();
       BK_T(t2);
       BK_ADD(3, t1 - t0);
       BK_ADD(4, t2 - t1);
     }
+    grad(nC - 1);  // GORD: the last chunk, after the chain's final barrier
   }
   if (FWD) {
-    if (chain) {
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-        if (ln.r[i] >= 0) {
-          xN[off[i]] = xr[i];
-          xN[off[i] + 1] = xi[i];
-        }
+    if (ok) {
+      xN[off] = xr;
+      xN[off + 1] = xi;
     }
     __syncthreads();
     chain_costs<double>(N, m, (const cx<double>*)g.Xt, [&](int q) { return cx<double>{xN[2 * q], xN[2 * q + 1]}; },
@@ -668,48 +1002,48 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   }
 }
 
-template <int NB>
+// S: prefix-product group (1, 2, 4, 8; 1 for the backward with additions)
+template <int NB, int S>
 __global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_fwd(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
-  blku_body<NB, true, false>(g, bk, bp, blockIdx.x, 0);
+  blku_body<NB, S, true, false>(g, bk, bp, blockIdx.x, 0);
 }
-// backward: ADD = the state penalty or the caller's co-state source (not in μ mode)
-template <int NB, bool ADD>
+// backward: ADD = the state penalty or the caller's co-state source (not in μ mode), which enter after every slice
+template <int NB, int S, bool ADD>
 __global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_bwd(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
-  blku_body<NB, false, ADD>(g, bk, bp, blockIdx.x, g.mu_mode);
+  static_assert(!ADD || S == 1, "additions after every slice: no prefix groups");
+  blku_body<NB, S, false, ADD>(g, bk, bp, blockIdx.x, g.mu_mode);
 }
-// the forward chain and the μ recurrence (mu_mode) of every seed in one launch of 2B workgroups (the direction
-// alternating every 8 workgroups, so that each XCD takes both)
-template <int NB>
-__global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_dual(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
-  const int i = blockIdx.x, B = gridDim.x >> 1;
-  const bool by8 = (B & 7) == 0;
-  const int dir = by8 ? (i >> 3) & 1 : i & 1;
-  const int seed = by8 ? ((i >> 4) << 3) | (i & 7) : i >> 1;
-  if (dir == 0) blku_body<NB, true, false>(g, bk, bp, seed, 0);
-  else blku_body<NB, false, false>(g, bk, bp, seed, 1);
+// the backward chain with the fused order-ORD gradient (qoc_eval_dev / grape_sensitivity without additions): λ stays
+// in LDS, dJdu -> bp.dJdu.
+template <int NB, int S, int ORD>
+__global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_bwdg(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
+  blku_body<NB, S, false, false, ORD>(g, bk, bp, blockIdx.x, 0);
 }
 
-// The order-ORD gradient per block (expm_jacobian! + _compute_u_sensitivity, src/gradient_computations.jl:177-223)
-// as one trace per generator: with X = A_k on the block and K = Σ_cols x_k λ_{k+1}^H (NB x NB),
-//   Σ_cols λ^H dU_j x = tr(dU_j K) = tr(A_j M),  M = Σ_{a+b<ORD} X^b K X^a / (a+b+1)! = Σ_n L_n / (n+1)!,
-//   L_0 = K, L_n = X L_{n-1} + K X^n
-// (dU_j = Σ_{a+b<ORD} X^a A_j X^b / (a+b+1)!, the reference's Taylor terms).  Order 3: 4 products of NB x NB
-// blocks instead of 4 m matvecs + 3 nu m contractions.  A unit is one (seed, slice); its nblk blocks are adjacent
-// lanes of one wave, 64 / nblk units per wave-iteration, and they reduce through a wave-private LDS slot in a fixed
-// order (no atomics, no workgroup barrier).  Persistent grid.  μ mode: L holds μ and λ = coef ⊙ μ per column.
-__host__ __device__ inline size_t blku_grad_lds(int NB, int nblk) { return (4 * 128 + (size_t)6 * NB * NB * nblk) * 8; }
+// The order-ORD block gradient over every (seed, slice) from the stored x_k and λ_{k+1} (blku_contract).  A unit is
+// one (seed, slice); its nblk blocks are adjacent lanes of one wave, 64 / nblk units per wave-iteration, and they
+// reduce through a wave-private LDS slot in a fixed order (no atomics, no workgroup barrier).  Persistent grid.
+// μ mode: L holds μ and λ = coef ⊙ μ per column.
+__host__ __device__ inline size_t blku_grad_lds(int NB, int nblk) { return (size_t)6 * NB * NB * nblk * 8; }
 
-template <int NB, int ORD>
+// Loaded operands of one gradient unit (the lane's block rows of x_k and λ_{k+1} for MM columns, u_k, the columns'
+// λ_N coefficients in μ mode)
+template <int NB, int MM>
+struct BlkuGradLd {
+  double2 x[MM][NB], l[MM][NB];
+  double u1, u2;
+};
+
+template <int NB, int ORD, int MM>
 __global__ __launch_bounds__(256) void k_blku_grad(const TChainArgs g, const BlkArgs bk, long long units, int mu_mode,
                                                    double* __restrict__ dJdu) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int E = NB * NB;
-  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, nblk = bk.nblk;
+  const int N = g.N, m = MM ? MM : g.m, nu = g.nu, Nt = g.Nt, nblk = bk.nblk;
   const size_t Nm = (size_t)N * m, NN = (size_t)N * N;
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double* rw = reinterpret_cast<double*>(smem) + 128 * w;
   // unshifted generator blocks A_0, A_1, A_2 [3][E][nblk] (row-major e), zero outside the block and for j > nu
-  double2* gsh = reinterpret_cast<double2*>(reinterpret_cast<double*>(smem) + 4 * 128);
+  double2* gsh = reinterpret_cast<double2*>(smem);
   {
     const cx<double>* A = (const cx<double>*)bk.A;
     for (int q = threadIdx.x; q < 3 * E * nblk; q += blockDim.x) {
@@ -721,127 +1055,107 @@ __global__ __launch_bounds__(256) void k_blku_grad(const TChainArgs g, const Blk
     }
   }
   __syncthreads();
-  const int UPW = 64 / nblk, ul = l / nblk, beta = l - ul * nblk;
-  const bool lact = ul < UPW;
-  const double2* G0 = gsh + beta;
-  const double2* G1 = gsh + E * nblk + beta;
-  const double2* G2 = gsh + 2 * E * nblk + beta;
+  const int NBP = blku_nbp(nblk), UPW = 64 / NBP, ul = l / NBP, beta = l - ul * NBP;
+  const bool lact = beta < nblk;
+  const int bc = min(beta, nblk - 1);
+  const double2* G0 = gsh + bc;
+  const double2* G1 = gsh + E * nblk + bc;
+  const double2* G2 = gsh + 2 * E * nblk + bc;
   int r[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) r[i] = lact ? bk.brow[beta * NB + i] : -1;
-  constexpr double invf[6] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120};
   const long long wpb = blockDim.x >> 6;
   const long long nw = (long long)gridDim.x * wpb, wid = (long long)blockIdx.x * wpb + w;
-  for (long long base = wid * UPW; base < units; base += nw * UPW) {
+  // K = Σ_c x_c λ_c^H from one column's rows, λ = coef μ in μ mode
+  auto kacc = [&](double (&kr)[E], double (&ki)[E], const double2 (&xv)[NB], double2 (&lv)[NB], int b, int c) {
+    if (mu_mode) {
+      const cx<double> cf = g.coef[(size_t)b * 2 * m + c];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) lv[i] = make_double2(cf.r * lv[i].x - cf.i * lv[i].y, cf.r * lv[i].y + cf.i * lv[i].x);
+    }
+    blku_kacc<NB>(kr, ki, xv, lv);
+  };
+  auto contract = [&](const double (&kr)[E], const double (&ki)[E], double u1, double u2, double& acc1, double& acc2) {
+    blku_contract<NB, ORD>(G0, G1, G2, nblk, kr, ki, u1, u2, acc1, acc2);
+  };
+  // per wave-iteration: the blocks of each unit reduce through the wave's LDS slot in a fixed order
+  auto reduce_store = [&](long long base, bool act, double acc1, double acc2) {
+    acc1 = blku_group_sum(act ? acc1 : 0.0, NBP);
+    acc2 = blku_group_sum(act ? acc2 : 0.0, NBP);
+    if (beta == 0 && base + ul < units) {
+      dJdu[(size_t)(base + ul) * nu] = acc1;
+      if (nu > 1) dJdu[(size_t)(base + ul) * nu + 1] = acc2;
+    }
+  };
+  auto unit_bk = [&](long long base, long long& uu, int& b, int& k) {
     const long long unit = base + ul;
-    const bool act = lact && unit < units;
-    const long long uu = act ? unit : 0;
-    const int b = (int)(uu / Nt), k = (int)(uu - (long long)b * Nt);
-    const double u1 = nu > 0 ? g.u[(size_t)uu * nu] : 0.0, u2 = nu > 1 ? g.u[(size_t)uu * nu + 1] : 0.0;
-    const double* Xs = reinterpret_cast<const double*>((const cx<double>*)g.X + ((size_t)b * (Nt + 1) + k) * Nm);
-    const double* Ls = reinterpret_cast<const double*>((const cx<double>*)g.L + ((size_t)b * (Nt + 1) + k + 1) * Nm);
-    // K = Σ_c x_c λ_c^H : K[p][q] = Σ_c x_c[p] conj(λ_c[q])
-    double kr[E], ki[E];
+    uu = unit < units ? unit : 0;
+    b = (int)(uu / Nt);
+    k = (int)(uu - (long long)b * Nt);
+  };
+  if constexpr (MM > 0) {
+    // compile-time column count: the next wave-iteration's operands are loaded before this one's products
+    auto load = [&](long long base, BlkuGradLd<NB, MM>& d) {
+      long long uu;
+      int b, k;
+      unit_bk(base, uu, b, k);
+      d.u1 = nu > 0 ? g.u[(size_t)uu * nu] : 0.0;
+      d.u2 = nu > 1 ? g.u[(size_t)uu * nu + 1] : 0.0;
+      const double* Xs = reinterpret_cast<const double*>((const cx<double>*)g.X + ((size_t)b * (Nt + 1) + k) * Nm);
+      const double* Ls = reinterpret_cast<const double*>((const cx<double>*)g.L + ((size_t)b * (Nt + 1) + k + 1) * Nm);
 #pragma unroll
-    for (int e = 0; e < E; ++e) kr[e] = ki[e] = 0.0;
-    for (int c = 0; c < m; ++c) {
-      double2 xv[NB], lv[NB];
+      for (int c = 0; c < MM; ++c)
 #pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const size_t o = 2 * ((size_t)c * N + max(r[i], 0));
-        xv[i] = r[i] >= 0 ? *reinterpret_cast<const double2*>(Xs + o) : make_double2(0.0, 0.0);
-        lv[i] = r[i] >= 0 ? *reinterpret_cast<const double2*>(Ls + o) : make_double2(0.0, 0.0);
-      }
-      if (mu_mode) {  // λ = coef μ
-        const cx<double> cf = g.coef[(size_t)b * 2 * m + c];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) lv[i] = make_double2(cf.r * lv[i].x - cf.i * lv[i].y, cf.r * lv[i].y + cf.i * lv[i].x);
-      }
-#pragma unroll
-      for (int p = 0; p < NB; ++p)
-#pragma unroll
-        for (int q = 0; q < NB; ++q) {  // x_p conj(λ_q)
-          kr[p * NB + q] = fma(xv[p].x, lv[q].x, fma(xv[p].y, lv[q].y, kr[p * NB + q]));
-          ki[p * NB + q] = fma(xv[p].y, lv[q].x, fma(-xv[p].x, lv[q].y, ki[p * NB + q]));
+        for (int i = 0; i < NB; ++i) {
+          const size_t o = 2 * ((size_t)c * N + max(r[i], 0));
+          d.x[c][i] = r[i] >= 0 ? *reinterpret_cast<const double2*>(Xs + o) : make_double2(0.0, 0.0);
+          d.l[c][i] = r[i] >= 0 ? *reinterpret_cast<const double2*>(Ls + o) : make_double2(0.0, 0.0);
         }
+    };
+    BlkuGradLd<NB, MM> cur, nxt;
+    long long base = wid * UPW;
+    if (base < units) load(base, cur);
+    for (; base < units; base += nw * UPW) {
+      const long long nb = base + nw * UPW;
+      load(nb < units ? nb : base, nxt);
+      long long uu;
+      int b, k;
+      unit_bk(base, uu, b, k);
+      double kr[E], ki[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) kr[e] = ki[e] = 0.0;
+#pragma unroll
+      for (int c = 0; c < MM; ++c) kacc(kr, ki, cur.x[c], cur.l[c], b, c);
+      double acc1, acc2;
+      contract(kr, ki, cur.u1, cur.u2, acc1, acc2);
+      reduce_store(base, lact && base + ul < units, acc1, acc2);
+      cur = nxt;
     }
-    // X = A_0 + u_1 A_1 + u_2 A_2
-    double xr_[E], xi_[E];
+  } else {
+    for (long long base = wid * UPW; base < units; base += nw * UPW) {
+      long long uu;
+      int b, k;
+      unit_bk(base, uu, b, k);
+      const double u1 = nu > 0 ? g.u[(size_t)uu * nu] : 0.0, u2 = nu > 1 ? g.u[(size_t)uu * nu + 1] : 0.0;
+      const double* Xs = reinterpret_cast<const double*>((const cx<double>*)g.X + ((size_t)b * (Nt + 1) + k) * Nm);
+      const double* Ls = reinterpret_cast<const double*>((const cx<double>*)g.L + ((size_t)b * (Nt + 1) + k + 1) * Nm);
+      double kr[E], ki[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const double2 a0 = G0[e * nblk], a1 = G1[e * nblk], a2 = G2[e * nblk];
-      xr_[e] = fma(u2, a2.x, fma(u1, a1.x, a0.x));
-      xi_[e] = fma(u2, a2.y, fma(u1, a1.y, a0.y));
-    }
-    // M = K + Σ_{n>=1} L_n / (n+1)!,  L_n = X L_{n-1} + R_n,  R_n = R_{n-1} X  (L_0 = R_0 = K)
-    double Mr[E], Mi[E], Lr[E], Li[E], Rr[E], Ri[E];
+      for (int e = 0; e < E; ++e) kr[e] = ki[e] = 0.0;
+      for (int c = 0; c < m; ++c) {
+        double2 xv[NB], lv[NB];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      Mr[e] = Lr[e] = Rr[e] = kr[e];
-      Mi[e] = Li[e] = Ri[e] = ki[e];
-    }
-#pragma unroll
-    for (int n = 1; n < ORD; ++n) {
-      double tr[E], ti[E];
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int kk = 0; kk < NB; ++kk) {  // R_{n-1} X
-          double sr = 0.0, si = 0.0;
-#pragma unroll
-          for (int q = 0; q < NB; ++q) {
-            sr = fma(Rr[i * NB + q], xr_[q * NB + kk], fma(-Ri[i * NB + q], xi_[q * NB + kk], sr));
-            si = fma(Rr[i * NB + q], xi_[q * NB + kk], fma(Ri[i * NB + q], xr_[q * NB + kk], si));
-          }
-          tr[i * NB + kk] = sr;
-          ti[i * NB + kk] = si;
+        for (int i = 0; i < NB; ++i) {
+          const size_t o = 2 * ((size_t)c * N + max(r[i], 0));
+          xv[i] = r[i] >= 0 ? *reinterpret_cast<const double2*>(Xs + o) : make_double2(0.0, 0.0);
+          lv[i] = r[i] >= 0 ? *reinterpret_cast<const double2*>(Ls + o) : make_double2(0.0, 0.0);
         }
-      double sr_[E], si_[E];
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int kk = 0; kk < NB; ++kk) {  // X L_{n-1} + R_n
-          double sr = tr[i * NB + kk], si = ti[i * NB + kk];
-#pragma unroll
-          for (int q = 0; q < NB; ++q) {
-            sr = fma(xr_[i * NB + q], Lr[q * NB + kk], fma(-xi_[i * NB + q], Li[q * NB + kk], sr));
-            si = fma(xr_[i * NB + q], Li[q * NB + kk], fma(xi_[i * NB + q], Lr[q * NB + kk], si));
-          }
-          sr_[i * NB + kk] = sr;
-          si_[i * NB + kk] = si;
-        }
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        Rr[e] = tr[e];
-        Ri[e] = ti[e];
-        Lr[e] = sr_[e];
-        Li[e] = si_[e];
-        Mr[e] = fma(invf[n + 1], Lr[e], Mr[e]);
-        Mi[e] = fma(invf[n + 1], Li[e], Mi[e]);
+        kacc(kr, ki, xv, lv, b, c);
       }
+      double acc1, acc2;
+      contract(kr, ki, u1, u2, acc1, acc2);
+      reduce_store(base, lact && base + ul < units, acc1, acc2);
     }
-    // Re tr(A_j M) = Re Σ_{i,q} A_j[i][q] M[q][i]
-    double acc1 = 0.0, acc2 = 0.0;
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const double2 a1 = G1[(i * NB + q) * nblk], a2 = G2[(i * NB + q) * nblk];
-        acc1 = fma(a1.x, Mr[q * NB + i], fma(-a1.y, Mi[q * NB + i], acc1));
-        acc2 = fma(a2.x, Mr[q * NB + i], fma(-a2.y, Mi[q * NB + i], acc2));
-      }
-    rw[2 * l] = act ? acc1 : 0.0;
-    rw[2 * l + 1] = act ? acc2 : 0.0;
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (l < UPW * nu) {
-      const int u2_ = l / nu, j = l - u2_ * nu;
-      double s = 0.0;
-      for (int q = 0; q < nblk; ++q) s += rw[2 * (u2_ * nblk + q) + j];
-      if (base + u2_ < units) dJdu[(size_t)(base + u2_) * nu + j] = s;
-    }
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 }
 

@@ -327,7 +327,8 @@ int forward(qoc_ctx* c) {
   return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
 }
 int backward(qoc_ctx* c, int order, double* d_dJdu) {
-  c->L_is_mu = false;  // every backward path below writes λ itself
+  c->L_is_mu = false;  // every backward path below writes λ itself (the fused block backward: on demand)
+  c->L_lazy = false;
   c->last_eval_mode = 0;
   if (c->src_on && c->prop_method == QOC_PROP_TSIT5)
     return fail(c, QOC_ERR_UNSUPPORTED, "a co-state source (dL_dx) is not part of the Tsit5 path (compute_pwc_gradient)");
@@ -499,7 +500,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->d_coef_mu) hipFree(c->d_coef_mu);
   if (c->d_brow) hipFree(c->d_brow);
   if (c->d_wrow) hipFree(c->d_wrow);
-  void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L,
+  void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L, c->d_u_lam, c->d_coef_lam,
                   c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_pws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec, c->d_sink, c->d_blkrec};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -902,6 +903,7 @@ int qoc_eval_dev(qoc_ctx* c, const double* d_u, int order, double* d_J, double* 
     const size_t nu_t = (size_t)c->B * c->nu * c->Nt;
     if (d_u != c->d_u) HIPCHK(c, hipMemcpyAsync(c->d_u, d_u, nu_t * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     c->have_prop = false;
+    c->L_lazy = false;
     r = blk_concurrent_ok(c, order)  ? blk_eval_concurrent(c, order, d_dJdu ? d_dJdu : c->d_dJdu)
         : c->prec == QOC_FP64 ? tchain_eval_concurrent<double>(c, d_dJdu ? d_dJdu : c->d_dJdu)
                               : tchain_eval_concurrent<float>(c, d_dJdu ? d_dJdu : c->d_dJdu);
@@ -991,6 +993,10 @@ int qoc_get_costates(qoc_ctx* c, int seed, int k, double* lam_out) {
   HIPCHK(c, hipSetDevice(c->dev));
   const size_t Nm = (size_t)c->N * c->m;
   const void* src = (char*)c->d_L + ((size_t)seed * (c->Nt + 1) + k) * Nm * c->esz;
+  if (c->L_lazy) {
+    const int r = blku_costates(c);
+    if (r) return r;
+  }
   if (!c->L_is_mu) return download_states(c, src, lam_out);
   // the concurrent eval left μ_k: λ_k = coef ⊙ μ_k (per row sector and packed column, lam_coef)
   std::vector<double> mu(2 * Nm), cf(4 * (size_t)c->m);

@@ -149,6 +149,10 @@ struct qoc_ctx {
   // N <= 48 (generators in LDS), 0 off: TChainMF everywhere (QOC_TCHAIN_ROT)
   int tchain_rot = 1;
   bool L_is_mu = false;          // d_L holds μ_k (qoc_get_costates applies the coefficients d_coef_mu)
+  bool L_lazy = false;           // the fused block backward left d_L unwritten: qoc_get_costates rebuilds it
+                                 // (blku_costates) from the saved u and λ_N coefficients
+  double* d_u_lam = nullptr;     // B x Nt x nu: u of that backward
+  cx<double>* d_coef_lam = nullptr;  // B x 2m: its λ_N coefficients
   cx<double>* d_coef_mu = nullptr;  // B x 2m: the λ_N coefficients of the eval that left μ in d_L
   int last_eval_mode = 0;        // 0 other, 1 captured sequential backward, 2 / 3 concurrent μ mode: two streams /
                                  // one dual launch, 4 block chains' concurrent eval (qoc_get_info)
@@ -285,6 +289,7 @@ int blk_detect(qoc_ctx* c);
 bool blk_active(const qoc_ctx* c);
 bool blk_rot(const qoc_ctx* c);
 bool blku_on(const qoc_ctx* c);
+int blku_costates(qoc_ctx* c);  // qoc_get_costates after the fused block backward
 int blk_forward(qoc_ctx* c);
 int blk_backward(qoc_ctx* c, int order, double* d_dJdu);
 bool blk_concurrent_ok(const qoc_ctx* c, int order);

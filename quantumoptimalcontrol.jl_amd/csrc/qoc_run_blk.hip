@@ -155,44 +155,54 @@ static bool blk_big(const qoc_ctx* c) { return c->blk_nb == 16; }
 bool blku_on(const qoc_ctx* c) {
   // QOC_BLOCKS=valu / real ask for those kernel variants explicitly (blk_jr != 1): they keep them
   if (!blk_active(c) || c->blk_jr != 1 || c->blk_nb > BLK_NBMAX || c->nu < 1 || c->nu > 2 || c->nblk > 32 ||
-      c->nblk * c->m > 256)
+      c->nblk * c->m * (c->blk_nb == 2 ? 2 : 4) > 64 * (c->blk_nb == 4 ? 2 : 4))
     return false;
   const char* env = getenv("QOC_BLKU");
   return !(env && !std::strcmp(env, "0"));
 }
 
 struct BlkuShape {
-  int C, CW, W;
+  int C, CW, W, S;
   size_t lds;
 };
-// Waves per workgroup: CW chain waves (one lane per (block, column)) and FW formation waves, sized so that forming
-// a chunk (C nblk propagators, ~190 / 450 / 2600 VALU operations each for NB = 2 / 3 / 4) takes about as long as the
-// chain waves' C matvecs (4 NB^2 FMAs + ~20 per slice); QOC_BLKU_FW overrides FW.  C: the most slices per chunk
-// (<= 64, <= the formation lanes, which compute one step record each) whose double-buffered propagators keep the
-// workgroup within 52 KB of LDS (three workgroups per CU).
-static BlkuShape blku_shape(const qoc_ctx* c) {
+// Waves per workgroup: CW chain waves (one lane per state element) and FW worker waves, sized so that a chunk's
+// worker VALU work -- forming C nblk propagators (~190 / 450 / 2600 operations each for NB = 2 / 3 / 4), and in the
+// fused backward (fused = true) also contracting C nblk gradient units (~250 / 500 / 1500) -- takes about as long as
+// the chain waves' C matvecs (4 NB^2 FMAs + ~20 per slice); QOC_BLKU_FW / QOC_BLKU_GFW override FW.  C: the most
+// slices per chunk (a power of two <= 64: chunks never straddle k_blku_rec's 64-slice (J, P) groups) whose LDS fits
+// the workgroups a CU holds at once (B / CUs of them, at most 3); QOC_BLKU_C / QOC_BLKU_GC override it.  S: the
+// prefix-product group (QOC_BLKU_S; 1 by default: the chains are store- or latency-bound at S = 1 and the scans
+// cost the workers more than they save).
+static BlkuShape blku_shape(const qoc_ctx* c, bool fused) {
   BlkuShape s{};
   const int NB = c->blk_nb, E = NB * NB;
-  s.CW = (c->nblk * c->m + 63) / 64;
+  s.CW = (c->nblk * c->m * (NB == 2 ? 2 : 4) + 63) / 64;  // one chain lane per state element (qoc_blku.hpp)
   const double costU = NB == 2 ? 190.0 : NB == 3 ? 450.0 : 2600.0, costC = 4.0 * E + 20.0;
-  int fw = (int)std::ceil(c->nblk * costU / (64.0 * costC));
-  if (const char* env = getenv("QOC_BLKU_FW")) fw = atoi(env);
-  fw = std::max(1, std::min(fw, 8 - s.CW));
+  const double costG = fused ? (NB == 2 ? 250.0 : NB == 3 ? 500.0 : 1500.0) : 0.0;
+  int fw = (int)std::ceil(c->nblk * (costU + costG) / (64.0 * costC));
+  if (const char* env = getenv(fused ? "QOC_BLKU_GFW" : "QOC_BLKU_FW")) fw = atoi(env);
+  fw = std::max(1, std::min(fw, (NB == 4 ? 4 : 8) - s.CW));
   s.W = s.CW + fw;
-  s.C = 64;  // a power of two: chunks never straddle k_blku_rec's 64-slice (J, P) groups
-  while (s.C > 4 && blku_lds(c->N, c->m, NB, c->nblk, s.C) > 52 * 1024) s.C >>= 1;
-  if (const char* env = getenv("QOC_BLKU_C")) {
+  s.S = 1;
+  if (const char* env = getenv("QOC_BLKU_S")) s.S = atoi(env) >= 2 && NB < 4 ? 2 : 1;
+  const int per_cu = std::max(1, std::min(3, (c->B + c->ncu - 1) / std::max(1, c->ncu)));
+  const size_t budget = (size_t)156 * 1024 / per_cu;
+  const int gw = fused ? fw : 0;
+  s.C = 64;
+  while (s.C > 4 && blku_lds(c->N, c->m, NB, c->nblk, s.C, gw) > budget) s.C >>= 1;
+  if (const char* env = getenv(fused ? "QOC_BLKU_GC" : "QOC_BLKU_C")) {
     int q = 1;
     while (q * 2 <= std::min(atoi(env), 64)) q *= 2;
     s.C = q;
   }
-  s.lds = blku_lds(c->N, c->m, NB, c->nblk, s.C);
+  s.C = std::max(s.C, s.S);
+  s.lds = blku_lds(c->N, c->m, NB, c->nblk, s.C, gw);
   return s;
 }
 
 static int blku_ntp(const qoc_ctx* c) { return (c->Nt + BLKU_RECBLK - 1) / BLKU_RECBLK * BLKU_RECBLK; }
 
-static BlkuParams blku_params(const qoc_ctx* c, const BlkuShape& s) {
+static BlkuParams blku_params(const qoc_ctx* c, const BlkuShape& s, double* d_dJdu = nullptr) {
   BlkuParams p{};
   for (int j = 0; j < 3; ++j) {
     const bool on = j <= c->nu;
@@ -207,11 +217,12 @@ static BlkuParams blku_params(const qoc_ctx* c, const BlkuShape& s) {
   p.Ntp = blku_ntp(c);
   p.rec = c->d_blkrec;
   p.terms = c->d_terms;
+  p.dJdu = d_dJdu;
   return p;
 }
 
 // the step records of every (seed, slice) of the current u (k_blku_rec); count: add Σ P 2^J to the terms counter
-static int blku_records(qoc_ctx* c, BlkuParams& bp, bool count) {
+static int blku_records(qoc_ctx* c, BlkuParams& bp, bool count, const double* d_u = nullptr) {
   const long long total = (long long)c->B * blku_ntp(c);
   if (!c->d_blkrec) {
     const size_t bytes = (size_t)total * BLKU_REC * sizeof(double);
@@ -223,7 +234,7 @@ static int blku_records(qoc_ctx* c, BlkuParams& bp, bool count) {
   rp.terms = count ? c->d_terms : nullptr;
   const int mk = mark_begin(c, 0);
   hipLaunchKernelGGL(k_blku_rec, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, c->stream, rp,
-                     (const double*)c->d_u, c->nu, c->Nt, total, c->d_blkrec);
+                     d_u ? d_u : (const double*)c->d_u, c->nu, c->Nt, total, c->d_blkrec);
   mark_end(c, mk);
   HIPCHK(c, hipGetLastError());
   return QOC_OK;
@@ -421,21 +432,49 @@ static hipError_t blku_dispatch(const qoc_ctx* c, F&& f) {
   return hipErrorInvalidValue;
 }
 
-static int blku_forward(qoc_ctx* c) {
+// the gradient order 1..4 as a compile-time constant
+template <typename F>
+static hipError_t blk_order_dispatch(int order, F&& f) {
+  using std::integral_constant;
+  switch (order) {
+    case 1: return f(integral_constant<int, 1>());
+    case 2: return f(integral_constant<int, 2>());
+    case 3: return f(integral_constant<int, 3>());
+    default: return f(integral_constant<int, 4>());
+  }
+}
+
+// the prefix-product group size as a compile-time constant (1, or 2 for blocks of <= 3 rows)
+template <int NB, typename F>
+static hipError_t blku_sdispatch(int S, F&& f) {
+  using std::integral_constant;
+  if constexpr (NB <= 3)
+    if (S == 2) return f(integral_constant<int, 2>());
+  return f(integral_constant<int, 1>());
+}
+
+static hipError_t blku_launch_fwd(qoc_ctx* c, const BlkuShape& s, const BlkuParams& bp) {
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
-  const BlkuShape s = blku_shape(c);
+  return blku_dispatch(c, [&](auto NB_) {
+    constexpr int NB = decltype(NB_)::value;
+    return blku_sdispatch<NB>(s.S, [&](auto S_) {
+      constexpr int S = decltype(S_)::value;
+      const hipError_t q = blk_lds_attr(k_blku_fwd<NB, S>, s.lds);
+      if (q != hipSuccess) return q;
+      hipLaunchKernelGGL((k_blku_fwd<NB, S>), dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, bp);
+      return hipGetLastError();
+    });
+  });
+}
+
+static int blku_forward(qoc_ctx* c) {
+  const BlkuShape s = blku_shape(c, false);
   BlkuParams bp = blku_params(c, s);
   int r = blku_records(c, bp, true);
   if (r) return r;
   const int mk = mark_begin(c, 1);
-  const hipError_t e = blku_dispatch(c, [&](auto NB_) {
-    constexpr int NB = decltype(NB_)::value;
-    const hipError_t q = blk_lds_attr(k_blku_fwd<NB>, s.lds);
-    if (q != hipSuccess) return q;
-    hipLaunchKernelGGL((k_blku_fwd<NB>), dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, bp);
-    return hipGetLastError();
-  });
+  const hipError_t e = blku_launch_fwd(c, s, bp);
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_fwd launch: %s", hipGetErrorString(e));
   c->fwd_captured = false;
@@ -448,39 +487,39 @@ static int blku_grad(qoc_ctx* c, int order, bool mu_mode, double* d_dJdu) {
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
   const long long units = (long long)c->B * c->Nt;
-  const int upw = 64 / c->nblk;
+  const int upw = 64 / blku_nbp(c->nblk);  // units per wave (blocks on power-of-two lane groups)
   if (upw < 1) return fail(c, QOC_ERR_UNSUPPORTED, "block gradient: %d blocks exceed one wave", c->nblk);
   const long long waves = (units + upw - 1) / upw;
   const unsigned blocks = (unsigned)std::max<long long>(1, std::min<long long>((waves + 3) / 4, (long long)c->ncu * 8));
   const size_t glds = blku_grad_lds(c->blk_nb, c->nblk);
   const int mk = mark_begin(c, 3);
+  // the column count as a compile-time constant (operand prefetch) for blocks of 2 rows with m = 2 (cavity)
+  const char* pf = getenv("QOC_BLKU_GRAD_PF");
+  const bool m2 = c->blk_nb == 2 && c->m == 2 && !(pf && !std::strcmp(pf, "0"));
   const hipError_t e = blku_dispatch(c, [&](auto NB_) {
     constexpr int NB = decltype(NB_)::value;
-    switch (order) {
-      case 1: hipLaunchKernelGGL((k_blku_grad<NB, 1>), dim3(blocks), dim3(256), glds, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
-      case 2: hipLaunchKernelGGL((k_blku_grad<NB, 2>), dim3(blocks), dim3(256), glds, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
-      case 3: hipLaunchKernelGGL((k_blku_grad<NB, 3>), dim3(blocks), dim3(256), glds, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
-      default: hipLaunchKernelGGL((k_blku_grad<NB, 4>), dim3(blocks), dim3(256), glds, c->stream, g, bk, units, (int)mu_mode, d_dJdu); break;
-    }
-    return hipGetLastError();
+    auto launch = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), glds, c->stream, g, bk, units, (int)mu_mode, d_dJdu);
+      return hipGetLastError();
+    };
+    auto by_m = [&](auto ORD_) {
+      constexpr int ORD = decltype(ORD_)::value;
+      if constexpr (NB == 2) {
+        if (m2) return launch(k_blku_grad<NB, ORD, 2>);
+      }
+      return launch(k_blku_grad<NB, ORD, 0>);
+    };
+    return blk_order_dispatch(order, by_m);
   });
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_grad launch: %s", hipGetErrorString(e));
   return QOC_OK;
 }
 
-// grape_sensitivity: λ by the block-propagator backward chain (penalty, co-state source and an external λ_N
-// included), then the block gradient for orders 1..4; the exact (Fréchet) gradient runs its dense kernel on λ.
-static int blku_backward(qoc_ctx* c, int order, double* d_dJdu) {
-  const TChainArgs g = tchain_args(c);
+// the plain backward chain (λ_Nt -> λ_0 into d_L; add: the penalty / co-state source after every slice)
+static hipError_t blku_launch_bwd(qoc_ctx* c, const TChainArgs& g, const BlkuShape& s, const BlkuParams& bp, bool add) {
   const BlkArgs bk = blk_args(c);
-  const BlkuShape s = blku_shape(c);
-  BlkuParams bp = blku_params(c, s);
-  int r = blku_records(c, bp, false);  // the u of the last propagate (stale-checked by the caller)
-  if (r) return r;
-  const bool add = g.pmask || g.src;
-  const int mk = mark_begin(c, 2);
-  const hipError_t e = blku_dispatch(c, [&](auto NB_) {
+  return blku_dispatch(c, [&](auto NB_) {
     constexpr int NB = decltype(NB_)::value;
     auto launch = [&](auto kern) {
       const hipError_t q = blk_lds_attr(kern, s.lds);
@@ -488,43 +527,109 @@ static int blku_backward(qoc_ctx* c, int order, double* d_dJdu) {
       hipLaunchKernelGGL(kern, dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, bp);
       return hipGetLastError();
     };
-    return add ? launch(k_blku_bwd<NB, true>) : launch(k_blku_bwd<NB, false>);
+    if (add) return launch(k_blku_bwd<NB, 1, true>);  // additions after every slice: no prefix groups
+    return blku_sdispatch<NB>(s.S, [&](auto S_) { return launch(k_blku_bwd<NB, decltype(S_)::value, false>); });
   });
+}
+
+// The fused backward (k_blku_bwdg): orders 1..4 without a penalty or co-state source.  λ stays in the workgroups;
+// qoc_get_costates recomputes it on demand from a copy of this evaluation's u and λ_N coefficients (blku_costates).
+static bool blku_fused_ok(const qoc_ctx* c, int order) {
+  const char* env = getenv("QOC_BLKU_FUSED");
+  return order >= 1 && order <= BLK_ORDMAX && c->mu == 0.0 && !c->src_on && !(env && !std::strcmp(env, "0"));
+}
+
+static int blku_bwdg(qoc_ctx* c, int order, double* d_dJdu) {
+  const TChainArgs g = tchain_args(c);
+  const BlkArgs bk = blk_args(c);
+  const BlkuShape s = blku_shape(c, true);
+  const BlkuParams bp = blku_params(c, s, d_dJdu);  // the records are current (the caller's)
+  const int mk = mark_begin(c, 2);
+  const hipError_t e = blku_dispatch(c, [&](auto NB_) {
+    constexpr int NB = decltype(NB_)::value;
+    return blku_sdispatch<NB>(s.S, [&](auto S_) {
+      constexpr int S = decltype(S_)::value;
+      return blk_order_dispatch(order, [&](auto ORD_) {
+        constexpr int ORD = decltype(ORD_)::value;
+        const hipError_t q = blk_lds_attr(k_blku_bwdg<NB, S, ORD>, s.lds);
+        if (q != hipSuccess) return q;
+        hipLaunchKernelGGL((k_blku_bwdg<NB, S, ORD>), dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, bp);
+        return hipGetLastError();
+      });
+    });
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_bwdg launch: %s", hipGetErrorString(e));
+  // what qoc_get_costates needs to rebuild λ: this u and the λ_N coefficients (external λ_N stays in d_L)
+  const size_t nu_t = (size_t)c->B * c->nu * c->Nt, ncf = (size_t)c->B * 2 * c->m;
+  if (!c->d_u_lam) {
+    HIPCHK(c, hipMalloc((void**)&c->d_u_lam, nu_t * sizeof(double)));
+    HIPCHK(c, hipMalloc((void**)&c->d_coef_lam, ncf * sizeof(cx<double>)));
+    c->dev_bytes += nu_t * sizeof(double) + ncf * sizeof(cx<double>);
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_u_lam, c->d_u, nu_t * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_coef_lam, c->d_coef, ncf * sizeof(cx<double>), hipMemcpyDeviceToDevice, c->stream));
+  c->L_lazy = true;
+  return QOC_OK;
+}
+
+// qoc_get_costates after a fused backward: the plain backward chain from the saved u and coefficients into d_L
+int blku_costates(qoc_ctx* c) {
+  if (!c->L_lazy) return QOC_OK;
+  TChainArgs g = tchain_args(c);
+  g.coef = c->d_coef_lam;
+  g.u = c->d_u_lam;
+  const BlkuShape s = blku_shape(c, false);
+  BlkuParams bp = blku_params(c, s);
+  int r = blku_records(c, bp, false, c->d_u_lam);
+  if (r) return r;
+  const hipError_t e = blku_launch_bwd(c, g, s, bp, false);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_bwd launch: %s", hipGetErrorString(e));
+  c->L_lazy = false;
+  return QOC_OK;
+}
+
+// grape_sensitivity: the fused backward when it applies; otherwise λ by the plain backward chain (penalty, co-state
+// source and an external λ_N included), then the block gradient for orders 1..4 or the dense exact (Fréchet) one
+static int blku_backward(qoc_ctx* c, int order, double* d_dJdu) {
+  const TChainArgs g = tchain_args(c);
+  const BlkuShape s = blku_shape(c, false);
+  BlkuParams bp = blku_params(c, s);
+  int r = blku_records(c, bp, false);  // the u of the last propagate (stale-checked by the caller)
+  if (r) return r;
+  if (blku_fused_ok(c, order)) return blku_bwdg(c, order, d_dJdu);
+  const int mk = mark_begin(c, 2);
+  const hipError_t e = blku_launch_bwd(c, g, s, bp, g.pmask || g.src);
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_bwd launch: %s", hipGetErrorString(e));
   if (order == QOC_DUKDP_EXACT) return dense_gradient<double>(c, order, d_dJdu);
   return blku_grad(c, order, false, d_dJdu);
 }
 
-// qoc_eval_dev: the forward chain and the μ recurrence in one launch of 2B workgroups, then the gradient
+// qoc_eval_dev (built-in cost, no penalty, no co-state source): the step records once, the forward chain (J and the
+// λ_N coefficients), then the fused backward -- x_k is written once and read once, λ never leaves the workgroups
 static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
-  if (!c->d_coef_mu) {
-    HIPCHK(c, hipMalloc((void**)&c->d_coef_mu, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
-    c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
-  }
-  const TChainArgs g = tchain_args(c);
-  const BlkArgs bk = blk_args(c);
-  const BlkuShape s = blku_shape(c);
+  const BlkuShape s = blku_shape(c, false);
   BlkuParams bp = blku_params(c, s);
-  int r0 = blku_records(c, bp, true);
-  if (r0) return r0;
+  int r = blku_records(c, bp, true);
+  if (r) return r;
   const int mk = mark_begin(c, 1);
-  const hipError_t e = blku_dispatch(c, [&](auto NB_) {
-    constexpr int NB = decltype(NB_)::value;
-    const hipError_t q = blk_lds_attr(k_blku_dual<NB>, s.lds);
-    if (q != hipSuccess) return q;
-    hipLaunchKernelGGL((k_blku_dual<NB>), dim3(2 * c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, bp);
-    return hipGetLastError();
-  });
+  const hipError_t e = blku_launch_fwd(c, s, bp);
   mark_end(c, mk);
-  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_dual launch: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_fwd launch: %s", hipGetErrorString(e));
   c->fwd_captured = false;
   c->props_since_reset++;
-  const int r = blku_grad(c, order, true, d_dJdu);
+  if (blku_fused_ok(c, order)) {
+    r = blku_bwdg(c, order, d_dJdu);
+  } else {
+    const int mb = mark_begin(c, 2);
+    const hipError_t eb = blku_launch_bwd(c, tchain_args(c), s, bp, false);
+    mark_end(c, mb);
+    if (eb != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_bwd launch: %s", hipGetErrorString(eb));
+    r = blku_grad(c, order, false, d_dJdu);
+  }
   if (r) return r;
-  HIPCHK(c, hipMemcpyAsync(c->d_coef_mu, c->d_coef, (size_t)c->B * 2 * c->m * sizeof(cx<double>),
-                           hipMemcpyDeviceToDevice, c->stream));
-  c->L_is_mu = true;
+  c->L_is_mu = false;
   c->last_eval_mode = 4;
   return QOC_OK;
 }

@@ -1,9 +1,10 @@
-// Segment cycle breakdown of the block-propagator dual launch (diagnostic; built with -DQOC_PROBE):
+// Segment cycle breakdown of the block-propagator launches (diagnostic; built with -DQOC_PROBE):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DQOC_PROBE -o tools/blku_probe tools/blku_probe.hip
-// A cavity-shaped problem (N = 2 n blocks of 2 rows {b, b + n}, m = 2, nu = 2) with synthetic skew-Hermitian
-// generators of the cavity's norms; prints the launch time per formation-wave count and chunk size, and for
-// workgroup 7 the cycles per chunk of: chain compute, chain barrier wait, formation, formation + records,
-// formation barrier wait; probe modes 1 (no formation) and 2 (no chain) give the floors of each role.
+// A cavity-shaped problem (N = 2 n blocks of 2 rows {b, b + n}, m = 2, nu = 2; NB = 3: the zz shape) with
+// synthetic skew-Hermitian generators of the cavity's norms; prints the launch time of k_blku_fwd and of the fused
+// backward k_blku_bwdg (order 3) per worker-wave count and chunk size, and for workgroup 7 the cycles per chunk
+// of: chain compute, chain barrier wait, worker (formation + records + gradient), of which gradient, worker
+// barrier wait.  Probe modes: 1 no formation, 2 no chain, 3 no chain stores, 5 no gradient.
 // Usage: blku_probe [NB=2|3] [B] [Nt]
 #include <cstdio>
 #include <cstdlib>
@@ -11,8 +12,8 @@
 #include "../quantumoptimalcontrol.jl_amd/csrc/qoc_blku.hpp"
 using namespace qoc;
 
-template <int NB>
-void run(int B, int Nt, int nblk, int m, int W, int C, int mode) {
+template <int NB, int S>
+void run(int B, int Nt, int nblk, int m, int W, int C, int mode, bool bwdg) {
   const int nu = 2, N = NB * nblk;
   const size_t NN = (size_t)N * N;
   std::vector<cx<double>> A((nu + 1) * NN, cx<double>{0, 0});
@@ -61,18 +62,29 @@ void run(int B, int Nt, int nblk, int m, int W, int C, int mode) {
   bp.rad[0] = 0.154; bp.rad[1] = bp.rad[2] = 0.5;
   bp.theta_cap = 0.978;
   bp.C = C;
-  bp.CW = (nblk * m + 63) / 64;
+  if (C < S) return;
+  bp.CW = (nblk * m * (NB == 2 ? 2 : 4) + 63) / 64;
   bp.Ntp = (Nt + 63) / 64 * 64;
   bp.terms = dterms;
   bp.probe_mode = mode;
+  double* ddJ;
+  (void)hipMalloc(&ddJ, (size_t)B * Nt * nu * 8);
+  bp.dJdu = ddJ;
+  {
+    std::vector<cx<double>> cf((size_t)B * 2 * m, cx<double>{0.3, -0.1});
+    (void)hipMemcpy(dcoef, cf.data(), cf.size() * 16, hipMemcpyHostToDevice);
+  }
+  (void)hipMemset(dX, 0, (size_t)B * (Nt + 1) * N * m * 16);
   double* drec;
   const long long total = (long long)B * bp.Ntp;
   (void)hipMalloc(&drec, total * BLKU_REC * 8);
   bp.rec = drec;
   hipLaunchKernelGGL(k_blku_rec, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, 0, bp, du, nu, Nt, total, drec);
   (void)hipDeviceSynchronize();
-  const size_t lds = blku_lds(N, m, NB, nblk, C);
-  (void)hipFuncSetAttribute((const void*)k_blku_dual<NB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const size_t lds = blku_lds(N, m, NB, nblk, C, bwdg ? W - bp.CW : 0);
+  if (lds > 160 * 1024) return;  // does not fit one CU
+  const void* kf = bwdg ? (const void*)k_blku_bwdg<NB, S, 3> : (const void*)k_blku_fwd<NB, S>;
+  (void)hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
@@ -81,7 +93,8 @@ void run(int B, int Nt, int nblk, int m, int W, int C, int mode) {
   for (int it = 0; it < 3; ++it) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bk), z, sizeof(z));
     (void)hipEventRecord(a);
-    hipLaunchKernelGGL((k_blku_dual<NB>), dim3(2 * B), dim3(64 * W), lds, 0, g, bk, bp);
+    if (bwdg) hipLaunchKernelGGL((k_blku_bwdg<NB, S, 3>), dim3(B), dim3(64 * W), lds, 0, g, bk, bp);
+    else hipLaunchKernelGGL((k_blku_fwd<NB, S>), dim3(B), dim3(64 * W), lds, 0, g, bk, bp);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     (void)hipEventElapsedTime(&ms, a, b);
@@ -93,12 +106,12 @@ void run(int B, int Nt, int nblk, int m, int W, int C, int mode) {
   unsigned long long tc[16];
   (void)hipMemcpyFromSymbol(tc, HIP_SYMBOL(g_bk), sizeof(tc));
   const int nC = (Nt + C - 1) / C, fw = W - bp.CW;
-  printf("NB=%d nblk=%d m=%d B=%d Nt=%d W=%d C=%2d mode=%d lds=%zu: %.4f ms  per chunk (cycles): chain %6.0f  wait %6.0f"
-         " | form %6.0f  form+rec %6.0f  wait %6.0f\n",
-         NB, nblk, m, B, Nt, W, C, mode, lds, ms, tc[0] / (double)nC / bp.CW, tc[1] / (double)nC / bp.CW,
-         tc[2] / (double)nC / fw, tc[3] / (double)nC / fw, tc[4] / (double)nC / fw);
+  printf("%s NB=%d S=%d B=%d Nt=%d W=%d C=%2d mode=%d lds=%6zu: %.4f ms  per chunk (cycles): chain %6.0f  wait %6.0f"
+         " | worker %6.0f  grad %6.0f  wait %6.0f\n",
+         bwdg ? "bwdg" : "fwd ", NB, S, B, Nt, W, C, mode, lds, ms, tc[0] / (double)nC / bp.CW,
+         tc[1] / (double)nC / bp.CW, tc[3] / (double)nC / fw, tc[5] / (double)nC / fw, tc[4] / (double)nC / fw);
   (void)hipFree(dA); (void)hipFree(du); (void)hipFree(dx0); (void)hipFree(dX); (void)hipFree(dL); (void)hipFree(dcoef);
-  (void)hipFree(dJ); (void)hipFree(dsink); (void)hipFree(dbrow); (void)hipFree(dterms); (void)hipFree(drec);
+  (void)hipFree(dJ); (void)hipFree(dsink); (void)hipFree(dbrow); (void)hipFree(dterms); (void)hipFree(drec); (void)hipFree(ddJ);
 }
 
 int main(int argc, char** argv) {
@@ -106,11 +119,15 @@ int main(int argc, char** argv) {
   const int B = argc > 2 ? atoi(argv[2]) : (NB == 2 ? 256 : 512);
   const int Nt = argc > 3 ? atoi(argv[3]) : (NB == 2 ? 1000 : 500);
   const int nblk = NB == 2 ? 20 : 3, m = NB == 2 ? 2 : 4;
-  for (int mode = 0; mode < 3; ++mode)
-    for (int W : {2, 3, 4, 5})
-      for (int C : {8, 16, 32, 64}) {
-        if (NB == 2) run<2>(B, Nt, nblk, m, W, C, mode);
-        else run<3>(B, Nt, nblk, m, W, C, mode);
-      }
+  const int W0 = NB == 2 ? 2 : 1;  // chain waves
+  for (int bw : {0, 1})
+    for (int mode : {0, 1, 2, 3, 5})
+      for (int W = W0 + 1; W <= 8; ++W)
+        for (int C : {8, 16, 32}) {
+          if ((mode == 3 && bw) || (mode == 5 && !bw)) continue;
+          if (mode && (W != W0 + 4 || C != 16)) continue;
+          if (NB == 2) run<2, 1>(B, Nt, nblk, m, W, C, mode, bw);
+          else run<3, 1>(B, Nt, nblk, m, W, C, mode, bw);
+        }
   return 0;
 }
