@@ -400,6 +400,7 @@ def main():
             traffic_all = {}
     taylor = info1.get("chain") == "taylor" and not large
     dual = info1.get("concurrent_launch") == "dual"
+    fused = info1.get("concurrent_launch") == "fused"  # block propagators: forward, then the backward with the gradient
     bsz = block_sizes(prob) if taylor and info1.get("chain_kernel") in ("blocks", "blocks_mfma", "blocks_prop") else None
     bprop = info1.get("chain_kernel") == "blocks_prop"
     # blocks of <= 4 rows (VALU lanes or packed MFMA block waves) with the block gradient; 5..16 rows: MFMA block
@@ -416,13 +417,18 @@ def main():
         dirs = 2 if dual else 1
         tl = terms / K * dirs
         p_avg = terms / K / max(B * Nt, 1)
-        rec = B * Nt * 8 * nu if bprop else B * Nt * (32 + 8 * (p_avg + 1) + 8 * nu)
+        # block propagators: k_blku_rec reads u_k and writes one 64-byte step record per slice (Nt rounded up to
+        # 64), which the chains read back; the fused backward (k_blku_bwdg) reads x_0..x_{Nt-1} and the records and
+        # writes dJdu -- λ never leaves the workgroup and no gradient launch follows
+        ntp = -(-Nt // 64) * 64
+        rec = B * Nt * 64 if bprop else B * Nt * (32 + 8 * (p_avg + 1) + 8 * nu)
         st = B * (Nt + 1) * N * m * esz
+        bwd_bytes = (st + rec) if not fused else (B * Nt * N * m * esz + rec + B * Nt * nu * 8)
         models = {
-            "k_expm": ("hbm", 0.0 if bprop else (B * Nt * (8 * nu + 32 + 8 * (p_avg + 1))) / 1e9, "GB/s",
-                       PEAK_HBM_GBS),
+            "k_expm": ("hbm", (B * Nt * 8 * nu + B * ntp * 64 if bprop
+                               else B * Nt * (8 * nu + 32 + 8 * (p_avg + 1))) / 1e9, "GB/s", PEAK_HBM_GBS),
             "k_chain_fwd": ("hbm", dirs * (st + rec) / 1e9, "GB/s", PEAK_HBM_GBS),
-            "k_chain_bwd": ("hbm", (st + rec) / 1e9, "GB/s", PEAK_HBM_GBS),
+            "k_chain_bwd": ("hbm", bwd_bytes / 1e9, "GB/s", PEAK_HBM_GBS),
             "k_grad": ("hbm", (2 * B * Nt * N * m * esz + 16 * nu * B * Nt) / 1e9, "GB/s", PEAK_HBM_GBS),
         }
         if bprop:
@@ -432,10 +438,10 @@ def main():
             # blocks and nu traces (8 flops per CMAC)
             nbk = block_sizes(prob).astype(np.float64)
             form = float(np.sum(8.0 * nbk * p_avg + 16.0 * nbk ** 3 + 40.0 * nbk ** 2)) * B * Nt
+            gflops = 8.0 * B * Nt * float(np.sum(m * nbk ** 2 + 2 * (args.order - 1) * nbk ** 3 + nu * nbk ** 2))
             block_flops = {"k_chain_fwd": dirs * (form + 8.0 * nb2 * m * B * Nt),
-                           "k_chain_bwd": form + 8.0 * nb2 * m * B * Nt,
-                           "k_grad": 8.0 * B * Nt * float(np.sum(m * nbk ** 2 + 2 * (args.order - 1) * nbk ** 3
-                                                                 + nu * nbk ** 2))}
+                           "k_chain_bwd": form + 8.0 * nb2 * m * B * Nt + (gflops if fused else 0.0),
+                           "k_grad": 0.0 if fused else gflops}
         else:
             block_flops = {"k_chain_fwd": 8.0 * nb2 * m * tl, "k_chain_bwd": 8.0 * nb2 * m * terms / K,
                            "k_grad": 8.0 * nb2 * m * B * Nt * (2 * (args.order - 1) + nu * args.order)}
@@ -502,8 +508,8 @@ def main():
     names = {"k_expm": "k_expm_rr", "k_chain_fwd": "k_chain_fwd", "k_chain_bwd": "k_chain_bwd", "k_grad": "k_grad_rr"}
     if blocks:
         kb = {"blocks_mfma": "k_blkrot", "blocks_prop": "k_blku"}.get(info1.get("chain_kernel"), "k_blk")
-        names = {"k_expm": "k_tchain_prep", "k_chain_fwd": kb + ("_dual" if dual else "_fwd"),
-                 "k_chain_bwd": kb + "_bwd", "k_grad": "k_blku_grad" if bprop else "k_blk_grad"}
+        names = {"k_expm": "k_blku_rec" if bprop else "k_tchain_prep", "k_chain_fwd": kb + ("_dual" if dual else "_fwd"),
+                 "k_chain_bwd": kb + ("_bwdg" if fused else "_bwd"), "k_grad": "k_blku_grad" if bprop else "k_blk_grad"}
         for k in ("k_chain_fwd", "k_chain_bwd", "k_grad"):
             kern[k]["kernel"] = names[k]
             t = per_step[k] / 1e3
@@ -531,7 +537,9 @@ def main():
                 "note": ("block chains (generators with invariant blocks): achieved = algorithmic HBM bytes per launch "
                          "(states written, step records / u_k read; the gradient: x_k and λ_{k+1} read) / launch time"
                          + ("; the forward chain and the μ recurrence of every seed in one launch (" +
-                            names["k_chain_fwd"] + ")" if dual else ""))}
+                            names["k_chain_fwd"] + ")" if dual else "")
+                         + ("; the backward chain contracts the gradient beside it (" + names["k_chain_bwd"] +
+                            "): x_k read once, λ kept in LDS" if fused else ""))}
     elif taylor:
         mf = prob.precision == "fp64"
         names = {"k_expm": "k_tchain_prep",

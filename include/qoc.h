@@ -184,7 +184,9 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
  * resident Taylor / Paterson-Stockmeyer, 2 LDS Paterson-Stockmeyer), info[6] = 1 when the Taylor-action chains
  * use Chebyshev terms (skew-Hermitian generators, fp64; QOC_TCHAIN_POLY=taylor keeps Taylor), info[7] = state columns the kernels run on (m, or max(nc1, nc2) with qoc_set_compression), info[8] = how the
  * last backward ran (0 generic, 1 from the chains' captured products, 2 concurrent μ recurrence of qoc_eval_dev on
- * a second stream, 3 the same in one launch with the forward chain, 4 the block chains' concurrent eval),
+ * a second stream, 3 the same in one launch with the forward chain, 4 the block chains' concurrent eval, 5 the block
+ * propagators' fused backward: λ kept on chip, the gradient contracted beside the chain; qoc_get_costates then
+ * rebuilds λ on demand),
  * info[9] = 1 when the last forward chain wrote its captured products, info[10] = the Taylor-action chain kernels
  * (0 none / the fp32 VALU ones, 1 MFMA with the state in LDS, 2 MFMA with the state in registers: N <= 32, nu <= 2,
  * QOC_TCHAIN_ROT=0 keeps 1; 3 block chains: the generators split into invariant blocks of <= 4 rows, one VALU lane

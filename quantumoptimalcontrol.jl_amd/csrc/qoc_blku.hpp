@@ -77,6 +77,7 @@ constexpr int BLKU_RECBLK = 64;  // slices sharing one (J, P)
 // Taylor degrees of the block propagators: ρ_k / 2^J <= θ_cap ≈ 0.98 needs P <= 18; the term loops are unrolled to
 // BLKU_TMAX with the coefficients 1/t! as compile-time constants
 constexpr int BLKU_TMAX = 20;
+constexpr int BLKU_XMAX = 20;  // fused backward: x_k elements staged per stager lane and chunk
 struct BlkuCoef {
   double inv[BLKU_TMAX + 2];   // 1/t
   double fact[BLKU_TMAX + 1];  // 1/t!
@@ -489,7 +490,11 @@ __host__ __device__ inline int blku_nbp(int nblk) {
   return p;
 }
 __device__ __forceinline__ double blku_group_sum(double v, int nbp) {
-  for (int o = nbp >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (nbp > 1) v += dpp_any<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (nbp > 2) v += dpp_any<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (nbp > 4) v += dpp_any<0x141>(v);  // row_half_mirror: the other quad of 8
+  if (nbp > 8) v += dpp_any<0x140>(v);  // row_mirror: the other 8 of 16
+  if (nbp > 16) v = swap_sum<16>(v);    // the other row of 32
   return v;
 }
 
@@ -510,19 +515,18 @@ __device__ __forceinline__ void blku_kacc(double (&kr)[NB * NB], double (&ki)[NB
       ki[p * NB + q] = fma(xv[p].y, lv[q].x, fma(-xv[p].x, lv[q].y, ki[p * NB + q]));
     }
 }
-// Re tr(A_j M) for j = 1, 2 from K and u_k; G0..G2: the unit's block of the unshifted generators A_0..A_2
-// (row-major entries at stride nblk)
-template <int NB, int ORD>
-__device__ __forceinline__ void blku_contract(const double2* G0, const double2* G1, const double2* G2, int nblk,
-                                              const double (&kr)[NB * NB], const double (&ki)[NB * NB], double u1,
-                                              double u2, double& acc1, double& acc2) {
+// Re tr(A_j M) for j = 1, 2 from K and u_k; ga(j, e): entry e (row-major) of the unit's block of the unshifted
+// generator A_j (from registers or LDS)
+template <int NB, int ORD, typename GA>
+__device__ __forceinline__ void blku_contract(GA&& ga, const double (&kr)[NB * NB], const double (&ki)[NB * NB],
+                                              double u1, double u2, double& acc1, double& acc2) {
   constexpr int E = NB * NB;
   constexpr double invf[6] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120};
   // X = A_0 + u_1 A_1 + u_2 A_2
   double xr_[E], xi_[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const double2 a0 = G0[e * nblk], a1 = G1[e * nblk], a2 = G2[e * nblk];
+    const double2 a0 = ga(0, e), a1 = ga(1, e), a2 = ga(2, e);
     xr_[e] = fma(u2, a2.x, fma(u1, a1.x, a0.x));
     xi_[e] = fma(u2, a2.y, fma(u1, a1.y, a0.y));
   }
@@ -586,7 +590,7 @@ __device__ __forceinline__ void blku_contract(const double2* G0, const double2* 
   for (int i = 0; i < NB; ++i)
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
-      const double2 a1 = G1[(i * NB + q) * nblk], a2 = G2[(i * NB + q) * nblk];
+      const double2 a1 = ga(1, i * NB + q), a2 = ga(2, i * NB + q);
       acc1 = fma(a1.x, Mr[q * NB + i], fma(-a1.y, Mi[q * NB + i], acc1));
       acc2 = fma(a2.x, Mr[q * NB + i], fma(-a2.y, Mi[q * NB + i], acc2));
     }
@@ -645,7 +649,14 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   const int nC = (Nt + C - 1) / C;
   auto chunk_of = [&](int c) { return FWD ? c : nC - 1 - c; };  // absolute chunk of sequence position c
   const bool chain = w < bp.CW;
-  const int fl = tid - 64 * bp.CW, FL = nthr - 64 * bp.CW;  // formation lanes
+  // the fused backward has one staging wave (wave CW) between the chain and the worker waves: it moves the step
+  // records and x_k global -> registers -> LDS one iteration apart, so that neither the chain (whose first matvec of a
+  // chunk would wait on the loads) nor the workers (whose registers go to the formation and the contraction) wait
+  constexpr int STG = GORD > 0 ? 1 : 0;
+  const bool stager = GORD > 0 && w == bp.CW;
+  const int fl = tid - 64 * (bp.CW + STG), FL = nthr - 64 * (bp.CW + STG);  // formation lanes
+  // staging lanes (global -> registers, one iteration later registers -> LDS): the stager, else the worker lanes
+  const int sl = GORD > 0 ? tid - 64 * bp.CW : fl, SLN = GORD > 0 ? 64 : FL;
   // step records of sequence chunk c: C x REC doubles from k_blku_rec (the tail of a partial chunk: clamped reads,
   // never used), through registers into the LDS ring slot c & 3
   constexpr int RMAX = 8;  // loads per lane: 64 x REC doubles / 64 lanes at most
@@ -654,16 +665,14 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   auto rec_load = [&](int c) {
     const size_t base = (size_t)chunk_of(c) * C * BLKU_REC;
 #pragma unroll
-    for (int i = 0; i < RMAX; ++i) {
-      const int e = fl + i * FL;
-      rr[i] = e < C * BLKU_REC ? recb[base + e] : 0.0;
-    }
+    for (int i = 0; i < RMAX; ++i)  // unconditional (clamped) loads: the waits before rec_store count them exactly
+      rr[i] = recb[base + min(sl + i * SLN, C * BLKU_REC - 1)];
   };
   auto rec_store = [&](int c) {
     double* dst = recs + (size_t)(c & 3) * C * BLKU_REC;
 #pragma unroll
     for (int i = 0; i < RMAX; ++i) {
-      const int e = fl + i * FL;
+      const int e = sl + i * SLN;
       if (e < C * BLKU_REC) dst[e] = rr[i];
     }
   };
@@ -676,16 +685,16 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   // adjacent lanes (S | 16: one DPP row) and scan by row shifts (Hillis-Steele, log2 S block products).  NU units per
   // lane at a time, at stride FL (independent recurrences interleaved).
   constexpr int NU = QOC_BLKU_NU(NB);
-  auto form = [&](int c) {
-    const int a = chunk_of(c), jn = min(C, Nt - a * C), units = (jn + S - 1) / S * S * nblk;
+  auto form_n = [&](auto NU_, int c, int units, int jn) {
+    constexpr int NV = decltype(NU_)::value;
     const double* rc = recs + (size_t)(c & 3) * C * BLKU_REC;
     double2* Uc = Ub + (size_t)(c & 1) * C * E * nblk;
-    for (int q = fl; q < units; q += NU * FL) {
-      int be[NU], pp[NU], jl[NU];
-      const double* rp[NU];
-      bool st[NU];
+    for (int q = fl; q < units; q += NV * FL) {
+      int be[NV], pp[NV], jl[NV];
+      const double* rp[NV];
+      bool st[NV];
 #pragma unroll
-      for (int u = 0; u < NU; ++u) {
+      for (int u = 0; u < NV; ++u) {
         const int qu = q + u * FL;
         const int qq = qu < units ? qu : q, t = qq / S, gq = t / nblk;
         jl[u] = qq - t * S;
@@ -695,14 +704,14 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
         pp[u] = posn(min(s_, jn - 1), jn);
         rp[u] = rc + (size_t)pp[u] * BLKU_REC;
       }
-      double ur[NU][E], ui[NU][E];
-      blku_form<NB, NU>(gb, nblk, be, rp, invt, ur, ui);
+      double ur[NV][E], ui[NV][E];
+      blku_form<NB, NV>(gb, nblk, be, rp, invt, ur, ui);
       if constexpr (S > 1) {
 #pragma unroll
-        for (int u = 0; u < NU; ++u) blku_scan<NB, S, FWD>(ur[u], ui[u], jl[u]);
+        for (int u = 0; u < NV; ++u) blku_scan<NB, S, FWD>(ur[u], ui[u], jl[u]);
       }
 #pragma unroll
-      for (int u = 0; u < NU; ++u)
+      for (int u = 0; u < NV; ++u)
         if (st[u]) {
           double2* o = Uc + (size_t)pp[u] * E * nblk + be[u];
 #pragma unroll
@@ -710,19 +719,36 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
         }
     }
   };
-  // x_k of sequence chunk cq (GORD > 0) into the x ring slot cq & 1 by LDS-DMA (global_load_lds_dwordx4, 16 bytes a
-  // lane): the chunk's jn N m complex are contiguous in HBM; lanes past them reload element 0 into the slot's tail
+  // NU units per lane only when the chunk has more units than formation lanes (else the second would be idle work)
+  auto form = [&](int c) {
+    const int a = chunk_of(c), jn = min(C, Nt - a * C), units = (jn + S - 1) / S * S * nblk;
+    if (NU > 1 && units > FL) form_n(std::integral_constant<int, NU>(), c, units, jn);
+    else form_n(std::integral_constant<int, 1>(), c, units, jn);
+  };
+  // x_k of sequence chunk cq (GORD > 0) through registers into the x ring slot cq & 1: loaded one iteration before
+  // it is stored (like the step records), so the wait falls on loads long landed (LDS-DMA instead would make every
+  // LDS access of the formation wait for the copy in flight); the chunk's jn N m complex are contiguous in HBM
+  constexpr int XMAX = GORD > 0 ? BLKU_XMAX : 1;  // loads per stager lane (the host keeps C N m <= 64 BLKU_XMAX)
   const int CNp = blku_cnp(N, m, C);
   double2* const xring = reinterpret_cast<double2*>(lds + blku_off_xs(N, m, NB, nblk, C));
-  auto xs_issue = [&](int cq) {
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  dv2 xreg[XMAX];  // (a clang vector type: an array of HIP's double2 struct is not promoted to registers)
+  auto xs_load = [&](int cq) {
     if constexpr (GORD > 0) {
       const int a = chunk_of(cq), n = min(C, Nt - a * C) * (int)Nm;
       const double2* src = reinterpret_cast<const double2*>((const cx<double>*)g.X + ((size_t)b * (Nt + 1) + (size_t)a * C) * Nm);
+#pragma unroll
+      for (int i = 0; i < XMAX; ++i)  // clamped, unconditional
+        xreg[i] = *reinterpret_cast<const dv2*>(src + min(sl + i * SLN, n - 1));
+    }
+  };
+  auto xs_store = [&](int cq) {
+    if constexpr (GORD > 0) {
       double2* dst = xring + (size_t)(cq & 1) * CNp;
-      for (int e0 = (w - bp.CW) * 64; e0 < n; e0 += FL) {
-        const int e = e0 + (tid & 63);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + (e < n ? e : 0)),
-                                         (__attribute__((address_space(3))) void*)(dst + e0), 16, 0, 0);
+#pragma unroll
+      for (int i = 0; i < XMAX; ++i) {
+        const int e = sl + i * SLN;
+        if (e < C * (int)Nm) *reinterpret_cast<dv2*>(dst + e) = xreg[i];
       }
     }
   };
@@ -731,7 +757,7 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   // Re tr(A_j M) reduced over the blocks through the wave's LDS slot in a fixed order
   auto grad = [&](int cq) {
     if constexpr (GORD > 0) {
-      const int a = chunk_of(cq), jn = min(C, Nt - a * C), gw = w - bp.CW, GW = (nthr >> 6) - bp.CW;
+      const int a = chunk_of(cq), jn = min(C, Nt - a * C), gw = w - bp.CW - STG, GW = (nthr >> 6) - bp.CW - STG;
       const int l = tid & 63, NBP = blku_nbp(nblk), UPW = 64 / NBP, ul = l / NBP, be = l - ul * NBP;
       const int bc = min(be, nblk - 1);
       const double2* lr = lam + (size_t)(cq & 1) * C * Nm;
@@ -740,6 +766,12 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       int r[NB];
 #pragma unroll
       for (int i = 0; i < NB; ++i) r[i] = be < nblk ? bk.brow[be * NB + i] : -1;
+      double2 areg[3][NB == 2 ? E : 1];
+      if constexpr (NB == 2)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int e = 0; e < E; ++e) areg[j][e] = ga[(j * E + e) * nblk + bc];
       for (int it = gw; it * UPW < jn; it += GW) {
         const int jj = it * UPW + ul;
         const bool act = be < nblk && jj < jn;
@@ -753,18 +785,27 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
         double kr[E], ki[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) kr[e] = ki[e] = 0.0;
-        for (int c = 0; c < m; ++c) {
-          double2 xv[NB], lv[NB];
+        constexpr int CB = NB == 2 ? 2 : 1;  // columns whose loads are in flight at once (a missing one: zeros)
+        for (int c0 = 0; c0 < m; c0 += CB) {
+          double2 xv[CB][NB], lv[CB][NB];
 #pragma unroll
-          for (int i = 0; i < NB; ++i) {
-            const int o = c * N + max(r[i], 0);
-            xv[i] = r[i] >= 0 ? xs[o] : make_double2(0.0, 0.0);
-            lv[i] = r[i] >= 0 ? ls[o] : make_double2(0.0, 0.0);
-          }
-          blku_kacc<NB>(kr, ki, xv, lv);
+          for (int cc = 0; cc < CB; ++cc)
+#pragma unroll
+            for (int i = 0; i < NB; ++i) {
+              const bool v = r[i] >= 0 && c0 + cc < m;
+              const int o = v ? (c0 + cc) * N + r[i] : 0;
+              xv[cc][i] = v ? xs[o] : make_double2(0.0, 0.0);
+              lv[cc][i] = v ? ls[o] : make_double2(0.0, 0.0);
+            }
+#pragma unroll
+          for (int cc = 0; cc < CB; ++cc) blku_kacc<NB>(kr, ki, xv[cc], lv[cc]);
         }
         double acc1, acc2;
-        blku_contract<NB, GORD>(ga + bc, ga + E * nblk + bc, ga + 2 * E * nblk + bc, nblk, kr, ki, u1, u2, acc1, acc2);
+        if constexpr (NB == 2)  // the lane's block of A_0..A_2 held in registers
+          blku_contract<NB, GORD>([&](int j, int e) { return areg[j][e]; }, kr, ki, u1, u2, acc1, acc2);
+        else
+          blku_contract<NB, GORD>([&](int j, int e) { return ga[(j * E + e) * nblk + bc]; }, kr, ki, u1, u2, acc1,
+                                  acc2);
         acc1 = blku_group_sum(act ? acc1 : 0.0, NBP);
         acc2 = blku_group_sum(act ? acc2 : 0.0, NBP);
         if (be == 0 && jj < jn) {
@@ -828,7 +869,7 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
     if (FWD && penon) pen += pm ? xr * xr + xi * xi : 0.0;
   }
   // prologue: records of sequence chunks 0 and 1 in LDS, chunk 2's in flight, propagators of chunk 0
-  if (!chain) {
+  if (GORD > 0 ? stager : !chain) {
     rec_load(0);
     rec_store(0);
     if (nC > 1) {
@@ -836,11 +877,20 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       rec_store(1);
     }
     if (nC > 2) rec_load(2);
+    xs_load(0);
   }
   lds_barrier();
-  if (!chain) form(0);
+  if (!chain && !stager) form(0);
   lds_barrier();
-  if (chain) {
+  if (stager) {  // GORD: the staging loop
+    for (int c = 0; c < nC; ++c) {
+      if (c + 2 < nC) rec_store(c + 2);  // loaded one iteration ago
+      if (c + 3 < nC) rec_load(c + 3);
+      xs_store(c);  // read by grad(c) in the next iteration
+      if (c + 1 < nC) xs_load(c + 1);
+      lds_barrier();
+    }
+  } else if (chain) {
     // the state element's running pointer (lanes without one go to the sink with stride 0: no branch around stores)
     double* sp = ok ? Sb + (FWD ? 2 * Nm : (size_t)(Nt - 1) * 2 * Nm) + off : sink;
     const long long sst = ok ? (FWD ? 2 * (long long)Nm : -2 * (long long)Nm) : 0;
@@ -966,9 +1016,12 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   } else {
     for (int c = 0; c < nC; ++c) {
       BK_T(t0);
-      if (c + 2 < nC) rec_store(c + 2);  // loaded one iteration ago
-      if (c + 3 < nC) rec_load(c + 3);
-      xs_issue(c);  // GORD: read by grad(c) in the next iteration
+      if constexpr (GORD == 0) {
+        if (c + 2 < nC) rec_store(c + 2);  // loaded one iteration ago
+        if (c + 3 < nC) rec_load(c + 3);
+      }
+      BK_T(tf);
+      BK_ADD(6, tf - t0);
 #ifdef QOC_PROBE
       if (c + 1 < nC && bp.probe_mode != 1) form(c + 1);
 #else
@@ -980,7 +1033,6 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
 #else
       if (GORD > 0 && c > 0) grad(c - 1);
 #endif
-      if constexpr (GORD > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c's x landed before the barrier
       BK_T(t1);
       BK_ADD(5, t1 - tg);
       lds_barrier();
@@ -1076,7 +1128,8 @@ __global__ __launch_bounds__(256) void k_blku_grad(const TChainArgs g, const Blk
     blku_kacc<NB>(kr, ki, xv, lv);
   };
   auto contract = [&](const double (&kr)[E], const double (&ki)[E], double u1, double u2, double& acc1, double& acc2) {
-    blku_contract<NB, ORD>(G0, G1, G2, nblk, kr, ki, u1, u2, acc1, acc2);
+    blku_contract<NB, ORD>([&](int j, int e) { return (j == 0 ? G0 : j == 1 ? G1 : G2)[e * nblk]; }, kr, ki, u1, u2,
+                           acc1, acc2);
   };
   // per wave-iteration: the blocks of each unit reduce through the wave's LDS slot in a fixed order
   auto reduce_store = [&](long long base, bool act, double acc1, double acc2) {

@@ -165,34 +165,36 @@ struct BlkuShape {
   int C, CW, W, S;
   size_t lds;
 };
-// Waves per workgroup: CW chain waves (one lane per state element) and FW worker waves, sized so that a chunk's
-// worker VALU work -- forming C nblk propagators (~190 / 450 / 2600 operations each for NB = 2 / 3 / 4), and in the
-// fused backward (fused = true) also contracting C nblk gradient units (~250 / 500 / 1500) -- takes about as long as
-// the chain waves' C matvecs (4 NB^2 FMAs + ~20 per slice); QOC_BLKU_FW / QOC_BLKU_GFW override FW.  C: the most
-// slices per chunk (a power of two <= 64: chunks never straddle k_blku_rec's 64-slice (J, P) groups) whose LDS fits
-// the workgroups a CU holds at once (B / CUs of them, at most 3); QOC_BLKU_C / QOC_BLKU_GC override it.  S: the
-// prefix-product group (QOC_BLKU_S; 1 by default: the chains are store- or latency-bound at S = 1 and the scans
-// cost the workers more than they save).
+// Waves per workgroup: CW chain waves (one lane per state element), in the fused backward one staging wave, and FW
+// worker waves (formation, in the fused backward also the contraction).  The workers are the critical path (their
+// chunk of formation + contraction takes longer than the chain's C matvecs), so FW takes every wave slot left:
+// 8 waves per CU at the kernels' > 128 VGPRs (2 per SIMD), shared by the B / CUs workgroups a CU holds at once
+// (QOC_BLKU_FW / QOC_BLKU_GFW override FW).  C: the most slices per chunk (a power of two <= 64: chunks never
+// straddle k_blku_rec's 64-slice (J, P) groups) whose LDS fits those workgroups (QOC_BLKU_C / QOC_BLKU_GC override
+// it).  S: the prefix-product group (QOC_BLKU_S; 1 by default: the chains are store- or latency-bound at S = 1 and
+// the scans cost the workers more than they save).
 static BlkuShape blku_shape(const qoc_ctx* c, bool fused) {
   BlkuShape s{};
-  const int NB = c->blk_nb, E = NB * NB;
+  const int NB = c->blk_nb;
   s.CW = (c->nblk * c->m * (NB == 2 ? 2 : 4) + 63) / 64;  // one chain lane per state element (qoc_blku.hpp)
-  const double costU = NB == 2 ? 190.0 : NB == 3 ? 450.0 : 2600.0, costC = 4.0 * E + 20.0;
-  const double costG = fused ? (NB == 2 ? 250.0 : NB == 3 ? 500.0 : 1500.0) : 0.0;
-  int fw = (int)std::ceil(c->nblk * (costU + costG) / (64.0 * costC));
+  const int per_cu = std::max(1, std::min(3, (c->B + c->ncu - 1) / std::max(1, c->ncu)));
+  const int stg = fused ? 1 : 0;  // the fused backward's staging wave
+  const int wmax = std::max(s.CW + stg + 1, (NB == 4 ? 4 : 8) / per_cu);
+  int fw = wmax - s.CW - stg;
   if (const char* env = getenv(fused ? "QOC_BLKU_GFW" : "QOC_BLKU_FW")) fw = atoi(env);
-  fw = std::max(1, std::min(fw, (NB == 4 ? 4 : 8) - s.CW));
-  s.W = s.CW + fw;
+  fw = std::max(1, std::min(fw, (NB == 4 ? 4 : 8) - s.CW - stg));
+  s.W = s.CW + stg + fw;
   s.S = 1;
   if (const char* env = getenv("QOC_BLKU_S")) s.S = atoi(env) >= 2 && NB < 4 ? 2 : 1;
-  const int per_cu = std::max(1, std::min(3, (c->B + c->ncu - 1) / std::max(1, c->ncu)));
   const size_t budget = (size_t)156 * 1024 / per_cu;
   const int gw = fused ? fw : 0;
   s.C = 64;
-  while (s.C > 4 && blku_lds(c->N, c->m, NB, c->nblk, s.C, gw) > budget) s.C >>= 1;
+  while (s.C > 4 && (blku_lds(c->N, c->m, NB, c->nblk, s.C, gw) > budget ||
+                     (fused && s.C * c->N * c->m > BLKU_XMAX * 64)))  // the stager's x registers
+    s.C >>= 1;
   if (const char* env = getenv(fused ? "QOC_BLKU_GC" : "QOC_BLKU_C")) {
     int q = 1;
-    while (q * 2 <= std::min(atoi(env), 64)) q *= 2;
+    while (q * 2 <= std::min(atoi(env), 64) && (!fused || q * 2 * c->N * c->m <= BLKU_XMAX * 64)) q *= 2;
     s.C = q;
   }
   s.C = std::max(s.C, s.S);
@@ -570,6 +572,7 @@ static int blku_bwdg(qoc_ctx* c, int order, double* d_dJdu) {
   HIPCHK(c, hipMemcpyAsync(c->d_u_lam, c->d_u, nu_t * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_coef_lam, c->d_coef, ncf * sizeof(cx<double>), hipMemcpyDeviceToDevice, c->stream));
   c->L_lazy = true;
+  c->last_eval_mode = 5;
   return QOC_OK;
 }
 
@@ -630,7 +633,6 @@ static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
   }
   if (r) return r;
   c->L_is_mu = false;
-  c->last_eval_mode = 4;
   return QOC_OK;
 }
 

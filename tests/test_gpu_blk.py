@@ -104,7 +104,9 @@ def test_blocks_match_oracle_and_dense_chains(built_lib, monkeypatch, name, devi
     J, g = _eval(e, u, device)
     info = e.info()
     assert info["chain_kernel"] == KIND_KERNEL[kind], info
-    assert info["backward"] == ("blocks" if device else "generic"), info
+    # block propagators: the backward contracts the gradient itself (k_blku_bwdg) on both the fused eval and
+    # grape_sensitivity; the polynomial-in-the-chain kernels: the block chains' concurrent eval or the generic split
+    assert info["backward"] == ("fused" if kind == "prop" else "blocks" if device else "generic"), info
     xs = [e.state(k, seed=0) for k in (1, prob.Nt // 2, prob.Nt)]
     lams = [e.costate(k, seed=0) for k in (0, prob.Nt // 2, prob.Nt)]
     e.close()

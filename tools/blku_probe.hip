@@ -105,11 +105,12 @@ void run(int B, int Nt, int nblk, int m, int W, int C, int mode, bool bwdg) {
   }
   unsigned long long tc[16];
   (void)hipMemcpyFromSymbol(tc, HIP_SYMBOL(g_bk), sizeof(tc));
-  const int nC = (Nt + C - 1) / C, fw = W - bp.CW;
+  const int nC = (Nt + C - 1) / C, fw = W - bp.CW - (bwdg ? 1 : 0);  // bwdg: one staging wave
   printf("%s NB=%d S=%d B=%d Nt=%d W=%d C=%2d mode=%d lds=%6zu: %.4f ms  per chunk (cycles): chain %6.0f  wait %6.0f"
-         " | worker %6.0f  grad %6.0f  wait %6.0f\n",
+         " | worker %6.0f  (recs %5.0f  grad %6.0f)  wait %6.0f\n",
          bwdg ? "bwdg" : "fwd ", NB, S, B, Nt, W, C, mode, lds, ms, tc[0] / (double)nC / bp.CW,
-         tc[1] / (double)nC / bp.CW, tc[3] / (double)nC / fw, tc[5] / (double)nC / fw, tc[4] / (double)nC / fw);
+         tc[1] / (double)nC / bp.CW, tc[3] / (double)nC / fw, tc[6] / (double)nC / fw, tc[5] / (double)nC / fw,
+         tc[4] / (double)nC / fw);
   (void)hipFree(dA); (void)hipFree(du); (void)hipFree(dx0); (void)hipFree(dX); (void)hipFree(dL); (void)hipFree(dcoef);
   (void)hipFree(dJ); (void)hipFree(dsink); (void)hipFree(dbrow); (void)hipFree(dterms); (void)hipFree(drec); (void)hipFree(ddJ);
 }
@@ -122,7 +123,7 @@ int main(int argc, char** argv) {
   const int W0 = NB == 2 ? 2 : 1;  // chain waves
   for (int bw : {0, 1})
     for (int mode : {0, 1, 2, 3, 5})
-      for (int W = W0 + 1; W <= 8; ++W)
+      for (int W = W0 + 1 + bw; W <= 8; ++W)
         for (int C : {8, 16, 32}) {
           if ((mode == 3 && bw) || (mode == 5 && !bw)) continue;
           if (mode && (W != W0 + 4 || C != 16)) continue;
