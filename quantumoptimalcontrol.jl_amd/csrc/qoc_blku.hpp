@@ -752,20 +752,27 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       }
     }
   };
+  // the gradient lane's block rows, read once (a global load inside the per-chunk contraction would expose its
+  // latency every chunk)
+  const int NBP = blku_nbp(nblk);
+  int grow[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int be = (tid & 63) % NBP;
+    grow[i] = GORD > 0 && be < nblk ? bk.brow[be * NB + i] : -1;
+  }
   // the fused gradient of sequence chunk cq (GORD > 0): the worker waves take 64 / nblk slices per wave-iteration, a
   // lane per (slice, block); K = Σ_c x_k λ_{k+1}^H from x_k in HBM and λ_{k+1} in the ring slot cq & 1, then
   // Re tr(A_j M) reduced over the blocks through the wave's LDS slot in a fixed order
   auto grad = [&](int cq) {
     if constexpr (GORD > 0) {
       const int a = chunk_of(cq), jn = min(C, Nt - a * C), gw = w - bp.CW - STG, GW = (nthr >> 6) - bp.CW - STG;
-      const int l = tid & 63, NBP = blku_nbp(nblk), UPW = 64 / NBP, ul = l / NBP, be = l - ul * NBP;
+      const int l = tid & 63, UPW = 64 / NBP, ul = l / NBP, be = l - ul * NBP;
       const int bc = min(be, nblk - 1);
       const double2* lr = lam + (size_t)(cq & 1) * C * Nm;
       const double2* xq = xring + (size_t)(cq & 1) * CNp;
       const double* rq = recs + (size_t)(cq & 3) * C * BLKU_REC;
-      int r[NB];
-#pragma unroll
-      for (int i = 0; i < NB; ++i) r[i] = be < nblk ? bk.brow[be * NB + i] : -1;
+      const int(&r)[NB] = grow;
       double2 areg[3][NB == 2 ? E : 1];
       if constexpr (NB == 2)
 #pragma unroll
