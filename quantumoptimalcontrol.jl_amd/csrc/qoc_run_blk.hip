@@ -630,6 +630,7 @@ static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
     mark_end(c, mb);
     if (eb != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_bwd launch: %s", hipGetErrorString(eb));
     r = blku_grad(c, order, false, d_dJdu);
+    c->last_eval_mode = 4;  // the block chains' eval, λ in HBM
   }
   if (r) return r;
   c->L_is_mu = false;

@@ -130,9 +130,9 @@ int tchain_prep(qoc_ctx* c) {
   }
   int mk = mark_begin(c, 0);
   const unsigned pb = (unsigned)std::min<long long>((units + 255) / 256, 2048);
-  if (cheb)
-    hipLaunchKernelGGL(k_tchain_prep_cheb, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u,
-                       c->tprm, c->d_steps, c->d_tcoef, c->d_terms);
+  if (cheb)  // one wave per workgroup (the coefficient rows are staged in its LDS)
+    hipLaunchKernelGGL(k_tchain_prep_cheb, dim3((unsigned)std::min<long long>((units + 63) / 64, 8192)), dim3(64), 0,
+                       c->stream, c->nu, units, (const double*)c->d_u, c->tprm, c->d_steps, c->d_tcoef, c->d_terms);
   else
     hipLaunchKernelGGL(k_tchain_prep, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u, c->tprm,
                        c->d_steps, c->d_terms);

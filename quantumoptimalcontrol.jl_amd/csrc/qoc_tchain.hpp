@@ -285,37 +285,62 @@ __device__ int cheb_series(double rho, double tol, double* __restrict__ ce, int 
   return P;
 }
 
-static __global__ void k_tchain_prep_cheb(int nu, long long units, const double* __restrict__ u, const TChainParams prm,
-                                   TStep* __restrict__ steps, double* __restrict__ coef,
-                                   unsigned long long* __restrict__ terms) {
+// One wave per workgroup, 64 consecutive (seed, slice) units per wave-iteration.  The coefficients are computed into
+// an LDS row per lane (65-double stride: conflict-free columns) and leave the wave as one coalesced block -- rows
+// e0 .. e0+63 are contiguous in HBM -- of the first PW = max(P + 1) entries of each row (the chains read 0 .. P).
+// Per-lane strided 8-byte stores straight to HBM left partially written lines L2 several times over (4x the
+// record bytes on the tunable bus).  Entries P+1 .. PW-1 are zero.
+constexpr int TCHEB_LDS_STRIDE = TCHEB_STRIDE + 1;
+static __global__ __launch_bounds__(64) void k_tchain_prep_cheb(int nu, long long units, const double* __restrict__ u,
+                                                                const TChainParams prm, TStep* __restrict__ steps,
+                                                                double* __restrict__ coef,
+                                                                unsigned long long* __restrict__ terms) {
+  __shared__ double rows[64 * TCHEB_LDS_STRIDE];
+  const int l = threadIdx.x;
+  double* ce = rows + l * TCHEB_LDS_STRIDE;
   unsigned long long cnt = 0;
   const double tol = 1.1102230246251565e-16;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < units; e += (long long)gridDim.x * blockDim.x) {
-    double beta = prm.rad[0], mr = prm.mur[0], mi = prm.mui[0];  // ρ_k >= the spectral radius of H̃_k (Weyl)
-    for (int j = 0; j < nu; ++j) {
-      const double uj = u[e * nu + j];
-      beta += fabs(uj) * prm.rad[j + 1];
-      mr += uj * prm.mur[j + 1];
-      mi += uj * prm.mui[j + 1];
+  for (long long e0 = (long long)blockIdx.x * 64; e0 < units; e0 += (long long)gridDim.x * 64) {
+    const long long e = e0 + l;
+    const bool valid = e < units;
+    for (int t = 0; t < TCHEB_STRIDE; ++t) ce[t] = 0.0;
+    int P = -1;
+    if (valid) {
+      double beta = prm.rad[0], mr = prm.mur[0], mi = prm.mui[0];  // ρ_k >= the spectral radius of H̃_k (Weyl)
+      for (int j = 0; j < nu; ++j) {
+        const double uj = u[e * nu + j];
+        beta += fabs(uj) * prm.rad[j + 1];
+        mr += uj * prm.mur[j + 1];
+        mi += uj * prm.mui[j + 1];
+      }
+      beta = fmax(beta, 1e-300);
+      int s = 1;
+      if (beta > 25.0) s = (int)ceil(beta / 25.0);  // substeps only beyond ρ = 25 (P <= 58 < TCHEB_PMAX)
+      const double rho = beta / s;
+      if (rho <= 2.0) {
+        P = cheb_series(rho, tol, ce, prm.pmin);
+      } else {
+        P = cheb_miller(rho, tol, ce);  // every coefficient 0..TCHEB_PMAX written
+        if (P < prm.pmin) P = prm.pmin;
+      }
+      const double er = exp(mr);
+      steps[e] = TStep{er * cos(mi), er * sin(mi), P, s, 2.0 / beta};
+      cnt += (unsigned long long)(P * s);
     }
-    beta = fmax(beta, 1e-300);
-    int s = 1;
-    if (beta > 25.0) s = (int)ceil(beta / 25.0);  // substeps only beyond ρ = 25 (P <= 58 < TCHEB_PMAX)
-    const double rho = beta / s;
-    double* ce = coef + (size_t)e * TCHEB_STRIDE;
-    int P = 0;
-    if (rho <= 2.0) {
-      P = cheb_series(rho, tol, ce, prm.pmin);
-    } else {
-      P = cheb_miller(rho, tol, ce);  // every coefficient 0..TCHEB_PMAX written
-      if (P < prm.pmin) P = prm.pmin;
+    int pw = P + 1;
+    for (int o = 32; o > 0; o >>= 1) pw = max(pw, __shfl_xor(pw, o));
+    pw = min((pw + 1) & ~1, TCHEB_STRIDE);
+    __syncthreads();
+    const int nrow = (int)min<long long>(64, units - e0);
+    double* dst = coef + (size_t)e0 * TCHEB_STRIDE;
+    for (int f = l; f < nrow * pw; f += 64) {
+      const int r = f / pw, j = f - r * pw;
+      dst[(size_t)r * TCHEB_STRIDE + j] = rows[r * TCHEB_LDS_STRIDE + j];
     }
-    const double er = exp(mr);
-    steps[e] = TStep{er * cos(mi), er * sin(mi), P, s, 2.0 / beta};
-    cnt += (unsigned long long)(P * s);
+    __syncthreads();
   }
   for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(terms, cnt);
+  if (l == 0 && cnt) atomicAdd(terms, cnt);
 }
 
 struct TChainArgs {

@@ -54,15 +54,20 @@ BLK = ("blocks", "blocks_mfma", "blocks_prop")
 # chain kernel of each block variant: block propagators formed apart from the chain (qoc_blku.hpp, the default for
 # blocks of <= 4 rows), the polynomial inside the recurrence on MFMA block waves (QOC_BLKU=0), on the real embedding
 # (QOC_BLOCKS=real), on VALU lanes (QOC_BLOCKS=valu)
-KIND_KERNEL = {"prop": "blocks_prop", "mfma": "blocks_mfma", "real": "blocks_mfma", "valu": "blocks"}
+KIND_KERNEL = {"prop": "blocks_prop", "propsplit": "blocks_prop", "props2": "blocks_prop", "mfma": "blocks_mfma",
+               "real": "blocks_mfma", "valu": "blocks"}
 
 
 def _engine(prob, B, blocks, monkeypatch, penalty=None, chain="taylor"):
-    """blocks: True / "prop" (default kernels), "mfma" (MFMA block waves, complex slots), "real" (blocks of <= 2 rows
-    on their real embedding), "valu" (blocks of <= 4 rows on VALU lanes), False (dense)."""
+    """blocks: True / "prop" (default kernels: block propagators, fused backward), "propsplit" (block propagators,
+    plain backward chain + separate gradient), "props2" (block propagators with prefix-product groups of 2 slices),
+    "mfma" (MFMA block waves, complex slots), "real" (blocks of <= 2 rows on their real embedding), "valu" (blocks
+    of <= 4 rows on VALU lanes), False (dense)."""
     from qoc_amd import GrapeEngine
     monkeypatch.setenv("QOC_BLOCKS", blocks if blocks in ("valu", "real") else "1" if blocks else "0")
     monkeypatch.setenv("QOC_BLKU", "0" if blocks == "mfma" else "1")
+    monkeypatch.setenv("QOC_BLKU_FUSED", "0" if blocks == "propsplit" else "1")
+    monkeypatch.setenv("QOC_BLKU_S", "2" if blocks == "props2" else "1")
     e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
     e.set_cost_trace(prob.x_target, prob.n)
     e.set_chain(chain)
@@ -93,7 +98,7 @@ def _assert_seed(J, g, Jr, gr, tag):
 
 @pytest.mark.parametrize("name", ["zz", "cavity20", "cavity40"])
 @pytest.mark.parametrize("device", [False, True])
-@pytest.mark.parametrize("kind", ["prop", "mfma", "real", "valu"])
+@pytest.mark.parametrize("kind", ["prop", "propsplit", "props2", "mfma", "real", "valu"])
 def test_blocks_match_oracle_and_dense_chains(built_lib, monkeypatch, name, device, kind):
     """Blocks of <= 4 rows: block propagators formed apart from the chain (default), or the polynomial inside the
     recurrence: packed into the 4-row slots of MFMA block waves, or one VALU lane per (block, column)
@@ -106,7 +111,7 @@ def test_blocks_match_oracle_and_dense_chains(built_lib, monkeypatch, name, devi
     assert info["chain_kernel"] == KIND_KERNEL[kind], info
     # block propagators: the backward contracts the gradient itself (k_blku_bwdg) on both the fused eval and
     # grape_sensitivity; the polynomial-in-the-chain kernels: the block chains' concurrent eval or the generic split
-    assert info["backward"] == ("fused" if kind == "prop" else "blocks" if device else "generic"), info
+    assert info["backward"] == ("fused" if kind in ("prop", "props2") else "blocks" if device else "generic"), info
     xs = [e.state(k, seed=0) for k in (1, prob.Nt // 2, prob.Nt)]
     lams = [e.costate(k, seed=0) for k in (0, prob.Nt // 2, prob.Nt)]
     e.close()
@@ -129,7 +134,7 @@ def test_blocks_match_oracle_and_dense_chains(built_lib, monkeypatch, name, devi
 
 @pytest.mark.parametrize("order", [1, 2, 3, 4, "exact"])
 @pytest.mark.parametrize("device", [False, True])
-@pytest.mark.parametrize("kind", ["prop", "mfma"])
+@pytest.mark.parametrize("kind", ["prop", "propsplit", "mfma"])
 def test_blocks_gradient_orders(built_lib, monkeypatch, order, device, kind):
     """expm_jacobian! orders 1..4 (src/gradient_computations.jl:177-213) in the block gradient; the exact Fréchet
     gradient (opt-in) runs its dense kernel on the block chains' states and co-states."""
@@ -181,7 +186,7 @@ def test_blocks_penalty_and_costate_source(built_lib, monkeypatch, poly, kind):
 
 @pytest.mark.parametrize("NB,nu,m", [(4, 2, 3), (4, 1, 1), (3, 2, 2), (2, 1, 5), (2, 2, 8)])
 @pytest.mark.parametrize("poly", ["taylor", "chebyshev"])
-@pytest.mark.parametrize("kind", ["prop", "mfma", "real", "valu"])
+@pytest.mark.parametrize("kind", ["prop", "propsplit", "props2", "mfma", "real", "valu"])
 def test_blocks_random_permuted_blocks(built_lib, monkeypatch, NB, nu, m, poly, kind):
     """Random block-diagonal skew-Hermitian generators hidden by a permutation (the detection works on the pattern,
     not on contiguous rows), a short last block (padding lanes), one or two controls, odd column counts."""
