@@ -157,6 +157,10 @@ bool blku_on(const qoc_ctx* c) {
   if (!blk_active(c) || c->blk_jr != 1 || c->blk_nb > BLK_NBMAX || c->nu < 1 || c->nu > 2 || c->nblk > 32 ||
       c->nblk * c->m * (c->blk_nb == 2 ? 2 : 4) > 64 * (c->blk_nb == 4 ? 2 : 4))
     return false;
+  // an explicit QOC_BLOCKS=valu / real keeps the polynomial-in-the-chain kernels, also where it falls back to the
+  // complex MFMA slots (real with blocks of more than 2 rows)
+  const char* bl = getenv("QOC_BLOCKS");
+  if (bl && (!std::strcmp(bl, "valu") || !std::strcmp(bl, "real"))) return false;
   const char* env = getenv("QOC_BLKU");
   return !(env && !std::strcmp(env, "0"));
 }
