@@ -43,6 +43,8 @@ struct BlkuParams {
   const double* rec;               // B x Ntp x BLKU_REC step records (k_blku_rec)
   unsigned long long* terms;       // Σ_k P_k 2^J_k per forward pass (k_blku_rec; nullptr: not counted)
   double* dJdu;                    // B x Nt x nu: the fused backward's gradient (k_blku_bwdg)
+  double2* Uout;                   // k_blku_fwd (S = 1): also store each slice's block propagators, B x Nt x NB^2 x nblk
+  const double2* Uin;              // k_blku_bwdg: read them instead of forming (the staging wave copies them to LDS)
   int probe_mode;                  // QOC_PROBE builds only: 1 skip the formation, 2 the chain, 3 the chain's stores,
                                    // 4 the chain's LDS reads
 };
@@ -652,11 +654,14 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   // the fused backward has one staging wave (wave CW) between the chain and the worker waves: it moves the step
   // records and x_k global -> registers -> LDS one iteration apart, so that neither the chain (whose first matvec of a
   // chunk would wait on the loads) nor the workers (whose registers go to the formation and the contraction) wait
-  constexpr int STG = GORD > 0 ? 1 : 0;
-  const bool stager = GORD > 0 && w == bp.CW;
+  // With stored propagators (bp.Uin) a second staging wave copies them (each stager holds one chunk's worth of
+  // registers: two in one wave would spill).
+  const int STG = GORD > 0 ? (bp.Uin ? 2 : 1) : 0;
+  const bool stager = GORD > 0 && w >= bp.CW && w < bp.CW + STG;
+  const int stg_i = w - bp.CW;  // 0: step records and x_k, 1: propagators
   const int fl = tid - 64 * (bp.CW + STG), FL = nthr - 64 * (bp.CW + STG);  // formation lanes
-  // staging lanes (global -> registers, one iteration later registers -> LDS): the stager, else the worker lanes
-  const int sl = GORD > 0 ? tid - 64 * bp.CW : fl, SLN = GORD > 0 ? 64 : FL;
+  // staging lanes (global -> registers, one iteration later registers -> LDS): a stager, else the worker lanes
+  const int sl = GORD > 0 ? (tid & 63) : fl, SLN = GORD > 0 ? 64 : FL;
   // step records of sequence chunk c: C x REC doubles from k_blku_rec (the tail of a partial chunk: clamped reads,
   // never used), through registers into the LDS ring slot c & 3
   constexpr int RMAX = 8;  // loads per lane: 64 x REC doubles / 64 lanes at most
@@ -716,6 +721,11 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
           double2* o = Uc + (size_t)pp[u] * E * nblk + be[u];
 #pragma unroll
           for (int e = 0; e < E; ++e) o[e * nblk] = make_double2(ur[u][e], ui[u][e]);
+          if (FWD && S == 1 && bp.Uout) {  // the same layout in HBM, at the absolute slice (coalesced over blocks)
+            double2* og = bp.Uout + ((size_t)b * Nt + (size_t)chunk_of(c) * C + pp[u]) * E * nblk + be[u];
+#pragma unroll
+            for (int e = 0; e < E; ++e) og[e * nblk] = make_double2(ur[u][e], ui[u][e]);
+          }
         }
     }
   };
@@ -752,6 +762,30 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       }
     }
   };
+  // the stored propagators of sequence chunk cq (GORD > 0 with bp.Uin): global -> stager registers -> the U slot
+  // cq & 1, one iteration apart (the chunk's jn NB^2 nblk complex are contiguous in HBM and in LDS)
+  constexpr int UMAX = GORD > 0 ? BLKU_XMAX : 1;
+  dv2 ureg[UMAX];
+  const bool uin = GORD > 0 && bp.Uin != nullptr;
+  auto us_load = [&](int cq) {
+    if constexpr (GORD > 0) {
+      const int a = chunk_of(cq), n = min(C, Nt - a * C) * E * nblk;
+      const double2* src = bp.Uin + ((size_t)b * Nt + (size_t)a * C) * E * nblk;
+#pragma unroll
+      for (int i = 0; i < UMAX; ++i)  // clamped, unconditional
+        ureg[i] = *reinterpret_cast<const dv2*>(src + min(sl + i * SLN, n - 1));
+    }
+  };
+  auto us_store = [&](int cq) {
+    if constexpr (GORD > 0) {
+      double2* dst = Ub + (size_t)(cq & 1) * C * E * nblk;
+#pragma unroll
+      for (int i = 0; i < UMAX; ++i) {
+        const int e = sl + i * SLN;
+        if (e < C * E * nblk) *reinterpret_cast<dv2*>(dst + e) = ureg[i];
+      }
+    }
+  };
   // the gradient lane's block rows, read once (a global load inside the per-chunk contraction would expose its
   // latency every chunk)
   const int NBP = blku_nbp(nblk);
@@ -779,46 +813,69 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
         for (int j = 0; j < 3; ++j)
 #pragma unroll
           for (int e = 0; e < E; ++e) areg[j][e] = ga[(j * E + e) * nblk + bc];
-      for (int it = gw; it * UPW < jn; it += GW) {
-        const int jj = it * UPW + ul;
-        const bool act = be < nblk && jj < jn;
-        const int jc = jj < jn ? jj : 0;
-        // u_k from the step record (2^-J u_j scaled back by 2^J: exact), x_k from the x ring, λ_{k+1} from the λ ring
-        const double* rk = rq + (size_t)jc * BLKU_REC;
-        const int Jk = (int)rk[6];
-        const double u1 = ldexp(rk[3], Jk), u2 = ldexp(rk[4], Jk);
-        const double2* xs = xq + (size_t)jc * Nm;
-        const double2* ls = lr + (size_t)jc * Nm;
-        double kr[E], ki[E];
+      // GU wave-iterations per pass, their units interleaved per lane (GU = 2 measured no faster on cavity: the
+      // workers are issue-bound, not latency-bound)
+      constexpr int GU = 1;
+      for (int it0 = gw; it0 * UPW < jn; it0 += GU * GW) {
+        int jjv[GU];
+        double u1[GU], u2[GU], kr[GU][E], ki[GU][E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) kr[e] = ki[e] = 0.0;
+        for (int gi = 0; gi < GU; ++gi) {
+          const int jj = (it0 + gi * GW) * UPW + ul;
+          jjv[gi] = jj;
+          const int jc = jj < jn ? jj : 0;
+          // u_k from the step record (2^-J u_j scaled back by 2^J: exact)
+          const double* rk = rq + (size_t)jc * BLKU_REC;
+          const int Jk = (int)rk[6];
+          u1[gi] = ldexp(rk[3], Jk);
+          u2[gi] = ldexp(rk[4], Jk);
+#pragma unroll
+          for (int e = 0; e < E; ++e) kr[gi][e] = ki[gi][e] = 0.0;
+        }
+        // K = Σ_c x_c λ_c^H from x_k in the x ring and λ_{k+1} in the λ ring
         constexpr int CB = NB == 2 ? 2 : 1;  // columns whose loads are in flight at once (a missing one: zeros)
         for (int c0 = 0; c0 < m; c0 += CB) {
-          double2 xv[CB][NB], lv[CB][NB];
+          double2 xv[GU][CB][NB], lv[GU][CB][NB];
 #pragma unroll
-          for (int cc = 0; cc < CB; ++cc)
+          for (int gi = 0; gi < GU; ++gi) {
+            const int jc = jjv[gi] < jn ? jjv[gi] : 0;
+            const double2* xs = xq + (size_t)jc * Nm;
+            const double2* ls = lr + (size_t)jc * Nm;
 #pragma unroll
-            for (int i = 0; i < NB; ++i) {
-              const bool v = r[i] >= 0 && c0 + cc < m;
-              const int o = v ? (c0 + cc) * N + r[i] : 0;
-              xv[cc][i] = v ? xs[o] : make_double2(0.0, 0.0);
-              lv[cc][i] = v ? ls[o] : make_double2(0.0, 0.0);
-            }
+            for (int cc = 0; cc < CB; ++cc)
 #pragma unroll
-          for (int cc = 0; cc < CB; ++cc) blku_kacc<NB>(kr, ki, xv[cc], lv[cc]);
+              for (int i = 0; i < NB; ++i) {
+                const bool v = r[i] >= 0 && c0 + cc < m;
+                const int o = v ? (c0 + cc) * N + r[i] : 0;
+                xv[gi][cc][i] = v ? xs[o] : make_double2(0.0, 0.0);
+                lv[gi][cc][i] = v ? ls[o] : make_double2(0.0, 0.0);
+              }
+          }
+#pragma unroll
+          for (int gi = 0; gi < GU; ++gi)
+#pragma unroll
+            for (int cc = 0; cc < CB; ++cc) blku_kacc<NB>(kr[gi], ki[gi], xv[gi][cc], lv[gi][cc]);
         }
-        double acc1, acc2;
-        if constexpr (NB == 2)  // the lane's block of A_0..A_2 held in registers
-          blku_contract<NB, GORD>([&](int j, int e) { return areg[j][e]; }, kr, ki, u1, u2, acc1, acc2);
-        else
-          blku_contract<NB, GORD>([&](int j, int e) { return ga[(j * E + e) * nblk + bc]; }, kr, ki, u1, u2, acc1,
-                                  acc2);
-        acc1 = blku_group_sum(act ? acc1 : 0.0, NBP);
-        acc2 = blku_group_sum(act ? acc2 : 0.0, NBP);
-        if (be == 0 && jj < jn) {
-          double* o = bp.dJdu + ((size_t)b * Nt + a * C + jj) * nu;
-          o[0] = acc1;
-          if (nu > 1) o[1] = acc2;
+        double acc1[GU], acc2[GU];
+#pragma unroll
+        for (int gi = 0; gi < GU; ++gi) {
+          if constexpr (NB == 2)  // the lane's block of A_0..A_2 held in registers
+            blku_contract<NB, GORD>([&](int j, int e) { return areg[j][e]; }, kr[gi], ki[gi], u1[gi], u2[gi],
+                                    acc1[gi], acc2[gi]);
+          else
+            blku_contract<NB, GORD>([&](int j, int e) { return ga[(j * E + e) * nblk + bc]; }, kr[gi], ki[gi],
+                                    u1[gi], u2[gi], acc1[gi], acc2[gi]);
+        }
+#pragma unroll
+        for (int gi = 0; gi < GU; ++gi) {
+          const bool act = be < nblk && jjv[gi] < jn;
+          const double s1 = blku_group_sum(act ? acc1[gi] : 0.0, NBP);
+          const double s2 = blku_group_sum(act ? acc2[gi] : 0.0, NBP);
+          if (be == 0 && jjv[gi] < jn) {
+            double* o = bp.dJdu + ((size_t)b * Nt + a * C + jjv[gi]) * nu;
+            o[0] = s1;
+            if (nu > 1) o[1] = s2;
+          }
         }
       }
     }
@@ -875,8 +932,19 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
     *reinterpret_cast<double2*>(p) = make_double2(xr, xi);
     if (FWD && penon) pen += pm ? xr * xr + xi * xi : 0.0;
   }
-  // prologue: records of sequence chunks 0 and 1 in LDS, chunk 2's in flight, propagators of chunk 0
-  if (GORD > 0 ? stager : !chain) {
+  // prologue: records of sequence chunks 0 and 1 in LDS, chunk 2's in flight, propagators of chunk 0.  The fused
+  // backward's stagers run their prologue inside their own branch, so that their staging registers are not live
+  // across the workers' first formation.
+  if (GORD == 0 && !chain) {
+    rec_load(0);
+    rec_store(0);
+    if (nC > 1) {
+      rec_load(1);
+      rec_store(1);
+    }
+    if (nC > 2) rec_load(2);
+  }
+  if (stager && stg_i == 0) {  // GORD: the staging loops (two prologue barriers of their own)
     rec_load(0);
     rec_store(0);
     if (nC > 1) {
@@ -885,11 +953,8 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
     }
     if (nC > 2) rec_load(2);
     xs_load(0);
-  }
-  lds_barrier();
-  if (!chain && !stager) form(0);
-  lds_barrier();
-  if (stager) {  // GORD: the staging loop
+    lds_barrier();
+    lds_barrier();
     for (int c = 0; c < nC; ++c) {
       if (c + 2 < nC) rec_store(c + 2);  // loaded one iteration ago
       if (c + 3 < nC) rec_load(c + 3);
@@ -897,7 +962,24 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       if (c + 1 < nC) xs_load(c + 1);
       lds_barrier();
     }
-  } else if (chain) {
+  } else if (stager) {
+    us_load(0);
+    us_store(0);
+    if (nC > 1) us_load(1);
+    lds_barrier();
+    lds_barrier();
+    for (int c = 0; c < nC; ++c) {
+      if (c + 1 < nC) {
+        us_store(c + 1);  // read by the chain in the next iteration
+        if (c + 2 < nC) us_load(c + 2);
+      }
+      lds_barrier();
+    }
+  } else {
+  lds_barrier();
+  if (!chain && !uin) form(0);
+  lds_barrier();
+  if (chain) {
     // the state element's running pointer (lanes without one go to the sink with stride 0: no branch around stores)
     double* sp = ok ? Sb + (FWD ? 2 * Nm : (size_t)(Nt - 1) * 2 * Nm) + off : sink;
     const long long sst = ok ? (FWD ? 2 * (long long)Nm : -2 * (long long)Nm) : 0;
@@ -1030,9 +1112,9 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       BK_T(tf);
       BK_ADD(6, tf - t0);
 #ifdef QOC_PROBE
-      if (c + 1 < nC && bp.probe_mode != 1) form(c + 1);
+      if (c + 1 < nC && bp.probe_mode != 1 && !uin) form(c + 1);
 #else
-      if (c + 1 < nC) form(c + 1);
+      if (c + 1 < nC && !uin) form(c + 1);
 #endif
       BK_T(tg);
 #ifdef QOC_PROBE
@@ -1049,6 +1131,7 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
     }
     grad(nC - 1);  // GORD: the last chunk, after the chain's final barrier
   }
+  }  // chain / worker waves
   if (FWD) {
     if (ok) {
       xN[off] = xr;

@@ -152,6 +152,7 @@ struct qoc_ctx {
   bool L_lazy = false;           // the fused block backward left d_L unwritten: qoc_get_costates rebuilds it
                                  // (blku_costates) from the saved u and λ_N coefficients
   double* d_u_lam = nullptr;     // B x Nt x nu: u of that backward
+  void* d_blkU = nullptr;        // B x Nt x NB^2 x nblk complex: block propagators of the eval's forward (fused backward)
   cx<double>* d_coef_lam = nullptr;  // B x 2m: its λ_N coefficients
   cx<double>* d_coef_mu = nullptr;  // B x 2m: the λ_N coefficients of the eval that left μ in d_L
   int last_eval_mode = 0;        // 0 other, 1 captured sequential backward, 2 / 3 concurrent μ mode: two streams /

@@ -177,12 +177,12 @@ struct BlkuShape {
 // straddle k_blku_rec's 64-slice (J, P) groups) whose LDS fits those workgroups (QOC_BLKU_C / QOC_BLKU_GC override
 // it).  S: the prefix-product group (QOC_BLKU_S; 1 by default: the chains are store- or latency-bound at S = 1 and
 // the scans cost the workers more than they save).
-static BlkuShape blku_shape(const qoc_ctx* c, bool fused) {
+static BlkuShape blku_shape(const qoc_ctx* c, bool fused, bool storeu = false) {
   BlkuShape s{};
   const int NB = c->blk_nb;
   s.CW = (c->nblk * c->m * (NB == 2 ? 2 : 4) + 63) / 64;  // one chain lane per state element (qoc_blku.hpp)
   const int per_cu = std::max(1, std::min(3, (c->B + c->ncu - 1) / std::max(1, c->ncu)));
-  const int stg = fused ? 1 : 0;  // the fused backward's staging wave
+  const int stg = fused ? (storeu ? 2 : 1) : 0;  // the fused backward's staging waves
   const int wmax = std::max(s.CW + stg + 1, (NB == 4 ? 4 : 8) / per_cu);
   int fw = wmax - s.CW - stg;
   if (const char* env = getenv(fused ? "QOC_BLKU_GFW" : "QOC_BLKU_FW")) fw = atoi(env);
@@ -193,12 +193,12 @@ static BlkuShape blku_shape(const qoc_ctx* c, bool fused) {
   const size_t budget = (size_t)156 * 1024 / per_cu;
   const int gw = fused ? fw : 0;
   s.C = 64;
-  while (s.C > 4 && (blku_lds(c->N, c->m, NB, c->nblk, s.C, gw) > budget ||
-                     (fused && s.C * c->N * c->m > BLKU_XMAX * 64)))  // the stager's x registers
-    s.C >>= 1;
+  // the stager's registers: x_k and the stored propagators of one chunk
+  auto stage_ok = [&](int C) { return !fused || std::max(C * c->N * c->m, C * NB * NB * c->nblk) <= BLKU_XMAX * 64; };
+  while (s.C > 4 && (blku_lds(c->N, c->m, NB, c->nblk, s.C, gw) > budget || !stage_ok(s.C))) s.C >>= 1;
   if (const char* env = getenv(fused ? "QOC_BLKU_GC" : "QOC_BLKU_C")) {
     int q = 1;
-    while (q * 2 <= std::min(atoi(env), 64) && (!fused || q * 2 * c->N * c->m <= BLKU_XMAX * 64)) q *= 2;
+    while (q * 2 <= std::min(atoi(env), 64) && stage_ok(q * 2)) q *= 2;
     s.C = q;
   }
   s.C = std::max(s.C, s.S);
@@ -545,11 +545,12 @@ static bool blku_fused_ok(const qoc_ctx* c, int order) {
   return order >= 1 && order <= BLK_ORDMAX && c->mu == 0.0 && !c->src_on && !(env && !std::strcmp(env, "0"));
 }
 
-static int blku_bwdg(qoc_ctx* c, int order, double* d_dJdu) {
+static int blku_bwdg(qoc_ctx* c, int order, double* d_dJdu, const double2* Uin = nullptr) {
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
-  const BlkuShape s = blku_shape(c, true);
-  const BlkuParams bp = blku_params(c, s, d_dJdu);  // the records are current (the caller's)
+  const BlkuShape s = blku_shape(c, true, Uin != nullptr);
+  BlkuParams bp = blku_params(c, s, d_dJdu);  // the records are current (the caller's)
+  bp.Uin = Uin;
   const int mk = mark_begin(c, 2);
   const hipError_t e = blku_dispatch(c, [&](auto NB_) {
     constexpr int NB = decltype(NB_)::value;
@@ -620,14 +621,25 @@ static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
   BlkuParams bp = blku_params(c, s);
   int r = blku_records(c, bp, true);
   if (r) return r;
+  // the forward also stores the block propagators for the fused backward (which then forms none): S = 1 only (with
+  // prefix groups the chunks hold products); QOC_BLKU_STOREU=0 keeps the backward forming its own
+  const char* su = getenv("QOC_BLKU_STOREU");
+  const bool fused = blku_fused_ok(c, order);
+  const bool storeu = fused && s.S == 1 && !(su && !std::strcmp(su, "0"));
+  if (storeu && !c->d_blkU) {
+    const size_t bytes = (size_t)c->B * c->Nt * c->blk_nb * c->blk_nb * c->nblk * sizeof(double2);
+    HIPCHK(c, hipMalloc((void**)&c->d_blkU, bytes));
+    c->dev_bytes += bytes;
+  }
+  bp.Uout = storeu ? (double2*)c->d_blkU : nullptr;
   const int mk = mark_begin(c, 1);
   const hipError_t e = blku_launch_fwd(c, s, bp);
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_fwd launch: %s", hipGetErrorString(e));
   c->fwd_captured = false;
   c->props_since_reset++;
-  if (blku_fused_ok(c, order)) {
-    r = blku_bwdg(c, order, d_dJdu);
+  if (fused) {
+    r = blku_bwdg(c, order, d_dJdu, storeu ? (const double2*)c->d_blkU : nullptr);
   } else {
     const int mb = mark_begin(c, 2);
     const hipError_t eb = blku_launch_bwd(c, tchain_args(c), s, bp, false);
