@@ -183,14 +183,14 @@ __global__ __launch_bounds__(256) void k_blku_rec(const BlkuParams bp, const dou
     r[2] = make_double2(sc * u2, (double)P);
     r[3] = make_double2((double)J, 0.0);
   }
-  if (bp.terms) {  // one atomic per workgroup (one per wave serialises thousands of them on one address)
+  if (bp.terms) {  // one atomic per workgroup, into the workgroup's partial-sum word
     __shared__ unsigned long long part[4];
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned long long tot = part[0] + part[1] + part[2] + part[3];
-      if (tot) atomicAdd(bp.terms, tot);
+      if (tot) atomicAdd(bp.terms + blockIdx.x % TERM_SLOTS, tot);
     }
   }
 }
@@ -1146,7 +1146,7 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
 
 // S: prefix-product group (1, 2, 4, 8; 1 for the backward with additions)
 template <int NB, int S>
-__global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_fwd(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
+__global__ __launch_bounds__(NB == 4 ? 256 : NB == 3 ? 512 : 768) void k_blku_fwd(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
   blku_body<NB, S, true, false>(g, bk, bp, blockIdx.x, 0);
 }
 // backward: ADD = the state penalty or the caller's co-state source (not in μ mode), which enter after every slice
@@ -1158,7 +1158,7 @@ __global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_bwd(const TChainAr
 // the backward chain with the fused order-ORD gradient (qoc_eval_dev / grape_sensitivity without additions): λ stays
 // in LDS, dJdu -> bp.dJdu.
 template <int NB, int S, int ORD>
-__global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_bwdg(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
+__global__ __launch_bounds__(NB == 4 ? 256 : NB == 3 ? 512 : 768) void k_blku_bwdg(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
   blku_body<NB, S, false, false, ORD>(g, bk, bp, blockIdx.x, 0);
 }
 

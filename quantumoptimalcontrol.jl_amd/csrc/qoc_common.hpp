@@ -6,6 +6,9 @@
 namespace qoc {
 
 constexpr int WAVE = 64;
+// executed-terms counter: partial sums in TERM_SLOTS words (workgroup b adds to word b % TERM_SLOTS), summed by
+// qoc_chain_terms -- one shared word serialised thousands of atomics per launch on one L2 address
+constexpr int TERM_SLOTS = 256;
 
 template <typename T>
 struct alignas(2 * sizeof(T)) cx {

@@ -444,13 +444,14 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
                        tchain_mf_lds(N, m, nu) <= 160 * 1024;
     c->tchain_ok = !c->big && nu <= TCHAIN_NUMAX && (precision == QOC_FP64 ? mf_ok || valu_ok : valu_ok);
     if (c->tchain_ok) {
-      const size_t bytes[3] = {(nu + 1) * NN * c->esz, (size_t)B * Nt * sizeof(TStep), sizeof(unsigned long long)};
+      const size_t bytes[3] = {(nu + 1) * NN * c->esz, (size_t)B * Nt * sizeof(TStep),
+                               TERM_SLOTS * sizeof(unsigned long long)};
       void** ptrs[3] = {&c->d_At, (void**)&c->d_steps, (void**)&c->d_terms};
       for (int i = 0; i < 3; ++i) {
         if ((e = hipMalloc(ptrs[i], bytes[i])) != hipSuccess) return bail(e, "hipMalloc");
         c->dev_bytes += bytes[i];
       }
-      hipMemset(c->d_terms, 0, sizeof(unsigned long long));
+      hipMemset(c->d_terms, 0, TERM_SLOTS * sizeof(unsigned long long));
     }
   }
   if (c->big) {
@@ -1389,9 +1390,13 @@ int qoc_chain_terms(qoc_ctx* c, long long* terms, int reset) {
   *terms = 0;
   if (!c->d_terms) return QOC_OK;
   HIPCHK(c, hipSetDevice(c->dev));
-  HIPCHK(c, hipMemcpyAsync(terms, c->d_terms, sizeof(long long), hipMemcpyDeviceToHost, c->stream));
-  if (reset) HIPCHK(c, hipMemsetAsync(c->d_terms, 0, sizeof(long long), c->stream));
+  unsigned long long part[TERM_SLOTS];
+  HIPCHK(c, hipMemcpyAsync(part, c->d_terms, sizeof(part), hipMemcpyDeviceToHost, c->stream));
+  if (reset) HIPCHK(c, hipMemsetAsync(c->d_terms, 0, sizeof(part), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  unsigned long long t = 0;
+  for (int i = 0; i < TERM_SLOTS; ++i) t += part[i];
+  *terms = (long long)t;
   return QOC_OK;
 }
 

@@ -183,10 +183,13 @@ static BlkuShape blku_shape(const qoc_ctx* c, bool fused, bool storeu = false) {
   s.CW = (c->nblk * c->m * (NB == 2 ? 2 : 4) + 63) / 64;  // one chain lane per state element (qoc_blku.hpp)
   const int per_cu = std::max(1, std::min(3, (c->B + c->ncu - 1) / std::max(1, c->ncu)));
   const int stg = fused ? (storeu ? 2 : 1) : 0;  // the fused backward's staging waves
-  const int wmax = std::max(s.CW + stg + 1, (NB == 4 ? 4 : 8) / per_cu);
+  // waves per workgroup at most: the launch bound (the forward and the fused backward for blocks of 2 rows are built
+  // for 12 waves, <= 168 VGPRs: 3 waves per SIMD), shared by the workgroups of a CU
+  const int wcap = NB == 4 ? 4 : NB == 2 ? 12 : 8;
+  const int wmax = std::max(s.CW + stg + 1, wcap / per_cu);
   int fw = wmax - s.CW - stg;
   if (const char* env = getenv(fused ? "QOC_BLKU_GFW" : "QOC_BLKU_FW")) fw = atoi(env);
-  fw = std::max(1, std::min(fw, (NB == 4 ? 4 : 8) - s.CW - stg));
+  fw = std::max(1, std::min(fw, wcap - s.CW - stg));
   s.W = s.CW + stg + fw;
   s.S = 1;
   if (const char* env = getenv("QOC_BLKU_S")) s.S = atoi(env) >= 2 && NB < 4 ? 2 : 1;

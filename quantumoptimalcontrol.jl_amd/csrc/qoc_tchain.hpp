@@ -137,7 +137,7 @@ static __global__ void k_tchain_prep(int nu, long long units, const double* __re
   }
   // one atomic per wave
   for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(terms, cnt);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(terms + blockIdx.x % TERM_SLOTS, cnt);
 }
 
 // Chebyshev variant (skew-Hermitian generators, Ã_k = -i H̃_k with spectrum within [-ρ, ρ], ρ = β_k):
@@ -340,7 +340,7 @@ static __global__ __launch_bounds__(64) void k_tchain_prep_cheb(int nu, long lon
     __syncthreads();
   }
   for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
-  if (l == 0 && cnt) atomicAdd(terms, cnt);
+  if (l == 0 && cnt) atomicAdd(terms + blockIdx.x % TERM_SLOTS, cnt);
 }
 
 struct TChainArgs {

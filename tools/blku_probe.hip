@@ -48,7 +48,7 @@ void run(int B, int Nt, int nblk, int m, int W, int C, int mode, bool bwdg) {
   (void)hipMalloc(&dJ, B * 8);
   (void)hipMalloc(&dsink, TCHAIN_SINK * 8);
   (void)hipMalloc(&dbrow, brow.size() * 4);
-  (void)hipMalloc(&dterms, 8);
+  (void)hipMalloc(&dterms, 256 * 8);  // TERM_SLOTS partial sums
   (void)hipMemcpy(dA, A.data(), A.size() * 16, hipMemcpyHostToDevice);
   (void)hipMemcpy(du, u.data(), u.size() * 8, hipMemcpyHostToDevice);
   (void)hipMemcpy(dx0, x0.data(), x0.size() * 16, hipMemcpyHostToDevice);
