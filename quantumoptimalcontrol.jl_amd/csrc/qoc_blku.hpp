@@ -132,6 +132,11 @@ __device__ __forceinline__ double dpp_any(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// The launch bound of the chain kernels (k_blku_fwd / _bwd / _bwdg): 8 waves, 4 for blocks of 4 rows (their
+// formation takes the whole register file).  The host sizes every launch within it (blku_shape).  (12 waves for
+// blocks of 2 rows, <= 168 VGPRs, measured no faster: forward 0.17 vs 0.15 ms, fused backward 0.196 vs 0.198 ms.)
+__host__ __device__ constexpr int blku_max_threads(int NB) { return NB == 4 ? 256 : 512; }
+
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
@@ -956,11 +961,16 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
     lds_barrier();
     lds_barrier();
     for (int c = 0; c < nC; ++c) {
+      BK_T(s0);
       if (c + 2 < nC) rec_store(c + 2);  // loaded one iteration ago
       if (c + 3 < nC) rec_load(c + 3);
       xs_store(c);  // read by grad(c) in the next iteration
       if (c + 1 < nC) xs_load(c + 1);
+      BK_T(s1);
       lds_barrier();
+      BK_T(s2);
+      BK_ADD(7, s1 - s0);
+      BK_ADD(8, s2 - s1);
     }
   } else if (stager) {
     us_load(0);
@@ -969,11 +979,16 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
     lds_barrier();
     lds_barrier();
     for (int c = 0; c < nC; ++c) {
+      BK_T(s0);
       if (c + 1 < nC) {
         us_store(c + 1);  // read by the chain in the next iteration
         if (c + 2 < nC) us_load(c + 2);
       }
+      BK_T(s1);
       lds_barrier();
+      BK_T(s2);
+      BK_ADD(9, s1 - s0);
+      BK_ADD(10, s2 - s1);
     }
   } else {
   lds_barrier();
@@ -1146,19 +1161,19 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
 
 // S: prefix-product group (1, 2, 4, 8; 1 for the backward with additions)
 template <int NB, int S>
-__global__ __launch_bounds__(NB == 4 ? 256 : NB == 3 ? 512 : 768) void k_blku_fwd(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
+__global__ __launch_bounds__(blku_max_threads(NB)) void k_blku_fwd(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
   blku_body<NB, S, true, false>(g, bk, bp, blockIdx.x, 0);
 }
 // backward: ADD = the state penalty or the caller's co-state source (not in μ mode), which enter after every slice
 template <int NB, int S, bool ADD>
-__global__ __launch_bounds__(NB == 4 ? 256 : 512) void k_blku_bwd(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
+__global__ __launch_bounds__(blku_max_threads(NB)) void k_blku_bwd(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
   static_assert(!ADD || S == 1, "additions after every slice: no prefix groups");
   blku_body<NB, S, false, ADD>(g, bk, bp, blockIdx.x, g.mu_mode);
 }
 // the backward chain with the fused order-ORD gradient (qoc_eval_dev / grape_sensitivity without additions): λ stays
 // in LDS, dJdu -> bp.dJdu.
 template <int NB, int S, int ORD>
-__global__ __launch_bounds__(NB == 4 ? 256 : NB == 3 ? 512 : 768) void k_blku_bwdg(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
+__global__ __launch_bounds__(blku_max_threads(NB)) void k_blku_bwdg(const TChainArgs g, const BlkArgs bk, const BlkuParams bp) {
   blku_body<NB, S, false, false, ORD>(g, bk, bp, blockIdx.x, 0);
 }
 

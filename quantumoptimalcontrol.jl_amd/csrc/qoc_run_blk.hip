@@ -183,9 +183,9 @@ static BlkuShape blku_shape(const qoc_ctx* c, bool fused, bool storeu = false) {
   s.CW = (c->nblk * c->m * (NB == 2 ? 2 : 4) + 63) / 64;  // one chain lane per state element (qoc_blku.hpp)
   const int per_cu = std::max(1, std::min(3, (c->B + c->ncu - 1) / std::max(1, c->ncu)));
   const int stg = fused ? (storeu ? 2 : 1) : 0;  // the fused backward's staging waves
-  // waves per workgroup at most: the launch bound (the forward and the fused backward for blocks of 2 rows are built
-  // for 12 waves, <= 168 VGPRs: 3 waves per SIMD), shared by the workgroups of a CU
-  const int wcap = NB == 4 ? 4 : NB == 2 ? 12 : 8;
+  // waves per workgroup at most: the kernels' launch bound (blku_max_threads: 12 waves for blocks of 2 rows), shared
+  // by the workgroups of a CU
+  const int wcap = blku_max_threads(NB) / 64;
   const int wmax = std::max(s.CW + stg + 1, wcap / per_cu);
   int fw = wmax - s.CW - stg;
   if (const char* env = getenv(fused ? "QOC_BLKU_GFW" : "QOC_BLKU_FW")) fw = atoi(env);
@@ -206,6 +206,7 @@ static BlkuShape blku_shape(const qoc_ctx* c, bool fused, bool storeu = false) {
   }
   s.C = std::max(s.C, s.S);
   s.lds = blku_lds(c->N, c->m, NB, c->nblk, s.C, gw);
+  s.W = std::min(s.W, wcap);  // never above the launch bound (a larger launch faults)
   return s;
 }
 

@@ -70,6 +70,13 @@ void run(int B, int Nt, int nblk, int m, int W, int C, int mode, bool bwdg) {
   double* ddJ;
   (void)hipMalloc(&ddJ, (size_t)B * Nt * nu * 8);
   bp.dJdu = ddJ;
+  double2* dU = nullptr;  // stored propagators for the fused backward (mode >= 10: mode - 10 with bp.Uin)
+  if (bwdg && mode >= 10) {
+    (void)hipMalloc(&dU, (size_t)B * Nt * NB * NB * nblk * 16);
+    (void)hipMemset(dU, 0, (size_t)B * Nt * NB * NB * nblk * 16);
+    bp.Uin = dU;
+    bp.probe_mode = mode - 10;
+  }
   {
     std::vector<cx<double>> cf((size_t)B * 2 * m, cx<double>{0.3, -0.1});
     (void)hipMemcpy(dcoef, cf.data(), cf.size() * 16, hipMemcpyHostToDevice);
@@ -81,7 +88,7 @@ void run(int B, int Nt, int nblk, int m, int W, int C, int mode, bool bwdg) {
   bp.rec = drec;
   hipLaunchKernelGGL(k_blku_rec, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, 0, bp, du, nu, Nt, total, drec);
   (void)hipDeviceSynchronize();
-  const size_t lds = blku_lds(N, m, NB, nblk, C, bwdg ? W - bp.CW : 0);
+  const size_t lds = blku_lds(N, m, NB, nblk, C, bwdg ? 1 : 0);
   if (lds > 160 * 1024) return;  // does not fit one CU
   const void* kf = bwdg ? (const void*)k_blku_bwdg<NB, S, 3> : (const void*)k_blku_fwd<NB, S>;
   (void)hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -105,14 +112,14 @@ void run(int B, int Nt, int nblk, int m, int W, int C, int mode, bool bwdg) {
   }
   unsigned long long tc[16];
   (void)hipMemcpyFromSymbol(tc, HIP_SYMBOL(g_bk), sizeof(tc));
-  const int nC = (Nt + C - 1) / C, fw = W - bp.CW - (bwdg ? 1 : 0);  // bwdg: one staging wave
+  const int nC = (Nt + C - 1) / C, fw = W - bp.CW - (bwdg ? (bp.Uin ? 2 : 1) : 0);  // bwdg: staging waves
   printf("%s NB=%d S=%d B=%d Nt=%d W=%d C=%2d mode=%d lds=%6zu: %.4f ms  per chunk (cycles): chain %6.0f  wait %6.0f"
-         " | worker %6.0f  (recs %5.0f  grad %6.0f)  wait %6.0f\n",
+         " | worker %6.0f  (recs %5.0f  grad %6.0f)  wait %6.0f | stage x %5.0f wait %5.0f  U %5.0f wait %5.0f\n",
          bwdg ? "bwdg" : "fwd ", NB, S, B, Nt, W, C, mode, lds, ms, tc[0] / (double)nC / bp.CW,
          tc[1] / (double)nC / bp.CW, tc[3] / (double)nC / fw, tc[6] / (double)nC / fw, tc[5] / (double)nC / fw,
-         tc[4] / (double)nC / fw);
+         tc[4] / (double)nC / fw, tc[7] / (double)nC, tc[8] / (double)nC, tc[9] / (double)nC, tc[10] / (double)nC);
   (void)hipFree(dA); (void)hipFree(du); (void)hipFree(dx0); (void)hipFree(dX); (void)hipFree(dL); (void)hipFree(dcoef);
-  (void)hipFree(dJ); (void)hipFree(dsink); (void)hipFree(dbrow); (void)hipFree(dterms); (void)hipFree(drec); (void)hipFree(ddJ);
+  (void)hipFree(dJ); (void)hipFree(dsink); (void)hipFree(dbrow); (void)hipFree(dterms); (void)hipFree(drec); (void)hipFree(ddJ); if (dU) (void)hipFree(dU);
 }
 
 int main(int argc, char** argv) {
@@ -121,14 +128,16 @@ int main(int argc, char** argv) {
   const int Nt = argc > 3 ? atoi(argv[3]) : (NB == 2 ? 1000 : 500);
   const int nblk = NB == 2 ? 20 : 3, m = NB == 2 ? 2 : 4;
   const int W0 = NB == 2 ? 2 : 1;  // chain waves
-  for (int bw : {0, 1})
-    for (int mode : {0, 1, 2, 3, 5})
-      for (int W = W0 + 1 + bw; W <= 8; ++W)
-        for (int C : {8, 16, 32}) {
-          if ((mode == 3 && bw) || (mode == 5 && !bw)) continue;
-          if (mode && (W != W0 + 4 || C != 16)) continue;
-          if (NB == 2) run<2, 1>(B, Nt, nblk, m, W, C, mode, bw);
-          else run<3, 1>(B, Nt, nblk, m, W, C, mode, bw);
-        }
+  for (int W = W0 + 1; W <= 8; ++W) {  // forward
+    if (NB == 2) run<2, 1>(B, Nt, nblk, m, W, NB == 2 ? 32 : 16, 0, false);
+    else run<3, 1>(B, Nt, nblk, m, W, 16, 0, false);
+  }
+  for (int mode : {10, 11, 15})  // fused backward with stored propagators: all, no chain formation (n/a), no grad
+    for (int W = W0 + 3; W <= 8; ++W)
+      for (int C : {8, 16}) {
+        if (mode != 10 && (W != 8 || C != 16)) continue;
+        if (NB == 2) run<2, 1>(B, Nt, nblk, m, W, C, mode, true);
+        else run<3, 1>(B, Nt, nblk, m, W, C, mode, true);
+      }
   return 0;
 }
