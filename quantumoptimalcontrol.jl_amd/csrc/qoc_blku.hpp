@@ -791,96 +791,86 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       }
     }
   };
-  // the gradient lane's block rows, read once (a global load inside the per-chunk contraction would expose its
-  // latency every chunk)
-  const int NBP = blku_nbp(nblk);
+  // the fused gradient of sequence chunk cq (GORD > 0): UPW = 64 / nblk slices per wave-iteration, a lane per (slice,
+  // block), the nblk blocks of a slice on adjacent lanes (lanes past UPW nblk idle); wave-iteration it on worker wave
+  // it % NWK (the host picks C so that the iterations come out even over the workers).  K = Σ_c x_k λ_{k+1}^H from the
+  // x ring and the λ ring (slots cq & 1), then Re tr(A_j M), summed over the slice's blocks by a segmented lane scan.
+  // (Packing the chunk's units densely over all 64 lanes splits slices between wave-iterations: their halves need
+  // atomic adds, whose round trips cost more than the idle lanes.)
+  const int wk = w - bp.CW - STG, NWK = nthr / 64 - bp.CW - STG;
+  const int UPW = 64 / nblk, gl = tid & 63, ul = gl / nblk, be = gl - ul * nblk;
+  // the lane's block rows, read once (a global load inside the contraction would expose its latency every chunk)
   int grow[NB];
 #pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int be = (tid & 63) % NBP;
-    grow[i] = GORD > 0 && be < nblk ? bk.brow[be * NB + i] : -1;
-  }
-  // the fused gradient of sequence chunk cq (GORD > 0): the worker waves take 64 / nblk slices per wave-iteration, a
-  // lane per (slice, block); K = Σ_c x_k λ_{k+1}^H from x_k in HBM and λ_{k+1} in the ring slot cq & 1, then
-  // Re tr(A_j M) reduced over the blocks through the wave's LDS slot in a fixed order
+  for (int i = 0; i < NB; ++i) grow[i] = GORD > 0 && wk >= 0 && ul < UPW ? bk.brow[be * NB + i] : -1;
   auto grad = [&](int cq) {
     if constexpr (GORD > 0) {
-      const int a = chunk_of(cq), jn = min(C, Nt - a * C), gw = w - bp.CW - STG, GW = (nthr >> 6) - bp.CW - STG;
-      const int l = tid & 63, UPW = 64 / NBP, ul = l / NBP, be = l - ul * NBP;
-      const int bc = min(be, nblk - 1);
+      const int a = chunk_of(cq), jn = min(C, Nt - a * C), nit = (jn + UPW - 1) / UPW;
       const double2* lr = lam + (size_t)(cq & 1) * C * Nm;
       const double2* xq = xring + (size_t)(cq & 1) * CNp;
       const double* rq = recs + (size_t)(cq & 3) * C * BLKU_REC;
-      const int(&r)[NB] = grow;
       double2 areg[3][NB == 2 ? E : 1];
-      if constexpr (NB == 2)
+      if constexpr (NB == 2)  // the lane's block of A_0..A_2 in registers
 #pragma unroll
         for (int j = 0; j < 3; ++j)
 #pragma unroll
-          for (int e = 0; e < E; ++e) areg[j][e] = ga[(j * E + e) * nblk + bc];
-      // GU wave-iterations per pass, their units interleaved per lane (GU = 2 measured no faster on cavity: the
-      // workers are issue-bound, not latency-bound)
-      constexpr int GU = 1;
-      for (int it0 = gw; it0 * UPW < jn; it0 += GU * GW) {
-        int jjv[GU];
-        double u1[GU], u2[GU], kr[GU][E], ki[GU][E];
+          for (int e = 0; e < E; ++e) areg[j][e] = ga[(j * E + e) * nblk + be];
+      for (int it = wk; it < nit; it += NWK) {
+        const int jj = it * UPW + ul;
+        const bool act = ul < UPW && jj < jn;
+        int r[NB];  // (opaque copies: nothing derived from them is hoisted out of the loop to sit in registers)
 #pragma unroll
-        for (int gi = 0; gi < GU; ++gi) {
-          const int jj = (it0 + gi * GW) * UPW + ul;
-          jjv[gi] = jj;
-          const int jc = jj < jn ? jj : 0;
-          // u_k from the step record (2^-J u_j scaled back by 2^J: exact)
-          const double* rk = rq + (size_t)jc * BLKU_REC;
-          const int Jk = (int)rk[6];
-          u1[gi] = ldexp(rk[3], Jk);
-          u2[gi] = ldexp(rk[4], Jk);
-#pragma unroll
-          for (int e = 0; e < E; ++e) kr[gi][e] = ki[gi][e] = 0.0;
+        for (int i = 0; i < NB; ++i) {
+          r[i] = grow[i];
+          if constexpr (NB > 2) asm volatile("" : "+v"(r[i]));
         }
+        const int jc = act ? jj : 0;
+        // u_k from the step record (2^-J u_j scaled back by 2^J: exact)
+        const double* rk = rq + (size_t)jc * BLKU_REC;
+        const int Jk = (int)rk[6];
+        const double u1 = ldexp(rk[3], Jk), u2 = ldexp(rk[4], Jk);
+        double kr[E], ki[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) kr[e] = ki[e] = 0.0;
         // K = Σ_c x_c λ_c^H from x_k in the x ring and λ_{k+1} in the λ ring
         constexpr int CB = NB == 2 ? 2 : 1;  // columns whose loads are in flight at once (a missing one: zeros)
+        const double2* xs = xq + (size_t)jc * Nm;
+        const double2* ls = lr + (size_t)jc * Nm;
         for (int c0 = 0; c0 < m; c0 += CB) {
-          double2 xv[GU][CB][NB], lv[GU][CB][NB];
+          double2 xv[CB][NB], lv[CB][NB];
 #pragma unroll
-          for (int gi = 0; gi < GU; ++gi) {
-            const int jc = jjv[gi] < jn ? jjv[gi] : 0;
-            const double2* xs = xq + (size_t)jc * Nm;
-            const double2* ls = lr + (size_t)jc * Nm;
+          for (int cc = 0; cc < CB; ++cc)
 #pragma unroll
-            for (int cc = 0; cc < CB; ++cc)
+            for (int i = 0; i < NB; ++i) {
+              const bool v = r[i] >= 0 && c0 + cc < m;
+              const int o = v ? (c0 + cc) * N + r[i] : 0;
+              xv[cc][i] = v ? xs[o] : make_double2(0.0, 0.0);
+              lv[cc][i] = v ? ls[o] : make_double2(0.0, 0.0);
+            }
 #pragma unroll
-              for (int i = 0; i < NB; ++i) {
-                const bool v = r[i] >= 0 && c0 + cc < m;
-                const int o = v ? (c0 + cc) * N + r[i] : 0;
-                xv[gi][cc][i] = v ? xs[o] : make_double2(0.0, 0.0);
-                lv[gi][cc][i] = v ? ls[o] : make_double2(0.0, 0.0);
-              }
-          }
-#pragma unroll
-          for (int gi = 0; gi < GU; ++gi)
-#pragma unroll
-            for (int cc = 0; cc < CB; ++cc) blku_kacc<NB>(kr[gi], ki[gi], xv[gi][cc], lv[gi][cc]);
+          for (int cc = 0; cc < CB; ++cc) blku_kacc<NB>(kr, ki, xv[cc], lv[cc]);
         }
-        double acc1[GU], acc2[GU];
-#pragma unroll
-        for (int gi = 0; gi < GU; ++gi) {
-          if constexpr (NB == 2)  // the lane's block of A_0..A_2 held in registers
-            blku_contract<NB, GORD>([&](int j, int e) { return areg[j][e]; }, kr[gi], ki[gi], u1[gi], u2[gi],
-                                    acc1[gi], acc2[gi]);
-          else
-            blku_contract<NB, GORD>([&](int j, int e) { return ga[(j * E + e) * nblk + bc]; }, kr[gi], ki[gi],
-                                    u1[gi], u2[gi], acc1[gi], acc2[gi]);
+        double acc1, acc2;
+        if constexpr (NB == 2)
+          blku_contract<NB, GORD>([&](int j, int e) { return areg[j][e]; }, kr, ki, u1, u2, acc1, acc2);
+        else {
+          // the block's A_j read from LDS where used: an opaque copy of the block index keeps the compiler from
+          // hoisting all 3 E of them out of the loop into registers (they spill)
+          int bc = be;
+          asm volatile("" : "+v"(bc));
+          blku_contract<NB, GORD>([&](int j, int e) { return ga[(j * E + e) * nblk + bc]; }, kr, ki, u1, u2, acc1,
+                                  acc2);
         }
-#pragma unroll
-        for (int gi = 0; gi < GU; ++gi) {
-          const bool act = be < nblk && jjv[gi] < jn;
-          const double s1 = blku_group_sum(act ? acc1[gi] : 0.0, NBP);
-          const double s2 = blku_group_sum(act ? acc2[gi] : 0.0, NBP);
-          if (be == 0 && jjv[gi] < jn) {
-            double* o = bp.dJdu + ((size_t)b * Nt + a * C + jjv[gi]) * nu;
-            o[0] = s1;
-            if (nu > 1) o[1] = s2;
-          }
+        double s1 = act ? acc1 : 0.0, s2 = act ? acc2 : 0.0;
+        for (int d = 1; d < nblk; d <<= 1) {  // inclusive scan within the slice's lanes
+          const double t1 = __shfl_up(s1, d), t2 = __shfl_up(s2, d);
+          s1 += be >= d ? t1 : 0.0;
+          s2 += be >= d ? t2 : 0.0;
+        }
+        if (act && be == nblk - 1) {
+          double* o = bp.dJdu + ((size_t)b * Nt + a * C + jj) * nu;
+          o[0] = s1;
+          if (nu > 1) o[1] = s2;
         }
       }
     }
@@ -956,16 +946,18 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       rec_load(1);
       rec_store(1);
     }
-    if (nC > 2) rec_load(2);
+    rec_load(min(2, nC - 1));
     xs_load(0);
     lds_barrier();
     lds_barrier();
     for (int c = 0; c < nC; ++c) {
       BK_T(s0);
-      if (c + 2 < nC) rec_store(c + 2);  // loaded one iteration ago
-      if (c + 3 < nC) rec_load(c + 3);
+      // the copies run unconditionally (past the last chunk: clamped reloads into free slots): no staged register is
+      // carried through a whole iteration
+      rec_store(c + 2);  // loaded one iteration ago
       xs_store(c);  // read by grad(c) in the next iteration
-      if (c + 1 < nC) xs_load(c + 1);
+      rec_load(min(c + 3, nC - 1));
+      xs_load(min(c + 1, nC - 1));
       BK_T(s1);
       lds_barrier();
       BK_T(s2);
@@ -975,15 +967,13 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   } else if (stager) {
     us_load(0);
     us_store(0);
-    if (nC > 1) us_load(1);
+    us_load(min(1, nC - 1));
     lds_barrier();
     lds_barrier();
     for (int c = 0; c < nC; ++c) {
       BK_T(s0);
-      if (c + 1 < nC) {
-        us_store(c + 1);  // read by the chain in the next iteration
-        if (c + 2 < nC) us_load(c + 2);
-      }
+      us_store(c + 1);  // read by the chain in the next iteration (past the last chunk: a free slot)
+      us_load(min(c + 2, nC - 1));
       BK_T(s1);
       lds_barrier();
       BK_T(s2);

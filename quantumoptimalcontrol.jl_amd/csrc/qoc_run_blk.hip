@@ -198,10 +198,27 @@ static BlkuShape blku_shape(const qoc_ctx* c, bool fused, bool storeu = false) {
   s.C = 64;
   // the stager's registers: x_k and the stored propagators of one chunk
   auto stage_ok = [&](int C) { return !fused || std::max(C * c->N * c->m, C * NB * NB * c->nblk) <= BLKU_XMAX * 64; };
-  while (s.C > 4 && (blku_lds(c->N, c->m, NB, c->nblk, s.C, gw) > budget || !stage_ok(s.C))) s.C >>= 1;
+  auto fits = [&](int C) { return blku_lds(c->N, c->m, NB, c->nblk, C, gw) <= budget && stage_ok(C); };
+  if (!fused) {
+    while (s.C > 4 && !fits(s.C)) s.C >>= 1;
+  } else {
+    // the fused backward: the largest C that fits, then within [Cmax / 2, Cmax] the C whose wave-iterations of the
+    // contraction (ceil(C / UPW), UPW = 64 / nblk slices each) come out most even over the fw workers: the fewest
+    // iterations of the busiest worker per slice (ties: the larger C, fewer chunk barriers)
+    while (s.C > 4 && !fits(s.C)) --s.C;
+    const int upw = std::max(1, 64 / std::max(1, c->nblk)), cmax = s.C;
+    auto per_slice = [&](int C) { return (double)(((C + upw - 1) / upw + fw - 1) / fw) / C; };
+    for (int C = cmax; C >= std::max(4, cmax / 2); --C)
+      if (per_slice(C) < per_slice(s.C) - 1e-12) s.C = C;
+  }
   if (const char* env = getenv(fused ? "QOC_BLKU_GC" : "QOC_BLKU_C")) {
     int q = 1;
-    while (q * 2 <= std::min(atoi(env), 64) && stage_ok(q * 2)) q *= 2;
+    if (fused) {
+      q = std::max(1, std::min(atoi(env), 64));
+      while (q > 1 && !stage_ok(q)) --q;
+    } else {
+      while (q * 2 <= std::min(atoi(env), 64) && stage_ok(q * 2)) q *= 2;
+    }
     s.C = q;
   }
   s.C = std::max(s.C, s.S);

@@ -128,16 +128,17 @@ int main(int argc, char** argv) {
   const int Nt = argc > 3 ? atoi(argv[3]) : (NB == 2 ? 1000 : 500);
   const int nblk = NB == 2 ? 20 : 3, m = NB == 2 ? 2 : 4;
   const int W0 = NB == 2 ? 2 : 1;  // chain waves
-  for (int W = W0 + 1; W <= 8; ++W) {  // forward
-    if (NB == 2) run<2, 1>(B, Nt, nblk, m, W, NB == 2 ? 32 : 16, 0, false);
-    else run<3, 1>(B, Nt, nblk, m, W, 16, 0, false);
-  }
-  for (int mode : {10, 11, 15})  // fused backward with stored propagators: all, no chain formation (n/a), no grad
-    for (int W = W0 + 3; W <= 8; ++W)
-      for (int C : {8, 16}) {
-        if (mode != 10 && (W != 8 || C != 16)) continue;
-        if (NB == 2) run<2, 1>(B, Nt, nblk, m, W, C, mode, true);
-        else run<3, 1>(B, Nt, nblk, m, W, C, mode, true);
-      }
+  (void)W0;
+  if (NB == 2) run<2, 1>(B, Nt, nblk, m, 8, 32, 0, false);  // forward
+  else run<3, 1>(B, Nt, nblk, m, 8, 16, 0, false);
+  // fused backward with stored propagators: all (10), no grad (15), per chunk size (the workgroups a CU holds: 8 waves)
+  const int Wb = NB == 2 ? 8 : 4;
+  for (int mode : {10, 15})
+    for (int C : {8, 12, 15, 16, 20, 21}) {
+      if (NB == 2 && C > 16) continue;
+      if (mode == 15 && C != 12 && C != 16) continue;
+      if (NB == 2) run<2, 1>(B, Nt, nblk, m, Wb, C, mode, true);
+      else run<3, 1>(B, Nt, nblk, m, Wb, C, mode, true);
+    }
   return 0;
 }
