@@ -37,7 +37,7 @@ struct BlkuParams {
   double rad[3];                   // ρ_k = rad[0] + Σ_j |u_jk| rad[j]
   double mur[3], mui[3];           // shifts μ_j (e^{μ_k} = exp(μ_0 + Σ_j u_jk μ_j))
   double theta_cap;                // ρ_k / 2^J <= theta_cap (< 1)
-  int C;                           // slices per chunk (divides 64)
+  int C;                           // slices per chunk (<= 64; the fused backward's need not divide 64)
   int CW;                          // chain waves (waves >= CW form propagators)
   int Ntp;                         // slices per seed in the record array: Nt rounded up to 64
   const double* rec;               // B x Ntp x BLKU_REC step records (k_blku_rec)
@@ -45,6 +45,8 @@ struct BlkuParams {
   double* dJdu;                    // B x Nt x nu: the fused backward's gradient (k_blku_bwdg)
   double2* Uout;                   // k_blku_fwd (S = 1): also store each slice's block propagators, B x Nt x NB^2 x nblk
   const double2* Uin;              // k_blku_bwdg: read them instead of forming (the staging wave copies them to LDS)
+  int ustg;                        // with Uin: 1 one staging wave copies the records, x_k and the propagators (small
+                                   // chunks), else a second one the propagators
   int probe_mode;                  // QOC_PROBE builds only: 1 skip the formation, 2 the chain, 3 the chain's stores,
                                    // 4 the chain's LDS reads
 };
@@ -661,7 +663,7 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   // chunk would wait on the loads) nor the workers (whose registers go to the formation and the contraction) wait
   // With stored propagators (bp.Uin) a second staging wave copies them (each stager holds one chunk's worth of
   // registers: two in one wave would spill).
-  const int STG = GORD > 0 ? (bp.Uin ? 2 : 1) : 0;
+  const int STG = GORD > 0 ? (bp.Uin && bp.ustg != 1 ? 2 : 1) : 0;
   const bool stager = GORD > 0 && w >= bp.CW && w < bp.CW + STG;
   const int stg_i = w - bp.CW;  // 0: step records and x_k, 1: propagators
   const int fl = tid - 64 * (bp.CW + STG), FL = nthr - 64 * (bp.CW + STG);  // formation lanes
@@ -673,10 +675,11 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
   double rr[RMAX];
   const double* recb = bp.rec + (size_t)b * bp.Ntp * BLKU_REC;
   auto rec_load = [&](int c) {
-    const size_t base = (size_t)chunk_of(c) * C * BLKU_REC;
+    const int a = chunk_of(c), n = min(C, Nt - a * C) * BLKU_REC;  // (a C not dividing 64 can pass Ntp)
+    const size_t base = (size_t)a * C * BLKU_REC;
 #pragma unroll
     for (int i = 0; i < RMAX; ++i)  // unconditional (clamped) loads: the waits before rec_store count them exactly
-      rr[i] = recb[base + min(sl + i * SLN, C * BLKU_REC - 1)];
+      rr[i] = recb[base + min(sl + i * SLN, n - 1)];
   };
   auto rec_store = [&](int c) {
     double* dst = recs + (size_t)(c & 3) * C * BLKU_REC;
@@ -948,6 +951,12 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
     }
     rec_load(min(2, nC - 1));
     xs_load(0);
+    const bool su = uin && STG == 1;  // this wave also copies the propagators
+    if (su) {
+      us_load(0);
+      us_store(0);
+      us_load(min(1, nC - 1));
+    }
     lds_barrier();
     lds_barrier();
     for (int c = 0; c < nC; ++c) {
@@ -956,8 +965,10 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       // carried through a whole iteration
       rec_store(c + 2);  // loaded one iteration ago
       xs_store(c);  // read by grad(c) in the next iteration
+      if (su) us_store(c + 1);  // read by the chain in the next iteration (past the last chunk: a free slot)
       rec_load(min(c + 3, nC - 1));
       xs_load(min(c + 1, nC - 1));
+      if (su) us_load(min(c + 2, nC - 1));
       BK_T(s1);
       lds_barrier();
       BK_T(s2);

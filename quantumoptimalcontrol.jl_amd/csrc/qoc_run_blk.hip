@@ -166,7 +166,7 @@ bool blku_on(const qoc_ctx* c) {
 }
 
 struct BlkuShape {
-  int C, CW, W, S;
+  int C, CW, W, S, ustg;
   size_t lds;
 };
 // Waves per workgroup: CW chain waves (one lane per state element), in the fused backward one staging wave, and FW
@@ -182,7 +182,11 @@ static BlkuShape blku_shape(const qoc_ctx* c, bool fused, bool storeu = false) {
   const int NB = c->blk_nb;
   s.CW = (c->nblk * c->m * (NB == 2 ? 2 : 4) + 63) / 64;  // one chain lane per state element (qoc_blku.hpp)
   const int per_cu = std::max(1, std::min(3, (c->B + c->ncu - 1) / std::max(1, c->ncu)));
-  const int stg = fused ? (storeu ? 2 : 1) : 0;  // the fused backward's staging waves
+  // the fused backward's staging waves: with stored propagators one more, unless one wave can hold a chunk's records,
+  // x_k and propagators (QOC_BLKU_USTG=1: then the freed wave slot is a worker's)
+  const char* us = getenv("QOC_BLKU_USTG");
+  s.ustg = storeu && us && atoi(us) == 1 ? 1 : 2;
+  const int stg = fused ? (storeu && s.ustg == 2 ? 2 : 1) : 0;
   // waves per workgroup at most: the kernels' launch bound (blku_max_threads: 12 waves for blocks of 2 rows), shared
   // by the workgroups of a CU
   const int wcap = blku_max_threads(NB) / 64;
@@ -572,6 +576,7 @@ static int blku_bwdg(qoc_ctx* c, int order, double* d_dJdu, const double2* Uin =
   const BlkuShape s = blku_shape(c, true, Uin != nullptr);
   BlkuParams bp = blku_params(c, s, d_dJdu);  // the records are current (the caller's)
   bp.Uin = Uin;
+  bp.ustg = s.ustg;
   const int mk = mark_begin(c, 2);
   const hipError_t e = blku_dispatch(c, [&](auto NB_) {
     constexpr int NB = decltype(NB_)::value;
