@@ -150,6 +150,31 @@ def test_blocks_gradient_orders(built_lib, monkeypatch, order, device, kind):
         _assert_seed(J[b], g[b], J0, g0, (order, b))
 
 
+@pytest.mark.parametrize("gc", [13, 21])
+@pytest.mark.parametrize("ustg", ["1", "2"])
+@pytest.mark.parametrize("name", ["zz", "cavity20"])
+def test_blocks_fused_chunk_sizes(built_lib, monkeypatch, gc, ustg, name):
+    """The fused backward's chunk size need not divide 64 (the host picks the one that spreads the contraction
+    evenly over the workers): Nt = 64 with C = 13 / 21 ends in a partial chunk past the padded record array, with
+    one staging wave for records, x_k and stored propagators (QOC_BLKU_USTG=1) or two."""
+    from qoc_amd import systems
+    if name == "zz":
+        prob = systems.zz_problem(64, tgate=6.0)
+        u = systems.zz_controls(3, 64, 6.0, seed=71)
+    else:
+        prob = systems.cavity_problem(N_cavity=10, Nt=64)
+        u = systems.cavity_controls(3, 64, seed=72)
+    monkeypatch.setenv("QOC_BLKU_GC", str(gc))
+    monkeypatch.setenv("QOC_BLKU_USTG", ustg)
+    e = _engine(prob, 3, "prop", monkeypatch)
+    J, g = _eval(e, u, True)
+    assert e.info()["backward"] == "fused"
+    e.close()
+    for b in range(3):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, (name, gc, ustg, b))
+
+
 @pytest.mark.parametrize("poly", ["taylor", "chebyshev"])
 @pytest.mark.parametrize("kind", ["prop", "mfma"])
 def test_blocks_penalty_and_costate_source(built_lib, monkeypatch, poly, kind):
