@@ -719,6 +719,15 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
       }
       double ur[NV][E], ui[NV][E];
       blku_form<NB, NV>(gb, nblk, be, rp, invt, ur, ui);
+      if (FWD && bp.Uout) {  // the propagators themselves (before any prefix scan) to HBM at the absolute slice
+#pragma unroll
+        for (int u = 0; u < NV; ++u)
+          if (st[u]) {
+            double2* og = bp.Uout + ((size_t)b * Nt + (size_t)chunk_of(c) * C + pp[u]) * E * nblk + be[u];
+#pragma unroll
+            for (int e = 0; e < E; ++e) og[e * nblk] = make_double2(ur[u][e], ui[u][e]);
+          }
+      }
       if constexpr (S > 1) {
 #pragma unroll
         for (int u = 0; u < NV; ++u) blku_scan<NB, S, FWD>(ur[u], ui[u], jl[u]);
@@ -729,11 +738,6 @@ __device__ __forceinline__ void blku_body(const TChainArgs& g, const BlkArgs& bk
           double2* o = Uc + (size_t)pp[u] * E * nblk + be[u];
 #pragma unroll
           for (int e = 0; e < E; ++e) o[e * nblk] = make_double2(ur[u][e], ui[u][e]);
-          if (FWD && S == 1 && bp.Uout) {  // the same layout in HBM, at the absolute slice (coalesced over blocks)
-            double2* og = bp.Uout + ((size_t)b * Nt + (size_t)chunk_of(c) * C + pp[u]) * E * nblk + be[u];
-#pragma unroll
-            for (int e = 0; e < E; ++e) og[e * nblk] = make_double2(ur[u][e], ui[u][e]);
-          }
         }
     }
   };

@@ -643,15 +643,20 @@ static int blku_backward(qoc_ctx* c, int order, double* d_dJdu) {
 // qoc_eval_dev (built-in cost, no penalty, no co-state source): the step records once, the forward chain (J and the
 // λ_N coefficients), then the fused backward -- x_k is written once and read once, λ never leaves the workgroups
 static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
-  const BlkuShape s = blku_shape(c, false);
+  BlkuShape s = blku_shape(c, false);
+  // the forward's prefix groups apart from the backward's (QOC_BLKU_FS; the stored propagators are the plain ones)
+  if (const char* fs = getenv("QOC_BLKU_FS")) {
+    s.S = atoi(fs) >= 2 && c->blk_nb < 4 ? 2 : 1;
+    s.C = std::max(s.C, s.S);
+  }
   BlkuParams bp = blku_params(c, s);
   int r = blku_records(c, bp, true);
   if (r) return r;
-  // the forward also stores the block propagators for the fused backward (which then forms none): S = 1 only (with
-  // prefix groups the chunks hold products); QOC_BLKU_STOREU=0 keeps the backward forming its own
+  // the forward also stores the block propagators for the fused backward (which then forms none; its S = 1 only:
+  // with prefix groups its chunks hold products); QOC_BLKU_STOREU=0 keeps the backward forming its own
   const char* su = getenv("QOC_BLKU_STOREU");
   const bool fused = blku_fused_ok(c, order);
-  const bool storeu = fused && s.S == 1 && !(su && !std::strcmp(su, "0"));
+  const bool storeu = fused && blku_shape(c, true, true).S == 1 && !(su && !std::strcmp(su, "0"));
   if (storeu && !c->d_blkU) {
     const size_t bytes = (size_t)c->B * c->Nt * c->blk_nb * c->blk_nb * c->nblk * sizeof(double2);
     HIPCHK(c, hipMalloc((void**)&c->d_blkU, bytes));

@@ -77,6 +77,11 @@ void run(int B, int Nt, int nblk, int m, int W, int C, int mode, bool bwdg) {
     bp.Uin = dU;
     bp.probe_mode = mode - 10;
   }
+  if (!bwdg && mode == 20) {  // the forward storing the propagators (the eval's)
+    (void)hipMalloc(&dU, (size_t)B * Nt * NB * NB * nblk * 16);
+    bp.Uout = dU;
+    bp.probe_mode = 0;
+  }
   {
     std::vector<cx<double>> cf((size_t)B * 2 * m, cx<double>{0.3, -0.1});
     (void)hipMemcpy(dcoef, cf.data(), cf.size() * 16, hipMemcpyHostToDevice);
@@ -129,8 +134,10 @@ int main(int argc, char** argv) {
   const int nblk = NB == 2 ? 20 : 3, m = NB == 2 ? 2 : 4;
   const int W0 = NB == 2 ? 2 : 1;  // chain waves
   (void)W0;
-  if (NB == 2) run<2, 1>(B, Nt, nblk, m, 8, 32, 0, false);  // forward
-  else run<3, 1>(B, Nt, nblk, m, 8, 16, 0, false);
+  for (int C : {16, 19, 21, 24, 28, 32}) {  // forward storing the propagators, per chunk size
+    if (NB == 2) run<2, 1>(B, Nt, nblk, m, 8, C, 20, false);
+    else run<3, 1>(B, Nt, nblk, m, 4, C, 20, false);
+  }
   // fused backward with stored propagators: all (10), no grad (15), per chunk size (the workgroups a CU holds: 8 waves)
   const int Wb = NB == 2 ? 8 : 4;
   for (int mode : {10, 15})
