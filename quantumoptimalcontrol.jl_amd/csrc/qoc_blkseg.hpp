@@ -1,0 +1,564 @@
+// qoc_blkseg.hpp — one evaluation (propagate + J + grape_sensitivity) on block propagators with the time axis cut
+// into segments, so that the serial depth per seed is about 2 Nt / S + log2 S instead of 2 Nt.
+//
+// The reference's two chains are serial in k (src/gradient_computations.jl:27-29 forward, :52-58 co-states); only
+// the exponentials are parallel (:17-25).  With generators whose invariant blocks have <= 3 rows (qoc_blk.hpp: cavity
+// 20 blocks of 2, zz 3 blocks of 3) every U_k is block-diagonal, and one block of it costs as much to form as to
+// apply.  One workgroup per seed; lane (s, β) owns block β of segment s = slices [s L, s L + L):
+//   phase 0  step records of every slice (e^{μ_k}, 2^-J u_k) into LDS, J and the Taylor degree P from the seed's
+//            largest ρ_k (one pair for the whole seed: every lane runs the same term loop);
+//   phase 1  the segment product P_s = U_{sL+L-1} .. U_{sL} on the block (U_k formed per slice, the k_blku_* block
+//            exponential: Taylor polynomial in the Cayley-Hamilton basis with the phase folded in);
+//   phase 2  inclusive prefix products Q_s = P_s .. P_0 over the segments (Hillis-Steele, log2 S rounds through LDS),
+//            x_N = Q_{S-1} x_0, the terminal cost J and λ_N (chain_costs, src/penalty_fcns.jl:15-42), then
+//            G_N = Σ_c x_N,c λ_N,c^H per block;
+//   phase 3  every segment backwards from its end, with G_k = Σ_c x_k,c λ_k,c^H instead of the states: because U_k is
+//            unitary (skew-Hermitian generators; the host checks them exactly),
+//              K_k = Σ_c x_k λ_{k+1}^H = U_k^H G_{k+1},    G_k = K_k U_k,
+//            and G at the segment's end is Q_s G_0 Q_s^H with G_0 = Q_{S-1}^H G_N Q_{S-1}.  The gradient of the slice is
+//            the trace form of expm_jacobian! + _compute_u_sensitivity (:177-223, blku_contract) on K_k:
+//              dJ/du_jk = Re tr(A_j M_k),  M = Σ_{a+b<ORD} X^b K X^a / (a+b+1)!,  X = A_k,
+//            summed over the slice's blocks (a wave-private LDS slot, fixed order: no atomics).
+// Neither x_k, λ_k nor U_k go to HBM: the launch reads u and writes J, the λ_N coefficients and dJdu.  qoc_get_states
+// and qoc_get_costates rebuild x_k / λ_k on demand with the k_blku_* chains (qoc_run_blk.hip).
+#pragma once
+#include "qoc_blku.hpp"
+
+namespace qoc {
+
+struct BlksegParams {
+  double rad[3];               // ρ_k = rad[0] + Σ_j |u_jk| rad[j] (spectral half-widths of the shifted generators)
+  double mur[3], mui[3];       // shifts μ_j: Ã_j = A_j - μ_j I, e^{μ_k} = exp(μ_0 + Σ_j u_jk μ_j)
+  double theta_cap;            // ρ / 2^J <= theta_cap
+  int S;                       // segments per seed
+  int L;                       // slices per segment (S L >= Nt; the last segment may be shorter)
+  int UPW;                     // segments per wave (64 / nblk)
+  const double* u;             // B x Nt x nu controls (the caller's buffer)
+  double* u_copy;              // copies of u written by the launch (the stale check, the lazy rebuilds), or nullptr
+  double* u_copy2;
+  double* J2;                  // a second copy of J (the caller's), or nullptr
+  cx<double>* coef2;           // a second copy of the λ_N coefficients (the lazy co-states), or nullptr
+  double* dJdu;                // B x Nt x nu
+  unsigned long long* terms;   // Σ P 2^J per pass over the slices (executed Taylor terms), nullptr: not counted
+};
+
+// LDS, in doubles: shifted generator blocks [nblk][3][E] complex | step records [Nt][4] | segment products [S][E][nblk]
+// complex | G_0 [E][nblk] complex | x_0 then x_N (N m complex) | λ_N coefficients (2 m complex) | scratch (24) |
+// per-wave partial sums [W][128] | dJdu [Nt][nu]
+__host__ __device__ inline size_t blkseg_off_rec(int NB, int nblk) { return (size_t)6 * NB * NB * nblk; }
+__host__ __device__ inline size_t blkseg_off_slot(int NB, int nblk, int Nt) { return blkseg_off_rec(NB, nblk) + 4 * (size_t)Nt; }
+__host__ __device__ inline size_t blkseg_off_g0(int NB, int nblk, int Nt, int S) {
+  return blkseg_off_slot(NB, nblk, Nt) + (size_t)2 * S * NB * NB * nblk;
+}
+__host__ __device__ inline size_t blkseg_off_xN(int NB, int nblk, int Nt, int S) {
+  return blkseg_off_g0(NB, nblk, Nt, S) + (size_t)2 * NB * NB * nblk;
+}
+__host__ __device__ inline size_t blkseg_off_cf(int N, int m, int NB, int nblk, int Nt, int S) {
+  return blkseg_off_xN(NB, nblk, Nt, S) + (size_t)2 * N * m;
+}
+__host__ __device__ inline size_t blkseg_off_red(int N, int m, int NB, int nblk, int Nt, int S) {
+  return blkseg_off_cf(N, m, NB, nblk, Nt, S) + (size_t)4 * m;
+}
+__host__ __device__ inline size_t blkseg_off_wred(int N, int m, int NB, int nblk, int Nt, int S) {
+  return blkseg_off_red(N, m, NB, nblk, Nt, S) + 24;
+}
+__host__ __device__ inline size_t blkseg_off_dJ(int N, int m, int NB, int nblk, int Nt, int S, int W) {
+  return blkseg_off_wred(N, m, NB, nblk, Nt, S) + (size_t)128 * W;
+}
+__host__ __device__ inline size_t blkseg_lds(int N, int m, int nu, int NB, int nblk, int Nt, int S, int W) {
+  return (blkseg_off_dJ(N, m, NB, nblk, Nt, S, W) + (size_t)Nt * nu) * sizeof(double);
+}
+
+// launch bound: 8 waves (2 per SIMD, <= 256 VGPRs)
+constexpr int BLKSEG_THREADS = 512;
+
+// c = a b, c = a^H b, c = a b^H on NB x NB complex blocks (row-major)
+template <int NB, bool AH, bool BH>
+__device__ __forceinline__ void seg_mm(const double (&ar)[NB * NB], const double (&ai)[NB * NB], const double (&br)[NB * NB],
+                                       const double (&bi)[NB * NB], double (&cr)[NB * NB], double (&ci)[NB * NB]) {
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      double sr = 0.0, si = 0.0;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int ea = AH ? q * NB + i : i * NB + q, eb = BH ? k * NB + q : q * NB + k;
+        const double xr = ar[ea], xi = AH ? -ai[ea] : ai[ea];
+        const double yr = br[eb], yi = BH ? -bi[eb] : bi[eb];
+        sr = fma(xr, yr, fma(-xi, yi, sr));
+        si = fma(xr, yi, fma(xi, yr, si));
+      }
+      cr[i * NB + k] = sr;
+      ci[i * NB + k] = si;
+    }
+}
+
+// Â = 2^-J Ã_k on the lane's block and U_k = e^{μ_k} (p(Â))^{2^J} for NV slices at once (independent recurrences
+// interleaved); rk[v]: the slice's record [Re e^μ, Im e^μ, 2^-J u_1, 2^-J u_2]; gen(j, e): entry e of Ã_j's block.
+// P and J are uniform over the workgroup (k_blkseg_eval's phase 0).
+template <int NB, int NV, typename GEN>
+__device__ __forceinline__ void seg_form(GEN&& gen, const double* const (&rk)[NV], double s0, int P, int J,
+                                         double (&ar)[NV][NB * NB], double (&ai)[NV][NB * NB], double (&ur)[NV][NB * NB],
+                                         double (&ui)[NV][NB * NB]) {
+  constexpr int E = NB * NB;
+  double pr[NV], pi[NV], qr[NV], qi[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double2 ph = *reinterpret_cast<const double2*>(rk[v]);
+    const double2 su = *reinterpret_cast<const double2*>(rk[v] + 2);
+    qr[v] = ph.x;
+    qi[v] = ph.y;
+    pr[v] = J ? 1.0 : ph.x;
+    pi[v] = J ? 0.0 : ph.y;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const double2 g0 = gen(0, e), g1 = gen(1, e), g2 = gen(2, e);
+      ar[v][e] = fma(su.y, g2.x, fma(su.x, g1.x, s0 * g0.x));
+      ai[v][e] = fma(su.y, g2.y, fma(su.x, g1.y, s0 * g0.y));
+    }
+  }
+  blku_taylor<NB, NV>(ar, ai, P, pr, pi, nullptr, ur, ui);
+  if (J) {  // squarings on the phase-free polynomial, then the phase
+    for (int q = 0; q < J; ++q)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) blku_square<NB>(ur[v], ui[v]);
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const double vr = ur[v][e], vi = ui[v][e];
+        ur[v][e] = qr[v] * vr - qi[v] * vi;
+        ui[v][e] = qr[v] * vi + qi[v] * vr;
+      }
+  }
+}
+
+// Re tr(A_j M) for j = 1, 2 with M = Σ_{a+b<ORD} X^b K X^a / (a+b+1)! (blku_contract's recurrence: L_0 = R_0 = K,
+// R_n = R_{n-1} X, L_n = X L_{n-1} + R_n, M = Σ_n L_n / (n+1)!) from the slice's X = A_k and the shifted generator
+// blocks: A_j = Ã_j + μ_j I, so Re tr(A_j M) = Re tr(Ã_j M) + Re(μ_j tr M).  The traces are accumulated order by
+// order (Re tr(A_j L_n) / (n+1)!), so that M is never held: three NB x NB matrices live (K -> L, R, X) instead of
+// four.  K is overwritten.
+template <int NB, typename GEN>
+__device__ __forceinline__ void seg_trace(GEN&& gen, const double (&Lr)[NB * NB], const double (&Li)[NB * NB], double f,
+                                          double m1r, double m1i, double m2r, double m2i, double& acc1, double& acc2) {
+  double a1 = 0.0, a2 = 0.0, tr = 0.0, ti = 0.0;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    tr += Lr[i * NB + i];
+    ti += Li[i * NB + i];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const double2 g1 = gen(1, i * NB + q), g2 = gen(2, i * NB + q);
+      a1 = fma(g1.x, Lr[q * NB + i], fma(-g1.y, Li[q * NB + i], a1));
+      a2 = fma(g2.x, Lr[q * NB + i], fma(-g2.y, Li[q * NB + i], a2));
+    }
+  }
+  acc1 = fma(f, fma(m1r, tr, fma(-m1i, ti, a1)), acc1);
+  acc2 = fma(f, fma(m2r, tr, fma(-m2i, ti, a2)), acc2);
+}
+
+template <int NB, int ORD, typename GEN>
+__device__ __forceinline__ void seg_contract(GEN&& gen, const double (&xr_)[NB * NB], const double (&xi_)[NB * NB],
+                                             double (&Lr)[NB * NB], double (&Li)[NB * NB], double m1r, double m1i,
+                                             double m2r, double m2i, double& acc1, double& acc2) {
+  constexpr int E = NB * NB;
+  constexpr double invf[6] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120};
+  acc1 = acc2 = 0.0;
+  seg_trace<NB>(gen, Lr, Li, 1.0, m1r, m1i, m2r, m2i, acc1, acc2);
+  if constexpr (ORD > 1) {
+    double Rr[E], Ri[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      Rr[e] = Lr[e];
+      Ri[e] = Li[e];
+    }
+#pragma unroll
+    for (int n = 1; n < ORD; ++n) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {  // R_n = R_{n-1} X, row by row in place
+        double tr[NB], ti[NB];
+#pragma unroll
+        for (int kk = 0; kk < NB; ++kk) {
+          double sr = 0.0, si = 0.0;
+#pragma unroll
+          for (int q = 0; q < NB; ++q) {
+            sr = fma(Rr[i * NB + q], xr_[q * NB + kk], fma(-Ri[i * NB + q], xi_[q * NB + kk], sr));
+            si = fma(Rr[i * NB + q], xi_[q * NB + kk], fma(Ri[i * NB + q], xr_[q * NB + kk], si));
+          }
+          tr[kk] = sr;
+          ti[kk] = si;
+        }
+#pragma unroll
+        for (int kk = 0; kk < NB; ++kk) {
+          Rr[i * NB + kk] = tr[kk];
+          Ri[i * NB + kk] = ti[kk];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk) {  // L_n = X L_{n-1} + R_n, column by column in place
+        double tr[NB], ti[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          double sr = Rr[i * NB + kk], si = Ri[i * NB + kk];
+#pragma unroll
+          for (int q = 0; q < NB; ++q) {
+            sr = fma(xr_[i * NB + q], Lr[q * NB + kk], fma(-xi_[i * NB + q], Li[q * NB + kk], sr));
+            si = fma(xr_[i * NB + q], Li[q * NB + kk], fma(xi_[i * NB + q], Lr[q * NB + kk], si));
+          }
+          tr[i] = sr;
+          ti[i] = si;
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          Lr[i * NB + kk] = tr[i];
+          Li[i * NB + kk] = ti[i];
+        }
+      }
+      seg_trace<NB>(gen, Lr, Li, invf[n + 1], m1r, m1i, m2r, m2i, acc1, acc2);
+    }
+  }
+}
+
+__device__ __forceinline__ double block_max(double v, double* scratch) {
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  double s = scratch[0];
+  const int nw = (blockDim.x + 63) >> 6;
+  for (int i = 1; i < nw; ++i) s = fmax(s, scratch[i]);
+  __syncthreads();
+  return s;
+}
+
+// wave-private LDS traffic between lanes of one wave: program order is LDS order within a wave; this keeps the
+// compiler from moving accesses across the exchange
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One workgroup per seed (blockIdx.x), W = blockDim / 64 waves, UPW segments of nblk lanes per wave (lanes past
+// UPW nblk idle).  Built-in costs only (TRACE / ZCAL), no state penalty, no co-state source, unpacked states,
+// skew-Hermitian generators (the host's blkseg_ok).
+template <int NB, int ORD>
+__global__ __launch_bounds__(BLKSEG_THREADS) void k_blkseg_eval(const TChainArgs g, const BlkArgs bk, const BlksegParams sp) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int E = NB * NB;
+  constexpr bool GREG = NB == 2;  // the lane's generator blocks in registers (blocks of 3 rows: from LDS)
+  constexpr int NV1 = NB == 2 ? 2 : 1;  // slices formed at once in phase 1
+  const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, nblk = bk.nblk, S = sp.S, L = sp.L;
+  const int tid = threadIdx.x, nthr = blockDim.x, w = tid >> 6, l = tid & 63, W = nthr >> 6;
+  const int b = blockIdx.x;
+  const size_t Nm = (size_t)N * m;
+  double* const lds = reinterpret_cast<double*>(smem);
+  double2* const gsh = reinterpret_cast<double2*>(lds);
+  double* const rec = lds + blkseg_off_rec(NB, nblk);
+  double2* const slot = reinterpret_cast<double2*>(lds + blkseg_off_slot(NB, nblk, Nt));
+  double2* const g0s = reinterpret_cast<double2*>(lds + blkseg_off_g0(NB, nblk, Nt, S));
+  double* const xN = lds + blkseg_off_xN(NB, nblk, Nt, S);
+  cx<double>* const cf = reinterpret_cast<cx<double>*>(lds + blkseg_off_cf(N, m, NB, nblk, Nt, S));
+  double* const red = lds + blkseg_off_red(N, m, NB, nblk, Nt, S);
+  double* const wred = lds + blkseg_off_wred(N, m, NB, nblk, Nt, S);
+  double* const dJ = lds + blkseg_off_dJ(N, m, NB, nblk, Nt, S, W);
+
+  // ---- prologue: generator blocks, x_0, the seed's largest ρ_k ----
+  {
+    const cx<double>* At = (const cx<double>*)g.At;
+    const size_t NN = (size_t)N * N;
+    for (int q = tid; q < 3 * E * nblk; q += nthr) {  // block-major [nblk][3][E]: compile-time offsets per block
+      const int beta = q / (3 * E), r = q - beta * 3 * E, j = r / E, e = r - j * E;
+      const int ri = bk.brow[beta * NB + e / NB], rk = bk.brow[beta * NB + e % NB];
+      cx<double> v = {0.0, 0.0};
+      if (j <= nu && ri >= 0 && rk >= 0) v = At[(size_t)j * NN + ri + (size_t)N * rk];
+      gsh[q] = make_double2(v.r, v.i);
+    }
+    const cx<double>* x0 = (const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0);
+    for (size_t o = tid; o < Nm; o += nthr) {
+      xN[2 * o] = x0[o].r;
+      xN[2 * o + 1] = x0[o].i;
+    }
+  }
+  const double* ub = sp.u + (size_t)b * Nt * nu;
+  double rmax = 0.0;
+  for (int k = tid; k < Nt; k += nthr) {
+    const double u1 = nu > 0 ? ub[(size_t)k * nu] : 0.0, u2 = nu > 1 ? ub[(size_t)k * nu + 1] : 0.0;
+    rmax = fmax(rmax, fma(fabs(u2), sp.rad[2], fma(fabs(u1), sp.rad[1], sp.rad[0])));
+  }
+  for (size_t i = tid; i < (size_t)Nt * nu; i += nthr) {  // the copies of u (the stale check, the lazy rebuilds)
+    const double v = ub[i];
+    if (sp.u_copy) sp.u_copy[(size_t)b * Nt * nu + i] = v;
+    if (sp.u_copy2) sp.u_copy2[(size_t)b * Nt * nu + i] = v;
+  }
+  rmax = block_max(rmax, red);
+  // J: the fewest halvings with ρ / 2^J <= θ_cap; P: the smallest degree whose tail bound
+  // b^{P+1} / (P+1)! / (1 - b / (P+2)) is <= 2^-53 (b = ρmax / 2^J; every slice's ρ_k is <= ρmax)
+  int J = 0;
+  double s0 = 1.0;
+  while (rmax * s0 > sp.theta_cap && J < 60) {
+    s0 *= 0.5;
+    ++J;
+  }
+  int P = 0;
+  {
+    const double bb = rmax * s0, tol = 1.1102230246251565e-16;
+    constexpr BlkuCoef K = blku_coef();
+    double term = bb;
+#pragma unroll
+    for (int q = 0; q < BLKU_TMAX; ++q) {
+      if (!(term > tol * fma(-bb, K.inv[q + 2], 1.0))) break;
+      P = q + 1;
+      term *= bb * K.inv[q + 2];
+    }
+  }
+  P = __builtin_amdgcn_readfirstlane(P);
+  J = __builtin_amdgcn_readfirstlane(J);
+  // records: e^{μ_k}, 2^-J u_1k, 2^-J u_2k
+  for (int k = tid; k < Nt; k += nthr) {
+    const double u1 = nu > 0 ? ub[(size_t)k * nu] : 0.0, u2 = nu > 1 ? ub[(size_t)k * nu + 1] : 0.0;
+    const double mr = fma(u2, sp.mur[2], fma(u1, sp.mur[1], sp.mur[0]));
+    const double mi = fma(u2, sp.mui[2], fma(u1, sp.mui[1], sp.mui[0]));
+    const double er = exp(mr);
+    double sn, cs;
+    sincos(mi, &sn, &cs);
+    double2* r = reinterpret_cast<double2*>(rec + 4 * (size_t)k);
+    r[0] = make_double2(er * cs, er * sn);
+    r[1] = make_double2(s0 * u1, s0 * u2);
+  }
+  __syncthreads();
+
+  // ---- the lane's unit: segment s, block beta ----
+  const int uw = l / nblk;
+  const bool lact = uw < sp.UPW;
+  const int beta = lact ? l - uw * nblk : 0;
+  const int s = w * sp.UPW + uw;
+  const bool sact = lact && s < S;
+  const int kb = sact ? s * L : 0;
+  const int ke = sact ? min(kb + L, Nt) : 0;
+  int brw[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) brw[i] = bk.brow[beta * NB + i];
+  double2 greg[GREG ? 3 : 1][GREG ? E : 1];
+  if constexpr (GREG) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int e = 0; e < E; ++e) greg[j][e] = gsh[(beta * 3 + j) * E + e];
+  }
+  // the generator blocks (blocks of 3 rows: read from LDS where used, through an opaque copy of the block index made
+  // inside each loop, so that the compiler does not hoist all 3 E of them into registers and spill)
+  auto gen_at = [&](int bc) {
+    return [&, bc](int j, int e) -> double2 {
+      if constexpr (GREG) return greg[j][e];
+      else return gsh[(bc * 3 + j) * E + e];
+    };
+  };
+  auto opaque = [](int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+
+  // ---- phase 1: the segment product P_s = U_{ke-1} .. U_{kb} ----
+  double qr[E], qi[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    qr[e] = e % (NB + 1) == 0 ? 1.0 : 0.0;
+    qi[e] = 0.0;
+  }
+  for (int jj = 0; jj < L; jj += NV1) {
+    const double* rk[NV1];
+    bool act[NV1];
+#pragma unroll
+    for (int v = 0; v < NV1; ++v) {
+      const int k = kb + jj + v;
+      act[v] = sact && jj + v < L && k < ke;
+      rk[v] = rec + 4 * (size_t)(act[v] ? k : 0);
+    }
+    double ar[NV1][E], ai[NV1][E], ur[NV1][E], ui[NV1][E];
+    seg_form<NB, NV1>(gen_at(GREG ? beta : opaque(beta)), rk, s0, P, J, ar, ai, ur, ui);
+#pragma unroll
+    for (int v = 0; v < NV1; ++v) {
+      double tr[E], ti[E];
+      seg_mm<NB, false, false>(ur[v], ui[v], qr, qi, tr, ti);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        qr[e] = act[v] ? tr[e] : qr[e];
+        qi[e] = act[v] ? ti[e] : qi[e];
+      }
+    }
+  }
+
+  // ---- phase 2: prefix products Q_s = P_s .. P_0 (Hillis-Steele over the segments) ----
+  auto slot_at = [&](int ss, int e) -> double2& { return slot[((size_t)ss * E + e) * nblk + beta]; };
+  if (sact)
+#pragma unroll
+    for (int e = 0; e < E; ++e) slot_at(s, e) = make_double2(qr[e], qi[e]);
+  lds_barrier();
+  for (int d = 1; d < S; d <<= 1) {
+    const bool take = sact && s >= d;
+    double tr[E], ti[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const double2 v = take ? slot_at(s - d, e) : make_double2(0.0, 0.0);
+      tr[e] = v.x;
+      ti[e] = v.y;
+    }
+    lds_barrier();
+    if (take) {
+      double cr[E], ci[E];
+      seg_mm<NB, false, false>(qr, qi, tr, ti, cr, ci);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        qr[e] = cr[e];
+        qi[e] = ci[e];
+        slot_at(s, e) = make_double2(cr[e], ci[e]);
+      }
+    }
+    lds_barrier();
+  }
+  // x_N = Q_{S-1} x_0 on each block (the last segment's lanes), in place in xN
+  const bool last = sact && s == S - 1;
+  if (last) {
+    for (int c = 0; c < m; ++c) {
+      double xr[NB], xi[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const size_t o = 2 * ((size_t)c * N + max(brw[i], 0));
+        xr[i] = brw[i] >= 0 ? xN[o] : 0.0;
+        xi[i] = brw[i] >= 0 ? xN[o + 1] : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        double yr = 0.0, yi = 0.0;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          yr = fma(qr[i * NB + q], xr[q], fma(-qi[i * NB + q], xi[q], yr));
+          yi = fma(qr[i * NB + q], xi[q], fma(qi[i * NB + q], xr[q], yi));
+        }
+        if (brw[i] >= 0) {
+          const size_t o = 2 * ((size_t)c * N + brw[i]);
+          xN[o] = yr;
+          xN[o + 1] = yi;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // J and the λ_N coefficients (src/penalty_fcns.jl:15-42)
+  chain_costs<double>(N, m, (const cx<double>*)g.Xt, [&](int q) { return cx<double>{xN[2 * q], xN[2 * q + 1]}; },
+                      g.cost_kind, g.n_norm, 0.0, red, red + 16, cf, g.sc);
+  __syncthreads();
+  if (tid < 2 * m) {
+    g.coef[(size_t)b * 2 * m + tid] = cf[tid];
+    if (sp.coef2) sp.coef2[(size_t)b * 2 * m + tid] = cf[tid];
+  }
+  if (tid == 0) {
+    g.J[b] = red[16];
+    if (sp.J2) sp.J2[b] = red[16];
+  }
+  // G_N = Σ_c x_N λ_N^H on each block, G_0 = Q_{S-1}^H G_N Q_{S-1}
+  if (last) {
+    const cx<double>* Xt = (const cx<double>*)g.Xt;
+    double gr[E], gi[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) gr[e] = gi[e] = 0.0;
+    for (int c = 0; c < m; ++c) {
+      double2 xv[NB], lv[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int r = brw[i];
+        const size_t o = (size_t)c * N + max(r, 0);
+        const cx<double> f = lam_coef(cf, g.sc, m, max(r, 0), c), t = Xt[o];
+        xv[i] = r >= 0 ? make_double2(xN[2 * o], xN[2 * o + 1]) : make_double2(0.0, 0.0);
+        lv[i] = r >= 0 ? make_double2(f.r * t.r - f.i * t.i, f.r * t.i + f.i * t.r) : make_double2(0.0, 0.0);
+      }
+      blku_kacc<NB>(gr, gi, xv, lv);
+    }
+    double tr[E], ti[E], cr[E], ci[E];
+    seg_mm<NB, true, false>(qr, qi, gr, gi, tr, ti);
+    seg_mm<NB, false, false>(tr, ti, qr, qi, cr, ci);
+#pragma unroll
+    for (int e = 0; e < E; ++e) g0s[e * nblk + beta] = make_double2(cr[e], ci[e]);
+  }
+  __syncthreads();
+  // G at the segment's end: Q_s G_0 Q_s^H
+  double Gr[E], Gi[E];
+  {
+    double hr[E], hi[E], tr[E], ti[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const double2 v = g0s[e * nblk + beta];
+      hr[e] = v.x;
+      hi[e] = v.y;
+    }
+    seg_mm<NB, false, false>(qr, qi, hr, hi, tr, ti);
+    seg_mm<NB, false, true>(tr, ti, qr, qi, Gr, Gi);
+  }
+
+  // ---- phase 3: each segment backwards, the gradient of every slice ----
+  const double mu1r = sp.mur[1], mu1i = sp.mui[1], mu2r = sp.mur[2], mu2i = sp.mui[2];
+  double* const wr = wred + 128 * w;
+  const int nred = sp.UPW * nu;  // reducing lanes: (segment of the wave, control)
+  const int ro = l / max(nu, 1), rj = l - ro * max(nu, 1);
+  for (int jj = L - 1; jj >= 0; --jj) {
+    const int k = kb + jj;
+    const bool act = sact && k < ke;
+    const double* rk[1] = {rec + 4 * (size_t)(act ? k : 0)};
+    const auto gen = gen_at(GREG ? beta : opaque(beta));
+    double ar[1][E], ai[1][E], ur[1][E], ui[1][E];
+    seg_form<NB, 1>(gen, rk, s0, P, J, ar, ai, ur, ui);
+    // K_k = U_k^H G_{k+1}, G_k = K_k U_k
+    double Kr[E], Ki[E], tr[E], ti[E];
+    seg_mm<NB, true, false>(ur[0], ui[0], Gr, Gi, Kr, Ki);
+    seg_mm<NB, false, false>(Kr, Ki, ur[0], ui[0], tr, ti);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      Gr[e] = act ? tr[e] : Gr[e];
+      Gi[e] = act ? ti[e] : Gi[e];
+    }
+    // X = A_k = 2^J Â + μ_k I, u_j = 2^J (2^-J u_j) exactly
+    const double2 su = *reinterpret_cast<const double2*>(rk[0] + 2);
+    const double u1 = ldexp(su.x, J), u2 = ldexp(su.y, J);
+    const double mkr = fma(u2, sp.mur[2], fma(u1, sp.mur[1], sp.mur[0]));
+    const double mki = fma(u2, sp.mui[2], fma(u1, sp.mui[1], sp.mui[0]));
+    double xr[E], xi[E];
+    if constexpr (GREG) {  // from the formation's Â
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        xr[e] = ldexp(ar[0][e], J) + (e % (NB + 1) == 0 ? mkr : 0.0);
+        xi[e] = ldexp(ai[0][e], J) + (e % (NB + 1) == 0 ? mki : 0.0);
+      }
+    } else {  // re-read (blocks of 3 rows: Â is not kept live across the two products)
+      const auto gen2 = gen_at(opaque(beta));
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const double2 g0 = gen2(0, e), g1 = gen2(1, e), g2 = gen2(2, e);
+        xr[e] = fma(u2, g2.x, fma(u1, g1.x, g0.x)) + (e % (NB + 1) == 0 ? mkr : 0.0);
+        xi[e] = fma(u2, g2.y, fma(u1, g1.y, g0.y)) + (e % (NB + 1) == 0 ? mki : 0.0);
+      }
+    }
+    double acc1, acc2;
+    seg_contract<NB, ORD>(gen, xr, xi, Kr, Ki, mu1r, mu1i, mu2r, mu2i, acc1, acc2);
+    // the slice's sum over its blocks: wave-private slot, fixed order
+    *reinterpret_cast<double2*>(wr + 2 * l) = make_double2(act ? acc1 : 0.0, act ? acc2 : 0.0);
+    wave_lds_sync();
+    if (l < nred) {
+      const int ss = w * sp.UPW + ro, kk = ss * L + jj;
+      if (ss < S && kk < Nt) {
+        double sum = 0.0;
+        for (int q = 0; q < nblk; ++q) sum += wr[2 * (ro * nblk + q) + rj];
+        dJ[(size_t)kk * nu + rj] = sum;
+      }
+    }
+    wave_lds_sync();
+  }
+  __syncthreads();
+  double* const og = sp.dJdu + (size_t)b * Nt * nu;
+  for (int i = tid; i < Nt * nu; i += nthr) og[i] = dJ[i];
+  if (sp.terms && tid == 0) atomicAdd(sp.terms + b % TERM_SLOTS, (unsigned long long)Nt * ((unsigned long long)P << J));
+}
+
+}  // namespace qoc

@@ -322,11 +322,16 @@ RcclApi& rccl() {
 }
 
 int forward(qoc_ctx* c) {
+  c->X_lazy = false;  // every forward path writes x_k
   if (blk_active(c)) return blk_forward(c);
   if (c->big) return c->prec == QOC_FP64 ? big_forward<double>(c) : big_forward<float>(c);
   return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
 }
 int backward(qoc_ctx* c, int order, double* d_dJdu) {
+  if (c->X_lazy) {  // after a segmented eval: the backward paths read x_k
+    const int r = blku_states(c);
+    if (r) return r;
+  }
   c->L_is_mu = false;  // every backward path below writes λ itself (the fused block backward: on demand)
   c->L_lazy = false;
   c->last_eval_mode = 0;
@@ -501,7 +506,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->d_coef_mu) hipFree(c->d_coef_mu);
   if (c->d_brow) hipFree(c->d_brow);
   if (c->d_wrow) hipFree(c->d_wrow);
-  void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L, c->d_u_lam, c->d_coef_lam, c->d_blkU,
+  void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L, c->d_u_lam, c->d_coef_lam, c->d_blkU, c->d_J_scr, c->d_coef_scr,
                   c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_pws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec, c->d_sink, c->d_blkrec};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -534,6 +539,7 @@ int qoc_synchronize(qoc_ctx* c) {
 int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
   if (!c || !A0 || !Aj) return fail(c, QOC_ERR_ARG, "null argument");
   HIPCHK(c, hipSetDevice(c->dev));
+  if (int r0 = blk_materialize(c)) return r0;  // x_k / λ_k kept lazily need the current system
   const size_t NN = (size_t)c->N * c->N;
   {  // host copy (compress_states needs block-diagonal generators; checked here and at qoc_set_compression)
     std::vector<double> g((size_t)(c->nu + 1) * 2 * NN);
@@ -598,7 +604,7 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
     c->tprm.pmin = c->cap_ok ? 2 : 1;  // the captured products are the first two of every slice
     // Chebyshev needs every Ã_j skew-Hermitian (A_j^H = -A_j, Schrödinger generators -i H Δt), so that
     // Ã_k = -i H̃_k has its spectrum on the imaginary axis within the bound ρ_k
-    bool skew = true;
+    bool skew = true, exact = true;
     for (int j = 0; j <= c->nu && skew; ++j) {
       const double* G = j == 0 ? A0 : Aj[j - 1];
       double amax = 0.0, dev = 0.0;
@@ -609,7 +615,9 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
           dev = std::max(dev, std::hypot(G[a] + G[b], G[a + 1] - G[b + 1]));  // |A + A^H|
         }
       skew = dev <= 1e-13 * std::max(amax, 1e-300);
+      exact = exact && dev <= 4.0 * 2.220446049250313e-16 * amax;  // -i H dt of an exactly Hermitian H: dev = 0
     }
+    c->skew_exact = skew && exact;
     std::vector<double> sh(2 * NN);
     for (int j = 0; j <= c->nu && r == QOC_OK; ++j) {
       const double* G = j == 0 ? A0 : Aj[j - 1];
@@ -665,6 +673,7 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
     else c->chain_mode = (cheb_run ? c->tprm.rad[0] <= 25.0 : c->tprm.nrm[0] <= 1.0) ? 1 : 0;
   } else {
     c->chain_mode = 0;
+    c->skew_exact = false;
   }
   if (c->tchain_ok) {  // invariant blocks of the generators (qoc_blk.hpp)
     r = blk_detect(c);
@@ -680,6 +689,7 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
 int qoc_set_x0(qoc_ctx* c, const double* x0, int per_seed) {
   if (!c || !x0) return fail(c, QOC_ERR_ARG, "null argument");
   HIPCHK(c, hipSetDevice(c->dev));
+  if (int r0 = blk_materialize(c)) return r0;  // x_k / λ_k kept lazily need the current system
   const size_t Nmu = (size_t)c->N * c->m_user, cnt = per_seed ? (size_t)c->B : 1;
   int r = upload_states(c, x0, c->d_x0, cnt, "x0");
   if (r != QOC_OK) return r;
@@ -700,6 +710,7 @@ int qoc_set_cost(qoc_ctx* c, int kind, const double* X_target, double n) {
   if (kind != QOC_COST_EXTERNAL && !X_target) return fail(c, QOC_ERR_ARG, "X_target is null");
   if (kind == QOC_COST_TRACE && !(n != 0.0)) return fail(c, QOC_ERR_ARG, "normalisation n must be nonzero");
   HIPCHK(c, hipSetDevice(c->dev));
+  if (int r0 = blk_materialize(c)) return r0;  // λ_k kept lazily needs the current target
   if (X_target) {
     int r = upload_states(c, X_target, c->d_Xt, 1, nullptr);
     if (r != QOC_OK) return r;
@@ -763,6 +774,7 @@ int qoc_set_compression(qoc_ctx* c, const int* rows1, int nr1, const int* cols1,
                         const int* cols2, int nc2) {
   if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
   HIPCHK(c, hipSetDevice(c->dev));
+  if (int r0 = blk_materialize(c)) return r0;  // x_k / λ_k kept lazily are in the current layout
   HIPCHK(c, hipStreamSynchronize(c->stream));  // queued kernels may still read the packed buffers
   const int N = c->N, mu_ = c->m_user;
   std::vector<unsigned char> rsec;
@@ -896,6 +908,22 @@ int qoc_grape_sensitivity_dev(qoc_ctx* c, const double* d_u, int order, double* 
 int qoc_eval_dev(qoc_ctx* c, const double* d_u, int order, double* d_J, double* d_dJdu) {
   if (c && c->cost_kind == QOC_COST_EXTERNAL)
     return fail(c, QOC_ERR_STATE, "qoc_eval_dev needs a device-side cost (TRACE or ZCAL)");
+  if (c && c->have_gen && blkseg_ok(c, order)) {
+    // block propagators with the time axis in segments: one launch reads u (and copies it to d_u) and writes J and
+    // dJdu; x_k and λ_k are rebuilt on demand (qoc_blkseg.hpp)
+    int r = check_ready(c);
+    if (r) return r;
+    if (!d_u) return fail(c, QOC_ERR_ARG, "d_u is null");
+    c->have_prop = false;
+    r = blkseg_eval(c, order, d_u, d_J, d_dJdu ? d_dJdu : c->d_dJdu);
+    if (r) return r;
+    c->props_since_reset++;
+    c->have_prop = true;
+    c->h_u.clear();
+    c->h_coef.clear();
+    return QOC_OK;
+  }
+  if (c) c->X_lazy = false;  // the other eval paths write x_k
   if (c && c->have_gen && (blk_concurrent_ok(c, order) || tchain_concurrent_ok(c, order))) {
     // forward chain and the μ recurrence side by side (tchain_eval_concurrent)
     int r = check_ready(c);
@@ -983,6 +1011,10 @@ int qoc_get_states(qoc_ctx* c, int seed, int k, double* x_out) {
   if (k == -1) k = c->Nt;
   if (seed < 0 || seed >= c->B || k < 0 || k > c->Nt) return fail(c, QOC_ERR_ARG, "index out of range");
   HIPCHK(c, hipSetDevice(c->dev));
+  if (c->X_lazy) {  // after a segmented eval: the states are rebuilt on demand
+    const int r = blku_states(c);
+    if (r) return r;
+  }
   const size_t Nm = (size_t)c->N * c->m;
   return download_states(c, (char*)c->d_X + ((size_t)seed * (c->Nt + 1) + k) * Nm * c->esz, x_out);
 }
@@ -1208,6 +1240,7 @@ int qoc_spline_constraints_dev(qoc_ctx* c, const double* d_c, double* d_g, doubl
 
 int qoc_set_propagation(qoc_ctx* c, int method, int nsub) {
   if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  if (int r0 = blk_materialize(c)) return r0;  // x_k / λ_k kept lazily are rebuilt by the current path
   if (method != QOC_PROP_EXPM && method != QOC_PROP_TSIT5) return fail(c, QOC_ERR_ARG, "unknown method %d", method);
   if (method == QOC_PROP_TSIT5) {
     if (nsub < 1) return fail(c, QOC_ERR_ARG, "nsub must be >= 1 (got %d)", nsub);
@@ -1270,7 +1303,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[5] = c->big ? c->expm_alg : c->expm_run;  // the large-N pipeline keeps its own (Taylor / Padé) choice
   info[6] = c->chain_mode == 1 && c->cheb && tchain_mf(c) ? 1 : 0;  // Taylor-action chains: Chebyshev terms
   info[7] = c->m;  // state columns the kernels run on (< the caller's m when compress_states packing is on)
-  info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 / 3 / 4 concurrent μ recurrence, 5 fused block gradient
+  info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 / 3 / 4 concurrent μ recurrence, 5 fused block gradient, 6 segmented block eval
   info[9] = c->fwd_captured ? 1 : 0;
   info[10] = blk_active(c) ? (blku_on(c) ? 5 : blk_rot(c) ? 4 : 3) : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
   return QOC_OK;
@@ -1278,6 +1311,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
 
 int qoc_set_chain(qoc_ctx* c, int mode) {
   if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  if (int r0 = blk_materialize(c)) return r0;  // x_k / λ_k kept lazily are rebuilt by the current path
   if (mode != QOC_CHAIN_AUTO && mode != QOC_CHAIN_PROPAGATORS && mode != QOC_CHAIN_TAYLOR)
     return fail(c, QOC_ERR_ARG, "unknown chain mode %d", mode);
   if (mode == QOC_CHAIN_TAYLOR && !c->tchain_ok)

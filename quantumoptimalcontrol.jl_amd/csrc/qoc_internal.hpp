@@ -153,6 +153,15 @@ struct qoc_ctx {
                                  // (blku_costates) from the saved u and λ_N coefficients
   double* d_u_lam = nullptr;     // B x Nt x nu: u of that backward
   void* d_blkU = nullptr;        // B x Nt x NB^2 x nblk complex: block propagators of the eval's forward (fused backward)
+  size_t blkU_bytes = 0;         // its allocated size (reallocated when a new block layout needs more)
+  // the segmented block eval (qoc_blkseg.hpp) writes neither x_k nor λ_k: qoc_get_states / a later backward rebuild
+  // the states on demand (blku_states) from the u in d_u, with J and the coefficients going to scratch
+  bool X_lazy = false;
+  double* d_J_scr = nullptr;         // B
+  cx<double>* d_coef_scr = nullptr;  // B x 2m
+  // every generator exactly skew-Hermitian (|A + A^H| <= 4 eps max|A|): the slice propagators are unitary, which the
+  // segmented eval's backward relies on (λ_{k+1} = U_k λ_k)
+  bool skew_exact = false;
   cx<double>* d_coef_lam = nullptr;  // B x 2m: its λ_N coefficients
   cx<double>* d_coef_mu = nullptr;  // B x 2m: the λ_N coefficients of the eval that left μ in d_L
   int last_eval_mode = 0;        // 0 other, 1 captured sequential backward, 2 / 3 concurrent μ mode: two streams /
@@ -295,5 +304,10 @@ int blk_forward(qoc_ctx* c);
 int blk_backward(qoc_ctx* c, int order, double* d_dJdu);
 bool blk_concurrent_ok(const qoc_ctx* c, int order);
 int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu);
+// the segmented block eval (qoc_blkseg.hpp): one launch for J and dJdu, x_k / λ_k rebuilt on demand
+bool blkseg_ok(const qoc_ctx* c, int order);
+int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d_dJdu);
+int blku_states(qoc_ctx* c);      // rebuild x_k after a segmented eval (no-op unless X_lazy)
+int blk_materialize(qoc_ctx* c);  // rebuild every lazily kept x_k / λ_k (before a setter changes what they need)
 
 }  // namespace qoc_host

@@ -4,6 +4,7 @@
 #include <numeric>
 
 #include "qoc_blk.hpp"
+#include "qoc_blkseg.hpp"
 #include "qoc_blku.hpp"
 #include "qoc_internal.hpp"
 
@@ -186,10 +187,16 @@ static BlkuShape blku_shape(const qoc_ctx* c, bool fused, bool storeu = false) {
   // x_k and propagators (QOC_BLKU_USTG=1: then the freed wave slot is a worker's)
   const char* us = getenv("QOC_BLKU_USTG");
   s.ustg = storeu && us && atoi(us) == 1 ? 1 : 2;
-  const int stg = fused ? (storeu && s.ustg == 2 ? 2 : 1) : 0;
+  int stg = fused ? (storeu && s.ustg == 2 ? 2 : 1) : 0;
   // waves per workgroup at most: the kernels' launch bound (blku_max_threads: 12 waves for blocks of 2 rows), shared
   // by the workgroups of a CU
   const int wcap = blku_max_threads(NB) / 64;
+  // the fused backward needs at least one worker wave (the contraction runs on workers only): with the second
+  // staging wave that would not fit (blocks of 4 rows, nblk m > 16: CW = 2 within 4 waves), one stager copies all
+  if (fused && stg == 2 && s.CW + stg + 1 > wcap) {
+    s.ustg = 1;
+    stg = 1;
+  }
   const int wmax = std::max(s.CW + stg + 1, wcap / per_cu);
   int fw = wmax - s.CW - stg;
   if (const char* env = getenv(fused ? "QOC_BLKU_GFW" : "QOC_BLKU_FW")) fw = atoi(env);
@@ -216,18 +223,20 @@ static BlkuShape blku_shape(const qoc_ctx* c, bool fused, bool storeu = false) {
       if (per_slice(C) < per_slice(s.C) - 1e-12) s.C = C;
   }
   if (const char* env = getenv(fused ? "QOC_BLKU_GC" : "QOC_BLKU_C")) {
+    // an override is clamped to what fits (the stager's registers and the LDS budget), never an invalid launch
     int q = 1;
     if (fused) {
       q = std::max(1, std::min(atoi(env), 64));
-      while (q > 1 && !stage_ok(q)) --q;
+      while (q > 1 && !fits(q)) --q;
     } else {
-      while (q * 2 <= std::min(atoi(env), 64) && stage_ok(q * 2)) q *= 2;
+      while (q * 2 <= std::min(atoi(env), 64) && fits(q * 2)) q *= 2;
     }
     s.C = q;
   }
   s.C = std::max(s.C, s.S);
   s.lds = blku_lds(c->N, c->m, NB, c->nblk, s.C, gw);
   s.W = std::min(s.W, wcap);  // never above the launch bound (a larger launch faults)
+  if (fused && s.W < s.CW + stg + 1) s.W = 0;  // no worker wave: not launchable (blku_fused_ok refuses it)
   return s;
 }
 
@@ -484,8 +493,7 @@ static hipError_t blku_sdispatch(int S, F&& f) {
   return f(integral_constant<int, 1>());
 }
 
-static hipError_t blku_launch_fwd(qoc_ctx* c, const BlkuShape& s, const BlkuParams& bp) {
-  const TChainArgs g = tchain_args(c);
+static hipError_t blku_launch_fwd_g(qoc_ctx* c, const TChainArgs& g, const BlkuShape& s, const BlkuParams& bp) {
   const BlkArgs bk = blk_args(c);
   return blku_dispatch(c, [&](auto NB_) {
     constexpr int NB = decltype(NB_)::value;
@@ -497,6 +505,10 @@ static hipError_t blku_launch_fwd(qoc_ctx* c, const BlkuShape& s, const BlkuPara
       return hipGetLastError();
     });
   });
+}
+
+static hipError_t blku_launch_fwd(qoc_ctx* c, const BlkuShape& s, const BlkuParams& bp) {
+  return blku_launch_fwd_g(c, tchain_args(c), s, bp);
 }
 
 static int blku_forward(qoc_ctx* c) {
@@ -567,13 +579,15 @@ static hipError_t blku_launch_bwd(qoc_ctx* c, const TChainArgs& g, const BlkuSha
 // qoc_get_costates recomputes it on demand from a copy of this evaluation's u and λ_N coefficients (blku_costates).
 static bool blku_fused_ok(const qoc_ctx* c, int order) {
   const char* env = getenv("QOC_BLKU_FUSED");
-  return order >= 1 && order <= BLK_ORDMAX && c->mu == 0.0 && !c->src_on && !(env && !std::strcmp(env, "0"));
+  return order >= 1 && order <= BLK_ORDMAX && c->mu == 0.0 && !c->src_on && !(env && !std::strcmp(env, "0")) &&
+         blku_shape(c, true, false).W > 0;
 }
 
 static int blku_bwdg(qoc_ctx* c, int order, double* d_dJdu, const double2* Uin = nullptr) {
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
   const BlkuShape s = blku_shape(c, true, Uin != nullptr);
+  if (s.W <= 0) return fail(c, QOC_ERR_UNSUPPORTED, "fused block backward: no worker wave fits the launch bound");
   BlkuParams bp = blku_params(c, s, d_dJdu);  // the records are current (the caller's)
   bp.Uin = Uin;
   bp.ustg = s.ustg;
@@ -657,10 +671,18 @@ static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
   const char* su = getenv("QOC_BLKU_STOREU");
   const bool fused = blku_fused_ok(c, order);
   const bool storeu = fused && blku_shape(c, true, true).S == 1 && !(su && !std::strcmp(su, "0"));
-  if (storeu && !c->d_blkU) {
-    const size_t bytes = (size_t)c->B * c->Nt * c->blk_nb * c->blk_nb * c->nblk * sizeof(double2);
-    HIPCHK(c, hipMalloc((void**)&c->d_blkU, bytes));
-    c->dev_bytes += bytes;
+  const size_t ubytes = (size_t)c->B * c->Nt * c->blk_nb * c->blk_nb * c->nblk * sizeof(double2);
+  if (storeu && c->blkU_bytes < ubytes) {  // a new block layout (qoc_set_generators) may need more
+    if (c->d_blkU) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipFree(c->d_blkU));
+      c->d_blkU = nullptr;
+      c->dev_bytes -= c->blkU_bytes;
+      c->blkU_bytes = 0;
+    }
+    HIPCHK(c, hipMalloc((void**)&c->d_blkU, ubytes));
+    c->blkU_bytes = ubytes;
+    c->dev_bytes += ubytes;
   }
   bp.Uout = storeu ? (double2*)c->d_blkU : nullptr;
   const int mk = mark_begin(c, 1);
@@ -682,6 +704,131 @@ static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
   if (r) return r;
   c->L_is_mu = false;
   return QOC_OK;
+}
+
+// ---- segmented block eval (qoc_blkseg.hpp) -------------------------------------------------------------------------
+struct BlksegShape {
+  int W, S, L, UPW;
+  size_t lds;
+};
+// One workgroup per seed with W waves (8 at one seed per CU, fewer when several seeds share a CU: 8 wave slots at the
+// kernel's <= 256 VGPRs), UPW = 64 / nblk segments per wave, S = W UPW segments of L = ceil(Nt / S) slices (then S
+// trimmed so that no segment is empty).  QOC_BLKSEG_W / QOC_BLKSEG_S override the waves / cap the segments.
+static BlksegShape blkseg_shape(const qoc_ctx* c) {
+  BlksegShape s{};
+  const int per_cu = std::max(1, std::min(8, (c->B + c->ncu - 1) / std::max(1, c->ncu)));
+  s.W = std::max(1, 8 / per_cu);
+  if (const char* env = getenv("QOC_BLKSEG_W")) s.W = std::max(1, std::min(8, atoi(env)));
+  s.UPW = 64 / std::max(1, c->nblk);
+  int S = std::max(1, std::min(s.W * s.UPW, c->Nt));
+  if (const char* env = getenv("QOC_BLKSEG_S")) S = std::max(1, std::min(S, atoi(env)));
+  s.L = (c->Nt + S - 1) / S;
+  s.S = (c->Nt + s.L - 1) / s.L;
+  s.W = (s.S + s.UPW - 1) / s.UPW;
+  s.lds = blkseg_lds(c->N, c->m, c->nu, c->blk_nb, c->nblk, c->Nt, s.S, s.W);
+  return s;
+}
+
+// The segmented eval applies to block propagators of blocks of <= 3 rows with exactly skew-Hermitian generators
+// (unitary slices), the built-in costs, no penalty and no co-state source; QOC_BLKSEG=0 keeps the forward + fused
+// backward of k_blku_*.
+bool blkseg_ok(const qoc_ctx* c, int order) {
+  if (!blku_on(c) || (c->blk_nb != 2 && c->blk_nb != 3) || !c->skew_exact || c->nblk > 32) return false;
+  if (order < 1 || order > BLK_ORDMAX || c->mu != 0.0 || c->src_on) return false;
+  if (c->cost_kind != QOC_COST_TRACE && c->cost_kind != QOC_COST_ZCAL) return false;
+  const char* env = getenv("QOC_BLKSEG");
+  if (env && !std::strcmp(env, "0")) return false;
+  return blkseg_shape(c).lds <= (size_t)160 * 1024;
+}
+
+template <typename F>
+static hipError_t blkseg_dispatch(int NB, int order, F&& f) {
+  return blk_order_dispatch(order, [&](auto ORD_) {
+    if (NB == 2) return f(std::integral_constant<int, 2>(), ORD_);
+    return f(std::integral_constant<int, 3>(), ORD_);
+  });
+}
+
+static int ensure_lazy_bufs(qoc_ctx* c) {
+  const size_t nu_t = (size_t)c->B * c->nu * c->Nt, ncf = (size_t)c->B * 2 * c->m_user;
+  if (!c->d_u_lam) {
+    HIPCHK(c, hipMalloc((void**)&c->d_u_lam, nu_t * sizeof(double)));
+    HIPCHK(c, hipMalloc((void**)&c->d_coef_lam, ncf * sizeof(cx<double>)));
+    c->dev_bytes += nu_t * sizeof(double) + ncf * sizeof(cx<double>);
+  }
+  return QOC_OK;
+}
+
+int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d_dJdu) {
+  const BlksegShape s = blkseg_shape(c);
+  int r = ensure_lazy_bufs(c);
+  if (r) return r;
+  const TChainArgs g = tchain_args(c);
+  const BlkArgs bk = blk_args(c);
+  BlksegParams sp{};
+  for (int j = 0; j < 3; ++j) {
+    const bool on = j <= c->nu;
+    sp.rad[j] = on ? c->tprm.rad[j] : 0.0;  // skew-Hermitian: spectral half-widths of the shifted generators
+    sp.mur[j] = on ? c->tprm.mur[j] : 0.0;
+    sp.mui[j] = on ? c->tprm.mui[j] : 0.0;
+  }
+  sp.theta_cap = c->tprm.theta[17];
+  sp.S = s.S;
+  sp.L = s.L;
+  sp.UPW = s.UPW;
+  sp.u = d_u;
+  sp.u_copy = d_u != c->d_u ? c->d_u : nullptr;
+  sp.u_copy2 = c->d_u_lam;  // the co-states' rebuild (blku_costates) reads this copy and d_coef_lam
+  sp.J2 = d_J && d_J != c->d_J ? d_J : nullptr;
+  sp.coef2 = c->d_coef_lam;
+  sp.dJdu = d_dJdu;
+  sp.terms = c->d_terms;
+  const int mk = mark_begin(c, 2);
+  const hipError_t e = blkseg_dispatch(c->blk_nb, order, [&](auto NB_, auto ORD_) {
+    constexpr int NB = decltype(NB_)::value, ORD = decltype(ORD_)::value;
+    const hipError_t q = blk_lds_attr(k_blkseg_eval<NB, ORD>, s.lds);
+    if (q != hipSuccess) return q;
+    hipLaunchKernelGGL((k_blkseg_eval<NB, ORD>), dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, sp);
+    return hipGetLastError();
+  });
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blkseg_eval launch: %s", hipGetErrorString(e));
+  c->fwd_captured = false;
+  c->L_is_mu = false;
+  c->X_lazy = true;
+  c->L_lazy = true;
+  c->last_eval_mode = 6;
+  return QOC_OK;
+}
+
+// x_k of the last segmented eval: the block forward chain on the u it left in d_u, J and the coefficients into
+// scratch (the eval's own values stay as they were)
+int blku_states(qoc_ctx* c) {
+  if (!c->X_lazy) return QOC_OK;
+  if (!c->d_J_scr) {
+    HIPCHK(c, hipMalloc((void**)&c->d_J_scr, (size_t)c->B * sizeof(double)));
+    HIPCHK(c, hipMalloc((void**)&c->d_coef_scr, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
+    c->dev_bytes += (size_t)c->B * (sizeof(double) + 2 * c->m_user * sizeof(cx<double>));
+  }
+  TChainArgs g = tchain_args(c);
+  g.J = c->d_J_scr;
+  g.coef = c->d_coef_scr;
+  g.pmask = nullptr;
+  const BlkuShape s = blku_shape(c, false);
+  BlkuParams bp = blku_params(c, s);
+  int r = blku_records(c, bp, false);
+  if (r) return r;
+  const hipError_t e = blku_launch_fwd_g(c, g, s, bp);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blku_fwd launch (states): %s", hipGetErrorString(e));
+  c->X_lazy = false;
+  return QOC_OK;
+}
+
+int blk_materialize(qoc_ctx* c) {
+  int r = QOC_OK;
+  if (c->X_lazy) r = blku_states(c);
+  if (r == QOC_OK && c->L_lazy) r = blku_costates(c);
+  return r;
 }
 
 }  // namespace qoc_host

@@ -68,6 +68,8 @@ def _engine(prob, B, blocks, monkeypatch, penalty=None, chain="taylor"):
     monkeypatch.setenv("QOC_BLKU", "0" if blocks == "mfma" else "1")
     monkeypatch.setenv("QOC_BLKU_FUSED", "0" if blocks == "propsplit" else "1")
     monkeypatch.setenv("QOC_BLKU_S", "2" if blocks == "props2" else "1")
+    # the forward + fused backward of k_blku_* on device evals too (the segmented eval: tests/test_gpu_blkseg.py)
+    monkeypatch.setenv("QOC_BLKSEG", "0")
     e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
     e.set_cost_trace(prob.x_target, prob.n)
     e.set_chain(chain)
