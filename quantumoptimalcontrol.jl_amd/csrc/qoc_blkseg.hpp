@@ -69,8 +69,25 @@ __host__ __device__ inline size_t blkseg_lds(int N, int m, int nu, int NB, int n
   return (blkseg_off_dJ(N, m, NB, nblk, Nt, S, W) + (size_t)Nt * nu) * sizeof(double);
 }
 
-// launch bound: 8 waves (2 per SIMD, <= 256 VGPRs)
-constexpr int BLKSEG_THREADS = 512;
+// Diagnostic per-wave stamps (tools/blkseg_probe.hip, -DQOC_PROBE): workgroup 7, wave w: phase 1 ends at
+// g_segw[w], phase 3 at g_segw[16 + w] (cycles from the workgroup's start)
+#ifdef QOC_PROBE
+static __device__ unsigned long long g_segw[32];
+#define SEGW_SET(slot, v)                                                        \
+  do {                                                                           \
+    if (blockIdx.x == 7 && (threadIdx.x & 63) == 0) g_segw[slot] = (v);          \
+  } while (0)
+static __device__ int g_seg_noturn;
+#define SEG_TURNS (!g_seg_noturn)
+#else
+#define SEG_TURNS true
+#define SEGW_SET(slot, v) \
+  do {                    \
+  } while (0)
+#endif
+
+// launch bounds: WMAX = 8 waves (2 per SIMD, <= 256 VGPRs: the lane's generator blocks in registers) or 12 (3 per
+// SIMD, <= 168 VGPRs: generator blocks read from LDS where used)
 
 // c = a b, c = a^H b, c = a b^H on NB x NB complex blocks (row-major)
 template <int NB, bool AH, bool BH>
@@ -92,6 +109,26 @@ __device__ __forceinline__ void seg_mm(const double (&ar)[NB * NB], const double
       cr[i * NB + k] = sr;
       ci[i * NB + k] = si;
     }
+}
+
+// cos x and sin x / x as polynomials in x^2 (Horner, a fixed degree BLKSEG_KMAX = 9: the terms of exp(B) up to
+// B^19, whose tail is below 2^-53 for every |x| <= θ_cap ≈ 0.98, so at least the Taylor polynomial's degree P; a
+// fixed count keeps the loop free of branches and uniform masks)
+constexpr int BLKSEG_KMAX = 9;
+struct BlksegTrig {
+  double c[BLKSEG_KMAX + 1];  // (-1)^k / (2k)!
+  double s[BLKSEG_KMAX + 1];  // (-1)^k / (2k+1)!
+};
+constexpr BlksegTrig blkseg_trig() {
+  BlksegTrig t{};
+  double f = 1.0;  // 1 / n!
+  for (int n = 0; n <= 2 * BLKSEG_KMAX + 1; ++n) {
+    if (n > 0) f /= n;
+    const double sg = (n / 2) % 2 ? -1.0 : 1.0;
+    if (n % 2 == 0) t.c[n / 2] = sg * f;
+    else t.s[n / 2] = sg * f;
+  }
+  return t;
 }
 
 // Â = 2^-J Ã_k on the lane's block and U_k = e^{μ_k} (p(Â))^{2^J} for NV slices at once (independent recurrences
@@ -116,6 +153,43 @@ __device__ __forceinline__ void seg_form(GEN&& gen, const double* const (&rk)[NV
       const double2 g0 = gen(0, e), g1 = gen(1, e), g2 = gen(2, e);
       ar[v][e] = fma(su.y, g2.x, fma(su.x, g1.x, s0 * g0.x));
       ai[v][e] = fma(su.y, g2.y, fma(su.x, g1.y, s0 * g0.y));
+    }
+  }
+  if constexpr (NB == 2) {
+    if (J == 0) {
+      // blocks of 2 rows without halvings: the closed form.  Â is exactly skew-Hermitian (the host checks the
+      // generators exactly; the scaled sums keep it so): Â = i t I + B with Â_00 = i (t + a), Â_11 = i (t - a),
+      // B_01 = Â_01, B_10 = Â_10 = -conj(Â_01), B^2 = -ω^2 I, ω^2 = a^2 + |Â_01|^2, so
+      //   exp(Â) = e^{i t} (cos ω I + (sin ω / ω) B)
+      // with |t|, ω <= ρ <= θ_cap (the eigenvalues i (t ± ω) of Â lie within ±i ρ_k): both series to degree 19,
+      // beyond the Taylor polynomial's P, so U_k agrees with it to rounding
+      constexpr BlksegTrig T = blkseg_trig();
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const double t = 0.5 * (ai[v][0] + ai[v][3]), a = 0.5 * (ai[v][0] - ai[v][3]);
+        const double w = fma(a, a, fma(ar[v][1], ar[v][1], ai[v][1] * ai[v][1])), t2 = t * t;
+        double cw = 0.0, sw = 0.0, ct = 0.0, st = 0.0;
+#pragma unroll
+        for (int k = BLKSEG_KMAX; k >= 0; --k) {
+          cw = fma(cw, w, T.c[k]);
+          sw = fma(sw, w, T.s[k]);
+          ct = fma(ct, t2, T.c[k]);
+          st = fma(st, t2, T.s[k]);
+        }
+        st *= t;  // sin t
+        // z = e^{μ_k} e^{i t};  U = z cos ω I + z sinc ω B
+        const double zr = qr[v] * ct - qi[v] * st, zi = fma(qr[v], st, qi[v] * ct);
+        const double cr = zr * cw, ci = zi * cw, sr = zr * sw, si = zi * sw;
+        ur[v][0] = fma(-si, a, cr);
+        ui[v][0] = fma(sr, a, ci);
+        ur[v][3] = fma(si, a, cr);
+        ui[v][3] = fma(-sr, a, ci);
+        ur[v][1] = fma(sr, ar[v][1], -si * ai[v][1]);
+        ui[v][1] = fma(sr, ai[v][1], si * ar[v][1]);
+        ur[v][2] = fma(sr, ar[v][2], -si * ai[v][2]);
+        ui[v][2] = fma(sr, ai[v][2], si * ar[v][2]);
+      }
+      return;
     }
   }
   blku_taylor<NB, NV>(ar, ai, P, pr, pi, nullptr, ur, ui);
@@ -158,14 +232,25 @@ __device__ __forceinline__ void seg_trace(GEN&& gen, const double (&Lr)[NB * NB]
   acc2 = fma(f, fma(m2r, tr, fma(-m2i, ti, a2)), acc2);
 }
 
-template <int NB, int ORD, typename GEN>
+// MACC: accumulate M = Σ_n L_n / (n+1)! and take the traces once (fewer flops, one more live matrix: blocks of 2
+// rows); otherwise the traces order by order (blocks of 3 rows, where the registers are short)
+template <int NB, int ORD, bool MACC, typename GEN>
 __device__ __forceinline__ void seg_contract(GEN&& gen, const double (&xr_)[NB * NB], const double (&xi_)[NB * NB],
                                              double (&Lr)[NB * NB], double (&Li)[NB * NB], double m1r, double m1i,
                                              double m2r, double m2i, double& acc1, double& acc2) {
   constexpr int E = NB * NB;
   constexpr double invf[6] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120};
   acc1 = acc2 = 0.0;
-  seg_trace<NB>(gen, Lr, Li, 1.0, m1r, m1i, m2r, m2i, acc1, acc2);
+  double Mr[MACC ? E : 1], Mi[MACC ? E : 1];
+  if constexpr (MACC) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      Mr[e] = Lr[e];
+      Mi[e] = Li[e];
+    }
+  } else {
+    seg_trace<NB>(gen, Lr, Li, 1.0, m1r, m1i, m2r, m2i, acc1, acc2);
+  }
   if constexpr (ORD > 1) {
     double Rr[E], Ri[E];
 #pragma unroll
@@ -213,11 +298,104 @@ __device__ __forceinline__ void seg_contract(GEN&& gen, const double (&xr_)[NB *
         for (int i = 0; i < NB; ++i) {
           Lr[i * NB + kk] = tr[i];
           Li[i * NB + kk] = ti[i];
+          if constexpr (MACC) {
+            Mr[i * NB + kk] = fma(invf[n + 1], tr[i], Mr[i * NB + kk]);
+            Mi[i * NB + kk] = fma(invf[n + 1], ti[i], Mi[i * NB + kk]);
+          }
         }
       }
-      seg_trace<NB>(gen, Lr, Li, invf[n + 1], m1r, m1i, m2r, m2i, acc1, acc2);
+      if constexpr (!MACC) seg_trace<NB>(gen, Lr, Li, invf[n + 1], m1r, m1i, m2r, m2i, acc1, acc2);
     }
   }
+  if constexpr (MACC) seg_trace<NB>(gen, Mr, Mi, 1.0, m1r, m1i, m2r, m2i, acc1, acc2);
+}
+
+// ---- blocks of 2 rows, exactly skew-Hermitian: [[i d0, r + i q], [-r + i q, i d1]] (4 reals instead of 8) ----
+struct Sk2 {
+  double d0, d1, r, q;
+};
+__device__ __forceinline__ Sk2 sk2_of(const double2 (&e)[4]) { return Sk2{e[0].y, e[3].y, e[1].x, e[1].y}; }
+
+// Â = Ã_0 + u_1 Ã_1 + u_2 Ã_2 (no halvings) and U = e^{μ_k} exp(Â) in the closed form of seg_form (ph = e^{μ_k})
+__device__ __forceinline__ void sk2_form(const Sk2 (&g)[3], double2 ph, double2 u, Sk2& ah, double (&ur)[4],
+                                         double (&ui)[4]) {
+  constexpr BlksegTrig T = blkseg_trig();
+  ah.d0 = fma(u.y, g[2].d0, fma(u.x, g[1].d0, g[0].d0));
+  ah.d1 = fma(u.y, g[2].d1, fma(u.x, g[1].d1, g[0].d1));
+  ah.r = fma(u.y, g[2].r, fma(u.x, g[1].r, g[0].r));
+  ah.q = fma(u.y, g[2].q, fma(u.x, g[1].q, g[0].q));
+  const double t = 0.5 * (ah.d0 + ah.d1), a = 0.5 * (ah.d0 - ah.d1);
+  const double w = fma(a, a, fma(ah.r, ah.r, ah.q * ah.q)), t2 = t * t;
+  double cw = 0.0, sw = 0.0, ct = 0.0, st = 0.0;
+#pragma unroll
+  for (int k = BLKSEG_KMAX; k >= 0; --k) {
+    cw = fma(cw, w, T.c[k]);
+    sw = fma(sw, w, T.s[k]);
+    ct = fma(ct, t2, T.c[k]);
+    st = fma(st, t2, T.s[k]);
+  }
+  st *= t;
+  const double zr = ph.x * ct - ph.y * st, zi = fma(ph.x, st, ph.y * ct);
+  const double cr = zr * cw, ci = zi * cw, sr = zr * sw, si = zi * sw;
+  ur[0] = fma(-si, a, cr);
+  ui[0] = fma(sr, a, ci);
+  ur[3] = fma(si, a, cr);
+  ui[3] = fma(-sr, a, ci);
+  ur[1] = fma(sr, ah.r, -si * ah.q);  // z sinc(ω) (r + i q)
+  ui[1] = fma(sr, ah.q, si * ah.r);
+  ur[2] = fma(-sr, ah.r, -si * ah.q);  // z sinc(ω) (-r + i q)
+  ui[2] = fma(sr, ah.q, -si * ah.r);
+}
+
+// R <- R X in place, X skew-Hermitian (x0, x1, yr + i yq): 12 FMAs per row instead of 16
+__device__ __forceinline__ void sk2_rx(double (&Rr)[4], double (&Ri)[4], const Sk2& x) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double p0r = Rr[2 * i], p0i = Ri[2 * i], p1r = Rr[2 * i + 1], p1i = Ri[2 * i + 1];
+    Rr[2 * i] = fma(-p0i, x.d0, fma(-p1r, x.r, -p1i * x.q));
+    Ri[2 * i] = fma(p0r, x.d0, fma(p1r, x.q, -p1i * x.r));
+    Rr[2 * i + 1] = fma(p0r, x.r, fma(-p0i, x.q, -p1i * x.d1));
+    Ri[2 * i + 1] = fma(p0r, x.q, fma(p0i, x.r, p1r * x.d1));
+  }
+}
+// L <- X L + R in place, X skew-Hermitian
+__device__ __forceinline__ void sk2_xlr(double (&Lr)[4], double (&Li)[4], const double (&Rr)[4], const double (&Ri)[4],
+                                        const Sk2& x) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const double c0r = Lr[k], c0i = Li[k], c1r = Lr[2 + k], c1i = Li[2 + k];
+    Lr[k] = fma(-x.d0, c0i, fma(x.r, c1r, fma(-x.q, c1i, Rr[k])));
+    Li[k] = fma(x.d0, c0r, fma(x.r, c1i, fma(x.q, c1r, Ri[k])));
+    Lr[2 + k] = fma(-x.r, c0r, fma(-x.q, c0i, fma(-x.d1, c1i, Rr[2 + k])));
+    Li[2 + k] = fma(-x.r, c0i, fma(x.q, c0r, fma(x.d1, c1r, Ri[2 + k])));
+  }
+}
+// Re tr(A_j M) for j = 1, 2 with M = Σ_{a+b<ORD} X^b K X^a / (a+b+1)! (seg_contract's recurrence on skew X) and
+// A_j = Ã_j + i m_j I: -(d0 + m) Im M00 - (d1 + m) Im M11 + r (Re M10 - Re M01) - q (Im M10 + Im M01); e_j = (d0 + m,
+// d1 + m, r, q) of each generator.  K is overwritten.
+template <int ORD>
+__device__ __forceinline__ void sk2_contract(const Sk2& x, const Sk2& e1, const Sk2& e2, double (&Lr)[4],
+                                             double (&Li)[4], double& acc1, double& acc2) {
+  constexpr double invf[6] = {1.0, 1.0, 0.5, 1.0 / 6, 1.0 / 24, 1.0 / 120};
+  double Mr[4], Mi[4], Rr[4], Ri[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    Mr[e] = Rr[e] = Lr[e];
+    Mi[e] = Ri[e] = Li[e];
+  }
+#pragma unroll
+  for (int n = 1; n < ORD; ++n) {
+    sk2_rx(Rr, Ri, x);
+    sk2_xlr(Lr, Li, Rr, Ri, x);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      Mr[e] = fma(invf[n + 1], Lr[e], Mr[e]);
+      Mi[e] = fma(invf[n + 1], Li[e], Mi[e]);
+    }
+  }
+  const double dr = Mr[2] - Mr[1], di = Mi[2] + Mi[1];
+  acc1 = fma(-e1.d0, Mi[0], fma(-e1.d1, Mi[3], fma(e1.r, dr, -e1.q * di)));
+  acc2 = fma(-e2.d0, Mi[0], fma(-e2.d1, Mi[3], fma(e2.r, dr, -e2.q * di)));
 }
 
 __device__ __forceinline__ double block_max(double v, double* scratch) {
@@ -241,19 +419,31 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Waves w, w + 4, w + 8 of a workgroup share a SIMD, and the oldest one wins the VALU issue arbitration: it would
+// finish its segments far ahead and leave its partners alone on the SIMD at the end of each phase.  The partners
+// take the priority in turns, one slice-step each.
+__device__ __forceinline__ void seg_turn(int grp, int ngrp, int jj) {
+  if ((grp + jj) % ngrp == 0) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
 // One workgroup per seed (blockIdx.x), W = blockDim / 64 waves, UPW segments of nblk lanes per wave (lanes past
 // UPW nblk idle).  Built-in costs only (TRACE / ZCAL), no state penalty, no co-state source, unpacked states,
 // skew-Hermitian generators (the host's blkseg_ok).
-template <int NB, int ORD>
-__global__ __launch_bounds__(BLKSEG_THREADS) void k_blkseg_eval(const TChainArgs g, const BlkArgs bk, const BlksegParams sp) {
+template <int NB, int ORD, int WMAX>
+__global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, const BlkArgs bk, const BlksegParams sp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int E = NB * NB;
-  constexpr bool GREG = NB == 2;  // the lane's generator blocks in registers (blocks of 3 rows: from LDS)
+  // the lane's generator blocks in registers (blocks of 2 rows at <= 8 waves), else from LDS where used; blocks of 2
+  // rows keep Â for X = A_k and accumulate M in the contraction
+  constexpr bool GREG = NB == 2 && WMAX <= 8;
+  constexpr bool XA = NB == 2;
   constexpr int NV1 = NB == 2 ? 2 : 1;  // slices formed at once in phase 1
   const int N = g.N, m = g.m, nu = g.nu, Nt = g.Nt, nblk = bk.nblk, S = sp.S, L = sp.L;
   const int tid = threadIdx.x, nthr = blockDim.x, w = tid >> 6, l = tid & 63, W = nthr >> 6;
   const int b = blockIdx.x;
   const size_t Nm = (size_t)N * m;
+  BK_T(t0);
   double* const lds = reinterpret_cast<double*>(smem);
   double2* const gsh = reinterpret_cast<double2*>(lds);
   double* const rec = lds + blkseg_off_rec(NB, nblk);
@@ -329,6 +519,8 @@ __global__ __launch_bounds__(BLKSEG_THREADS) void k_blkseg_eval(const TChainArgs
     r[1] = make_double2(s0 * u1, s0 * u2);
   }
   __syncthreads();
+  BK_T(t1);
+  BK_ADD(0, t1 - t0);
 
   // ---- the lane's unit: segment s, block beta ----
   const int uw = l / nblk;
@@ -361,6 +553,9 @@ __global__ __launch_bounds__(BLKSEG_THREADS) void k_blkseg_eval(const TChainArgs
     return v;
   };
 
+  // SIMD partners (w, w + 4) alternate the issue priority (seg_turn); QOC_PROBE builds: g_seg_noturn turns it off
+  const int grp = __builtin_amdgcn_readfirstlane(w >> 2), ngrp = (W + 3) >> 2;
+  const bool turns = ngrp > 1 && SEG_TURNS;
   // ---- phase 1: the segment product P_s = U_{ke-1} .. U_{kb} ----
   double qr[E], qi[E];
 #pragma unroll
@@ -368,29 +563,82 @@ __global__ __launch_bounds__(BLKSEG_THREADS) void k_blkseg_eval(const TChainArgs
     qr[e] = e % (NB + 1) == 0 ? 1.0 : 0.0;
     qi[e] = 0.0;
   }
-  for (int jj = 0; jj < L; jj += NV1) {
-    const double* rk[NV1];
-    bool act[NV1];
+  // every segment but the last has L slices; below Lf (the last one's length) no lane of a segment is past its end,
+  // so those steps need no selects
+  const int Lf = Nt - (S - 1) * L;
+  // the fast path (blocks of 2 rows, no halvings): skew-Hermitian blocks in 4 reals, the closed-form exponential
+  const bool fast = NB == 2 && J == 0;
+  Sk2 gk[3];
+  if constexpr (NB == 2) {
 #pragma unroll
-    for (int v = 0; v < NV1; ++v) {
-      const int k = kb + jj + v;
-      act[v] = sact && jj + v < L && k < ke;
-      rk[v] = rec + 4 * (size_t)(act[v] ? k : 0);
+    for (int j = 0; j < 3; ++j) {
+      double2 e4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) e4[e] = gsh[(beta * 3 + j) * E + e];
+      gk[j] = sk2_of(e4);
     }
-    double ar[NV1][E], ai[NV1][E], ur[NV1][E], ui[NV1][E];
-    seg_form<NB, NV1>(gen_at(GREG ? beta : opaque(beta)), rk, s0, P, J, ar, ai, ur, ui);
+  }
+  auto p1_fast = [&](int jj, auto SEL_) {
+    constexpr bool SEL = decltype(SEL_)::value;
+    if constexpr (NB == 2) {
+      double ur[2][4], ui[2][4];
+      bool act[2];
 #pragma unroll
-    for (int v = 0; v < NV1; ++v) {
-      double tr[E], ti[E];
-      seg_mm<NB, false, false>(ur[v], ui[v], qr, qi, tr, ti);
+      for (int v = 0; v < 2; ++v) {
+        const int k = kb + jj + v;
+        act[v] = !SEL || (sact && jj + v < L && k < ke);
+        const double* r = rec + 4 * (size_t)(act[v] ? k : 0);
+        Sk2 ah;
+        sk2_form(gk, *reinterpret_cast<const double2*>(r), *reinterpret_cast<const double2*>(r + 2), ah, ur[v], ui[v]);
+      }
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        qr[e] = act[v] ? tr[e] : qr[e];
-        qi[e] = act[v] ? ti[e] : qi[e];
+      for (int v = 0; v < 2; ++v) {
+        double tr[4], ti[4];
+        seg_mm<2, false, false>(ur[v], ui[v], qr, qi, tr, ti);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          qr[e] = !SEL || act[v] ? tr[e] : qr[e];
+          qi[e] = !SEL || act[v] ? ti[e] : qi[e];
+        }
+      }
+    }
+  };
+  if (fast) {
+    for (int jj = 0; jj < L; jj += 2) {
+      if (turns) seg_turn(grp, ngrp, jj >> 1);
+      if (jj + 1 < Lf) p1_fast(jj, std::false_type());
+      else p1_fast(jj, std::true_type());
+    }
+  } else {
+    for (int jj = 0; jj < L; jj += NV1) {
+      if (turns) seg_turn(grp, ngrp, jj / NV1);
+      const double* rk[NV1];
+      bool act[NV1];
+#pragma unroll
+      for (int v = 0; v < NV1; ++v) {
+        const int k = kb + jj + v;
+        act[v] = sact && jj + v < L && k < ke;
+        rk[v] = rec + 4 * (size_t)(act[v] ? k : 0);
+      }
+      double ar[NV1][E], ai[NV1][E], ur[NV1][E], ui[NV1][E];
+      seg_form<NB, NV1>(gen_at(GREG ? beta : opaque(beta)), rk, s0, P, J, ar, ai, ur, ui);
+#pragma unroll
+      for (int v = 0; v < NV1; ++v) {
+        double tr[E], ti[E];
+        seg_mm<NB, false, false>(ur[v], ui[v], qr, qi, tr, ti);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          qr[e] = act[v] ? tr[e] : qr[e];
+          qi[e] = act[v] ? ti[e] : qi[e];
+        }
       }
     }
   }
 
+  if (turns) __builtin_amdgcn_s_setprio(0);
+  BK_T(t2);
+  BK_ADD(1, t2 - t1);
+  SEGW_SET(w, t2 - t0);
   // ---- phase 2: prefix products Q_s = P_s .. P_0 (Hillis-Steele over the segments) ----
   auto slot_at = [&](int ss, int e) -> double2& { return slot[((size_t)ss * E + e) * nblk + beta]; };
   if (sact)
@@ -498,52 +746,16 @@ __global__ __launch_bounds__(BLKSEG_THREADS) void k_blkseg_eval(const TChainArgs
     seg_mm<NB, false, true>(tr, ti, qr, qi, Gr, Gi);
   }
 
+  BK_T(t3);
+  BK_ADD(2, t3 - t2);
   // ---- phase 3: each segment backwards, the gradient of every slice ----
   const double mu1r = sp.mur[1], mu1i = sp.mui[1], mu2r = sp.mur[2], mu2i = sp.mui[2];
   double* const wr = wred + 128 * w;
   const int nred = sp.UPW * nu;  // reducing lanes: (segment of the wave, control)
   const int ro = l / max(nu, 1), rj = l - ro * max(nu, 1);
-  for (int jj = L - 1; jj >= 0; --jj) {
-    const int k = kb + jj;
-    const bool act = sact && k < ke;
-    const double* rk[1] = {rec + 4 * (size_t)(act ? k : 0)};
-    const auto gen = gen_at(GREG ? beta : opaque(beta));
-    double ar[1][E], ai[1][E], ur[1][E], ui[1][E];
-    seg_form<NB, 1>(gen, rk, s0, P, J, ar, ai, ur, ui);
-    // K_k = U_k^H G_{k+1}, G_k = K_k U_k
-    double Kr[E], Ki[E], tr[E], ti[E];
-    seg_mm<NB, true, false>(ur[0], ui[0], Gr, Gi, Kr, Ki);
-    seg_mm<NB, false, false>(Kr, Ki, ur[0], ui[0], tr, ti);
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      Gr[e] = act ? tr[e] : Gr[e];
-      Gi[e] = act ? ti[e] : Gi[e];
-    }
-    // X = A_k = 2^J Â + μ_k I, u_j = 2^J (2^-J u_j) exactly
-    const double2 su = *reinterpret_cast<const double2*>(rk[0] + 2);
-    const double u1 = ldexp(su.x, J), u2 = ldexp(su.y, J);
-    const double mkr = fma(u2, sp.mur[2], fma(u1, sp.mur[1], sp.mur[0]));
-    const double mki = fma(u2, sp.mui[2], fma(u1, sp.mui[1], sp.mui[0]));
-    double xr[E], xi[E];
-    if constexpr (GREG) {  // from the formation's Â
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        xr[e] = ldexp(ar[0][e], J) + (e % (NB + 1) == 0 ? mkr : 0.0);
-        xi[e] = ldexp(ai[0][e], J) + (e % (NB + 1) == 0 ? mki : 0.0);
-      }
-    } else {  // re-read (blocks of 3 rows: Â is not kept live across the two products)
-      const auto gen2 = gen_at(opaque(beta));
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const double2 g0 = gen2(0, e), g1 = gen2(1, e), g2 = gen2(2, e);
-        xr[e] = fma(u2, g2.x, fma(u1, g1.x, g0.x)) + (e % (NB + 1) == 0 ? mkr : 0.0);
-        xi[e] = fma(u2, g2.y, fma(u1, g1.y, g0.y)) + (e % (NB + 1) == 0 ? mki : 0.0);
-      }
-    }
-    double acc1, acc2;
-    seg_contract<NB, ORD>(gen, xr, xi, Kr, Ki, mu1r, mu1i, mu2r, mu2i, acc1, acc2);
-    // the slice's sum over its blocks: wave-private slot, fixed order
-    *reinterpret_cast<double2*>(wr + 2 * l) = make_double2(act ? acc1 : 0.0, act ? acc2 : 0.0);
+  // the slice's sum over its blocks: a wave-private slot, summed in a fixed order
+  auto reduce = [&](int jj, double acc1, double acc2) {
+    *reinterpret_cast<double2*>(wr + 2 * l) = make_double2(acc1, acc2);
     wave_lds_sync();
     if (l < nred) {
       const int ss = w * sp.UPW + ro, kk = ss * L + jj;
@@ -554,11 +766,97 @@ __global__ __launch_bounds__(BLKSEG_THREADS) void k_blkseg_eval(const TChainArgs
       }
     }
     wave_lds_sync();
+  };
+  auto p3_fast = [&](int jj, auto SEL_) {
+    constexpr bool SEL = decltype(SEL_)::value;
+    if constexpr (NB == 2) {
+      const int k = kb + jj;
+      const bool act = !SEL || (sact && k < ke);
+      const double* r = rec + 4 * (size_t)(act ? k : 0);
+      const double2 u = *reinterpret_cast<const double2*>(r + 2);
+      Sk2 ah;
+      double ur[4], ui[4];
+      sk2_form(gk, *reinterpret_cast<const double2*>(r), u, ah, ur, ui);
+      // K_k = U_k^H G_{k+1}, G_k = K_k U_k
+      double Kr[4], Ki[4], tr[4], ti[4];
+      seg_mm<2, true, false>(ur, ui, Gr, Gi, Kr, Ki);
+      seg_mm<2, false, false>(Kr, Ki, ur, ui, tr, ti);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        Gr[e] = !SEL || act ? tr[e] : Gr[e];
+        Gi[e] = !SEL || act ? ti[e] : Gi[e];
+      }
+      // X = A_k = Â + μ_k I (skew: μ_k = i (Im μ_0 + u_1 Im μ_1 + u_2 Im μ_2))
+      const double mki = fma(u.y, mu2i, fma(u.x, mu1i, sp.mui[0]));
+      const Sk2 x{ah.d0 + mki, ah.d1 + mki, ah.r, ah.q};
+      const Sk2 e1{gk[1].d0 + mu1i, gk[1].d1 + mu1i, gk[1].r, gk[1].q};
+      const Sk2 e2{gk[2].d0 + mu2i, gk[2].d1 + mu2i, gk[2].r, gk[2].q};
+      double acc1, acc2;
+      sk2_contract<ORD>(x, e1, e2, Kr, Ki, acc1, acc2);
+      reduce(jj, !SEL || act ? acc1 : 0.0, !SEL || act ? acc2 : 0.0);
+    }
+  };
+  if (fast) {
+    for (int jj = L - 1; jj >= 0; --jj) {
+      if (turns) seg_turn(grp, ngrp, jj);
+      if (jj < Lf) p3_fast(jj, std::false_type());
+      else p3_fast(jj, std::true_type());
+    }
+  } else {
+    for (int jj = L - 1; jj >= 0; --jj) {
+      if (turns) seg_turn(grp, ngrp, jj);
+      const int k = kb + jj;
+      const bool act = sact && k < ke;
+      const double* rk[1] = {rec + 4 * (size_t)(act ? k : 0)};
+      const auto gen = gen_at(GREG ? beta : opaque(beta));
+      double ar[1][E], ai[1][E], ur[1][E], ui[1][E];
+      seg_form<NB, 1>(gen, rk, s0, P, J, ar, ai, ur, ui);
+      // K_k = U_k^H G_{k+1}, G_k = K_k U_k
+      double Kr[E], Ki[E], tr[E], ti[E];
+      seg_mm<NB, true, false>(ur[0], ui[0], Gr, Gi, Kr, Ki);
+      seg_mm<NB, false, false>(Kr, Ki, ur[0], ui[0], tr, ti);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        Gr[e] = act ? tr[e] : Gr[e];
+        Gi[e] = act ? ti[e] : Gi[e];
+      }
+      // X = A_k = 2^J Â + μ_k I, u_j = 2^J (2^-J u_j) exactly
+      const double2 su = *reinterpret_cast<const double2*>(rk[0] + 2);
+      const double u1 = ldexp(su.x, J), u2 = ldexp(su.y, J);
+      const double mkr = fma(u2, sp.mur[2], fma(u1, sp.mur[1], sp.mur[0]));
+      const double mki = fma(u2, sp.mui[2], fma(u1, sp.mui[1], sp.mui[0]));
+      double xr[E], xi[E];
+      if constexpr (XA) {  // from the formation's Â
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          xr[e] = (J ? ldexp(ar[0][e], J) : ar[0][e]) + (e % (NB + 1) == 0 ? mkr : 0.0);
+          xi[e] = (J ? ldexp(ai[0][e], J) : ai[0][e]) + (e % (NB + 1) == 0 ? mki : 0.0);
+        }
+      } else {  // re-read (blocks of 3 rows: Â is not kept live across the two products)
+        const auto gen2 = gen_at(opaque(beta));
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const double2 g0 = gen2(0, e), g1 = gen2(1, e), g2 = gen2(2, e);
+          xr[e] = fma(u2, g2.x, fma(u1, g1.x, g0.x)) + (e % (NB + 1) == 0 ? mkr : 0.0);
+          xi[e] = fma(u2, g2.y, fma(u1, g1.y, g0.y)) + (e % (NB + 1) == 0 ? mki : 0.0);
+        }
+      }
+      double acc1, acc2;
+      seg_contract<NB, ORD, XA>(gen, xr, xi, Kr, Ki, mu1r, mu1i, mu2r, mu2i, acc1, acc2);
+      reduce(jj, act ? acc1 : 0.0, act ? acc2 : 0.0);
+    }
   }
+  if (turns) __builtin_amdgcn_s_setprio(0);
+  BK_T(t4);
+  BK_ADD(3, t4 - t3);
+  SEGW_SET(16 + w, t4 - t0);
   __syncthreads();
   double* const og = sp.dJdu + (size_t)b * Nt * nu;
   for (int i = tid; i < Nt * nu; i += nthr) og[i] = dJ[i];
   if (sp.terms && tid == 0) atomicAdd(sp.terms + b % TERM_SLOTS, (unsigned long long)Nt * ((unsigned long long)P << J));
+  BK_T(t5);
+  BK_ADD(4, t5 - t4);
+  BK_ADD(5, t5 - t0);
 }
 
 }  // namespace qoc

@@ -786,9 +786,9 @@ int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d
   const int mk = mark_begin(c, 2);
   const hipError_t e = blkseg_dispatch(c->blk_nb, order, [&](auto NB_, auto ORD_) {
     constexpr int NB = decltype(NB_)::value, ORD = decltype(ORD_)::value;
-    const hipError_t q = blk_lds_attr(k_blkseg_eval<NB, ORD>, s.lds);
+    const hipError_t q = blk_lds_attr(k_blkseg_eval<NB, ORD, 8>, s.lds);
     if (q != hipSuccess) return q;
-    hipLaunchKernelGGL((k_blkseg_eval<NB, ORD>), dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, sp);
+    hipLaunchKernelGGL((k_blkseg_eval<NB, ORD, 8>), dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, sp);
     return hipGetLastError();
   });
   mark_end(c, mk);
