@@ -94,6 +94,21 @@ def block_sizes(prob):
     return np.bincount(lab)
 
 
+def blkseg_unit_flops(nb, order, P=None):
+    """Executed fp64 flops of the segmented block eval (csrc/qoc_blkseg.hpp) per (slice, block) unit, counted from
+    the kernel's code (FMA = 2, add / mul = 1), phase 1 and phase 3 (the block exponential is formed in both: it is
+    recomputed, not stored).  Blocks of 2 rows (the skew-Hermitian fast path): closed-form exponential (Â 16, the
+    cos / sinc series of degree 19 in omega^2 and t^2 80, the rest 41: 137), 2x2 complex products 64 each, the
+    contraction 16 + 104 (order - 1) on skew X; blocks of 3 rows: the Taylor polynomial of degree P in the
+    Cayley-Hamilton basis (478 + 26 (P + 1)), 3x3 products 216 each, the contraction 86 + 518 (order - 1)."""
+    if nb == 2:
+        form, prod, contr = 137.0, 64.0, 16.0 + 104.0 * (order - 1)
+        return form + prod, form + 2 * prod + 6.0 + contr + 2.0
+    form = 478.0 + 26.0 * ((P or 8) + 1)
+    prod, contr = 216.0, 86.0 + 518.0 * (order - 1)
+    return form + prod, form + 2 * prod + 76.0 + contr + 2.0
+
+
 def chain_bytes(N, m, Nt, B, esz):
     """Compulsory HBM bytes of one chain launch: read all U_k once, write the N x m state per slice."""
     return B * Nt * N * N * esz + B * (Nt + 1) * N * m * esz
@@ -399,15 +414,46 @@ def main():
         except Exception:
             traffic_all = {}
     taylor = info1.get("chain") == "taylor" and not large
+    seg = info1.get("backward") == "segmented"  # the one-launch segmented block eval (k_blkseg_eval)
     dual = info1.get("concurrent_launch") == "dual"
     fused = info1.get("concurrent_launch") == "fused"  # block propagators: forward, then the backward with the gradient
     bsz = block_sizes(prob) if taylor and info1.get("chain_kernel") in ("blocks", "blocks_mfma", "blocks_prop") else None
     bprop = info1.get("chain_kernel") == "blocks_prop"
     # blocks of <= 4 rows (VALU lanes or packed MFMA block waves) with the block gradient; 5..16 rows: MFMA block
     # waves with the dense gradient
-    blocks = bsz is not None and bsz.max() <= 4
+    blocks = bsz is not None and bsz.max() <= 4 and not seg
     rot_blocks = bsz is not None and bsz.max() > 4
-    if blocks:
+    if seg:
+        # one launch per eval: segment products, prefix scan, every segment backwards with the gradient (phase slot
+        # k_chain_bwd); HBM traffic is u in (and its two copies out), J / λ_N coefficients and dJdu out -- x_k, λ_k and
+        # U_k stay on chip, so the kernel is bound by its fp64 VALU work (executed flops, blkseg_unit_flops)
+        bsz_s = block_sizes(prob)
+        nbk = int(bsz_s.max())
+        nblk = len(bsz_s)
+        p_avg = terms / K / max(B * Nt, 1)  # Taylor degree (blocks of 3 rows; the kernel counts Nt P 2^J per seed)
+        f1, f3 = blkseg_unit_flops(nbk, args.order, p_avg)
+        units = B * Nt * nblk
+        flops = units * (f1 + f3)
+        hbm = B * Nt * nu * 8 * 4 + B * (8 + 2 * 2 * m * 16)
+        t = per_step["k_chain_bwd"] / 1e3
+        ach = flops / 1e12 / t if t > 0 else 0.0
+        kern = {"k_blkseg_eval": {
+            "ms_per_launch": per_launch["k_chain_bwd"], "launches_per_step": lps["k_chain_bwd"], "bound": "valu",
+            "achieved": ach, "unit": "TFLOP/s", "peak": peak, "frac": ach / peak,
+            "executed_gflop_per_launch": flops / 1e9, "flops_per_unit": {"phase1": f1, "phase3": f3},
+            "units_per_launch": units, "hbm_bytes_per_launch": hbm,
+            "hbm_gbs": hbm / 1e9 / t if t > 0 else 0.0, "taylor_degree": p_avg if nbk == 3 else None}}
+        for k in ("k_expm", "k_chain_fwd", "k_grad"):
+            kern[k] = {"ms_per_launch": per_launch[k], "launches_per_step": lps[k]}
+        roof = {"kernel": "k_blkseg_eval", "bound": "valu", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
+                "frac": ach / peak, "traffic": traffic_all.get("k_blkseg_eval"), "traffic_source": traffic_src,
+                "ms_per_launch": per_launch["k_chain_bwd"], "launches_per_step": lps["k_chain_bwd"],
+                "blocks": [int(x) for x in bsz_s],
+                "note": ("segmented block eval, one launch per eval (csrc/qoc_blkseg.hpp): achieved = executed fp64 "
+                         "flops per launch (bench.py blkseg_unit_flops x B Nt nblk) / launch time, against the fp64 "
+                         "peak (vector = dense MFMA, 78.6 TF/s); HBM traffic is u, J and dJdu only "
+                         "(hbm_bytes_per_launch), so the bound is the VALU issue, not bandwidth")}
+    elif blocks:
         # block chains (csrc/qoc_blk.hpp, qoc_blku.hpp); the launch's algorithmic bytes are the states it writes (x_k,
         # and μ_k in the dual launch) plus what it reads per slice: the step records of k_tchain_prep (32 B record +
         # P+1 Chebyshev coefficients + u_k) for the polynomial-in-the-chain kernels, u_k alone for the block
@@ -499,14 +545,19 @@ def main():
             "k_chain_bwd": ("mfma", f_chain / 1e12, "TFLOP/s", peak),
             "k_grad": ("mfma", f_grad / 1e12, "TFLOP/s", peak),
         }
-    kern = {}
+    if seg:
+        models = {}
+    else:
+        kern = {}
     for k, (bound, work, unit, pk) in models.items():
         t = per_step[k] / 1e3
         ach = work / t if t > 0 else 0.0
         kern[k] = {"ms_per_launch": per_launch[k], "launches_per_step": lps[k], "bound": bound, "achieved": ach,
                    "unit": unit, "peak": pk, "frac": ach / pk}
     names = {"k_expm": "k_expm_rr", "k_chain_fwd": "k_chain_fwd", "k_chain_bwd": "k_chain_bwd", "k_grad": "k_grad_rr"}
-    if blocks:
+    if seg:
+        pass  # kern and roof set above
+    elif blocks:
         kb = {"blocks_mfma": "k_blkrot", "blocks_prop": "k_blku"}.get(info1.get("chain_kernel"), "k_blk")
         names = {"k_expm": "k_blku_rec" if bprop else "k_tchain_prep", "k_chain_fwd": kb + ("_dual" if dual else "_fwd"),
                  "k_chain_bwd": kb + ("_bwdg" if fused else "_bwd"), "k_grad": "k_blku_grad" if bprop else "k_blk_grad"}

@@ -204,8 +204,10 @@ def test_device_pointer_eval_matches_host_path(built_lib):
     gd = torch.empty(4, 30, 2, dtype=torch.float64, device="cuda")
     e.eval_device(ud.data_ptr(), 3, Jd.data_ptr(), gd.data_ptr())
     e.synchronize()
-    assert np.array_equal(Jd.cpu().numpy(), Jh)
-    # the device eval runs the μ recurrence beside the forward chain (λ = coef ⊙ μ): the same gradient to rounding
+    # the device eval runs the segmented block eval (csrc/qoc_blkseg.hpp: segment products and a prefix scan, the
+    # closed-form block exponential) where the host path runs the sequential chains: the same J and gradient to
+    # rounding, not bit for bit
+    assert np.abs(Jd.cpu().numpy() - Jh).max() <= 1e-13
     gdh = np.transpose(gd.cpu().numpy(), (0, 2, 1))
     for b in range(4):
         assert np.linalg.norm(gdh[b] - gh[b]) / np.linalg.norm(gh[b]) <= 1e-12

@@ -54,8 +54,8 @@ def test_eval_spline_matches_oracle(built_lib):
 
 def test_f_alone_then_f_grad_like_the_reference_callbacks(built_lib):
     """Ipopt's f only propagates (examples/ipopt_callbacks_exp.jl:11-19) and f_grad runs the sensitivity for the
-    coefficients f last saw (:21-31): qoc_propagate_spline + qoc_sensitivity_spline give the fused eval's J (bitwise)
-    and dJdc; the sensitivity refuses other coefficients (the reference's stale-u error)."""
+    coefficients f last saw (:21-31): qoc_propagate_spline + qoc_sensitivity_spline give the fused eval's J and dJdc
+    (to rounding); the sensitivity refuses other coefficients (the reference's stale-u error)."""
     from qoc_amd import GrapeEngine, StaleCacheError
     prob, Bs = _zz()
     ns = Bs.shape[1]
@@ -66,7 +66,9 @@ def test_f_alone_then_f_grad_like_the_reference_callbacks(built_lib):
     e.set_spline_basis(Bs)
     J0, g0 = e.eval_spline(c)
     J1 = e.propagate_spline(c)
-    assert np.array_equal(J0, J1)
+    # the fused eval (the segmented block eval: segment products, prefix scan) and the sequential forward chain of
+    # propagate: the same J to rounding
+    assert np.abs(J0 - J1).max() <= 1e-13
     g1 = e.sensitivity_spline(c)
     # the fused eval runs the co-state recurrence beside the forward chain (λ = coef ⊙ μ), the split calls after it:
     # the same gradient to rounding
