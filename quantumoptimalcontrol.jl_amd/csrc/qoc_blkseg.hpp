@@ -40,6 +40,11 @@ struct BlksegParams {
   cx<double>* coef2;           // a second copy of the λ_N coefficients (the lazy co-states), or nullptr
   double* dJdu;                // B x Nt x nu
   unsigned long long* terms;   // Σ P 2^J per pass over the slices (executed Taylor terms), nullptr: not counted
+  // the best (J, global seed) of this launch for qoc_allgather_best_dev (the last workgroup to publish its J reduces
+  // them; done counts the published ones and is reset by that workgroup), or nullptr
+  unsigned int* done;
+  double* best;
+  long long seed_offset;
 };
 
 // LDS, in doubles: shifted generator blocks [nblk][3][E] complex | step records [Nt][4] | segment products [S][E][nblk]
@@ -746,6 +751,49 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
     seg_mm<NB, false, true>(tr, ti, qr, qi, Gr, Gi);
   }
 
+  if (w == 0 && sp.done) {
+    // J is published after the last barrier before phase 3, so that only wave 0 (one of the fast waves, seg_turn)
+    // waits for the fences; the last workgroup to publish finds the best (J, seed) of the launch (k_argmin_seed's
+    // order: NaN never wins, ties go to the lower seed).  The hand-off follows the agent-scope release / acquire
+    // recipe (MI355X_MICROARCH.md, inter-workgroup visibility): store, vmcnt(0), release fence, vmcnt(0), counter
+    // add; the last adder acquires and then reads every J with plain loads.
+    unsigned int prev = 0;
+    if (l == 0) {
+      {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        prev = atomicAdd(sp.done, 1u);
+      }
+    }
+    prev = __shfl(prev, 0);
+    if (sp.done && prev == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      double bv = __builtin_inf();
+      long long bi = -1;
+      for (int e = l; e < (int)gridDim.x; e += 64) {
+        const double v = g.J[e];
+        if (v < bv || (v == bv && e < bi)) {
+          bv = v;
+          bi = e;
+        }
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(bv, off);
+        const long long oi = __shfl_xor(bi, off);
+        if (ov < bv || (ov == bv && oi >= 0 && (bi < 0 || oi < bi))) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      if (l == 0) {
+        sp.best[0] = bv;
+        sp.best[1] = bi >= 0 ? (double)(bi + sp.seed_offset) : -1.0;
+        *sp.done = 0;  // ready for the next launch (the kernel boundary orders it)
+      }
+    }
+  }
   BK_T(t3);
   BK_ADD(2, t3 - t2);
   // ---- phase 3: each segment backwards, the gradient of every slice ----

@@ -52,7 +52,8 @@ static __global__ void k_argmin_seed(const double* __restrict__ J, int B, long l
 }
 
 // Reduce the gathered (J, seed) pairs of `world` ranks to the best one (lowest seed on ties).
-static __global__ void k_pick_best(const double* __restrict__ g, int world, double* __restrict__ out) {
+static __global__ void k_pick_best(const double* __restrict__ g, int world, double* __restrict__ out,
+                                   double* __restrict__ out2) {
   if (threadIdx.x != 0) return;
   double best = g[0], seed = g[1];
   for (int r = 1; r < world; ++r) {
@@ -64,6 +65,10 @@ static __global__ void k_pick_best(const double* __restrict__ g, int world, doub
   }
   out[0] = best;
   out[1] = seed;
+  if (out2) {
+    out2[0] = best;
+    out2[1] = seed;
+  }
 }
 
 // The RCCL entry points the epilogue uses, resolved from librccl at run time.

@@ -323,6 +323,7 @@ RcclApi& rccl() {
 
 int forward(qoc_ctx* c) {
   c->X_lazy = false;  // every forward path writes x_k
+  c->best_ready = false;
   if (blk_active(c)) return blk_forward(c);
   if (c->big) return c->prec == QOC_FP64 ? big_forward<double>(c) : big_forward<float>(c);
   return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
@@ -502,6 +503,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->comm && rccl().commDestroy) rccl().commDestroy(c->comm);
   if (c->d_best) hipFree(c->d_best);
+  if (c->d_done) hipFree(c->d_done);
   if (c->d_tcoef) hipFree(c->d_tcoef);
   if (c->d_coef_mu) hipFree(c->d_coef_mu);
   if (c->d_brow) hipFree(c->d_brow);
@@ -923,7 +925,10 @@ int qoc_eval_dev(qoc_ctx* c, const double* d_u, int order, double* d_J, double* 
     c->h_coef.clear();
     return QOC_OK;
   }
-  if (c) c->X_lazy = false;  // the other eval paths write x_k
+  if (c) {
+    c->X_lazy = false;  // the other eval paths write x_k
+    c->best_ready = false;
+  }
   if (c && c->have_gen && (blk_concurrent_ok(c, order) || tchain_concurrent_ok(c, order))) {
     // forward chain and the μ recurrence side by side (tchain_eval_concurrent)
     int r = check_ready(c);
@@ -1270,6 +1275,7 @@ int qoc_propagate_envelope(qoc_ctx* c, int kind, const double* params, int np, d
   HIPCHK(c, hipMalloc((void**)&dP, (size_t)c->B * np * sizeof(double)));
   hipError_t e = hipMemcpy(dP, params, (size_t)c->B * np * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = launch_envelope(c, kind, dP, np, dt, nsteps);
+  c->best_ready = false;  // J is rewritten below
   if (e == hipSuccess && c->cost_kind != QOC_COST_EXTERNAL) e = launch_terminal_cost(c);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess && J_out && c->cost_kind != QOC_COST_EXTERNAL)
@@ -1350,6 +1356,7 @@ int qoc_comm_init(qoc_ctx* c, int world, int rank, const void* id, long long see
   }
   if (c->d_best) HIPCHK(c, hipFree(c->d_best));
   c->d_best = nullptr;
+  c->best_ready = false;
   c->world = 1;
   c->rank = 0;
   c->seed_offset = 0;
@@ -1393,18 +1400,21 @@ int qoc_allgather_best_dev(qoc_ctx* c, double* d_out) {
     c->rank = 0;
   }
   double* res = c->d_best + 2 + 2 * c->world;
-  hipLaunchKernelGGL(k_argmin_seed, dim3(1), dim3(256), 0, c->stream, (const double*)c->d_J, c->B, c->seed_offset,
-                     c->d_best);
-  HIPCHK(c, hipGetLastError());
-  if (c->comm && rccl().ok) {
-    const ncclResult_t e = rccl().allGather(c->d_best, c->d_best + 2, 2, ncclFloat64, c->comm, c->stream);
-    if (e != ncclSuccess) return fail(c, QOC_ERR_HIP, "ncclAllGather: %s", rccl().getErrorString(e));
-    hipLaunchKernelGGL(k_pick_best, dim3(1), dim3(64), 0, c->stream, (const double*)(c->d_best + 2), c->world, res);
-  } else {
-    HIPCHK(c, hipMemcpyAsync(res, c->d_best, 2 * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  double* slot = c->d_best + 2 + 2 * c->rank;  // this rank's pair in the gathered array (in-place all-gather)
+  // the segmented eval already reduced its J in its last workgroup (best_ready); otherwise k_argmin_seed
+  if (!c->best_ready) {
+    hipLaunchKernelGGL(k_argmin_seed, dim3(1), dim3(256), 0, c->stream, (const double*)c->d_J, c->B, c->seed_offset,
+                       slot);
+    HIPCHK(c, hipGetLastError());
   }
+  if (c->comm && rccl().ok) {
+    const ncclResult_t e = rccl().allGather(slot, c->d_best + 2, 2, ncclFloat64, c->comm, c->stream);
+    if (e != ncclSuccess) return fail(c, QOC_ERR_HIP, "ncclAllGather: %s", rccl().getErrorString(e));
+  }
+  // the best over the gathered pairs, into the context's result and the caller's buffer
+  hipLaunchKernelGGL(k_pick_best, dim3(1), dim3(64), 0, c->stream, (const double*)(c->d_best + 2),
+                     c->comm && rccl().ok ? c->world : 1, res, d_out);
   HIPCHK(c, hipGetLastError());
-  if (d_out) HIPCHK(c, hipMemcpyAsync(d_out, res, 2 * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
   return QOC_OK;
 }
 

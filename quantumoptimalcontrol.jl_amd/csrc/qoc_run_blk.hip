@@ -783,6 +783,19 @@ int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d
   sp.coef2 = c->d_coef_lam;
   sp.dJdu = d_dJdu;
   sp.terms = c->d_terms;
+  // the best (J, seed) for qoc_allgather_best_dev, found by the launch's last workgroup
+  if (!c->d_best) {  // no communicator yet: this context alone (the epilogue's own layout)
+    HIPCHK(c, hipMalloc((void**)&c->d_best, 6 * sizeof(double)));
+    c->world = 1;
+    c->rank = 0;
+  }
+  if (!c->d_done) {
+    HIPCHK(c, hipMalloc((void**)&c->d_done, sizeof(unsigned int)));
+    HIPCHK(c, hipMemsetAsync(c->d_done, 0, sizeof(unsigned int), c->stream));
+  }
+  sp.done = c->d_done;
+  sp.best = c->d_best + 2 + 2 * c->rank;
+  sp.seed_offset = c->seed_offset;
   const int mk = mark_begin(c, 2);
   const hipError_t e = blkseg_dispatch(c->blk_nb, order, [&](auto NB_, auto ORD_) {
     constexpr int NB = decltype(NB_)::value, ORD = decltype(ORD_)::value;
@@ -797,6 +810,7 @@ int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d
   c->L_is_mu = false;
   c->X_lazy = true;
   c->L_lazy = true;
+  c->best_ready = true;
   c->last_eval_mode = 6;
   return QOC_OK;
 }

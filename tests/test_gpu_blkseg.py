@@ -269,3 +269,25 @@ def test_segmented_full_size(built_lib, monkeypatch, name, B):
     Jc, gc = cpuref.grape_eval_batch(prob, u[idx], order=3, mode=0)
     for i, b in enumerate(idx):
         _assert_seed(J[b], g[b], Jc[i], gc[i], (name, b))
+
+
+def test_segmented_eval_best_pair_for_the_all_gather(built_lib, monkeypatch):
+    """The launch's last workgroup reduces the batch's J to the best (J, global seed) for qoc_allgather_best (no
+    k_argmin_seed launch): more seeds than CUs (several workgroups per CU), with and without a seed offset, and a later
+    propagate (whose J the epilogue reduces again)."""
+    from qoc_amd import systems
+    prob = systems.cavity_problem(N_cavity=10, Nt=24)
+    B = 300
+    u = systems.cavity_controls(B, prob.Nt, seed=91) * 6.0  # spread the fidelities
+    e = _engine(prob, B, monkeypatch)
+    J, _ = _eval_dev(e, u)
+    assert e.info()["backward"] == "segmented"
+    assert e.allgather_best() == (J.min(), int(np.argmin(J)))
+    e.comm_init(1, 0, None, 1000)  # no communicator, seed offset 1000
+    J, _ = _eval_dev(e, u[::-1].copy())
+    assert e.allgather_best() == (J.min(), 1000 + int(np.argmin(J)))
+    J2 = e.propagate(u * 0.5)
+    assert e.allgather_best() == (J2.min(), 1000 + int(np.argmin(J2)))
+    J, _ = _eval_dev(e, u)
+    assert e.allgather_best() == (J.min(), 1000 + int(np.argmin(J)))
+    e.close()
