@@ -8,7 +8,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "libqoc_cpuref.so")
+# QOC_CPUREF_LIB: another build of cpu_ref.c (the sanitizer build of `make -C oracle asan`, tools/asan_oracle.sh)
+LIB = os.environ.get("QOC_CPUREF_LIB") or os.path.join(HERE, "build", "libqoc_cpuref.so")
 _dp = C.POINTER(C.c_double)
 _lib = None
 

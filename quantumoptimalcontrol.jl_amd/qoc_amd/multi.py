@@ -74,7 +74,23 @@ def init_engine_comm(engine, seed_offset: int) -> str:
     box = [own_id if rank == 0 else None]
     if world > 1:
         dist.broadcast_object_list(box, src=0)
-    engine.comm_init(world, rank, box[0], seed_offset)  # collective; raises on failure
-    if engine.comm_ranks() != world:
-        raise _lib.QOCError(_lib.QOC_ERR_STATE, f"RCCL communicator has {engine.comm_ranks()} ranks, expected {world}")
+    err = None
+    try:
+        engine.comm_init(world, rank, box[0], seed_offset)  # collective
+        if engine.comm_ranks() != world:
+            err = f"RCCL communicator has {engine.comm_ranks()} ranks, expected {world}"
+    except _lib.QOCError as ex:
+        err = str(ex)
+    if world > 1:
+        # a join that failed on one rank (after the collective part, or with the others already through it) becomes
+        # an error on every rank instead of a rank that later waits alone in an all-gather
+        import torch
+        flag = torch.tensor([0 if err else 1], dtype=torch.int32)
+        if dist.get_backend() == "nccl":
+            flag = flag.cuda()
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not bool(flag.item()) and err is None:
+            err = "RCCL communicator: the join failed on another rank"
+    if err:
+        raise _lib.QOCError(_lib.QOC_ERR_STATE, err)
     return "rccl-libqoc"

@@ -341,3 +341,42 @@ def test_blocks_mfma_random_permuted_blocks(built_lib, monkeypatch, NB, nblk, nu
         for o, g in gs.items():
             J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=o, penalty=pen)
             _assert_seed(J[b], g[b], J0, g0, ("penalty", o, b))
+
+
+def test_fused_backward_blocks_of_4_rows_two_chain_waves(built_lib, monkeypatch):
+    """Blocks of 4 rows with nblk m = 20 (two chain waves inside the 4-wave launch bound of blocks of 4 rows): the
+    fused backward keeps a worker wave (one staging wave copies the stored propagators as well), so dJdu is the
+    contraction's, not whatever the buffer held."""
+    prob, u = _block_problem(NB=4, nblk=5, nu=2, m=4, Nt=40, seed=11)
+    e = _engine(prob, 2, "prop", monkeypatch)
+    J, g = _eval(e, u, True)
+    assert e.info()["backward"] == "fused", e.info()
+    e.close()
+    for b in range(2):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, b)
+
+
+def test_new_block_layout_reallocates_stored_propagators(built_lib, monkeypatch):
+    """qoc_set_generators with a block layout whose propagators need more room (blocks of 2 rows, then of 4 rows at
+    the same N = 11): the fused eval's stored-propagator buffer grows with it; co-states that the fused eval left to be
+    rebuilt on demand come from the system they were computed for, also after the generators changed."""
+    p2, u2 = _block_problem(NB=2, nblk=6, nu=2, m=2, Nt=30, seed=12)
+    p4, u4 = _block_problem(NB=4, nblk=3, nu=2, m=2, Nt=30, seed=13)
+    assert p2.N == p4.N
+    e = _engine(p2, 2, "prop", monkeypatch)
+    J, g = _eval(e, u2, True)
+    assert e.info()["backward"] == "fused"
+    _, _, c0 = O.grape_eval(p2.A0, p2.A, u2[1], p2.x0, p2.x_target, p2.n, order=3)
+    e.set_generators(p4.A0, p4.A)
+    lam = e.costate(7, seed=1)  # the first system's co-state (rebuilt before the generators changed)
+    lsc = max(np.abs(x).max() for x in c0.lam)
+    assert np.abs(lam - c0.lam[7]).max() <= 1e-12 * lsc
+    e.set_x0(p4.x0)
+    e.set_cost_trace(p4.x_target, p4.n)
+    J, g = _eval(e, u4, True)
+    assert e.info()["backward"] == "fused"
+    e.close()
+    for b in range(2):
+        J0, g0, _ = O.grape_eval(p4.A0, p4.A, u4[b], p4.x0, p4.x_target, p4.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, b)
