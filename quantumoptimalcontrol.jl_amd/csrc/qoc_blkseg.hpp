@@ -712,6 +712,51 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
     g.J[b] = red[16];
     if (sp.J2) sp.J2[b] = red[16];
   }
+  // J is published after the cost: before the barrier that precedes G_0 when no waves share a SIMD within the
+  // workgroup (early: all waves wait for the fences together), else after the last barrier before phase 3, so that
+  // only wave 0 (one of the fast waves, seg_turn) waits for them.  The last workgroup to publish finds the best
+  // (J, seed) of the launch (k_argmin_seed's order: NaN never wins, ties go to the lower seed).  The hand-off follows
+  // the agent-scope release / acquire recipe (MI355X_MICROARCH.md, inter-workgroup visibility): store, vmcnt(0),
+  // release fence, vmcnt(0), counter add; the last adder acquires and then reads every J with plain loads.
+  const bool early = W <= 4;
+  auto publish = [&]() {
+    if (w != 0 || !sp.done) return;
+    unsigned int prev = 0;
+    if (l == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      prev = atomicAdd(sp.done, 1u);
+    }
+    prev = __shfl(prev, 0);
+    if (prev == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      double bv = __builtin_inf();
+      long long bi = -1;
+      for (int e = l; e < (int)gridDim.x; e += 64) {
+        const double v = g.J[e];
+        if (v < bv || (v == bv && e < bi)) {
+          bv = v;
+          bi = e;
+        }
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(bv, off);
+        const long long oi = __shfl_xor(bi, off);
+        if (ov < bv || (ov == bv && oi >= 0 && (bi < 0 || oi < bi))) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      if (l == 0) {
+        sp.best[0] = bv;
+        sp.best[1] = bi >= 0 ? (double)(bi + sp.seed_offset) : -1.0;
+        *sp.done = 0;  // ready for the next launch (the kernel boundary orders it)
+      }
+    }
+  };
+  if (early) publish();
   // G_N = Σ_c x_N λ_N^H on each block, G_0 = Q_{S-1}^H G_N Q_{S-1}
   if (last) {
     const cx<double>* Xt = (const cx<double>*)g.Xt;
@@ -751,49 +796,7 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
     seg_mm<NB, false, true>(tr, ti, qr, qi, Gr, Gi);
   }
 
-  if (w == 0 && sp.done) {
-    // J is published after the last barrier before phase 3, so that only wave 0 (one of the fast waves, seg_turn)
-    // waits for the fences; the last workgroup to publish finds the best (J, seed) of the launch (k_argmin_seed's
-    // order: NaN never wins, ties go to the lower seed).  The hand-off follows the agent-scope release / acquire
-    // recipe (MI355X_MICROARCH.md, inter-workgroup visibility): store, vmcnt(0), release fence, vmcnt(0), counter
-    // add; the last adder acquires and then reads every J with plain loads.
-    unsigned int prev = 0;
-    if (l == 0) {
-      {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        prev = atomicAdd(sp.done, 1u);
-      }
-    }
-    prev = __shfl(prev, 0);
-    if (sp.done && prev == gridDim.x - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      double bv = __builtin_inf();
-      long long bi = -1;
-      for (int e = l; e < (int)gridDim.x; e += 64) {
-        const double v = g.J[e];
-        if (v < bv || (v == bv && e < bi)) {
-          bv = v;
-          bi = e;
-        }
-      }
-      for (int off = 32; off > 0; off >>= 1) {
-        const double ov = __shfl_xor(bv, off);
-        const long long oi = __shfl_xor(bi, off);
-        if (ov < bv || (ov == bv && oi >= 0 && (bi < 0 || oi < bi))) {
-          bv = ov;
-          bi = oi;
-        }
-      }
-      if (l == 0) {
-        sp.best[0] = bv;
-        sp.best[1] = bi >= 0 ? (double)(bi + sp.seed_offset) : -1.0;
-        *sp.done = 0;  // ready for the next launch (the kernel boundary orders it)
-      }
-    }
-  }
+  if (!early) publish();
   BK_T(t3);
   BK_ADD(2, t3 - t2);
   // ---- phase 3: each segment backwards, the gradient of every slice ----
