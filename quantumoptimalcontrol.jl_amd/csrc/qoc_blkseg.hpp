@@ -33,6 +33,7 @@ struct BlksegParams {
   int S;                       // segments per seed
   int L;                       // slices per segment (S L >= Nt; the last segment may be shorter)
   int UPW;                     // segments per wave (64 / nblk)
+  int RB;                      // slice-steps per block-sum reduction (blkseg_rb)
   const double* u;             // B x Nt x nu controls (the caller's buffer)
   double* u_copy;              // copies of u written by the launch (the stale check, the lazy rebuilds), or nullptr
   double* u_copy2;
@@ -49,7 +50,7 @@ struct BlksegParams {
 
 // LDS, in doubles: shifted generator blocks [nblk][3][E] complex | step records [Nt][4] | segment products [S][E][nblk]
 // complex | G_0 [E][nblk] complex | x_0 then x_N (N m complex) | λ_N coefficients (2 m complex) | scratch (24) |
-// per-wave partial sums [W][128] | dJdu [Nt][nu]
+// per-wave partial sums [W][RB][64][2] | dJdu [Nt][nu]
 __host__ __device__ inline size_t blkseg_off_rec(int NB, int nblk) { return (size_t)6 * NB * NB * nblk; }
 __host__ __device__ inline size_t blkseg_off_slot(int NB, int nblk, int Nt) { return blkseg_off_rec(NB, nblk) + 4 * (size_t)Nt; }
 __host__ __device__ inline size_t blkseg_off_g0(int NB, int nblk, int Nt, int S) {
@@ -67,11 +68,17 @@ __host__ __device__ inline size_t blkseg_off_red(int N, int m, int NB, int nblk,
 __host__ __device__ inline size_t blkseg_off_wred(int N, int m, int NB, int nblk, int Nt, int S) {
   return blkseg_off_red(N, m, NB, nblk, Nt, S) + 24;
 }
-__host__ __device__ inline size_t blkseg_off_dJ(int N, int m, int NB, int nblk, int Nt, int S, int W) {
-  return blkseg_off_wred(N, m, NB, nblk, Nt, S) + (size_t)128 * W;
+__host__ __device__ inline size_t blkseg_off_dJ(int N, int m, int NB, int nblk, int Nt, int S, int W, int RB) {
+  return blkseg_off_wred(N, m, NB, nblk, Nt, S) + (size_t)128 * W * RB;
 }
-__host__ __device__ inline size_t blkseg_lds(int N, int m, int nu, int NB, int nblk, int Nt, int S, int W) {
-  return (blkseg_off_dJ(N, m, NB, nblk, Nt, S, W) + (size_t)Nt * nu) * sizeof(double);
+__host__ __device__ inline size_t blkseg_lds(int N, int m, int nu, int NB, int nblk, int Nt, int S, int W, int RB) {
+  return (blkseg_off_dJ(N, m, NB, nblk, Nt, S, W, RB) + (size_t)Nt * nu) * sizeof(double);
+}
+// slice-steps whose block sums are reduced together (phase 3): as many as the reducing lanes of one wave allow
+// (RB x segments per wave x controls <= 64), at most 4
+__host__ __device__ inline int blkseg_rb(int upw, int nu) {
+  const int r = 64 / (upw * (nu > 0 ? nu : 1));
+  return r < 1 ? 1 : r > 4 ? 4 : r;
 }
 
 // Diagnostic per-wave stamps (tools/blkseg_probe.hip, -DQOC_PROBE): workgroup 7, wave w: phase 1 ends at
@@ -458,7 +465,8 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   cx<double>* const cf = reinterpret_cast<cx<double>*>(lds + blkseg_off_cf(N, m, NB, nblk, Nt, S));
   double* const red = lds + blkseg_off_red(N, m, NB, nblk, Nt, S);
   double* const wred = lds + blkseg_off_wred(N, m, NB, nblk, Nt, S);
-  double* const dJ = lds + blkseg_off_dJ(N, m, NB, nblk, Nt, S, W);
+  const int RB = sp.RB;
+  double* const dJ = lds + blkseg_off_dJ(N, m, NB, nblk, Nt, S, W, RB);
 
   // ---- prologue: generator blocks, x_0, the seed's largest ρ_k ----
   {
@@ -477,18 +485,28 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       xN[2 * o + 1] = x0[o].i;
     }
   }
+  // one pass over u: ρ_k, the copies of u (the stale check, the lazy rebuilds) and the records
+  // [Re e^{μ_k}, Im e^{μ_k}, u_1k, u_2k] (e^{μ_k} does not depend on J; u is scaled by 2^-J below when J > 0)
   const double* ub = sp.u + (size_t)b * Nt * nu;
   double rmax = 0.0;
   for (int k = tid; k < Nt; k += nthr) {
     const double u1 = nu > 0 ? ub[(size_t)k * nu] : 0.0, u2 = nu > 1 ? ub[(size_t)k * nu + 1] : 0.0;
+    for (int j = 0; j < nu; ++j) {
+      const double v = j ? u2 : u1;
+      if (sp.u_copy) sp.u_copy[((size_t)b * Nt + k) * nu + j] = v;
+      if (sp.u_copy2) sp.u_copy2[((size_t)b * Nt + k) * nu + j] = v;
+    }
     rmax = fmax(rmax, fma(fabs(u2), sp.rad[2], fma(fabs(u1), sp.rad[1], sp.rad[0])));
+    const double mr = fma(u2, sp.mur[2], fma(u1, sp.mur[1], sp.mur[0]));
+    const double mi = fma(u2, sp.mui[2], fma(u1, sp.mui[1], sp.mui[0]));
+    const double er = exp(mr);
+    double sn, cs;
+    sincos(mi, &sn, &cs);
+    double2* r = reinterpret_cast<double2*>(rec + 4 * (size_t)k);
+    r[0] = make_double2(er * cs, er * sn);
+    r[1] = make_double2(u1, u2);
   }
-  for (size_t i = tid; i < (size_t)Nt * nu; i += nthr) {  // the copies of u (the stale check, the lazy rebuilds)
-    const double v = ub[i];
-    if (sp.u_copy) sp.u_copy[(size_t)b * Nt * nu + i] = v;
-    if (sp.u_copy2) sp.u_copy2[(size_t)b * Nt * nu + i] = v;
-  }
-  rmax = block_max(rmax, red);
+  rmax = block_max(rmax, red);  // (its barriers also publish the records)
   // J: the fewest halvings with ρ / 2^J <= θ_cap; P: the smallest degree whose tail bound
   // b^{P+1} / (P+1)! / (1 - b / (P+2)) is <= 2^-53 (b = ρmax / 2^J; every slice's ρ_k is <= ρmax)
   int J = 0;
@@ -511,17 +529,11 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   }
   P = __builtin_amdgcn_readfirstlane(P);
   J = __builtin_amdgcn_readfirstlane(J);
-  // records: e^{μ_k}, 2^-J u_1k, 2^-J u_2k
-  for (int k = tid; k < Nt; k += nthr) {
-    const double u1 = nu > 0 ? ub[(size_t)k * nu] : 0.0, u2 = nu > 1 ? ub[(size_t)k * nu + 1] : 0.0;
-    const double mr = fma(u2, sp.mur[2], fma(u1, sp.mur[1], sp.mur[0]));
-    const double mi = fma(u2, sp.mui[2], fma(u1, sp.mui[1], sp.mui[0]));
-    const double er = exp(mr);
-    double sn, cs;
-    sincos(mi, &sn, &cs);
-    double2* r = reinterpret_cast<double2*>(rec + 4 * (size_t)k);
-    r[0] = make_double2(er * cs, er * sn);
-    r[1] = make_double2(s0 * u1, s0 * u2);
+  if (J) {  // the records hold 2^-J u (exact scaling)
+    for (int k = tid; k < Nt; k += nthr) {
+      rec[4 * (size_t)k + 2] *= s0;
+      rec[4 * (size_t)k + 3] *= s0;
+    }
   }
   __syncthreads();
   BK_T(t1);
@@ -801,22 +813,28 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   BK_ADD(2, t3 - t2);
   // ---- phase 3: each segment backwards, the gradient of every slice ----
   const double mu1r = sp.mur[1], mu1i = sp.mui[1], mu2r = sp.mur[2], mu2i = sp.mui[2];
-  double* const wr = wred + 128 * w;
-  const int nred = sp.UPW * nu;  // reducing lanes: (segment of the wave, control)
-  const int ro = l / max(nu, 1), rj = l - ro * max(nu, 1);
-  // the slice's sum over its blocks: a wave-private slot, summed in a fixed order
+  double* const wr = wred + 128 * RB * w;
+  // the slices' sums over their blocks: each step's partial sums go to slot (L - 1 - jj) % RB of a wave-private
+  // area; every RB steps (and after the last) one lane per (step, segment of the wave, control) adds its nblk
+  // entries in a fixed order
+  const int nrl = sp.UPW * max(nu, 1);  // reducing lanes per step
+  const int rq = l / nrl, rrem = l - rq * nrl, ro = rrem / max(nu, 1), rj = rrem - ro * max(nu, 1);
   auto reduce = [&](int jj, double acc1, double acc2) {
-    *reinterpret_cast<double2*>(wr + 2 * l) = make_double2(acc1, acc2);
-    wave_lds_sync();
-    if (l < nred) {
-      const int ss = w * sp.UPW + ro, kk = ss * L + jj;
-      if (ss < S && kk < Nt) {
-        double sum = 0.0;
-        for (int q = 0; q < nblk; ++q) sum += wr[2 * (ro * nblk + q) + rj];
-        dJ[(size_t)kk * nu + rj] = sum;
+    const int r = (L - 1 - jj) % RB;
+    *reinterpret_cast<double2*>(wr + 128 * r + 2 * l) = make_double2(acc1, acc2);
+    if (r == RB - 1 || jj == 0) {  // uniform
+      wave_lds_sync();
+      if (rq <= r) {  // slot rq holds step jj + r - rq
+        const int ss = w * sp.UPW + ro, kk = ss * L + jj + r - rq;
+        if (ss < S && kk < Nt) {
+          const double* src = wr + 128 * rq + 2 * ro * nblk + rj;
+          double sum = 0.0;
+          for (int q = 0; q < nblk; ++q) sum += src[2 * q];
+          dJ[(size_t)kk * nu + rj] = sum;
+        }
       }
+      wave_lds_sync();
     }
-    wave_lds_sync();
   };
   auto p3_fast = [&](int jj, auto SEL_) {
     constexpr bool SEL = decltype(SEL_)::value;

@@ -725,7 +725,7 @@ static BlksegShape blkseg_shape(const qoc_ctx* c) {
   s.L = (c->Nt + S - 1) / S;
   s.S = (c->Nt + s.L - 1) / s.L;
   s.W = (s.S + s.UPW - 1) / s.UPW;
-  s.lds = blkseg_lds(c->N, c->m, c->nu, c->blk_nb, c->nblk, c->Nt, s.S, s.W);
+  s.lds = blkseg_lds(c->N, c->m, c->nu, c->blk_nb, c->nblk, c->Nt, s.S, s.W, blkseg_rb(s.UPW, c->nu));
   return s;
 }
 
@@ -776,6 +776,7 @@ int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d
   sp.S = s.S;
   sp.L = s.L;
   sp.UPW = s.UPW;
+  sp.RB = blkseg_rb(s.UPW, c->nu);
   sp.u = d_u;
   sp.u_copy = d_u != c->d_u ? c->d_u : nullptr;
   sp.u_copy2 = c->d_u_lam;  // the co-states' rebuild (blku_costates) reads this copy and d_coef_lam

@@ -62,9 +62,10 @@ void run(int B, int Nt, int nblk, int m, int W, int Scap, int noturn = 0) {
   sp.L = (Nt + S - 1) / S;
   sp.S = (Nt + sp.L - 1) / sp.L;
   W = (sp.S + sp.UPW - 1) / sp.UPW;
+  sp.RB = blkseg_rb(sp.UPW, nu);
   sp.u = du;
   sp.dJdu = ddJ;
-  const size_t lds = blkseg_lds(N, m, nu, NB, nblk, Nt, sp.S, W);
+  const size_t lds = blkseg_lds(N, m, nu, NB, nblk, Nt, sp.S, W, sp.RB);
   if (lds > 160 * 1024) return;
   (void)hipFuncSetAttribute((const void*)k_blkseg_eval<NB, 3, WMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipEvent_t a, b;
