@@ -399,6 +399,197 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_bgemm_glds: the fp32 MODE-0 product of k_bgemm (same GemmArgs, tiles, XCD order, epilogue) with its operand
+// slabs staged by LDS-DMA (global_load_lds_dwordx4) three slabs deep.  k_bgemm stages each 16-deep slab through
+// registers one slab ahead; at N = 256 the items a CU works on at once do not fit the XCD's L2, most slab loads come
+// from HBM, and the waves waited for them at every slab (the MFMA pipe ~55 % busy by PMC).  Here the slab s + 2 is
+// in flight while slab s is multiplied, with no registers held for it, and each wave waits with a counted vmcnt for
+// its own DMA pieces of slab s + 1 only, followed by a raw s_barrier (a __syncthreads would drain every DMA).
+//
+// LDS image per stage: A and B slabs of 64 "rows" (A: rows of op(A); B: columns of op(B)) x 16 k, complex
+// interleaved (8 B), 8 KB each.  The DMA writes 16 B per lane at a lane-linear position, so each image takes the
+// layout in which 16 B are contiguous in HBM, with the XOR swizzle on the source address:
+//   KR (memory contiguous along the row: A, or B^H):  (r, k) at k*512 + ((r/16 ^ k&1) * 128) + (r%16)*8
+//   RK (memory contiguous along k: A^H, or B):        (r, k) at r*128 + (((k/2) ^ ((r/2)&7)) * 16) + (k&1)*8
+// Fragment reads are ds_read_b64 (one complex): lane (i = l%16, kq = l/16) at MFMA step t reads (row 16x + i,
+// k = 4t + kq).  The 32 lanes of one LDS cycle then cover all 64 banks once in both layouts.
+// Requirements (bgemm_glds_ok): T = float, K % 16 == 0, M and Ncol even (a 16-byte piece is two elements).
+constexpr int BGG_STAGES = 3, BGG_STAGE_FLOATS = 2 * 64 * 16 * 2;  // A + B, complex fp32
+template <bool KR>
+__device__ __forceinline__ int bgg_off(int r, int k) {  // byte offset of (r, k) in an operand image
+  return KR ? k * 512 + (((r >> 4) ^ (k & 1)) << 7) + ((r & 15) << 3)
+            : r * 128 + ((((k >> 1) ^ ((r >> 1) & 7))) << 4) + ((k & 1) << 3);
+}
+// the (row, k) of the first of the two elements lane j of DMA piece q (0..7) writes
+template <bool KR>
+__device__ __forceinline__ void bgg_piece(int q, int j, int& r, int& k) {
+  if (KR) {
+    k = 2 * q + (j >> 5);
+    r = 16 * (((j >> 3) & 3) ^ (k & 1)) + 2 * (j & 7);
+  } else {
+    r = 8 * q + (j >> 3);
+    k = 2 * ((j & 7) ^ ((r >> 1) & 7));
+  }
+}
+// One DMA piece: 16 B per lane from src (per lane) to LDS byte address lds_base + 16 lane (lds_base wave-uniform).
+// Inline asm rather than the builtin: for the builtin hipcc inserts vmcnt(0) before the next ds_read of the (one)
+// LDS array, which would drain the slabs kept in flight; the waits are counted by hand (k_bgemm_glds).  M0 is set
+// and restored in the same statement.
+__device__ __forceinline__ void bgg_dma(const void* src, unsigned lds_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_base)
+               : "memory");
+}
+
+template <int OPA, int OPB>
+__global__ __launch_bounds__(BG_THREADS) void k_bgemm_glds(GemmArgs g) {
+  using MFT = MF<float>;
+  using v4 = typename MFT::v4;
+  constexpr bool KRA = OPA == 0, KRB = OPB == 1;  // layouts of the A and B images
+  __shared__ __attribute__((aligned(16))) float lds[BGG_STAGES * BGG_STAGE_FLOATS];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int Lb = blockIdx.x;
+  const int total = g.nitems * g.tiles;
+  const int lin = (total & 7) == 0 ? (Lb & 7) * (total >> 3) + (Lb >> 3) : Lb;
+  const int item = lin / g.tiles, tile = lin - item * g.tiles;
+  const int tm = tile % g.tiles_m, tn = tile / g.tiles_m;
+  const int row0 = tm * BG_BM, col0 = tn * BG_BN;
+  const cx<float>* Ab = opd_ptr<float>(g.A, item);
+  const cx<float>* Bb = opd_ptr<float>(g.B, item);
+  const int M = g.M, K = g.K, NC = g.Ncol;
+  const long long ldA = OPA ? K : M, ldB = OPB ? NC : K;
+  // this wave's two DMA pieces per operand (q = 2 wave + h): per-lane source element at slab 0, and the per-slab step
+  long long srcA[2], srcB[2];
+  const long long stepA = KRA ? 16 * ldA : 16, stepB = KRB ? 16 * ldB : 16;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    int r, k;
+    bgg_piece<KRA>(2 * wave + h, lane, r, k);
+    // rows past M: any valid row (their outputs are not stored); KR pieces hold the row pair (r, r + 1), r even
+    const int gr = min(row0 + r, KRA ? M - 2 : M - 1);
+    srcA[h] = KRA ? gr + ldA * k : k + ldA * gr;
+    bgg_piece<KRB>(2 * wave + h, lane, r, k);
+    const int gc = min(col0 + r, KRB ? NC - 2 : NC - 1);
+    srcB[h] = KRB ? gc + ldB * k : k + ldB * gc;
+  }
+  const int nslab = K / 16;
+  const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) float*)lds;
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    const unsigned st = lds0 + (unsigned)((s % BGG_STAGES) * BGG_STAGE_FLOATS * 4);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const unsigned q = (unsigned)__builtin_amdgcn_readfirstlane(2 * wave + h);
+      bgg_dma(Ab + srcA[h] + s * stepA, st + q * 1024);
+      bgg_dma(Bb + srcB[h] + s * stepB, st + 8192 + q * 1024);
+    }
+  };
+  v4 cr[2][2], ci[2][2], cs[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      cr[x][y] = v4{0, 0, 0, 0};
+      ci[x][y] = v4{0, 0, 0, 0};
+      cs[x][y] = v4{0, 0, 0, 0};
+    }
+  const int wr = (wave & 1) * 32, wc = (wave >> 1) * 32;
+  const int li = lane & 15, kq = lane >> 4;
+  // fragment byte offsets in an image at step t = 0 (step t adds 4t to k: KR +2048 B, RK via the slot XOR)
+  issue(0);
+  if (nslab > 1) issue(1);
+  if (nslab > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int s = 0; s < nslab; ++s) {
+    if (s + 2 < nslab) issue(s + 2);
+    const char* cur = reinterpret_cast<const char*>(lds + (s % BGG_STAGES) * BGG_STAGE_FLOATS);
+    const char* curB = cur + 8192;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = 4 * t + kq;
+      float ar[2], ai[2], br[2], bi[2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const float2 v = *reinterpret_cast<const float2*>(cur + bgg_off<KRA>(wr + 16 * x + li, k));
+        ar[x] = v.x;
+        ai[x] = OPA ? -v.y : v.y;
+      }
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {
+        const float2 v = *reinterpret_cast<const float2*>(curB + bgg_off<KRB>(wc + 16 * y + li, k));
+        br[y] = v.x;
+        bi[y] = OPB ? -v.y : v.y;
+      }
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          cr[x][y] = MFT::mma(ar[x], br[y], cr[x][y]);
+          ci[x][y] = MFT::mma(ai[x], bi[y], ci[x][y]);
+          cs[x][y] = MFT::mma(ar[x] + ai[x], br[y] + bi[y], cs[x][y]);
+        }
+    }
+    // slab s + 1 landed (this wave's pieces; slab s + 2's stay in flight), every read of slab s done, then the
+    // barrier: after it slab s + 1 is readable and slab s's buffer may be refilled (by slab s + 3)
+    if (s + 2 < nslab) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  // ---- epilogue (k_bgemm MODE 0) ----
+  cx<float>* C1 = const_cast<cx<float>*>(opd_ptr<float>(g.C1, item));
+  cx<float>* C2 = g.C2.p ? const_cast<cx<float>*>(opd_ptr<float>(g.C2, item)) : nullptr;
+  cx<float>* C3 = g.C3.p ? const_cast<cx<float>*>(opd_ptr<float>(g.C3, item)) : nullptr;
+  const cx<float>* Y0 = g.nY > 0 ? opd_ptr<float>(g.Y[0], item) : nullptr;
+  const cx<float>* Y1 = g.nY > 1 ? opd_ptr<float>(g.Y[1], item) : nullptr;
+  const cx<float>* Y2 = g.nY > 2 ? opd_ptr<float>(g.Y[2], item) : nullptr;
+  double mx = 0.0;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const int col = col0 + wc + 16 * y + li;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = row0 + wr + 16 * x + MFT::drow(lane, i);
+        if (row < M && col < NC) {
+          const size_t o = row + (size_t)M * col;
+          const double pr = (double)cr[x][y][i] - (double)ci[x][y][i];
+          const double pi = (double)cs[x][y][i] - (double)cr[x][y][i] - (double)ci[x][y][i];
+          double r1 = g.alpha1 * pr, i1 = g.alpha1 * pi;
+          double r2 = g.alpha2 * pr, i2 = g.alpha2 * pi;
+          double r3 = g.alpha3 * pr, i3 = g.alpha3 * pi;
+#define QOC_EPI_Y(YP, t)                                        \
+  if (YP) {                                                     \
+    const cx<float> v = YP[o];                                  \
+    r1 += g.w1[t] * v.r; i1 += g.w1[t] * v.i;                   \
+    r2 += g.w2[t] * v.r; i2 += g.w2[t] * v.i;                   \
+    r3 += g.w3[t] * v.r; i3 += g.w3[t] * v.i;                   \
+  }
+          QOC_EPI_Y(Y0, 0)
+          QOC_EPI_Y(Y1, 1)
+          QOC_EPI_Y(Y2, 2)
+#undef QOC_EPI_Y
+          if (row == col) {
+            r1 += g.gamma1;
+            r2 += g.gamma2;
+            r3 += g.gamma3;
+          }
+          C1[o] = cx<float>{(float)r1, (float)i1};
+          if (C2) C2[o] = cx<float>{(float)r2, (float)i2};
+          if (C3) C3[o] = cx<float>{(float)r3, (float)i3};
+          mx += r1 * r1 + i1 * i1;
+        }
+      }
+    }
+  if (g.sumsq) {
+    for (int off = 32; off > 0; off >>= 1) mx += __shfl_xor(mx, off);
+    if (lane == 0) atomicAdd(g.sumsq + item, mx);
+  }
+}
+
 // 2-norm bound of every A_k of a chunk for skew-Hermitian generators: ||A_k||_2 <= Σ_j |c_jk| ρ_j with c_0 = 1,
 // c_j = u_jk, ρ_j = ||A_j||_2 (the spectral radius, A_j normal) -> atomic max in bmax (one thread per unit).
 struct SpecBound {
@@ -457,9 +648,12 @@ __global__ void k_lincomb(LinArgs a) {
   }
 }
 
-// A_unit = A0 + sum_j u[unit, j] A_j for units [unit0, unit0 + count) -> out (count x N x N), and the
-// 1-norm (max column sum of |a_ij|) of each, max-reduced into *nmax.  One workgroup per slice;
-// each wave owns whole columns (coalesced column reads, shuffle reduction).
+// A_unit = A0 + sum_j u[unit, j] A_j for units [unit0, unit0 + count) -> out (count x N x N), and (nmax set) the
+// 1-norm (max column sum of |a_ij|) of each, max-reduced into *nmax.  One workgroup per slice; each wave takes
+// batches of FN_C whole columns at a time, FN_R rows per lane per batch, so that FN_C * FN_R independent loads of
+// each generator are in flight per lane (one column per wave-iteration left every load's L2 round trip exposed:
+// ~0.8 TB/s of writes at N = 256).  The atomic max is skipped when the running value is already larger.
+constexpr int FN_C = 4, FN_R = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void k_form_norm(int N, int nu, long long unit0, const cx<T>* __restrict__ Agen,
                                                    const double* __restrict__ u, cx<T>* __restrict__ out,
@@ -472,26 +666,59 @@ __global__ __launch_bounds__(256) void k_form_norm(int N, int nu, long long unit
   for (int j = 0; j < 8; ++j) uj[j] = j < nu ? (T)u[unit * nu + j] : T(0);
   cx<T>* ob = out + (size_t)it * NN;
   double best = 0.0;
-  for (int c = wave; c < N; c += 4) {
-    double s = 0.0;
-    for (int r = lane; r < N; r += 64) {
-      const size_t e = r + (size_t)N * c;
-      cx<T> a = Agen[e];
+  for (int c0 = wave * FN_C; c0 < N; c0 += 4 * FN_C) {
+    double s[FN_C];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (j < nu) {
-          const cx<T> v = Agen[(size_t)(j + 1) * NN + e];
-          a.r += uj[j] * v.r;
-          a.i += uj[j] * v.i;
+    for (int x = 0; x < FN_C; ++x) s[x] = 0.0;
+    for (int r0 = 0; r0 < N; r0 += 64 * FN_R) {
+      size_t e[FN_C][FN_R];
+      bool ok[FN_C][FN_R];
+      cx<T> a[FN_C][FN_R];
+#pragma unroll
+      for (int x = 0; x < FN_C; ++x)
+#pragma unroll
+        for (int q = 0; q < FN_R; ++q) {
+          const int r = r0 + lane + 64 * q, c = c0 + x;
+          ok[x][q] = r < N && c < N;
+          e[x][q] = ok[x][q] ? r + (size_t)N * c : 0;
+          a[x][q] = Agen[e[x][q]];
         }
+      for (int j = 0; j < nu && j < 8; ++j) {
+        const cx<T>* Aj = Agen + (size_t)(j + 1) * NN;
+        T w = uj[0];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) w = j == q ? uj[q] : w;
+#pragma unroll
+        for (int x = 0; x < FN_C; ++x)
+#pragma unroll
+          for (int q = 0; q < FN_R; ++q) {
+            const cx<T> v = Aj[e[x][q]];
+            a[x][q].r += w * v.r;
+            a[x][q].i += w * v.i;
+          }
       }
-      ob[e] = a;
-      s += sqrt((double)a.r * a.r + (double)a.i * a.i);
+#pragma unroll
+      for (int x = 0; x < FN_C; ++x)
+#pragma unroll
+        for (int q = 0; q < FN_R; ++q)
+          if (ok[x][q]) {
+            ob[e[x][q]] = a[x][q];
+            if (nmax) s[x] += sqrt((double)a[x][q].r * a[x][q].r + (double)a[x][q].i * a[x][q].i);
+          }
     }
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    best = fmax(best, s);
+    if (nmax) {
+#pragma unroll
+      for (int x = 0; x < FN_C; ++x) {
+        double v = s[x];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        best = fmax(best, v);
+      }
+    }
   }
-  if (lane == 0 && nmax) atomicMax(nmax, (unsigned long long)__double_as_longlong(best));
+  if (nmax && lane == 0) {
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(best);
+    if (bits > __hip_atomic_load(nmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(nmax, bits);
+  }
 }
 
 // Guard-state penalty over all stored states: J[b] = mu * sum_{k, masked} |x_k|^2 (one WG per seed).

@@ -654,6 +654,7 @@ __device__ __forceinline__ void blkrot_fwd_body(const TChainArgs& g, const BlkAr
   double* c1b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm) : nullptr;
   double* c2b = cap ? reinterpret_cast<double*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm) : nullptr;
   double pen = 0.0;
+  for (size_t e = tid; e < 2 * Nm; e += nthr) xN[e] = 0.0;  // the rows of blocks without a wave (blk_live) stay 0
   __syncthreads();
   *(ln.act ? Xb + oe : sink) = acc;
   pen += pm ? acc * acc : 0.0;
@@ -756,6 +757,21 @@ __device__ __forceinline__ void blkrot_bwd_body(const TChainArgs& g, const BlkAr
         *(to ? c2b + ok_ : sink + 1) = cd2;
       }
     }
+  }
+}
+
+// Zeros on the rows of the blocks that carry no state (qoc_run_blk.hip blk_live): rows[0..nrow) of each of the
+// `cols` N-row columns of up to six state-shaped buffers (x_k, μ_k and the chains' captured products)
+struct ZeroRows {
+  double2* buf[6];
+  int nbuf;
+};
+static __global__ void k_zero_rows(const ZeroRows z, long long cols, int N, const int* __restrict__ rows, int nrow) {
+  const long long total = cols * nrow;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long q = e / nrow;
+    const size_t o = (size_t)q * N + rows[e - q * nrow];
+    for (int i = 0; i < z.nbuf; ++i) z.buf[i][o] = make_double2(0.0, 0.0);
   }
 }
 

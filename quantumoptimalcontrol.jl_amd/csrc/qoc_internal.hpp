@@ -175,6 +175,11 @@ struct qoc_ctx {
   bool blk_real = false;         // MFMA block waves on the real embedding of blocks of <= 2 rows (k_blkrot_*<0>)
   int nwb = 0;                   // MFMA block waves per column pair
   int* d_wrow = nullptr;         // nwb x 16 rows of each wave's state (-1 padding)
+  std::vector<int> h_wrow;       // host copy (blocks of 5..16 rows: one wave per block)
+  // blocks of 5..16 rows with x_0 and X_target zero on their rows (blk_live): the waves of the others, the dead rows
+  std::vector<int> h_wrow_live, h_dead_rows;
+  int* d_wrow_live = nullptr;
+  int* d_dead_rows = nullptr;
   size_t blk_dev_bytes = 0;      // d_brow + d_wrow (counted in dev_bytes)
   double* d_blkrec = nullptr;    // block propagators: B x Ntp x BLKU_REC step records (k_blku_rec, allocated on first use)
   // multi-GPU epilogue (qoc_comm.hpp): RCCL communicator over the ranks' contexts

@@ -1,5 +1,6 @@
 // qoc_run_big.hip — the large-N batched-GEMM pipeline (qoc_bgemm.hpp), the GEMM-shaped order-3 gradient and the
 // exact (Fréchet) gradient (qoc_frechet.hpp).
+#include <type_traits>
 #include "qoc_bgemm.hpp"
 #include "qoc_frechet.hpp"
 #include "qoc_internal.hpp"
@@ -66,7 +67,16 @@ int big_gemm(qoc_ctx* c, int opa, int opb, GemmArgs g, int mode = 0) {
     gm.b = take_event(c);
     (void)hipEventRecord(gm.a, c->stream);
   }
-  if (mode == 1) hipLaunchKernelGGL((k_bgemm<T, 0, 0, true, 1, 2, 1>), grid, blk, 0, c->stream, g);
+  // fp32 products with K % 16 == 0 and even M, Ncol: the LDS-DMA staged kernel (QOC_BGEMM_GLDS=0 keeps k_bgemm)
+  static const bool glds_env = !(getenv("QOC_BGEMM_GLDS") && atoi(getenv("QOC_BGEMM_GLDS")) == 0);
+  const bool glds = std::is_same<T, float>::value && mode == 0 && glds_env && g.K % 16 == 0 && g.M % 2 == 0 &&
+                    g.Ncol % 2 == 0 && g.M >= 2 && g.Ncol >= 2;
+  if (glds) {
+    if (opa == 0 && opb == 0) hipLaunchKernelGGL((k_bgemm_glds<0, 0>), grid, blk, 0, c->stream, g);
+    else if (opa == 1 && opb == 0) hipLaunchKernelGGL((k_bgemm_glds<1, 0>), grid, blk, 0, c->stream, g);
+    else if (opa == 0 && opb == 1) hipLaunchKernelGGL((k_bgemm_glds<0, 1>), grid, blk, 0, c->stream, g);
+    else hipLaunchKernelGGL((k_bgemm_glds<1, 1>), grid, blk, 0, c->stream, g);
+  } else if (mode == 1) hipLaunchKernelGGL((k_bgemm<T, 0, 0, true, 1, 2, 1>), grid, blk, 0, c->stream, g);
   else if (mode == 2) hipLaunchKernelGGL((k_bgemm<T, 0, 0, true, 1, 2, 2>), grid, blk, 0, c->stream, g);
   else if (opa == 0 && opb == 0) hipLaunchKernelGGL((k_bgemm<T, 0, 0>), grid, blk, 0, c->stream, g);
   else if (opa == 1 && opb == 0) hipLaunchKernelGGL((k_bgemm<T, 1, 0>), grid, blk, 0, c->stream, g);

@@ -111,7 +111,10 @@ int blk_detect(qoc_ctx* c) {
     while (slot.size() % 16) slot.push_back(-1);
     wrow = slot;
   }
-  for (int** p : {&c->d_brow, &c->d_wrow})
+  c->h_wrow = wrow;
+  c->h_wrow_live.clear();
+  c->h_dead_rows.clear();
+  for (int** p : {&c->d_brow, &c->d_wrow, &c->d_wrow_live, &c->d_dead_rows})
     if (*p) {
       HIPCHK(c, hipFree(*p));
       *p = nullptr;
@@ -290,12 +293,81 @@ static BlkArgs blk_args(const qoc_ctx* c) {
   return bk;
 }
 
-static int blk_threads(const qoc_ctx* c) {
-  if (c->blk_real) return 64 * c->nwb * ((c->m + 3) / 4);  // 4 state columns per real-embedded wave
-  return blk_rot(c) ? 64 * c->nwb * ((c->m + 1) / 2) : 64 * ((c->nblk * c->m + 63) / 64);
+static int blk_threads(const qoc_ctx* c, int nwb = -1) {
+  if (nwb < 0) nwb = c->nwb;
+  if (c->blk_real) return 64 * nwb * ((c->m + 3) / 4);  // 4 state columns per real-embedded wave
+  return blk_rot(c) ? 64 * nwb * ((c->m + 1) / 2) : 64 * ((c->nblk * c->m + 63) / 64);
 }
-static size_t blk_lds_of(const qoc_ctx* c) {
-  return blk_rot(c) ? blkrot_lds(c->N, c->m, blk_threads(c) / 64) : blk_lds(c->N, c->m);
+static size_t blk_lds_of(const qoc_ctx* c, int nwb = -1) {
+  return blk_rot(c) ? blkrot_lds(c->N, c->m, blk_threads(c, nwb) / 64) : blk_lds(c->N, c->m);
+}
+
+// Blocks of 5..16 rows that carry no state: x_0 (every seed) and X_target are zero on all their rows.  The generators
+// keep every block invariant, so such a block's x_k and μ_k are exactly zero at every k, and it adds nothing to J
+// (its overlaps are zero) or to dJ/du (each generator's contribution is λ_β^H A_jβ x_β = 0).  The reference exploits
+// the same structure by hand with compress_states (src/utils.jl:96-109; the tunable bus' parity blocks,
+// test/test_utils.jl:23): here the concurrent eval launches waves for the live blocks only and k_zero_rows writes
+// the dead rows' zeros into the state-shaped buffers, so every output (x_k, λ_k, J, dJ/du) is what the full launch
+// gives.  The tunable bus (m = 1, |110> -> |200>) carries its state in the 14-row even-parity block only.
+// QOC_BLK_DEAD=0 launches every block.  Sets bk.wrow / bk.nwb; leaves them when every block is live.
+static int blk_live(qoc_ctx* c, BlkArgs& bk) {
+  if (!blk_big(c) || c->h_wrow.empty() || c->h_Xt.empty() || !c->have_x0) return QOC_OK;
+  const char* env = getenv("QOC_BLK_DEAD");
+  if (env && atoi(env) == 0) return QOC_OK;
+  const int N = c->N, mu = c->m_user;
+  const size_t cnt = c->x0_per_seed ? (size_t)c->B : 1, Nmu = (size_t)N * mu;
+  if (c->h_x0.size() < 2 * Nmu * cnt || c->h_Xt.size() < 2 * Nmu) return QOC_OK;
+  std::vector<char> live(N, 0);
+  auto mark = [&](const double* v) {
+    for (size_t e = 0; e < Nmu; ++e)
+      if (v[2 * e] != 0.0 || v[2 * e + 1] != 0.0) live[e % N] = 1;
+  };
+  for (size_t q = 0; q < cnt; ++q) mark(c->h_x0.data() + 2 * Nmu * q);
+  mark(c->h_Xt.data());
+  std::vector<int> wl, dead;
+  for (int w = 0; w < c->nwb; ++w) {
+    bool lv = false;
+    for (int i = 0; i < 16; ++i) {
+      const int r = c->h_wrow[16 * w + i];
+      lv = lv || (r >= 0 && live[r]);
+    }
+    for (int i = 0; i < 16; ++i) {
+      const int r = c->h_wrow[16 * w + i];
+      if (lv) wl.push_back(r);
+      else if (r >= 0) dead.push_back(r);
+    }
+  }
+  if (dead.empty() || wl.empty()) return QOC_OK;
+  if (wl != c->h_wrow_live || dead != c->h_dead_rows) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int** p : {&c->d_wrow_live, &c->d_dead_rows})
+      if (*p) {
+        HIPCHK(c, hipFree(*p));
+        *p = nullptr;
+      }
+    HIPCHK(c, hipMalloc((void**)&c->d_wrow_live, wl.size() * sizeof(int)));
+    HIPCHK(c, hipMemcpy(c->d_wrow_live, wl.data(), wl.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMalloc((void**)&c->d_dead_rows, dead.size() * sizeof(int)));
+    HIPCHK(c, hipMemcpy(c->d_dead_rows, dead.data(), dead.size() * sizeof(int), hipMemcpyHostToDevice));
+    c->h_wrow_live = wl;
+    c->h_dead_rows = dead;
+  }
+  bk.wrow = c->d_wrow_live;
+  bk.nwb = (int)(wl.size() / 16);
+  return QOC_OK;
+}
+// the dead rows' zeros (blk_live) in up to six state-shaped buffers of B (Nt + 1) m columns
+static int blk_zero_dead(qoc_ctx* c, std::initializer_list<void*> bufs) {
+  ZeroRows z{};
+  for (void* p : bufs)
+    if (p && z.nbuf < 6) z.buf[z.nbuf++] = (double2*)p;
+  const long long cols = (long long)c->B * (c->Nt + 1) * c->m;
+  const long long total = cols * (long long)c->h_dead_rows.size();
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_zero_rows, dim3(grid), dim3(256), 0, c->stream, z, cols, c->N, c->d_dead_rows,
+                     (int)c->h_dead_rows.size());
+  HIPCHK(c, hipGetLastError());
+  return QOC_OK;
 }
 // dynamic LDS above the 64 KiB default (up to 16 MFMA block waves of staging)
 template <typename K>
@@ -427,8 +499,15 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
     gb.cap1 = c->d_gws;
     gb.cap2 = (cx<double>*)c->d_gws + bufN;
   }
-  const BlkArgs bk = blk_args(c);
-  const size_t lds = blk_lds_of(c);
+  BlkArgs bk = blk_args(c);
+  if ((r = blk_live(c, bk))) return r;
+  const bool skip = bk.nwb != c->nwb;
+  const size_t lds = blk_lds_of(c, bk.nwb);
+  const int thr = blk_threads(c, bk.nwb);
+  if (skip) {
+    if ((r = blk_zero_dead(c, {c->d_X, c->d_L, (void*)gf.cap1, (void*)gf.cap2, (void*)gb.cap1, (void*)gb.cap2})))
+      return r;
+  }
   const int mk = mark_begin(c, 1);
   const hipError_t e = blk_dispatch(c, [&](auto NB_, auto CH_) {
     constexpr int NB = decltype(NB_)::value;
@@ -436,9 +515,9 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
     if constexpr (NB < 100) {
       const hipError_t q = blk_lds_attr(k_blkrot_dual<NB, CH>, lds);
       if (q != hipSuccess) return q;
-      hipLaunchKernelGGL((k_blkrot_dual<NB, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
+      hipLaunchKernelGGL((k_blkrot_dual<NB, CH>), dim3(2 * c->B), dim3(thr), lds, c->stream, gf, gb, bk);
     }
-    else hipLaunchKernelGGL((k_blk_dual<NB - 100, CH>), dim3(2 * c->B), dim3(blk_threads(c)), lds, c->stream, gf, gb, bk);
+    else hipLaunchKernelGGL((k_blk_dual<NB - 100, CH>), dim3(2 * c->B), dim3(thr), lds, c->stream, gf, gb, bk);
     return hipGetLastError();
   });
   mark_end(c, mk);

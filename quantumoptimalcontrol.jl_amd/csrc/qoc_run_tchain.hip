@@ -130,9 +130,21 @@ int tchain_prep(qoc_ctx* c) {
   }
   int mk = mark_begin(c, 0);
   const unsigned pb = (unsigned)std::min<long long>((units + 255) / 256, 2048);
-  if (cheb)  // one wave per workgroup (the coefficient rows are staged in its LDS)
+  // The Chebyshev prep: one thread per unit storing its coefficient row (default), or QOC_TCHEB_PREP=1 one wave per
+  // 64 units with the rows staged in LDS and stored coalesced (round 4).  Same-box A/B on the tunable bus
+  // (profiles/bench_r05k_tb_*.json): the staged form writes fewer bytes but its prep is slower (0.41 vs 0.35 ms) and
+  // the block chain after it ran 22.0 instead of 18.4 ms (writing full 64-entry rows, QOC_TCHEB_PW=64, did not
+  // change that); with dead blocks skipped (blk_live) both give 15.1 ms.
+  const char* pk = getenv("QOC_TCHEB_PREP");
+  const char* pwe = getenv("QOC_TCHEB_PW");  // smallest coefficient row width the staged form writes
+  const int prep_kind = pk ? atoi(pk) : 0, prep_pw = pwe ? atoi(pwe) : 0;
+  if (cheb && prep_kind == 0)
+    hipLaunchKernelGGL(k_tchain_prep_cheb_strided, dim3(pb), dim3(256), 0, c->stream, c->nu, units,
+                       (const double*)c->d_u, c->tprm, c->d_steps, c->d_tcoef, c->d_terms);
+  else if (cheb)  // one wave per workgroup (the coefficient rows are staged in its LDS)
     hipLaunchKernelGGL(k_tchain_prep_cheb, dim3((unsigned)std::min<long long>((units + 63) / 64, 8192)), dim3(64), 0,
-                       c->stream, c->nu, units, (const double*)c->d_u, c->tprm, c->d_steps, c->d_tcoef, c->d_terms);
+                       c->stream, c->nu, units, (const double*)c->d_u, c->tprm, c->d_steps, c->d_tcoef, c->d_terms,
+                       prep_pw);
   else
     hipLaunchKernelGGL(k_tchain_prep, dim3(pb), dim3(256), 0, c->stream, c->nu, units, (const double*)c->d_u, c->tprm,
                        c->d_steps, c->d_terms);

@@ -294,7 +294,7 @@ constexpr int TCHEB_LDS_STRIDE = TCHEB_STRIDE + 1;
 static __global__ __launch_bounds__(64) void k_tchain_prep_cheb(int nu, long long units, const double* __restrict__ u,
                                                                 const TChainParams prm, TStep* __restrict__ steps,
                                                                 double* __restrict__ coef,
-                                                                unsigned long long* __restrict__ terms) {
+                                                                unsigned long long* __restrict__ terms, int pwmin) {
   __shared__ double rows[64 * TCHEB_LDS_STRIDE];
   const int l = threadIdx.x;
   double* ce = rows + l * TCHEB_LDS_STRIDE;
@@ -329,7 +329,7 @@ static __global__ __launch_bounds__(64) void k_tchain_prep_cheb(int nu, long lon
     }
     int pw = P + 1;
     for (int o = 32; o > 0; o >>= 1) pw = max(pw, __shfl_xor(pw, o));
-    pw = min((pw + 1) & ~1, TCHEB_STRIDE);
+    pw = min(max((pw + 1) & ~1, pwmin), TCHEB_STRIDE);
     __syncthreads();
     const int nrow = (int)min<long long>(64, units - e0);
     double* dst = coef + (size_t)e0 * TCHEB_STRIDE;
@@ -341,6 +341,41 @@ static __global__ __launch_bounds__(64) void k_tchain_prep_cheb(int nu, long lon
   }
   for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
   if (l == 0 && cnt) atomicAdd(terms + blockIdx.x % TERM_SLOTS, cnt);
+}
+
+// The Chebyshev prep's default form (qoc_run_tchain.hip tchain_prep: the A/B against k_tchain_prep_cheb): one thread
+// per unit, its coefficient row stored straight to HBM
+static __global__ void k_tchain_prep_cheb_strided(int nu, long long units, const double* __restrict__ u,
+                                                  const TChainParams prm, TStep* __restrict__ steps,
+                                                  double* __restrict__ coef, unsigned long long* __restrict__ terms) {
+  unsigned long long cnt = 0;
+  const double tol = 1.1102230246251565e-16;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < units; e += (long long)gridDim.x * blockDim.x) {
+    double beta = prm.rad[0], mr = prm.mur[0], mi = prm.mui[0];
+    for (int j = 0; j < nu; ++j) {
+      const double uj = u[e * nu + j];
+      beta += fabs(uj) * prm.rad[j + 1];
+      mr += uj * prm.mur[j + 1];
+      mi += uj * prm.mui[j + 1];
+    }
+    beta = fmax(beta, 1e-300);
+    int s = 1;
+    if (beta > 25.0) s = (int)ceil(beta / 25.0);
+    const double rho = beta / s;
+    double* ce = coef + (size_t)e * TCHEB_STRIDE;
+    int P = 0;
+    if (rho <= 2.0) {
+      P = cheb_series(rho, tol, ce, prm.pmin);
+    } else {
+      P = cheb_miller(rho, tol, ce);
+      if (P < prm.pmin) P = prm.pmin;
+    }
+    const double er = exp(mr);
+    steps[e] = TStep{er * cos(mi), er * sin(mi), P, s, 2.0 / beta};
+    cnt += (unsigned long long)(P * s);
+  }
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(terms + blockIdx.x % TERM_SLOTS, cnt);
 }
 
 struct TChainArgs {

@@ -380,3 +380,41 @@ def test_new_block_layout_reallocates_stored_propagators(built_lib, monkeypatch)
     for b in range(2):
         J0, g0, _ = O.grape_eval(p4.A0, p4.A, u4[b], p4.x0, p4.x_target, p4.n, order=3)
         _assert_seed(J[b], g[b], J0, g0, b)
+
+
+def test_blocks_mfma_dead_blocks_skipped(built_lib, monkeypatch):
+    """Blocks of 5..16 rows whose x0 and target rows are all zero (the tunable bus at m = 1: |110> -> |200> lives in
+    the 14-row even-parity block) get no waves in the concurrent eval; their rows of x_k and λ_k are written as zeros.
+    J, dJ/du, states and co-states equal the all-blocks launch (QOC_BLK_DEAD=0) exactly, also after an eval whose
+    live block was the other one left nonzero rows behind, and match the oracle."""
+    from qoc_amd import systems
+    Nt = 48
+    prob = systems.tunable_bus_problem(Nt=Nt, tgate=350.0 * Nt / 2000)
+    u = systems.tunable_bus_controls(2, Nt, seed=71)
+    qb = systems.QuantumBasis([3, 3, 3])
+    x_odd, t_odd = qb.columns(["100"]).astype(complex), qb.columns(["001"]).astype(complex)
+    assert np.abs(x_odd[0::2]).max() == 0 and np.abs(prob.x0[1::2]).max() == 0
+    ks = (0, 1, Nt // 2, Nt)
+    out = {}
+    for dead in ("1", "0"):
+        monkeypatch.setenv("QOC_BLK_DEAD", dead)
+        e = _engine(prob, 2, True, monkeypatch)
+        e.set_x0(x_odd)
+        e.set_cost_trace(t_odd, prob.n)
+        _eval(e, u, True)  # the odd block live: nonzero odd rows in every buffer
+        e.set_x0(prob.x0)
+        e.set_cost_trace(prob.x_target, prob.n)
+        J, g = _eval(e, u, True)
+        assert e.info()["chain_kernel"] == "blocks_mfma"
+        xs = [e.state(k, seed=b) for k in ks for b in (0, 1)]
+        ls = [e.costate(k, seed=b) for k in ks for b in (0, 1)]
+        e.close()
+        out[dead] = (J, g, xs, ls)
+    J, g, xs, ls = out["1"]
+    assert np.array_equal(J, out["0"][0]) and np.array_equal(g, out["0"][1])
+    for a, b in zip(xs + ls, out["0"][2] + out["0"][3]):
+        assert np.array_equal(a, b)
+        assert np.abs(a[1::2]).max() == 0.0  # the dead odd rows
+    for b in range(2):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, b)

@@ -102,6 +102,42 @@ int main(int argc, char** argv) {
   VARIANT(1, 1)
   VARIANT(2, 1)
   VARIANT(2, 2)
+  if (Kd % 16 == 0 && N % 2 == 0) {
+    auto f = [&]() { hipLaunchKernelGGL((k_bgemm_glds<0, 0>), grid, dim3(256), 0, 0, g); };
+    check("glds 3M", timeit(f, 5));
+    // op variants against their k_bgemm counterparts (A^H: square N = K only)
+    auto cmp = [&](const char* name, auto kref, auto kg) {
+      kref();
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(r0.data(), C1, perC * items * sizeof(cx<float>), hipMemcpyDeviceToHost));
+      const float t = timeit(kg, 5);
+      check(name, t);
+    };
+    if (Kd == N) {
+      cmp("glds 3M opA=H", [&]() { hipLaunchKernelGGL((k_bgemm<float, 1, 0, true, 1, 2>), grid, dim3(256), 0, 0, g); },
+          [&]() { hipLaunchKernelGGL((k_bgemm_glds<1, 0>), grid, dim3(256), 0, 0, g); });
+      cmp("glds 3M opB=H", [&]() { hipLaunchKernelGGL((k_bgemm<float, 0, 1, true, 1, 2>), grid, dim3(256), 0, 0, g); },
+          [&]() { hipLaunchKernelGGL((k_bgemm_glds<0, 1>), grid, dim3(256), 0, 0, g); });
+      cmp("glds 3M opA=H opB=H", [&]() { hipLaunchKernelGGL((k_bgemm<float, 1, 1, true, 1, 2>), grid, dim3(256), 0, 0, g); },
+          [&]() { hipLaunchKernelGGL((k_bgemm_glds<1, 1>), grid, dim3(256), 0, 0, g); });
+    }
+    // ragged M (rows past M clamped), items not a multiple of 8 (no XCD remap)
+    {
+      GemmArgs h = g;
+      h.M = N - 6;
+      h.nitems = items - 3;
+      h.tiles_m = (h.M + BG_BM - 1) / BG_BM;
+      h.tiles = h.tiles_m * ((N + BG_BN - 1) / BG_BN);
+      const dim3 gr2(h.nitems * h.tiles);
+      CK(hipMemset(C1, 0, perC * items * sizeof(cx<float>)));
+      hipLaunchKernelGGL((k_bgemm<float, 0, 0, true, 1, 2>), gr2, dim3(256), 0, 0, h);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(r0.data(), C1, perC * items * sizeof(cx<float>), hipMemcpyDeviceToHost));
+      CK(hipMemset(C1, 0, perC * items * sizeof(cx<float>)));
+      const float t = timeit([&]() { hipLaunchKernelGGL((k_bgemm_glds<0, 0>), gr2, dim3(256), 0, 0, h); }, 2);
+      check("glds ragged M", t);
+    }
+  }
   {
     auto f = [&]() { hipLaunchKernelGGL((k_bgemm<float, 1, 0, true, 1, 2>), grid, dim3(256), 0, 0, g); };
     const float t = timeit(f, 5);
