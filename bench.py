@@ -99,10 +99,12 @@ def blkseg_unit_flops(nb, order, P=None):
     the kernel's code (FMA = 2, add / mul = 1), phase 1 and phase 3 (the block exponential is formed in both: it is
     recomputed, not stored).  Blocks of 2 rows (the skew-Hermitian fast path): closed-form exponential (Â 16, the
     cos / sinc series of degree 19 in omega^2 and t^2 80, the rest 41: 137), 2x2 complex products 64 each, the
-    contraction 16 + 104 (order - 1) on skew X; blocks of 3 rows: the Taylor polynomial of degree P in the
+    contraction in the Pauli basis (sk2_contract_pauli) 20 / 53 / 75 at orders 1 / 2 / 3, 16 + 104 (order - 1) on
+    skew X at order 4 (sk2_contract); blocks of 3 rows: the Taylor polynomial of degree P in the
     Cayley-Hamilton basis (478 + 26 (P + 1)), 3x3 products 216 each, the contraction 86 + 518 (order - 1)."""
     if nb == 2:
-        form, prod, contr = 137.0, 64.0, 16.0 + 104.0 * (order - 1)
+        form, prod = 137.0, 64.0
+        contr = {1: 20.0, 2: 53.0, 3: 75.0}.get(order, 16.0 + 104.0 * (order - 1))
         return form + prod, form + 2 * prod + 6.0 + contr + 2.0
     form = 478.0 + 26.0 * ((P or 8) + 1)
     prod, contr = 216.0, 86.0 + 518.0 * (order - 1)
