@@ -94,16 +94,30 @@ def block_sizes(prob):
     return np.bincount(lab)
 
 
-def blkseg_unit_flops(nb, order, P=None):
+def blkseg_series_k(prob, u_all):
+    """Per seed, the closed-form series degree K the segmented eval picks for blocks of 2 rows (qoc_blkseg.hpp
+    blkseg_series_k): from ρ = ρ_0 + max_k Σ_j |u_jk| ρ_j with ρ_j the spectral half-width of the generator (the
+    engine adds a small backward-error margin to ρ_j, which can move a seed at a class edge)."""
+    import numpy as np
+    rad = []
+    for A in [prob.A0] + list(prob.A):
+        ev = np.linalg.eigvalsh(1j * np.asarray(A))
+        rad.append(0.5 * (ev.max() - ev.min()))
+    rho = rad[0] + np.max(np.einsum("bjk,j->bk", np.abs(u_all), np.asarray(rad[1:])), axis=1)
+    return np.where(rho <= 0.24, 5, np.where(rho <= 0.66, 7, 9))
+
+
+def blkseg_unit_flops(nb, order, P=None, K=9):
     """Executed fp64 flops of the segmented block eval (csrc/qoc_blkseg.hpp) per (slice, block) unit, counted from
     the kernel's code (FMA = 2, add / mul = 1), phase 1 and phase 3 (the block exponential is formed in both: it is
     recomputed, not stored).  Blocks of 2 rows (the skew-Hermitian fast path): closed-form exponential (Â 16, the
-    cos / sinc series of degree 19 in omega^2 and t^2 80, the rest 41: 137), 2x2 complex products 64 each, the
+    cos / sinc series of degree 2K + 1 in omega^2 and t^2 8 (K + 1): 80 at K = 9, the rest 41), 2x2 complex products
+    64 each, the
     contraction in the Pauli basis (sk2_contract_pauli) 20 / 53 / 75 at orders 1 / 2 / 3, 16 + 104 (order - 1) on
     skew X at order 4 (sk2_contract); blocks of 3 rows: the Taylor polynomial of degree P in the
     Cayley-Hamilton basis (478 + 26 (P + 1)), 3x3 products 216 each, the contraction 86 + 518 (order - 1)."""
     if nb == 2:
-        form, prod = 137.0, 64.0
+        form, prod = 57.0 + 8.0 * (K + 1), 64.0
         contr = {1: 20.0, 2: 53.0, 3: 75.0}.get(order, 16.0 + 104.0 * (order - 1))
         return form + prod, form + 2 * prod + 6.0 + contr + 2.0
     form = 478.0 + 26.0 * ((P or 8) + 1)
@@ -433,8 +447,14 @@ def main():
         nbk = int(bsz_s.max())
         nblk = len(bsz_s)
         p_avg = terms / K / max(B * Nt, 1)  # Taylor degree (blocks of 3 rows; the kernel counts Nt P 2^J per seed)
-        f1, f3 = blkseg_unit_flops(nbk, args.order, p_avg)
         units = B * Nt * nblk
+        if nbk == 2:  # the series degree per seed
+            ks = blkseg_series_k(prob, u_all)
+            fl = [blkseg_unit_flops(2, args.order, None, int(k)) for k in ks]
+            f1, f3 = float(np.mean([a for a, _ in fl])), float(np.mean([c for _, c in fl]))
+        else:
+            ks = None
+            f1, f3 = blkseg_unit_flops(nbk, args.order, p_avg)
         flops = units * (f1 + f3)
         hbm = B * Nt * nu * 8 * 4 + B * (8 + 2 * 2 * m * 16)
         t = per_step["k_chain_bwd"] / 1e3
@@ -444,7 +464,8 @@ def main():
             "achieved": ach, "unit": "TFLOP/s", "peak": peak, "frac": ach / peak,
             "executed_gflop_per_launch": flops / 1e9, "flops_per_unit": {"phase1": f1, "phase3": f3},
             "units_per_launch": units, "hbm_bytes_per_launch": hbm,
-            "hbm_gbs": hbm / 1e9 / t if t > 0 else 0.0, "taylor_degree": p_avg if nbk == 3 else None}}
+            "hbm_gbs": hbm / 1e9 / t if t > 0 else 0.0, "taylor_degree": p_avg if nbk == 3 else None,
+            "series_degree_k": ({str(int(k)): int(np.sum(ks == k)) for k in np.unique(ks)} if ks is not None else None)}}
         for k in ("k_expm", "k_chain_fwd", "k_grad"):
             kern[k] = {"ms_per_launch": per_launch[k], "launches_per_step": lps[k]}
         roof = {"kernel": "k_blkseg_eval", "bound": "valu", "achieved": ach, "peak": peak, "unit": "TFLOP/s",

@@ -66,7 +66,7 @@ __host__ __device__ inline size_t blkseg_off_red(int N, int m, int NB, int nblk,
   return blkseg_off_cf(N, m, NB, nblk, Nt, S) + (size_t)4 * m;
 }
 __host__ __device__ inline size_t blkseg_off_wred(int N, int m, int NB, int nblk, int Nt, int S) {
-  return blkseg_off_red(N, m, NB, nblk, Nt, S) + 24;
+  return blkseg_off_red(N, m, NB, nblk, Nt, S) + 32;  // red[0..23]: reductions, red[24..31]: wave progress
 }
 __host__ __device__ inline size_t blkseg_off_dJ(int N, int m, int NB, int nblk, int Nt, int S, int W, int RB) {
   return blkseg_off_wred(N, m, NB, nblk, Nt, S) + (size_t)128 * W * RB;
@@ -89,10 +89,12 @@ static __device__ unsigned long long g_segw[32];
   do {                                                                           \
     if (blockIdx.x == 7 && (threadIdx.x & 63) == 0) g_segw[slot] = (v);          \
   } while (0)
-static __device__ int g_seg_noturn;
+static __device__ int g_seg_noturn, g_seg_turnmode;
 #define SEG_TURNS (!g_seg_noturn)
+#define SEG_TURNMODE g_seg_turnmode
 #else
 #define SEG_TURNS true
+#define SEG_TURNMODE 1
 #define SEGW_SET(slot, v) \
   do {                    \
   } while (0)
@@ -131,6 +133,11 @@ struct BlksegTrig {
   double c[BLKSEG_KMAX + 1];  // (-1)^k / (2k)!
   double s[BLKSEG_KMAX + 1];  // (-1)^k / (2k+1)!
 };
+// The series degree K (terms up to x^(2K+1)) a seed needs: the first omitted term ρ^(2K+2) / (2K+2)! below 2^-53 for
+// every |x| <= ρ (both ω and |t| are bounded by the seed's largest ρ_k: the eigenvalues i(t ± ω) of a shifted block lie
+// within [-ρ, ρ]).  K = 5 up to ρ = 0.24, 7 up to 0.66, else 9 (covers θ_cap ≈ 0.98); the bounds leave margin
+// (exact limits 0.248 / 0.684 / 1.32).
+__host__ __device__ constexpr int blkseg_series_k(double rho) { return rho <= 0.24 ? 5 : rho <= 0.66 ? 7 : BLKSEG_KMAX; }
 constexpr BlksegTrig blkseg_trig() {
   BlksegTrig t{};
   double f = 1.0;  // 1 / n!
@@ -329,6 +336,7 @@ struct Sk2 {
 __device__ __forceinline__ Sk2 sk2_of(const double2 (&e)[4]) { return Sk2{e[0].y, e[3].y, e[1].x, e[1].y}; }
 
 // Â = Ã_0 + u_1 Ã_1 + u_2 Ã_2 (no halvings) and U = e^{μ_k} exp(Â) in the closed form of seg_form (ph = e^{μ_k})
+template <int K = BLKSEG_KMAX>
 __device__ __forceinline__ void sk2_form(const Sk2 (&g)[3], double2 ph, double2 u, Sk2& ah, double (&ur)[4],
                                          double (&ui)[4]) {
   constexpr BlksegTrig T = blkseg_trig();
@@ -340,7 +348,7 @@ __device__ __forceinline__ void sk2_form(const Sk2 (&g)[3], double2 ph, double2 
   const double w = fma(a, a, fma(ah.r, ah.r, ah.q * ah.q)), t2 = t * t;
   double cw = 0.0, sw = 0.0, ct = 0.0, st = 0.0;
 #pragma unroll
-  for (int k = BLKSEG_KMAX; k >= 0; --k) {
+  for (int k = K; k >= 0; --k) {
     cw = fma(cw, w, T.c[k]);
     sw = fma(sw, w, T.s[k]);
     ct = fma(ct, t2, T.c[k]);
@@ -491,6 +499,21 @@ __device__ __forceinline__ void seg_turn(int grp, int ngrp, int jj) {
   if ((grp + jj) % ngrp == 0) __builtin_amdgcn_s_setprio(1);
   else __builtin_amdgcn_s_setprio(0);
 }
+// SIMD partners by progress (QOC_PROBE builds: g_seg_turnmode 1): each wave posts its step count in LDS and runs the
+// next step at the higher issue priority when its partner (w ^ 4) is ahead (ties: the younger wave, which loses the
+// arbitration otherwise).  The partner's count is read one step early, so the LDS latency hides behind the step.
+struct SegProg {
+  int* prog;
+  int partner, other;
+  bool on, young;
+  __device__ __forceinline__ void step(int t) {
+    if (!on) return;
+    if (other > t || (other == t && young)) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+    prog[threadIdx.x >> 6] = t;
+    other = __builtin_amdgcn_readfirstlane(prog[partner]);
+  }
+};
 
 // One workgroup per seed (blockIdx.x), W = blockDim / 64 waves, UPW segments of nblk lanes per wave (lanes past
 // UPW nblk idle).  Built-in costs only (TRACE / ZCAL), no state penalty, no co-state source, unpacked states,
@@ -582,6 +605,7 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   }
   P = __builtin_amdgcn_readfirstlane(P);
   J = __builtin_amdgcn_readfirstlane(J);
+  if (tid < 8) reinterpret_cast<int*>(red + 24)[tid] = 0;  // wave progress (SegProg)
   if (J) {  // the records hold 2^-J u (exact scaling)
     for (int k = tid; k < Nt; k += nthr) {
       rec[4 * (size_t)k + 2] *= s0;
@@ -625,7 +649,13 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
 
   // SIMD partners (w, w + 4) alternate the issue priority (seg_turn); QOC_PROBE builds: g_seg_noturn turns it off
   const int grp = __builtin_amdgcn_readfirstlane(w >> 2), ngrp = (W + 3) >> 2;
-  const bool turns = ngrp > 1 && SEG_TURNS;
+  const bool turns = ngrp > 1 && SEG_TURNS && SEG_TURNMODE == 0;
+  SegProg sprog;
+  sprog.prog = reinterpret_cast<int*>(red + 24);
+  sprog.partner = __builtin_amdgcn_readfirstlane(w ^ 4);
+  sprog.on = ngrp > 1 && SEG_TURNS && SEG_TURNMODE == 1 && sprog.partner < W;
+  sprog.young = grp == 1;
+  sprog.other = 0;
   // ---- phase 1: the segment product P_s = U_{ke-1} .. U_{kb} ----
   double qr[E], qi[E];
 #pragma unroll
@@ -648,8 +678,9 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       gk[j] = sk2_of(e4);
     }
   }
-  auto p1_fast = [&](int jj, auto SEL_) {
+  auto p1_fast = [&](int jj, auto SEL_, auto K_) {
     constexpr bool SEL = decltype(SEL_)::value;
+    constexpr int KS = decltype(K_)::value;
     if constexpr (NB == 2) {
       double ur[2][4], ui[2][4];
       bool act[2];
@@ -659,7 +690,8 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
         act[v] = !SEL || (sact && jj + v < L && k < ke);
         const double* r = rec + 4 * (size_t)(act[v] ? k : 0);
         Sk2 ah;
-        sk2_form(gk, *reinterpret_cast<const double2*>(r), *reinterpret_cast<const double2*>(r + 2), ah, ur[v], ui[v]);
+        sk2_form<KS>(gk, *reinterpret_cast<const double2*>(r), *reinterpret_cast<const double2*>(r + 2), ah, ur[v],
+                     ui[v]);
       }
 #pragma unroll
       for (int v = 0; v < 2; ++v) {
@@ -673,15 +705,24 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       }
     }
   };
-  if (fast) {
+  // the fast path's series degree (uniform per seed: one loop instance per degree class)
+  const int ksel = __builtin_amdgcn_readfirstlane(blkseg_series_k(rmax * s0));
+  auto loop1 = [&](auto K_) {
     for (int jj = 0; jj < L; jj += 2) {
       if (turns) seg_turn(grp, ngrp, jj >> 1);
-      if (jj + 1 < Lf) p1_fast(jj, std::false_type());
-      else p1_fast(jj, std::true_type());
+      sprog.step(jj >> 1);
+      if (jj + 1 < Lf) p1_fast(jj, std::false_type(), K_);
+      else p1_fast(jj, std::true_type(), K_);
     }
+  };
+  if (fast) {
+    if (ksel == 5) loop1(std::integral_constant<int, 5>());
+    else if (ksel == 7) loop1(std::integral_constant<int, 7>());
+    else loop1(std::integral_constant<int, BLKSEG_KMAX>());
   } else {
     for (int jj = 0; jj < L; jj += NV1) {
       if (turns) seg_turn(grp, ngrp, jj / NV1);
+      sprog.step(jj / NV1);
       const double* rk[NV1];
       bool act[NV1];
 #pragma unroll
@@ -705,7 +746,7 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
     }
   }
 
-  if (turns) __builtin_amdgcn_s_setprio(0);
+  if (turns || sprog.on) __builtin_amdgcn_s_setprio(0);
   BK_T(t2);
   BK_ADD(1, t2 - t1);
   SEGW_SET(w, t2 - t0);
@@ -894,8 +935,9 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
     sk2_pauli2(Sk2{gk[1].d0 + mu1i, gk[1].d1 + mu1i, gk[1].r, gk[1].q}, pa1);
     sk2_pauli2(Sk2{gk[2].d0 + mu2i, gk[2].d1 + mu2i, gk[2].r, gk[2].q}, pa2);
   }
-  auto p3_fast = [&](int jj, auto SEL_) {
+  auto p3_fast = [&](int jj, auto SEL_, auto K_) {
     constexpr bool SEL = decltype(SEL_)::value;
+    constexpr int KS = decltype(K_)::value;
     if constexpr (NB == 2) {
       const int k = kb + jj;
       const bool act = !SEL || (sact && k < ke);
@@ -903,7 +945,7 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       const double2 u = *reinterpret_cast<const double2*>(r + 2);
       Sk2 ah;
       double ur[4], ui[4];
-      sk2_form(gk, *reinterpret_cast<const double2*>(r), u, ah, ur, ui);
+      sk2_form<KS>(gk, *reinterpret_cast<const double2*>(r), u, ah, ur, ui);
       // K_k = U_k^H G_{k+1}, G_k = K_k U_k
       double Kr[4], Ki[4], tr[4], ti[4];
       seg_mm<2, true, false>(ur, ui, Gr, Gi, Kr, Ki);
@@ -927,15 +969,22 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       reduce(jj, !SEL || act ? acc1 : 0.0, !SEL || act ? acc2 : 0.0);
     }
   };
-  if (fast) {
+  auto loop3 = [&](auto K_) {
     for (int jj = L - 1; jj >= 0; --jj) {
       if (turns) seg_turn(grp, ngrp, jj);
-      if (jj < Lf) p3_fast(jj, std::false_type());
-      else p3_fast(jj, std::true_type());
+      sprog.step(L + (L - 1 - jj));
+      if (jj < Lf) p3_fast(jj, std::false_type(), K_);
+      else p3_fast(jj, std::true_type(), K_);
     }
+  };
+  if (fast) {
+    if (ksel == 5) loop3(std::integral_constant<int, 5>());
+    else if (ksel == 7) loop3(std::integral_constant<int, 7>());
+    else loop3(std::integral_constant<int, BLKSEG_KMAX>());
   } else {
     for (int jj = L - 1; jj >= 0; --jj) {
       if (turns) seg_turn(grp, ngrp, jj);
+      sprog.step(L + (L - 1 - jj));
       const int k = kb + jj;
       const bool act = sact && k < ke;
       const double* rk[1] = {rec + 4 * (size_t)(act ? k : 0)};
@@ -977,7 +1026,7 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       reduce(jj, act ? acc1 : 0.0, act ? acc2 : 0.0);
     }
   }
-  if (turns) __builtin_amdgcn_s_setprio(0);
+  if (turns || sprog.on) __builtin_amdgcn_s_setprio(0);
   BK_T(t4);
   BK_ADD(3, t4 - t3);
   SEGW_SET(16 + w, t4 - t0);

@@ -291,3 +291,20 @@ def test_segmented_eval_best_pair_for_the_all_gather(built_lib, monkeypatch):
     J, _ = _eval_dev(e, u)
     assert e.allgather_best() == (J.min(), 1000 + int(np.argmin(J)))
     e.close()
+
+
+@pytest.mark.parametrize("amp", [1.0, 8.0, 14.0, 22.0])
+def test_segmented_series_degree_classes(built_lib, monkeypatch, amp):
+    """Blocks of 2 rows: the closed-form exponential's series degree is chosen per seed from its largest ρ_k (K = 5 /
+    7 / 9 for ρ <= 0.24 / 0.66 / θ_cap; beyond θ_cap the halving path).  The cavity's controls scaled by amp move ρ
+    through every class (ρ = 0.154 + 0.05 amp at |u| = 0.05 amp per control); each seed against the oracle."""
+    from qoc_amd import systems
+    p = systems.cavity_problem(N_cavity=10, Nt=40)
+    u = systems.cavity_controls(3, p.Nt, seed=91) * amp
+    e = _engine(p, 3, monkeypatch)
+    J, g = _eval_dev(e, u)
+    assert e.info()["backward"] == "segmented"
+    e.close()
+    for b in range(3):
+        J0, g0, _ = O.grape_eval(p.A0, p.A, u[b], p.x0, p.x_target, p.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, (amp, b))

@@ -12,8 +12,9 @@
 using namespace qoc;
 
 template <int NB, int WMAX = 8>
-void run(int B, int Nt, int nblk, int m, int W, int Scap, int noturn = 0) {
+void run(int B, int Nt, int nblk, int m, int W, int Scap, int noturn = 0, int turnmode = 1) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_seg_noturn), &noturn, sizeof(int));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_seg_turnmode), &turnmode, sizeof(int));
   const int nu = 2, N = NB * nblk;
   const size_t NN = (size_t)N * N;
   std::vector<cx<double>> A((nu + 1) * NN, cx<double>{0, 0});
@@ -90,7 +91,7 @@ void run(int B, int Nt, int nblk, int m, int W, int Scap, int noturn = 0) {
   (void)hipMemcpyFromSymbol(tc, HIP_SYMBOL(g_bk), sizeof(tc));
   printf("%s NB=%d B=%d Nt=%d W=%d S=%3d L=%3d lds=%6zu: %.4f ms (best of 5) | cycles per wave: prologue %6.0f  seg %6.0f"
          "  scan+cost %6.0f  backward %7.0f  epilogue %5.0f  total %7.0f  (per slice-step: seg %.0f, bwd %.0f)\n",
-         noturn ? "noturn" : "turns ", NB, B, Nt, W, sp.S, sp.L, lds, best, tc[0] / (double)W, tc[1] / (double)W, tc[2] / (double)W,
+         noturn ? "noturn" : turnmode ? "progr " : "turns ", NB, B, Nt, W, sp.S, sp.L, lds, best, tc[0] / (double)W, tc[1] / (double)W, tc[2] / (double)W,
          tc[3] / (double)W, tc[4] / (double)W, tc[5] / (double)W, tc[1] / (double)W / sp.L,
          tc[3] / (double)W / sp.L);
   unsigned long long sw[32];
@@ -110,12 +111,14 @@ int main(int argc, char** argv) {
   const int Nt = argc > 3 ? atoi(argv[3]) : (NB == 2 ? 1000 : 500);
   const int nblk = NB == 2 ? 20 : 3, m = NB == 2 ? 2 : 4;
   if (NB == 2) {
-    run<2, 8>(B, Nt, nblk, m, 8, 1 << 20);
+    run<2, 8>(B, Nt, nblk, m, 8, 1 << 20, 0, 1);
+    run<2, 8>(B, Nt, nblk, m, 8, 1 << 20, 0, 0);
     run<2, 8>(B, Nt, nblk, m, 8, 1 << 20, 1);
-    run<2, 8>(B, Nt, nblk, m, 4, 1 << 20);
+    run<2, 8>(B, Nt, nblk, m, 8, 1 << 20, 0, 1);
   } else {
     run<3, 8>(B, Nt, nblk, m, 4, 1 << 20);
-    run<3, 8>(B, Nt, nblk, m, 8, 1 << 20);
+    run<3, 8>(B, Nt, nblk, m, 8, 1 << 20, 0, 1);
+    run<3, 8>(B, Nt, nblk, m, 8, 1 << 20, 0, 0);
   }
   return 0;
 }
