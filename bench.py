@@ -94,6 +94,23 @@ def block_sizes(prob):
     return np.bincount(lab)
 
 
+def live_block_sizes(prob):
+    """Row counts of the invariant blocks that carry state: x0 or X_target nonzero on some row of the block.  The
+    concurrent eval gives blocks of 5..16 rows without state no chain waves (qoc_run_blk.hip blk_live; the tunable
+    bus' odd-parity block at m = 1), so their work is not counted."""
+    import numpy as np
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import connected_components
+    M = np.abs(np.asarray(prob.A0)) > 0
+    for a in prob.A:
+        M |= np.abs(np.asarray(a)) > 0
+    nb, lab = connected_components(csr_matrix(M), directed=False)
+    rows = (np.abs(np.asarray(prob.x0)).sum(axis=1) > 0) | (np.abs(np.asarray(prob.x_target)).sum(axis=1) > 0)
+    sizes = np.bincount(lab, minlength=nb)
+    live = np.bincount(lab, weights=rows.astype(np.float64), minlength=nb) > 0
+    return sizes[live] if live.any() else sizes
+
+
 def blkseg_series_k(prob, u_all):
     """Per seed, the closed-form series degree K the segmented eval picks for blocks of 2 rows (qoc_blkseg.hpp
     blkseg_series_k): from ρ = ρ_0 + max_k Σ_j |u_jk| ρ_j with ρ_j the spectral half-width of the generator (the
@@ -524,7 +541,9 @@ def main():
         if rot_blocks:
             # algorithmic block work: one n_b x n_b complex matvec per block and column (8 n_b^2 m flops), not the
             # executed MFMA flops of the 16-row padded waves (8 v_mfma_f64_4x4x4_4b of 4 x 128 flops per column pair)
-            mv_flops = 8.0 * float(np.sum(block_sizes(prob).astype(np.float64) ** 2)) * m
+            dead_skip = dual and os.environ.get("QOC_BLK_DEAD", "1") != "0"
+            mv_flops = 8.0 * float(np.sum((live_block_sizes(prob) if dead_skip else block_sizes(prob))
+                                          .astype(np.float64) ** 2)) * m
         models = {
             "k_expm": ("mfma", 0.0, "TFLOP/s", peak),  # k_tchain_prep: (P, s, e^mu) per slice, no flops counted
             "k_grad": ("mfma", grad_flops(N, m, nu, Nt, B, args.order,

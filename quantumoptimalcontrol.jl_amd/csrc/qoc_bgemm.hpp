@@ -721,6 +721,66 @@ __global__ __launch_bounds__(256) void k_form_norm(int N, int nu, long long unit
   }
 }
 
+// The same A_k and norm for N <= 64 RQ with the generators held in registers: workgroup (column block, slice group),
+// wave w owns column 4 cb + w and keeps its RQ rows of A_0..A_nu in registers (lane rows r = lane + 64 q), then forms
+// A_k for the group's slices in turn.  One workgroup per slice (k_form_norm) re-read the generators for every slice
+// (3 x 512 KB per slice at N = 256, nu = 2: the kernel ran at ~2.6 TB/s of mostly generator reads); here they are
+// read once per workgroup and the launch writes A_k at the store rate.  Column sums complete in the wave (the norm
+// is the max column sum), one atomic max per workgroup.
+constexpr int FN2_SG = 16;  // slices per workgroup
+template <typename T, int RQ>
+__global__ __launch_bounds__(256) void k_form_norm2(int N, int nu, long long unit0, int cnt,
+                                                    const cx<T>* __restrict__ Agen, const double* __restrict__ u,
+                                                    cx<T>* __restrict__ out, unsigned long long* __restrict__ nmax) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = 4 * blockIdx.x + wave, it0 = blockIdx.y * FN2_SG;
+  const size_t NN = (size_t)N * N;
+  const bool cok = c < N;
+  cx<T> g[3][RQ];
+  bool ok[RQ];
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    const int r = lane + 64 * q;
+    ok[q] = cok && r < N;
+    const size_t e = ok[q] ? r + (size_t)N * c : 0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) g[j][q] = j <= nu ? Agen[(size_t)j * NN + e] : cx<T>{T(0), T(0)};
+  }
+  double best = 0.0;
+  const int nit = min(FN2_SG, cnt - it0);
+  for (int i = 0; i < nit; ++i) {
+    const int it = it0 + i;
+    const long long unit = unit0 + it;
+    const T u1 = nu > 0 ? (T)u[unit * nu] : T(0), u2 = nu > 1 ? (T)u[unit * nu + 1] : T(0);
+    cx<T>* ob = out + (size_t)it * NN + (size_t)N * c;
+    double sum = 0.0;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      cx<T> a;
+      a.r = g[0][q].r + u1 * g[1][q].r + u2 * g[2][q].r;
+      a.i = g[0][q].i + u1 * g[1][q].i + u2 * g[2][q].i;
+      if (ok[q]) {
+        ob[lane + 64 * q] = a;
+        if (nmax) sum += sqrt((double)a.r * a.r + (double)a.i * a.i);
+      }
+    }
+    if (nmax) {
+      for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+      best = fmax(best, sum);
+    }
+  }
+  if (nmax) {
+    __shared__ double wb[4];
+    if (lane == 0) wb[wave] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const double bw = fmax(fmax(wb[0], wb[1]), fmax(wb[2], wb[3]));
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(bw);
+      if (bits > __hip_atomic_load(nmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(nmax, bits);
+    }
+  }
+}
+
 // Guard-state penalty over all stored states: J[b] = mu * sum_{k, masked} |x_k|^2 (one WG per seed).
 template <typename T>
 __global__ void k_penalty_sum(int N, int m, int Nt, const cx<T>* __restrict__ X, const unsigned char* __restrict__ pmask,

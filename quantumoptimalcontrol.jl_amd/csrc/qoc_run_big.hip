@@ -403,6 +403,25 @@ int expm_gemm_chunk(qoc_ctx* c, int N, int cnt, void* ws, size_t ws_items, doubl
   return QOC_OK;
 }
 
+// A_k = A_0 + Σ_j u_jk A_j for units [u0, u0 + cnt) -> out, and (nmax set) the chunk's max 1-norm: the generators in
+// registers per (column block, slice group) for nu <= 2 and N <= 512 (k_form_norm2), else one workgroup per slice
+template <typename T>
+static int form_norm(qoc_ctx* c, long long u0, int cnt, cx<T>* out, unsigned long long* nmax) {
+  const int N = c->N;
+  const dim3 g2((unsigned)((N + 3) / 4), (unsigned)((cnt + FN2_SG - 1) / FN2_SG));
+  if (c->nu <= 2 && N <= 256)
+    hipLaunchKernelGGL((k_form_norm2<T, 4>), g2, dim3(256), 0, c->stream, N, c->nu, u0, cnt, (const cx<T>*)c->d_A,
+                       (const double*)c->d_u, out, nmax);
+  else if (c->nu <= 2 && N <= 512)
+    hipLaunchKernelGGL((k_form_norm2<T, 8>), g2, dim3(256), 0, c->stream, N, c->nu, u0, cnt, (const cx<T>*)c->d_A,
+                       (const double*)c->d_u, out, nmax);
+  else
+    hipLaunchKernelGGL((k_form_norm<T>), dim3(cnt), dim3(256), 0, c->stream, N, c->nu, u0, (const cx<T>*)c->d_A,
+                       (const double*)c->d_u, out, nmax);
+  HIPCHK(c, hipGetLastError());
+  return QOC_OK;
+}
+
 // exp(A_k) for units [u0, u0+cnt) -> d_U (forms A_k from the generators, chunk max norm, then the GEMM expm)
 template <typename T>
 int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
@@ -410,9 +429,7 @@ int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
   const size_t NN = (size_t)N * N, esz = c->esz;
   cx<T>* a0 = (cx<T>*)c->d_ws;
   HIPCHK(c, hipMemsetAsync(c->d_red, 0, 2 * sizeof(double), c->stream));
-  hipLaunchKernelGGL((k_form_norm<T>), dim3(cnt), dim3(256), 0, c->stream, N, c->nu, u0, (const cx<T>*)c->d_A,
-                     (const double*)c->d_u, a0, (unsigned long long*)c->d_red);
-  HIPCHK(c, hipGetLastError());
+  if (int r = form_norm<T>(c, u0, cnt, a0, (unsigned long long*)c->d_red)) return r;
   if (c->big_rho_ok) {
     SpecBound sb{};
     for (int j = 0; j <= c->nu && j < 9; ++j) sb.rho[j] = c->big_rho[j];
@@ -538,9 +555,7 @@ int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
   if (const char* s = getenv("QOC_GRAD_SANDWICH")) sandwich = o == 3 && atoi(s) != 0;
   for (long long u0 = 0; u0 < units; u0 += c->chunk) {
     const int cnt = (int)std::min<long long>(c->chunk, units - u0);
-    hipLaunchKernelGGL((k_form_norm<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)c->d_A,
-                       (const double*)c->d_u, (cx<T>*)((char*)c->d_ws + offX * esz), (unsigned long long*)nullptr);
-    HIPCHK(c, hipGetLastError());
+    if (int r = form_norm<T>(c, u0, cnt, (cx<T>*)((char*)c->d_ws + offX * esz), nullptr)) return r;
     const Opd Xk = mk_opd(c->d_ws, offX, esz, (long long)NN);
     if (sandwich) {  // workspace: X, then three N x N blocks per item (G / R, T1 / M', S) — 4 NN of the 8 NN
       const size_t offG = C * NN, offT = 2 * C * NN, offS = 3 * C * NN;
