@@ -329,6 +329,7 @@ int forward(qoc_ctx* c) {
   return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
 }
 int backward(qoc_ctx* c, int order, double* d_dJdu) {
+  if (c->cost_kind == QOC_COST_EXTERNAL || c->src_on) c->dead_dirty = true;  // λ may be nonzero on dead rows
   if (c->X_lazy) {  // after a segmented eval: the backward paths read x_k
     const int r = blku_states(c);
     if (r) return r;
@@ -700,6 +701,7 @@ int qoc_set_x0(qoc_ctx* c, const double* x0, int per_seed) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->h_x0.assign(x0, x0 + 2 * Nmu * cnt);
   c->x0_per_seed = per_seed ? 1 : 0;
+  c->dead_dirty = true;  // rows live under the previous x0 may hold nonzero states
   c->have_x0 = true;
   c->have_prop = false;
   return QOC_OK;
@@ -725,6 +727,7 @@ int qoc_set_cost(qoc_ctx* c, int kind, const double* X_target, double n) {
   }
   c->cost_kind = kind;
   c->cost_n = n;
+  c->dead_dirty = true;  // rows live under the previous target may hold nonzero co-states
   c->have_cost = true;
   c->have_prop = false;
   return QOC_OK;
@@ -780,6 +783,7 @@ int qoc_set_compression(qoc_ctx* c, const int* rows1, int nr1, const int* cols1,
   HIPCHK(c, hipSetDevice(c->dev));
   if (int r0 = blk_materialize(c)) return r0;  // x_k / λ_k kept lazily are in the current layout
   HIPCHK(c, hipStreamSynchronize(c->stream));  // queued kernels may still read the packed buffers
+  c->dead_dirty = true;
   const int N = c->N, mu_ = c->m_user;
   std::vector<unsigned char> rsec;
   std::vector<int> cols[2], pos[2];

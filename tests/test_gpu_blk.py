@@ -404,7 +404,12 @@ def test_blocks_mfma_dead_blocks_skipped(built_lib, monkeypatch):
         _eval(e, u, True)  # the odd block live: nonzero odd rows in every buffer
         e.set_x0(prob.x0)
         e.set_cost_trace(prob.x_target, prob.n)
-        J, g = _eval(e, u, True)
+        _eval(e, u, True)  # odd rows zeroed
+        e.set_x0(prob.x0 + x_odd)  # both blocks live: nonzero odd rows again
+        _eval(e, u, True)
+        e.set_x0(prob.x0)
+        _eval(e, u, True)  # the same dead rows as two evals ago: must be zeroed again
+        J, g = _eval(e, u, True)  # and this one may skip the zeroing
         assert e.info()["chain_kernel"] == "blocks_mfma"
         xs = [e.state(k, seed=b) for k in ks for b in (0, 1)]
         ls = [e.costate(k, seed=b) for k in ks for b in (0, 1)]
