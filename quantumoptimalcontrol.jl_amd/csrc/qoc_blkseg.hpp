@@ -913,8 +913,10 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   // entries in a fixed order
   const int nrl = sp.UPW * max(nu, 1);  // reducing lanes per step
   const int rq = l / nrl, rrem = l - rq * nrl, ro = rrem / max(nu, 1), rj = rrem - ro * max(nu, 1);
+  int rslot = 0;  // (L - 1 - jj) % RB as a counter (jj runs down from L - 1 by one)
   auto reduce = [&](int jj, double acc1, double acc2) {
-    const int r = (L - 1 - jj) % RB;
+    const int r = rslot;
+    rslot = r == RB - 1 ? 0 : r + 1;
     *reinterpret_cast<double2*>(wr + 128 * r + 2 * l) = make_double2(acc1, acc2);
     if (r == RB - 1 || jj == 0) {  // uniform
       wave_lds_sync();

@@ -69,7 +69,7 @@ int big_gemm(qoc_ctx* c, int opa, int opb, GemmArgs g, int mode = 0) {
   }
   // fp32 products with K % 16 == 0 and even M, Ncol: the LDS-DMA staged kernel (QOC_BGEMM_GLDS=0 keeps k_bgemm)
   static const bool glds_env = !(getenv("QOC_BGEMM_GLDS") && atoi(getenv("QOC_BGEMM_GLDS")) == 0);
-  const bool glds = std::is_same<T, float>::value && mode == 0 && glds_env && g.K % 16 == 0 && g.M % 2 == 0 &&
+  const bool glds = std::is_same<T, float>::value && mode == 0 && glds_env && g.K >= 16 && g.K % 16 == 0 && g.M % 2 == 0 &&
                     g.Ncol % 2 == 0 && g.M >= 2 && g.Ncol >= 2;
   if (glds) {
     if (opa == 0 && opb == 0) hipLaunchKernelGGL((k_bgemm_glds<0, 0>), grid, blk, 0, c->stream, g);
