@@ -815,24 +815,25 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
     if (sp.coef2) sp.coef2[(size_t)b * 2 * m + tid] = cf[tid];
   }
   if (tid == 0) {
-    g.J[b] = red[16];
+    // J is the one value other workgroups read in this launch (publish): stored write-through at agent scope (sc1),
+    // so the hand-off needs no release fence (no L2 write-back of everything this XCD holds dirty)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(g.J + b),
+                       (unsigned long long)__double_as_longlong(red[16]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (sp.J2) sp.J2[b] = red[16];
   }
   // J is published after the cost: before the barrier that precedes G_0 when no waves share a SIMD within the
   // workgroup (early: all waves wait for the fences together), else after the last barrier before phase 3, so that
   // only wave 0 (one of the fast waves, seg_turn) waits for them.  The last workgroup to publish finds the best
-  // (J, seed) of the launch (k_argmin_seed's order: NaN never wins, ties go to the lower seed).  The hand-off follows
-  // the agent-scope release / acquire recipe (MI355X_MICROARCH.md, inter-workgroup visibility): store, vmcnt(0),
-  // release fence, vmcnt(0), counter add; the last adder acquires and then reads every J with plain loads.
+  // (J, seed) of the launch (k_argmin_seed's order: NaN never wins, ties go to the lower seed).  The hand-off is the
+  // write-through form of the guide's counter recipe (cdna_hip_programming.md, split-K combine / Guideline 16 R1):
+  // J stored sc1, vmcnt(0), relaxed agent counter add; the last adder acquires and then reads every J.
   const bool early = W <= 4;
   auto publish = [&]() {
     if (w != 0 || !sp.done) return;
     unsigned int prev = 0;
     if (l == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      prev = atomicAdd(sp.done, 1u);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 J store has reached memory
+      prev = __hip_atomic_fetch_add(sp.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     prev = __shfl(prev, 0);
     if (prev == gridDim.x - 1) {
