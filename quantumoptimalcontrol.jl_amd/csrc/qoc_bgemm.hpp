@@ -415,7 +415,7 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm(GemmArgs g) {
 // Fragment reads are ds_read_b64 (one complex): lane (i = l%16, kq = l/16) at MFMA step t reads (row 16x + i,
 // k = 4t + kq).  The 32 lanes of one LDS cycle then cover all 64 banks once in both layouts.
 // Requirements (bgemm_glds_ok): T = float, K % 16 == 0, M and Ncol even (a 16-byte piece is two elements).
-constexpr int BGG_STAGES = 3, BGG_STAGE_FLOATS = 2 * 64 * 16 * 2;  // A + B, complex fp32
+constexpr int BGG_STAGE_FLOATS = 2 * 64 * 16 * 2;  // A + B, complex fp32
 template <bool KR>
 __device__ __forceinline__ int bgg_off(int r, int k) {  // byte offset of (r, k) in an operand image
   return KR ? k * 512 + (((r >> 4) ^ (k & 1)) << 7) + ((r & 15) << 3)
@@ -444,8 +444,13 @@ __device__ __forceinline__ void bgg_dma(const void* src, unsigned lds_base) {
                : "memory");
 }
 
-template <int OPA, int OPB>
+// NS LDS stages: 2 (the default: slab s + 1 in flight while s is multiplied, 32 KB, four workgroups per CU) or 3
+// (s + 2 in flight, 48 KB, three per CU).  Microbench (profiles/bgemm_bench_r05g.txt): 2 stages 1.360 vs 1.389 ms
+// at 1260 items, 0.131 vs 0.134 ms at 128 (the chain GEMMs' size).
+template <int OPA, int OPB, int NS = 2>
 __global__ __launch_bounds__(BG_THREADS) void k_bgemm_glds(GemmArgs g) {
+  static_assert(NS == 2 || NS == 3, "two or three stages");
+  constexpr int BGG_STAGES = NS;
   using MFT = MF<float>;
   using v4 = typename MFT::v4;
   constexpr bool KRA = OPA == 0, KRB = OPB == 1;  // layouts of the A and B images
@@ -499,12 +504,12 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm_glds(GemmArgs g) {
   const int li = lane & 15, kq = lane >> 4;
   // fragment byte offsets in an image at step t = 0 (step t adds 4t to k: KR +2048 B, RK via the slot XOR)
   issue(0);
-  if (nslab > 1) issue(1);
-  if (nslab > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  if (NS == 3 && nslab > 1) issue(1);
+  if (NS == 3 && nslab > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   for (int s = 0; s < nslab; ++s) {
-    if (s + 2 < nslab) issue(s + 2);
+    if (s + NS - 1 < nslab) issue(s + NS - 1);
     const char* cur = reinterpret_cast<const char*>(lds + (s % BGG_STAGES) * BGG_STAGE_FLOATS);
     const char* curB = cur + 8192;
 #pragma unroll
@@ -534,7 +539,7 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgemm_glds(GemmArgs g) {
     }
     // slab s + 1 landed (this wave's pieces; slab s + 2's stay in flight), every read of slab s done, then the
     // barrier: after it slab s + 1 is readable and slab s's buffer may be refilled (by slab s + 3)
-    if (s + 2 < nslab) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    if (NS == 3 && s + 2 < nslab) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }

@@ -105,6 +105,8 @@ int main(int argc, char** argv) {
   if (Kd % 16 == 0 && N % 2 == 0) {
     auto f = [&]() { hipLaunchKernelGGL((k_bgemm_glds<0, 0>), grid, dim3(256), 0, 0, g); };
     check("glds 3M", timeit(f, 5));
+    auto f2 = [&]() { hipLaunchKernelGGL((k_bgemm_glds<0, 0, 2>), grid, dim3(256), 0, 0, g); };
+    check("glds 3M 2 stages", timeit(f2, 5));
     // op variants against their k_bgemm counterparts (A^H: square N = K only)
     auto cmp = [&](const char* name, auto kref, auto kg) {
       kref();
