@@ -867,6 +867,69 @@ __global__ __launch_bounds__(256) void k_gen_contract(int N, int nu, long long u
   }
 }
 
+// The same contraction with the generators in registers (k_form_norm2's layout): workgroup (block of 4 columns, group
+// of GC2_SG slices), wave w owns column 4 cb + w and keeps its rows of A_1..A_nu (nu <= 2) in registers, so only M'
+// streams (k_gen_contract re-read 2 x 512 KB of generators per slice at N = 256).  Each workgroup writes its column
+// block's partial sums part[(it * ncb + cb) * nu + j] (the four columns added in a fixed order); k_gen_reduce adds the
+// ncb partials of every (slice, j) in a fixed order: the result does not depend on scheduling.
+constexpr int GC2_SG = 16;
+template <typename T, int RQ>
+__global__ __launch_bounds__(256) void k_gen_contract2(int N, int nu, int cnt, const cx<T>* __restrict__ Agen,
+                                                       const cx<T>* __restrict__ Mp, double* __restrict__ part) {
+  __shared__ double wsum[4][GC2_SG][2];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int cb = blockIdx.x, c = 4 * cb + wave, it0 = blockIdx.y * GC2_SG, ncb = gridDim.x;
+  const size_t NN = (size_t)N * N;
+  const bool cok = c < N;
+  cx<T> a[2][RQ];
+  bool ok[RQ];
+#pragma unroll
+  for (int q = 0; q < RQ; ++q) {
+    const int r = lane + 64 * q;
+    ok[q] = cok && r < N;
+    const size_t e = ok[q] ? r + (size_t)N * c : 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) a[j][q] = j < nu && ok[q] ? Agen[(size_t)(j + 1) * NN + e] : cx<T>{T(0), T(0)};
+  }
+  const int nit = min(GC2_SG, cnt - it0);
+  for (int i = 0; i < nit; ++i) {
+    const cx<T>* Mb = Mp + (size_t)(it0 + i) * NN + (size_t)N * (cok ? c : 0);
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      if (ok[q]) {
+        const cx<T> mv = Mb[lane + 64 * q];
+        s0 += (double)a[0][q].r * mv.r + (double)a[0][q].i * mv.i;
+        s1 += (double)a[1][q].r * mv.r + (double)a[1][q].i * mv.i;
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      s0 += __shfl_xor(s0, off);
+      s1 += __shfl_xor(s1, off);
+    }
+    if (lane == 0) {
+      wsum[wave][i][0] = s0;
+      wsum[wave][i][1] = s1;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < nit * nu; e += blockDim.x) {
+    const int i = e / nu, j = e - i * nu;
+    const double v = ((wsum[0][i][j] + wsum[1][i][j]) + wsum[2][i][j]) + wsum[3][i][j];
+    part[((size_t)(it0 + i) * ncb + cb) * nu + j] = v;
+  }
+}
+static __global__ void k_gen_reduce(int cnt, int nu, int ncb, long long unit0, const double* __restrict__ part,
+                                    double* __restrict__ dJdu) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < cnt * nu; e += gridDim.x * blockDim.x) {
+    const int it = e / nu, j = e - it * nu;
+    const double* p = part + (size_t)it * ncb * nu + j;
+    double s = 0.0;
+    for (int q = 0; q < ncb; ++q) s += p[(size_t)q * nu];
+    dJdu[(unit0 + it) * nu + j] = s;
+  }
+}
+
 // Auxiliary generator layouts for the GEMM-shaped gradient of the LDS-resident path:
 //   AH  = [A0^H | A1^H | ... | A_nu^H]   (N x (nu+1) N, column blocks)
 //   Cst = [A1; A2; ...; A_nu]            (nu N x N, row blocks)

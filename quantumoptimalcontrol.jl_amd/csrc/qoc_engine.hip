@@ -511,6 +511,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->d_wrow) hipFree(c->d_wrow);
   if (c->d_wrow_live) hipFree(c->d_wrow_live);
   if (c->d_dead_rows) hipFree(c->d_dead_rows);
+  if (c->d_gc_part) hipFree(c->d_gc_part);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L, c->d_u_lam, c->d_coef_lam, c->d_blkU, c->d_J_scr, c->d_coef_scr,
                   c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_pws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec, c->d_sink, c->d_blkrec};
   for (void* p : ptrs)

@@ -178,6 +178,8 @@ struct qoc_ctx {
   std::vector<int> h_wrow;       // host copy (blocks of 5..16 rows: one wave per block)
   // blocks of 5..16 rows with x_0 and X_target zero on their rows (blk_live): the waves of the others, the dead rows
   std::vector<int> h_wrow_live, h_dead_rows;
+  double* d_gc_part = nullptr;   // large-N gradient: per (slice, column block) partial traces (k_gen_contract2)
+  size_t gc_part_bytes = 0;
   // the dead rows known to hold zeros in the six state-shaped buffers (blk_zero_dead), and those buffers: a backward
   // with an external λ_N or a co-state source (the only writers of nonzero values into rows whose x0 and target are
   // zero) sets dead_dirty

@@ -422,6 +422,44 @@ static int form_norm(qoc_ctx* c, long long u0, int cnt, cx<T>* out, unsigned lon
   return QOC_OK;
 }
 
+// dJdu[unit, j] = Re <A_j, M'_unit> for units [u0, u0 + cnt): the generators in registers per column block
+// (k_gen_contract2 + k_gen_reduce, nu <= 2, N <= 512), else one workgroup per slice (k_gen_contract)
+template <typename T>
+static int gen_contract(qoc_ctx* c, long long u0, int cnt, const cx<T>* Mp, double* d_dJdu) {
+  const int N = c->N, nu = c->nu;
+  if (nu >= 1 && nu <= 2 && N <= 512) {
+    const int ncb = (N + 3) / 4;
+    const size_t need = (size_t)c->chunk * ncb * nu * sizeof(double);
+    if (need > c->gc_part_bytes) {
+      if (c->d_gc_part) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(c->d_gc_part));
+        c->dev_bytes -= c->gc_part_bytes;
+      }
+      c->d_gc_part = nullptr;
+      c->gc_part_bytes = 0;
+      HIPCHK(c, hipMalloc((void**)&c->d_gc_part, need));
+      c->gc_part_bytes = need;
+      c->dev_bytes += need;
+    }
+    const dim3 g2((unsigned)ncb, (unsigned)((cnt + GC2_SG - 1) / GC2_SG));
+    if (N <= 256)
+      hipLaunchKernelGGL((k_gen_contract2<T, 4>), g2, dim3(256), 0, c->stream, N, nu, cnt, (const cx<T>*)c->d_A, Mp,
+                         c->d_gc_part);
+    else
+      hipLaunchKernelGGL((k_gen_contract2<T, 8>), g2, dim3(256), 0, c->stream, N, nu, cnt, (const cx<T>*)c->d_A, Mp,
+                         c->d_gc_part);
+    HIPCHK(c, hipGetLastError());
+    const unsigned rb = (unsigned)std::min<long long>(((long long)cnt * nu + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_gen_reduce, dim3(rb), dim3(256), 0, c->stream, cnt, nu, ncb, u0, c->d_gc_part, d_dJdu);
+  } else {
+    hipLaunchKernelGGL((k_gen_contract<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)c->d_A, Mp,
+                       d_dJdu);
+  }
+  HIPCHK(c, hipGetLastError());
+  return QOC_OK;
+}
+
 // exp(A_k) for units [u0, u0+cnt) -> d_U (forms A_k from the generators, chunk max norm, then the GEMM expm)
 template <typename T>
 int big_expm_chunk(qoc_ctx* c, long long u0, int cnt) {
@@ -579,9 +617,7 @@ int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
       g = gemm_args(N, N, N, cnt);  // M' = X^H S / 6 + R   (over T1)
       g.A = Xk; g.B = Sk; g.C1 = Tk; g.alpha1 = 1.0 / 6; g.nY = 1; g.Y[0] = Gk; g.w1[0] = 1.0;
       if ((r = big_gemm<T>(c, 1, 0, g))) return r;
-      hipLaunchKernelGGL((k_gen_contract<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)c->d_A,
-                         (const cx<T>*)((char*)c->d_ws + offT * esz), d_dJdu);
-      HIPCHK(c, hipGetLastError());
+      if ((r = gen_contract<T>(c, u0, cnt, (const cx<T>*)((char*)c->d_ws + offT * esz), d_dJdu))) return r;
       continue;
     }
     auto Pa = [&](int a) { return mk_opd(c->d_ws, offP + a * Nm, esz, (long long)(o * Nm)); };
@@ -642,9 +678,7 @@ int big_backward(qoc_ctx* c, int order, double* d_dJdu) {
     g.B = mk_opd(c->d_ws, offP, esz, (long long)(o * Nm));
     g.C1 = mk_opd(c->d_ws, offM, esz, (long long)NN);
     if ((r = big_gemm<T>(c, 0, 1, g))) return r;  // M' = W P^H
-    hipLaunchKernelGGL((k_gen_contract<T>), dim3(cnt), dim3(256), 0, c->stream, N, nu, u0, (const cx<T>*)c->d_A,
-                       (const cx<T>*)((char*)c->d_ws + offM * esz), d_dJdu);
-    HIPCHK(c, hipGetLastError());
+    if ((r = gen_contract<T>(c, u0, cnt, (const cx<T>*)((char*)c->d_ws + offM * esz), d_dJdu))) return r;
   }
   mark_end(c, mk);
   return QOC_OK;
