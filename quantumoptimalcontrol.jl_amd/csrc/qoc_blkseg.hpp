@@ -9,7 +9,8 @@
 //            largest ρ_k (one pair for the whole seed: every lane runs the same term loop);
 //   phase 1  the segment product P_s = U_{sL+L-1} .. U_{sL} on the block (U_k formed per slice, the k_blku_* block
 //            exponential: Taylor polynomial in the Cayley-Hamilton basis with the phase folded in);
-//   phase 2  inclusive prefix products Q_s = P_s .. P_0 over the segments (Hillis-Steele, log2 S rounds through LDS),
+//   phase 2  inclusive prefix products Q_s = P_s .. P_0 over the segments (a Hillis-Steele scan inside each wave,
+//            then the earlier waves' totals; one workgroup barrier),
 //            x_N = Q_{S-1} x_0, the terminal cost J and λ_N (chain_costs, src/penalty_fcns.jl:15-42), then
 //            G_N = Σ_c x_N,c λ_N,c^H per block;
 //   phase 3  every segment backwards from its end, with G_k = Σ_c x_k,c λ_k,c^H instead of the states: because U_k is
@@ -750,14 +751,20 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   BK_T(t2);
   BK_ADD(1, t2 - t1);
   SEGW_SET(w, t2 - t0);
-  // ---- phase 2: prefix products Q_s = P_s .. P_0 (Hillis-Steele over the segments) ----
+  // ---- phase 2: prefix products Q_s = P_s .. P_0 ----
+  // Two levels: a Hillis-Steele scan over the UPW segments of each wave through its own slot rows (one wave's LDS
+  // accesses are ordered, so the rounds need wave syncs only), then every lane multiplies by the product of the
+  // earlier waves' totals T_v (the local Q of their last segments), read after the one workgroup barrier.  Lanes of
+  // segments past S hold the identity (phase 1 left their P = I), so the last wave's scan needs no masks.  14 of the
+  // 15 barriers of the plain scan over 84 segments (zz) are gone.
   auto slot_at = [&](int ss, int e) -> double2& { return slot[((size_t)ss * E + e) * nblk + beta]; };
+  const int UPW = sp.UPW, uw0 = lact ? uw : 0;
   if (sact)
 #pragma unroll
     for (int e = 0; e < E; ++e) slot_at(s, e) = make_double2(qr[e], qi[e]);
-  lds_barrier();
-  for (int d = 1; d < S; d <<= 1) {
-    const bool take = sact && s >= d;
+  wave_lds_sync();
+  for (int d = 1; d < UPW; d <<= 1) {
+    const bool take = sact && uw0 >= d;
     double tr[E], ti[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -765,7 +772,7 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       tr[e] = v.x;
       ti[e] = v.y;
     }
-    lds_barrier();
+    wave_lds_sync();
     if (take) {
       double cr[E], ci[E];
       seg_mm<NB, false, false>(qr, qi, tr, ti, cr, ci);
@@ -776,7 +783,39 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
         slot_at(s, e) = make_double2(cr[e], ci[e]);
       }
     }
-    lds_barrier();
+    wave_lds_sync();
+  }
+  lds_barrier();
+  if (sact && w > 0) {  // E_w = T_{w-1} .. T_0, then Q_s = Q_s(local) E_w
+    double er[E], ei[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const double2 v = slot_at(UPW - 1, e);
+      er[e] = v.x;
+      ei[e] = v.y;
+    }
+    for (int v = 1; v < w; ++v) {
+      double tr[E], ti[E], cr[E], ci[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const double2 x = slot_at(v * UPW + UPW - 1, e);
+        tr[e] = x.x;
+        ti[e] = x.y;
+      }
+      seg_mm<NB, false, false>(tr, ti, er, ei, cr, ci);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        er[e] = cr[e];
+        ei[e] = ci[e];
+      }
+    }
+    double cr[E], ci[E];
+    seg_mm<NB, false, false>(qr, qi, er, ei, cr, ci);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      qr[e] = cr[e];
+      qi[e] = ci[e];
+    }
   }
   // x_N = Q_{S-1} x_0 on each block (the last segment's lanes), in place in xN
   const bool last = sact && s == S - 1;
