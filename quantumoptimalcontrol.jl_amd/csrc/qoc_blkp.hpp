@@ -1,0 +1,494 @@
+// qoc_blkp.hpp — stored propagators for invariant blocks of 5..16 rows (the tunable bus' parity blocks).
+//
+// The reference forms every slice propagator U_k = exp(A_k) (src/gradient_computations.jl:17-24) and then runs one
+// matvec per slice in the chains (:27-29 forward, :52-58 backward).  The MFMA block waves (k_blkrot_*, qoc_blk.hpp)
+// instead apply the slice polynomial to the state inside the serial chain: on the tunable bus (‖A_k‖ ≈ 30) that is
+// ~42 Chebyshev terms per slice, one wave per (seed, block, direction) and one wave per SIMD, so the serial term
+// latency bounds the whole eval.  Here the exponentials leave the chain:
+//   * k_blkp_exp: U_k on each live 16-row wave block (BlkArgs::wrow, -1 padding), one wave per (seed, slice, block),
+//     every matrix in registers in the v_mfma_f64_16x16x4 D layout ("C layout": lane j + 16 g, register e holds
+//     M[g + 4e][j]).  A product L R takes L as its transpose's C layout (register e of L^T is the A operand of k-step e)
+//     and R as is (register e is the B operand), so a product needs no data movement; transposes go through a
+//     wave-private LDS tile.  Complex products run as three real ones (12 MFMAs).  U_k = e^{μ_k} T_{4r}(2^-s Ã_k)^{2^s}
+//     with the degree-4r Taylor polynomial by Paterson-Stockmeyer (X², X³, X⁴, then r - 1 Horner products in X⁴)
+//     and s squarings; (r, s) per unit minimise the r + 2 + s products subject to Σ_{k>4r} ρ^k / k! <= 2^-53 at
+//     ρ = 2^-s ρ̂, ρ̂ = min(‖Ã_k‖_F, sqrt(‖Ã_k‖_1 ‖Ã_k‖_∞)) >= ‖Ã_k‖_2.
+//   * k_blkp_dual: the forward chain x_{k+1} = U_k x_k and the μ recurrence μ_k = U_k^H μ_{k+1} (μ_N = X_target,
+//     λ_k = coef ⊙ μ_k) from the stored propagators, one wave per (seed, block, column, direction): lane i + 16 q
+//     takes row i and the column quarter 4q..4q+3 of U_k, the quarters are summed with permlane swaps and the new
+//     state goes to the next slice through a 16-entry LDS row.  Beside the chain each wave forms Ã_k's block rows and
+//     writes the order-3 gradient's captures D1 = Ã_k v, D2 = Ã_k D1 (v = x_k forward, Ã_k^H and μ_{k+1} backward),
+//     which k_grad_rr_c contracts with scale 1 and κ = 1 (qoc_grad_rr.hpp).
+#pragma once
+#include "qoc_blk.hpp"
+
+namespace qoc {
+
+constexpr int BLKP_WG = 256;  // formation: waves of one workgroup
+constexpr int BLKP_RMIN = 2, BLKP_RMAX = 8;
+constexpr int BLKP_TP = 16 * 17;  // transpose tile per wave (double2, padded rows)
+// θ_{4r}: the largest ρ with Σ_{k>4r} ρ^k / k! <= 2^-53 (r = 1..8)
+__constant__ double kBlkpTheta[9] = {0.0,
+                                     0.0016783942982781048,
+                                     0.06993278480782539,
+                                     0.33521368782861477,
+                                     0.8246031916386087,
+                                     1.504147322395163,
+                                     2.3324673844012387,
+                                     3.2752135590741402,
+                                     4.3063288801167054};
+__constant__ double kBlkpInvFact[33] = {1.0,
+                                        1.0,
+                                        0.5,
+                                        1.6666666666666666e-01,
+                                        4.1666666666666664e-02,
+                                        8.3333333333333332e-03,
+                                        1.3888888888888889e-03,
+                                        1.9841269841269841e-04,
+                                        2.4801587301587302e-05,
+                                        2.7557319223985893e-06,
+                                        2.7557319223985888e-07,
+                                        2.5052108385441720e-08,
+                                        2.0876756987868100e-09,
+                                        1.6059043836821613e-10,
+                                        1.1470745597729725e-11,
+                                        7.6471637318198164e-13,
+                                        4.7794773323873853e-14,
+                                        2.8114572543455206e-15,
+                                        1.5619206968586225e-16,
+                                        8.2206352466243295e-18,
+                                        4.1103176233121648e-19,
+                                        1.9572941063391263e-20,
+                                        8.8967913924505741e-22,
+                                        3.8681701706306835e-23,
+                                        1.6117375710961184e-24,
+                                        6.4469502843844736e-26,
+                                        2.4795962632247972e-27,
+                                        9.1836898637955460e-29,
+                                        3.2798892370698380e-30,
+                                        1.1309962886447717e-31,
+                                        3.7699876288159054e-33,
+                                        1.2161250415535179e-34,
+                                        3.8003907548547434e-36};
+
+struct BlkpArgs {
+  int N, nu, nwb;
+  long long units;             // B Nt nwb: unit = (b Nt + k) nwb + β
+  const int* wrow;             // nwb x 16 rows of the live wave blocks
+  const cx<double>* At;        // (nu+1) N x N shifted generators Ã_j, column-major
+  const double* u;             // B x Nt x nu
+  double mur[3], mui[3];       // μ_k = μ_0 + Σ_j u_j μ_j
+  double2* U;                  // units x 256: U_k of the block, row-major (U[i][j] at 16 i + j), e^{μ_k} included
+  unsigned long long* prods;   // TERM_SLOTS counters: executed 16 x 16 complex products (nullptr: not counted)
+};
+
+using BV4 = MF<double>::v4;
+struct CMat {  // 16 x 16 complex in the C layout
+  BV4 r, i;
+};
+
+// Z = L R (+ I0): Lt = C layout of L^T, R and I0 in C layout; 3 real products (Zr = T1 - T2, Zi = T3 - T1 - T2 with
+// T3 = (Lr + Li)(Rr + Ri)), the addend folded into the accumulators' start values
+template <bool INIT>
+__device__ __forceinline__ CMat cm_mul(const CMat& Lt, const CMat& R, const CMat& I0) {
+  BV4 t1 = INIT ? I0.r : BV4{0.0, 0.0, 0.0, 0.0};
+  BV4 t2 = BV4{0.0, 0.0, 0.0, 0.0};
+  BV4 t3 = INIT ? I0.r + I0.i : BV4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const double ar = Lt.r[e], ai = Lt.i[e], br = R.r[e], bi = R.i[e];
+    t1 = MF<double>::mma(ar, br, t1);
+    t2 = MF<double>::mma(ai, bi, t2);
+    t3 = MF<double>::mma(ar + ai, br + bi, t3);
+  }
+  return CMat{t1 - t2, t3 - t1 - t2};
+}
+
+// C layout of X^T through the wave's LDS tile (row pitch 17: the transposed reads of a 16-lane row fall on distinct
+// banks).  Within a wave LDS operations complete in order; the fences keep the compiler from moving them.
+__device__ __forceinline__ CMat cm_transpose(const CMat& X, double2* tile) {
+  const int l = threadIdx.x & 63, j = l & 15, g = l >> 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) tile[(g + 4 * e) * 17 + j] = make_double2(X.r[e], X.i[e]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  CMat T;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const double2 v = tile[j * 17 + g + 4 * e];
+    T.r[e] = v.x;
+    T.i[e] = v.y;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return T;
+}
+
+// v + v(lane ^ 16) and v + v(lane ^ 32) with the gfx950 row swaps (VALU, no LDS crossbar): each swap returns the two
+// registers with the partner rows exchanged, so the two results hold v and its partner in some order
+__device__ __forceinline__ double2 swap16_f64(double v) {
+  const unsigned long long q = (unsigned long long)__double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)q, (unsigned)q, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(q >> 32), (unsigned)(q >> 32), false, false);
+  return make_double2(__longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0])),
+                      __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1])));
+}
+__device__ __forceinline__ double2 swap32_f64(double v) {
+  const unsigned long long q = (unsigned long long)__double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)q, (unsigned)q, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(q >> 32), (unsigned)(q >> 32), false, false);
+  return make_double2(__longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0])),
+                      __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1])));
+}
+__device__ __forceinline__ double xsum_rows(double v) {  // over the four lanes i, i + 16, i + 32, i + 48
+  double2 a = swap16_f64(v);
+  v = a.x + a.y;
+  a = swap32_f64(v);
+  return a.x + a.y;
+}
+__device__ __forceinline__ double xmax_rows(double v) {
+  double2 a = swap16_f64(v);
+  v = fmax(a.x, a.y);
+  a = swap32_f64(v);
+  return fmax(a.x, a.y);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long q = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)q, CTRL, 0xf, 0xf, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(q >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// over the 16 lanes of a DPP row (quad xor 1, quad xor 2, half mirror, mirror); the result in every lane
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+  return v + dpp_f64<0x140>(v);
+}
+__device__ __forceinline__ double row_max16(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));
+  v = fmax(v, dpp_f64<0x4E>(v));
+  v = fmax(v, dpp_f64<0x141>(v));
+  return fmax(v, dpp_f64<0x140>(v));
+}
+__device__ __forceinline__ double uniform_f64(double v) {
+  const unsigned long long q = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)q);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(q >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// B_i = c_{4i} I + c_{4i+1} X + c_{4i+2} X² + c_{4i+3} X³ (c_k = 1/k!)
+__device__ __forceinline__ CMat blkp_horner_b(int i, const CMat& X, const CMat& X2, const CMat& X3) {
+  const int l = threadIdx.x & 63, j = l & 15, g = l >> 4;
+  const double c0 = kBlkpInvFact[4 * i], c1 = kBlkpInvFact[4 * i + 1], c2 = kBlkpInvFact[4 * i + 2],
+               c3 = kBlkpInvFact[4 * i + 3];
+  CMat B;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    B.r[e] = fma(c3, X3.r[e], fma(c2, X2.r[e], fma(c1, X.r[e], g + 4 * e == j ? c0 : 0.0)));
+    B.i[e] = fma(c3, X3.i[e], fma(c2, X2.i[e], c1 * X.i[e]));
+  }
+  return B;
+}
+
+// One workgroup of BLKP_WG / 64 waves walks the units wave by wave (persistent grid).  LDS: the generators' blocks in
+// C layout ([β][j][e][lane] double2) and one transpose tile per wave.
+template <int NU>
+__global__ __launch_bounds__(BLKP_WG) void k_blkp_exp(const BlkpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double2* gen = reinterpret_cast<double2*>(smem);
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
+  const int N = a.N, nwb = a.nwb;
+  const size_t NN = (size_t)N * N;
+  const int ngen = nwb * 3 * 256;
+  for (int e = tid; e < ngen; e += blockDim.x) {
+    const int ll = e & 63, ee = (e >> 6) & 3, jb = e >> 8, jg = jb % 3, bb = jb / 3;
+    const int* rb = a.wrow + 16 * bb;
+    const int row = rb[(ll >> 4) + 4 * ee], col = rb[ll & 15];
+    double2 v = make_double2(0.0, 0.0);
+    if (row >= 0 && col >= 0 && jg <= NU) {
+      const cx<double> z = a.At[jg * NN + row + (size_t)N * col];
+      v = make_double2(z.r, z.i);
+    }
+    gen[e] = v;
+  }
+  double2* tile = gen + ngen + w * BLKP_TP;
+  __syncthreads();
+  const int WPG = BLKP_WG / 64;
+  const long long TW = (long long)gridDim.x * WPG;
+  unsigned long long prods = 0;
+  for (long long unit = (long long)blockIdx.x * WPG + w; unit < a.units; unit += TW) {
+    const long long bk = unit / nwb;
+    const int beta = (int)(unit - bk * nwb);
+    const double u1 = a.u[bk * NU], u2 = NU > 1 ? a.u[bk * NU + (NU > 1 ? 1 : 0)] : 0.0;
+    const double2* gb = gen + (size_t)beta * 768;
+    CMat X;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const double2 g0 = gb[64 * e + l], g1 = gb[256 + 64 * e + l];
+      const double2 g2 = NU > 1 ? gb[512 + 64 * e + l] : make_double2(0.0, 0.0);
+      X.r[e] = fma(u2, g2.x, fma(u1, g1.x, g0.x));
+      X.i[e] = fma(u2, g2.y, fma(u1, g1.y, g0.y));
+    }
+    // ρ̂ >= ‖X‖_2: Frobenius, and sqrt(‖X‖_1 ‖X‖_∞) with |re| + |im| >= |z| in the sums
+    double f2 = 0.0, cs = 0.0, rmax = 0.0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const double az = fabs(X.r[e]) + fabs(X.i[e]);
+      f2 = fma(X.r[e], X.r[e], fma(X.i[e], X.i[e], f2));
+      cs += az;
+      rmax = fmax(rmax, row_sum16(az));  // row g + 4e
+    }
+    const double n1 = row_max16(xsum_rows(cs)), ninf = xmax_rows(rmax);
+    f2 = xsum_rows(row_sum16(f2));
+    const double rho = uniform_f64(fmin(sqrt(f2), sqrt(n1 * ninf)));
+    int r = BLKP_RMAX, s = 0, best = 1 << 30;
+    for (int rr = BLKP_RMIN; rr <= BLKP_RMAX; ++rr) {
+      int ss = 0;
+      for (double t = rho; t > kBlkpTheta[rr] && ss < 64; t *= 0.5) ++ss;
+      if (rr + 2 + ss < best) {
+        best = rr + 2 + ss;
+        r = rr;
+        s = ss;
+      }
+    }
+    const double sc = ldexp(1.0, -s);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      X.r[e] *= sc;
+      X.i[e] *= sc;
+    }
+    const CMat Xt = cm_transpose(X, tile);
+    const CMat X2 = cm_mul<false>(Xt, X, X);
+    const CMat X3 = cm_mul<false>(Xt, X2, X);
+    CMat R;
+    CMat X4t;
+    {
+      const CMat X4 = cm_mul<false>(Xt, X3, X);
+      X4t = cm_transpose(X4, tile);
+      R = blkp_horner_b(r - 1, X, X2, X3);
+      const double cm = kBlkpInvFact[4 * r];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        R.r[e] = fma(cm, X4.r[e], R.r[e]);
+        R.i[e] = fma(cm, X4.i[e], R.i[e]);
+      }
+    }
+    for (int i = r - 2; i >= 0; --i) R = cm_mul<true>(X4t, R, blkp_horner_b(i, X, X2, X3));
+    for (int t = 0; t < s; ++t) {
+      const CMat Rt = cm_transpose(R, tile);
+      R = cm_mul<false>(Rt, R, R);
+    }
+    const double mr = fma(u2, a.mur[2], fma(u1, a.mur[1], a.mur[0]));
+    const double mi = fma(u2, a.mui[2], fma(u1, a.mui[1], a.mui[0]));
+    const double em = exp(mr);
+    double sn, cn;
+    sincos(mi, &sn, &cn);
+    const double pr = em * cn, pi = em * sn;
+    double2* Ub = a.U + unit * 256;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      Ub[(g + 4 * e) * 16 + j] = make_double2(fma(pr, R.r[e], -pi * R.i[e]), fma(pr, R.i[e], pi * R.r[e]));
+    prods += (unsigned long long)(r + 2 + s);
+  }
+  if (a.prods && l == 0 && prods) atomicAdd(a.prods + (blockIdx.x & (TERM_SLOTS - 1)), prods);
+}
+
+// ---- chains from the stored propagators ----
+// LDS: [32 doubles reduction scratch][x_N: 2 N m doubles][per wave: 16 + 16 double2 exchange rows]
+__host__ __device__ inline size_t blkp_chain_lds(int N, int m, int waves) {
+  return (size_t)(32 + 2 * N * m) * sizeof(double) + (size_t)waves * 32 * sizeof(double2);
+}
+constexpr int BLKP_PD = 4;  // slices of propagator rows in flight per lane
+
+// this lane's view of wave block β: rows rb[i] (i = lane & 15) and the quarter rows / columns rb[4q + t]
+struct BlkpLane {
+  int i, q, beta, c, row;
+  int qr[4];
+  __device__ __forceinline__ void setup(const BlkArgs& bk) {
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    i = l & 15;
+    q = l >> 4;
+    beta = w % bk.nwb;
+    c = w / bk.nwb;
+    const int* rb = bk.wrow + 16 * beta;
+    row = rb[i];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) qr[t] = rb[4 * q + t];
+  }
+};
+
+// Σ_t a_t b_t (complex) over this lane's quarter, two partial sums per part
+__device__ __forceinline__ double2 blkp_dot4(const double (&ar)[4], const double (&ai)[4], const double (&br)[4],
+                                             const double (&bi)[4]) {
+  const double r0 = fma(ar[0], br[0], fma(-ai[0], bi[0], ar[1] * br[1] - ai[1] * bi[1]));
+  const double r1 = fma(ar[2], br[2], fma(-ai[2], bi[2], ar[3] * br[3] - ai[3] * bi[3]));
+  const double i0 = fma(ar[0], bi[0], fma(ai[0], br[0], fma(ar[1], bi[1], ai[1] * br[1])));
+  const double i1 = fma(ar[2], bi[2], fma(ai[2], br[2], fma(ar[3], bi[3], ai[3] * br[3])));
+  return make_double2(r0 + r1, i0 + i1);
+}
+
+// FWD: x_{k+1} = U_k x_k, lane (i, q) holds U_k[i][4q + t]; else μ_k = U_k^H μ_{k+1}, lane (i, q) holds U_k[4q + t][i]
+// (conjugated on use).  Generators: Ã_j[row][qr[t]] forward, conj(Ã_j[qr[t]][row]) = (Ã_j^H)[row][qr[t]] backward.
+template <int NU, bool FWD>
+__device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkArgs& bk, const double2* __restrict__ U,
+                                                const int b) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* red = reinterpret_cast<double*>(smem);
+  double* xN = red + 32;
+  const int N = g.N, m = g.m, Nt = g.Nt, nwb = bk.nwb, tid = threadIdx.x, nthr = blockDim.x;
+  const size_t Nm = (size_t)N * m, NN = (size_t)N * N;
+  BlkpLane ln;
+  ln.setup(bk);
+  double2* xs = reinterpret_cast<double2*>(xN + 2 * Nm) + (tid >> 6) * 32;
+  double2* fs = xs + 16;
+  const bool act = ln.row >= 0;
+  // the block rows of Ã_0..Ã_NU at this lane's quarter
+  double gr[NU + 1][4], gi[NU + 1][4];
+  const cx<double>* At = (const cx<double>*)g.At;
+#pragma unroll
+  for (int jg = 0; jg <= NU; ++jg)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int cq = ln.qr[t];
+      const bool ok = act && cq >= 0;
+      const size_t o = FWD ? (size_t)max(ln.row, 0) + (size_t)N * max(cq, 0) : (size_t)max(cq, 0) + (size_t)N * max(ln.row, 0);
+      const cx<double> v = ok ? At[jg * NN + o] : cx<double>{0.0, 0.0};
+      gr[jg][t] = v.r;
+      gi[jg][t] = FWD ? v.i : -v.i;
+    }
+  double* const sink = tchain_sink(g);
+  double2* const sink2 = reinterpret_cast<double2*>(sink);
+  const size_t oe = (size_t)ln.c * N + max(ln.row, 0);  // element offset (complex) of this lane's row
+  double2* const Sb = reinterpret_cast<double2*>((cx<double>*)(FWD ? g.X : g.L) + (size_t)b * (Nt + 1) * Nm);
+  double2* const C1 = reinterpret_cast<double2*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm);
+  double2* const C2 = reinterpret_cast<double2*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm);
+  const bool own = act && ln.q == 0;
+  if (FWD)
+    for (size_t e = tid; e < 2 * Nm; e += nthr) xN[e] = 0.0;
+  double2 v0 = make_double2(0.0, 0.0);
+  if (act) {
+    cx<double> v;
+    if (FWD) v = ((const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0))[oe];
+    else v = ((const cx<double>*)g.Xt)[oe];
+    v0 = make_double2(v.r, v.i);
+  }
+  xs[ln.i] = v0;
+  __syncthreads();
+  *(own ? Sb + (FWD ? 0 : (size_t)Nt * Nm) + oe : sink2) = v0;
+  double xr[4], xi[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const double2 v = xs[4 * ln.q + t];
+    xr[t] = v.x;
+    xi[t] = v.y;
+  }
+  // propagator entries and u of the slices in flight (vector loads: the per-lane zero keeps u off the scalar cache)
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  const double* ub = g.u + (size_t)b * Nt * g.nu;
+  const double2* Ubase = U + (size_t)b * Nt * nwb * 256 + (size_t)ln.beta * 256 +
+                         (FWD ? (size_t)ln.i * 16 + 4 * ln.q : (size_t)(4 * ln.q) * 16 + ln.i) + z;
+  const size_t ustep = (size_t)nwb * 256;
+  double2 pu[BLKP_PD][4];
+  double pc[BLKP_PD][2];
+  auto issue = [&](int slot, int j) __attribute__((always_inline)) {
+    const int k = FWD ? min(j, Nt - 1) : max(Nt - 1 - j, 0);
+    const double2* p = Ubase + (size_t)k * ustep;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) pu[slot][t] = p[FWD ? t : 16 * t];
+    pc[slot][0] = ub[(size_t)k * g.nu + z];
+    pc[slot][1] = NU > 1 ? ub[(size_t)k * g.nu + (NU > 1 ? 1 : 0) + z] : 0.0;
+  };
+#pragma unroll
+  for (int p = 0; p < BLKP_PD; ++p) issue(p, p);
+  for (int j0 = 0; j0 < Nt; j0 += BLKP_PD) {
+#pragma unroll
+    for (int p = 0; p < BLKP_PD; ++p) {
+      const int j = j0 + p;
+      if (j >= Nt) break;
+      const int k = FWD ? j : Nt - 1 - j;
+      double ur[4], ui[4], ar[4], ai[4];
+      const double u1 = pc[p][0], u2 = pc[p][1];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        ur[t] = pu[p][t].x;
+        ui[t] = FWD ? pu[p][t].y : -pu[p][t].y;
+        ar[t] = fma(u1, gr[1][t], gr[0][t]);
+        ai[t] = fma(u1, gi[1][t], gi[0][t]);
+        if constexpr (NU > 1) {
+          ar[t] = fma(u2, gr[NU > 1 ? 2 : 0][t], ar[t]);
+          ai[t] = fma(u2, gi[NU > 1 ? 2 : 0][t], ai[t]);
+        }
+      }
+      issue(p, j + BLKP_PD);
+      // the loads stay here, BLKP_PD slices ahead of their use (the scheduler would sink them towards the stores)
+      __builtin_amdgcn_sched_barrier(0);
+      double2 y = blkp_dot4(ur, ui, xr, xi);
+      double2 f1 = blkp_dot4(ar, ai, xr, xi);
+      y.x = xsum_rows(y.x);
+      y.y = xsum_rows(y.y);
+      f1.x = xsum_rows(f1.x);
+      f1.y = xsum_rows(f1.y);
+      xs[ln.i] = y;
+      fs[ln.i] = f1;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double fr[4], fi[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const double2 v = xs[4 * ln.q + t], f = fs[4 * ln.q + t];
+        xr[t] = v.x;
+        xi[t] = v.y;
+        fr[t] = f.x;
+        fi[t] = f.y;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double2 f2 = blkp_dot4(ar, ai, fr, fi);
+      f2.x = xsum_rows(f2.x);
+      f2.y = xsum_rows(f2.y);
+      // branch-free stores (lanes without an element write the sink): the pointers are opaque, so no exec branch
+      // (global address space: a generic pointer would store through flat_*, which the waitcnt pass cannot count)
+      using G2 = __attribute__((address_space(1))) double2;
+      G2* p0 = (G2*)(own ? Sb + (size_t)(FWD ? k + 1 : k) * Nm + oe : sink2);
+      G2* p1 = (G2*)(own ? C1 + (size_t)k * Nm + oe : sink2 + 1);
+      G2* p2 = (G2*)(own ? C2 + (size_t)k * Nm + oe : sink2 + 2);
+      asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2));
+      *p0 = y;
+      *p1 = f1;
+      *p2 = f2;
+    }
+  }
+  if (FWD) {
+    if (own) {  // x_N: the exchange row holds the last slice's result
+      const double2 v = xs[ln.i];
+      xN[2 * oe] = v.x;
+      xN[2 * oe + 1] = v.y;
+    }
+    __syncthreads();
+    chain_costs<double>(N, m, (const cx<double>*)g.Xt, [&](int o) { return cx<double>{xN[2 * o], xN[2 * o + 1]}; },
+                        g.cost_kind, g.n_norm, 0.0, red, g.J + b, g.coef + (size_t)b * 2 * m, g.sc);
+  }
+}
+
+// forward chain and μ recurrence of every seed in one launch of 2B workgroups (seed-direction interleave as
+// k_blkrot_dual), nwb m waves each
+template <int NU>
+__global__ __launch_bounds__(512) void k_blkp_dual(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk,
+                                                   const double2* __restrict__ U) {
+  const int i = blockIdx.x, B = gridDim.x >> 1;
+  const bool by8 = (B & 7) == 0;
+  const int dir = by8 ? (i >> 3) & 1 : i & 1;
+  const int seed = by8 ? ((i >> 4) << 3) | (i & 7) : i >> 1;
+  if (dir == 0) blkp_chain_body<NU, true>(gf, bk, U, seed);
+  else blkp_chain_body<NU, false>(gb, bk, U, seed);
+}
+
+}  // namespace qoc

@@ -1316,9 +1316,10 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[5] = c->big ? c->expm_alg : c->expm_run;  // the large-N pipeline keeps its own (Taylor / Padé) choice
   info[6] = c->chain_mode == 1 && c->cheb && tchain_mf(c) ? 1 : 0;  // Taylor-action chains: Chebyshev terms
   info[7] = c->m;  // state columns the kernels run on (< the caller's m when compress_states packing is on)
-  info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 / 3 / 4 concurrent μ recurrence, 5 fused block gradient, 6 segmented block eval
+  info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 / 3 / 4 concurrent μ recurrence, 5 fused block gradient, 6 segmented block eval, 7 stored propagators of blocks of 5..16 rows
   info[9] = c->fwd_captured ? 1 : 0;
-  info[10] = blk_active(c) ? (blku_on(c) ? 5 : blk_rot(c) ? 4 : 3) : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
+  // 6: the last eval ran the stored-propagator chains of blocks of 5..16 rows (propagate / grape_sensitivity: 4)
+  info[10] = blk_active(c) ? (blku_on(c) ? 5 : blkp_on(c) && c->last_eval_mode == 7 ? 6 : blk_rot(c) ? 4 : 3) : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
   return QOC_OK;
 }
 

@@ -411,7 +411,7 @@ struct GradCapArgs {
   const void* F2;
   const void* G1;            // backward captures D1, D2 at slice k
   const void* G2;
-  const double* steps;       // TStep records, 4 doubles each (scale at [3])
+  const double* steps;       // TStep records, 4 doubles each (scale at [3]); nullptr: scale 1 (qoc_blkp.hpp)
   double mur[3], mui[3];     // shifts μ_j: μ_k = μ_0 + Σ_j u_jk μ_j
   double kappa;              // 2 Chebyshev, 1 Taylor
   const cx<double>* coef;    // μ mode: λ_N coefficients (B x 2m, chain_costs); nullptr: L holds λ
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(256, 2) void k_grad_rr_c(const GradCapArgs a) {
       sj[j] = 0.0;
       s2[j] = 0.0;
     }
-    const double r = 1.0 / a.steps[4 * g.unit + 3], kr2 = a.kappa * r * r;
+    const double r = a.steps ? 1.0 / a.steps[4 * g.unit + 3] : 1.0, kr2 = a.kappa * r * r;
     const bool scl = a.coef != nullptr;
     cx<double> f0 = {1.0, 0.0}, f1 = {1.0, 0.0};
     if (scl) {

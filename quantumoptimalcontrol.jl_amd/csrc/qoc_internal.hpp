@@ -135,6 +135,7 @@ struct qoc_ctx {
   bool cheb_ok = false;          // generators skew-Hermitian with imaginary shifts: Chebyshev applies
   bool cheb = false;             // Chebyshev terms (k_tchain_prep_cheb) instead of Taylor (QOC_TCHAIN_POLY=taylor)
   bool cheb_ran = false;         // what the last forward pass used (the backward pass reuses its steps)
+  bool steps_stale = false;      // the last eval formed its propagators without step records (blkp): re-prep first
   double* d_tcoef = nullptr;     // B x Nt x TCHEB_STRIDE Chebyshev coefficients (allocated on first use)
   long long props_since_reset = 0;  // forward passes since the last Padé-histogram reset (chain mode 1)
   // Captured products (register-resident MFMA chains, order-3 fused gradient): the chains write their first two
@@ -276,7 +277,9 @@ hipError_t launch_gen_aux(qoc_ctx* c);
 template <typename T>
 int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode = 0);
 // k_grad_rr_c: the order-3 contraction from the chains' captures (mu_mode: L holds μ, λ = coef ⊙ μ)
-int grad_rr_cap(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode);
+// unit_scale: the captures are D1 = Ã_k v, D2 = Ã_k² v (stored-propagator chains, qoc_blkp.hpp), not the step
+// records' scaled products
+int grad_rr_cap(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode, bool unit_scale = false);
 
 // ---- qoc_run_ode.hip ----
 template <typename T>
@@ -314,6 +317,7 @@ int blk_detect(qoc_ctx* c);
 bool blk_active(const qoc_ctx* c);
 bool blk_rot(const qoc_ctx* c);
 bool blku_on(const qoc_ctx* c);
+bool blkp_on(const qoc_ctx* c);  // blocks of 5..16 rows: the concurrent eval on stored propagators (qoc_blkp.hpp)
 int blku_costates(qoc_ctx* c);  // qoc_get_costates after the fused block backward
 int blk_forward(qoc_ctx* c);
 int blk_backward(qoc_ctx* c, int order, double* d_dJdu);

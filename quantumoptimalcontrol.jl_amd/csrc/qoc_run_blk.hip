@@ -4,6 +4,7 @@
 #include <numeric>
 
 #include "qoc_blk.hpp"
+#include "qoc_blkp.hpp"
 #include "qoc_blkseg.hpp"
 #include "qoc_blku.hpp"
 #include "qoc_internal.hpp"
@@ -460,6 +461,9 @@ static int blk_grad(qoc_ctx* c, int order, bool mu_mode, double* d_dJdu) {
 // block gradient for orders 1..4; the exact (Fréchet) gradient runs its own dense kernel on the same λ.
 int blk_backward(qoc_ctx* c, int order, double* d_dJdu) {
   if (blku_on(c)) return blku_backward(c, order, d_dJdu);
+  if (c->steps_stale) {  // the last forward was the stored-propagator eval (blkp): this u's step records first
+    if (int r0 = tchain_prep(c)) return r0;
+  }
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
   const size_t lds = blk_lds_of(c);
@@ -490,6 +494,92 @@ bool blk_concurrent_ok(const qoc_ctx* c, int order) {
          (c->cost_kind == QOC_COST_TRACE || c->cost_kind == QOC_COST_ZCAL) && c->mu == 0.0 && !c->src_on;
 }
 
+// ---- stored propagators for blocks of 5..16 rows (qoc_blkp.hpp) ------------------------------------------------------
+// The concurrent eval on the MFMA block waves' systems (the tunable bus): U_k per (seed, slice, live block) on MFMA,
+// then the one-matvec chains with the gradient's captures, then k_grad_rr_c (scale 1, κ = 1).  QOC_BLKP=0 keeps the
+// Chebyshev-action chains (k_blkrot_dual).
+bool blkp_on(const qoc_ctx* c) {
+  if (!blk_active(c) || !blk_big(c) || c->nu < 1 || c->nu > 2) return false;
+  const char* env = getenv("QOC_BLKP");
+  return !(env && atoi(env) == 0);
+}
+
+static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
+  TChainArgs gf = tchain_args(c);
+  TChainArgs gb = tchain_args(c);
+  gb.mu_mode = 1;
+  const size_t bufN = (size_t)c->N * ((size_t)c->B * (c->Nt + 1) * c->m);
+  gf.cap1 = c->d_pws;
+  gf.cap2 = (cx<double>*)c->d_pws + bufN;
+  gb.cap1 = c->d_gws;
+  gb.cap2 = (cx<double>*)c->d_gws + bufN;
+  int r;
+  if (bk.nwb != c->nwb) {
+    if ((r = blk_zero_dead(c, {c->d_X, c->d_L, (void*)gf.cap1, (void*)gf.cap2, (void*)gb.cap1, (void*)gb.cap2})))
+      return r;
+  }
+  const long long units = (long long)c->B * c->Nt * bk.nwb;
+  const size_t ubytes = (size_t)units * 256 * sizeof(double2);
+  if (c->blkU_bytes < ubytes) {
+    if (c->d_blkU) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipFree(c->d_blkU));
+      c->d_blkU = nullptr;
+      c->dev_bytes -= c->blkU_bytes;
+      c->blkU_bytes = 0;
+    }
+    HIPCHK(c, hipMalloc((void**)&c->d_blkU, ubytes));
+    c->blkU_bytes = ubytes;
+    c->dev_bytes += ubytes;
+  }
+  BlkpArgs a{};
+  a.N = c->N;
+  a.nu = c->nu;
+  a.nwb = bk.nwb;
+  a.units = units;
+  a.wrow = bk.wrow;
+  a.At = (const cx<double>*)c->d_At;
+  a.u = c->d_u;
+  for (int j = 0; j < 3; ++j) {
+    a.mur[j] = j <= c->nu ? c->tprm.mur[j] : 0.0;
+    a.mui[j] = j <= c->nu ? c->tprm.mui[j] : 0.0;
+  }
+  a.U = (double2*)c->d_blkU;
+  a.prods = c->d_terms;  // qoc_chain_terms: executed 16 x 16 complex products on this path
+  const size_t lds = (size_t)bk.nwb * 768 * sizeof(double2) + (size_t)(BLKP_WG / 64) * BLKP_TP * sizeof(double2);
+  auto kern = c->nu == 1 ? k_blkp_exp<1> : k_blkp_exp<2>;
+  HIPCHK(c, blk_lds_attr(kern, lds));
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, BLKP_WG, lds) != hipSuccess || per_cu < 1)
+    per_cu = 2;
+  const unsigned grid = (unsigned)std::max<long long>(
+      1, std::min<long long>((units + BLKP_WG / 64 - 1) / (BLKP_WG / 64), (long long)c->ncu * per_cu));
+  int mk = mark_begin(c, 0);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(BLKP_WG), lds, c->stream, a);
+  mark_end(c, mk);
+  HIPCHK(c, hipGetLastError());
+  const int waves = bk.nwb * c->m;
+  const size_t clds = blkp_chain_lds(c->N, c->m, waves);
+  auto chain = c->nu == 1 ? k_blkp_dual<1> : k_blkp_dual<2>;
+  HIPCHK(c, blk_lds_attr(chain, clds));
+  mk = mark_begin(c, 1);
+  hipLaunchKernelGGL(chain, dim3(2 * c->B), dim3(64 * waves), clds, c->stream, gf, gb, bk, (const double2*)c->d_blkU);
+  mark_end(c, mk);
+  HIPCHK(c, hipGetLastError());
+  c->fwd_captured = false;
+  c->props_since_reset++;
+  c->steps_stale = true;  // d_steps still holds the last k_tchain_prep's records, not this u's
+  const int mg = mark_begin(c, 3);
+  r = grad_rr_cap(c, d_dJdu, c->stream, 0, c->Nt, true, true);
+  mark_end(c, mg);
+  if (r) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_coef_mu, c->d_coef, (size_t)c->B * 2 * c->m * sizeof(cx<double>),
+                           hipMemcpyDeviceToDevice, c->stream));
+  c->L_is_mu = true;
+  c->last_eval_mode = 7;
+  return QOC_OK;
+}
+
 int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
   if (blku_on(c)) return blku_eval_concurrent(c, order, d_dJdu);
   if (!c->d_coef_mu) {
@@ -498,6 +588,11 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
   }
   int r = blk_big(c) ? ensure_pws(c) : QOC_OK;
   if (r) return r;
+  if (blkp_on(c)) {
+    BlkArgs bk = blk_args(c);
+    if ((r = blk_live(c, bk))) return r;
+    if (bk.nwb * c->m <= 8) return blkp_eval_concurrent(c, d_dJdu, bk);
+  }
   if ((r = tchain_prep(c))) return r;
   TChainArgs gf = tchain_args(c);
   TChainArgs gb = tchain_args(c);

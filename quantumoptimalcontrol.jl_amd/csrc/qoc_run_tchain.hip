@@ -151,6 +151,7 @@ int tchain_prep(qoc_ctx* c) {
   mark_end(c, mk);
   HIPCHK(c, hipGetLastError());
   c->cheb_ran = cheb;
+  c->steps_stale = false;
   return QOC_OK;
 }
 

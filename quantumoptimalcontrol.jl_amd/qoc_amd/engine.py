@@ -317,11 +317,12 @@ class GrapeEngine:
                 "expm": {0: "pade", 1: "taylor_rr", 2: "ps_lds"}.get(int(v[5]), "?"),
                 "chain_poly": "chebyshev" if v[6] else "taylor", "kernel_m": int(v[7]),
                 "backward": {0: "generic", 1: "captured", 2: "concurrent", 3: "concurrent", 4: "blocks",
-                             5: "fused", 6: "segmented"}.get(int(v[8]), "?"),
+                             5: "fused", 6: "segmented", 7: "blocks_prop16"}.get(int(v[8]), "?"),
                 "concurrent_launch": {2: "two_streams", 3: "dual", 4: "dual", 5: "fused",
-                                      6: "segmented"}.get(int(v[8])),
+                                      6: "segmented", 7: "dual"}.get(int(v[8])),
                 "fwd_captured": bool(v[9]),
-                "chain_kernel": {0: None, 1: "mfma_lds", 2: "mfma_regs", 3: "blocks", 4: "blocks_mfma", 5: "blocks_prop"}.get(int(v[10]))}
+                "chain_kernel": {0: None, 1: "mfma_lds", 2: "mfma_regs", 3: "blocks", 4: "blocks_mfma", 5: "blocks_prop",
+                                 6: "blocks_prop16"}.get(int(v[10]))}
 
     def set_chain(self, mode: str = "auto"):
         """How the chains apply exp(A_k) (include/qoc.h qoc_set_chain): 'propagators' forms every U_k (the

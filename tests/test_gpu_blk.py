@@ -70,6 +70,9 @@ def _engine(prob, B, blocks, monkeypatch, penalty=None, chain="taylor"):
     monkeypatch.setenv("QOC_BLKU_S", "2" if blocks == "props2" else "1")
     # the forward + fused backward of k_blku_* on device evals too (the segmented eval: tests/test_gpu_blkseg.py)
     monkeypatch.setenv("QOC_BLKSEG", "0")
+    # blocks of 5..16 rows: the Chebyshev-action block chains on device evals too (the stored-propagator eval:
+    # tests/test_gpu_blkp.py)
+    monkeypatch.setenv("QOC_BLKP", "0")
     e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
     e.set_cost_trace(prob.x_target, prob.n)
     e.set_chain(chain)

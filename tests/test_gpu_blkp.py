@@ -1,0 +1,147 @@
+"""Stored propagators for invariant blocks of 5..16 rows (csrc/qoc_blkp.hpp: k_blkp_exp, k_blkp_dual + k_grad_rr_c),
+the concurrent eval of the tunable bus' parity blocks: U_k = exp(A_k) per (seed, slice, live block) on MFMA, then one
+matvec per slice in the chains (the reference's structure, src/gradient_computations.jl:17-29 forward, :52-58
+co-states, :65-74 + :177-223 the order-3 gradient).  Against the oracle and the Chebyshev-action block chains
+(QOC_BLKP=0) at the fp64 bar of SURVEY.md §8c: |ΔJ| <= 1e-12, ||ΔdJdu|| / ||dJdu|| <= 1e-10 per seed, states and
+co-states 1e-12 relative to their largest entry.
+"""
+import numpy as np
+import pytest
+
+import qoc_oracle as O
+from test_gpu_blk import _assert_seed, _block_problem, _eval
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(prob, B, monkeypatch, blkp=True):
+    from qoc_amd import GrapeEngine
+    monkeypatch.setenv("QOC_BLOCKS", "1")
+    monkeypatch.setenv("QOC_BLKP", "1" if blkp else "0")
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
+    e.set_cost_trace(prob.x_target, prob.n)
+    e.set_chain("taylor")
+    return e
+
+
+def _check_states(e, prob, u, b, ks):
+    _, _, c0 = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+    xsc = max(np.abs(x).max() for x in c0.x)
+    lsc = max(np.abs(lam).max() for lam in c0.lam)
+    for k in ks:
+        assert np.abs(e.state(k, seed=b) - c0.x[k]).max() <= 1e-12 * xsc, ("x", b, k)
+        assert np.abs(e.costate(k, seed=b) - c0.lam[k]).max() <= 1e-12 * lsc, ("lambda", b, k)
+
+
+@pytest.mark.parametrize("which", ["tunable_bus", "tunable_bus_cz"])
+def test_blkp_tunable_bus_matches_oracle(built_lib, monkeypatch, which):
+    """The tunable bus (m = 1: the 14-row even block alone is live) and its CZ variant (m = 4, x0 columns in both
+    blocks: two live wave blocks, 8 chain waves per seed and direction)."""
+    from qoc_amd import systems
+    Nt = 48
+    mk = systems.tunable_bus_problem if which == "tunable_bus" else systems.tunable_bus_cz_problem
+    prob = mk(Nt=Nt, tgate=350.0 * Nt / 2000)
+    u = systems.tunable_bus_controls(3, Nt, seed=81)
+    e = _engine(prob, 3, monkeypatch)
+    J, g = _eval(e, u, True)
+    info = e.info()
+    assert info["chain_kernel"] == "blocks_prop16" and info["backward"] == "blocks_prop16", info
+    for b in range(3):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, (which, b))
+    _check_states(e, prob, u, 1, (0, 1, Nt // 2, Nt))
+    e.close()
+    ep = _engine(prob, 3, monkeypatch, blkp=False)
+    Jp, gp = _eval(ep, u, True)
+    assert ep.info()["chain_kernel"] == "blocks_mfma"
+    ep.close()
+    for b in range(3):
+        _assert_seed(J[b], g[b], Jp[b], gp[b], (which, b, "chebyshev chains"))
+
+
+@pytest.mark.parametrize("NB,nblk,nu,m", [(10, 3, 2, 2), (16, 2, 1, 1), (7, 4, 2, 2), (12, 3, 1, 2), (5, 6, 2, 1)])
+def test_blkp_random_permuted_blocks(built_lib, monkeypatch, NB, nblk, nu, m):
+    """Random skew-Hermitian generators with permuted blocks of 5..16 rows (a short last block: padding rows and
+    columns in the propagator tiles), nu = 1 and 2, up to 8 chain waves."""
+    prob, u = _block_problem(NB=NB, nblk=nblk, nu=nu, m=m, Nt=40, seed=NB * 7 + nblk + nu + m)
+    e = _engine(prob, 2, monkeypatch)
+    J, g = _eval(e, u, True)
+    assert e.info()["backward"] == "blocks_prop16", e.info()
+    for b in range(2):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, (NB, nblk, nu, m, b))
+    _check_states(e, prob, u, 0, (0, 1, 20, 40))
+    e.close()
+
+
+@pytest.mark.parametrize("scale", [1e-3, 0.3, 8.0, 40.0])
+def test_blkp_norm_range(built_lib, monkeypatch, scale):
+    """Slice norms from ~1e-3 (Taylor degree 8, no squaring) to ~100 (degree 24 and 5+ squarings): the per-unit
+    (degree, squarings) choice holds the fp64 bar over the whole range."""
+    from qoc_amd import systems
+    prob, u = _block_problem(NB=14, nblk=2, nu=2, m=1, Nt=24, seed=5)
+    prob = systems.Problem("blocks", prob.A0 * scale, [a * scale for a in prob.A], prob.x0, prob.x_target, prob.n,
+                           prob.Nt, "fp64")
+    e = _engine(prob, 2, monkeypatch)
+    e.chain_terms(reset=True)
+    J, g = _eval(e, u, True)
+    prods = e.chain_terms()
+    assert e.info()["backward"] == "blocks_prop16"
+    e.close()
+    for b in range(2):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, (scale, b))
+    # executed 16 x 16 products per (seed, slice, block): r + 2 + s with r >= 2
+    assert prods >= 4 * 2 * 24 * 2, prods
+
+
+def test_blkp_eval_then_host_backward(built_lib, monkeypatch):
+    """A device eval (stored propagators, no step records) followed by grape_sensitivity on the same u: the block
+    backward prepares its step records first (steps_stale) and gives the oracle's gradient for every order."""
+    from qoc_amd import systems
+    Nt = 40
+    prob = systems.tunable_bus_problem(Nt=Nt, tgate=350.0 * Nt / 2000)
+    u = systems.tunable_bus_controls(2, Nt, seed=82)
+    e = _engine(prob, 2, monkeypatch)
+    J, g = _eval(e, u, True)
+    assert e.info()["backward"] == "blocks_prop16"
+    gs = {o: e.grape_sensitivity(u, o) for o in (3, 1, 2)}
+    e.close()
+    for b in range(2):
+        for o, go in gs.items():
+            J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=o)
+            _assert_seed(J[b], go[b], J0, g0, ("host", o, b))
+
+
+def test_blkp_dead_block_rows_zero(built_lib, monkeypatch):
+    """The tunable bus at m = 1 with the odd block live first (nonzero odd rows in every state buffer), then the even
+    block: the stored-propagator eval zeroes the dead rows, so states, co-states, J and dJ/du equal the all-blocks
+    launch (QOC_BLK_DEAD=0)."""
+    from qoc_amd import systems
+    Nt = 32
+    prob = systems.tunable_bus_problem(Nt=Nt, tgate=350.0 * Nt / 2000)
+    u = systems.tunable_bus_controls(2, Nt, seed=83)
+    qb = systems.QuantumBasis([3, 3, 3])
+    x_odd, t_odd = qb.columns(["100"]).astype(complex), qb.columns(["001"]).astype(complex)
+    out = {}
+    for dead in ("1", "0"):
+        monkeypatch.setenv("QOC_BLK_DEAD", dead)
+        e = _engine(prob, 2, monkeypatch)
+        e.set_x0(x_odd)
+        e.set_cost_trace(t_odd, prob.n)
+        _eval(e, u, True)
+        e.set_x0(prob.x0)
+        e.set_cost_trace(prob.x_target, prob.n)
+        J, g = _eval(e, u, True)
+        assert e.info()["backward"] == "blocks_prop16"
+        xs = [e.state(k, seed=b) for k in (0, 1, Nt) for b in (0, 1)]
+        ls = [e.costate(k, seed=b) for k in (0, 1, Nt) for b in (0, 1)]
+        e.close()
+        out[dead] = (J, g, xs, ls)
+    J, g, xs, ls = out["1"]
+    assert np.array_equal(J, out["0"][0]) and np.array_equal(g, out["0"][1])
+    for a, b in zip(xs + ls, out["0"][2] + out["0"][3]):
+        assert np.array_equal(a, b)
+    for b in range(2):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, ("dead", b))
