@@ -448,6 +448,8 @@ def main():
             traffic_all = {}
     taylor = info1.get("chain") == "taylor" and not large
     seg = info1.get("backward") == "segmented"  # the one-launch segmented block eval (k_blkseg_eval)
+    # blocks of 5..16 rows on stored propagators (k_blkp_exp + k_blkp_dual + k_blkp_grad, csrc/qoc_blkp.hpp)
+    p16 = info1.get("chain_kernel") == "blocks_prop16"
     dual = info1.get("concurrent_launch") == "dual"
     fused = info1.get("concurrent_launch") == "fused"  # block propagators: forward, then the backward with the gradient
     bsz = block_sizes(prob) if taylor and info1.get("chain_kernel") in ("blocks", "blocks_mfma", "blocks_prop") else None
@@ -493,6 +495,27 @@ def main():
                          "flops per launch (bench.py blkseg_unit_flops x B Nt nblk) / launch time, against the fp64 "
                          "peak (vector = dense MFMA, 78.6 TF/s); HBM traffic is u, J and dJdu only "
                          "(hbm_bytes_per_launch), so the bound is the VALU issue, not bandwidth")}
+    elif p16:
+        # stored propagators: per (seed, slice, live block) one 16 x 16 exponential on v_mfma_f64_16x16x4 (executed
+        # products counted by the kernel: qoc_chain_terms; 12 MFMAs of 2048 flops each, the three-real-product form),
+        # the two one-matvec chains reading UF / UB (4 KB per slice and direction) and writing the live rows' states,
+        # and the batched gradient (per 16 slices: 2(nu+1) co-state and 3 nu + 2 state-side 16 x 16 x 16 complex GEMMs
+        # per live block and column, 12 MFMAs each)
+        lsz = live_block_sizes(prob)
+        nlive = len(lsz)
+        prods = terms / K  # executed 16 x 16 complex products per step
+        f_exp = prods * 12 * 2048.0
+        tiles = B * -(-Nt // 16)
+        f_grad = tiles * nlive * m * (2 * (nu + 1) + 3 * nu + 2) * 12 * 2048.0
+        u_bytes = 2 * B * Nt * nlive * 256 * 16  # UF + UB
+        chain_bytes = u_bytes + 2 * B * Nt * float(np.sum(lsz)) * m * 16
+        grad_bytes = 2 * B * Nt * float(np.sum(lsz)) * m * 16 + B * Nt * nu * 8 * 2
+        models = {
+            "k_expm": ("mfma", f_exp / 1e12, "TFLOP/s", peak),
+            "k_chain_fwd": ("hbm", chain_bytes / 1e9, "GB/s", PEAK_HBM_GBS),
+            "k_chain_bwd": ("hbm", 0.0, "GB/s", PEAK_HBM_GBS),
+            "k_grad": ("mfma", f_grad / 1e12, "TFLOP/s", peak),
+        }
     elif blocks:
         # block chains (csrc/qoc_blk.hpp, qoc_blku.hpp); the launch's algorithmic bytes are the states it writes (x_k,
         # and μ_k in the dual launch) plus what it reads per slice: the step records of k_tchain_prep (32 B record +
@@ -599,6 +622,29 @@ def main():
     names = {"k_expm": "k_expm_rr", "k_chain_fwd": "k_chain_fwd", "k_chain_bwd": "k_chain_bwd", "k_grad": "k_grad_rr"}
     if seg:
         pass  # kern and roof set above
+    elif p16:
+        names = {"k_expm": "k_blkp_exp", "k_chain_fwd": "k_blkp_dual", "k_chain_bwd": "k_blkp_dual",
+                 "k_grad": "k_blkp_grad"}
+        for k in ("k_expm", "k_chain_fwd", "k_grad"):
+            kern[k]["kernel"] = names[k]
+        kern["k_expm"]["products_per_unit"] = prods / max(B * Nt * nlive, 1)
+        kern["k_expm"]["executed_gflop_per_launch"] = f_exp / 1e9
+        kern["k_expm"]["hbm_bytes_per_launch"] = u_bytes
+        kern["k_chain_fwd"]["note"] = ("forward chain and mu recurrence of every seed in one launch, one matvec per "
+                                       "slice from the stored propagators (LDS-DMA staged)")
+        kern["k_chain_fwd"]["ns_per_serial_step"] = per_launch["k_chain_fwd"] * 1e6 / Nt
+        kern["k_grad"]["executed_gflop_per_launch"] = f_grad / 1e9
+        dom = max(("k_expm", "k_chain_fwd", "k_grad"), key=lambda k: per_step[k])
+        roof = {"kernel": names[dom], "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
+                "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
+                "traffic": traffic_all.get(names[dom]), "traffic_source": traffic_src,
+                "ms_per_launch": kern[dom]["ms_per_launch"], "launches_per_step": lps[dom],
+                "blocks": [int(x) for x in block_sizes(prob)], "live_blocks": [int(x) for x in lsz],
+                "note": ("stored block propagators (csrc/qoc_blkp.hpp): the dominant kernel forms every slice's "
+                         "16 x 16 block exponential on MFMA (Taylor / Paterson-Stockmeyer + squarings, degree and "
+                         "squarings per slice); achieved = executed MFMA flops (12 v_mfma_f64_16x16x4 of 2048 "
+                         "flops per complex product, products counted by the kernel) / launch time, against the "
+                         "dense fp64 MFMA peak")}
     elif blocks:
         kb = {"blocks_mfma": "k_blkrot", "blocks_prop": "k_blku"}.get(info1.get("chain_kernel"), "k_blk")
         names = {"k_expm": "k_blku_rec" if bprop else "k_tchain_prep", "k_chain_fwd": kb + ("_dual" if dual else "_fwd"),

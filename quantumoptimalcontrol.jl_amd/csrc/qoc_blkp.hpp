@@ -73,12 +73,17 @@ __constant__ double kBlkpInvFact[33] = {1.0,
 
 struct BlkpArgs {
   int N, nu, nwb;
-  long long units;             // B Nt nwb: unit = (b Nt + k) nwb + β
+  int skew;                    // every Ã_j exactly skew-Hermitian (qoc_ctx::skew_exact, imaginary shifts)
+  long long unit0, units;      // this launch's units [unit0, units) of B Nt nwb: unit = (b Nt + k) nwb + β
   const int* wrow;             // nwb x 16 rows of the live wave blocks
   const cx<double>* At;        // (nu+1) N x N shifted generators Ã_j, column-major
   const double* u;             // B x Nt x nu
   double mur[3], mui[3];       // μ_k = μ_0 + Σ_j u_j μ_j
-  double2* U;                  // units x 256: U_k of the block, row-major (U[i][j] at 16 i + j), e^{μ_k} included
+  // U_k of the block (e^{μ_k} included) twice, units x 256 each, in the chains' lane order: UF holds U[i][4q + t] at
+  // [t][i + 16 q] (the forward's row quarters), UB holds (U^H)[i][4q + t] = conj(U[4q + t][i]) likewise (the
+  // backward's), so that each of a chain's four DMA pieces per slice reads 1 KB contiguous
+  double2* UF;
+  double2* UB;
   unsigned long long* prods;   // TERM_SLOTS counters: executed 16 x 16 complex products (nullptr: not counted)
 };
 
@@ -102,6 +107,14 @@ __device__ __forceinline__ CMat cm_mul(const CMat& Lt, const CMat& R, const CMat
     t3 = MF<double>::mma(ar + ai, br + bi, t3);
   }
   return CMat{t1 - t2, t3 - t1 - t2};
+}
+
+// LDS traffic between the lanes of one wave: LDS operations of a wave complete in order, the fences keep the compiler
+// from moving them across the exchange
+__device__ __forceinline__ void blkp_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // C layout of X^T through the wave's LDS tile (row pitch 17: the transposed reads of a 16-lane row fall on distinct
@@ -197,8 +210,9 @@ __device__ __forceinline__ CMat blkp_horner_b(int i, const CMat& X, const CMat& 
 
 // One workgroup of BLKP_WG / 64 waves walks the units wave by wave (persistent grid).  LDS: the generators' blocks in
 // C layout ([β][j][e][lane] double2) and one transpose tile per wave.
-template <int NU>
-__global__ __launch_bounds__(BLKP_WG) void k_blkp_exp(const BlkpArgs a) {
+// OCC: workgroups per CU the launch bound asks for (3: 168 VGPRs, 3 spilled; 2: 214 with AGPRs, no spills)
+template <int NU, int OCC>
+__global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double2* gen = reinterpret_cast<double2*>(smem);
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, j = l & 15, g = l >> 4;
@@ -221,7 +235,7 @@ __global__ __launch_bounds__(BLKP_WG) void k_blkp_exp(const BlkpArgs a) {
   const int WPG = BLKP_WG / 64;
   const long long TW = (long long)gridDim.x * WPG;
   unsigned long long prods = 0;
-  for (long long unit = (long long)blockIdx.x * WPG + w; unit < a.units; unit += TW) {
+  for (long long unit = a.unit0 + (long long)blockIdx.x * WPG + w; unit < a.units; unit += TW) {
     const long long bk = unit / nwb;
     const int beta = (int)(unit - bk * nwb);
     const double u1 = a.u[bk * NU], u2 = NU > 1 ? a.u[bk * NU + (NU > 1 ? 1 : 0)] : 0.0;
@@ -246,31 +260,54 @@ __global__ __launch_bounds__(BLKP_WG) void k_blkp_exp(const BlkpArgs a) {
     const double n1 = row_max16(xsum_rows(cs)), ninf = xmax_rows(rmax);
     f2 = xsum_rows(row_sum16(f2));
     const double rho = uniform_f64(fmin(sqrt(f2), sqrt(n1 * ninf)));
+    // (the sharper α_p = max(‖X^p‖^{1/p}, ‖X^{p+1}‖^{1/(p+1)}) of Al-Mohy & Higham from the computed powers chose the
+    // same (r, s) on the tunable bus -- 10.75 products per unit either way -- and cost three more reductions)
     int r = BLKP_RMAX, s = 0, best = 1 << 30;
-    for (int rr = BLKP_RMIN; rr <= BLKP_RMAX; ++rr) {
-      int ss = 0;
-      for (double t = rho; t > kBlkpTheta[rr] && ss < 64; t *= 0.5) ++ss;
+    for (int rr = BLKP_RMIN; rr <= BLKP_RMAX; ++rr) {  // the fewest products r + 2 + s with 2^-s ρ̂ <= θ_{4r}
+      // s = max(0, ceil(log2(ρ̂ / θ))): with ρ̂ / θ = f 2^e, f in [0.5, 1), that is e, or e - 1 when f = 1/2
+      const double q = rho / kBlkpTheta[rr];
+      const int e = q > 1.0 ? __builtin_amdgcn_frexp_exp(q) : 0;
+      const int ss = q > 1.0 ? (__builtin_amdgcn_frexp_mant(q) == 0.5 ? e - 1 : e) : 0;
       if (rr + 2 + ss < best) {
         best = rr + 2 + ss;
         r = rr;
         s = ss;
       }
     }
-    const double sc = ldexp(1.0, -s);
+    {
+      const double sc = ldexp(1.0, -s);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      X.r[e] *= sc;
-      X.i[e] *= sc;
+      for (int e = 0; e < 4; ++e) {
+        X.r[e] *= sc;
+        X.i[e] *= sc;
+      }
     }
-    const CMat Xt = cm_transpose(X, tile);
+    // X^T: for skew-Hermitian blocks -conj(X) (no LDS round trip), else through the tile
+    CMat Xt;
+    if (a.skew) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        Xt.r[e] = -X.r[e];
+        Xt.i[e] = X.i[e];
+      }
+    } else {
+      Xt = cm_transpose(X, tile);
+    }
     const CMat X2 = cm_mul<false>(Xt, X, X);
     const CMat X3 = cm_mul<false>(Xt, X2, X);
-    CMat R;
-    CMat X4t;
-    {
-      const CMat X4 = cm_mul<false>(Xt, X3, X);
+    const CMat X4 = cm_mul<false>(Xt, X3, X);
+    CMat X4t;  // X^4 of a skew-Hermitian X is Hermitian: its transpose is conj(X^4)
+    if (a.skew) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        X4t.r[e] = X4.r[e];
+        X4t.i[e] = -X4.i[e];
+      }
+    } else {
       X4t = cm_transpose(X4, tile);
-      R = blkp_horner_b(r - 1, X, X2, X3);
+    }
+    CMat R = blkp_horner_b(r - 1, X, X2, X3);
+    {
       const double cm = kBlkpInvFact[4 * r];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -289,36 +326,54 @@ __global__ __launch_bounds__(BLKP_WG) void k_blkp_exp(const BlkpArgs a) {
     double sn, cn;
     sincos(mi, &sn, &cn);
     const double pr = em * cn, pi = em * sn;
-    double2* Ub = a.U + unit * 256;
+    double2* const uf = a.UF + unit * 256;
+    double2* const ubh = a.UB + unit * 256;
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      Ub[(g + 4 * e) * 16 + j] = make_double2(fma(pr, R.r[e], -pi * R.i[e]), fma(pr, R.i[e], pi * R.r[e]));
+    for (int e = 0; e < 4; ++e) {  // this lane holds U[g + 4e][j]
+      const double vr = fma(pr, R.r[e], -pi * R.i[e]), vi = fma(pr, R.i[e], pi * R.r[e]);
+      uf[(j & 3) * 64 + g + 4 * e + 16 * (j >> 2)] = make_double2(vr, vi);
+      ubh[g * 64 + j + 16 * e] = make_double2(vr, -vi);
+    }
     prods += (unsigned long long)(r + 2 + s);
   }
   if (a.prods && l == 0 && prods) atomicAdd(a.prods + (blockIdx.x & (TERM_SLOTS - 1)), prods);
 }
 
 // ---- chains from the stored propagators ----
-// LDS: [32 doubles reduction scratch][x_N: 2 N m doubles][per wave: 16 + 16 double2 exchange rows]
-__host__ __device__ inline size_t blkp_chain_lds(int N, int m, int waves) {
-  return (size_t)(32 + 2 * N * m) * sizeof(double) + (size_t)waves * 32 * sizeof(double2);
+// The chains are bound by the propagators they read (4 KB per slice and direction, 8.4 GB per tunable-bus eval).  The
+// slices run in chunks of CH: the propagator quarters of chunk c + 1 stream into the wave's LDS by LDS-DMA
+// (global_load_lds_dwordx4, two buffers) while chunk c runs, and the new states collect in LDS and are stored at the
+// next chunk start, so the slices touch LDS only and the one wait for memory per chunk (vmcnt(0), by hand: the
+// compiler does not see the DMA) finds loads and stores a whole chunk old.  (Per-slice register prefetches did not
+// work: the compiler's waits at the loop head also covered the newest loads.)  The gradient's products are not formed
+// here (k_blkp_grad forms them from x_k and μ_{k+1}, all slices in parallel): with them every slice of the one wave per
+// SIMD carried three times the dependent instructions (2.9 ms per tunable-bus eval against 0.9 ms without).
+// LDS: [32 doubles scratch][x_N: 2 N m doubles][per wave, double2: exchange row 32 | new states CH x 16 |
+// propagators 2 x CH x 4 x 64]
+__host__ __device__ constexpr int blkp_wave_lds2(int CH) { return 32 + CH * 16 + 2 * CH * 256; }
+__host__ __device__ inline size_t blkp_chain_lds(int N, int m, int waves, int CH) {
+  return (size_t)(32 + 2 * N * m) * sizeof(double) + (size_t)waves * blkp_wave_lds2(CH) * sizeof(double2);
 }
-constexpr int BLKP_PD = 4;  // slices of propagator rows in flight per lane
+__host__ __device__ inline int blkp_chunk(int waves) { return waves <= 2 ? 4 : waves <= 4 ? 2 : 1; }
+// 16 B per lane from src to LDS byte address lds + 16 lane (lds wave-uniform); M0 set and restored in the statement
+__device__ __forceinline__ void blkp_dma(const void* src, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
 
-// this lane's view of wave block β: rows rb[i] (i = lane & 15) and the quarter rows / columns rb[4q + t]
+// this lane's view of wave block β: row rb[i] (i = lane & 15), quarter q = lane >> 4, state column c
 struct BlkpLane {
   int i, q, beta, c, row;
-  int qr[4];
   __device__ __forceinline__ void setup(const BlkArgs& bk) {
     const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
     i = l & 15;
     q = l >> 4;
     beta = w % bk.nwb;
     c = w / bk.nwb;
-    const int* rb = bk.wrow + 16 * beta;
-    row = rb[i];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) qr[t] = rb[4 * q + t];
+    row = bk.wrow[16 * beta + i];
   }
 };
 
@@ -332,42 +387,25 @@ __device__ __forceinline__ double2 blkp_dot4(const double (&ar)[4], const double
   return make_double2(r0 + r1, i0 + i1);
 }
 
-// FWD: x_{k+1} = U_k x_k, lane (i, q) holds U_k[i][4q + t]; else μ_k = U_k^H μ_{k+1}, lane (i, q) holds U_k[4q + t][i]
-// (conjugated on use).  Generators: Ã_j[row][qr[t]] forward, conj(Ã_j[qr[t]][row]) = (Ã_j^H)[row][qr[t]] backward.
-template <int NU, bool FWD>
+// FWD: x_{k+1} = U_k x_k from UF (lane (i, q) holds U_k[i][4q + t]); else μ_k = U_k^H μ_{k+1} from UB (lane (i, q)
+// holds (U_k^H)[i][4q + t]), μ_N = X_target (λ_k = coef ⊙ μ_k).  The forward ends with J and the λ_N coefficients.
+template <bool FWD, int CH>
 __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkArgs& bk, const double2* __restrict__ U,
                                                 const int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* red = reinterpret_cast<double*>(smem);
   double* xN = red + 32;
-  const int N = g.N, m = g.m, Nt = g.Nt, nwb = bk.nwb, tid = threadIdx.x, nthr = blockDim.x;
-  const size_t Nm = (size_t)N * m, NN = (size_t)N * N;
+  const int N = g.N, m = g.m, Nt = g.Nt, nwb = bk.nwb, tid = threadIdx.x, nthr = blockDim.x, l = tid & 63;
+  const size_t Nm = (size_t)N * m;
   BlkpLane ln;
   ln.setup(bk);
-  double2* xs = reinterpret_cast<double2*>(xN + 2 * Nm) + (tid >> 6) * 32;
-  double2* fs = xs + 16;
-  const bool act = ln.row >= 0;
-  // the block rows of Ã_0..Ã_NU at this lane's quarter
-  double gr[NU + 1][4], gi[NU + 1][4];
-  const cx<double>* At = (const cx<double>*)g.At;
-#pragma unroll
-  for (int jg = 0; jg <= NU; ++jg)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int cq = ln.qr[t];
-      const bool ok = act && cq >= 0;
-      const size_t o = FWD ? (size_t)max(ln.row, 0) + (size_t)N * max(cq, 0) : (size_t)max(cq, 0) + (size_t)N * max(ln.row, 0);
-      const cx<double> v = ok ? At[jg * NN + o] : cx<double>{0.0, 0.0};
-      gr[jg][t] = v.r;
-      gi[jg][t] = FWD ? v.i : -v.i;
-    }
-  double* const sink = tchain_sink(g);
-  double2* const sink2 = reinterpret_cast<double2*>(sink);
+  double2* const xs = reinterpret_cast<double2*>(xN + 2 * Nm) + (tid >> 6) * blkp_wave_lds2(CH);
+  double2* const Os = xs + 32;        // [jj][i]: x_{k+1} / μ_k of row i
+  double2* const Ub2 = Os + CH * 16;  // [buffer][jj][t][lane]: this lane's propagator quarter of chunk slice jj
+  const bool act = ln.row >= 0, own = act && ln.q == 0;
+  double2* const sink2 = reinterpret_cast<double2*>(tchain_sink(g));
   const size_t oe = (size_t)ln.c * N + max(ln.row, 0);  // element offset (complex) of this lane's row
   double2* const Sb = reinterpret_cast<double2*>((cx<double>*)(FWD ? g.X : g.L) + (size_t)b * (Nt + 1) * Nm);
-  double2* const C1 = reinterpret_cast<double2*>((cx<double>*)g.cap1 + (size_t)b * (Nt + 1) * Nm);
-  double2* const C2 = reinterpret_cast<double2*>((cx<double>*)g.cap2 + (size_t)b * (Nt + 1) * Nm);
-  const bool own = act && ln.q == 0;
   if (FWD)
     for (size_t e = tid; e < 2 * Nm; e += nthr) xN[e] = 0.0;
   double2 v0 = make_double2(0.0, 0.0);
@@ -387,85 +425,75 @@ __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkAr
     xr[t] = v.x;
     xi[t] = v.y;
   }
-  // propagator entries and u of the slices in flight (vector loads: the per-lane zero keeps u off the scalar cache)
   int z;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-  const double* ub = g.u + (size_t)b * Nt * g.nu;
-  const double2* Ubase = U + (size_t)b * Nt * nwb * 256 + (size_t)ln.beta * 256 +
-                         (FWD ? (size_t)ln.i * 16 + 4 * ln.q : (size_t)(4 * ln.q) * 16 + ln.i) + z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // per-lane (VGPR) source addresses
+  const double2* Ubase = U + (size_t)b * Nt * nwb * 256 + (size_t)ln.beta * 256 + l + z;
   const size_t ustep = (size_t)nwb * 256;
-  double2 pu[BLKP_PD][4];
-  double pc[BLKP_PD][2];
-  auto issue = [&](int slot, int j) __attribute__((always_inline)) {
-    const int k = FWD ? min(j, Nt - 1) : max(Nt - 1 - j, 0);
-    const double2* p = Ubase + (size_t)k * ustep;
+  const unsigned ub_lds = (unsigned)(size_t)(__attribute__((address_space(3))) double2*)Ub2;
+  // chunk cc's propagator quarters by DMA into buffer cc & 1 (1 KB contiguous per piece)
+  auto issue = [&](int cc) __attribute__((always_inline)) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) pu[slot][t] = p[FWD ? t : 16 * t];
-    pc[slot][0] = ub[(size_t)k * g.nu + z];
-    pc[slot][1] = NU > 1 ? ub[(size_t)k * g.nu + (NU > 1 ? 1 : 0) + z] : 0.0;
+    for (int jj = 0; jj < CH; ++jj) {
+      const int j = cc * CH + jj;
+      const int k = FWD ? min(j, Nt - 1) : max(Nt - 1 - j, 0);
+      const double2* p = Ubase + (size_t)k * ustep;
+      const unsigned dst =
+          (unsigned)__builtin_amdgcn_readfirstlane((int)(ub_lds + (unsigned)((((cc & 1) * CH + jj) * 4) * 1024)));
+#pragma unroll
+      for (int t = 0; t < 4; ++t) blkp_dma(p + 64 * t, dst + t * 1024);
+    }
   };
+  typedef double D2V __attribute__((ext_vector_type(2)));
+  using G2 = __attribute__((address_space(1))) D2V;
+  // chunk cc's new states from LDS to HBM, branch-free (lanes without an element write the sink)
+  auto flush = [&](int cc) __attribute__((always_inline)) {
 #pragma unroll
-  for (int p = 0; p < BLKP_PD; ++p) issue(p, p);
-  for (int j0 = 0; j0 < Nt; j0 += BLKP_PD) {
-#pragma unroll
-    for (int p = 0; p < BLKP_PD; ++p) {
-      const int j = j0 + p;
-      if (j >= Nt) break;
+    for (int jj = 0; jj < CH; ++jj) {
+      const int j = cc * CH + jj;
       const int k = FWD ? j : Nt - 1 - j;
-      double ur[4], ui[4], ar[4], ai[4];
-      const double u1 = pc[p][0], u2 = pc[p][1];
+      G2* p = (G2*)(own && j < Nt ? Sb + (size_t)(FWD ? k + 1 : k) * Nm + oe : sink2);
+      asm volatile("" : "+v"(p));
+      const double2 v = Os[jj * 16 + ln.i];
+      *p = D2V{v.x, v.y};
+    }
+  };
+  issue(0);
+  int c = 0;
+  for (int j0 = 0; j0 < Nt; j0 += CH, ++c) {
+    // chunk c's DMA and chunk c - 2's stores were issued a chunk ago
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    blkp_wave_sync();
+    issue(c + 1);
+    if (c > 0) flush(c - 1);
+    blkp_wave_sync();
+    const double2* const Us = Ub2 + (c & 1) * CH * 256;
+    for (int jj = 0; jj < CH; ++jj) {
+      if (j0 + jj >= Nt) break;
+      double ur[4], ui[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        ur[t] = pu[p][t].x;
-        ui[t] = FWD ? pu[p][t].y : -pu[p][t].y;
-        ar[t] = fma(u1, gr[1][t], gr[0][t]);
-        ai[t] = fma(u1, gi[1][t], gi[0][t]);
-        if constexpr (NU > 1) {
-          ar[t] = fma(u2, gr[NU > 1 ? 2 : 0][t], ar[t]);
-          ai[t] = fma(u2, gi[NU > 1 ? 2 : 0][t], ai[t]);
-        }
+        const double2 pv = Us[(jj * 4 + t) * 64 + l];
+        ur[t] = pv.x;
+        ui[t] = pv.y;
       }
-      issue(p, j + BLKP_PD);
-      // the loads stay here, BLKP_PD slices ahead of their use (the scheduler would sink them towards the stores)
-      __builtin_amdgcn_sched_barrier(0);
       double2 y = blkp_dot4(ur, ui, xr, xi);
-      double2 f1 = blkp_dot4(ar, ai, xr, xi);
       y.x = xsum_rows(y.x);
       y.y = xsum_rows(y.y);
-      f1.x = xsum_rows(f1.x);
-      f1.y = xsum_rows(f1.y);
       xs[ln.i] = y;
-      fs[ln.i] = f1;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      double fr[4], fi[4];
+      blkp_wave_sync();
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const double2 v = xs[4 * ln.q + t], f = fs[4 * ln.q + t];
+        const double2 v = xs[4 * ln.q + t];
         xr[t] = v.x;
         xi[t] = v.y;
-        fr[t] = f.x;
-        fi[t] = f.y;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      double2 f2 = blkp_dot4(ar, ai, fr, fi);
-      f2.x = xsum_rows(f2.x);
-      f2.y = xsum_rows(f2.y);
-      // branch-free stores (lanes without an element write the sink): the pointers are opaque, so no exec branch
-      // (global address space: a generic pointer would store through flat_*, which the waitcnt pass cannot count)
-      using G2 = __attribute__((address_space(1))) double2;
-      G2* p0 = (G2*)(own ? Sb + (size_t)(FWD ? k + 1 : k) * Nm + oe : sink2);
-      G2* p1 = (G2*)(own ? C1 + (size_t)k * Nm + oe : sink2 + 1);
-      G2* p2 = (G2*)(own ? C2 + (size_t)k * Nm + oe : sink2 + 2);
-      asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2));
-      *p0 = y;
-      *p1 = f1;
-      *p2 = f2;
+      blkp_wave_sync();
+      if (ln.q == 0) Os[jj * 16 + ln.i] = y;
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) DMA must land before the LDS is reused
+  blkp_wave_sync();
+  flush(c - 1);
   if (FWD) {
     if (own) {  // x_N: the exchange row holds the last slice's result
       const double2 v = xs[ln.i];
@@ -480,15 +508,161 @@ __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkAr
 
 // forward chain and μ recurrence of every seed in one launch of 2B workgroups (seed-direction interleave as
 // k_blkrot_dual), nwb m waves each
-template <int NU>
+// (seeds seed0 .. seed0 + gridDim.x / 2 - 1)
+template <int CH>
 __global__ __launch_bounds__(512) void k_blkp_dual(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk,
-                                                   const double2* __restrict__ U) {
+                                                   const double2* __restrict__ UF, const double2* __restrict__ UB,
+                                                   int seed0) {
   const int i = blockIdx.x, B = gridDim.x >> 1;
   const bool by8 = (B & 7) == 0;
   const int dir = by8 ? (i >> 3) & 1 : i & 1;
-  const int seed = by8 ? ((i >> 4) << 3) | (i & 7) : i >> 1;
-  if (dir == 0) blkp_chain_body<NU, true>(gf, bk, U, seed);
-  else blkp_chain_body<NU, false>(gb, bk, U, seed);
+  const int seed = seed0 + (by8 ? ((i >> 4) << 3) | (i & 7) : i >> 1);
+  if (dir == 0) blkp_chain_body<true, CH>(gf, bk, UF, seed);
+  else blkp_chain_body<false, CH>(gb, bk, UB, seed);
+}
+
+// ---- the order-3 gradient on the stored states (the reference's expm_jacobian! + _compute_u_sensitivity,
+// src/gradient_computations.jl:177-223): with A_k = Σ_j u_jk A_j (unshifted generators), P_1 = A_k x_k,
+// P_2 = A_k P_1, Q_1 = A_k^H λ_{k+1}, Q_2 = A_k^H Q_1, W_0 = λ + Q_1 / 2 + Q_2 / 6, W_1 = λ / 2 + Q_1 / 6:
+//   dJ/du_jk = Re[<W_0, A_j x_k> + <W_1, A_j P_1> + <λ / 6, A_j P_2>]
+// One wave per (seed, 16 consecutive slices): the 16 slices are the columns of 16 x 16 complex matrices in the C
+// layout (lane j + 16 g: slice k0 + j, block rows g + 4e), so every generator product is a 16 x 16 x 16 GEMM on MFMA
+// with the generator block as the left operand (from LDS) and the per-slice u_jk a per-lane scale; summed over the
+// live blocks and state columns.  λ = coef ⊙ μ (the μ recurrence's coefficients).
+struct BlkpGradArgs {
+  int N, m, Nt, nwb;
+  const int* wrow;           // nwb x 16 rows of the live wave blocks
+  const cx<double>* A;       // (nu+1) N x N unshifted generators, column-major
+  const double* u;           // B x Nt x nu
+  const cx<double>* X;       // B x (Nt+1) x N x m states
+  const cx<double>* L;       // μ_k, same layout
+  const cx<double>* coef;    // B x 2m λ_N coefficients
+  double* dJdu;              // B x Nt x nu
+  long long tiles;           // B ceil(Nt / 16)
+};
+__host__ __device__ inline size_t blkp_grad_lds(int nwb, int nu) { return (size_t)nwb * (nu + 1) * 2 * 256 * sizeof(double2); }
+
+__device__ __forceinline__ double blkp_redot(const CMat& W, const CMat& Y) {  // Re Σ conj(W) Y over this lane's entries
+  double a = 0.0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) a = fma(W.r[e], Y.r[e], fma(W.i[e], Y.i[e], a));
+  return a;
+}
+__device__ __forceinline__ void blkp_axpy(CMat& Y, double a, const CMat& X) {  // Y += a X
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    Y.r[e] = fma(a, X.r[e], Y.r[e]);
+    Y.i[e] = fma(a, X.i[e], Y.i[e]);
+  }
+}
+
+template <int NU>
+__global__ __launch_bounds__(256, 2) void k_blkp_grad(const BlkpGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double2* gen = reinterpret_cast<double2*>(smem);  // [β][j][form][e][lane]: form 0 A_j, form 1 A_j^H as left operands
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, jl = l & 15, g = l >> 4;
+  const int N = a.N, m = a.m, Nt = a.Nt, nwb = a.nwb;
+  const size_t NN = (size_t)N * N, Nm = (size_t)N * m;
+  const int ngen = nwb * (NU + 1) * 2 * 256;
+  for (int e = tid; e < ngen; e += blockDim.x) {
+    const int ll = e & 63, ee = (e >> 6) & 3, form = (e >> 8) & 1, jg = (e >> 9) % (NU + 1), bb = (e >> 9) / (NU + 1);
+    const int* rb = a.wrow + 16 * bb;
+    const int r1 = rb[ll & 15], r2 = rb[(ll >> 4) + 4 * ee];
+    double2 v = make_double2(0.0, 0.0);
+    if (r1 >= 0 && r2 >= 0) {  // form 0: A[r1][r2]; form 1: conj(A[r2][r1])
+      const cx<double> z = form == 0 ? a.A[jg * NN + r1 + (size_t)N * r2] : a.A[jg * NN + r2 + (size_t)N * r1];
+      v = make_double2(z.r, form == 0 ? z.i : -z.i);
+    }
+    gen[e] = v;
+  }
+  __syncthreads();
+  const int T16 = (Nt + 15) >> 4;
+  for (long long tile = (long long)blockIdx.x * 4 + w; tile < a.tiles; tile += (long long)gridDim.x * 4) {
+    const int b = (int)(tile / T16), k0 = (int)(tile - (long long)b * T16) * 16;
+    const int kj = k0 + jl, kc = min(kj, Nt - 1);
+    double uj[NU];
+#pragma unroll
+    for (int q = 0; q < NU; ++q) uj[q] = a.u[((size_t)b * Nt + kc) * NU + q];
+    double acc[NU];
+#pragma unroll
+    for (int q = 0; q < NU; ++q) acc[q] = 0.0;
+    for (int beta = 0; beta < nwb; ++beta) {
+      const int* rb = a.wrow + 16 * beta;
+      int rows[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rows[e] = rb[g + 4 * e];
+      const double2* G = gen + (size_t)beta * (NU + 1) * 512;
+      // a generator operand from LDS at each use (an opaque lane index: hoisted out of the loops, the 2 (nu + 1)
+      // operands would hold 16 (nu + 1) VGPRs for the whole kernel)
+      auto op = [&](int jg, int form) __attribute__((always_inline)) {
+        CMat M;
+        int ll = l;
+        asm volatile("" : "+v"(ll));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double2 v = G[(jg * 2 + form) * 256 + 64 * e + ll];
+          M.r[e] = v.x;
+          M.i[e] = v.y;
+        }
+        return M;
+      };
+      for (int c = 0; c < m; ++c) {
+        const cx<double> cf = a.coef[(size_t)b * 2 * m + c];
+        const cx<double>* xb = a.X + ((size_t)b * (Nt + 1) + kc) * Nm + (size_t)c * N;  // x_k
+        const cx<double>* lb = a.L + ((size_t)b * (Nt + 1) + kc + 1) * Nm + (size_t)c * N;  // μ_{k+1}
+        CMat X, Lm;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = rows[e] >= 0;
+          const cx<double> xv = ok ? xb[rows[e]] : cx<double>{0.0, 0.0};
+          const cx<double> mv = ok ? lb[rows[e]] : cx<double>{0.0, 0.0};
+          X.r[e] = xv.r;
+          X.i[e] = xv.i;
+          Lm.r[e] = cf.r * mv.r - cf.i * mv.i;
+          Lm.i[e] = cf.r * mv.i + cf.i * mv.r;
+        }
+        // the co-state side: Q_1 = A_k^H λ, Q_2 = A_k^H Q_1
+        CMat Q1 = cm_mul<false>(op(0, 1), Lm, Lm);
+#pragma unroll
+        for (int q = 0; q < NU; ++q) blkp_axpy(Q1, uj[q], cm_mul<false>(op(q + 1, 1), Lm, Lm));
+        CMat Q2 = cm_mul<false>(op(0, 1), Q1, Q1);
+#pragma unroll
+        for (int q = 0; q < NU; ++q) blkp_axpy(Q2, uj[q], cm_mul<false>(op(q + 1, 1), Q1, Q1));
+        CMat W0, W1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          W0.r[e] = Lm.r[e] + 0.5 * Q1.r[e] + (1.0 / 6.0) * Q2.r[e];
+          W0.i[e] = Lm.i[e] + 0.5 * Q1.i[e] + (1.0 / 6.0) * Q2.i[e];
+          W1.r[e] = 0.5 * Lm.r[e] + (1.0 / 6.0) * Q1.r[e];
+          W1.i[e] = 0.5 * Lm.i[e] + (1.0 / 6.0) * Q1.i[e];
+          Lm.r[e] *= 1.0 / 6.0;
+          Lm.i[e] *= 1.0 / 6.0;
+        }
+        // the state side: <W_0, A_j x>, P_1, <W_1, A_j P_1>, P_2, <λ/6, A_j P_2>
+        CMat P1 = cm_mul<false>(op(0, 0), X, X);
+#pragma unroll
+        for (int q = 0; q < NU; ++q) {
+          const CMat Y = cm_mul<false>(op(q + 1, 0), X, X);
+          acc[q] += blkp_redot(W0, Y);
+          blkp_axpy(P1, uj[q], Y);
+        }
+        CMat P2 = cm_mul<false>(op(0, 0), P1, P1);
+#pragma unroll
+        for (int q = 0; q < NU; ++q) {
+          const CMat Y = cm_mul<false>(op(q + 1, 0), P1, P1);
+          acc[q] += blkp_redot(W1, Y);
+          blkp_axpy(P2, uj[q], Y);
+        }
+#pragma unroll
+        for (int q = 0; q < NU; ++q) acc[q] += blkp_redot(Lm, cm_mul<false>(op(q + 1, 0), P2, P2));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NU; ++q) {
+      const double v = xsum_rows(acc[q]);
+      if (g == 0 && kj < Nt) a.dJdu[((size_t)b * Nt + kj) * NU + q] = v;
+    }
+  }
 }
 
 }  // namespace qoc

@@ -403,7 +403,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
       {&c->d_x0, (size_t)B * Nm * c->esz},
       {&c->d_Xt, Nm * c->esz},
       {(void**)&c->d_pmask, Nm},
-      {(void**)&c->d_u, (size_t)B * nu * Nt * sizeof(double)},
+      {(void**)&c->d_u, (size_t)B * nu * Nt * sizeof(double) + 16},  // + 16: k_blkp_dual's 16-byte u reads
       {&c->d_U, (size_t)B * Nt * NN * c->esz},
       {&c->d_X, (size_t)B * (Nt + 1) * Nm * c->esz},
       {&c->d_L, (size_t)B * (Nt + 1) * Nm * c->esz},

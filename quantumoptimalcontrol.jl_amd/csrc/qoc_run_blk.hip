@@ -508,18 +508,12 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
   TChainArgs gf = tchain_args(c);
   TChainArgs gb = tchain_args(c);
   gb.mu_mode = 1;
-  const size_t bufN = (size_t)c->N * ((size_t)c->B * (c->Nt + 1) * c->m);
-  gf.cap1 = c->d_pws;
-  gf.cap2 = (cx<double>*)c->d_pws + bufN;
-  gb.cap1 = c->d_gws;
-  gb.cap2 = (cx<double>*)c->d_gws + bufN;
   int r;
   if (bk.nwb != c->nwb) {
-    if ((r = blk_zero_dead(c, {c->d_X, c->d_L, (void*)gf.cap1, (void*)gf.cap2, (void*)gb.cap1, (void*)gb.cap2})))
-      return r;
+    if ((r = blk_zero_dead(c, {c->d_X, c->d_L}))) return r;
   }
   const long long units = (long long)c->B * c->Nt * bk.nwb;
-  const size_t ubytes = (size_t)units * 256 * sizeof(double2);
+  const size_t ubytes = (size_t)units * 2 * 256 * sizeof(double2);  // UF and UB
   if (c->blkU_bytes < ubytes) {
     if (c->d_blkU) {
       HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -536,6 +530,7 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
   a.N = c->N;
   a.nu = c->nu;
   a.nwb = bk.nwb;
+  a.skew = c->skew_exact && c->tprm.mur[0] == 0.0 && c->tprm.mur[1] == 0.0 && c->tprm.mur[2] == 0.0;
   a.units = units;
   a.wrow = bk.wrow;
   a.At = (const cx<double>*)c->d_At;
@@ -544,35 +539,86 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
     a.mur[j] = j <= c->nu ? c->tprm.mur[j] : 0.0;
     a.mui[j] = j <= c->nu ? c->tprm.mui[j] : 0.0;
   }
-  a.U = (double2*)c->d_blkU;
+  a.UF = (double2*)c->d_blkU;
+  a.UB = a.UF + (size_t)units * 256;
   a.prods = c->d_terms;  // qoc_chain_terms: executed 16 x 16 complex products on this path
   const size_t lds = (size_t)bk.nwb * 768 * sizeof(double2) + (size_t)(BLKP_WG / 64) * BLKP_TP * sizeof(double2);
-  auto kern = c->nu == 1 ? k_blkp_exp<1> : k_blkp_exp<2>;
+  const char* oc = getenv("QOC_BLKP_OCC");
+  const bool occ3 = !(oc && atoi(oc) == 2);
+  auto kern = c->nu == 1 ? (occ3 ? k_blkp_exp<1, 3> : k_blkp_exp<1, 2>) : (occ3 ? k_blkp_exp<2, 3> : k_blkp_exp<2, 2>);
   HIPCHK(c, blk_lds_attr(kern, lds));
+  const int waves = bk.nwb * c->m;
+  const int ch = blkp_chunk(waves);
+  const size_t clds = blkp_chain_lds(c->N, c->m, waves, ch);
+  auto chain = ch == 4 ? k_blkp_dual<4> : ch == 2 ? k_blkp_dual<2> : k_blkp_dual<1>;
+  HIPCHK(c, blk_lds_attr(chain, clds));
+  // The formation is MFMA-bound and the chains are bound by their propagator reads: the seeds go in `parts` groups,
+  // the chains of group p (second stream) beside the formation of group p + 1, with the formation at two workgroups
+  // per CU so that a chain workgroup fits beside them (QOC_BLKP_PARTS, default 4; 1: one formation, then the chains)
+  int parts = 4;
+  if (const char* pe = getenv("QOC_BLKP_PARTS")) parts = atoi(pe);
+  parts = std::max(1, std::min(parts, c->B));
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, BLKP_WG, lds) != hipSuccess || per_cu < 1)
     per_cu = 2;
-  const unsigned grid = (unsigned)std::max<long long>(
-      1, std::min<long long>((units + BLKP_WG / 64 - 1) / (BLKP_WG / 64), (long long)c->ncu * per_cu));
-  int mk = mark_begin(c, 0);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(BLKP_WG), lds, c->stream, a);
-  mark_end(c, mk);
-  HIPCHK(c, hipGetLastError());
-  const int waves = bk.nwb * c->m;
-  const size_t clds = blkp_chain_lds(c->N, c->m, waves);
-  auto chain = c->nu == 1 ? k_blkp_dual<1> : k_blkp_dual<2>;
-  HIPCHK(c, blk_lds_attr(chain, clds));
-  mk = mark_begin(c, 1);
-  hipLaunchKernelGGL(chain, dim3(2 * c->B), dim3(64 * waves), clds, c->stream, gf, gb, bk, (const double2*)c->d_blkU);
-  mark_end(c, mk);
-  HIPCHK(c, hipGetLastError());
+  if (parts > 1) {
+    per_cu = std::min(per_cu, 2);
+    if ((r = ensure_stream2(c, parts + 1))) return r;
+    HIPCHK(c, hipEventRecord(c->sync_ev[parts], c->stream));  // the second stream after everything queued so far
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[parts], 0));
+  }
+  hipStream_t cs = parts > 1 ? c->stream2 : c->stream;
+  for (int p = 0; p < parts; ++p) {
+    const int s0 = (int)((long long)c->B * p / parts), s1 = (int)((long long)c->B * (p + 1) / parts);
+    if (s1 <= s0) continue;
+    a.unit0 = (long long)s0 * c->Nt * bk.nwb;
+    a.units = (long long)s1 * c->Nt * bk.nwb;
+    const unsigned grid = (unsigned)std::max<long long>(
+        1, std::min<long long>((a.units - a.unit0 + BLKP_WG / 64 - 1) / (BLKP_WG / 64), (long long)c->ncu * per_cu));
+    int mk = mark_begin(c, 0);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(BLKP_WG), lds, c->stream, a);
+    mark_end(c, mk);
+    HIPCHK(c, hipGetLastError());
+    if (parts > 1) {
+      HIPCHK(c, hipEventRecord(c->sync_ev[p], c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[p], 0));
+    }
+    mk = mark_begin(c, 1, cs);
+    hipLaunchKernelGGL(chain, dim3(2 * (s1 - s0)), dim3(64 * waves), clds, cs, gf, gb, bk, (const double2*)a.UF,
+                       (const double2*)a.UB, s0);
+    mark_end(c, mk, cs);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (parts > 1) {  // the gradient (and everything after it on the engine stream) after the last chains
+    HIPCHK(c, hipEventRecord(c->sync_ev[parts], c->stream2));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->sync_ev[parts], 0));
+  }
   c->fwd_captured = false;
   c->props_since_reset++;
   c->steps_stale = true;  // d_steps still holds the last k_tchain_prep's records, not this u's
+  BlkpGradArgs ga{};
+  ga.N = c->N;
+  ga.m = c->m;
+  ga.Nt = c->Nt;
+  ga.nwb = bk.nwb;
+  ga.wrow = bk.wrow;
+  ga.A = (const cx<double>*)c->d_A;
+  ga.u = c->d_u;
+  ga.X = (const cx<double>*)c->d_X;
+  ga.L = (const cx<double>*)c->d_L;
+  ga.coef = c->d_coef;
+  ga.dJdu = d_dJdu;
+  ga.tiles = (long long)c->B * ((c->Nt + 15) / 16);
+  const size_t glds = blkp_grad_lds(bk.nwb, c->nu);
+  auto gk = c->nu == 1 ? k_blkp_grad<1> : k_blkp_grad<2>;
+  HIPCHK(c, blk_lds_attr(gk, glds));
+  int gpc = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&gpc, (const void*)gk, 256, glds) != hipSuccess || gpc < 1) gpc = 2;
+  const unsigned ggrid = (unsigned)std::max<long long>(1, std::min<long long>((ga.tiles + 3) / 4, (long long)c->ncu * gpc));
   const int mg = mark_begin(c, 3);
-  r = grad_rr_cap(c, d_dJdu, c->stream, 0, c->Nt, true, true);
+  hipLaunchKernelGGL(gk, dim3(ggrid), dim3(256), glds, c->stream, ga);
   mark_end(c, mg);
-  if (r) return r;
+  HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->d_coef_mu, c->d_coef, (size_t)c->B * 2 * c->m * sizeof(cx<double>),
                            hipMemcpyDeviceToDevice, c->stream));
   c->L_is_mu = true;
@@ -586,13 +632,16 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
     HIPCHK(c, hipMalloc((void**)&c->d_coef_mu, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
     c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
   }
-  int r = blk_big(c) ? ensure_pws(c) : QOC_OK;
-  if (r) return r;
+  int r;
   if (blkp_on(c)) {
     BlkArgs bk = blk_args(c);
     if ((r = blk_live(c, bk))) return r;
-    if (bk.nwb * c->m <= 8) return blkp_eval_concurrent(c, d_dJdu, bk);
+    const int waves = bk.nwb * c->m;
+    if (waves <= 8 && blkp_chain_lds(c->N, c->m, waves, blkp_chunk(waves)) <= 160 * 1024 &&
+        blkp_grad_lds(bk.nwb, c->nu) <= 160 * 1024)
+      return blkp_eval_concurrent(c, d_dJdu, bk);
   }
+  if ((r = blk_big(c) ? ensure_pws(c) : QOC_OK)) return r;
   if ((r = tchain_prep(c))) return r;
   TChainArgs gf = tchain_args(c);
   TChainArgs gb = tchain_args(c);

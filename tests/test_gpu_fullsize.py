@@ -102,6 +102,33 @@ def test_tunable_bus_full_size(built_lib, chain, monkeypatch):
     assert (info["chain_kernel"] == "blocks_mfma") == (chain == "auto")
 
 
+def test_tunable_bus_full_size_device_eval(built_lib):
+    """config 4 through the bench's entry point (qoc_eval_dev): the stored block propagators of the live 14-row block
+    (k_blkp_exp / k_blkp_dual / k_blkp_grad, seed groups pipelined over two streams), every seed of B = 512 over
+    Nt = 2000 slices against the C port."""
+    import torch
+    from qoc_amd import GrapeEngine, systems
+    mk_prob, mk_u, B = systems.CONFIGS["tunable_bus"]
+    prob = mk_prob()
+    u = mk_u(B, 0)
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
+    e.set_cost_trace(prob.x_target, prob.n)
+    ud = torch.from_numpy(np.ascontiguousarray(np.transpose(u, (0, 2, 1)))).cuda()
+    Jd = torch.empty(B, dtype=torch.float64, device="cuda")
+    gd = torch.empty(B, prob.Nt, prob.nu, dtype=torch.float64, device="cuda")
+    e.eval_device(ud.data_ptr(), 3, Jd.data_ptr(), gd.data_ptr())
+    e.synchronize()
+    info = e.info()
+    e.close()
+    assert info["chain_kernel"] == "blocks_prop16" and info["backward"] == "blocks_prop16", info
+    J = Jd.cpu().numpy()
+    g = np.transpose(gd.cpu().numpy(), (0, 2, 1))
+    Jc, gc = _cpu(prob, u)
+    assert np.abs(J - Jc).max() <= 1e-12, np.abs(J - Jc).max()
+    rel = max(np.linalg.norm(g[b] - gc[b]) / np.linalg.norm(gc[b]) for b in range(B))
+    assert rel <= 1e-10, rel
+
+
 def test_synthetic_full_size_fp32(built_lib, golden_dir):
     """config 5: synthetic GUE N=256, m=256 (x0 = I), nu=2, Nt=1000, B=128, fp32 on the large-N pipeline."""
     import qoc_oracle as O
