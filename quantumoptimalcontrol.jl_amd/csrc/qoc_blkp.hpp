@@ -74,6 +74,8 @@ __constant__ double kBlkpInvFact[33] = {1.0,
 struct BlkpArgs {
   int N, nu, nwb;
   int skew;                    // every Ã_j exactly skew-Hermitian (qoc_ctx::skew_exact, imaginary shifts)
+  int four;                    // complex products from four real ones (QOC_BLKP_4M)
+  int slack;                   // up to this many products more for each squaring fewer (QOC_BLKP_SLACK)
   long long unit0, units;      // this launch's units [unit0, units) of B Nt nwb: unit = (b Nt + k) nwb + β
   const int* wrow;             // nwb x 16 rows of the live wave blocks
   const cx<double>* At;        // (nu+1) N x N shifted generators Ã_j, column-major
@@ -115,6 +117,25 @@ __device__ __forceinline__ void blkp_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// the same product from four real ones (16 MFMAs, no cancellation in the imaginary part)
+template <bool INIT>
+__device__ __forceinline__ CMat cm_mul4(const CMat& Lt, const CMat& R, const CMat& I0) {
+  BV4 tr = INIT ? I0.r : BV4{0.0, 0.0, 0.0, 0.0};
+  BV4 ti = INIT ? I0.i : BV4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    tr = MF<double>::mma(Lt.r[e], R.r[e], tr);
+    ti = MF<double>::mma(Lt.r[e], R.i[e], ti);
+    tr = MF<double>::mma(-Lt.i[e], R.i[e], tr);
+    ti = MF<double>::mma(Lt.i[e], R.r[e], ti);
+  }
+  return CMat{tr, ti};
+}
+template <bool INIT>
+__device__ __forceinline__ CMat cm_mulx(bool four, const CMat& Lt, const CMat& R, const CMat& I0) {
+  return four ? cm_mul4<INIT>(Lt, R, I0) : cm_mul<INIT>(Lt, R, I0);
 }
 
 // C layout of X^T through the wave's LDS tile (row pitch 17: the transposed reads of a 16-lane row fall on distinct
@@ -235,6 +256,7 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
   const int WPG = BLKP_WG / 64;
   const long long TW = (long long)gridDim.x * WPG;
   unsigned long long prods = 0;
+  const bool four = a.four != 0;
   for (long long unit = a.unit0 + (long long)blockIdx.x * WPG + w; unit < a.units; unit += TW) {
     const long long bk = unit / nwb;
     const int beta = (int)(unit - bk * nwb);
@@ -262,17 +284,32 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
     const double rho = uniform_f64(fmin(sqrt(f2), sqrt(n1 * ninf)));
     // (the sharper α_p = max(‖X^p‖^{1/p}, ‖X^{p+1}‖^{1/(p+1)}) of Al-Mohy & Higham from the computed powers chose the
     // same (r, s) on the tunable bus -- 10.75 products per unit either way -- and cost three more reductions)
-    int r = BLKP_RMAX, s = 0, best = 1 << 30;
-    for (int rr = BLKP_RMIN; rr <= BLKP_RMAX; ++rr) {  // the fewest products r + 2 + s with 2^-s ρ̂ <= θ_{4r}
+    // the fewest products r + 2 + s with 2^-s ρ̂ <= θ_{4r}, or (slack) the fewest squarings within slack of that; each
+    // squaring doubles the rounding error the slice carries into the chain
+    int ssel[BLKP_RMAX + 1];
+    int best = 1 << 30;
+#pragma unroll
+    for (int rr = BLKP_RMIN; rr <= BLKP_RMAX; ++rr) {
       // s = max(0, ceil(log2(ρ̂ / θ))): with ρ̂ / θ = f 2^e, f in [0.5, 1), that is e, or e - 1 when f = 1/2
       const double q = rho / kBlkpTheta[rr];
       const int e = q > 1.0 ? __builtin_amdgcn_frexp_exp(q) : 0;
-      const int ss = q > 1.0 ? (__builtin_amdgcn_frexp_mant(q) == 0.5 ? e - 1 : e) : 0;
-      if (rr + 2 + ss < best) {
-        best = rr + 2 + ss;
+      ssel[rr] = q > 1.0 ? (__builtin_amdgcn_frexp_mant(q) == 0.5 ? e - 1 : e) : 0;
+      best = min(best, rr + 2 + ssel[rr]);
+    }
+    int r = BLKP_RMAX, s = 1 << 30;
+#pragma unroll
+    for (int rr = BLKP_RMAX; rr >= BLKP_RMIN; --rr)
+      if (rr + 2 + ssel[rr] <= best + a.slack && ssel[rr] < s) {
+        s = ssel[rr];
         r = rr;
-        s = ss;
       }
+    if (a.slack == 0) {  // the fewest products, the smaller r on ties (as measured for the default)
+#pragma unroll
+      for (int rr = BLKP_RMAX; rr >= BLKP_RMIN; --rr)
+        if (rr + 2 + ssel[rr] == best) {
+          s = ssel[rr];
+          r = rr;
+        }
     }
     {
       const double sc = ldexp(1.0, -s);
@@ -293,9 +330,9 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
     } else {
       Xt = cm_transpose(X, tile);
     }
-    const CMat X2 = cm_mul<false>(Xt, X, X);
-    const CMat X3 = cm_mul<false>(Xt, X2, X);
-    const CMat X4 = cm_mul<false>(Xt, X3, X);
+    const CMat X2 = cm_mulx<false>(four, Xt, X, X);
+    const CMat X3 = cm_mulx<false>(four, Xt, X2, X);
+    const CMat X4 = cm_mulx<false>(four, Xt, X3, X);
     CMat X4t;  // X^4 of a skew-Hermitian X is Hermitian: its transpose is conj(X^4)
     if (a.skew) {
 #pragma unroll
@@ -315,10 +352,10 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
         R.i[e] = fma(cm, X4.i[e], R.i[e]);
       }
     }
-    for (int i = r - 2; i >= 0; --i) R = cm_mul<true>(X4t, R, blkp_horner_b(i, X, X2, X3));
+    for (int i = r - 2; i >= 0; --i) R = cm_mulx<true>(four, X4t, R, blkp_horner_b(i, X, X2, X3));
     for (int t = 0; t < s; ++t) {
       const CMat Rt = cm_transpose(R, tile);
-      R = cm_mul<false>(Rt, R, R);
+      R = cm_mulx<false>(four, Rt, R, R);
     }
     const double mr = fma(u2, a.mur[2], fma(u1, a.mur[1], a.mur[0]));
     const double mi = fma(u2, a.mui[2], fma(u1, a.mui[1], a.mui[0]));

@@ -532,6 +532,11 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
   a.nwb = bk.nwb;
   a.skew = c->skew_exact && c->tprm.mur[0] == 0.0 && c->tprm.mur[1] == 0.0 && c->tprm.mur[2] == 0.0;
   a.units = units;
+  a.four = getenv("QOC_BLKP_4M") && atoi(getenv("QOC_BLKP_4M")) != 0;
+  // one product more for one squaring fewer (default): each squaring doubles the rounding error a slice carries over
+  // 2000 chained slices (tunable bus, all 512 seeds against the C port: max |ΔJ| 4.7e-12 with the fewest products,
+  // 9.1e-13 with slack 1 at 11.75 instead of 10.75 products per unit; tools/blkp_accuracy.py)
+  a.slack = getenv("QOC_BLKP_SLACK") ? std::max(0, atoi(getenv("QOC_BLKP_SLACK"))) : 1;
   a.wrow = bk.wrow;
   a.At = (const cx<double>*)c->d_At;
   a.u = c->d_u;
