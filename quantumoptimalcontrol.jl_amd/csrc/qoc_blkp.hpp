@@ -391,7 +391,11 @@ __host__ __device__ constexpr int blkp_wave_lds2(int CH) { return 32 + CH * 16 +
 __host__ __device__ inline size_t blkp_chain_lds(int N, int m, int waves, int CH) {
   return (size_t)(32 + 2 * N * m) * sizeof(double) + (size_t)waves * blkp_wave_lds2(CH) * sizeof(double2);
 }
-__host__ __device__ inline int blkp_chunk(int waves) { return waves <= 2 ? 4 : waves <= 4 ? 2 : 1; }
+// slices per chunk: the LDS of 4 one-wave chain workgroups per CU at CH = 4 (QOC_BLKP_CH overrides: 1, 2, 4, 8)
+__host__ __device__ inline int blkp_chunk(int waves, int parts = 1) {
+  (void)parts;  // CH = 8 beside the formation measured the same as 4 (1.63 vs 1.62 ms per group): latency, not DMA depth
+  return waves <= 2 ? 4 : waves <= 4 ? 2 : 1;
+}
 // 16 B per lane from src to LDS byte address lds + 16 lane (lds wave-uniform); M0 set and restored in the statement
 __device__ __forceinline__ void blkp_dma(const void* src, unsigned lds) {
   unsigned keep;
@@ -549,7 +553,10 @@ __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkAr
 template <int CH>
 __global__ __launch_bounds__(512) void k_blkp_dual(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk,
                                                    const double2* __restrict__ UF, const double2* __restrict__ UB,
-                                                   int seed0) {
+                                                   int seed0, int prio) {
+  // beside the formation's MFMA waves the chain's dependent VALU steps would queue behind their MFMAs: the chain wave
+  // can take the issue priority (prio, QOC_BLKP_PRIO)
+  if (prio) __builtin_amdgcn_s_setprio(3);
   const int i = blockIdx.x, B = gridDim.x >> 1;
   const bool by8 = (B & 7) == 0;
   const int dir = by8 ? (i >> 3) & 1 : i & 1;

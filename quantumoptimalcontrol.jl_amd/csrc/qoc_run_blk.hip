@@ -553,16 +553,21 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
   auto kern = c->nu == 1 ? (occ3 ? k_blkp_exp<1, 3> : k_blkp_exp<1, 2>) : (occ3 ? k_blkp_exp<2, 3> : k_blkp_exp<2, 2>);
   HIPCHK(c, blk_lds_attr(kern, lds));
   const int waves = bk.nwb * c->m;
-  const int ch = blkp_chunk(waves);
-  const size_t clds = blkp_chain_lds(c->N, c->m, waves, ch);
-  auto chain = ch == 4 ? k_blkp_dual<4> : ch == 2 ? k_blkp_dual<2> : k_blkp_dual<1>;
-  HIPCHK(c, blk_lds_attr(chain, clds));
   // The formation is MFMA-bound and the chains are bound by their propagator reads: the seeds go in `parts` groups,
   // the chains of group p (second stream) beside the formation of group p + 1, with the formation at two workgroups
   // per CU so that a chain workgroup fits beside them (QOC_BLKP_PARTS, default 4; 1: one formation, then the chains)
   int parts = 4;
   if (const char* pe = getenv("QOC_BLKP_PARTS")) parts = atoi(pe);
   parts = std::max(1, std::min(parts, c->B));
+  int ch = blkp_chunk(waves, parts);
+  if (const char* ce = getenv("QOC_BLKP_CH")) {
+    const int v = atoi(ce);
+    if (v == 1 || v == 2 || v == 4 || v == 8) ch = v;
+  }
+  if (blkp_chain_lds(c->N, c->m, waves, ch) > 160 * 1024) ch = blkp_chunk(waves);
+  const size_t clds = blkp_chain_lds(c->N, c->m, waves, ch);
+  auto chain = ch == 8 ? k_blkp_dual<8> : ch == 4 ? k_blkp_dual<4> : ch == 2 ? k_blkp_dual<2> : k_blkp_dual<1>;
+  HIPCHK(c, blk_lds_attr(chain, clds));
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, BLKP_WG, lds) != hipSuccess || per_cu < 1)
     per_cu = 2;
@@ -573,6 +578,10 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[parts], 0));
   }
   hipStream_t cs = parts > 1 ? c->stream2 : c->stream;
+  // QOC_BLKP_PRIO=1: the chain waves at the top issue priority.  Measured: each group's chains 1.63 -> 1.07 ms, the
+  // formation beside them 1.85 -> 1.97 ms per group, and the formation is the critical path (8.72 vs 8.93 ms per
+  // eval), so off by default
+  const int cprio = getenv("QOC_BLKP_PRIO") ? atoi(getenv("QOC_BLKP_PRIO")) : 0;
   for (int p = 0; p < parts; ++p) {
     const int s0 = (int)((long long)c->B * p / parts), s1 = (int)((long long)c->B * (p + 1) / parts);
     if (s1 <= s0) continue;
@@ -590,7 +599,7 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
     }
     mk = mark_begin(c, 1, cs);
     hipLaunchKernelGGL(chain, dim3(2 * (s1 - s0)), dim3(64 * waves), clds, cs, gf, gb, bk, (const double2*)a.UF,
-                       (const double2*)a.UB, s0);
+                       (const double2*)a.UB, s0, cprio);
     mark_end(c, mk, cs);
     HIPCHK(c, hipGetLastError());
   }
