@@ -629,7 +629,7 @@ def main():
             kern[k]["kernel"] = names[k]
         kern["k_expm"]["products_per_unit"] = prods / max(B * Nt * nlive, 1)
         kern["k_expm"]["executed_gflop_per_launch"] = f_exp / 1e9
-        kern["k_expm"]["hbm_bytes_per_launch"] = u_bytes
+        kern["k_expm"]["hbm_bytes_per_launch"] = u_bytes / max(lps["k_expm"], 1.0)  # one launch per seed group
         kern["k_chain_fwd"]["note"] = ("forward chain and mu recurrence of every seed in one launch, one matvec per "
                                        "slice from the stored propagators (LDS-DMA staged)")
         kern["k_chain_fwd"]["ns_per_serial_step"] = per_launch["k_chain_fwd"] * 1e6 / Nt
