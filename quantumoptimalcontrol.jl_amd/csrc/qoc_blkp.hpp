@@ -37,6 +37,15 @@ __constant__ double kBlkpTheta[9] = {0.0,
                                      2.3324673844012387,
                                      3.2752135590741402,
                                      4.3063288801167054};
+__constant__ double kBlkpInvTheta[9] = {0.0,
+                                        1.0 / 0.0016783942982781048,
+                                        1.0 / 0.06993278480782539,
+                                        1.0 / 0.33521368782861477,
+                                        1.0 / 0.8246031916386087,
+                                        1.0 / 1.504147322395163,
+                                        1.0 / 2.3324673844012387,
+                                        1.0 / 3.2752135590741402,
+                                        1.0 / 4.3063288801167054};
 __constant__ double kBlkpInvFact[33] = {1.0,
                                         1.0,
                                         0.5,
@@ -291,7 +300,7 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
 #pragma unroll
     for (int rr = BLKP_RMIN; rr <= BLKP_RMAX; ++rr) {
       // s = max(0, ceil(log2(ρ̂ / θ))): with ρ̂ / θ = f 2^e, f in [0.5, 1), that is e, or e - 1 when f = 1/2
-      const double q = rho / kBlkpTheta[rr];
+      const double q = rho * kBlkpInvTheta[rr];  // (a product: ρ̂ θ⁻¹ rounds the same side of 2^s but a few ulps)
       const int e = q > 1.0 ? __builtin_amdgcn_frexp_exp(q) : 0;
       ssel[rr] = q > 1.0 ? (__builtin_amdgcn_frexp_mant(q) == 0.5 ? e - 1 : e) : 0;
       best = min(best, rr + 2 + ssel[rr]);
@@ -359,7 +368,7 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
     }
     const double mr = fma(u2, a.mur[2], fma(u1, a.mur[1], a.mur[0]));
     const double mi = fma(u2, a.mui[2], fma(u1, a.mui[1], a.mui[0]));
-    const double em = exp(mr);
+    const double em = a.skew ? 1.0 : exp(mr);  // skew-Hermitian blocks: imaginary shifts
     double sn, cn;
     sincos(mi, &sn, &cn);
     const double pr = em * cn, pi = em * sn;
