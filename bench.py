@@ -498,7 +498,8 @@ def main():
     elif p16:
         # stored propagators: per (seed, slice, live block) one 16 x 16 exponential on v_mfma_f64_16x16x4 (executed
         # products counted by the kernel: qoc_chain_terms; 12 MFMAs of 2048 flops each, the three-real-product form),
-        # the two one-matvec chains reading UF / UB (4 KB per slice and direction) and writing the live rows' states,
+        # the two one-matvec chains each reading the one stored propagator (4 KB per slice and direction) and writing
+        # the live rows' states,
         # and the batched gradient (per 16 slices: 2(nu+1) co-state and 3 nu + 2 state-side 16 x 16 x 16 complex GEMMs
         # per live block and column, 12 MFMAs each)
         lsz = live_block_sizes(prob)
@@ -507,8 +508,8 @@ def main():
         f_exp = prods * 12 * 2048.0
         tiles = B * -(-Nt // 16)
         f_grad = tiles * nlive * m * (2 * (nu + 1) + 3 * nu + 2) * 12 * 2048.0
-        u_bytes = 2 * B * Nt * nlive * 256 * 16  # UF + UB
-        chain_bytes = u_bytes + 2 * B * Nt * float(np.sum(lsz)) * m * 16
+        u_bytes = B * Nt * nlive * 256 * 16  # written once by the formation
+        chain_bytes = 2 * u_bytes + 2 * B * Nt * float(np.sum(lsz)) * m * 16  # read by both chains
         grad_bytes = 2 * B * Nt * float(np.sum(lsz)) * m * 16 + B * Nt * nu * 8 * 2
         models = {
             "k_expm": ("mfma", f_exp / 1e12, "TFLOP/s", peak),

@@ -80,6 +80,12 @@ __constant__ double kBlkpInvFact[33] = {1.0,
                                         1.2161250415535179e-34,
                                         3.8003907548547434e-36};
 
+// position of U[r][c] (r, c < 16) in a slice's 256 entries: column quarter c & 3 of 64 entries, row group c >> 2 of 16,
+// row r swizzled by c.  The forward lane (i, q) reads U[i][4q + t] at 64t + 16q + (i ^ (4q + t)), the backward lane
+// reads U[4q + t][i] at 64(i & 3) + 16(i >> 2) + (i ^ (4q + t)): in either, the 16 lanes of a quarter hit 16 distinct
+// 16-byte slots modulo 16 (no LDS bank conflicts), and one 1 KB DMA piece holds one column quarter.
+__host__ __device__ constexpr int blkp_upos(int r, int c) { return 64 * (c & 3) + 16 * (c >> 2) + (r ^ c); }
+
 struct BlkpArgs {
   int N, nu, nwb;
   int skew;                    // every Ã_j exactly skew-Hermitian (qoc_ctx::skew_exact, imaginary shifts)
@@ -90,11 +96,9 @@ struct BlkpArgs {
   const cx<double>* At;        // (nu+1) N x N shifted generators Ã_j, column-major
   const double* u;             // B x Nt x nu
   double mur[3], mui[3];       // μ_k = μ_0 + Σ_j u_j μ_j
-  // U_k of the block (e^{μ_k} included) twice, units x 256 each, in the chains' lane order: UF holds U[i][4q + t] at
-  // [t][i + 16 q] (the forward's row quarters), UB holds (U^H)[i][4q + t] = conj(U[4q + t][i]) likewise (the
-  // backward's), so that each of a chain's four DMA pieces per slice reads 1 KB contiguous
+  // U_k of the block (e^{μ_k} included), units x 256: U[r][c] at blkp_upos(r, c), so that a chain's four DMA pieces
+  // per slice read 1 KB contiguous each and both chains read their quarters from LDS without bank conflicts
   double2* UF;
-  double2* UB;
   unsigned long long* prods;   // TERM_SLOTS counters: executed 16 x 16 complex products (nullptr: not counted)
 };
 
@@ -381,12 +385,10 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
     sincos(mi, &sn, &cn);
     const double pr = em * cn, pi = em * sn;
     double2* const uf = a.UF + unit * 256;
-    double2* const ubh = a.UB + unit * 256;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {  // this lane holds U[g + 4e][j]
       const double vr = fma(pr, R.r[e], -pi * R.i[e]), vi = fma(pr, R.i[e], pi * R.r[e]);
-      uf[(j & 3) * 64 + g + 4 * e + 16 * (j >> 2)] = make_double2(vr, vi);
-      ubh[g * 64 + j + 16 * e] = make_double2(vr, -vi);
+      uf[blkp_upos(g + 4 * e, j)] = make_double2(vr, vi);
     }
     prods += (unsigned long long)(r + 2 + s);
   }
@@ -445,8 +447,9 @@ __device__ __forceinline__ double2 blkp_dot4(const double (&ar)[4], const double
   return make_double2(r0 + r1, i0 + i1);
 }
 
-// FWD: x_{k+1} = U_k x_k from UF (lane (i, q) holds U_k[i][4q + t]); else μ_k = U_k^H μ_{k+1} from UB (lane (i, q)
-// holds (U_k^H)[i][4q + t]), μ_N = X_target (λ_k = coef ⊙ μ_k).  The forward ends with J and the λ_N coefficients.
+// FWD: x_{k+1} = U_k x_k (lane (i, q) reads U_k[i][4q + t]); else μ_k = U_k^H μ_{k+1} (lane (i, q) reads
+// (U_k^H)[i][4q + t] = conj(U_k[4q + t][i])), μ_N = X_target (λ_k = coef ⊙ μ_k).  The forward ends with J and the λ_N
+// coefficients.
 template <bool FWD, int CH>
 __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkArgs& bk, const double2* __restrict__ U,
                                                 const int b) {
@@ -488,6 +491,9 @@ __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkAr
   const double2* Ubase = U + (size_t)b * Nt * nwb * 256 + (size_t)ln.beta * 256 + l + z;
   const size_t ustep = (size_t)nwb * 256;
   const unsigned ub_lds = (unsigned)(size_t)(__attribute__((address_space(3))) double2*)Ub2;
+  int uo[4];  // this lane's four propagator entries within a slice's LDS copy
+#pragma unroll
+  for (int t = 0; t < 4; ++t) uo[t] = FWD ? blkp_upos(ln.i, 4 * ln.q + t) : blkp_upos(4 * ln.q + t, ln.i);
   // chunk cc's propagator quarters by DMA into buffer cc & 1 (1 KB contiguous per piece)
   auto issue = [&](int cc) __attribute__((always_inline)) {
 #pragma unroll
@@ -528,9 +534,9 @@ __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkAr
     double ur[4], ui[4];  // slice jj's propagator quarter, read one slice ahead (off the chain's critical path)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const double2 pv = Us[t * 64 + l];
+      const double2 pv = Us[uo[t]];
       ur[t] = pv.x;
-      ui[t] = pv.y;
+      ui[t] = FWD ? pv.y : -pv.y;
     }
     for (int jj = 0; jj < CH; ++jj) {
       if (j0 + jj >= Nt) break;
@@ -538,9 +544,9 @@ __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkAr
       const int jn = min(jj + 1, CH - 1);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const double2 pv = Us[(jn * 4 + t) * 64 + l];
+        const double2 pv = Us[jn * 256 + uo[t]];
         ur[t] = pv.x;
-        ui[t] = pv.y;
+        ui[t] = FWD ? pv.y : -pv.y;
       }
       y = xsum_rows2(y);
       xs[ln.i] = y;
@@ -575,8 +581,7 @@ __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkAr
 // (seeds seed0 .. seed0 + gridDim.x / 2 - 1)
 template <int CH>
 __global__ __launch_bounds__(512) void k_blkp_dual(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk,
-                                                   const double2* __restrict__ UF, const double2* __restrict__ UB,
-                                                   int seed0, int prio) {
+                                                   const double2* __restrict__ U, int seed0, int prio) {
   // beside the formation's MFMA waves the chain's dependent VALU steps would queue behind their MFMAs: the chain wave
   // can take the issue priority (prio, QOC_BLKP_PRIO)
   if (prio) __builtin_amdgcn_s_setprio(3);
@@ -584,8 +589,8 @@ __global__ __launch_bounds__(512) void k_blkp_dual(const TChainArgs gf, const TC
   const bool by8 = (B & 7) == 0;
   const int dir = by8 ? (i >> 3) & 1 : i & 1;
   const int seed = seed0 + (by8 ? ((i >> 4) << 3) | (i & 7) : i >> 1);
-  if (dir == 0) blkp_chain_body<true, CH>(gf, bk, UF, seed);
-  else blkp_chain_body<false, CH>(gb, bk, UB, seed);
+  if (dir == 0) blkp_chain_body<true, CH>(gf, bk, U, seed);
+  else blkp_chain_body<false, CH>(gb, bk, U, seed);
 }
 
 // ---- the order-3 gradient on the stored states (the reference's expm_jacobian! + _compute_u_sensitivity,

@@ -513,7 +513,7 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
     if ((r = blk_zero_dead(c, {c->d_X, c->d_L}))) return r;
   }
   const long long units = (long long)c->B * c->Nt * bk.nwb;
-  const size_t ubytes = (size_t)units * 2 * 256 * sizeof(double2);  // UF and UB
+  const size_t ubytes = (size_t)units * 256 * sizeof(double2);  // one propagator per unit
   if (c->blkU_bytes < ubytes) {
     if (c->d_blkU) {
       HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -545,7 +545,6 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
     a.mui[j] = j <= c->nu ? c->tprm.mui[j] : 0.0;
   }
   a.UF = (double2*)c->d_blkU;
-  a.UB = a.UF + (size_t)units * 256;
   a.prods = c->d_terms;  // qoc_chain_terms: executed 16 x 16 complex products on this path
   const size_t lds = (size_t)bk.nwb * 768 * sizeof(double2) + (size_t)(BLKP_WG / 64) * BLKP_TP * sizeof(double2);
   const char* oc = getenv("QOC_BLKP_OCC");
@@ -598,8 +597,8 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
       HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[p], 0));
     }
     mk = mark_begin(c, 1, cs);
-    hipLaunchKernelGGL(chain, dim3(2 * (s1 - s0)), dim3(64 * waves), clds, cs, gf, gb, bk, (const double2*)a.UF,
-                       (const double2*)a.UB, s0, cprio);
+    hipLaunchKernelGGL(chain, dim3(2 * (s1 - s0)), dim3(64 * waves), clds, cs, gf, gb, bk, (const double2*)a.UF, s0,
+                       cprio);
     mark_end(c, mk, cs);
     HIPCHK(c, hipGetLastError());
   }
