@@ -410,10 +410,12 @@ __host__ __device__ constexpr int blkp_wave_lds2(int CH) { return 32 + CH * 16 +
 __host__ __device__ inline size_t blkp_chain_lds(int N, int m, int waves, int CH) {
   return (size_t)(32 + 2 * N * m) * sizeof(double) + (size_t)waves * blkp_wave_lds2(CH) * sizeof(double2);
 }
-// slices per chunk: the LDS of 4 one-wave chain workgroups per CU at CH = 4 (QOC_BLKP_CH overrides: 1, 2, 4, 8)
+// slices per chunk (QOC_BLKP_CH overrides: 1, 2, 4, 8): one-wave chains (one live block, one state column: the tunable
+// bus) at CH = 8, 69 KB of LDS each (with the trimmed formation beside them 64.25k vs 63.79k evals/s at CH = 4, same
+// box, profiles/r05ab7/; before the trims the two measured the same), else the LDS of 4 chain waves per CU
 __host__ __device__ inline int blkp_chunk(int waves, int parts = 1) {
-  (void)parts;  // CH = 8 beside the formation measured the same as 4 (1.63 vs 1.62 ms per group): latency, not DMA depth
-  return waves <= 2 ? 4 : waves <= 4 ? 2 : 1;
+  (void)parts;
+  return waves <= 1 ? 8 : waves <= 2 ? 4 : waves <= 4 ? 2 : 1;
 }
 // 16 B per lane from src to LDS byte address lds + 16 lane (lds wave-uniform); M0 set and restored in the statement
 __device__ __forceinline__ void blkp_dma(const void* src, unsigned lds) {
@@ -437,11 +439,12 @@ struct BlkpLane {
   }
 };
 
-// Σ_t a_t b_t (complex) over this lane's quarter, two partial sums per part
+// Σ_t a_t b_t (complex) over this lane's quarter, two partial sums per part; every fma spelled out, so that each
+// chunk-size instantiation rounds alike (a free a b - c d is contracted either way round)
 __device__ __forceinline__ double2 blkp_dot4(const double (&ar)[4], const double (&ai)[4], const double (&br)[4],
                                              const double (&bi)[4]) {
-  const double r0 = fma(ar[0], br[0], fma(-ai[0], bi[0], ar[1] * br[1] - ai[1] * bi[1]));
-  const double r1 = fma(ar[2], br[2], fma(-ai[2], bi[2], ar[3] * br[3] - ai[3] * bi[3]));
+  const double r0 = fma(ar[0], br[0], fma(-ai[0], bi[0], fma(ar[1], br[1], -(ai[1] * bi[1]))));
+  const double r1 = fma(ar[2], br[2], fma(-ai[2], bi[2], fma(ar[3], br[3], -(ai[3] * bi[3]))));
   const double i0 = fma(ar[0], bi[0], fma(ai[0], br[0], fma(ar[1], bi[1], ai[1] * br[1])));
   const double i1 = fma(ar[2], bi[2], fma(ai[2], br[2], fma(ar[3], bi[3], ai[3] * br[3])));
   return make_double2(r0 + r1, i0 + i1);
