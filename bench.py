@@ -8,8 +8,14 @@ examples/ipopt_callbacks_exp.jl:11-31 without the spline map.  Inputs (u) are re
 in HBM before the timed region.  Seeds are sharded across ranks (weak scaling); the only
 collective is the RCCL all-gather of each rank's best (J, seed) per step.
 
-Run:  python bench.py [--gpus N --steps K --warmup W --config cavity]
+Run:  python bench.py [--gpus N --steps K --warmup W --config cavity --call-form fused]
       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+--call-form: "fused" (default) one device call per eval (qoc_eval_dev); "split" the reference's own call form,
+qoc_propagate_dev then qoc_grape_sensitivity_dev (Ipopt's f then f_grad, examples/ipopt_callbacks_exp.jl:11-31) on the
+same HBM-resident u; "ipopt" the Julia shim's callbacks verbatim: qoc_propagate_spline then qoc_sensitivity_spline with
+host spline coefficients (10 B-splines per control, PCIe and both host syncs inside the timed region: a latency figure,
+not the contract's resident-input rate).
 """
 from __future__ import annotations
 
@@ -140,6 +146,15 @@ def blkseg_unit_flops(nb, order, P=None, K=9):
     form = 478.0 + 26.0 * ((P or 8) + 1)
     prod, contr = 216.0, 86.0 + 518.0 * (order - 1)
     return form + prod, form + 2 * prod + 76.0 + contr + 2.0
+
+
+def blkseg_segments(B, Nt, nblk, ncu=256):
+    """Segments per seed of the segmented eval (qoc_run_blk.hip blkseg_shape): 8 waves per CU shared by the seeds a CU
+    holds, 64 / nblk segments per wave, then trimmed so that no segment is empty."""
+    per_cu = max(1, min(8, -(-B // ncu)))
+    S = max(1, min(max(1, 8 // per_cu) * (64 // max(1, nblk)), Nt))
+    L = -(-Nt // S)
+    return -(-Nt // L)
 
 
 def chain_bytes(N, m, Nt, B, esz):
@@ -316,6 +331,9 @@ def main():
     ap.add_argument("--seeds", type=int, default=0, help="override seeds per GPU")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--call-form", default="fused", choices=["fused", "split", "ipopt"],
+                    help="fused: qoc_eval_dev; split: qoc_propagate_dev + qoc_grape_sensitivity_dev; ipopt: the spline "
+                         "callbacks qoc_propagate_spline + qoc_sensitivity_spline on host coefficients")
     ap.add_argument("--cpu-plumbing", action="store_true",
                     help="no GPU: check the launcher and the best-(J, seed) exchange over gloo (CPU tests)")
     args = ap.parse_args()
@@ -348,6 +366,15 @@ def main():
     u_all = mk_u(B, rank)  # (B, nu, Nt), rank-seeded synthetic controls
     eng = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B, precision=prob.precision, device=local_rank)
     eng.set_cost_trace(prob.x_target, prob.n)
+    coef = None
+    if args.call_form == "ipopt":
+        # Ipopt's variables: 10 cubic B-spline coefficients per control (examples/zz_coupling_ipopt_exp.jl:27-37), in
+        # the config's control range; u = (Bs c)^T is what the kernels see (and what the parity leg checks)
+        ns = 10
+        Bs = systems.spline_matrix(float(prob.Nt), prob.Nt, ns)
+        coef = np.random.default_rng(1000 + rank).uniform(u_all.min(), u_all.max(), size=(B, ns, prob.nu))
+        u_all = np.ascontiguousarray(np.einsum("tn,bnj->bjt", Bs, coef))
+        eng.set_spline_basis(Bs)
 
     # device-resident buffers in the engine's layout: u[b, k, j]
     u_d = torch.from_numpy(np.ascontiguousarray(np.transpose(u_all, (0, 2, 1)))).to(dev)
@@ -373,7 +400,14 @@ def main():
         os.close(saved_fd)
 
     def step():
-        eng.eval_device(u_d.data_ptr(), args.order, J_d.data_ptr(), g_d.data_ptr())
+        if args.call_form == "fused":
+            eng.eval_device(u_d.data_ptr(), args.order, J_d.data_ptr(), g_d.data_ptr())
+        elif args.call_form == "split":
+            eng.propagate_device(u_d.data_ptr(), J_d.data_ptr())
+            eng.grape_sensitivity_device(u_d.data_ptr(), args.order, g_d.data_ptr())
+        else:
+            eng.propagate_spline(coef)
+            eng.sensitivity_spline(coef, args.order)
         if transport in ("rccl-libqoc", "local"):
             eng.allgather_best_device(best_d.data_ptr())  # on the engine stream, after its kernels
         elif world > 1:
@@ -415,6 +449,10 @@ def main():
     elapsed = float(el.item())
 
     phases = eng.phase_times()
+    if args.call_form == "ipopt":  # the parity leg checks the split kernels on the spline controls' u
+        eng.propagate_device(u_d.data_ptr(), J_d.data_ptr())
+        eng.grape_sensitivity_device(u_d.data_ptr(), args.order, g_d.data_ptr())
+        eng.synchronize()
     hist = eng.pade_histogram()
     thist = eng.taylor_histogram()
     terms = eng.chain_terms()  # Taylor-action chains: Σ P s over all slices, per direction
@@ -474,22 +512,35 @@ def main():
         else:
             ks = None
             f1, f3 = blkseg_unit_flops(nbk, args.order, p_avg)
-        flops = units * (f1 + f3)
-        hbm = B * Nt * nu * 8 * 4 + B * (8 + 2 * 2 * m * 16)
-        t = per_step["k_chain_bwd"] / 1e3
-        ach = flops / 1e12 / t if t > 0 else 0.0
-        kern = {"k_blkseg_eval": {
-            "ms_per_launch": per_launch["k_chain_bwd"], "launches_per_step": lps["k_chain_bwd"], "bound": "valu",
-            "achieved": ach, "unit": "TFLOP/s", "peak": peak, "frac": ach / peak,
-            "executed_gflop_per_launch": flops / 1e9, "flops_per_unit": {"phase1": f1, "phase3": f3},
-            "units_per_launch": units, "hbm_bytes_per_launch": hbm,
-            "hbm_gbs": hbm / 1e9 / t if t > 0 else 0.0, "taylor_degree": p_avg if nbk == 3 else None,
-            "series_degree_k": ({str(int(k)): int(np.sum(ks == k)) for k in np.unique(ks)} if ks is not None else None)}}
-        for k in ("k_expm", "k_chain_fwd", "k_grad"):
+        sdeg = {str(int(k)): int(np.sum(ks == k)) for k in np.unique(ks)} if ks is not None else None
+        # the split call form: the forward launch (phases 0-2, phase slot k_chain_fwd) writes G at the S segment ends
+        # (B S nblk nb^2 complex), the backward launch (phase 3, slot k_chain_bwd) reads them back
+        split_seg = lps["k_chain_fwd"] > 0
+        gbytes = B * blkseg_segments(B, Nt, nblk) * nblk * nbk * nbk * 16
+        parts = ([("k_blkseg_fwd", "k_chain_fwd", f1, B * Nt * nu * 8 * 2 + B * (8 + 2 * m * 16) + gbytes),
+                  ("k_blkseg_bwd", "k_chain_bwd", f3, B * Nt * nu * 8 * 3 + B * 2 * m * 16 * 2 + gbytes)]
+                 if split_seg else
+                 [("k_blkseg_eval", "k_chain_bwd", f1 + f3, B * Nt * nu * 8 * 4 + B * (8 + 2 * 2 * m * 16))])
+        kern = {}
+        for kname, slot, fu, hbm in parts:
+            flops = units * fu
+            t = per_step[slot] / 1e3
+            ach = flops / 1e12 / t if t > 0 else 0.0
+            kern[kname] = {
+                "ms_per_launch": per_launch[slot], "launches_per_step": lps[slot], "bound": "valu",
+                "achieved": ach, "unit": "TFLOP/s", "peak": peak, "frac": ach / peak,
+                "executed_gflop_per_launch": flops / 1e9,
+                "flops_per_unit": {"phase1": f1, "phase3": f3} if not split_seg else fu,
+                "units_per_launch": units, "hbm_bytes_per_launch": hbm,
+                "hbm_gbs": hbm / 1e9 / t if t > 0 else 0.0, "taylor_degree": p_avg if nbk == 3 else None,
+                "series_degree_k": sdeg}
+        for k in ("k_expm", "k_grad"):
             kern[k] = {"ms_per_launch": per_launch[k], "launches_per_step": lps[k]}
-        roof = {"kernel": "k_blkseg_eval", "bound": "valu", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
-                "frac": ach / peak, "traffic": traffic_all.get("k_blkseg_eval"), "traffic_source": traffic_src,
-                "ms_per_launch": per_launch["k_chain_bwd"], "launches_per_step": lps["k_chain_bwd"],
+        dom_k, dom_slot = max(((kn, sl) for kn, sl, _, _ in parts), key=lambda x: per_step[x[1]])
+        ach = kern[dom_k]["achieved"]
+        roof = {"kernel": dom_k, "bound": "valu", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
+                "frac": ach / peak, "traffic": traffic_all.get(dom_k), "traffic_source": traffic_src,
+                "ms_per_launch": per_launch[dom_slot], "launches_per_step": lps[dom_slot],
                 "blocks": [int(x) for x in bsz_s],
                 "note": ("segmented block eval, one launch per eval (csrc/qoc_blkseg.hpp): achieved = executed fp64 "
                          "flops per launch (bench.py blkseg_unit_flops x B Nt nblk) / launch time, against the fp64 "
@@ -509,12 +560,14 @@ def main():
         tiles = B * -(-Nt // 16)
         f_grad = tiles * nlive * m * (2 * (nu + 1) + 3 * nu + 2) * 12 * 2048.0
         u_bytes = B * Nt * nlive * 256 * 16  # written once by the formation
-        chain_bytes = 2 * u_bytes + 2 * B * Nt * float(np.sum(lsz)) * m * 16  # read by both chains
-        grad_bytes = 2 * B * Nt * float(np.sum(lsz)) * m * 16 + B * Nt * nu * 8 * 2
+        one_chain = u_bytes + B * Nt * float(np.sum(lsz)) * m * 16  # one direction: read every U_k, write the states
+        # the split call form runs the two directions as separate launches (k_blkp_chain: forward in propagate, μ in
+        # grape_sensitivity); the eval runs both in one (k_blkp_dual)
+        split16 = lps["k_chain_bwd"] > 0
         models = {
             "k_expm": ("mfma", f_exp / 1e12, "TFLOP/s", peak),
-            "k_chain_fwd": ("hbm", chain_bytes / 1e9, "GB/s", PEAK_HBM_GBS),
-            "k_chain_bwd": ("hbm", 0.0, "GB/s", PEAK_HBM_GBS),
+            "k_chain_fwd": ("hbm", (1 if split16 else 2) * one_chain / 1e9, "GB/s", PEAK_HBM_GBS),
+            "k_chain_bwd": ("hbm", one_chain / 1e9 if split16 else 0.0, "GB/s", PEAK_HBM_GBS),
             "k_grad": ("mfma", f_grad / 1e12, "TFLOP/s", peak),
         }
     elif blocks:
@@ -624,18 +677,25 @@ def main():
     if seg:
         pass  # kern and roof set above
     elif p16:
-        names = {"k_expm": "k_blkp_exp", "k_chain_fwd": "k_blkp_dual", "k_chain_bwd": "k_blkp_dual",
-                 "k_grad": "k_blkp_grad"}
-        for k in ("k_expm", "k_chain_fwd", "k_grad"):
+        names = {"k_expm": "k_blkp_exp", "k_chain_fwd": "k_blkp_chain" if split16 else "k_blkp_dual",
+                 "k_chain_bwd": "k_blkp_chain" if split16 else "k_blkp_dual", "k_grad": "k_blkp_grad"}
+        live_k = ("k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad") if split16 else ("k_expm", "k_chain_fwd", "k_grad")
+        for k in live_k:
             kern[k]["kernel"] = names[k]
+        # per-launch figures: the step's work over its launches (the formation runs once per seed group)
         kern["k_expm"]["products_per_unit"] = prods / max(B * Nt * nlive, 1)
-        kern["k_expm"]["executed_gflop_per_launch"] = f_exp / 1e9
-        kern["k_expm"]["hbm_bytes_per_launch"] = u_bytes / max(lps["k_expm"], 1.0)  # one launch per seed group
-        kern["k_chain_fwd"]["note"] = ("forward chain and mu recurrence of every seed in one launch, one matvec per "
-                                       "slice from the stored propagators (LDS-DMA staged)")
-        kern["k_chain_fwd"]["ns_per_serial_step"] = per_launch["k_chain_fwd"] * 1e6 / Nt
-        kern["k_grad"]["executed_gflop_per_launch"] = f_grad / 1e9
-        dom = max(("k_expm", "k_chain_fwd", "k_grad"), key=lambda k: per_step[k])
+        kern["k_expm"]["executed_gflop_per_launch"] = f_exp / 1e9 / max(lps["k_expm"], 1.0)
+        kern["k_expm"]["hbm_bytes_per_launch"] = u_bytes / max(lps["k_expm"], 1.0)
+        for k in ("k_chain_fwd", "k_chain_bwd") if split16 else ("k_chain_fwd",):
+            kern[k]["hbm_bytes_per_launch"] = models[k][1] * 1e9 / max(lps[k], 1.0)
+            kern[k]["ns_per_serial_step"] = per_launch[k] * 1e6 / Nt
+        kern["k_chain_fwd"]["note"] = (("forward chain alone (propagate), one matvec per slice from the stored "
+                                        "propagators (LDS-DMA staged); k_chain_bwd: the mu recurrence alone "
+                                        "(grape_sensitivity)") if split16 else
+                                       ("forward chain and mu recurrence of every seed in one launch, one matvec per "
+                                        "slice from the stored propagators (LDS-DMA staged)"))
+        kern["k_grad"]["executed_gflop_per_launch"] = f_grad / 1e9 / max(lps["k_grad"], 1.0)
+        dom = max(live_k, key=lambda k: per_step[k])
         roof = {"kernel": names[dom], "bound": kern[dom]["bound"], "achieved": kern[dom]["achieved"],
                 "peak": kern[dom]["peak"], "unit": kern[dom]["unit"], "frac": kern[dom]["frac"],
                 "traffic": traffic_all.get(names[dom]), "traffic_source": traffic_src,
@@ -728,7 +788,8 @@ def main():
         ach = gs["flops"] / 1e12 / (gs["ms"] / 1e3) if gs["ms"] > 0 else 0.0
         kern["phases_note"] = "large-N path: k_expm/k_chain_*/k_grad entries are phase totals per step"
         roof = {"kernel": "k_bgemm", "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s",
-                "frac": ach / peak, "traffic": traffic_all.get("k_bgemm"), "traffic_source": traffic_src,
+                "frac": ach / peak, "traffic": traffic_all.get("k_bgemm_glds", traffic_all.get("k_bgemm")),
+                "traffic_source": traffic_src,
                 "ms_per_launch": gs["ms"] / max(gs["launches"], 1),
                 "launches_per_step": gs["launches"] / K,
                 "gflop_per_launch": gs["flops"] / max(gs["launches"], 1) / 1e9,
@@ -778,6 +839,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": WORKLOADS[args.config], "name": args.config, "N": N, "m": m, "nu": nu,
                        "Nt": Nt, "seeds_per_gpu": B, "global_seeds": B * world, "order": args.order,
+                       "call_form": args.call_form,
                        "parallelism": f"seed-sharded x{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -195,8 +195,12 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
  * from the serial chain, one block matvec per slice (the default for blocks of <= 4 rows); QOC_BLOCKS=0 at
  * qoc_set_generators keeps the dense kernels).  QOC_FORCE_LARGE_N=1 in the environment at qoc_create selects the
  * large-N path for any size (testing).  qoc_get_info_n takes the capacity of info and fails (QOC_ERR_ARG) when it is
- * below QOC_INFO_ENTRIES; qoc_get_info (no capacity) writes QOC_INFO_ENTRIES entries. */
-#define QOC_INFO_ENTRIES 11
+ * below QOC_INFO_ENTRIES; qoc_get_info (no capacity) writes QOC_INFO_ENTRIES entries.  info[11] = what the last
+ * propagate left for grape_sensitivity (the reference's split call form, examples/ipopt_callbacks_exp.jl:11-31):
+ * 0 the states x_k, 1 the segmented forward (blocks of 2-3 rows: G at every segment's end, x_k rebuilt on demand;
+ * grape_sensitivity then runs the segmented backward alone), 2 the stored propagators of blocks of 5..16 rows
+ * (grape_sensitivity: the co-state chain and the gradient on them). */
+#define QOC_INFO_ENTRIES 12
 int qoc_get_info(qoc_ctx* ctx, long long* info /*[QOC_INFO_ENTRIES]*/);
 int qoc_get_info_n(qoc_ctx* ctx, long long* info, int n);
 

@@ -16,9 +16,10 @@
 //   * k_blkp_dual: the forward chain x_{k+1} = U_k x_k and the μ recurrence μ_k = U_k^H μ_{k+1} (μ_N = X_target,
 //     λ_k = coef ⊙ μ_k) from the stored propagators, one wave per (seed, block, column, direction): lane i + 16 q
 //     takes row i and the column quarter 4q..4q+3 of U_k, the quarters are summed with permlane swaps and the new
-//     state goes to the next slice through a 16-entry LDS row.  Beside the chain each wave forms Ã_k's block rows and
-//     writes the order-3 gradient's captures D1 = Ã_k v, D2 = Ã_k D1 (v = x_k forward, Ã_k^H and μ_{k+1} backward),
-//     which k_grad_rr_c contracts with scale 1 and κ = 1 (qoc_grad_rr.hpp).
+//     state goes to the next slice through a 16-entry LDS row.  k_blkp_chain runs one direction alone (the split
+//     call form: the forward chain in propagate, the μ recurrence in grape_sensitivity).
+//   * k_blkp_grad: the order-3 gradient from x_k and μ_{k+1}, 16 slices per wave as the columns of 16 x 16 x 16
+//     generator GEMMs on MFMA.
 #pragma once
 #include "qoc_blk.hpp"
 
@@ -96,9 +97,11 @@ struct BlkpArgs {
   const cx<double>* At;        // (nu+1) N x N shifted generators Ã_j, column-major
   const double* u;             // B x Nt x nu
   double mur[3], mui[3];       // μ_k = μ_0 + Σ_j u_j μ_j
-  // U_k of the block (e^{μ_k} included), units x 256: U[r][c] at blkp_upos(r, c), so that a chain's four DMA pieces
-  // per slice read 1 KB contiguous each and both chains read their quarters from LDS without bank conflicts
+  // U_k of the block (e^{μ_k} included), 256 entries per unit from unit ubase on: U[r][c] at blkp_upos(r, c), so that
+  // a chain's four DMA pieces per slice read 1 KB contiguous each and both chains read their quarters from LDS without
+  // bank conflicts (the eval keeps two seed groups' slabs, the split propagate every seed's)
   double2* UF;
+  long long ubase;
   unsigned long long* prods;   // TERM_SLOTS counters: executed 16 x 16 complex products (nullptr: not counted)
 };
 
@@ -384,7 +387,7 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
     double sn, cn;
     sincos(mi, &sn, &cn);
     const double pr = em * cn, pi = em * sn;
-    double2* const uf = a.UF + unit * 256;
+    double2* const uf = a.UF + (unit - a.ubase) * 256;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {  // this lane holds U[g + 4e][j]
       const double vr = fma(pr, R.r[e], -pi * R.i[e]), vi = fma(pr, R.i[e], pi * R.r[e]);
@@ -455,7 +458,7 @@ __device__ __forceinline__ double2 blkp_dot4(const double (&ar)[4], const double
 // coefficients.
 template <bool FWD, int CH>
 __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkArgs& bk, const double2* __restrict__ U,
-                                                const int b) {
+                                                const int b, const int useed0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* red = reinterpret_cast<double*>(smem);
   double* xN = red + 32;
@@ -491,7 +494,7 @@ __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkAr
   }
   int z;
   asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // per-lane (VGPR) source addresses
-  const double2* Ubase = U + (size_t)b * Nt * nwb * 256 + (size_t)ln.beta * 256 + l + z;
+  const double2* Ubase = U + (size_t)(b - useed0) * Nt * nwb * 256 + (size_t)ln.beta * 256 + l + z;  // U: seed useed0's
   const size_t ustep = (size_t)nwb * 256;
   const unsigned ub_lds = (unsigned)(size_t)(__attribute__((address_space(3))) double2*)Ub2;
   int uo[4];  // this lane's four propagator entries within a slice's LDS copy
@@ -581,10 +584,10 @@ __device__ __forceinline__ void blkp_chain_body(const TChainArgs& g, const BlkAr
 
 // forward chain and μ recurrence of every seed in one launch of 2B workgroups (seed-direction interleave as
 // k_blkrot_dual), nwb m waves each
-// (seeds seed0 .. seed0 + gridDim.x / 2 - 1)
+// (seeds seed0 .. seed0 + gridDim.x / 2 - 1; U holds the propagators from seed useed0 on)
 template <int CH>
 __global__ __launch_bounds__(512) void k_blkp_dual(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk,
-                                                   const double2* __restrict__ U, int seed0, int prio) {
+                                                   const double2* __restrict__ U, int seed0, int useed0, int prio) {
   // beside the formation's MFMA waves the chain's dependent VALU steps would queue behind their MFMAs: the chain wave
   // can take the issue priority (prio, QOC_BLKP_PRIO)
   if (prio) __builtin_amdgcn_s_setprio(3);
@@ -592,8 +595,18 @@ __global__ __launch_bounds__(512) void k_blkp_dual(const TChainArgs gf, const TC
   const bool by8 = (B & 7) == 0;
   const int dir = by8 ? (i >> 3) & 1 : i & 1;
   const int seed = seed0 + (by8 ? ((i >> 4) << 3) | (i & 7) : i >> 1);
-  if (dir == 0) blkp_chain_body<true, CH>(gf, bk, U, seed);
-  else blkp_chain_body<false, CH>(gb, bk, U, seed);
+  if (dir == 0) blkp_chain_body<true, CH>(gf, bk, U, seed, useed0);
+  else blkp_chain_body<false, CH>(gb, bk, U, seed, useed0);
+}
+
+// one direction alone (the reference's split call form: the forward chain in propagate, the μ recurrence in
+// grape_sensitivity), one workgroup per seed seed0 + blockIdx.x; stale: a stale-u flag queued before the launch
+// (nonzero: nothing is written)
+template <bool FWD, int CH>
+__global__ __launch_bounds__(512) void k_blkp_chain(const TChainArgs g, const BlkArgs bk, const double2* __restrict__ U,
+                                                    int seed0, int useed0, const int* stale) {
+  if (stale && *stale != 0) return;
+  blkp_chain_body<FWD, CH>(g, bk, U, seed0 + (int)blockIdx.x, useed0);
 }
 
 // ---- the order-3 gradient on the stored states (the reference's expm_jacobian! + _compute_u_sensitivity,
@@ -614,6 +627,8 @@ struct BlkpGradArgs {
   const cx<double>* coef;    // B x 2m λ_N coefficients
   double* dJdu;              // B x Nt x nu
   long long tiles;           // B ceil(Nt / 16)
+  const int* stale;          // a stale-u flag queued before the launch (nonzero: nothing is written), or nullptr
+  cx<double>* coef_out;      // a copy of coef (qoc_get_costates' λ = coef ⊙ μ), written by workgroup 0, or nullptr
 };
 __host__ __device__ inline size_t blkp_grad_lds(int nwb, int nu) { return (size_t)nwb * (nu + 1) * 2 * 256 * sizeof(double2); }
 
@@ -634,9 +649,14 @@ __device__ __forceinline__ void blkp_axpy(CMat& Y, double a, const CMat& X) {  /
 template <int NU>
 __global__ __launch_bounds__(256, 2) void k_blkp_grad(const BlkpGradArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (a.stale && *a.stale != 0) return;
   double2* gen = reinterpret_cast<double2*>(smem);  // [β][j][form][e][lane]: form 0 A_j, form 1 A_j^H as left operands
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, jl = l & 15, g = l >> 4;
   const int N = a.N, m = a.m, Nt = a.Nt, nwb = a.nwb;
+  if (a.coef_out && blockIdx.x == 0) {
+    const long long nc = a.tiles / ((Nt + 15) / 16) * 2 * m;  // B 2m
+    for (long long e = tid; e < nc; e += blockDim.x) a.coef_out[e] = a.coef[e];
+  }
   const size_t NN = (size_t)N * N, Nm = (size_t)N * m;
   const int ngen = nwb * (NU + 1) * 2 * 256;
   for (int e = tid; e < ngen; e += blockDim.x) {

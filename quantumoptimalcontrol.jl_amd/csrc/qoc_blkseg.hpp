@@ -22,6 +22,12 @@
 //            summed over the slice's blocks (a wave-private LDS slot, fixed order: no atomics).
 // Neither x_k, λ_k nor U_k go to HBM: the launch reads u and writes J, the λ_N coefficients and dJdu.  qoc_get_states
 // and qoc_get_costates rebuild x_k / λ_k on demand with the k_blku_* chains (qoc_run_blk.hip).
+//
+// The reference's own call form runs the two halves apart: Ipopt's f calls propagate, its f_grad grape_sensitivity
+// (examples/ipopt_callbacks_exp.jl:11-31; f alone in every line-search trial).  MODE splits the launch at the end of
+// phase 2 (BLKSEG_FWD: phases 0-2, which also write G at every segment's end, Q_s G_0 Q_s^H, to HBM: S nblk NB^2
+// complex per seed, 31 KB at cavity size) and BLKSEG_BWD (phase 0's records and (J, P) again -- the same arithmetic on
+// the same u, so the same values -- then phase 3 from those G): bitwise the fused launch's J and dJdu.
 #pragma once
 #include "qoc_blku.hpp"
 
@@ -47,7 +53,12 @@ struct BlksegParams {
   unsigned int* done;
   double* best;
   long long seed_offset;
+  // the split launches: G at every segment's end, B x [NB^2][S][nblk] complex (written by BLKSEG_FWD, read by
+  // BLKSEG_BWD); stale: the stale-u flag of the check queued before BLKSEG_BWD (nonzero: the launch writes nothing)
+  double2* gseg;
+  const int* stale;
 };
+enum { BLKSEG_FUSED = 0, BLKSEG_FWD = 1, BLKSEG_BWD = 2 };
 
 // LDS, in doubles: shifted generator blocks [nblk][3][E] complex | step records [Nt][4] | segment products [S][E][nblk]
 // complex | G_0 [E][nblk] complex | x_0 then x_N (N m complex) | λ_N coefficients (2 m complex) | scratch (24) |
@@ -519,9 +530,12 @@ struct SegProg {
 // One workgroup per seed (blockIdx.x), W = blockDim / 64 waves, UPW segments of nblk lanes per wave (lanes past
 // UPW nblk idle).  Built-in costs only (TRACE / ZCAL), no state penalty, no co-state source, unpacked states,
 // skew-Hermitian generators (the host's blkseg_ok).
-template <int NB, int ORD, int WMAX>
+template <int NB, int ORD, int WMAX, int MODE = BLKSEG_FUSED>
 __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, const BlkArgs bk, const BlksegParams sp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if constexpr (MODE == BLKSEG_BWD) {  // a stale u (the check queued before this launch): leave every output alone
+    if (sp.stale && *sp.stale != 0) return;
+  }
   constexpr int E = NB * NB;
   // the lane's generator blocks in registers (blocks of 2 rows at <= 8 waves), else from LDS where used; blocks of 2
   // rows keep Â for X = A_k and accumulate M in the contraction
@@ -556,10 +570,12 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       if (j <= nu && ri >= 0 && rk >= 0) v = At[(size_t)j * NN + ri + (size_t)N * rk];
       gsh[q] = make_double2(v.r, v.i);
     }
-    const cx<double>* x0 = (const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0);
-    for (size_t o = tid; o < Nm; o += nthr) {
-      xN[2 * o] = x0[o].r;
-      xN[2 * o + 1] = x0[o].i;
+    if constexpr (MODE != BLKSEG_BWD) {
+      const cx<double>* x0 = (const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0);
+      for (size_t o = tid; o < Nm; o += nthr) {
+        xN[2 * o] = x0[o].r;
+        xN[2 * o + 1] = x0[o].i;
+      }
     }
   }
   // one pass over u: ρ_k, the copies of u (the stale check, the lazy rebuilds) and the records
@@ -716,6 +732,19 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       else p1_fast(jj, std::true_type(), K_);
     }
   };
+  // G at the end of the lane's segment (phase 3's start): formed here, or read back (BLKSEG_BWD)
+  double Gr[E], Gi[E];
+  auto gseg_at = [&](int e) -> double2& { return sp.gseg[(((size_t)b * E + e) * S + s) * nblk + beta]; };
+  if constexpr (MODE == BLKSEG_BWD) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const double2 v = sact ? gseg_at(e) : make_double2(0.0, 0.0);
+      Gr[e] = v.x;
+      Gi[e] = v.y;
+    }
+    // the co-states' rebuild source (blku_costates): this u (copied in the prologue) and the forward's λ_N coefficients
+    if (sp.coef2 && tid < 2 * m) sp.coef2[(size_t)b * 2 * m + tid] = g.coef[(size_t)b * 2 * m + tid];
+  } else {
   if (fast) {
     if (ksel == 5) loop1(std::integral_constant<int, 5>());
     else if (ksel == 7) loop1(std::integral_constant<int, 7>());
@@ -866,6 +895,12 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   // (J, seed) of the launch (k_argmin_seed's order: NaN never wins, ties go to the lower seed).  The hand-off is the
   // write-through form of the guide's counter recipe (cdna_hip_programming.md, split-K combine / Guideline 16 R1):
   // J stored sc1, vmcnt(0), relaxed agent counter add; the last adder acquires and then reads every J.
+  // This hand-off leans on gfx950's memory subsystem (the write-through sc1 store is complete at vmcnt(0), before the
+  // counter add), not on a release/acquire pair, which would write back the whole L2 of the XCD; the build targets
+  // gfx950 only (the check below keeps another target from compiling it silently).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "k_blkseg_eval's best-(J, seed) hand-off is written for gfx950"
+#endif
   const bool early = W <= 4;
   auto publish = [&]() {
     if (w != 0 || !sp.done) return;
@@ -881,7 +916,9 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       double bv = __builtin_inf();
       long long bi = -1;
       for (int e = l; e < (int)gridDim.x; e += 64) {
-        const double v = g.J[e];
+        // agent-scope atomic loads (sc1 on gfx950): the other workgroups' J stores were write-through at agent scope
+        const double v = __longlong_as_double((long long)__hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(g.J + e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (v < bv || (v == bv && e < bi)) {
           bv = v;
           bi = e;
@@ -929,7 +966,6 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   }
   __syncthreads();
   // G at the segment's end: Q_s G_0 Q_s^H
-  double Gr[E], Gi[E];
   {
     double hr[E], hi[E], tr[E], ti[E];
 #pragma unroll
@@ -943,8 +979,17 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   }
 
   if (!early) publish();
+  BK_T(t2e);
+  BK_ADD(2, t2e - t2);
+  if constexpr (MODE == BLKSEG_FWD) {  // the forward half ends here: G to HBM for the backward launch
+    if (sact)
+#pragma unroll
+      for (int e = 0; e < E; ++e) gseg_at(e) = make_double2(Gr[e], Gi[e]);
+    if (sp.terms && tid == 0) atomicAdd(sp.terms + b % TERM_SLOTS, (unsigned long long)Nt * ((unsigned long long)P << J));
+    return;
+  }
+  }  // MODE != BLKSEG_BWD
   BK_T(t3);
-  BK_ADD(2, t3 - t2);
   // ---- phase 3: each segment backwards, the gradient of every slice ----
   const double mu1r = sp.mur[1], mu1i = sp.mui[1], mu2r = sp.mur[2], mu2i = sp.mui[2];
   double* const wr = wred + 128 * RB * w;
@@ -1075,7 +1120,8 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   __syncthreads();
   double* const og = sp.dJdu + (size_t)b * Nt * nu;
   for (int i = tid; i < Nt * nu; i += nthr) og[i] = dJ[i];
-  if (sp.terms && tid == 0) atomicAdd(sp.terms + b % TERM_SLOTS, (unsigned long long)Nt * ((unsigned long long)P << J));
+  if (MODE == BLKSEG_FUSED && sp.terms && tid == 0)
+    atomicAdd(sp.terms + b % TERM_SLOTS, (unsigned long long)Nt * ((unsigned long long)P << J));
   BK_T(t5);
   BK_ADD(4, t5 - t4);
   BK_ADD(5, t5 - t0);

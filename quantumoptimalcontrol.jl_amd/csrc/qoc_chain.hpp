@@ -682,10 +682,19 @@ __global__ __launch_bounds__(GRAD_THREADS) void k_grad(int N, int m, int nu, int
 // ---------------------------------------------------------------------------
 // Small helpers used by the host API.
 // ---------------------------------------------------------------------------
-static __global__ void k_compare_u(const double* __restrict__ a, const double* __restrict__ b, size_t n, int* flag) {
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
-    // bitwise comparison (the reference's `u != cache.u` is elementwise ==; NaN never occurs here)
-    if (__double_as_longlong(a[e]) != __double_as_longlong(b[e])) atomicOr(flag, 1);
+// The stale-u check (bitwise: the reference's `u != cache.u` is elementwise ==, and NaN never occurs here) without a
+// memset or a copy around it: mismatches set the device flag
+// `cur` (read by the split backward's launches behind this one) and the host-mapped flag `host` (the host zeroes it
+// before the launch and reads it after the launch's event); block 0 zeroes `next`, the device flag of the next check.
+static __global__ void k_compare_u_flags(const double* __restrict__ a, const double* __restrict__ b, size_t n, int* cur,
+                                         int* next, int* host) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *next = 0;
+  bool diff = false;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    diff = diff || __double_as_longlong(a[e]) != __double_as_longlong(b[e]);
+  if (__any(diff) && (threadIdx.x & 63) == 0) {
+    atomicOr(cur, 1);
+    __hip_atomic_store(host, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

@@ -321,14 +321,30 @@ RcclApi& rccl() {
   return api;
 }
 
-int forward(qoc_ctx* c) {
-  c->X_lazy = false;  // every forward path writes x_k
+// d_src: the caller's device u when it is not yet in d_u (the segmented forward copies it itself), d_J: the caller's J
+// buffer (written by that launch; the other paths leave J in d_J)
+int forward(qoc_ctx* c, const double* d_src = nullptr, double* d_J = nullptr) {
+  c->X_lazy = false;  // every forward path but the segmented one writes x_k
   c->best_ready = false;
-  if (blk_active(c)) return blk_forward(c);
-  if (c->big) return c->prec == QOC_FP64 ? big_forward<double>(c) : big_forward<float>(c);
-  return c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
+  c->fwd_kind = 0;
+  if (blkseg_split_ok(c)) return blkseg_forward(c, d_src ? d_src : c->d_u, d_J);
+  if (d_src && d_src != c->d_u)
+    HIPCHK(c, hipMemcpyAsync(c->d_u, d_src, (size_t)c->B * c->nu * c->Nt * sizeof(double), hipMemcpyDeviceToDevice,
+                             c->stream));
+  int r = QOC_OK;
+  if (blk_active(c)) r = blk_forward(c);
+  else if (c->big) r = c->prec == QOC_FP64 ? big_forward<double>(c) : big_forward<float>(c);
+  else r = c->prec == QOC_FP64 ? run_forward<double>(c) : run_forward<float>(c);
+  if (r == QOC_OK && d_J && d_J != c->d_J)
+    HIPCHK(c, hipMemcpyAsync(d_J, c->d_J, c->B * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  return r;
 }
-int backward(qoc_ctx* c, int order, double* d_dJdu) {
+// stale: a device stale-u flag the segmented backward checks itself (queue_stale_check), or nullptr
+int backward(qoc_ctx* c, int order, double* d_dJdu, const int* stale = nullptr) {
+  // the segmented forward left G at every segment's end: the backward half only (x_k never formed); the stored block
+  // propagators: the μ recurrence and the gradient on them
+  if (c->fwd_kind == 1 && blkseg_ok(c, order)) return blkseg_backward(c, order, d_dJdu, stale);
+  if (blkp_backward_ok(c, order)) return blkp_backward(c, d_dJdu, stale);
   if (c->cost_kind == QOC_COST_EXTERNAL || c->src_on) c->dead_dirty = true;  // λ may be nonzero on dead rows
   if (c->X_lazy) {  // after a segmented eval: the backward paths read x_k
     const int r = blku_states(c);
@@ -343,6 +359,32 @@ int backward(qoc_ctx* c, int order, double* d_dJdu) {
   if (c->big)
     return c->prec == QOC_FP64 ? big_backward<double>(c, order, d_dJdu) : big_backward<float>(c, order, d_dJdu);
   return c->prec == QOC_FP64 ? run_backward<double>(c, order, d_dJdu) : run_backward<float>(c, order, d_dJdu);
+}
+
+// the bitwise comparison of d_u with the u of the last propagate (src/gradient_computations.jl:37-39) on the stream,
+// one launch: its device flag (returned in *dflag, for launches queued behind it) and the host-mapped flag c->h_flag,
+// read at c->flag_ev (wait_stale_check).  The two device flags take turns, each check zeroing the next one's.
+int queue_stale_check(qoc_ctx* c, const double* d_u, const int** dflag) {
+  if (!c->h_flag) HIPCHK(c, hipHostMalloc((void**)&c->h_flag, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+  if (!c->flag_ev) HIPCHK(c, hipEventCreateWithFlags(&c->flag_ev, hipEventDisableTiming));
+  int* hdev = nullptr;
+  HIPCHK(c, hipHostGetDevicePointer((void**)&hdev, c->h_flag, 0));
+  const size_t nu_t = (size_t)c->B * c->nu * c->Nt;
+  const int cur = c->flag_turn, nxt = cur ^ 1;
+  c->flag_turn = nxt;
+  *(volatile int*)c->h_flag = 0;  // no launch that writes it is pending: the last one's event was waited for
+  const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((nu_t + 255) / 256, 1024));
+  hipLaunchKernelGGL(k_compare_u_flags, dim3(grid), dim3(256), 0, c->stream, d_u, c->d_u, nu_t, c->d_flag + cur,
+                     c->d_flag + nxt, hdev);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->flag_ev, c->stream));
+  if (dflag) *dflag = c->d_flag + cur;
+  return QOC_OK;
+}
+int wait_stale_check(qoc_ctx* c) {
+  HIPCHK(c, hipEventSynchronize(c->flag_ev));
+  if (*(volatile int*)c->h_flag) return fail(c, QOC_ERR_STALE, "Cache data from other control signal u");
+  return QOC_OK;
 }
 
 int check_ready(qoc_ctx* c) {
@@ -403,7 +445,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
       {&c->d_x0, (size_t)B * Nm * c->esz},
       {&c->d_Xt, Nm * c->esz},
       {(void**)&c->d_pmask, Nm},
-      {(void**)&c->d_u, (size_t)B * nu * Nt * sizeof(double) + 16},  // + 16: k_blkp_dual's 16-byte u reads
+      {(void**)&c->d_u, (size_t)B * nu * Nt * sizeof(double) + 16},  // + 16: slack past the last control
       {&c->d_U, (size_t)B * Nt * NN * c->esz},
       {&c->d_X, (size_t)B * (Nt + 1) * Nm * c->esz},
       {&c->d_L, (size_t)B * (Nt + 1) * Nm * c->esz},
@@ -411,7 +453,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
       {(void**)&c->d_coef, (size_t)B * 2 * m * sizeof(cx<double>)},
       {(void**)&c->d_rsec, (size_t)N},
       {(void**)&c->d_dJdu, (size_t)B * nu * Nt * sizeof(double)},
-      {(void**)&c->d_flag, sizeof(int)},
+      {(void**)&c->d_flag, 2 * sizeof(int)},  // [0] the synchronous checks, [0] / [1] in turns the queued ones
       {(void**)&c->d_hist, 13 * 64 * sizeof(unsigned long long)},
       {(void**)&c->d_sink, TCHAIN_SINK * sizeof(double)},
       {(void**)&c->d_ps, ((size_t)std::max<long long>((long long)B * Nt, 16384) + 1) * sizeof(int)},
@@ -420,6 +462,7 @@ int qoc_create(qoc_ctx** out, int device, int N, int m, int nu, int Nt, int B, i
     if ((e = hipMalloc(a.p, a.bytes)) != hipSuccess) return bail(e, "hipMalloc");
     c->dev_bytes += a.bytes;
   }
+  if ((e = hipMemset(c->d_flag, 0, 2 * sizeof(int))) != hipSuccess) return bail(e, "hipMemset");
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
@@ -512,6 +555,9 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->d_wrow_live) hipFree(c->d_wrow_live);
   if (c->d_dead_rows) hipFree(c->d_dead_rows);
   if (c->d_gc_part) hipFree(c->d_gc_part);
+  if (c->d_gseg) hipFree(c->d_gseg);
+  if (c->h_flag) hipHostFree(c->h_flag);
+  if (c->flag_ev) hipEventDestroy(c->flag_ev);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L, c->d_u_lam, c->d_coef_lam, c->d_blkU, c->d_J_scr, c->d_coef_scr,
                   c->d_J, c->d_coef, c->d_dJdu, c->d_flag, c->d_hist, c->d_stage, c->d_ws, c->d_red, c->d_Bs, c->d_cstage, c->d_fws, c->d_AH, c->d_Cst, c->d_gws, c->d_pws, c->d_ps, c->d_At, c->d_steps, c->d_terms, c->d_src, c->d_rsec, c->d_sink, c->d_blkrec};
   for (void* p : ptrs)
@@ -882,12 +928,8 @@ int qoc_propagate_dev(qoc_ctx* c, const double* d_u, double* d_J) {
   int r = check_ready(c);
   if (r) return r;
   if (!d_u) return fail(c, QOC_ERR_ARG, "d_u is null");
-  const size_t nu_t = (size_t)c->B * c->nu * c->Nt;
-  if (d_u != c->d_u) HIPCHK(c, hipMemcpyAsync(c->d_u, d_u, nu_t * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
-  r = forward(c);
+  r = forward(c, d_u, d_J);  // u into d_u (kept for the stale check), J into d_J and the caller's buffer
   if (r) return r;
-  if (d_J && d_J != c->d_J)
-    HIPCHK(c, hipMemcpyAsync(d_J, c->d_J, c->B * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
   c->have_prop = true;
   c->h_u.clear();  // host copy unknown for device-side u
   c->h_coef.clear();
@@ -901,23 +943,33 @@ int qoc_grape_sensitivity_dev(qoc_ctx* c, const double* d_u, int order, double* 
   if (order < 0 || order > 4) return fail(c, QOC_ERR_ARG, "dUkdp_order must be 1..4 or QOC_DUKDP_EXACT (got %d)", order);
   if (c->cost_kind == QOC_COST_EXTERNAL)
     return fail(c, QOC_ERR_STATE, "QOC_COST_EXTERNAL needs qoc_grape_sensitivity (host lambda_final)");
-  const size_t nu_t = (size_t)c->B * c->nu * c->Nt;
-  if (d_u && d_u != c->d_u) {
-    HIPCHK(c, hipMemsetAsync(c->d_flag, 0, sizeof(int), c->stream));
-    hipLaunchKernelGGL(k_compare_u, dim3(256), dim3(256), 0, c->stream, d_u, c->d_u, nu_t, c->d_flag);
-    HIPCHK(c, hipGetLastError());
-    int flag = 0;
-    HIPCHK(c, hipMemcpyAsync(&flag, c->d_flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (flag) return fail(c, QOC_ERR_STALE, "Cache data from other control signal u");
+  double* const out = d_dJdu ? d_dJdu : c->d_dJdu;
+  if (!d_u || d_u == c->d_u) return backward(c, order, out);  // the cache's own u (the reference passes cache.u)
+  const int* dflag = nullptr;
+  if ((r = queue_stale_check(c, d_u, &dflag))) return r;
+  if ((c->fwd_kind == 1 && blkseg_ok(c, order)) || blkp_backward_ok(c, order)) {
+    // the split backward's launches read the flag themselves and write nothing on a stale u: they are queued behind
+    // the check, and the host waits for the check alone, not for them (the stream never idles between the calls)
+    const bool lmu = c->L_is_mu, llazy = c->L_lazy;
+    const int lmode = c->last_eval_mode;
+    r = backward(c, order, out, dflag);
+    const int w = wait_stale_check(c);
+    if (w) {  // nothing was written: the co-states are still the last grape_sensitivity's
+      c->L_is_mu = lmu;
+      c->L_lazy = llazy;
+      c->last_eval_mode = lmode;
+    }
+    return w ? w : r;
   }
-  return backward(c, order, d_dJdu ? d_dJdu : c->d_dJdu);
+  if ((r = wait_stale_check(c))) return r;
+  return backward(c, order, out);
 }
 
 int qoc_eval_dev(qoc_ctx* c, const double* d_u, int order, double* d_J, double* d_dJdu) {
   if (c && c->cost_kind == QOC_COST_EXTERNAL)
     return fail(c, QOC_ERR_STATE, "qoc_eval_dev needs a device-side cost (TRACE or ZCAL)");
-  if (c && c->have_gen && blkseg_ok(c, order)) {
+  if (c) c->fwd_kind = 0;  // whatever runs below leaves no split forward behind
+  if (c && c->have_gen && c->concurrent && blkseg_ok(c, order)) {
     // block propagators with the time axis in segments: one launch reads u (and copies it to d_u) and writes J and
     // dJdu; x_k and λ_k are rebuilt on demand (qoc_blkseg.hpp)
     int r = check_ready(c);
@@ -992,12 +1044,8 @@ int qoc_grape_sensitivity(qoc_ctx* c, const double* u, int order, const double* 
   } else {
     // last propagate came from device memory: compare on the device
     HIPCHK(c, hipMemcpyAsync(c->d_dJdu, u, nu_t * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->d_flag, 0, sizeof(int), c->stream));
-    hipLaunchKernelGGL(k_compare_u, dim3(256), dim3(256), 0, c->stream, c->d_dJdu, c->d_u, nu_t, c->d_flag);
-    int flag = 0;
-    HIPCHK(c, hipMemcpyAsync(&flag, c->d_flag, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (flag) return fail(c, QOC_ERR_STALE, "Cache data from other control signal u");
+    if ((r = queue_stale_check(c, c->d_dJdu, nullptr))) return r;
+    if ((r = wait_stale_check(c))) return r;
   }
   if (c->cost_kind == QOC_COST_EXTERNAL) {
     if (!lambda_final) return fail(c, QOC_ERR_ARG, "lambda_final is required for QOC_COST_EXTERNAL");
@@ -1319,6 +1367,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[8] = c->last_eval_mode;  // last backward: 0 other, 1 captured products, 2 / 3 / 4 concurrent μ recurrence, 5 fused block gradient, 6 segmented block eval, 7 stored propagators of blocks of 5..16 rows
   info[9] = c->fwd_captured ? 1 : 0;
   // 6: the last eval ran the stored-propagator chains of blocks of 5..16 rows (propagate / grape_sensitivity: 4)
+  info[11] = c->fwd_kind;
   info[10] = blk_active(c) ? (blku_on(c) ? 5 : blkp_on(c) && c->last_eval_mode == 7 ? 6 : blk_rot(c) ? 4 : 3) : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
   return QOC_OK;
 }

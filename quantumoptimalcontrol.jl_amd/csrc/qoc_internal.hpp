@@ -158,6 +158,16 @@ struct qoc_ctx {
   // the segmented block eval (qoc_blkseg.hpp) writes neither x_k nor λ_k: qoc_get_states / a later backward rebuild
   // the states on demand (blku_states) from the u in d_u, with J and the coefficients going to scratch
   bool X_lazy = false;
+  // what the last propagate left for grape_sensitivity (the reference's split call form,
+  // examples/ipopt_callbacks_exp.jl:11-31): 0 states in d_X (every path), 1 the segmented forward's G at every
+  // segment end (d_gseg, qoc_blkseg.hpp BLKSEG_FWD), 2 the stored block propagators and states of blocks of 5..16 rows
+  // (d_blkU + d_X, qoc_blkp.hpp).  Reset by every other forward or eval.
+  int fwd_kind = 0;
+  double2* d_gseg = nullptr;         // B x NB^2 x S x nblk complex
+  size_t gseg_bytes = 0;
+  int* h_flag = nullptr;             // host-mapped stale-u flag of the queued check (k_compare_u_flags)
+  int flag_turn = 0;                 // which of the two device flags d_flag[0 / 1] the next queued check writes
+  hipEvent_t flag_ev = nullptr;      // recorded after that copy
   double* d_J_scr = nullptr;         // B
   cx<double>* d_coef_scr = nullptr;  // B x 2m
   // every generator exactly skew-Hermitian (|A + A^H| <= 4 eps max|A|): the slice propagators are unitary, which the
@@ -327,6 +337,16 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu);
 bool blkseg_ok(const qoc_ctx* c, int order);
 int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d_dJdu);
 int blku_states(qoc_ctx* c);      // rebuild x_k after a segmented eval (no-op unless X_lazy)
+// the reference's split call form on the segmented eval: propagate = phases 0-2 (G at the segment ends to HBM),
+// grape_sensitivity = phase 3 (stale: the device flag of a stale-u check queued before it, or nullptr)
+bool blkseg_split_ok(const qoc_ctx* c);
+int blkseg_forward(qoc_ctx* c, const double* d_u, double* d_J);
+int blkseg_backward(qoc_ctx* c, int order, double* d_dJdu, const int* stale);
+// the same for blocks of 5..16 rows on stored propagators: propagate = formation + forward chain (1: not applicable),
+// grape_sensitivity = the μ recurrence + the order-3 gradient
+int blkp_forward(qoc_ctx* c);
+bool blkp_backward_ok(const qoc_ctx* c, int order);
+int blkp_backward(qoc_ctx* c, double* d_dJdu, const int* stale);
 int blk_materialize(qoc_ctx* c);  // rebuild every lazily kept x_k / λ_k (before a setter changes what they need)
 
 }  // namespace qoc_host

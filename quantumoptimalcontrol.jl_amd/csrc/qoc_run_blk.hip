@@ -405,7 +405,9 @@ static hipError_t blk_dispatch(const qoc_ctx* c, F&& f) {
 
 int blk_forward(qoc_ctx* c) {
   if (blku_on(c)) return blku_forward(c);
-  int r = tchain_prep(c);
+  int r = blkp_forward(c);  // blocks of 5..16 rows: stored propagators (1: not applicable)
+  if (r != 1) return r;
+  r = tchain_prep(c);
   if (r) return r;
   const TChainArgs g = tchain_args(c);
   const BlkArgs bk = blk_args(c);
@@ -504,34 +506,46 @@ bool blkp_on(const qoc_ctx* c) {
   return !(env && atoi(env) == 0);
 }
 
-static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
-  TChainArgs gf = tchain_args(c);
-  TChainArgs gb = tchain_args(c);
-  gb.mu_mode = 1;
-  int r;
-  if (bk.nwb != c->nwb) {
-    if ((r = blk_zero_dead(c, {c->d_X, c->d_L}))) return r;
+// the propagator store d_blkU of at least `bytes` (reallocated when a larger batch part or block layout needs more);
+// soft: a failed allocation is no error (returns 1: the caller takes the Chebyshev block chains instead)
+static int blkp_ensure_store(qoc_ctx* c, size_t bytes, bool soft) {
+  if (c->blkU_bytes >= bytes) return QOC_OK;
+  if (c->d_blkU) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->stream2) HIPCHK(c, hipStreamSynchronize(c->stream2));
+    HIPCHK(c, hipFree(c->d_blkU));
+    c->d_blkU = nullptr;
+    c->dev_bytes -= c->blkU_bytes;
+    c->blkU_bytes = 0;
   }
-  const long long units = (long long)c->B * c->Nt * bk.nwb;
-  const size_t ubytes = (size_t)units * 256 * sizeof(double2);  // one propagator per unit
-  if (c->blkU_bytes < ubytes) {
-    if (c->d_blkU) {
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      HIPCHK(c, hipFree(c->d_blkU));
-      c->d_blkU = nullptr;
-      c->dev_bytes -= c->blkU_bytes;
-      c->blkU_bytes = 0;
-    }
-    HIPCHK(c, hipMalloc((void**)&c->d_blkU, ubytes));
-    c->blkU_bytes = ubytes;
-    c->dev_bytes += ubytes;
+  const hipError_t e = hipMalloc((void**)&c->d_blkU, bytes);
+  if (e != hipSuccess) {
+    c->d_blkU = nullptr;
+    (void)hipGetLastError();  // clear the sticky error of the failed allocation
+    if (soft) return 1;
+    return fail(c, QOC_ERR_HIP, "stored block propagators (%zu bytes): %s", bytes, hipGetErrorString(e));
   }
-  BlkpArgs a{};
+  c->blkU_bytes = bytes;
+  c->dev_bytes += bytes;
+  return QOC_OK;
+}
+
+// The formation's arguments and launch shape, the chain kernels' chunk size
+struct BlkpPlan {
+  BlkpArgs a;
+  void (*kern)(BlkpArgs);
+  size_t lds;
+  int per_cu;
+  int ch;
+  size_t clds;
+};
+static int blkp_plan(qoc_ctx* c, const BlkArgs& bk, int parts, BlkpPlan& pl) {
+  BlkpArgs& a = pl.a;
+  a = BlkpArgs{};
   a.N = c->N;
   a.nu = c->nu;
   a.nwb = bk.nwb;
   a.skew = c->skew_exact && c->tprm.mur[0] == 0.0 && c->tprm.mur[1] == 0.0 && c->tprm.mur[2] == 0.0;
-  a.units = units;
   a.four = getenv("QOC_BLKP_4M") && atoi(getenv("QOC_BLKP_4M")) != 0;
   // one product more for one squaring fewer (default): each squaring doubles the rounding error a slice carries over
   // 2000 chained slices (tunable bus, all 512 seeds against the C port: max |ΔJ| 4.7e-12 with the fewest products,
@@ -544,71 +558,59 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
     a.mur[j] = j <= c->nu ? c->tprm.mur[j] : 0.0;
     a.mui[j] = j <= c->nu ? c->tprm.mui[j] : 0.0;
   }
-  a.UF = (double2*)c->d_blkU;
   a.prods = c->d_terms;  // qoc_chain_terms: executed 16 x 16 complex products on this path
-  const size_t lds = (size_t)bk.nwb * 768 * sizeof(double2) + (size_t)(BLKP_WG / 64) * BLKP_TP * sizeof(double2);
+  pl.lds = (size_t)bk.nwb * 768 * sizeof(double2) + (size_t)(BLKP_WG / 64) * BLKP_TP * sizeof(double2);
   const char* oc = getenv("QOC_BLKP_OCC");
   const bool occ3 = !(oc && atoi(oc) == 2);
-  auto kern = c->nu == 1 ? (occ3 ? k_blkp_exp<1, 3> : k_blkp_exp<1, 2>) : (occ3 ? k_blkp_exp<2, 3> : k_blkp_exp<2, 2>);
-  HIPCHK(c, blk_lds_attr(kern, lds));
+  pl.kern = c->nu == 1 ? (occ3 ? k_blkp_exp<1, 3> : k_blkp_exp<1, 2>) : (occ3 ? k_blkp_exp<2, 3> : k_blkp_exp<2, 2>);
+  HIPCHK(c, blk_lds_attr(pl.kern, pl.lds));
   const int waves = bk.nwb * c->m;
-  // The formation is MFMA-bound and the chains are bound by their propagator reads: the seeds go in `parts` groups,
-  // the chains of group p (second stream) beside the formation of group p + 1, with the formation at two workgroups
-  // per CU so that a chain workgroup fits beside them (QOC_BLKP_PARTS, default 4; 1: one formation, then the chains)
-  int parts = 4;
-  if (const char* pe = getenv("QOC_BLKP_PARTS")) parts = atoi(pe);
-  parts = std::max(1, std::min(parts, c->B));
   int ch = blkp_chunk(waves, parts);
   if (const char* ce = getenv("QOC_BLKP_CH")) {
     const int v = atoi(ce);
     if (v == 1 || v == 2 || v == 4 || v == 8) ch = v;
   }
   if (blkp_chain_lds(c->N, c->m, waves, ch) > 160 * 1024) ch = blkp_chunk(waves);
-  const size_t clds = blkp_chain_lds(c->N, c->m, waves, ch);
-  auto chain = ch == 8 ? k_blkp_dual<8> : ch == 4 ? k_blkp_dual<4> : ch == 2 ? k_blkp_dual<2> : k_blkp_dual<1>;
-  HIPCHK(c, blk_lds_attr(chain, clds));
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, BLKP_WG, lds) != hipSuccess || per_cu < 1)
-    per_cu = 2;
-  if (parts > 1) {
-    per_cu = std::min(per_cu, 2);
-    if ((r = ensure_stream2(c, parts + 1))) return r;
-    HIPCHK(c, hipEventRecord(c->sync_ev[parts], c->stream));  // the second stream after everything queued so far
-    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[parts], 0));
-  }
-  hipStream_t cs = parts > 1 ? c->stream2 : c->stream;
-  // QOC_BLKP_PRIO=1: the chain waves at the top issue priority.  Measured: each group's chains 1.63 -> 1.07 ms, the
-  // formation beside them 1.85 -> 1.97 ms per group, and the formation is the critical path (8.72 vs 8.93 ms per
-  // eval), so off by default
-  const int cprio = getenv("QOC_BLKP_PRIO") ? atoi(getenv("QOC_BLKP_PRIO")) : 0;
-  for (int p = 0; p < parts; ++p) {
-    const int s0 = (int)((long long)c->B * p / parts), s1 = (int)((long long)c->B * (p + 1) / parts);
-    if (s1 <= s0) continue;
-    a.unit0 = (long long)s0 * c->Nt * bk.nwb;
-    a.units = (long long)s1 * c->Nt * bk.nwb;
-    const unsigned grid = (unsigned)std::max<long long>(
-        1, std::min<long long>((a.units - a.unit0 + BLKP_WG / 64 - 1) / (BLKP_WG / 64), (long long)c->ncu * per_cu));
-    int mk = mark_begin(c, 0);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(BLKP_WG), lds, c->stream, a);
-    mark_end(c, mk);
-    HIPCHK(c, hipGetLastError());
-    if (parts > 1) {
-      HIPCHK(c, hipEventRecord(c->sync_ev[p], c->stream));
-      HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[p], 0));
-    }
-    mk = mark_begin(c, 1, cs);
-    hipLaunchKernelGGL(chain, dim3(2 * (s1 - s0)), dim3(64 * waves), clds, cs, gf, gb, bk, (const double2*)a.UF, s0,
-                       cprio);
-    mark_end(c, mk, cs);
-    HIPCHK(c, hipGetLastError());
-  }
-  if (parts > 1) {  // the gradient (and everything after it on the engine stream) after the last chains
-    HIPCHK(c, hipEventRecord(c->sync_ev[parts], c->stream2));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->sync_ev[parts], 0));
-  }
-  c->fwd_captured = false;
-  c->props_since_reset++;
-  c->steps_stale = true;  // d_steps still holds the last k_tchain_prep's records, not this u's
+  pl.ch = ch;
+  pl.clds = blkp_chain_lds(c->N, c->m, waves, ch);
+  pl.per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pl.per_cu, (const void*)pl.kern, BLKP_WG, pl.lds) != hipSuccess ||
+      pl.per_cu < 1)
+    pl.per_cu = 2;
+  if (parts > 1) pl.per_cu = std::min(pl.per_cu, 2);  // a chain workgroup fits beside the formation
+  return QOC_OK;
+}
+// the formation of units [unit0, units) into UF (which holds unit ubase at its start)
+static int blkp_launch_exp(qoc_ctx* c, BlkpPlan& pl, long long unit0, long long units, double2* UF, long long ubase) {
+  pl.a.unit0 = unit0;
+  pl.a.units = units;
+  pl.a.UF = UF;
+  pl.a.ubase = ubase;
+  const unsigned grid = (unsigned)std::max<long long>(
+      1, std::min<long long>((units - unit0 + BLKP_WG / 64 - 1) / (BLKP_WG / 64), (long long)c->ncu * pl.per_cu));
+  const int mk = mark_begin(c, 0);
+  hipLaunchKernelGGL(pl.kern, dim3(grid), dim3(BLKP_WG), pl.lds, c->stream, pl.a);
+  mark_end(c, mk);
+  HIPCHK(c, hipGetLastError());
+  return QOC_OK;
+}
+// one direction's chains for seeds [s0, s1) from the propagators in U (seed useed0's first)
+template <bool FWD>
+static int blkp_launch_chain(qoc_ctx* c, const BlkpPlan& pl, const TChainArgs& g, const BlkArgs& bk, const double2* U,
+                             int s0, int s1, int useed0, hipStream_t st, const int* stale) {
+  auto chain = pl.ch == 8   ? k_blkp_chain<FWD, 8>
+               : pl.ch == 4 ? k_blkp_chain<FWD, 4>
+               : pl.ch == 2 ? k_blkp_chain<FWD, 2>
+                            : k_blkp_chain<FWD, 1>;
+  HIPCHK(c, blk_lds_attr(chain, pl.clds));
+  const int mk = mark_begin(c, FWD ? 1 : 2, st);
+  hipLaunchKernelGGL(chain, dim3(s1 - s0), dim3(64 * bk.nwb * c->m), pl.clds, st, g, bk, U, s0, useed0, stale);
+  mark_end(c, mk, st);
+  HIPCHK(c, hipGetLastError());
+  return QOC_OK;
+}
+// the order-3 gradient from x_k, μ_{k+1} and the λ_N coefficients
+static int blkp_launch_grad(qoc_ctx* c, const BlkArgs& bk, double* d_dJdu, const int* stale, cx<double>* coef_out) {
   BlkpGradArgs ga{};
   ga.N = c->N;
   ga.m = c->m;
@@ -622,6 +624,8 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
   ga.coef = c->d_coef;
   ga.dJdu = d_dJdu;
   ga.tiles = (long long)c->B * ((c->Nt + 15) / 16);
+  ga.stale = stale;
+  ga.coef_out = coef_out;
   const size_t glds = blkp_grad_lds(bk.nwb, c->nu);
   auto gk = c->nu == 1 ? k_blkp_grad<1> : k_blkp_grad<2>;
   HIPCHK(c, blk_lds_attr(gk, glds));
@@ -632,8 +636,161 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
   hipLaunchKernelGGL(gk, dim3(ggrid), dim3(256), glds, c->stream, ga);
   mark_end(c, mg);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->d_coef_mu, c->d_coef, (size_t)c->B * 2 * c->m * sizeof(cx<double>),
-                           hipMemcpyDeviceToDevice, c->stream));
+  return QOC_OK;
+}
+static int blkp_parts(const qoc_ctx* c) {
+  int parts = 4;
+  if (const char* pe = getenv("QOC_BLKP_PARTS")) parts = atoi(pe);
+  return std::max(1, std::min(parts, c->B));
+}
+
+// qoc_eval_dev: U_k per (seed, slice, live block) on MFMA, the forward chain and the μ recurrence from the stored
+// propagators, then the order-3 gradient.  The formation is MFMA-bound and the chains are bound by their propagator
+// reads: the seeds go in `parts` groups, the chains of group p (second stream) beside the formation of group p + 1, with
+// the formation at two workgroups per CU so that a chain workgroup fits beside them (QOC_BLKP_PARTS, default 4; 1: one
+// formation, then the chains).  The propagators of two groups are held at a time (the formation of group p + 2 waits
+// for the chains of group p): 2.1 GB at the tunable bus' B = 512 instead of every seed's 4.2 GB.  Returns 1 (nothing
+// launched) when even that does not fit in the free HBM: the Chebyshev block chains then run.
+static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
+  TChainArgs gf = tchain_args(c);
+  TChainArgs gb = tchain_args(c);
+  gb.mu_mode = 1;
+  int r;
+  const int parts = blkp_parts(c);
+  const long long per_seed = (long long)c->Nt * bk.nwb;  // units per seed
+  const int gmax = (c->B + parts - 1) / parts;           // seeds of the largest group
+  const int nslab = parts > 1 ? 2 : 1;
+  const size_t slab = (size_t)gmax * per_seed * 256;      // double2 per slab
+  if ((r = blkp_ensure_store(c, nslab * slab * sizeof(double2), true))) return r;  // 1: does not fit
+  if (bk.nwb != c->nwb) {
+    if ((r = blk_zero_dead(c, {c->d_X, c->d_L}))) return r;
+  }
+  BlkpPlan pl;
+  if ((r = blkp_plan(c, bk, parts, pl))) return r;
+  // events: [p] group p formed, [parts + p] group p's chains done, [2 parts] everything queued before
+  if (parts > 1) {
+    if ((r = ensure_stream2(c, 2 * parts + 1))) return r;
+    HIPCHK(c, hipEventRecord(c->sync_ev[2 * parts], c->stream));  // the second stream after everything queued so far
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[2 * parts], 0));
+  }
+  hipStream_t cs = parts > 1 ? c->stream2 : c->stream;
+  // QOC_BLKP_PRIO=1: the chain waves at the top issue priority.  Measured: each group's chains 1.63 -> 1.07 ms, the
+  // formation beside them 1.85 -> 1.97 ms per group, and the formation is the critical path (8.72 vs 8.93 ms per
+  // eval), so off by default
+  const int cprio = getenv("QOC_BLKP_PRIO") ? atoi(getenv("QOC_BLKP_PRIO")) : 0;
+  auto chain = pl.ch == 8 ? k_blkp_dual<8> : pl.ch == 4 ? k_blkp_dual<4> : pl.ch == 2 ? k_blkp_dual<2> : k_blkp_dual<1>;
+  HIPCHK(c, blk_lds_attr(chain, pl.clds));
+  const int waves = bk.nwb * c->m;
+  for (int p = 0; p < parts; ++p) {
+    const int s0 = (int)((long long)c->B * p / parts), s1 = (int)((long long)c->B * (p + 1) / parts);
+    if (s1 <= s0) continue;
+    double2* const U = (double2*)c->d_blkU + (size_t)(p % nslab) * slab;
+    if (p >= 2) HIPCHK(c, hipStreamWaitEvent(c->stream, c->sync_ev[parts + p - 2], 0));  // slab p % 2 read out
+    if ((r = blkp_launch_exp(c, pl, (long long)s0 * per_seed, (long long)s1 * per_seed, U, (long long)s0 * per_seed)))
+      return r;
+    if (parts > 1) {
+      HIPCHK(c, hipEventRecord(c->sync_ev[p], c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[p], 0));
+    }
+    const int mk = mark_begin(c, 1, cs);
+    hipLaunchKernelGGL(chain, dim3(2 * (s1 - s0)), dim3(64 * waves), pl.clds, cs, gf, gb, bk, (const double2*)U, s0, s0,
+                       cprio);
+    mark_end(c, mk, cs);
+    HIPCHK(c, hipGetLastError());
+    if (parts > 1) HIPCHK(c, hipEventRecord(c->sync_ev[parts + p], c->stream2));
+  }
+  if (parts > 1) {  // the gradient (and everything after it on the engine stream) after the last chains
+    HIPCHK(c, hipEventRecord(c->sync_ev[2 * parts], c->stream2));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->sync_ev[2 * parts], 0));
+  }
+  c->fwd_captured = false;
+  c->props_since_reset++;
+  c->steps_stale = true;  // d_steps still holds the last k_tchain_prep's records, not this u's
+  if ((r = blkp_launch_grad(c, bk, d_dJdu, nullptr, c->d_coef_mu))) return r;
+  c->L_is_mu = true;
+  c->last_eval_mode = 7;
+  return QOC_OK;
+}
+
+// the stored-propagator eval applies (blocks of 5..16 rows with a live-wave layout that fits the chain and gradient
+// kernels)
+static bool blkp_fits(qoc_ctx* c, const BlkArgs& bk) {
+  const int waves = bk.nwb * c->m;
+  return waves <= 8 && blkp_chain_lds(c->N, c->m, waves, blkp_chunk(waves)) <= 160 * 1024 &&
+         blkp_grad_lds(bk.nwb, c->nu) <= 160 * 1024;
+}
+
+// propagate on stored propagators (the reference's own structure, src/gradient_computations.jl:17-29): every U_k of
+// the live blocks formed on MFMA, the forward chain from them (seed groups pipelined as in the eval), states in d_X;
+// the propagators stay for grape_sensitivity (every seed's: 4.2 GB at the tunable bus' B = 512).  Built-in costs, no
+// penalty; QOC_BLKP_SPLIT=0 keeps the Chebyshev block chains.  Returns 1 (nothing launched) when it does not apply.
+int blkp_forward(qoc_ctx* c) {
+  const char* env = getenv("QOC_BLKP_SPLIT");
+  if ((env && atoi(env) == 0) || !blkp_on(c) || c->mu != 0.0 ||
+      (c->cost_kind != QOC_COST_TRACE && c->cost_kind != QOC_COST_ZCAL))
+    return 1;
+  BlkArgs bk = blk_args(c);
+  int r = blk_live(c, bk);
+  if (r) return r;
+  if (!blkp_fits(c, bk)) return 1;
+  const long long per_seed = (long long)c->Nt * bk.nwb;
+  if ((r = blkp_ensure_store(c, (size_t)c->B * per_seed * 256 * sizeof(double2), true))) return r;
+  if (bk.nwb != c->nwb) {
+    if ((r = blk_zero_dead(c, {c->d_X, c->d_L}))) return r;
+  }
+  const int parts = blkp_parts(c);
+  BlkpPlan pl;
+  if ((r = blkp_plan(c, bk, parts, pl))) return r;
+  const TChainArgs gf = tchain_args(c);
+  if (parts > 1) {
+    if ((r = ensure_stream2(c, parts + 1))) return r;
+    HIPCHK(c, hipEventRecord(c->sync_ev[parts], c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[parts], 0));
+  }
+  hipStream_t cs = parts > 1 ? c->stream2 : c->stream;
+  double2* const U = (double2*)c->d_blkU;
+  for (int p = 0; p < parts; ++p) {
+    const int s0 = (int)((long long)c->B * p / parts), s1 = (int)((long long)c->B * (p + 1) / parts);
+    if (s1 <= s0) continue;
+    if ((r = blkp_launch_exp(c, pl, (long long)s0 * per_seed, (long long)s1 * per_seed, U, 0))) return r;
+    if (parts > 1) {
+      HIPCHK(c, hipEventRecord(c->sync_ev[p], c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->stream2, c->sync_ev[p], 0));
+    }
+    if ((r = blkp_launch_chain<true>(c, pl, gf, bk, U, s0, s1, 0, cs, nullptr))) return r;
+  }
+  if (parts > 1) {
+    HIPCHK(c, hipEventRecord(c->sync_ev[parts], c->stream2));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->sync_ev[parts], 0));
+  }
+  c->fwd_captured = false;
+  c->props_since_reset++;
+  c->steps_stale = true;  // d_steps holds another u's step records (the Chebyshev backward re-preps first)
+  c->fwd_kind = 2;
+  return QOC_OK;
+}
+
+bool blkp_backward_ok(const qoc_ctx* c, int order) {
+  return c->fwd_kind == 2 && order == 3 && c->mu == 0.0 && !c->src_on &&
+         (c->cost_kind == QOC_COST_TRACE || c->cost_kind == QOC_COST_ZCAL) && c->d_blkU;
+}
+
+// grape_sensitivity after blkp_forward: the μ recurrence from the stored propagators (μ_N = X_target, λ_k = coef ⊙ μ_k,
+// src/penalty_fcns.jl:19-22, 35-40), then the order-3 gradient; stale: the device flag of a queued stale-u check
+int blkp_backward(qoc_ctx* c, double* d_dJdu, const int* stale) {
+  BlkArgs bk = blk_args(c);
+  int r = blk_live(c, bk);
+  if (r) return r;
+  if (!c->d_coef_mu) {
+    HIPCHK(c, hipMalloc((void**)&c->d_coef_mu, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
+    c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
+  }
+  BlkpPlan pl;
+  if ((r = blkp_plan(c, bk, 1, pl))) return r;
+  TChainArgs gb = tchain_args(c);
+  gb.mu_mode = 1;
+  if ((r = blkp_launch_chain<false>(c, pl, gb, bk, (const double2*)c->d_blkU, 0, c->B, 0, c->stream, stale))) return r;
+  if ((r = blkp_launch_grad(c, bk, d_dJdu, stale, c->d_coef_mu))) return r;
   c->L_is_mu = true;
   c->last_eval_mode = 7;
   return QOC_OK;
@@ -649,10 +806,10 @@ int blk_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
   if (blkp_on(c)) {
     BlkArgs bk = blk_args(c);
     if ((r = blk_live(c, bk))) return r;
-    const int waves = bk.nwb * c->m;
-    if (waves <= 8 && blkp_chain_lds(c->N, c->m, waves, blkp_chunk(waves)) <= 160 * 1024 &&
-        blkp_grad_lds(bk.nwb, c->nu) <= 160 * 1024)
-      return blkp_eval_concurrent(c, d_dJdu, bk);
+    if (blkp_fits(c, bk)) {
+      r = blkp_eval_concurrent(c, d_dJdu, bk);
+      if (r != 1) return r;  // 1: the propagators do not fit in HBM: the Chebyshev block chains below
+    }
   }
   if ((r = blk_big(c) ? ensure_pws(c) : QOC_OK)) return r;
   if ((r = tchain_prep(c))) return r;
@@ -1005,13 +1162,9 @@ static int ensure_lazy_bufs(qoc_ctx* c) {
   return QOC_OK;
 }
 
-int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d_dJdu) {
-  const BlksegShape s = blkseg_shape(c);
-  int r = ensure_lazy_bufs(c);
-  if (r) return r;
-  const TChainArgs g = tchain_args(c);
-  const BlkArgs bk = blk_args(c);
-  BlksegParams sp{};
+// the launch parameters every mode shares; the best-(J, seed) epilogue's buffers on first use
+static int blkseg_params(qoc_ctx* c, const BlksegShape& s, BlksegParams& sp) {
+  sp = BlksegParams{};
   for (int j = 0; j < 3; ++j) {
     const bool on = j <= c->nu;
     sp.rad[j] = on ? c->tprm.rad[j] : 0.0;  // skew-Hermitian: spectral half-widths of the shifted generators
@@ -1023,12 +1176,6 @@ int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d
   sp.L = s.L;
   sp.UPW = s.UPW;
   sp.RB = blkseg_rb(s.UPW, c->nu);
-  sp.u = d_u;
-  sp.u_copy = d_u != c->d_u ? c->d_u : nullptr;
-  sp.u_copy2 = c->d_u_lam;  // the co-states' rebuild (blku_costates) reads this copy and d_coef_lam
-  sp.J2 = d_J && d_J != c->d_J ? d_J : nullptr;
-  sp.coef2 = c->d_coef_lam;
-  sp.dJdu = d_dJdu;
   sp.terms = c->d_terms;
   // the best (J, seed) for qoc_allgather_best_dev, found by the launch's last workgroup
   if (!c->d_best) {  // no communicator yet: this context alone (the epilogue's own layout)
@@ -1043,14 +1190,42 @@ int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d
   sp.done = c->d_done;
   sp.best = c->d_best + 2 + 2 * c->rank;
   sp.seed_offset = c->seed_offset;
-  const int mk = mark_begin(c, 2);
-  const hipError_t e = blkseg_dispatch(c->blk_nb, order, [&](auto NB_, auto ORD_) {
+  return QOC_OK;
+}
+
+template <int MODE>
+static hipError_t blkseg_launch(qoc_ctx* c, int order, const BlksegShape& s, const BlksegParams& sp) {
+  const TChainArgs g = tchain_args(c);
+  const BlkArgs bk = blk_args(c);
+  return blkseg_dispatch(c->blk_nb, MODE == BLKSEG_FWD ? 1 : order, [&](auto NB_, auto ORD_) {
     constexpr int NB = decltype(NB_)::value, ORD = decltype(ORD_)::value;
-    const hipError_t q = blk_lds_attr(k_blkseg_eval<NB, ORD, 8>, s.lds);
-    if (q != hipSuccess) return q;
-    hipLaunchKernelGGL((k_blkseg_eval<NB, ORD, 8>), dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, sp);
-    return hipGetLastError();
+    // the forward half has no gradient: one instantiation (ORD 1) serves every order
+    if constexpr (MODE == BLKSEG_FWD && ORD != 1) {
+      return hipErrorInvalidValue;
+    } else {
+      auto kern = k_blkseg_eval<NB, ORD, 8, MODE>;
+      const hipError_t q = blk_lds_attr(kern, s.lds);
+      if (q != hipSuccess) return q;
+      hipLaunchKernelGGL(kern, dim3(c->B), dim3(64 * s.W), s.lds, c->stream, g, bk, sp);
+      return hipGetLastError();
+    }
   });
+}
+
+int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d_dJdu) {
+  const BlksegShape s = blkseg_shape(c);
+  int r = ensure_lazy_bufs(c);
+  if (r) return r;
+  BlksegParams sp;
+  if ((r = blkseg_params(c, s, sp))) return r;
+  sp.u = d_u;
+  sp.u_copy = d_u != c->d_u ? c->d_u : nullptr;
+  sp.u_copy2 = c->d_u_lam;  // the co-states' rebuild (blku_costates) reads this copy and d_coef_lam
+  sp.J2 = d_J && d_J != c->d_J ? d_J : nullptr;
+  sp.coef2 = c->d_coef_lam;
+  sp.dJdu = d_dJdu;
+  const int mk = mark_begin(c, 2);
+  const hipError_t e = blkseg_launch<BLKSEG_FUSED>(c, order, s, sp);
   mark_end(c, mk);
   if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blkseg_eval launch: %s", hipGetErrorString(e));
   c->fwd_captured = false;
@@ -1058,6 +1233,74 @@ int blkseg_eval(qoc_ctx* c, int order, const double* d_u, double* d_J, double* d
   c->X_lazy = true;
   c->L_lazy = true;
   c->best_ready = true;
+  c->last_eval_mode = 6;
+  return QOC_OK;
+}
+
+// propagate on the segmented eval (the reference's f, examples/ipopt_callbacks_exp.jl:11-19): J, the λ_N coefficients
+// and G at every segment's end, x_k rebuilt on demand.  Applies where the fused eval does (any order: the forward half
+// has none) unless QOC_BLKSEG_SPLIT=0.
+bool blkseg_split_ok(const qoc_ctx* c) {
+  const char* env = getenv("QOC_BLKSEG_SPLIT");
+  if (env && !std::strcmp(env, "0")) return false;
+  return blkseg_ok(c, 3);
+}
+
+int blkseg_forward(qoc_ctx* c, const double* d_u, double* d_J) {
+  const BlksegShape s = blkseg_shape(c);
+  int r = ensure_lazy_bufs(c);
+  if (r) return r;
+  const size_t gbytes = (size_t)c->B * s.S * c->nblk * c->blk_nb * c->blk_nb * sizeof(double2);
+  if (c->gseg_bytes < gbytes) {  // a new block layout (qoc_set_generators) may need more
+    if (c->d_gseg) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipFree(c->d_gseg));
+      c->d_gseg = nullptr;
+      c->dev_bytes -= c->gseg_bytes;
+      c->gseg_bytes = 0;
+    }
+    HIPCHK(c, hipMalloc((void**)&c->d_gseg, gbytes));
+    c->gseg_bytes = gbytes;
+    c->dev_bytes += gbytes;
+  }
+  BlksegParams sp;
+  if ((r = blkseg_params(c, s, sp))) return r;
+  sp.u = d_u;
+  sp.u_copy = d_u != c->d_u ? c->d_u : nullptr;  // the backward half and the stale check read d_u
+  sp.J2 = d_J && d_J != c->d_J ? d_J : nullptr;
+  sp.gseg = c->d_gseg;  // (the co-states' rebuild source stays the last grape_sensitivity's: the backward writes it)
+  const int mk = mark_begin(c, 1);
+  const hipError_t e = blkseg_launch<BLKSEG_FWD>(c, 1, s, sp);
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blkseg_eval (forward) launch: %s", hipGetErrorString(e));
+  c->fwd_captured = false;
+  c->X_lazy = true;
+  c->best_ready = true;
+  c->fwd_kind = 1;
+  c->props_since_reset++;
+  return QOC_OK;
+}
+
+// grape_sensitivity after blkseg_forward (the reference's f_grad, :21-31): phase 3 from the stored G; the co-states are
+// rebuilt on demand from the forward's copies of u and the λ_N coefficients
+int blkseg_backward(qoc_ctx* c, int order, double* d_dJdu, const int* stale) {
+  const BlksegShape s = blkseg_shape(c);
+  BlksegParams sp;
+  int r = blkseg_params(c, s, sp);
+  if (r) return r;
+  if ((r = ensure_lazy_bufs(c))) return r;
+  sp.u = c->d_u;
+  sp.u_copy2 = c->d_u_lam;  // λ_k rebuilt on demand from this u and the forward's λ_N coefficients
+  sp.coef2 = c->d_coef_lam;
+  sp.dJdu = d_dJdu;
+  sp.gseg = c->d_gseg;
+  sp.stale = stale;
+  const int mk = mark_begin(c, 2);
+  const hipError_t e = blkseg_launch<BLKSEG_BWD>(c, order, s, sp);
+  mark_end(c, mk);
+  if (e != hipSuccess) return fail(c, QOC_ERR_HIP, "k_blkseg_eval (backward) launch: %s", hipGetErrorString(e));
+  c->L_is_mu = false;
+  c->L_lazy = true;
   c->last_eval_mode = 6;
   return QOC_OK;
 }

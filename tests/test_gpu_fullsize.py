@@ -95,11 +95,13 @@ def test_cavity_dense_full_size(built_lib, chain, monkeypatch):
 @pytest.mark.parametrize("chain", ["auto", "dense", "propagators"])
 def test_tunable_bus_full_size(built_lib, chain, monkeypatch):
     """config 4: two_qubit_tunable_bus N=27, m=1, Nt=2000, B=512 per GPU, ||A_k||_1 ~ 30: every seed against
-    the C port, over 2000 chained slices: the default Chebyshev Taylor-action chains (spectral radius ~14 per
-    slice) and the propagators (the reference's Padé-13)."""
+    the C port, over 2000 chained slices: the default stored block propagators (propagate: k_blkp_exp + the forward
+    chain, grape_sensitivity: the μ recurrence + k_blkp_grad), the dense Chebyshev Taylor-action chains (spectral
+    radius ~14 per slice) and the propagators (the reference's Padé-13)."""
     info = _check_config("tunable_bus", list(range(512)), None if chain == "auto" else chain, monkeypatch)
     assert info["chain"] == ("propagators" if chain == "propagators" else "taylor")
-    assert (info["chain_kernel"] == "blocks_mfma") == (chain == "auto")
+    assert (info["chain_kernel"] == "blocks_prop16") == (chain == "auto"), info
+    assert (info["backward"] == "blocks_prop16") == (chain == "auto"), info
 
 
 def test_tunable_bus_full_size_device_eval(built_lib):
