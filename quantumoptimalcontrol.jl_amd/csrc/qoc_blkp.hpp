@@ -92,6 +92,15 @@ struct BlkpArgs {
   int skew;                    // every Ã_j exactly skew-Hermitian (qoc_ctx::skew_exact, imaginary shifts)
   int four;                    // complex products from four real ones (QOC_BLKP_4M)
   int slack;                   // up to this many products more for each squaring fewer (QOC_BLKP_SLACK)
+  // the truncation criterion with the squarings counted (tail > 0): s squarings amplify the degree-4r polynomial's
+  // truncation R of exp(2^-s X) 2^s times (U = (e^{2^-s X} - R)^{2^s} = e^X - 2^s R + ..., ||e^{2^-s X}|| = 1), and over
+  // the chain the slices' truncations add up coherently; so s is the fewest squarings with
+  // tail_{4r}(2^-s ρ̂) <= 2^-53 2^-(s + tail), theta[r][s] the largest ρ meeting it (blkp_theta_table, host).
+  // tail = 0: the plain bound tail_{4r}(2^-s ρ̂) <= 2^-53 of kBlkpTheta.
+  int tail;
+  double theta[BLKP_RMAX + 1][16];
+  double rcap;                 // > 0: the accurate (r, s) choice, 2^-s ρ̂ <= rcap (QOC_BLKP_RCAP, default 1); 0: the
+                               // fewest products (slack / tail)
   long long unit0, units;      // this launch's units [unit0, units) of B Nt nwb: unit = (b Nt + k) nwb + β
   const int* wrow;             // nwb x 16 rows of the live wave blocks
   const cx<double>* At;        // (nu+1) N x N shifted generators Ã_j, column-major
@@ -308,32 +317,66 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
     const double rho = uniform_f64(sqrt(n1 * ninf));
     // (the sharper α_p = max(‖X^p‖^{1/p}, ‖X^{p+1}‖^{1/(p+1)}) of Al-Mohy & Higham from the computed powers chose the
     // same (r, s) on the tunable bus -- 10.75 products per unit either way -- and cost three more reductions)
-    // the fewest products r + 2 + s with 2^-s ρ̂ <= θ_{4r}, or (slack) the fewest squarings within slack of that; each
-    // squaring doubles the rounding error the slice carries into the chain
-    int ssel[BLKP_RMAX + 1];
-    int best = 1 << 30;
-#pragma unroll
-    for (int rr = BLKP_RMIN; rr <= BLKP_RMAX; ++rr) {
-      // s = max(0, ceil(log2(ρ̂ / θ))): with ρ̂ / θ = f 2^e, f in [0.5, 1), that is e, or e - 1 when f = 1/2
-      const double q = rho * kBlkpInvTheta[rr];  // (a product: ρ̂ θ⁻¹ rounds the same side of 2^s but a few ulps)
-      const int e = q > 1.0 ? __builtin_amdgcn_frexp_exp(q) : 0;
-      ssel[rr] = q > 1.0 ? (__builtin_amdgcn_frexp_mant(q) == 0.5 ? e - 1 : e) : 0;
-      best = min(best, rr + 2 + ssel[rr]);
-    }
-    int r = BLKP_RMAX, s = 1 << 30;
-#pragma unroll
-    for (int rr = BLKP_RMAX; rr >= BLKP_RMIN; --rr)
-      if (rr + 2 + ssel[rr] <= best + a.slack && ssel[rr] < s) {
-        s = ssel[rr];
-        r = rr;
+    int r = BLKP_RMAX, s = 0;
+    if (a.rcap > 0.0) {
+      // the accurate choice (default): halve until 2^-s ρ̂ <= rcap (1), then the smallest degree whose truncation,
+      // amplified by the squarings, stays 2^-tail below an ulp (θ[r][s]).  The polynomial's rounding grows like
+      // e^{2^-s ρ̂} (its terms cancel on the imaginary axis) and the squarings' like 2^s, so the pieces are kept near
+      // norm 1: on the tunable bus (ρ̂ ≈ 14.7: r = 5, s = 4, 11 products) the bias of J over 2000 chained slices
+      // against an extended-precision propagation drops ~5x from the fewest-products choice (tools/tb_truth.py)
+      double q = rho;
+      while (s < 15 && q > a.rcap) {
+        q *= 0.5;
+        ++s;
       }
-    if (a.slack == 0) {  // the fewest products, the smaller r on ties (as measured for the default)
+      r = 0;
 #pragma unroll
       for (int rr = BLKP_RMAX; rr >= BLKP_RMIN; --rr)
-        if (rr + 2 + ssel[rr] == best) {
+        if (q <= a.theta[rr][s]) r = rr;
+      while (r == 0 && s < 15) {  // a cap above θ_{4 RMAX}: more halvings at the top degree
+        q *= 0.5;
+        ++s;
+        if (q <= a.theta[BLKP_RMAX][s]) r = BLKP_RMAX;
+      }
+      if (r == 0) r = BLKP_RMAX;
+    } else {
+      // the fewest products r + 2 + s with 2^-s ρ̂ <= θ_{4r} (tail > 0: θ[r][s], the squarings counted), or (slack)
+      // the fewest squarings within slack of that
+      int ssel[BLKP_RMAX + 1];
+      int best = 1 << 30;
+#pragma unroll
+      for (int rr = BLKP_RMIN; rr <= BLKP_RMAX; ++rr) {
+        if (a.tail > 0) {  // the fewest s with 2^-s ρ̂ <= θ[r][s] (ρ̂ is wave-uniform: a scalar loop)
+          int sq = 0;
+          double q = rho;
+          while (sq < 15 && q > a.theta[rr][sq]) {
+            q *= 0.5;
+            ++sq;
+          }
+          ssel[rr] = sq;
+        } else {
+          // s = max(0, ceil(log2(ρ̂ / θ))): with ρ̂ / θ = f 2^e, f in [0.5, 1), that is e, or e - 1 when f = 1/2
+          const double q = rho * kBlkpInvTheta[rr];  // (a product: ρ̂ θ⁻¹ rounds the same side of 2^s but a few ulps)
+          const int e = q > 1.0 ? __builtin_amdgcn_frexp_exp(q) : 0;
+          ssel[rr] = q > 1.0 ? (__builtin_amdgcn_frexp_mant(q) == 0.5 ? e - 1 : e) : 0;
+        }
+        best = min(best, rr + 2 + ssel[rr]);
+      }
+      s = 1 << 30;
+#pragma unroll
+      for (int rr = BLKP_RMAX; rr >= BLKP_RMIN; --rr)
+        if (rr + 2 + ssel[rr] <= best + a.slack && ssel[rr] < s) {
           s = ssel[rr];
           r = rr;
         }
+      if (a.slack == 0) {  // the fewest products, the smaller r on ties
+#pragma unroll
+        for (int rr = BLKP_RMAX; rr >= BLKP_RMIN; --rr)
+          if (rr + 2 + ssel[rr] == best) {
+            s = ssel[rr];
+            r = rr;
+          }
+      }
     }
     {
       const double sc = ldexp(1.0, -s);

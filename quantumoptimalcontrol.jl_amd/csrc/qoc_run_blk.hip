@@ -530,6 +530,34 @@ static int blkp_ensure_store(qoc_ctx* c, size_t bytes, bool soft) {
   return QOC_OK;
 }
 
+// θ[r][s] of BlkpArgs::tail: the largest ρ with Σ_{k > 4r} ρ^k / k! <= 2^-53 2^-(s + tail) (bisection; the tail sum from
+// its first term, exp((4r + 1) ln ρ - lgamma(4r + 2)), 40 terms)
+static void blkp_theta_table(int tail, double (&theta)[BLKP_RMAX + 1][16]) {
+  for (int r = 0; r <= BLKP_RMAX; ++r)
+    for (int s = 0; s < 16; ++s) {
+      if (r < BLKP_RMIN) {
+        theta[r][s] = 0.0;
+        continue;
+      }
+      const int m = 4 * r;
+      const double tol = std::ldexp(1.0, -53 - s - tail);
+      auto tailsum = [&](double rho) {
+        double t = std::exp((m + 1) * std::log(rho) - std::lgamma(m + 2.0)), sum = 0.0;
+        for (int k = m + 1; k < m + 41; ++k) {
+          sum += t;
+          t *= rho / (k + 1);
+        }
+        return sum;
+      };
+      double lo = 0.0, hi = 16.0;
+      for (int it = 0; it < 200; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        (tailsum(mid) <= tol ? lo : hi) = mid;
+      }
+      theta[r][s] = lo;
+    }
+}
+
 // The formation's arguments and launch shape, the chain kernels' chunk size
 struct BlkpPlan {
   BlkpArgs a;
@@ -551,6 +579,11 @@ static int blkp_plan(qoc_ctx* c, const BlkArgs& bk, int parts, BlkpPlan& pl) {
   // 2000 chained slices (tunable bus, all 512 seeds against the C port: max |ΔJ| 4.7e-12 with the fewest products,
   // 9.1e-13 with slack 1 at 11.75 instead of 10.75 products per unit; tools/blkp_accuracy.py)
   a.slack = getenv("QOC_BLKP_SLACK") ? std::max(0, atoi(getenv("QOC_BLKP_SLACK"))) : 1;
+  // the accurate (r, s) choice by default (BlkpArgs::rcap): pieces of norm <= 1, truncation 2^-3 ulp after the
+  // squarings; QOC_BLKP_RCAP=0 keeps the fewest-products choice (QOC_BLKP_SLACK, QOC_BLKP_TAIL)
+  a.rcap = getenv("QOC_BLKP_RCAP") ? std::max(0.0, atof(getenv("QOC_BLKP_RCAP"))) : 1.0;
+  a.tail = getenv("QOC_BLKP_TAIL") ? std::max(0, atoi(getenv("QOC_BLKP_TAIL"))) : a.rcap > 0.0 ? 3 : 0;
+  if (a.tail > 0) blkp_theta_table(a.tail, a.theta);
   a.wrow = bk.wrow;
   a.At = (const cx<double>*)c->d_At;
   a.u = c->d_u;

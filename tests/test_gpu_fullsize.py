@@ -131,6 +131,38 @@ def test_tunable_bus_full_size_device_eval(built_lib):
     assert rel <= 1e-10, rel
 
 
+def test_tunable_bus_every_rank_seeds(built_lib):
+    """config 4 is 4096 seeds over 8 ranks, each rank's u seeded by its rank (bench.py mk_u(B, rank)): ranks 1..7 on
+    this GPU (the stored block propagators through qoc_eval_dev), 64 seeds of each against the C port at the fp64 bar
+    (rank 0's 512: test_tunable_bus_full_size_device_eval)."""
+    import torch
+    from qoc_amd import GrapeEngine, systems
+    mk_prob, mk_u, B = systems.CONFIGS["tunable_bus"]
+    prob = mk_prob()
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B)
+    e.set_cost_trace(prob.x_target, prob.n)
+    worst = (0.0, 0.0)
+    for rank in range(1, 8):
+        u = mk_u(B, rank)
+        ud = torch.from_numpy(np.ascontiguousarray(np.transpose(u, (0, 2, 1)))).cuda()
+        Jd = torch.empty(B, dtype=torch.float64, device="cuda")
+        gd = torch.empty(B, prob.Nt, prob.nu, dtype=torch.float64, device="cuda")
+        e.eval_device(ud.data_ptr(), 3, Jd.data_ptr(), gd.data_ptr())
+        e.synchronize()
+        assert e.info()["backward"] == "blocks_prop16"
+        idx = np.arange(0, B, B // 64)
+        J = Jd.cpu().numpy()[idx]
+        g = np.transpose(gd.cpu().numpy(), (0, 2, 1))[idx]
+        Jc, gc = _cpu(prob, u[idx])
+        dJ = np.abs(J - Jc).max()
+        rel = max(np.linalg.norm(g[i] - gc[i]) / np.linalg.norm(gc[i]) for i in range(len(idx)))
+        worst = (max(worst[0], dJ), max(worst[1], rel))
+        assert dJ <= 1e-12, (rank, dJ)
+        assert rel <= 1e-10, (rank, rel)
+    e.close()
+    print("tunable bus ranks 1..7, 64 seeds each: max |dJ|", worst[0], "max rel dJdu", worst[1])
+
+
 def test_synthetic_full_size_fp32(built_lib, golden_dir):
     """config 5: synthetic GUE N=256, m=256 (x0 = I), nu=2, Nt=1000, B=128, fp32 on the large-N pipeline."""
     import qoc_oracle as O
