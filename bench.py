@@ -564,8 +564,12 @@ def main():
         # the split call form runs the two directions as separate launches (k_blkp_chain: forward in propagate, μ in
         # grape_sensitivity); the eval runs both in one (k_blkp_dual)
         split16 = lps["k_chain_bwd"] > 0
+        # one control: the propagators interpolated in u (k_blkp_int: Σ_{i<=D} T_i(ξ) M_i, 4 flops per complex entry
+        # and term, no MFMA); its algorithmic traffic is the 4 KB propagator written per unit
+        ideg = info1.get("interp_degree", 0)
+        f_int = B * Nt * nlive * 256 * (ideg + 1) * 4.0
         models = {
-            "k_expm": ("mfma", f_exp / 1e12, "TFLOP/s", peak),
+            "k_expm": ("hbm", u_bytes / 1e9, "GB/s", PEAK_HBM_GBS) if ideg else ("mfma", f_exp / 1e12, "TFLOP/s", peak),
             "k_chain_fwd": ("hbm", (1 if split16 else 2) * one_chain / 1e9, "GB/s", PEAK_HBM_GBS),
             "k_chain_bwd": ("hbm", one_chain / 1e9 if split16 else 0.0, "GB/s", PEAK_HBM_GBS),
             "k_grad": ("mfma", f_grad / 1e12, "TFLOP/s", peak),
@@ -677,14 +681,19 @@ def main():
     if seg:
         pass  # kern and roof set above
     elif p16:
-        names = {"k_expm": "k_blkp_exp", "k_chain_fwd": "k_blkp_chain" if split16 else "k_blkp_dual",
+        names = {"k_expm": "k_blkp_int" if ideg else "k_blkp_exp",
+                 "k_chain_fwd": "k_blkp_chain" if split16 else "k_blkp_dual",
                  "k_chain_bwd": "k_blkp_chain" if split16 else "k_blkp_dual", "k_grad": "k_blkp_grad"}
         live_k = ("k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad") if split16 else ("k_expm", "k_chain_fwd", "k_grad")
         for k in live_k:
             kern[k]["kernel"] = names[k]
         # per-launch figures: the step's work over its launches (the formation runs once per seed group)
         kern["k_expm"]["products_per_unit"] = prods / max(B * Nt * nlive, 1)
-        kern["k_expm"]["executed_gflop_per_launch"] = f_exp / 1e9 / max(lps["k_expm"], 1.0)
+        kern["k_expm"]["executed_gflop_per_launch"] = (f_int if ideg else f_exp) / 1e9 / max(lps["k_expm"], 1.0)
+        if ideg:
+            kern["k_expm"]["interp_degree"] = ideg
+            t = per_step["k_expm"] / 1e3
+            kern["k_expm"]["executed_tflops"] = f_int / 1e12 / t if t > 0 else 0.0
         kern["k_expm"]["hbm_bytes_per_launch"] = u_bytes / max(lps["k_expm"], 1.0)
         for k in ("k_chain_fwd", "k_chain_bwd") if split16 else ("k_chain_fwd",):
             kern[k]["hbm_bytes_per_launch"] = models[k][1] * 1e9 / max(lps[k], 1.0)

@@ -199,8 +199,10 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
  * propagate left for grape_sensitivity (the reference's split call form, examples/ipopt_callbacks_exp.jl:11-31):
  * 0 the states x_k, 1 the segmented forward (blocks of 2-3 rows: G at every segment's end, x_k rebuilt on demand;
  * grape_sensitivity then runs the segmented backward alone), 2 the stored propagators of blocks of 5..16 rows
- * (grape_sensitivity: the co-state chain and the gradient on them). */
-#define QOC_INFO_ENTRIES 12
+ * (grape_sensitivity: the co-state chain and the gradient on them).  info[12] = the degree of the last stored-propagator
+ * formation's interpolation in u (one control: U(u) = Σ_i T_i(ξ) M_i over the batch's control range), 0 when the
+ * exponentials were formed per slice. */
+#define QOC_INFO_ENTRIES 13
 int qoc_get_info(qoc_ctx* ctx, long long* info /*[QOC_INFO_ENTRIES]*/);
 int qoc_get_info_n(qoc_ctx* ctx, long long* info, int n);
 

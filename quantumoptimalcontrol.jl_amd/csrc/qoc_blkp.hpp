@@ -101,6 +101,11 @@ struct BlkpArgs {
   double theta[BLKP_RMAX + 1][16];
   double rcap;                 // > 0: the accurate (r, s) choice, 2^-s ρ̂ <= rcap (QOC_BLKP_RCAP, default 1); 0: the
                                // fewest products (slack / tail)
+  // skew-Hermitian blocks, Chebyshev form (k_blkp_exp<.., CM > 0>): the coefficient table (blkp_cheb_table, one row of
+  // BLKP_CT_STRIDE doubles per grid point ρ_c(g) = 2^((g - BLKP_CT_G0) / 4), g < cgn <= ρ_c = crmax)
+  const double* ctab;
+  int cgn;
+  double crmax;
   long long unit0, units;      // this launch's units [unit0, units) of B Nt nwb: unit = (b Nt + k) nwb + β
   const int* wrow;             // nwb x 16 rows of the live wave blocks
   const cx<double>* At;        // (nu+1) N x N shifted generators Ã_j, column-major
@@ -262,10 +267,140 @@ __device__ __forceinline__ CMat blkp_horner_b(int i, const CMat& X, const CMat& 
   return B;
 }
 
+// ---- the Chebyshev form for skew-Hermitian blocks ----
+// exp(X) for X = -i H (H Hermitian, ||H||_2 <= ρ̂): with s halvings (2^-s ρ̂ <= crmax) and the grid point ρ_c >= 2^-s ρ̂,
+// Y = 2^-s H / ρ_c has its spectrum in [-1, 1], and the Jacobi-Anger series
+//   exp(2^-s X) = exp(-i ρ_c Y) = J_0(ρ_c) + 2 Σ_{k>=1} (-i)^k J_k(ρ_c) T_k(Y)
+// converges without cancellation (|T_k(Y)| <= 1, the Bessel coefficients decay): no e^ρ growth of the rounding as in
+// the Taylor terms, and few or no squarings to amplify it.  Truncated at degree n (tail <= 2^-57, host), evaluated
+// by block Clenshaw in Z = T_CM(Y): p = Σ_{q=0}^{Q} A_q(Y) T_q(Z), A_q = Σ_{j<CM} β_{q,j} (-i)^j T_j(Y) (the host's
+// exact rewrite of the series, T_j T_{CM q} = (T_{CM q + j} + T_{CM q - j}) / 2; β real since CM is even), so CM - 1
+// products for T_2..T_CM and Q for the recurrence b_q = A_q + 2 Z b_{q+1} - b_{q+2}, p = A_0 + Z b_1 - b_2.  Every left
+// operand is Hermitian (its transpose is its conjugate): no LDS round trip but the squarings'.
+// Table row: [ρ_c, 1 / ρ_c, Q, -, β[q][j] (q = 0..Q, j < CM)]
+constexpr int BLKP_CT_STRIDE = 64, BLKP_CT_G0 = 32;
+
+// (2 T)^T for a Hermitian T (the left operand of a product with 2 T)
+__device__ __forceinline__ CMat blkp_herm2t(const CMat& T) {
+  CMat o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    o.r[e] = 2.0 * T.r[e];
+    o.i[e] = -2.0 * T.i[e];
+  }
+  return o;
+}
+
+template <int CM>
+__device__ __forceinline__ CMat blkp_cheb(const CMat& X, double rho, const BlkpArgs& a, double2* tile, bool four,
+                                          int& nprod) {
+  const int l = threadIdx.x & 63, j = l & 15, g = l >> 4;
+  int s = 0;
+  double q = rho;
+  while (s < 15 && q > a.crmax) {
+    q *= 0.5;
+    ++s;
+  }
+  // the smallest grid point ρ_c(gi) >= q (a float log2 guess, corrected against the table)
+  int gi = q > 0.0 ? (int)ceilf(4.0f * __builtin_amdgcn_logf((float)q)) + BLKP_CT_G0 : 0;
+  gi = min(max(gi, 0), a.cgn - 1);
+  while (gi < a.cgn - 1 && a.ctab[(size_t)gi * BLKP_CT_STRIDE] < q) ++gi;
+  while (gi > 0 && a.ctab[(size_t)(gi - 1) * BLKP_CT_STRIDE] >= q) --gi;
+  gi = __builtin_amdgcn_readfirstlane(gi);
+  const double* ct = a.ctab + (size_t)gi * BLKP_CT_STRIDE;
+  const double sc = ldexp(ct[1], -s);
+  const int Q = __builtin_amdgcn_readfirstlane((int)ct[2]);
+  // T[1] = Y = i X sc (Hermitian), T[2..CM-1], Z = T_CM
+  CMat T[CM];
+  CMat mI, Z;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    T[1].r[e] = -X.i[e] * sc;
+    T[1].i[e] = X.r[e] * sc;
+    mI.r[e] = g + 4 * e == j ? -1.0 : 0.0;
+    mI.i[e] = 0.0;
+  }
+  auto neg = [](const CMat& M) {
+    CMat o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o.r[e] = -M.r[e];
+      o.i[e] = -M.i[e];
+    }
+    return o;
+  };
+  // T_{a+b} = 2 T_a T_b - T_{|a-b|}
+  T[2] = cm_mulx<true>(four, blkp_herm2t(T[1]), T[1], mI);
+  T[3] = cm_mulx<true>(four, blkp_herm2t(T[1]), T[2], neg(T[1]));
+  if constexpr (CM == 4) {
+    Z = cm_mulx<true>(four, blkp_herm2t(T[2]), T[2], mI);
+  } else {
+    static_assert(CM == 6, "block size 4 or 6");
+    T[4] = cm_mulx<true>(four, blkp_herm2t(T[2]), T[2], mI);
+    T[5] = cm_mulx<true>(four, blkp_herm2t(T[2]), T[3], neg(T[1]));
+    Z = cm_mulx<true>(four, blkp_herm2t(T[3]), T[3], mI);
+  }
+  // A_q = Σ_j β_{q,j} (-i)^j T_j, minus an addend D (the recurrence's b_{q+2})
+  auto Aq = [&](int qq, const CMat& D) {
+    const double* bq = ct + 4 + qq * CM;
+    CMat A;
+    const double b0 = bq[0];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      A.r[e] = (g + 4 * e == j ? b0 : 0.0) - D.r[e];
+      A.i[e] = -D.i[e];
+    }
+#pragma unroll
+    for (int jj = 1; jj < CM; ++jj) {
+      const double b = bq[jj];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const double tr = T[jj].r[e], ti = T[jj].i[e];
+        switch (jj & 3) {  // (-i)^jj
+          case 0: A.r[e] = fma(b, tr, A.r[e]); A.i[e] = fma(b, ti, A.i[e]); break;
+          case 1: A.r[e] = fma(b, ti, A.r[e]); A.i[e] = fma(-b, tr, A.i[e]); break;
+          case 2: A.r[e] = fma(-b, tr, A.r[e]); A.i[e] = fma(-b, ti, A.i[e]); break;
+          default: A.r[e] = fma(-b, ti, A.r[e]); A.i[e] = fma(b, tr, A.i[e]); break;
+        }
+      }
+    }
+    return A;
+  };
+  CMat zero;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) zero.r[e] = zero.i[e] = 0.0;
+  CMat R;
+  if (Q == 0) {
+    R = Aq(0, zero);
+  } else {
+    const CMat Z2t = blkp_herm2t(Z);
+    CMat b1 = Aq(Q, zero), b2 = zero;
+    for (int qq = Q - 1; qq >= 1; --qq) {
+      const CMat nb = cm_mulx<true>(four, Z2t, b1, Aq(qq, b2));
+      b2 = b1;
+      b1 = nb;
+    }
+    CMat Zt;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      Zt.r[e] = 0.5 * Z2t.r[e];
+      Zt.i[e] = 0.5 * Z2t.i[e];
+    }
+    R = cm_mulx<true>(four, Zt, b1, Aq(0, b2));
+  }
+  for (int t = 0; t < s; ++t) {
+    const CMat Rt = cm_transpose(R, tile);
+    R = cm_mulx<false>(four, Rt, R, R);
+  }
+  nprod = CM - 1 + Q + s;
+  return R;
+}
+
 // One workgroup of BLKP_WG / 64 waves walks the units wave by wave (persistent grid).  LDS: the generators' blocks in
-// C layout ([β][j][e][lane] double2) and one transpose tile per wave.
+// C layout ([β][j][e][lane] double2) and one transpose tile per wave.  CM > 0: skew-Hermitian blocks in the Chebyshev
+// form (blkp_cheb, block size CM); 0: Taylor / Paterson-Stockmeyer and squarings.
 // OCC: workgroups per CU the launch bound asks for (3: 168 VGPRs, 3 spilled; 2: 214 with AGPRs, no spills)
-template <int NU, int OCC>
+template <int NU, int OCC, int CM = 0>
 __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double2* gen = reinterpret_cast<double2*>(smem);
@@ -315,6 +450,11 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
     }
     const double n1 = row_max16(xsum_rows(cs)), ninf = xmax_rows(rmax);
     const double rho = uniform_f64(sqrt(n1 * ninf));
+    CMat R;
+    int nprod = 0;
+    if constexpr (CM > 0) {
+      R = blkp_cheb<CM>(X, rho, a, tile, four, nprod);
+    } else {
     // (the sharper α_p = max(‖X^p‖^{1/p}, ‖X^{p+1}‖^{1/(p+1)}) of Al-Mohy & Higham from the computed powers chose the
     // same (r, s) on the tunable bus -- 10.75 products per unit either way -- and cost three more reductions)
     int r = BLKP_RMAX, s = 0;
@@ -410,7 +550,7 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
     } else {
       X4t = cm_transpose(X4, tile);
     }
-    CMat R = blkp_horner_b(r - 1, X, X2, X3);
+    R = blkp_horner_b(r - 1, X, X2, X3);
     {
       const double cm = kBlkpInvFact[4 * r];
 #pragma unroll
@@ -424,6 +564,8 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
       const CMat Rt = cm_transpose(R, tile);
       R = cm_mulx<false>(four, Rt, R, R);
     }
+    nprod = r + 2 + s;
+    }  // CM == 0
     const double mr = fma(u2, a.mur[2], fma(u1, a.mur[1], a.mur[0]));
     const double mi = fma(u2, a.mui[2], fma(u1, a.mui[1], a.mui[0]));
     const double em = a.skew ? 1.0 : exp(mr);  // skew-Hermitian blocks: imaginary shifts
@@ -436,9 +578,127 @@ __global__ __launch_bounds__(BLKP_WG, OCC) void k_blkp_exp(const BlkpArgs a) {
       const double vr = fma(pr, R.r[e], -pi * R.i[e]), vi = fma(pr, R.i[e], pi * R.r[e]);
       uf[blkp_upos(g + 4 * e, j)] = make_double2(vr, vi);
     }
-    prods += (unsigned long long)(r + 2 + s);
+    prods += (unsigned long long)nprod;
   }
   if (a.prods && l == 0 && prods) atomicAdd(a.prods + (blockIdx.x & (TERM_SLOTS - 1)), prods);
+}
+
+// ---- one control: the propagators interpolated in u (k_blkp_int) ----
+// With a single control (nu = 1, the tunable bus' flux) every slice propagator lies on one curve,
+// U(u) = e^{μ(u)} exp(Ã_0 + u Ã_1), an entire function of the scalar u.  On the batch's control range [lo, hi] its
+// Chebyshev expansion in ξ = (2u - lo - hi) / (hi - lo) converges super-exponentially (|c_i| ~ (ρ_1 w / 4)^i / i!,
+// w = hi - lo), so a degree D ~ 20 reaches the ulp: exp(Ã_0 + u Ã_1) = Σ_{i<=D} T_i(ξ) M_i.  The host forms the D + 1
+// coefficient matrices once per range (exponentials at 40 Chebyshev points in long double, then the discrete cosine
+// transform: blkp_interp_setup); a unit is then D + 1 scaled sums of LDS-resident 16 x 16 matrices -- ~200 VALU
+// instructions instead of 11 MFMA products -- and its accuracy is that of the interpolant (truncation < 2^-56, no
+// squarings: tools/tb_truth.py).
+struct BlkpIntArgs {
+  int nwb, D;                  // live wave blocks, the largest interpolation degree (the coefficients' stride D + 1)
+  int beta0, nb;               // this launch's blocks [beta0, beta0 + nb) (their coefficients fill the LDS)
+  int Db[8];                   // each block's own degree (its coefficients alone decide it: a block's propagators do
+                               // not depend on which other blocks the launch carries)
+  long long slot0, slots;      // this launch's (seed, slice) slots [slot0, slots) of B Nt; unit = slot nwb + β
+  long long ubase;             // the unit whose propagator sits at UF[0]
+  const double* u;             // B x Nt (nu = 1)
+  double xa, xb;               // ξ = xa u + xb
+  double mur[2], mui[2];       // μ(u) = μ_0 + u μ_1
+  int skew;                    // imaginary shifts: e^{μ} = e^{i Im μ}
+  const double2* M;            // [β][i][p]: M_i of block β at the propagator store positions p = blkp_upos(r, c)
+                               // (lane l, register e: p = 64 e + l), so that loads and stores are contiguous
+  double2* UF;
+  unsigned long long* prods;   // counted as 0 products (none run)
+};
+__host__ __device__ inline size_t blkp_int_lds(int nwb, int D) { return (size_t)nwb * (D + 1) * 256 * sizeof(double2); }
+
+// UPW consecutive slots of one block per wave: each M_i entry read from LDS once serves UPW units
+template <int UPW, int WG>
+__global__ __launch_bounds__(WG) void k_blkp_int(const BlkpIntArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double2* Ms = reinterpret_cast<double2*>(smem);
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int nwb = a.nwb, D = a.D, nb = a.nb;
+  for (int e = tid; e < nb * (D + 1) * 256; e += blockDim.x) Ms[e] = a.M[(size_t)a.beta0 * (D + 1) * 256 + e];
+  __syncthreads();
+  const long long nsg = (a.slots - a.slot0 + UPW - 1) / UPW, items = nsg * nb;
+  for (long long it = (long long)blockIdx.x * (blockDim.x >> 6) + w; it < items; it += (long long)gridDim.x * (blockDim.x >> 6)) {
+    const long long sg = it / nb;
+    const int bl = (int)(it - sg * nb), beta = a.beta0 + bl;
+    const long long s0 = a.slot0 + sg * UPW;
+    double uu[UPW], xi[UPW], tm[UPW], tc[UPW];
+    double ar[UPW][4], ai[UPW][4];
+#pragma unroll
+    for (int t = 0; t < UPW; ++t) {
+      uu[t] = a.u[min(s0 + t, a.slots - 1)];
+      xi[t] = fma(a.xa, uu[t], a.xb);
+      tm[t] = 1.0;  // T_{i-1}
+      tc[t] = 1.0;  // T_i (i = 0)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ar[t][e] = ai[t][e] = 0.0;
+    }
+    const double2* Mb = Ms + (size_t)bl * (D + 1) * 256 + l;
+    const int Dq = a.Db[beta];
+    for (int i = 0; i <= Dq; ++i) {
+      double2 mv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mv[e] = Mb[(size_t)i * 256 + 64 * e];
+#pragma unroll
+      for (int t = 0; t < UPW; ++t) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ar[t][e] = fma(tc[t], mv[e].x, ar[t][e]);
+          ai[t][e] = fma(tc[t], mv[e].y, ai[t][e]);
+        }
+        // T_{i+1} = 2 ξ T_i - T_{i-1} (T_1 = ξ)
+        const double tn = i == 0 ? xi[t] : fma(2.0 * xi[t], tc[t], -tm[t]);
+        tm[t] = tc[t];
+        tc[t] = tn;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < UPW; ++t) {
+      const long long slot = s0 + t;
+      if (slot >= a.slots) break;  // uniform
+      const double mr = fma(uu[t], a.mur[1], a.mur[0]), mi = fma(uu[t], a.mui[1], a.mui[0]);
+      const double em = a.skew ? 1.0 : exp(mr);
+      double sn, cn;
+      sincos(mi, &sn, &cn);
+      const double pr = em * cn, pi = em * sn;
+      double2* const uf = a.UF + (slot * nwb + beta - a.ubase) * 256;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // store position 64 e + l (1 KB contiguous per store)
+        const double vr = fma(pr, ar[t][e], -pi * ai[t][e]), vi = fma(pr, ai[t][e], pi * ar[t][e]);
+        uf[64 * e + l] = make_double2(vr, vi);
+      }
+    }
+  }
+}
+
+// min / max of n doubles: per block into part[2 blockIdx.x], [2 blockIdx.x + 1] (the host finishes)
+static __global__ void k_minmax(const double* __restrict__ v, long long n, double* part) {
+  double lo = __builtin_inf(), hi = -__builtin_inf();
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    lo = fmin(lo, v[e]);
+    hi = fmax(hi, v[e]);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, off));
+    hi = fmax(hi, __shfl_xor(hi, off));
+  }
+  __shared__ double sl[16], sh[16];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sl[w] = lo;
+    sh[w] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) {
+      lo = fmin(lo, sl[i]);
+      hi = fmax(hi, sh[i]);
+    }
+    part[2 * blockIdx.x] = lo;
+    part[2 * blockIdx.x + 1] = hi;
+  }
 }
 
 // ---- chains from the stored propagators ----

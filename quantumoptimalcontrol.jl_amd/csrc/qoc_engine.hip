@@ -556,6 +556,10 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->d_dead_rows) hipFree(c->d_dead_rows);
   if (c->d_gc_part) hipFree(c->d_gc_part);
   if (c->d_gseg) hipFree(c->d_gseg);
+  if (c->d_blkp_ctab) hipFree(c->d_blkp_ctab);
+  if (c->d_blkp_M) hipFree(c->d_blkp_M);
+  if (c->d_minmax) hipFree(c->d_minmax);
+  if (c->h_minmax) hipHostFree(c->h_minmax);
   if (c->h_flag) hipHostFree(c->h_flag);
   if (c->flag_ev) hipEventDestroy(c->flag_ev);
   void* ptrs[] = {c->d_A, c->d_x0, c->d_Xt, c->d_pmask, c->d_u,    c->d_U,    c->d_X, c->d_L, c->d_u_lam, c->d_coef_lam, c->d_blkU, c->d_J_scr, c->d_coef_scr,
@@ -728,6 +732,7 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
     c->skew_exact = false;
   }
   if (c->tchain_ok) {  // invariant blocks of the generators (qoc_blk.hpp)
+    c->int_ok = c->int_failed = false;  // the interpolated propagators belong to the old generators
     r = blk_detect(c);
     if (r) return r;
   } else {
@@ -1368,6 +1373,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[9] = c->fwd_captured ? 1 : 0;
   // 6: the last eval ran the stored-propagator chains of blocks of 5..16 rows (propagate / grape_sensitivity: 4)
   info[11] = c->fwd_kind;
+  info[12] = c->last_int_D;  // the stored block propagators' last formation: interpolation degree in u (0: exponentials)
   info[10] = blk_active(c) ? (blku_on(c) ? 5 : blkp_on(c) && c->last_eval_mode == 7 ? 6 : blk_rot(c) ? 4 : 3) : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
   return QOC_OK;
 }

@@ -155,6 +155,23 @@ struct qoc_ctx {
   double* d_u_lam = nullptr;     // B x Nt x nu: u of that backward
   void* d_blkU = nullptr;        // B x Nt x NB^2 x nblk complex: block propagators of the eval's forward (fused backward)
   size_t blkU_bytes = 0;         // its allocated size (reallocated when a new block layout needs more)
+  // one control: the propagators interpolated in u (qoc_blkp.hpp k_blkp_int): the coefficient matrices of the control
+  // range [int_lo, int_hi] for the live-wave layout int_wrow, degree int_D (int_ok: valid for the current generators)
+  double2* d_blkp_M = nullptr;
+  size_t blkp_M_bytes = 0;
+  bool int_ok = false;
+  int int_D = 0;
+  std::vector<int> int_Db;           // per live wave block
+  double int_lo = 0.0, int_hi = 0.0;
+  std::vector<int> int_wrow;
+  bool int_failed = false;           // [int_fail_lo, int_fail_hi] did not converge (a wider range will not either)
+  double int_fail_lo = 0.0, int_fail_hi = 0.0;
+  double* d_minmax = nullptr;        // k_minmax partials (256 blocks x 2)
+  double* h_minmax = nullptr;        // pinned host copy
+  int last_int_D = 0;                // the degree the last formation ran with (0: not interpolated; qoc_get_info)
+  double* d_blkp_ctab = nullptr; // the Chebyshev form's coefficient table (qoc_blkp.hpp blkp_cheb), for ctab_cm / ctab_rmax
+  int ctab_cm = 0;
+  double ctab_rmax = 0.0;
   // the segmented block eval (qoc_blkseg.hpp) writes neither x_k nor λ_k: qoc_get_states / a later backward rebuild
   // the states on demand (blku_states) from the u in d_u, with J and the coefficients going to scratch
   bool X_lazy = false;

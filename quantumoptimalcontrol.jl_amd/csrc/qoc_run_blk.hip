@@ -558,6 +558,294 @@ static void blkp_theta_table(int tail, double (&theta)[BLKP_RMAX + 1][16]) {
     }
 }
 
+// The Chebyshev form's table (qoc_blkp.hpp blkp_cheb) for block size cm up to ρ_c = crmax: per grid point
+// ρ_c = 2^((g - BLKP_CT_G0) / 4) the Bessel values J_k(ρ_c) (Miller's backward recurrence in long double, normalised
+// by J_0 + 2 Σ J_2k = 1), the degree n with Σ_{k>n} 2 |J_k| <= 2^-57, and the series rewritten for block Clenshaw in
+// Z = T_cm: c_k = (2 - δ_k0) (-i)^k J_k, then from the top block down a_{q,j} = 2 c_{cm q + j}, c_{cm q - j} -= c_{cm q + j}
+// (j = 1..cm-1), a_{q,0} = c_{cm q}; β_{q,j} = i^j a_{q,j} is real for even cm.
+static int blkp_cheb_table(qoc_ctx* c, int cm, double crmax) {
+  if (c->d_blkp_ctab && c->ctab_cm == cm && c->ctab_rmax == crmax) return QOC_OK;
+  const int gn = BLKP_CT_G0 + (int)std::lround(4.0 * std::log2(crmax)) + 1;
+  std::vector<double> tab((size_t)gn * BLKP_CT_STRIDE, 0.0);
+  typedef long double LD;
+  for (int g = 0; g < gn; ++g) {
+    const LD rc = std::pow((LD)2, (LD)(g - BLKP_CT_G0) / 4);
+    const int K = 100, M = K + 60 + (int)(4 * rc);
+    std::vector<LD> jb(M + 2, 0.0L);
+    jb[M] = 1e-300L;
+    for (int k = M; k >= 1; --k) jb[k - 1] = (2.0L * k / rc) * jb[k] - jb[k + 1];
+    LD nrm = jb[0];
+    for (int k = 2; k <= M; k += 2) nrm += 2 * jb[k];
+    std::vector<LD> J(K + 1);
+    for (int k = 0; k <= K; ++k) J[k] = jb[k] / nrm;
+    int n = K;
+    LD tail = 0;
+    while (n > 0 && tail + 2 * std::fabs(J[n]) <= std::ldexp(1.0L, -57)) tail += 2 * std::fabs(J[n--]);
+    const int Q = n <= cm - 1 ? 0 : (n - (cm - 1) + cm - 1) / cm;
+    if (4 + (Q + 1) * cm > BLKP_CT_STRIDE) return fail(c, QOC_ERR_UNSUPPORTED, "Chebyshev table: degree %d at rho %g", n, (double)rc);
+    const int L = cm * (Q + 1);
+    std::vector<LD> cr(L, 0.0L), ci(L, 0.0L);  // c_k = (2 - δ) (-i)^k J_k
+    for (int k = 0; k <= n && k < L; ++k) {
+      const LD v = (k ? 2 : 1) * J[k];
+      switch (k & 3) {
+        case 0: cr[k] = v; break;
+        case 1: ci[k] = -v; break;
+        case 2: cr[k] = -v; break;
+        default: ci[k] = v; break;
+      }
+    }
+    double* row = tab.data() + (size_t)g * BLKP_CT_STRIDE;
+    row[0] = (double)rc;
+    row[1] = (double)(1.0L / rc);
+    row[2] = Q;
+    for (int qq = Q; qq >= 0; --qq)
+      for (int jj = cm - 1; jj >= 0; --jj) {
+        const int k = cm * qq + jj;
+        LD ar = cr[k], ai = ci[k];
+        if (qq > 0 && jj > 0) {
+          ar *= 2;
+          ai *= 2;
+          cr[cm * qq - jj] -= cr[k];
+          ci[cm * qq - jj] -= ci[k];
+        }
+        // β = i^j a (real)
+        LD br = ar, bi = ai;
+        for (int t = 0; t < (jj & 3); ++t) {
+          const LD nr = -bi, ni = br;
+          br = nr;
+          bi = ni;
+        }
+        if (std::fabs(bi) > 1e-12L * (std::fabs(br) + 1e-300L) && std::fabs(bi) > 1e-300L)
+          return fail(c, QOC_ERR_UNSUPPORTED, "Chebyshev table: complex coefficient (g %d, q %d, j %d)", g, qq, jj);
+        row[4 + qq * cm + jj] = (double)br;
+      }
+  }
+  if (c->d_blkp_ctab) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(c->d_blkp_ctab));
+    c->d_blkp_ctab = nullptr;
+  }
+  HIPCHK(c, hipMalloc((void**)&c->d_blkp_ctab, tab.size() * sizeof(double)));
+  HIPCHK(c, hipMemcpy(c->d_blkp_ctab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
+  c->ctab_cm = cm;
+  c->ctab_rmax = crmax;
+  return QOC_OK;
+}
+
+// ---- one control: the propagators interpolated in u (qoc_blkp.hpp k_blkp_int) ----
+typedef long double LD;
+// exp(X) of an n x n complex matrix in long double (row-major, re / im apart): scaling to ||X||_1 <= 1/2, Taylor
+// degree 30 (tail < 1e-40), squarings; 64-bit mantissas, so its own error (~1e-18) is far below the fp64 result
+static void ld_expm(int n, const std::vector<LD>& Xr, const std::vector<LD>& Xi, std::vector<LD>& Er, std::vector<LD>& Ei) {
+  LD n1 = 0;
+  for (int c = 0; c < n; ++c) {
+    LD sum = 0;
+    for (int r = 0; r < n; ++r) sum += std::hypot(Xr[r * n + c], Xi[r * n + c]);
+    n1 = std::max(n1, sum);
+  }
+  int s = 0;
+  while (n1 > 0.5L && s < 60) {
+    n1 *= 0.5L;
+    ++s;
+  }
+  const LD sc = std::ldexp(1.0L, -s);
+  std::vector<LD> Yr(n * n), Yi(n * n), Tr(n * n, 0), Ti(n * n, 0), Nr(n * n), Ni(n * n);
+  for (int e = 0; e < n * n; ++e) {
+    Yr[e] = Xr[e] * sc;
+    Yi[e] = Xi[e] * sc;
+  }
+  Er.assign(n * n, 0);
+  Ei.assign(n * n, 0);
+  for (int d = 0; d < n; ++d) Tr[d * n + d] = Er[d * n + d] = 1;
+  auto mul = [&](const std::vector<LD>& Ar, const std::vector<LD>& Ai, const std::vector<LD>& Br, const std::vector<LD>& Bi) {
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c < n; ++c) {
+        LD sr = 0, si = 0;
+        for (int q = 0; q < n; ++q) {
+          sr += Ar[r * n + q] * Br[q * n + c] - Ai[r * n + q] * Bi[q * n + c];
+          si += Ar[r * n + q] * Bi[q * n + c] + Ai[r * n + q] * Br[q * n + c];
+        }
+        Nr[r * n + c] = sr;
+        Ni[r * n + c] = si;
+      }
+  };
+  for (int k = 1; k <= 30; ++k) {
+    mul(Tr, Ti, Yr, Yi);
+    for (int e = 0; e < n * n; ++e) {
+      Tr[e] = Nr[e] / k;
+      Ti[e] = Ni[e] / k;
+      Er[e] += Tr[e];
+      Ei[e] += Ti[e];
+    }
+  }
+  for (int t = 0; t < s; ++t) {
+    mul(Er, Ei, Er, Ei);
+    Er = Nr;
+    Ei = Ni;
+  }
+}
+
+// the control range [lo, hi] of the batch in d_u (nu = 1): a partial min / max per block, finished on the host
+static int blkp_urange(qoc_ctx* c, double& lo, double& hi) {
+  const long long n = (long long)c->B * c->Nt * c->nu;
+  const int grid = (int)std::max<long long>(1, std::min<long long>(256, (n + 255) / 256));
+  if (!c->d_minmax) {
+    HIPCHK(c, hipMalloc((void**)&c->d_minmax, 512 * sizeof(double)));
+    HIPCHK(c, hipHostMalloc((void**)&c->h_minmax, 512 * sizeof(double), hipHostMallocDefault));
+  }
+  hipLaunchKernelGGL(k_minmax, dim3(grid), dim3(256), 0, c->stream, (const double*)c->d_u, n, c->d_minmax);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->h_minmax, c->d_minmax, 2 * grid * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  lo = c->h_minmax[0];
+  hi = c->h_minmax[1];
+  for (int b = 1; b < grid; ++b) {
+    lo = std::min(lo, c->h_minmax[2 * b]);
+    hi = std::max(hi, c->h_minmax[2 * b + 1]);
+  }
+  return QOC_OK;
+}
+
+// The coefficient matrices of exp(Ã_0 + u Ã_1) on [lo, hi] for every live wave block: the exponentials at NI
+// Chebyshev points θ_k = π (k + 1/2) / NI in long double, M_i = (2 - δ_i0) / NI Σ_k F_k cos(i θ_k), D the last index
+// whose tail max_{i > D} |M_i| is <= 2^-56 (the coefficients of an entire function fall super-exponentially; the
+// aliasing of the NI-point transform is below the last ones).  Returns 1 when the series has not converged within NI
+// points (a control range too wide) or the coefficients exceed the LDS.
+static int blkp_interp_coeffs(qoc_ctx* c, const std::vector<int>& wrow, double lo, double hi) {
+  constexpr int NI = 40;
+  const int N = c->N, nwb = (int)(wrow.size() / 16);
+  const size_t NN = (size_t)N * N;
+  const LD pi = std::acos(-1.0L), mid = ((LD)lo + hi) / 2, half = ((LD)hi - lo) / 2;
+  std::vector<std::vector<LD>> Mr((size_t)nwb * NI, std::vector<LD>(256, 0)), Mi = Mr;
+  std::vector<LD> Xr(256), Xi(256), Er, Ei;
+  for (int b = 0; b < nwb; ++b)
+    for (int k = 0; k < NI; ++k) {
+      const LD th = pi * (k + 0.5L) / NI, u = mid + half * std::cos(th);
+      for (int r = 0; r < 16; ++r)
+        for (int q = 0; q < 16; ++q) {
+          const int row = wrow[16 * b + r], col = wrow[16 * b + q];
+          LD vr = 0, vi = 0;
+          if (row >= 0 && col >= 0) {
+            for (int j = 0; j <= 1; ++j) {
+              const double* a = c->h_gen.data() + 2 * (j * NN + row + (size_t)N * col);
+              LD ar = a[0], ai = a[1];
+              if (row == col) {
+                ar -= c->tprm.mur[j];
+                ai -= c->tprm.mui[j];
+              }
+              const LD f = j ? u : 1.0L;
+              vr += f * ar;
+              vi += f * ai;
+            }
+          }
+          Xr[r * 16 + q] = vr;
+          Xi[r * 16 + q] = vi;
+        }
+      ld_expm(16, Xr, Xi, Er, Ei);
+      for (int i = 0; i < NI; ++i) {
+        const LD w = std::cos(i * th) * (i ? 2.0L : 1.0L) / NI;
+        auto& mr = Mr[(size_t)b * NI + i];
+        auto& mi = Mi[(size_t)b * NI + i];
+        for (int e = 0; e < 256; ++e) {
+          mr[e] += w * Er[e];
+          mi[e] += w * Ei[e];
+        }
+      }
+    }
+  // per block (its own degree: a block's propagators do not depend on the other blocks of the launch); the long-double
+  // transform's own rounding leaves a floor near 1e-18 under the converged coefficients
+  const LD tol = std::ldexp(1.0L, -56);
+  if (nwb > 8) return 1;
+  std::vector<int> Db(nwb);
+  int D = 0;
+  for (int b = 0; b < nwb; ++b) {
+    std::vector<LD> mx(NI, 0);
+    for (int i = 0; i < NI; ++i)
+      for (int e = 0; e < 256; ++e)
+        mx[i] = std::max(mx[i], std::max(std::fabs(Mr[(size_t)b * NI + i][e]), std::fabs(Mi[(size_t)b * NI + i][e])));
+    if (mx[NI - 1] > tol || mx[NI - 2] > tol) return 1;
+    int d = NI - 1;
+    while (d > 0 && mx[d] <= tol) --d;
+    Db[b] = d;
+    D = std::max(D, d);
+  }
+  if (blkp_int_lds(1, D) > (size_t)150 * 1024) return 1;  // one block's coefficients per launch at least
+  std::vector<double2> h((size_t)nwb * (D + 1) * 256);
+  for (int b = 0; b < nwb; ++b)
+    for (int i = 0; i <= D; ++i)
+      for (int p = 0; p < 256; ++p) {  // store position p = blkp_upos(r, col): col = 4 ((p >> 4) & 3) + (p >> 6)
+        const int col = 4 * ((p >> 4) & 3) + (p >> 6), row = (p & 15) ^ col, ent = row * 16 + col;
+        h[((size_t)b * (D + 1) + i) * 256 + p] =
+            make_double2((double)Mr[(size_t)b * NI + i][ent], (double)Mi[(size_t)b * NI + i][ent]);
+      }
+  const size_t bytes = h.size() * sizeof(double2);
+  if (c->blkp_M_bytes < bytes) {
+    if (c->d_blkp_M) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if (c->stream2) HIPCHK(c, hipStreamSynchronize(c->stream2));
+      HIPCHK(c, hipFree(c->d_blkp_M));
+      c->d_blkp_M = nullptr;
+    }
+    HIPCHK(c, hipMalloc((void**)&c->d_blkp_M, bytes));
+    c->blkp_M_bytes = bytes;
+  }
+  HIPCHK(c, hipMemcpy(c->d_blkp_M, h.data(), bytes, hipMemcpyHostToDevice));
+  c->int_D = D;
+  c->int_Db = Db;
+  c->int_lo = lo;
+  c->int_hi = hi;
+  c->int_wrow = wrow;
+  c->int_ok = true;
+  return QOC_OK;
+}
+
+// 0: the formation interpolates (ia filled), 1: it forms the exponentials.  One control (nu = 1) and
+// QOC_BLKP_INTERP != 0; the coefficients are recomputed when the batch's control range leaves the one they were made
+// for (then widened by 5 % each side, so that an optimiser's drifting controls rarely trigger it) or the generators
+// or the live-block layout changed.
+static int blkp_interp_setup(qoc_ctx* c, const BlkArgs& bk, BlkpIntArgs& ia) {
+  const char* env = getenv("QOC_BLKP_INTERP");
+  if (c->nu != 1 || (env && atoi(env) == 0)) return 1;
+  double lo, hi;
+  int r = blkp_urange(c, lo, hi);
+  if (r) return r;
+  if (!std::isfinite(lo) || !std::isfinite(hi)) return 1;
+  const std::vector<int>& wrow = bk.wrow == c->d_wrow_live ? c->h_wrow_live : c->h_wrow;  // the host copy of bk's rows
+  if (wrow.size() != 16 * (size_t)bk.nwb) return 1;
+  if (!(c->int_ok && lo >= c->int_lo && hi <= c->int_hi && wrow == c->int_wrow)) {
+    // a range already found too wide (within the failed one, same layout and generators): no second attempt
+    if (c->int_failed && lo <= c->int_fail_lo && hi >= c->int_fail_hi && wrow == c->int_wrow) return 1;
+    const double w = std::max(hi - lo, 1e-3 * std::max(1.0, std::max(std::fabs(lo), std::fabs(hi))));
+    r = blkp_interp_coeffs(c, wrow, lo - 0.05 * w, hi + 0.05 * w);
+    if (r == 1) r = blkp_interp_coeffs(c, wrow, lo, hi);  // without the margin
+    if (r) {
+      c->int_ok = false;
+      if (r == 1) {
+        c->int_failed = true;
+        c->int_fail_lo = lo;
+        c->int_fail_hi = hi;
+        c->int_wrow = wrow;
+      }
+      return r;
+    }
+    c->int_failed = false;
+  }
+  ia = BlkpIntArgs{};
+  ia.nwb = bk.nwb;
+  ia.D = c->int_D;
+  for (int b = 0; b < bk.nwb && b < 8; ++b) ia.Db[b] = c->int_Db[b];
+  ia.u = c->d_u;
+  ia.xa = 2.0 / (c->int_hi - c->int_lo);
+  ia.xb = -(c->int_hi + c->int_lo) / (c->int_hi - c->int_lo);
+  for (int j = 0; j < 2; ++j) {
+    ia.mur[j] = c->tprm.mur[j];
+    ia.mui[j] = c->tprm.mui[j];
+  }
+  ia.skew = c->skew_exact && c->tprm.mur[0] == 0.0 && c->tprm.mur[1] == 0.0;
+  ia.M = c->d_blkp_M;
+  return QOC_OK;
+}
+
 // The formation's arguments and launch shape, the chain kernels' chunk size
 struct BlkpPlan {
   BlkpArgs a;
@@ -566,8 +854,11 @@ struct BlkpPlan {
   int per_cu;
   int ch;
   size_t clds;
+  bool interp;  // the formation interpolates (k_blkp_int)
+  BlkpIntArgs ia;
 };
-static int blkp_plan(qoc_ctx* c, const BlkArgs& bk, int parts, BlkpPlan& pl) {
+// form: the plan of a launch that forms propagators (the interpolation's setup reads the control range)
+static int blkp_plan(qoc_ctx* c, const BlkArgs& bk, int parts, BlkpPlan& pl, bool form = true) {
   BlkpArgs& a = pl.a;
   a = BlkpArgs{};
   a.N = c->N;
@@ -596,6 +887,21 @@ static int blkp_plan(qoc_ctx* c, const BlkArgs& bk, int parts, BlkpPlan& pl) {
   const char* oc = getenv("QOC_BLKP_OCC");
   const bool occ3 = !(oc && atoi(oc) == 2);
   pl.kern = c->nu == 1 ? (occ3 ? k_blkp_exp<1, 3> : k_blkp_exp<1, 2>) : (occ3 ? k_blkp_exp<2, 3> : k_blkp_exp<2, 2>);
+  // skew-Hermitian blocks: the Chebyshev form (QOC_BLKP_CHEB = block size 4 or 6, 0 off; QOC_BLKP_CRMAX the largest
+  // ρ_c before a squaring, 8 or 16)
+  int cm = 0;
+  if (const char* ce = getenv("QOC_BLKP_CHEB")) cm = atoi(ce);
+  if (cm != 4 && cm != 6) cm = 0;
+  if (!a.skew) cm = 0;
+  if (cm) {
+    const double crmax = getenv("QOC_BLKP_CRMAX") && atof(getenv("QOC_BLKP_CRMAX")) >= 16.0 ? 16.0 : 8.0;
+    if (int r = blkp_cheb_table(c, cm, crmax)) return r;
+    a.ctab = c->d_blkp_ctab;
+    a.cgn = BLKP_CT_G0 + (int)std::lround(4.0 * std::log2(crmax)) + 1;
+    a.crmax = crmax;
+    pl.kern = cm == 4 ? (c->nu == 1 ? k_blkp_exp<1, 3, 4> : k_blkp_exp<2, 3, 4>)
+                      : (c->nu == 1 ? k_blkp_exp<1, 2, 6> : k_blkp_exp<2, 2, 6>);
+  }
   HIPCHK(c, blk_lds_attr(pl.kern, pl.lds));
   const int waves = bk.nwb * c->m;
   int ch = blkp_chunk(waves, parts);
@@ -611,10 +917,44 @@ static int blkp_plan(qoc_ctx* c, const BlkArgs& bk, int parts, BlkpPlan& pl) {
       pl.per_cu < 1)
     pl.per_cu = 2;
   if (parts > 1) pl.per_cu = std::min(pl.per_cu, 2);  // a chain workgroup fits beside the formation
+  pl.interp = false;
+  if (form) {
+    const int ri = blkp_interp_setup(c, bk, pl.ia);
+    if (ri > 1 || ri < 0) return ri;
+    pl.interp = ri == 0;
+    c->last_int_D = pl.interp ? pl.ia.D : 0;
+  }
   return QOC_OK;
 }
 // the formation of units [unit0, units) into UF (which holds unit ubase at its start)
 static int blkp_launch_exp(qoc_ctx* c, BlkpPlan& pl, long long unit0, long long units, double2* UF, long long ubase) {
+  if (pl.interp) {  // seed groups cover whole (seed, slice) slots: units are multiples of nwb
+    BlkpIntArgs& ia = pl.ia;
+    ia.slot0 = unit0 / ia.nwb;
+    ia.slots = units / ia.nwb;
+    ia.ubase = ubase;
+    ia.UF = UF;
+    // as many blocks per launch as their coefficients fit the LDS
+    const int per = std::max(1, std::min(ia.nwb, (int)((size_t)150 * 1024 / blkp_int_lds(1, ia.D))));
+    for (int b0 = 0; b0 < ia.nwb; b0 += per) {
+      ia.beta0 = b0;
+      ia.nb = std::min(per, ia.nwb - b0);
+      // workgroups of 4 waves (QOC_BLKP_INT_WG=8: 8 waves), 4 units per wave (QOC_BLKP_INT_UPW=8: 8), up to 4
+      // workgroups per CU in the grid (one holds the LDS at a time when the coefficients exceed 80 KB)
+      const bool w8 = getenv("QOC_BLKP_INT_WG") && atoi(getenv("QOC_BLKP_INT_WG")) == 8;
+      const bool u8 = getenv("QOC_BLKP_INT_UPW") && atoi(getenv("QOC_BLKP_INT_UPW")) == 8;
+      const int iw = w8 ? 8 : 4, upw = u8 ? 8 : 4;
+      auto kern = u8 ? (w8 ? k_blkp_int<8, 512> : k_blkp_int<8, 256>) : (w8 ? k_blkp_int<4, 512> : k_blkp_int<4, 256>);
+      HIPCHK(c, blk_lds_attr(kern, blkp_int_lds(ia.nb, ia.D)));
+      const long long items = (ia.slots - ia.slot0 + upw - 1) / upw * ia.nb;
+      const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>((items + iw - 1) / iw, (long long)c->ncu * 4));
+      const int mk = mark_begin(c, 0);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * iw), blkp_int_lds(ia.nb, ia.D), c->stream, ia);
+      mark_end(c, mk);
+      HIPCHK(c, hipGetLastError());
+    }
+    return QOC_OK;
+  }
   pl.a.unit0 = unit0;
   pl.a.units = units;
   pl.a.UF = UF;
@@ -819,7 +1159,7 @@ int blkp_backward(qoc_ctx* c, double* d_dJdu, const int* stale) {
     c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
   }
   BlkpPlan pl;
-  if ((r = blkp_plan(c, bk, 1, pl))) return r;
+  if ((r = blkp_plan(c, bk, 1, pl, false))) return r;
   TChainArgs gb = tchain_args(c);
   gb.mu_mode = 1;
   if ((r = blkp_launch_chain<false>(c, pl, gb, bk, (const double2*)c->d_blkU, 0, c->B, 0, c->stream, stale))) return r;

@@ -145,3 +145,44 @@ def test_blkp_dead_block_rows_zero(built_lib, monkeypatch):
     for b in range(2):
         J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
         _assert_seed(J[b], g[b], J0, g0, ("dead", b))
+
+
+def test_blkp_interpolated_propagators(built_lib, monkeypatch):
+    """One control (nu = 1): the propagators interpolated in u (k_blkp_int, U(u) = Σ T_i(ξ) M_i over the batch's control
+    range, coefficients from long-double exponentials at Chebyshev points) against the oracle and against the
+    per-slice exponentials (QOC_BLKP_INTERP=0); a later batch outside the range recomputes the coefficients; a range too
+    wide for the series falls back to the exponentials."""
+    from qoc_amd import systems
+    Nt = 40
+    prob = systems.tunable_bus_problem(Nt=Nt, tgate=350.0 * Nt / 2000)
+    u = systems.tunable_bus_controls(3, Nt, seed=86)
+    e = _engine(prob, 3, monkeypatch)
+    J, g = _eval(e, u, True)
+    info = e.info()
+    assert info["interp_degree"] > 0 and info["backward"] == "blocks_prop16", info
+    for b in range(3):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, ("interp", b))
+    # controls beyond the first range (0.3..1.0 -> up to 1.6): new coefficients
+    u2 = u * 1.6
+    J2, g2 = _eval(e, u2, True)
+    assert e.info()["interp_degree"] > 0
+    for b in range(3):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u2[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J2[b], g2[b], J0, g0, ("interp wider", b))
+    # a range the 40-point series cannot resolve: the per-slice exponentials
+    u3 = u.copy()
+    u3[0, 0, 0] = -40.0
+    J3, g3 = _eval(e, u3, True)
+    assert e.info()["interp_degree"] == 0
+    for b in range(3):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u3[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J3[b], g3[b], J0, g0, ("fallback", b))
+    e.close()
+    monkeypatch.setenv("QOC_BLKP_INTERP", "0")
+    ep = _engine(prob, 3, monkeypatch)
+    Jp, gp = _eval(ep, u, True)
+    assert ep.info()["interp_degree"] == 0
+    ep.close()
+    for b in range(3):
+        _assert_seed(J[b], g[b], Jp[b], gp[b], ("interp vs exponentials", b))

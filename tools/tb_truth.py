@@ -21,9 +21,9 @@ from qoc_amd import systems  # noqa: E402
 
 SEEDS = int(os.environ.get("TB_SEEDS", "8"))
 RANKS = range(8)
-VARIANTS = [("blkp", {}), ("rcap0.5", {"QOC_BLKP_RCAP": "0.5"}), ("rcap2", {"QOC_BLKP_RCAP": "2"}),
-            ("fewest_products", {"QOC_BLKP_RCAP": "0"}), ("chebyshev_chain", {"QOC_BLKP": "0"})]
-ENV_KEYS = ("QOC_BLKP", "QOC_BLKP_TAIL", "QOC_BLKP_RCAP")
+VARIANTS = [("blkp", {}), ("taylor", {"QOC_BLKP_INTERP": "0"}),
+            ("cheb6", {"QOC_BLKP_INTERP": "0", "QOC_BLKP_CHEB": "6"}), ("chebyshev_chain", {"QOC_BLKP": "0"})]
+ENV_KEYS = ("QOC_BLKP", "QOC_BLKP_TAIL", "QOC_BLKP_RCAP", "QOC_BLKP_CHEB", "QOC_BLKP_CRMAX", "QOC_BLKP_INTERP")
 
 
 def dump(tag):
