@@ -473,6 +473,9 @@ def main():
     info1 = eng.info()
     large = info1["path"] == "large_n"
     traffic_file = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if args.call_form != "fused":  # the split forms run other kernels (tools/profile.sh <config> <tag> <form>)
+        alt = os.path.join(ROOT, "profiles", f"traffic_{args.config}_{args.call_form}.json")
+        traffic_file = alt if os.path.exists(alt) else traffic_file
     traffic_all, traffic_src = {}, None
     if os.path.exists(traffic_file):
         try:

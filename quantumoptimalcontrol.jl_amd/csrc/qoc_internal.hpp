@@ -304,9 +304,7 @@ hipError_t launch_gen_aux(qoc_ctx* c);
 template <typename T>
 int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int mode = 0);
 // k_grad_rr_c: the order-3 contraction from the chains' captures (mu_mode: L holds μ, λ = coef ⊙ μ)
-// unit_scale: the captures are D1 = Ã_k v, D2 = Ã_k² v (stored-propagator chains, qoc_blkp.hpp), not the step
-// records' scaled products
-int grad_rr_cap(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode, bool unit_scale = false);
+int grad_rr_cap(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode);
 
 // ---- qoc_run_ode.hip ----
 template <typename T>

@@ -497,9 +497,9 @@ bool blk_concurrent_ok(const qoc_ctx* c, int order) {
 }
 
 // ---- stored propagators for blocks of 5..16 rows (qoc_blkp.hpp) ------------------------------------------------------
-// The concurrent eval on the MFMA block waves' systems (the tunable bus): U_k per (seed, slice, live block) on MFMA,
-// then the one-matvec chains with the gradient's captures, then k_grad_rr_c (scale 1, κ = 1).  QOC_BLKP=0 keeps the
-// Chebyshev-action chains (k_blkrot_dual).
+// The tunable bus' parity blocks: U_k per (seed, slice, live block) -- interpolated in u for one control
+// (k_blkp_int), else on MFMA (k_blkp_exp) --, then the one-matvec chains (k_blkp_dual / k_blkp_chain) and the order-3
+// gradient on MFMA (k_blkp_grad).  QOC_BLKP=0 keeps the Chebyshev-action chains (k_blkrot_dual).
 bool blkp_on(const qoc_ctx* c) {
   if (!blk_active(c) || !blk_big(c) || c->nu < 1 || c->nu > 2) return false;
   const char* env = getenv("QOC_BLKP");
@@ -1484,7 +1484,7 @@ static int blku_eval_concurrent(qoc_ctx* c, int order, double* d_dJdu) {
 
 // ---- segmented block eval (qoc_blkseg.hpp) -------------------------------------------------------------------------
 struct BlksegShape {
-  int W, S, L, UPW;
+  int W, S, L, UPW, RB;
   size_t lds;
 };
 // One workgroup per seed with W waves (8 at one seed per CU, fewer when several seeds share a CU: 8 wave slots at the
@@ -1501,7 +1501,10 @@ static BlksegShape blkseg_shape(const qoc_ctx* c) {
   s.L = (c->Nt + S - 1) / S;
   s.S = (c->Nt + s.L - 1) / s.L;
   s.W = (s.S + s.UPW - 1) / s.UPW;
-  s.lds = blkseg_lds(c->N, c->m, c->nu, c->blk_nb, c->nblk, c->Nt, s.S, s.W, blkseg_rb(s.UPW, c->nu));
+  s.RB = blkseg_rb(s.UPW, c->nu);
+  // QOC_BLKSEG_RB: slice-steps per block-sum reduction up to 64 / (UPW nu) (A/B; the LDS must still fit)
+  if (const char* e = getenv("QOC_BLKSEG_RB")) s.RB = std::max(1, std::min(atoi(e), std::max(1, 64 / (s.UPW * std::max(1, c->nu)))));
+  s.lds = blkseg_lds(c->N, c->m, c->nu, c->blk_nb, c->nblk, c->Nt, s.S, s.W, s.RB);
   return s;
 }
 
@@ -1548,7 +1551,7 @@ static int blkseg_params(qoc_ctx* c, const BlksegShape& s, BlksegParams& sp) {
   sp.S = s.S;
   sp.L = s.L;
   sp.UPW = s.UPW;
-  sp.RB = blkseg_rb(s.UPW, c->nu);
+  sp.RB = s.RB;
   sp.terms = c->d_terms;
   // the best (J, seed) for qoc_allgather_best_dev, found by the launch's last workgroup
   if (!c->d_best) {  // no communicator yet: this context alone (the epilogue's own layout)

@@ -72,7 +72,7 @@ int grad_rr_o3(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, int m
 
 // k_grad_rr_c over the units of slices [k0, k0 + nk) (fp64: the captures come from the MFMA chains)
 template <int NT, int KS, int NU>
-int grad_cap_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode, bool unit_scale) {
+int grad_cap_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode) {
   using G = GradRR<double, NT>;
   const int N = c->N, m = c->m, Nt = c->Nt, B = c->B;
   const size_t lds = G::lds_bytes(N, NU);
@@ -106,12 +106,12 @@ int grad_cap_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, 
   a.F2 = (const cx<double>*)c->d_pws + bufN;
   a.G1 = c->d_gws;
   a.G2 = (const cx<double>*)c->d_gws + bufN;
-  a.steps = unit_scale ? nullptr : (const double*)c->d_steps;
+  a.steps = (const double*)c->d_steps;
   for (int j = 0; j < 3; ++j) {
     a.mur[j] = j <= c->nu ? c->tprm.mur[j] : 0.0;
     a.mui[j] = j <= c->nu ? c->tprm.mui[j] : 0.0;
   }
-  a.kappa = !unit_scale && c->cheb_ran ? 2.0 : 1.0;
+  a.kappa = c->cheb_ran ? 2.0 : 1.0;
   a.coef = mu_mode ? c->d_coef : nullptr;
   a.rsec_mask = 0;
   if (c->packed)
@@ -123,25 +123,25 @@ int grad_cap_launch(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, 
 }
 
 template <int NT, int NU>
-int grad_cap_nt(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode, bool us) {
+int grad_cap_nt(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode) {
   const int ks = (c->N + 3) / 4;
-  if (ks == 4 * NT - 3) return grad_cap_launch<NT, 4 * NT - 3, NU>(c, d_dJdu, st, k0, nk, mu_mode, us);
-  if (ks == 4 * NT - 2) return grad_cap_launch<NT, 4 * NT - 2, NU>(c, d_dJdu, st, k0, nk, mu_mode, us);
-  if (ks == 4 * NT - 1) return grad_cap_launch<NT, 4 * NT - 1, NU>(c, d_dJdu, st, k0, nk, mu_mode, us);
-  return grad_cap_launch<NT, 4 * NT, NU>(c, d_dJdu, st, k0, nk, mu_mode, us);
+  if (ks == 4 * NT - 3) return grad_cap_launch<NT, 4 * NT - 3, NU>(c, d_dJdu, st, k0, nk, mu_mode);
+  if (ks == 4 * NT - 2) return grad_cap_launch<NT, 4 * NT - 2, NU>(c, d_dJdu, st, k0, nk, mu_mode);
+  if (ks == 4 * NT - 1) return grad_cap_launch<NT, 4 * NT - 1, NU>(c, d_dJdu, st, k0, nk, mu_mode);
+  return grad_cap_launch<NT, 4 * NT, NU>(c, d_dJdu, st, k0, nk, mu_mode);
 }
 
-int grad_rr_cap(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode, bool us) {
+int grad_rr_cap(qoc_ctx* c, double* d_dJdu, hipStream_t st, int k0, int nk, bool mu_mode) {
   if (c->prec != QOC_FP64 || !c->d_pws || !c->d_gws) return fail(c, QOC_ERR_STATE, "captured gradient: no captures");
   const int NT = (c->N + 15) / 16;
   if (c->nu == 1) {
-    if (NT == 1) return grad_cap_nt<1, 1>(c, d_dJdu, st, k0, nk, mu_mode, us);
-    if (NT == 2) return grad_cap_nt<2, 1>(c, d_dJdu, st, k0, nk, mu_mode, us);
-    return grad_cap_nt<3, 1>(c, d_dJdu, st, k0, nk, mu_mode, us);
+    if (NT == 1) return grad_cap_nt<1, 1>(c, d_dJdu, st, k0, nk, mu_mode);
+    if (NT == 2) return grad_cap_nt<2, 1>(c, d_dJdu, st, k0, nk, mu_mode);
+    return grad_cap_nt<3, 1>(c, d_dJdu, st, k0, nk, mu_mode);
   }
-  if (NT == 1) return grad_cap_nt<1, 2>(c, d_dJdu, st, k0, nk, mu_mode, us);
-  if (NT == 2) return grad_cap_nt<2, 2>(c, d_dJdu, st, k0, nk, mu_mode, us);
-  return grad_cap_nt<3, 2>(c, d_dJdu, st, k0, nk, mu_mode, us);
+  if (NT == 1) return grad_cap_nt<1, 2>(c, d_dJdu, st, k0, nk, mu_mode);
+  if (NT == 2) return grad_cap_nt<2, 2>(c, d_dJdu, st, k0, nk, mu_mode);
+  return grad_cap_nt<3, 2>(c, d_dJdu, st, k0, nk, mu_mode);
 }
 
 template int grad_rr_o3<double>(qoc_ctx*, double*, hipStream_t, int, int, int);

@@ -3,7 +3,7 @@
 # Usage: tools/profile_large.sh <tag>
 set -eo pipefail
 TAG=${1:-r01}
-OUT=gpurun_out/prof_${TAG}_synthetic
+OUT=gpurun_out/prof_${TAG}_synthetic_fused
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 B="python3 bench.py --config synthetic --steps 1 --warmup 1 --no-cpu"
