@@ -270,6 +270,72 @@ def cpu_baseline(prob, u_all, order, nthreads, target_s=12.0):
     }, (J, g, S2)
 
 
+SIDE_LEGS = "zz_batch:fused,tunable_bus:fused,cavity_dense:fused,cavity:split,zz_batch:split,tunable_bus:split"
+
+
+def side_legs(spec, local_rank, order, steps, warmup, parity_seeds=4):
+    """The other configs' rates in the same process (rank 0 at N = 1, after the contract line's timed region): per
+    leg "config:form" a fresh engine on that config's rank-0 seeds, `warmup` untimed evals, `steps` timed ones
+    (device sync on both sides), and parity of the first `parity_seeds` seeds against the C port (oracle/cpu_ref.c,
+    checker only).  Not the metric: the contract's value is the main line's config."""
+    import numpy as np
+    import torch
+    from qoc_amd import GrapeEngine, systems
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpuref  # checker only (oracle/)
+    out = {}
+    for leg in [s for s in spec.split(",") if s]:
+        name, form = (leg.split(":") + ["fused"])[:2]
+        t_leg = time.perf_counter()
+        try:
+            mk_prob, mk_u, B = systems.CONFIGS[name]
+            prob = mk_prob()
+            u_all = mk_u(B, 0)
+            eng = GrapeEngine(prob.A0, prob.A, prob.x0, prob.Nt, B=B, precision=prob.precision, device=local_rank)
+            eng.set_cost_trace(prob.x_target, prob.n)
+            dev = torch.device("cuda", local_rank)
+            u_d = torch.from_numpy(np.ascontiguousarray(np.transpose(u_all, (0, 2, 1)))).to(dev)
+            J_d = torch.empty(B, dtype=torch.float64, device=dev)
+            g_d = torch.empty(B, prob.Nt, prob.nu, dtype=torch.float64, device=dev)
+
+            def step():
+                if form == "split":
+                    eng.propagate_device(u_d.data_ptr(), J_d.data_ptr())
+                    eng.grape_sensitivity_device(u_d.data_ptr(), order, g_d.data_ptr())
+                else:
+                    eng.eval_device(u_d.data_ptr(), order, J_d.data_ptr(), g_d.data_ptr())
+
+            for _ in range(warmup):
+                step()
+            eng.synchronize()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            eng.synchronize()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            info = eng.info()
+            S = min(parity_seeds, B)
+            cpuref.use_blas(False)
+            Jc, gc = cpuref.grape_eval_batch(prob, u_all[:S], order=order, mode=0, nthreads=cpu_threads())
+            Jg = J_d[:S].cpu().numpy()
+            gg = np.transpose(g_d[:S].cpu().numpy(), (0, 2, 1))
+            eng.close()
+            out[f"{name}:{form}"] = {
+                "value": B * steps / el, "unit": "evals/s", "ms_per_step": el / steps * 1e3, "steps": steps,
+                "warmup": warmup, "seeds": B, "workload": WORKLOADS[name],
+                "path": {k: info.get(k) for k in ("path", "chain", "chain_kernel", "backward", "split_forward",
+                                                  "interp_degree")},
+                "parity_vs_cpu_port": {"seeds_checked": S, "max_abs_dJ": float(np.abs(Jg - Jc).max()),
+                                       "max_rel_dJdu": float(max(np.linalg.norm(gg[b] - gc[b]) / np.linalg.norm(gc[b])
+                                                                 for b in range(S)))},
+                "leg_wall_s": time.perf_counter() - t_leg}
+        except Exception as ex:  # a report beside the metric, never the metric
+            out[f"{name}:{form}"] = {"value": None, "error": str(ex)}
+    return out
+
+
 def launch_ranks(n: int) -> int:
     """Start n ranks of this script (torch.distributed.run, rendezvous on 127.0.0.1) and return their exit
     code.  Called before anything touches the GPU: the ranks are child processes, this one only waits."""
@@ -334,6 +400,9 @@ def main():
     ap.add_argument("--call-form", default="fused", choices=["fused", "split", "ipopt"],
                     help="fused: qoc_eval_dev; split: qoc_propagate_dev + qoc_grape_sensitivity_dev; ipopt: the spline "
                          "callbacks qoc_propagate_spline + qoc_sensitivity_spline on host coefficients")
+    ap.add_argument("--side", default=None,
+                    help="comma list of config:form legs timed after the main line (rank 0, N = 1; default: the "
+                         "other BASELINE configs when the main config is the default one, none otherwise; '' for none)")
     ap.add_argument("--cpu-plumbing", action="store_true",
                     help="no GPU: check the launcher and the best-(J, seed) exchange over gloo (CPU tests)")
     args = ap.parse_args()
@@ -835,6 +904,15 @@ def main():
         except Exception as ex:  # the baseline is a report, not the product
             cpu = {"value": None, "unit": "evals/s", "cores": nthreads, "kind": "port", "sample": f"failed: {ex}"}
 
+    side = None
+    comm_ranks = eng.comm_ranks()
+    spec = args.side if args.side is not None else (SIDE_LEGS if args.config == "cavity" and args.call_form == "fused"
+                                                    and not args.seeds else "")
+    if rank == 0 and world == 1 and spec:
+        eng.close()
+        eng = None
+        side = side_legs(spec, local_rank, args.order, max(args.steps, 5), max(args.warmup, 2))
+
     if rank == 0:
         out = {
             "metric": "GRAPE gradient evals/sec (dim N, T slices, B seeds) @ 1/2/4/8 GPU",
@@ -866,12 +944,15 @@ def main():
             "parity_vs_cpu_port": parity,
             "engine": info1,
             "best_over_ranks": {"J": best[0], "seed": int(best[1]), "transport": transport,
-                                "communicator_ranks": eng.comm_ranks()},
+                                "communicator_ranks": comm_ranks},
         }
         if cpu and cpu.get("value"):
             out["speedup_vs_cpu"] = value / cpu["value"]
+        if side is not None:
+            out["side_legs"] = side
         print(json.dumps(out), flush=True)
-    eng.close()
+    if eng is not None:
+        eng.close()
     if world > 1:
         dist.destroy_process_group()
 
