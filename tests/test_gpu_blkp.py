@@ -186,3 +186,28 @@ def test_blkp_interpolated_propagators(built_lib, monkeypatch):
     ep.close()
     for b in range(3):
         _assert_seed(J[b], g[b], Jp[b], gp[b], ("interp vs exponentials", b))
+
+
+@pytest.mark.parametrize("ch", ["2", "4", "8"])
+def test_blkp_tail_chunk(built_lib, monkeypatch, ch):
+    """Nt = 37, not a multiple of any chain chunk: the chains' last chunk is partial (the j0 + jj >= Nt exit, the state
+    sinks flushed at the end, the clamped DMA slices), for every chunk size the chain kernels instantiate
+    (QOC_BLKP_CH), in the device eval (k_blkp_dual) and in the split call form (k_blkp_chain in propagate and in
+    grape_sensitivity): the oracle's J, dJ/du and states."""
+    from qoc_amd import systems
+    Nt = 37
+    monkeypatch.setenv("QOC_BLKP_CH", ch)
+    prob = systems.tunable_bus_problem(Nt=Nt, tgate=350.0 * Nt / 2000)
+    u = systems.tunable_bus_controls(3, Nt, seed=91)
+    e = _engine(prob, 3, monkeypatch)
+    J, g = _eval(e, u, True)
+    assert e.info()["backward"] == "blocks_prop16", e.info()
+    Js = e.propagate(u)
+    gs = e.grape_sensitivity(u, 3)
+    assert e.info()["backward"] == "blocks_prop16", e.info()
+    for b in range(3):
+        J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+        _assert_seed(J[b], g[b], J0, g0, ("eval", ch, b))
+        _assert_seed(Js[b], gs[b], J0, g0, ("split", ch, b))
+    _check_states(e, prob, u, 2, (0, 1, 31, 32, 33, 36, Nt))
+    e.close()
