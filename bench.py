@@ -640,12 +640,23 @@ def main():
         # and term, no MFMA); its algorithmic traffic is the 4 KB propagator written per unit
         ideg = info1.get("interp_degree", 0)
         f_int = B * Nt * nlive * 256 * (ideg + 1) * 4.0
+        # the interpolating chains (k_blkp_ichain, info interp_chain 1 / 2): each chain wave forms its slices'
+        # propagators in registers (every entry, or the 128 packed upper-triangle slots of symmetric propagators), once
+        # per direction, then the one-matvec step; HBM: u and the slices' phases read, the live rows' states written
+        ichain = int(info1.get("interp_chain", 0))
+        ient = 256 if ichain == 1 else 128
+        dirs_i = 1 if split16 else 2
+        f_ichain = dirs_i * B * Nt * nlive * (ient * (ideg + 1) * 4.0 + 8.0 * 256 * m)
+        b_ichain = dirs_i * (B * Nt * (8 + 16) + B * Nt * float(np.sum(lsz)) * m * 16)
         models = {
             "k_expm": ("hbm", u_bytes / 1e9, "GB/s", PEAK_HBM_GBS) if ideg else ("mfma", f_exp / 1e12, "TFLOP/s", peak),
             "k_chain_fwd": ("hbm", (1 if split16 else 2) * one_chain / 1e9, "GB/s", PEAK_HBM_GBS),
             "k_chain_bwd": ("hbm", one_chain / 1e9 if split16 else 0.0, "GB/s", PEAK_HBM_GBS),
             "k_grad": ("mfma", f_grad / 1e12, "TFLOP/s", peak),
         }
+        if ichain:
+            models["k_chain_fwd"] = ("valu", f_ichain / 1e12, "TFLOP/s", peak)
+            models["k_chain_bwd"] = ("valu", f_ichain / 1e12 if split16 else 0.0, "TFLOP/s", peak)
     elif blocks:
         # block chains (csrc/qoc_blk.hpp, qoc_blku.hpp); the launch's algorithmic bytes are the states it writes (x_k,
         # and μ_k in the dual launch) plus what it reads per slice: the step records of k_tchain_prep (32 B record +
@@ -756,21 +767,36 @@ def main():
         names = {"k_expm": "k_blkp_int" if ideg else "k_blkp_exp",
                  "k_chain_fwd": "k_blkp_chain" if split16 else "k_blkp_dual",
                  "k_chain_bwd": "k_blkp_chain" if split16 else "k_blkp_dual", "k_grad": "k_blkp_grad"}
+        if ichain:
+            names.update({"k_chain_fwd": "k_blkp_ichain", "k_chain_bwd": "k_blkp_ichain"})
         live_k = ("k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad") if split16 else ("k_expm", "k_chain_fwd", "k_grad")
+        if ichain:
+            live_k = tuple(k for k in live_k if k != "k_expm")
         for k in live_k:
             kern[k]["kernel"] = names[k]
         # per-launch figures: the step's work over its launches (the formation runs once per seed group)
-        kern["k_expm"]["products_per_unit"] = prods / max(B * Nt * nlive, 1)
-        kern["k_expm"]["executed_gflop_per_launch"] = (f_int if ideg else f_exp) / 1e9 / max(lps["k_expm"], 1.0)
-        if ideg:
-            kern["k_expm"]["interp_degree"] = ideg
-            t = per_step["k_expm"] / 1e3
-            kern["k_expm"]["executed_tflops"] = f_int / 1e12 / t if t > 0 else 0.0
-        kern["k_expm"]["hbm_bytes_per_launch"] = u_bytes / max(lps["k_expm"], 1.0)
+        if ichain:
+            kern["k_expm"] = {"ms_per_launch": 0.0, "launches_per_step": 0.0, "interp_degree": ideg,
+                              "note": "no formation launch: the chains interpolate their propagators (k_blkp_ichain)"}
+        else:
+            kern["k_expm"]["products_per_unit"] = prods / max(B * Nt * nlive, 1)
+            kern["k_expm"]["executed_gflop_per_launch"] = (f_int if ideg else f_exp) / 1e9 / max(lps["k_expm"], 1.0)
+            if ideg:
+                kern["k_expm"]["interp_degree"] = ideg
+                t = per_step["k_expm"] / 1e3
+                kern["k_expm"]["executed_tflops"] = f_int / 1e12 / t if t > 0 else 0.0
+            kern["k_expm"]["hbm_bytes_per_launch"] = u_bytes / max(lps["k_expm"], 1.0)
         for k in ("k_chain_fwd", "k_chain_bwd") if split16 else ("k_chain_fwd",):
-            kern[k]["hbm_bytes_per_launch"] = models[k][1] * 1e9 / max(lps[k], 1.0)
+            kern[k]["hbm_bytes_per_launch"] = (b_ichain if ichain else models[k][1] * 1e9) / max(lps[k], 1.0)
             kern[k]["ns_per_serial_step"] = per_launch[k] * 1e6 / Nt
-        kern["k_chain_fwd"]["note"] = (("forward chain alone (propagate), one matvec per slice from the stored "
+            if ichain:
+                kern[k]["executed_gflop_per_launch"] = f_ichain / 1e9 / max(lps[k], 1.0)
+        kern["k_chain_fwd"]["note"] = (("interpolating chains (k_blkp_ichain): each (seed, direction) wave forms its "
+                                        "slices' propagators from the interpolation coefficients in LDS ("
+                                        + ("the symmetric propagators' upper triangle" if ichain == 2 else "every entry")
+                                        + "), then one matvec per slice; achieved = executed fp64 flops of both / time "
+                                        "(the step is latency- and issue-bound at one wave per SIMD)") if ichain else
+                                       ("forward chain alone (propagate), one matvec per slice from the stored "
                                         "propagators (LDS-DMA staged); k_chain_bwd: the mu recurrence alone "
                                         "(grape_sensitivity)") if split16 else
                                        ("forward chain and mu recurrence of every seed in one launch, one matvec per "
@@ -782,7 +808,9 @@ def main():
                 "traffic": traffic_all.get(names[dom]), "traffic_source": traffic_src,
                 "ms_per_launch": kern[dom]["ms_per_launch"], "launches_per_step": lps[dom],
                 "blocks": [int(x) for x in block_sizes(prob)], "live_blocks": [int(x) for x in lsz],
-                "note": ("stored block propagators (csrc/qoc_blkp.hpp): the dominant kernel forms every slice's "
+                "interp_chain": ichain,
+                "note": kern["k_chain_fwd"]["note"] if ichain else
+                        ("stored block propagators (csrc/qoc_blkp.hpp): the dominant kernel forms every slice's "
                          "16 x 16 block exponential on MFMA (Taylor / Paterson-Stockmeyer + squarings, degree and "
                          "squarings per slice); achieved = executed MFMA flops (12 v_mfma_f64_16x16x4 of 2048 "
                          "flops per complex product, products counted by the kernel) / launch time, against the "

@@ -201,8 +201,10 @@ int qoc_propagate_envelope(qoc_ctx* ctx, int kind, const double* params, int np,
  * grape_sensitivity then runs the segmented backward alone), 2 the stored propagators of blocks of 5..16 rows
  * (grape_sensitivity: the co-state chain and the gradient on them).  info[12] = the degree of the last stored-propagator
  * formation's interpolation in u (one control: U(u) = Σ_i T_i(ξ) M_i over the batch's control range), 0 when the
- * exponentials were formed per slice. */
-#define QOC_INFO_ENTRIES 13
+ * exponentials were formed per slice.  info[13] = 1 when the last eval / propagate on blocks of 5..16 rows ran the
+ * interpolating chains (each chain forms its slice propagators from those coefficients in registers: none stored),
+ * 2 when they formed the upper triangle alone (complex-symmetric generators), 0 otherwise. */
+#define QOC_INFO_ENTRIES 14
 int qoc_get_info(qoc_ctx* ctx, long long* info /*[QOC_INFO_ENTRIES]*/);
 int qoc_get_info_n(qoc_ctx* ctx, long long* info, int n);
 

@@ -605,6 +605,9 @@ struct BlkpIntArgs {
   int skew;                    // imaginary shifts: e^{μ} = e^{i Im μ}
   const double2* M;            // [β][i][p]: M_i of block β at the propagator store positions p = blkp_upos(r, c)
                                // (lane l, register e: p = 64 e + l), so that loads and stores are contiguous
+  const double2* Msym;         // complex-symmetric generators: [i][slot] the packed upper triangle of block 0's nl
+  int nl;                      // live rows (k_blkp_ichain<., true>, blkp_sym_slot), else nullptr / 0
+  double2* ph;                 // B x Nt: e^{μ(u_k)} of every (seed, slice) (k_blkp_phase, read by k_blkp_ichain)
   double2* UF;
   unsigned long long* prods;   // counted as 0 products (none run)
 };
@@ -910,6 +913,224 @@ __global__ __launch_bounds__(512) void k_blkp_chain(const TChainArgs g, const Bl
                                                     int seed0, int useed0, const int* stale) {
   if (stale && *stale != 0) return;
   blkp_chain_body<FWD, CH>(g, bk, U, seed0 + (int)blockIdx.x, useed0);
+}
+
+// ---- one control, fused: the chains interpolate their own propagators (k_blkp_ichain) ----
+// With the interpolation a propagator is D + 1 scaled sums of LDS-resident 16 x 16 matrices, which costs a chain wave
+// less than storing it (4 KB) and reading it back (twice: forward and μ recurrence), and the four seed groups of the
+// stored form left one chain wave per CU beside the formation.  Here one wave per (seed, direction) for one live wave
+// block and one state column (the tunable bus): per chunk of SL slices the wave forms the SL propagators' entries in
+// registers (each coefficient entry read once from LDS for the SL slices; k_blkp_int's arithmetic term by term), then
+// runs the SL chain steps on them (blkp_chain_body's arithmetic), then stores the SL new states.  No propagator reaches
+// HBM; all B seeds and both directions run at once (4 waves per workgroup, the coefficients in its LDS).  The
+// forward's terminal cost is k_terminal_cost's (one 64-thread workgroup per seed: chain_costs as the chains' one-wave
+// workgroups run it).
+//   SYM: complex-symmetric generators (A_j^T = A_j: -i H Δt with H real symmetric, the tunable bus) give symmetric
+// propagators, so only the nl (nl + 1) / 2 <= 128 entries of the upper triangle of the nl live rows are formed, two
+// per lane (half the interpolation's FMAs), from packed coefficients [D + 1][128] (slot k of entry (a, b), a <= b:
+// blkp_sym_slot); each slice's 128 entries go through a wave-private LDS slab to the lanes that apply them (lane (i, q)
+// the entries (i, 4q + t) forward, their conjugates backward: U^H = conj(U)).  The host symmetrises the coefficients
+// of such generators for every form (the stored one too), so both give the same bits.
+// LDS: the coefficients [D + 1][256] (at blkp_upos positions) or [D + 1][128] (SYM) double2 | per wave: exchange row
+// 32 | new states SL x 16 | SYM: the entry slab SL x 128 (double2)
+__host__ __device__ constexpr int blkp_ichain_wave_lds(int SL, bool sym) { return 32 + SL * 16 + (sym ? SL * 128 : 0); }
+__host__ __device__ inline size_t blkp_ichain_lds(int D, int SL, int waves, bool sym) {
+  return ((size_t)(D + 1) * (sym ? 128 : 256) + (size_t)waves * blkp_ichain_wave_lds(SL, sym)) * sizeof(double2);
+}
+// slot of the upper-triangle entry (a, b), a <= b < nl, in the packed layout (row-major triangle)
+__host__ __device__ constexpr int blkp_sym_slot(int a, int b, int nl) { return a * nl - a * (a - 1) / 2 + (b - a); }
+
+// the interpolation of SL slices' propagator entries, NE per lane (k_blkp_int's arithmetic, term by term)
+template <bool FWD, int SL, int NE>
+struct BlkpIAcc {
+  double ur[SL][NE], ui[SL][NE], uu[SL], xv[SL], tm[SL], tc[SL];
+  // the slices j0 .. j0 + SL - 1 of this direction (clamped at the ends)
+  __device__ __forceinline__ void start(const BlkpIntArgs& ia, const double* ub, int Nt, int j0) {
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {
+      const int j = j0 + s;
+      uu[s] = ub[FWD ? min(j, Nt - 1) : max(Nt - 1 - j, 0)];
+      xv[s] = fma(ia.xa, uu[s], ia.xb);
+      tm[s] = 1.0;
+      tc[s] = 1.0;
+#pragma unroll
+      for (int t = 0; t < NE; ++t) ur[s][t] = ui[s][t] = 0.0;
+    }
+  }
+  // terms [t0, t1) of Σ T_i(ξ) M_i: this lane's entries at off[] in each coefficient matrix of `stride` entries
+  __device__ __forceinline__ void terms(const double2* Ms, const int (&off)[NE], int stride, int t0, int t1) {
+#pragma unroll 2
+    for (int ti = t0; ti < t1; ++ti) {
+      double2 mv[NE];
+#pragma unroll
+      for (int t = 0; t < NE; ++t) mv[t] = Ms[ti * stride + off[t]];
+#pragma unroll
+      for (int s = 0; s < SL; ++s) {
+#pragma unroll
+        for (int t = 0; t < NE; ++t) {
+          ur[s][t] = fma(tc[s], mv[t].x, ur[s][t]);
+          ui[s][t] = fma(tc[s], mv[t].y, ui[s][t]);
+        }
+        const double tn = ti == 0 ? xv[s] : fma(2.0 * xv[s], tc[s], -tm[s]);
+        tm[s] = tc[s];
+        tc[s] = tn;
+      }
+    }
+  }
+  // times e^{μ(u)} (phs[s]: k_blkp_phase's); conj: the conjugates (the μ recurrence's U^H entries)
+  __device__ __forceinline__ void finish(const double2 (&phs)[SL], bool conj) {
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {
+      const double pr = phs[s].x, pi = phs[s].y;
+#pragma unroll
+      for (int t = 0; t < NE; ++t) {
+        const double vr = fma(pr, ur[s][t], -pi * ui[s][t]), vi = fma(pr, ui[s][t], pi * ur[s][t]);
+        ur[s][t] = vr;
+        ui[s][t] = conj ? -vi : vi;
+      }
+    }
+  }
+};
+
+template <bool FWD, int SL, bool SYM>
+__device__ __forceinline__ void blkp_ichain_body(const TChainArgs& g, const BlkArgs& bk, const BlkpIntArgs& ia,
+                                                 const double2* Ms, double2* xs, const int b) {
+  const int N = g.N, Nt = g.Nt, l = threadIdx.x & 63, i = l & 15, q = l >> 4;
+  const size_t Nm = (size_t)N;  // one state column
+  const int row = bk.wrow[i];   // wave block 0
+  const bool act = row >= 0, own = act && q == 0;
+  double2* const Os = xs + 32;         // [s][i]: x_{k+1} / μ_k of row i
+  double2* const Es = Os + SL * 16;    // SYM: [s][slot] the slices' packed entries
+  double2* const sink2 = reinterpret_cast<double2*>(tchain_sink(g));
+  const size_t oe = (size_t)max(row, 0);
+  double2* const Sb = reinterpret_cast<double2*>((cx<double>*)(FWD ? g.X : g.L) + (size_t)b * (Nt + 1) * Nm);
+  double2 v0 = make_double2(0.0, 0.0);
+  if (act) {
+    cx<double> v;
+    if (FWD) v = ((const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0))[oe];
+    else v = ((const cx<double>*)g.Xt)[oe];
+    v0 = make_double2(v.r, v.i);
+  }
+  xs[i] = v0;
+  blkp_wave_sync();
+  *(own ? Sb + (FWD ? 0 : (size_t)Nt * Nm) + oe : sink2) = v0;
+  double xr[4], xi[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const double2 v = xs[4 * q + t];
+    xr[t] = v.x;
+    xi[t] = v.y;
+  }
+  constexpr int NE = SYM ? 2 : 4;
+  int off[NE];   // this lane's entries in a coefficient matrix
+  int ks[4];     // SYM: the packed slots of this lane's four entries (i, 4q + t), -1: a padding row or column
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int c = 4 * q + t, a = min(i, c), bb = max(i, c);
+    ks[t] = bb < ia.nl ? blkp_sym_slot(a, bb, ia.nl) : -1;
+  }
+#pragma unroll
+  for (int t = 0; t < NE; ++t) off[t] = SYM ? 64 * t + l : FWD ? blkp_upos(i, 4 * q + t) : blkp_upos(4 * q + t, i);
+  const double* const ub = ia.u + (size_t)b * Nt;
+  const int Dq = ia.Db[0];
+  typedef double D2V __attribute__((ext_vector_type(2)));
+  using G2 = __attribute__((address_space(1))) D2V;
+  const double2* const phb = ia.ph + (size_t)b * Nt;
+  for (int j0 = 0; j0 < Nt; j0 += SL) {
+    BlkpIAcc<FWD, SL, NE> a;
+    double2 phs[SL];  // the slices' e^{μ(u)}, loaded with the controls, used after the terms
+#pragma unroll
+    for (int s = 0; s < SL; ++s) phs[s] = phb[FWD ? min(j0 + s, Nt - 1) : max(Nt - 1 - j0 - s, 0)];
+    a.start(ia, ub, Nt, j0);
+    a.terms(Ms, off, SYM ? 128 : 256, 0, Dq + 1);
+    a.finish(phs, !SYM && !FWD);
+    double ur[SL][4], ui[SL][4];
+    if constexpr (SYM) {  // the packed entries through the slab to the lanes that apply them
+#pragma unroll
+      for (int s = 0; s < SL; ++s)
+#pragma unroll
+        for (int t = 0; t < NE; ++t) Es[s * 128 + 64 * t + l] = make_double2(a.ur[s][t], a.ui[s][t]);
+      blkp_wave_sync();
+#pragma unroll
+      for (int s = 0; s < SL; ++s)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const double2 v = ks[t] >= 0 ? Es[s * 128 + ks[t]] : make_double2(0.0, 0.0);
+          ur[s][t] = v.x;
+          ui[s][t] = FWD ? v.y : -v.y;
+        }
+    } else {
+#pragma unroll
+      for (int s = 0; s < SL; ++s)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          ur[s][t] = a.ur[s][t];
+          ui[s][t] = a.ui[s][t];
+        }
+    }
+    // the SL chain steps (blkp_chain_body's arithmetic)
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {
+      if (j0 + s >= Nt) break;  // uniform
+      double2 y = blkp_dot4(ur[s], ui[s], xr, xi);
+      y = xsum_rows2(y);
+      xs[i] = y;
+      blkp_wave_sync();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const double2 v = xs[4 * q + t];
+        xr[t] = v.x;
+        xi[t] = v.y;
+      }
+      blkp_wave_sync();
+      if (q == 0) Os[s * 16 + i] = y;
+    }
+    blkp_wave_sync();
+    // the chunk's new states to HBM, branch-free (lanes without an element write the sink)
+#pragma unroll
+    for (int s = 0; s < SL; ++s) {
+      const int j = j0 + s;
+      const int k = FWD ? j : Nt - 1 - j;
+      G2* p = (G2*)(own && j < Nt ? Sb + (size_t)(FWD ? k + 1 : k) * Nm + oe : sink2);
+      asm volatile("" : "+v"(p));
+      const double2 v = Os[s * 16 + i];
+      *p = D2V{v.x, v.y};
+    }
+    blkp_wave_sync();  // Os and Es are rewritten by the next chunk
+  }
+}
+
+// e^{μ(u_k)} of every (seed, slice), as k_blkp_int forms it (the two chain directions of a seed share them)
+static __global__ void k_blkp_phase(const BlkpIntArgs ia, long long n) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const double uu = ia.u[e];
+    const double mr = fma(uu, ia.mur[1], ia.mur[0]), mi = fma(uu, ia.mui[1], ia.mui[0]);
+    const double em = ia.skew ? 1.0 : exp(mr);
+    double sn, cn;
+    sincos(mi, &sn, &cn);
+    ia.ph[e] = make_double2(em * cn, em * sn);
+  }
+}
+
+// nseeds seeds from seed0 on; dual: both directions (wave pair 2 s + d: seed seed0 + s, d = 0 forward, 1 μ), else
+// the direction dir alone; every wave passes the coefficients' barrier before it may leave
+template <int SL, bool SYM>
+__global__ __launch_bounds__(256) void k_blkp_ichain(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk,
+                                                     const BlkpIntArgs ia, int seed0, int nseeds, int dual, int dir,
+                                                     const int* stale) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (stale && *stale != 0) return;  // uniform over the grid
+  double2* const Ms = reinterpret_cast<double2*>(smem);
+  const int D = ia.D, tid = threadIdx.x, w = tid >> 6, msz = (D + 1) * (SYM ? 128 : 256);
+  const double2* const src = SYM ? ia.Msym : ia.M;
+  for (int e = tid; e < msz; e += blockDim.x) Ms[e] = src[e];
+  __syncthreads();
+  double2* const xs = Ms + msz + (size_t)w * blkp_ichain_wave_lds(SL, SYM);
+  const int p = (int)blockIdx.x * (int)(blockDim.x >> 6) + w;
+  if (p >= (dual ? 2 : 1) * nseeds) return;
+  const int s = dual ? p >> 1 : p, d = dual ? p & 1 : dir;
+  if (d == 0) blkp_ichain_body<true, SL, SYM>(gf, bk, ia, Ms, xs, seed0 + s);
+  else blkp_ichain_body<false, SL, SYM>(gb, bk, ia, Ms, xs, seed0 + s);
 }
 
 // ---- the order-3 gradient on the stored states (the reference's expm_jacobian! + _compute_u_sensitivity,

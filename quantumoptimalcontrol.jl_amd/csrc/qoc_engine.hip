@@ -558,6 +558,7 @@ void qoc_destroy(qoc_ctx* c) {
   if (c->d_gseg) hipFree(c->d_gseg);
   if (c->d_blkp_ctab) hipFree(c->d_blkp_ctab);
   if (c->d_blkp_M) hipFree(c->d_blkp_M);
+  if (c->d_blkp_ph) hipFree(c->d_blkp_ph);
   if (c->d_minmax) hipFree(c->d_minmax);
   if (c->h_minmax) hipHostFree(c->h_minmax);
   if (c->h_flag) hipHostFree(c->h_flag);
@@ -733,6 +734,8 @@ int qoc_set_generators(qoc_ctx* c, const double* A0, const double* const* Aj) {
   }
   if (c->tchain_ok) {  // invariant blocks of the generators (qoc_blk.hpp)
     c->int_ok = c->int_failed = false;  // the interpolated propagators belong to the old generators
+    c->ichain_fwd = false;
+    c->fwd_kind = 0;  // a split forward's propagators or coefficients belong to the old generators
     r = blk_detect(c);
     if (r) return r;
   } else {
@@ -1373,6 +1376,7 @@ int qoc_get_info(qoc_ctx* c, long long* info) {
   info[9] = c->fwd_captured ? 1 : 0;
   // 6: the last eval ran the stored-propagator chains of blocks of 5..16 rows (propagate / grape_sensitivity: 4)
   info[11] = c->fwd_kind;
+  info[13] = c->ichain_last;  // the last eval / propagate on blocks of 5..16 rows: interpolating chains (2: triangle)
   info[12] = c->last_int_D;  // the stored block propagators' last formation: interpolation degree in u (0: exponentials)
   info[10] = blk_active(c) ? (blku_on(c) ? 5 : blkp_on(c) && c->last_eval_mode == 7 ? 6 : blk_rot(c) ? 4 : 3) : c->big || c->chain_mode != 1 || !tchain_mf(c) ? 0 : tchain_mf_rot(c) ? 2 : 1;
   return QOC_OK;

@@ -164,11 +164,21 @@ struct qoc_ctx {
   std::vector<int> int_Db;           // per live wave block
   double int_lo = 0.0, int_hi = 0.0;
   std::vector<int> int_wrow;
+  bool int_sym = false;              // complex-symmetric generators on one live wave block: d_blkp_M also holds its
+  int int_nl = 0;                    // packed upper triangle of int_nl live rows, from element int_nfull on
+  size_t int_nfull = 0;
   bool int_failed = false;           // [int_fail_lo, int_fail_hi] did not converge (a wider range will not either)
   double int_fail_lo = 0.0, int_fail_hi = 0.0;
   double* d_minmax = nullptr;        // k_minmax partials (256 blocks x 2)
   double* h_minmax = nullptr;        // pinned host copy
   int last_int_D = 0;                // the degree the last formation ran with (0: not interpolated; qoc_get_info)
+  // the last eval / propagate ran the interpolating chains (k_blkp_ichain: no stored propagators); for the split call
+  // form: grape_sensitivity's μ recurrence interpolates from the same coefficients (set by blkp_forward, cleared by
+  // every other forward and by new generators)
+  double2* d_blkp_ph = nullptr;      // B x Nt: e^{μ(u_k)} for the interpolating chains (k_blkp_phase)
+  size_t blkp_ph_n = 0;
+  int ichain_last = 0;               // 0: no, 1: every entry, 2: the symmetric propagators' upper triangle
+  bool ichain_fwd = false;
   double* d_blkp_ctab = nullptr; // the Chebyshev form's coefficient table (qoc_blkp.hpp blkp_cheb), for ctab_cm / ctab_rmax
   int ctab_cm = 0;
   double ctab_rmax = 0.0;
@@ -178,7 +188,8 @@ struct qoc_ctx {
   // what the last propagate left for grape_sensitivity (the reference's split call form,
   // examples/ipopt_callbacks_exp.jl:11-31): 0 states in d_X (every path), 1 the segmented forward's G at every
   // segment end (d_gseg, qoc_blkseg.hpp BLKSEG_FWD), 2 the stored block propagators and states of blocks of 5..16 rows
-  // (d_blkU + d_X, qoc_blkp.hpp).  Reset by every other forward or eval.
+  // (d_blkU + d_X, qoc_blkp.hpp; or the interpolating chains' states alone, ichain_fwd).  Reset by every other
+  // forward or eval.
   int fwd_kind = 0;
   double2* d_gseg = nullptr;         // B x NB^2 x S x nblk complex
   size_t gseg_bytes = 0;

@@ -752,6 +752,38 @@ static int blkp_interp_coeffs(qoc_ctx* c, const std::vector<int>& wrow, double l
         }
       }
     }
+  // complex-symmetric generators on a block's rows (A_j^T = A_j: -i H Δt with H real symmetric) give symmetric
+  // propagators: the coefficients are symmetrised (the long-double transform leaves the two triangles a rounding
+  // apart), so every form gives U[r][c] = U[c][r] bit for bit, and the interpolating chains may form the upper triangle
+  // alone (k_blkp_ichain SYM: block 0, its nl live rows first in the wave block, nl (nl + 1) / 2 <= 128)
+  std::vector<char> bsym(nwb, 1);
+  for (int b = 0; b < nwb; ++b) {
+    for (int r = 0; r < 16 && bsym[b]; ++r)
+      for (int q = r + 1; q < 16 && bsym[b]; ++q) {
+        const int row = wrow[16 * b + r], col = wrow[16 * b + q];
+        if (row < 0 || col < 0) continue;
+        for (int j = 0; j <= 1; ++j) {
+          const double* x = c->h_gen.data() + 2 * (j * NN + row + (size_t)N * col);
+          const double* y = c->h_gen.data() + 2 * (j * NN + col + (size_t)N * row);
+          if (x[0] != y[0] || x[1] != y[1]) bsym[b] = 0;
+        }
+      }
+    if (!bsym[b]) continue;
+    for (int i = 0; i < NI; ++i) {
+      auto& mr = Mr[(size_t)b * NI + i];
+      auto& mi = Mi[(size_t)b * NI + i];
+      for (int r = 0; r < 16; ++r)
+        for (int q = r + 1; q < 16; ++q) {
+          const LD ar = (mr[r * 16 + q] + mr[q * 16 + r]) / 2, ai = (mi[r * 16 + q] + mi[q * 16 + r]) / 2;
+          mr[r * 16 + q] = mr[q * 16 + r] = ar;
+          mi[r * 16 + q] = mi[q * 16 + r] = ai;
+        }
+    }
+  }
+  int nl = 0;
+  while (nl < 16 && wrow[nl] >= 0) ++nl;
+  bool sym = nwb == 1 && bsym[0] && nl * (nl + 1) / 2 <= 128;
+  for (int r = nl; r < 16 && sym; ++r) sym = wrow[r] < 0;
   // per block (its own degree: a block's propagators do not depend on the other blocks of the launch); the long-double
   // transform's own rounding leaves a floor near 1e-18 under the converged coefficients
   const LD tol = std::ldexp(1.0L, -56);
@@ -778,6 +810,15 @@ static int blkp_interp_coeffs(qoc_ctx* c, const std::vector<int>& wrow, double l
         h[((size_t)b * (D + 1) + i) * 256 + p] =
             make_double2((double)Mr[(size_t)b * NI + i][ent], (double)Mi[(size_t)b * NI + i][ent]);
       }
+  const size_t nfull = h.size();
+  if (sym) {  // block 0's packed upper triangle after the full layout: [i][slot], slots past nl (nl + 1) / 2 zero
+    h.resize(nfull + (size_t)(D + 1) * 128, make_double2(0.0, 0.0));
+    for (int i = 0; i <= D; ++i)
+      for (int a = 0; a < nl; ++a)
+        for (int b2 = a; b2 < nl; ++b2)
+          h[nfull + (size_t)i * 128 + blkp_sym_slot(a, b2, nl)] =
+              make_double2((double)Mr[i][a * 16 + b2], (double)Mi[i][a * 16 + b2]);
+  }
   const size_t bytes = h.size() * sizeof(double2);
   if (c->blkp_M_bytes < bytes) {
     if (c->d_blkp_M) {
@@ -792,11 +833,33 @@ static int blkp_interp_coeffs(qoc_ctx* c, const std::vector<int>& wrow, double l
   HIPCHK(c, hipMemcpy(c->d_blkp_M, h.data(), bytes, hipMemcpyHostToDevice));
   c->int_D = D;
   c->int_Db = Db;
+  c->int_sym = sym;
+  c->int_nl = nl;
+  c->int_nfull = nfull;
   c->int_lo = lo;
   c->int_hi = hi;
   c->int_wrow = wrow;
   c->int_ok = true;
   return QOC_OK;
+}
+
+// the interpolation's launch arguments from the cached coefficients (c->int_*: valid for bk's layout)
+static void blkp_interp_args(const qoc_ctx* c, const BlkArgs& bk, BlkpIntArgs& ia) {
+  ia = BlkpIntArgs{};
+  ia.nwb = bk.nwb;
+  ia.D = c->int_D;
+  for (int b = 0; b < bk.nwb && b < 8; ++b) ia.Db[b] = c->int_Db[b];
+  ia.u = c->d_u;
+  ia.xa = 2.0 / (c->int_hi - c->int_lo);
+  ia.xb = -(c->int_hi + c->int_lo) / (c->int_hi - c->int_lo);
+  for (int j = 0; j < 2; ++j) {
+    ia.mur[j] = c->tprm.mur[j];
+    ia.mui[j] = c->tprm.mui[j];
+  }
+  ia.skew = c->skew_exact && c->tprm.mur[0] == 0.0 && c->tprm.mur[1] == 0.0;
+  ia.M = c->d_blkp_M;
+  ia.Msym = c->int_sym && bk.nwb == 1 ? c->d_blkp_M + c->int_nfull : nullptr;
+  ia.nl = ia.Msym ? c->int_nl : 0;
 }
 
 // 0: the formation interpolates (ia filled), 1: it forms the exponentials.  One control (nu = 1) and
@@ -830,19 +893,7 @@ static int blkp_interp_setup(qoc_ctx* c, const BlkArgs& bk, BlkpIntArgs& ia) {
     }
     c->int_failed = false;
   }
-  ia = BlkpIntArgs{};
-  ia.nwb = bk.nwb;
-  ia.D = c->int_D;
-  for (int b = 0; b < bk.nwb && b < 8; ++b) ia.Db[b] = c->int_Db[b];
-  ia.u = c->d_u;
-  ia.xa = 2.0 / (c->int_hi - c->int_lo);
-  ia.xb = -(c->int_hi + c->int_lo) / (c->int_hi - c->int_lo);
-  for (int j = 0; j < 2; ++j) {
-    ia.mur[j] = c->tprm.mur[j];
-    ia.mui[j] = c->tprm.mui[j];
-  }
-  ia.skew = c->skew_exact && c->tprm.mur[0] == 0.0 && c->tprm.mur[1] == 0.0;
-  ia.M = c->d_blkp_M;
+  blkp_interp_args(c, bk, ia);
   return QOC_OK;
 }
 
@@ -1011,6 +1062,62 @@ static int blkp_launch_grad(qoc_ctx* c, const BlkArgs& bk, double* d_dJdu, const
   HIPCHK(c, hipGetLastError());
   return QOC_OK;
 }
+// the interpolating chains (k_blkp_ichain) apply: the interpolation (one control), one live wave block, one state
+// column, and the block's coefficients in the LDS beside four waves' rows (QOC_BLKP_ICHAIN=0: the stored form)
+constexpr int BLKP_ISL = 8;  // slices per chunk
+static bool blkp_ichain_sym(const BlkpIntArgs& ia) {  // complex-symmetric generators: the upper triangle alone
+  return ia.Msym && !(getenv("QOC_BLKP_ISYM") && atoi(getenv("QOC_BLKP_ISYM")) == 0);
+}
+// 0: the stored form, 1: the interpolating chains (every entry), 2: the same on the upper triangle
+static int blkp_ichain_on(const qoc_ctx* c, const BlkArgs& bk, const BlkpPlan& pl) {
+  const char* env = getenv("QOC_BLKP_ICHAIN");
+  if (env && atoi(env) == 0) return 0;
+  const bool sym = pl.interp && blkp_ichain_sym(pl.ia);
+  if (!(pl.interp && bk.nwb == 1 && c->m == 1 && blkp_ichain_lds(pl.ia.D, BLKP_ISL, 4, sym) <= 160 * 1024)) return 0;
+  return sym ? 2 : 1;
+}
+// dual: the forward chain and the μ recurrence of every seed (one launch), else direction dir alone; the forward's
+// terminal cost and λ_N coefficients by k_terminal_cost (64 threads: chain_costs as the one-wave chain workgroups run
+// it, the same sums); stale: a queued stale-u flag (nonzero: nothing is written)
+static int blkp_launch_ichain(qoc_ctx* c, const TChainArgs& gf, const TChainArgs& gb, const BlkArgs& bk,
+                              const BlkpIntArgs& ia0, bool dual, int dir, const int* stale) {
+  // the slices' e^{μ(u_k)} first (one sincos per (seed, slice) instead of one per chain wave)
+  const size_t nph = (size_t)c->B * c->Nt;
+  if (c->blkp_ph_n < nph) {
+    if (c->d_blkp_ph) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipFree(c->d_blkp_ph));
+      c->d_blkp_ph = nullptr;
+    }
+    HIPCHK(c, hipMalloc((void**)&c->d_blkp_ph, nph * sizeof(double2)));
+    c->blkp_ph_n = nph;
+  }
+  BlkpIntArgs ia = ia0;
+  ia.ph = c->d_blkp_ph;
+  hipLaunchKernelGGL(k_blkp_phase, dim3((unsigned)std::min<size_t>((nph + 255) / 256, 4096)), dim3(256), 0, c->stream, ia,
+                     (long long)nph);
+  HIPCHK(c, hipGetLastError());
+  // (the next chunk's interpolation interleaved with this chunk's steps measured slower: 2.45 ms at SL = 4, 2.68 ms at
+  // SL = 8 with AGPR spills, against 1.95 ms in sequence; profiles/r06v_ichain_ab.txt)
+  // complex-symmetric generators: the upper triangle alone (QOC_BLKP_ISYM=0: every entry)
+  const bool sym = blkp_ichain_sym(ia);
+  auto kern = sym ? k_blkp_ichain<BLKP_ISL, true> : k_blkp_ichain<BLKP_ISL, false>;
+  const size_t lds = blkp_ichain_lds(ia.D, BLKP_ISL, 4, sym);
+  HIPCHK(c, blk_lds_attr(kern, lds));
+  const int pairs = (dual ? 2 : 1) * c->B;
+  const int mk = mark_begin(c, dual || dir == 0 ? 1 : 2);
+  hipLaunchKernelGGL(kern, dim3((pairs + 3) / 4), dim3(256), lds, c->stream, gf, gb, bk, ia, 0, c->B, dual ? 1 : 0, dir,
+                     stale);
+  mark_end(c, mk);
+  HIPCHK(c, hipGetLastError());
+  if (dual || dir == 0) {
+    hipLaunchKernelGGL(k_terminal_cost<double>, dim3(c->B), dim3(64), 0, c->stream, c->N, c->m, c->Nt,
+                       (const cx<double>*)gf.X, (const cx<double>*)gf.Xt, gf.cost_kind, gf.n_norm, 0, gf.J, gf.coef,
+                       gf.sc);
+    HIPCHK(c, hipGetLastError());
+  }
+  return QOC_OK;
+}
 static int blkp_parts(const qoc_ctx* c) {
   int parts = 4;
   if (const char* pe = getenv("QOC_BLKP_PARTS")) parts = atoi(pe);
@@ -1034,12 +1141,26 @@ static int blkp_eval_concurrent(qoc_ctx* c, double* d_dJdu, const BlkArgs& bk) {
   const int gmax = (c->B + parts - 1) / parts;           // seeds of the largest group
   const int nslab = parts > 1 ? 2 : 1;
   const size_t slab = (size_t)gmax * per_seed * 256;      // double2 per slab
+  BlkpPlan pl;
+  if ((r = blkp_plan(c, bk, parts, pl))) return r;
+  c->ichain_last = blkp_ichain_on(c, bk, pl);
+  if (c->ichain_last) {  // both chains interpolate their own propagators: nothing stored
+    if (bk.nwb != c->nwb) {
+      if ((r = blk_zero_dead(c, {c->d_X, c->d_L}))) return r;
+    }
+    if ((r = blkp_launch_ichain(c, gf, gb, bk, pl.ia, true, 0, nullptr))) return r;
+    c->fwd_captured = false;
+    c->props_since_reset++;
+    c->steps_stale = true;
+    if ((r = blkp_launch_grad(c, bk, d_dJdu, nullptr, c->d_coef_mu))) return r;
+    c->L_is_mu = true;
+    c->last_eval_mode = 7;
+    return QOC_OK;
+  }
   if ((r = blkp_ensure_store(c, nslab * slab * sizeof(double2), true))) return r;  // 1: does not fit
   if (bk.nwb != c->nwb) {
     if ((r = blk_zero_dead(c, {c->d_X, c->d_L}))) return r;
   }
-  BlkpPlan pl;
-  if ((r = blkp_plan(c, bk, parts, pl))) return r;
   // events: [p] group p formed, [parts + p] group p's chains done, [2 parts] everything queued before
   if (parts > 1) {
     if ((r = ensure_stream2(c, 2 * parts + 1))) return r;
@@ -1107,14 +1228,27 @@ int blkp_forward(qoc_ctx* c) {
   if (r) return r;
   if (!blkp_fits(c, bk)) return 1;
   const long long per_seed = (long long)c->Nt * bk.nwb;
-  if ((r = blkp_ensure_store(c, (size_t)c->B * per_seed * 256 * sizeof(double2), true))) return r;
-  if (bk.nwb != c->nwb) {
-    if ((r = blk_zero_dead(c, {c->d_X, c->d_L}))) return r;
-  }
   const int parts = blkp_parts(c);
   BlkpPlan pl;
   if ((r = blkp_plan(c, bk, parts, pl))) return r;
   const TChainArgs gf = tchain_args(c);
+  c->ichain_last = blkp_ichain_on(c, bk, pl);
+  c->ichain_fwd = c->ichain_last != 0;
+  if (c->ichain_fwd) {  // the forward chain interpolates its propagators; grape_sensitivity's μ recurrence will too
+    if (bk.nwb != c->nwb) {
+      if ((r = blk_zero_dead(c, {c->d_X, c->d_L}))) return r;
+    }
+    if ((r = blkp_launch_ichain(c, gf, gf, bk, pl.ia, false, 0, nullptr))) return r;
+    c->fwd_captured = false;
+    c->props_since_reset++;
+    c->steps_stale = true;
+    c->fwd_kind = 2;
+    return QOC_OK;
+  }
+  if ((r = blkp_ensure_store(c, (size_t)c->B * per_seed * 256 * sizeof(double2), true))) return r;
+  if (bk.nwb != c->nwb) {
+    if ((r = blk_zero_dead(c, {c->d_X, c->d_L}))) return r;
+  }
   if (parts > 1) {
     if ((r = ensure_stream2(c, parts + 1))) return r;
     HIPCHK(c, hipEventRecord(c->sync_ev[parts], c->stream));
@@ -1145,7 +1279,7 @@ int blkp_forward(qoc_ctx* c) {
 
 bool blkp_backward_ok(const qoc_ctx* c, int order) {
   return c->fwd_kind == 2 && order == 3 && c->mu == 0.0 && !c->src_on &&
-         (c->cost_kind == QOC_COST_TRACE || c->cost_kind == QOC_COST_ZCAL) && c->d_blkU;
+         (c->cost_kind == QOC_COST_TRACE || c->cost_kind == QOC_COST_ZCAL) && (c->ichain_fwd || c->d_blkU);
 }
 
 // grape_sensitivity after blkp_forward: the μ recurrence from the stored propagators (μ_N = X_target, λ_k = coef ⊙ μ_k,
@@ -1158,11 +1292,18 @@ int blkp_backward(qoc_ctx* c, double* d_dJdu, const int* stale) {
     HIPCHK(c, hipMalloc((void**)&c->d_coef_mu, (size_t)c->B * 2 * c->m_user * sizeof(cx<double>)));
     c->dev_bytes += (size_t)c->B * 2 * c->m_user * sizeof(cx<double>);
   }
-  BlkpPlan pl;
-  if ((r = blkp_plan(c, bk, 1, pl, false))) return r;
   TChainArgs gb = tchain_args(c);
   gb.mu_mode = 1;
-  if ((r = blkp_launch_chain<false>(c, pl, gb, bk, (const double2*)c->d_blkU, 0, c->B, 0, c->stream, stale))) return r;
+  if (c->ichain_fwd) {  // the propagate interpolated: the μ recurrence from the same coefficients (the same u)
+    BlkpIntArgs ia;
+    blkp_interp_args(c, bk, ia);
+    if ((r = blkp_launch_ichain(c, gb, gb, bk, ia, false, 1, stale))) return r;
+  } else {
+    BlkpPlan pl;
+    if ((r = blkp_plan(c, bk, 1, pl, false))) return r;
+    if ((r = blkp_launch_chain<false>(c, pl, gb, bk, (const double2*)c->d_blkU, 0, c->B, 0, c->stream, stale)))
+      return r;
+  }
   if ((r = blkp_launch_grad(c, bk, d_dJdu, stale, c->d_coef_mu))) return r;
   c->L_is_mu = true;
   c->last_eval_mode = 7;

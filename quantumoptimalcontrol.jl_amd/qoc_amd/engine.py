@@ -310,7 +310,7 @@ class GrapeEngine:
 
     def info(self) -> dict:
         """Which pipeline the context runs (qoc_get_info): 'lds' kernels or the 'large_n' GEMM path."""
-        v = np.zeros(13, dtype=np.int64)
+        v = np.zeros(14, dtype=np.int64)
         self._chk(self._lib.qoc_get_info_n(self._h, v.ctypes.data_as(C.POINTER(C.c_longlong)), v.size))
         return {"path": "large_n" if v[0] else "lds", "chunk": int(v[1]), "ns_iters": int(v[2]),
                 "device_bytes": int(v[3]), "chain": "taylor" if v[4] == 1 else "propagators",
@@ -324,7 +324,7 @@ class GrapeEngine:
                 "chain_kernel": {0: None, 1: "mfma_lds", 2: "mfma_regs", 3: "blocks", 4: "blocks_mfma", 5: "blocks_prop",
                                  6: "blocks_prop16"}.get(int(v[10])),
                 "split_forward": {0: "states", 1: "segmented", 2: "blocks_prop16"}.get(int(v[11])),
-                "interp_degree": int(v[12])}
+                "interp_degree": int(v[12]), "interp_chain": int(v[13])}
 
     def set_chain(self, mode: str = "auto"):
         """How the chains apply exp(A_k) (include/qoc.h qoc_set_chain): 'propagators' forms every U_k (the

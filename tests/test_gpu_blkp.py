@@ -197,11 +197,12 @@ def test_blkp_tail_chunk(built_lib, monkeypatch, ch):
     from qoc_amd import systems
     Nt = 37
     monkeypatch.setenv("QOC_BLKP_CH", ch)
+    monkeypatch.setenv("QOC_BLKP_ICHAIN", "0")  # the stored form (test_blkp_interpolating_chains: the fused one)
     prob = systems.tunable_bus_problem(Nt=Nt, tgate=350.0 * Nt / 2000)
     u = systems.tunable_bus_controls(3, Nt, seed=91)
     e = _engine(prob, 3, monkeypatch)
     J, g = _eval(e, u, True)
-    assert e.info()["backward"] == "blocks_prop16", e.info()
+    assert e.info()["backward"] == "blocks_prop16" and e.info()["interp_chain"] == 0, e.info()
     Js = e.propagate(u)
     gs = e.grape_sensitivity(u, 3)
     assert e.info()["backward"] == "blocks_prop16", e.info()
@@ -211,3 +212,58 @@ def test_blkp_tail_chunk(built_lib, monkeypatch, ch):
         _assert_seed(Js[b], gs[b], J0, g0, ("split", ch, b))
     _check_states(e, prob, u, 2, (0, 1, 31, 32, 33, 36, Nt))
     e.close()
+
+
+def test_blkp_interpolating_chains(built_lib, monkeypatch):
+    """The interpolating chains (k_blkp_ichain: each chain wave forms its slices' propagators from the interpolation
+    coefficients in registers, nothing stored), on the symmetric propagators' upper triangle (the tunable bus' H is
+    real) and on every entry (QOC_BLKP_ISYM=0): the oracle's J, dJ/du, states and co-states, and bit for bit the stored
+    form (k_blkp_int + k_blkp_dual / k_blkp_chain, QOC_BLKP_ICHAIN=0) in the device eval and in the split call form.
+    Nt = 37 (a partial last chunk of 8 slices), B = 5 (a last workgroup with two of its four waves idle)."""
+    from qoc_amd import systems
+    Nt, B = 37, 5
+    prob = systems.tunable_bus_problem(Nt=Nt, tgate=350.0 * Nt / 2000)
+    u = systems.tunable_bus_controls(B, Nt, seed=93)
+    out = {}
+    for ich, isym, want in (("1", "1", 2), ("1", "0", 1), ("0", "1", 0)):
+        monkeypatch.setenv("QOC_BLKP_ICHAIN", ich)
+        monkeypatch.setenv("QOC_BLKP_ISYM", isym)
+        e = _engine(prob, B, monkeypatch)
+        J, g = _eval(e, u, True)
+        info = e.info()
+        assert info["backward"] == "blocks_prop16" and info["interp_degree"] > 0, info
+        assert info["interp_chain"] == want, info
+        xs = [e.state(k, seed=b) for k in (0, 1, 8, 9, 36, Nt) for b in (0, 4)]
+        ls = [e.costate(k, seed=b) for k in (0, 1, 8, 9, 36, Nt) for b in (0, 4)]
+        Js = e.propagate(u)
+        gs = e.grape_sensitivity(u, 3)
+        assert e.info()["interp_chain"] == want
+        xs2 = [e.state(k, seed=3) for k in (0, 17, Nt)]
+        e.close()
+        out[want] = (J, g, xs, ls, Js, gs, xs2)
+    ref = out[0]
+    for form in (2, 1):
+        J, g, xs, ls, Js, gs, xs2 = out[form]
+        for b in range(B):
+            J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)
+            _assert_seed(J[b], g[b], J0, g0, ("ichain eval", form, b))
+            _assert_seed(Js[b], gs[b], J0, g0, ("ichain split", form, b))
+        _check_states(_Reader(xs, ls, (0, 1, 8, 9, 36, Nt), (0, 4)), prob, u, 4, (0, 1, 8, 9, 36, Nt))
+        for a, r, what in zip((J, g, Js, gs), (ref[0], ref[1], ref[4], ref[5]), ("J", "dJdu", "split J", "split dJdu")):
+            assert np.array_equal(a, r), (form, what)
+        for a, r in zip(xs + ls + xs2, ref[2] + ref[3] + ref[6]):
+            assert np.array_equal(a, r), form
+
+
+class _Reader:
+    """states / co-states read back before the engine closed, served as e.state / e.costate"""
+
+    def __init__(self, xs, ls, ks, seeds):
+        self.x = {(k, b): xs[i * len(seeds) + j] for i, k in enumerate(ks) for j, b in enumerate(seeds)}
+        self.l = {(k, b): ls[i * len(seeds) + j] for i, k in enumerate(ks) for j, b in enumerate(seeds)}
+
+    def state(self, k, seed=0):
+        return self.x[(k, seed)]
+
+    def costate(self, k, seed=0):
+        return self.l[(k, seed)]
