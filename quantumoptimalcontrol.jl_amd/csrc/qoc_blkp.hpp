@@ -992,73 +992,82 @@ struct BlkpIAcc {
   }
 };
 
+// One chain wave's view of its (seed, direction): state rows, output and sink pointers, this lane's entries
 template <bool FWD, int SL, bool SYM>
-__device__ __forceinline__ void blkp_ichain_body(const TChainArgs& g, const BlkArgs& bk, const BlkpIntArgs& ia,
-                                                 const double2* Ms, double2* xs, const int b) {
-  const int N = g.N, Nt = g.Nt, l = threadIdx.x & 63, i = l & 15, q = l >> 4;
-  const size_t Nm = (size_t)N;  // one state column
-  const int row = bk.wrow[i];   // wave block 0
-  const bool act = row >= 0, own = act && q == 0;
-  double2* const Os = xs + 32;         // [s][i]: x_{k+1} / μ_k of row i
-  double2* const Es = Os + SL * 16;    // SYM: [s][slot] the slices' packed entries
-  double2* const sink2 = reinterpret_cast<double2*>(tchain_sink(g));
-  const size_t oe = (size_t)max(row, 0);
-  double2* const Sb = reinterpret_cast<double2*>((cx<double>*)(FWD ? g.X : g.L) + (size_t)b * (Nt + 1) * Nm);
-  double2 v0 = make_double2(0.0, 0.0);
-  if (act) {
-    cx<double> v;
-    if (FWD) v = ((const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0))[oe];
-    else v = ((const cx<double>*)g.Xt)[oe];
-    v0 = make_double2(v.r, v.i);
-  }
-  xs[i] = v0;
-  blkp_wave_sync();
-  *(own ? Sb + (FWD ? 0 : (size_t)Nt * Nm) + oe : sink2) = v0;
-  double xr[4], xi[4];
+struct BlkpIChain {
+  static constexpr int NE = SYM ? 2 : 4;
+  static constexpr int SLB = SL < 4 ? SL : 4;  // SYM: slices per pass through the entry slab
+  int Nt, l, i, q;
+  bool act, own;
+  size_t Nm, oe;
+  double2 *Sb, *sink2;
+  const double* ub;
+  const double2* phb;
+  int off[NE];  // this lane's entries in a coefficient matrix
+  int ks[4];    // SYM: the packed slots of this lane's four entries (i, 4q + t), -1: a padding row or column
+  __device__ __forceinline__ void setup(const TChainArgs& g, const BlkArgs& bk, const BlkpIntArgs& ia, int b) {
+    Nt = g.Nt;
+    l = threadIdx.x & 63;
+    i = l & 15;
+    q = l >> 4;
+    Nm = (size_t)g.N;  // one state column
+    const int row = bk.wrow[i];  // wave block 0
+    act = row >= 0;
+    own = act && q == 0;
+    oe = (size_t)max(row, 0);
+    Sb = reinterpret_cast<double2*>((cx<double>*)(FWD ? g.X : g.L) + (size_t)b * (Nt + 1) * Nm);
+    sink2 = reinterpret_cast<double2*>(tchain_sink(g));
+    ub = ia.u + (size_t)b * Nt;
+    phb = ia.ph + (size_t)b * Nt;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const double2 v = xs[4 * q + t];
-    xr[t] = v.x;
-    xi[t] = v.y;
-  }
-  constexpr int NE = SYM ? 2 : 4;
-  int off[NE];   // this lane's entries in a coefficient matrix
-  int ks[4];     // SYM: the packed slots of this lane's four entries (i, 4q + t), -1: a padding row or column
+    for (int t = 0; t < 4; ++t) {
+      const int c = 4 * q + t, a = min(i, c), bb = max(i, c);
+      ks[t] = bb < ia.nl ? blkp_sym_slot(a, bb, ia.nl) : -1;
+    }
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int c = 4 * q + t, a = min(i, c), bb = max(i, c);
-    ks[t] = bb < ia.nl ? blkp_sym_slot(a, bb, ia.nl) : -1;
+    for (int t = 0; t < NE; ++t) off[t] = SYM ? 64 * t + l : FWD ? blkp_upos(i, 4 * q + t) : blkp_upos(4 * q + t, i);
   }
-#pragma unroll
-  for (int t = 0; t < NE; ++t) off[t] = SYM ? 64 * t + l : FWD ? blkp_upos(i, 4 * q + t) : blkp_upos(4 * q + t, i);
-  const double* const ub = ia.u + (size_t)b * Nt;
-  const int Dq = ia.Db[0];
-  typedef double D2V __attribute__((ext_vector_type(2)));
-  using G2 = __attribute__((address_space(1))) D2V;
-  const double2* const phb = ia.ph + (size_t)b * Nt;
-  for (int j0 = 0; j0 < Nt; j0 += SL) {
+  // x_0 / μ_N into the exchange row xs and to HBM
+  __device__ __forceinline__ void init(const TChainArgs& g, double2* xs, int b) {
+    double2 v0 = make_double2(0.0, 0.0);
+    if (act) {
+      cx<double> v;
+      if (FWD) v = ((const cx<double>*)g.x0 + (g.x0_per_seed ? (size_t)b * Nm : 0))[oe];
+      else v = ((const cx<double>*)g.Xt)[oe];
+      v0 = make_double2(v.r, v.i);
+    }
+    xs[i] = v0;
+    *(own ? Sb + (FWD ? 0 : (size_t)Nt * Nm) + oe : sink2) = v0;
+  }
+  // the propagator entries this lane applies in slices j0 .. j0 + SL - 1 (k_blkp_int's arithmetic term by term; SYM:
+  // the packed entries through the slab Es)
+  __device__ __forceinline__ void form(const BlkpIntArgs& ia, const double2* Ms, double2* Es, int j0, double (&ur)[SL][4],
+                                       double (&ui)[SL][4]) {
     BlkpIAcc<FWD, SL, NE> a;
     double2 phs[SL];  // the slices' e^{μ(u)}, loaded with the controls, used after the terms
 #pragma unroll
     for (int s = 0; s < SL; ++s) phs[s] = phb[FWD ? min(j0 + s, Nt - 1) : max(Nt - 1 - j0 - s, 0)];
     a.start(ia, ub, Nt, j0);
-    a.terms(Ms, off, SYM ? 128 : 256, 0, Dq + 1);
+    a.terms(Ms, off, SYM ? 128 : 256, 0, ia.Db[0] + 1);
     a.finish(phs, !SYM && !FWD);
-    double ur[SL][4], ui[SL][4];
-    if constexpr (SYM) {  // the packed entries through the slab to the lanes that apply them
+    if constexpr (SYM) {
 #pragma unroll
-      for (int s = 0; s < SL; ++s)
+      for (int s0 = 0; s0 < SL; s0 += SLB) {
 #pragma unroll
-        for (int t = 0; t < NE; ++t) Es[s * 128 + 64 * t + l] = make_double2(a.ur[s][t], a.ui[s][t]);
-      blkp_wave_sync();
+        for (int s = 0; s < SLB; ++s)
 #pragma unroll
-      for (int s = 0; s < SL; ++s)
+          for (int t = 0; t < NE; ++t) Es[s * 128 + 64 * t + l] = make_double2(a.ur[s0 + s][t], a.ui[s0 + s][t]);
+        blkp_wave_sync();
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const double2 v = ks[t] >= 0 ? Es[s * 128 + ks[t]] : make_double2(0.0, 0.0);
-          ur[s][t] = v.x;
-          ui[s][t] = FWD ? v.y : -v.y;
-        }
+        for (int s = 0; s < SLB; ++s)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const double2 v = ks[t] >= 0 ? Es[s * 128 + ks[t]] : make_double2(0.0, 0.0);
+            ur[s0 + s][t] = v.x;
+            ui[s0 + s][t] = FWD ? v.y : -v.y;
+          }
+        blkp_wave_sync();
+      }
     } else {
 #pragma unroll
       for (int s = 0; s < SL; ++s)
@@ -1068,12 +1077,24 @@ __device__ __forceinline__ void blkp_ichain_body(const TChainArgs& g, const BlkA
           ui[s][t] = a.ui[s][t];
         }
     }
-    // the SL chain steps (blkp_chain_body's arithmetic)
+  }
+  // the chunk's chain steps from the state in the exchange row xs (blkp_chain_body's arithmetic); the new states to
+  // Os, the last one left in xs
+  __device__ __forceinline__ void steps(const double (&ur)[SL][4], const double (&ui)[SL][4], double2* xs, double2* Os,
+                                        int j0) {
+    double xr[4], xi[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const double2 v = xs[4 * q + t];
+      xr[t] = v.x;
+      xi[t] = v.y;
+    }
 #pragma unroll
     for (int s = 0; s < SL; ++s) {
       if (j0 + s >= Nt) break;  // uniform
       double2 y = blkp_dot4(ur[s], ui[s], xr, xi);
       y = xsum_rows2(y);
+      blkp_wave_sync();  // every lane has read the row
       xs[i] = y;
       blkp_wave_sync();
 #pragma unroll
@@ -1082,11 +1103,14 @@ __device__ __forceinline__ void blkp_ichain_body(const TChainArgs& g, const BlkA
         xr[t] = v.x;
         xi[t] = v.y;
       }
-      blkp_wave_sync();
       if (q == 0) Os[s * 16 + i] = y;
     }
     blkp_wave_sync();
-    // the chunk's new states to HBM, branch-free (lanes without an element write the sink)
+  }
+  // the chunk's new states to HBM, branch-free (lanes without an element write the sink)
+  __device__ __forceinline__ void flush(const double2* Os, int j0) {
+    typedef double D2V __attribute__((ext_vector_type(2)));
+    using G2 = __attribute__((address_space(1))) D2V;
 #pragma unroll
     for (int s = 0; s < SL; ++s) {
       const int j = j0 + s;
@@ -1096,7 +1120,59 @@ __device__ __forceinline__ void blkp_ichain_body(const TChainArgs& g, const BlkA
       const double2 v = Os[s * 16 + i];
       *p = D2V{v.x, v.y};
     }
+  }
+};
+
+// one wave per (seed, direction): form, steps, flush, chunk after chunk
+template <bool FWD, int SL, bool SYM>
+__device__ __forceinline__ void blkp_ichain_body(const TChainArgs& g, const BlkArgs& bk, const BlkpIntArgs& ia,
+                                                 const double2* Ms, double2* xs, const int b) {
+  BlkpIChain<FWD, SL, SYM> cw;
+  cw.setup(g, bk, ia, b);
+  double2* const Os = xs + 32;       // [s][i]: x_{k+1} / μ_k of row i
+  double2* const Es = Os + SL * 16;  // SYM: [s][slot] the slices' packed entries
+  cw.init(g, xs, b);
+  blkp_wave_sync();
+  for (int j0 = 0; j0 < g.Nt; j0 += SL) {
+    double ur[SL][4], ui[SL][4];
+    cw.form(ia, Ms, Es, j0, ur, ui);
+    cw.steps(ur, ui, xs, Os, j0);
+    cw.flush(Os, j0);
     blkp_wave_sync();  // Os and Es are rewritten by the next chunk
+  }
+}
+
+// two waves per (seed, direction), on one SIMD (waves w and w + 4 of an 8-wave workgroup): wave role r takes the
+// chunks c = r, r + 2, ...; it forms chunk c's propagator entries, waits until its partner has run chunk c - 1 (the
+// pair's chunk counter in LDS), runs chunk c's steps from the state the partner left in the pair's exchange row at the
+// top issue priority, stores the chunk's states and publishes c + 1.  So one wave's latency-bound chain steps run while
+// the other forms the next chunk on the same SIMD.
+template <bool FWD, int SL, bool SYM>
+__device__ __forceinline__ void blkp_ichain_pair_body(const TChainArgs& g, const BlkArgs& bk, const BlkpIntArgs& ia,
+                                                      const double2* Ms, double2* xs, int* flag, double2* wl,
+                                                      const int role, const int b) {
+  BlkpIChain<FWD, SL, SYM> cw;
+  cw.setup(g, bk, ia, b);
+  double2* const Os = wl;            // this wave's [s][i]
+  double2* const Es = Os + SL * 16;  // SYM: this wave's slab
+  const int Nt = g.Nt, C = (Nt + SL - 1) / SL;
+  for (int c = role; c < C; c += 2) {
+    const int j0 = c * SL;
+    double ur[SL][4], ui[SL][4];
+    cw.form(ia, Ms, Es, j0, ur, ui);
+    if (c == 0) {
+      cw.init(g, xs, b);
+    } else {
+      while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < c) __builtin_amdgcn_s_sleep(1);
+    }
+    blkp_wave_sync();
+    __builtin_amdgcn_s_setprio(2);
+    cw.steps(ur, ui, xs, Os, j0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the exchange row is written before the counter
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(flag, c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    cw.flush(Os, j0);
+    blkp_wave_sync();
   }
 }
 
@@ -1131,6 +1207,34 @@ __global__ __launch_bounds__(256) void k_blkp_ichain(const TChainArgs gf, const 
   const int s = dual ? p >> 1 : p, d = dual ? p & 1 : dir;
   if (d == 0) blkp_ichain_body<true, SL, SYM>(gf, bk, ia, Ms, xs, seed0 + s);
   else blkp_ichain_body<false, SL, SYM>(gb, bk, ia, Ms, xs, seed0 + s);
+}
+
+// the paired form: 8 waves per workgroup, pairs (w, w + 4) = (seed, direction) 4 blockIdx.x + (w & 3); LDS: the
+// coefficients | per pair: exchange row 32 + counter | per wave: new states SL x 16 | SYM: slab 4 x 128 (double2)
+__host__ __device__ constexpr int blkp_ipair_wave_lds(int SL, bool sym) { return SL * 16 + (sym ? 4 * 128 : 0); }
+__host__ __device__ inline size_t blkp_ipair_lds(int D, int SL, bool sym) {
+  return ((size_t)(D + 1) * (sym ? 128 : 256) + 4 * 34 + 8 * (size_t)blkp_ipair_wave_lds(SL, sym)) * sizeof(double2);
+}
+template <int SL, bool SYM>
+__global__ __launch_bounds__(512) void k_blkp_ichain2(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk,
+                                                      const BlkpIntArgs ia, int seed0, int nseeds, int dual, int dir,
+                                                      const int* stale) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (stale && *stale != 0) return;  // uniform over the grid
+  double2* const Ms = reinterpret_cast<double2*>(smem);
+  const int D = ia.D, tid = threadIdx.x, w = tid >> 6, msz = (D + 1) * (SYM ? 128 : 256);
+  const double2* const src = SYM ? ia.Msym : ia.M;
+  for (int e = tid; e < msz; e += blockDim.x) Ms[e] = src[e];
+  double2* const pr = Ms + msz + 34 * (w & 3);  // the pair's exchange row (32) and counter
+  int* const flag = reinterpret_cast<int*>(pr + 32);
+  if (w < 4 && (tid & 63) == 0) *flag = 0;
+  __syncthreads();
+  double2* const wl = Ms + msz + 4 * 34 + (size_t)w * blkp_ipair_wave_lds(SL, SYM);
+  const int p = (int)blockIdx.x * 4 + (w & 3);
+  if (p >= (dual ? 2 : 1) * nseeds) return;  // both waves of the pair
+  const int s = dual ? p >> 1 : p, d = dual ? p & 1 : dir;
+  if (d == 0) blkp_ichain_pair_body<true, SL, SYM>(gf, bk, ia, Ms, pr, flag, wl, w >> 2, seed0 + s);
+  else blkp_ichain_pair_body<false, SL, SYM>(gb, bk, ia, Ms, pr, flag, wl, w >> 2, seed0 + s);
 }
 
 // ---- the order-3 gradient on the stored states (the reference's expm_jacobian! + _compute_u_sensitivity,

@@ -1101,13 +1101,17 @@ static int blkp_launch_ichain(qoc_ctx* c, const TChainArgs& gf, const TChainArgs
   // SL = 8 with AGPR spills, against 1.95 ms in sequence; profiles/r06v_ichain_ab.txt)
   // complex-symmetric generators: the upper triangle alone (QOC_BLKP_ISYM=0: every entry)
   const bool sym = blkp_ichain_sym(ia);
-  auto kern = sym ? k_blkp_ichain<BLKP_ISL, true> : k_blkp_ichain<BLKP_ISL, false>;
-  const size_t lds = blkp_ichain_lds(ia.D, BLKP_ISL, 4, sym);
+  // two waves per (seed, direction) on one SIMD, taking alternate chunks (QOC_BLKP_IPAIR=0: one wave)
+  const bool pair = !(getenv("QOC_BLKP_IPAIR") && atoi(getenv("QOC_BLKP_IPAIR")) == 0) &&
+                    blkp_ipair_lds(ia.D, BLKP_ISL, sym) <= 160 * 1024;
+  auto kern = pair ? (sym ? k_blkp_ichain2<BLKP_ISL, true> : k_blkp_ichain2<BLKP_ISL, false>)
+                   : (sym ? k_blkp_ichain<BLKP_ISL, true> : k_blkp_ichain<BLKP_ISL, false>);
+  const size_t lds = pair ? blkp_ipair_lds(ia.D, BLKP_ISL, sym) : blkp_ichain_lds(ia.D, BLKP_ISL, 4, sym);
   HIPCHK(c, blk_lds_attr(kern, lds));
   const int pairs = (dual ? 2 : 1) * c->B;
   const int mk = mark_begin(c, dual || dir == 0 ? 1 : 2);
-  hipLaunchKernelGGL(kern, dim3((pairs + 3) / 4), dim3(256), lds, c->stream, gf, gb, bk, ia, 0, c->B, dual ? 1 : 0, dir,
-                     stale);
+  hipLaunchKernelGGL(kern, dim3((pairs + 3) / 4), dim3(pair ? 512 : 256), lds, c->stream, gf, gb, bk, ia, 0, c->B,
+                     dual ? 1 : 0, dir, stale);
   mark_end(c, mk);
   HIPCHK(c, hipGetLastError());
   if (dual || dir == 0) {
