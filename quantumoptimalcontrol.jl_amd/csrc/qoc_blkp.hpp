@@ -992,11 +992,12 @@ struct BlkpIAcc {
   }
 };
 
+constexpr int BLKP_ISLB = 2;  // SYM: slices per pass through the entry slab (its LDS: BLKP_ISLB x 128 double2 per wave)
 // One chain wave's view of its (seed, direction): state rows, output and sink pointers, this lane's entries
 template <bool FWD, int SL, bool SYM>
 struct BlkpIChain {
   static constexpr int NE = SYM ? 2 : 4;
-  static constexpr int SLB = SL < 4 ? SL : 4;  // SYM: slices per pass through the entry slab
+  static constexpr int SLB = SL < BLKP_ISLB ? SL : BLKP_ISLB;  // SYM: slices per pass through the entry slab
   int Nt, l, i, q;
   bool act, own;
   size_t Nm, oe;
@@ -1209,11 +1210,14 @@ __global__ __launch_bounds__(256) void k_blkp_ichain(const TChainArgs gf, const 
   else blkp_ichain_body<false, SL, SYM>(gb, bk, ia, Ms, xs, seed0 + s);
 }
 
-// the paired form: 8 waves per workgroup, pairs (w, w + 4) = (seed, direction) 4 blockIdx.x + (w & 3); LDS: the
-// coefficients | per pair: exchange row 32 + counter | per wave: new states SL x 16 | SYM: slab 4 x 128 (double2)
-__host__ __device__ constexpr int blkp_ipair_wave_lds(int SL, bool sym) { return SL * 16 + (sym ? 4 * 128 : 0); }
-__host__ __device__ inline size_t blkp_ipair_lds(int D, int SL, bool sym) {
-  return ((size_t)(D + 1) * (sym ? 128 : 256) + 4 * 34 + 8 * (size_t)blkp_ipair_wave_lds(SL, sym)) * sizeof(double2);
+// the paired form: npw pairs per workgroup of 2 npw waves (blockDim.x = 128 npw), pair (w, w + npw) = (seed,
+// direction) npw blockIdx.x + w % npw (npw = 4: the two waves of a pair on one SIMD; npw = 2 when the pairs would
+// fill only half the CUs, the single-direction launches at B = 512); LDS: the coefficients | per pair: exchange row
+// 32 + counter | per wave: new states SL x 16 | SYM: slab BLKP_ISLB x 128 (double2)
+__host__ __device__ constexpr int blkp_ipair_wave_lds(int SL, bool sym) { return SL * 16 + (sym ? BLKP_ISLB * 128 : 0); }
+__host__ __device__ inline size_t blkp_ipair_lds(int D, int SL, bool sym, int npw) {
+  return ((size_t)(D + 1) * (sym ? 128 : 256) + (size_t)npw * 34 + 2 * (size_t)npw * blkp_ipair_wave_lds(SL, sym)) *
+         sizeof(double2);
 }
 template <int SL, bool SYM>
 __global__ __launch_bounds__(512) void k_blkp_ichain2(const TChainArgs gf, const TChainArgs gb, const BlkArgs bk,
@@ -1225,16 +1229,17 @@ __global__ __launch_bounds__(512) void k_blkp_ichain2(const TChainArgs gf, const
   const int D = ia.D, tid = threadIdx.x, w = tid >> 6, msz = (D + 1) * (SYM ? 128 : 256);
   const double2* const src = SYM ? ia.Msym : ia.M;
   for (int e = tid; e < msz; e += blockDim.x) Ms[e] = src[e];
-  double2* const pr = Ms + msz + 34 * (w & 3);  // the pair's exchange row (32) and counter
+  const int npw = (int)(blockDim.x >> 7), pw = w % npw;
+  double2* const pr = Ms + msz + 34 * pw;  // the pair's exchange row (32) and counter
   int* const flag = reinterpret_cast<int*>(pr + 32);
-  if (w < 4 && (tid & 63) == 0) *flag = 0;
+  if (w < npw && (tid & 63) == 0) *flag = 0;
   __syncthreads();
-  double2* const wl = Ms + msz + 4 * 34 + (size_t)w * blkp_ipair_wave_lds(SL, SYM);
-  const int p = (int)blockIdx.x * 4 + (w & 3);
+  double2* const wl = Ms + msz + npw * 34 + (size_t)w * blkp_ipair_wave_lds(SL, SYM);
+  const int p = (int)blockIdx.x * npw + pw;
   if (p >= (dual ? 2 : 1) * nseeds) return;  // both waves of the pair
   const int s = dual ? p >> 1 : p, d = dual ? p & 1 : dir;
-  if (d == 0) blkp_ichain_pair_body<true, SL, SYM>(gf, bk, ia, Ms, pr, flag, wl, w >> 2, seed0 + s);
-  else blkp_ichain_pair_body<false, SL, SYM>(gb, bk, ia, Ms, pr, flag, wl, w >> 2, seed0 + s);
+  if (d == 0) blkp_ichain_pair_body<true, SL, SYM>(gf, bk, ia, Ms, pr, flag, wl, w / npw, seed0 + s);
+  else blkp_ichain_pair_body<false, SL, SYM>(gb, bk, ia, Ms, pr, flag, wl, w / npw, seed0 + s);
 }
 
 // ---- the order-3 gradient on the stored states (the reference's expm_jacobian! + _compute_u_sensitivity,

@@ -1102,16 +1102,21 @@ static int blkp_launch_ichain(qoc_ctx* c, const TChainArgs& gf, const TChainArgs
   // complex-symmetric generators: the upper triangle alone (QOC_BLKP_ISYM=0: every entry)
   const bool sym = blkp_ichain_sym(ia);
   // two waves per (seed, direction) on one SIMD, taking alternate chunks (QOC_BLKP_IPAIR=0: one wave)
+  const int pairs = (dual ? 2 : 1) * c->B;
+  // pairs per workgroup: 4 (the two waves of a pair on one SIMD) unless that leaves CUs without one, then 2
+  int npw = pairs >= 4 * c->ncu ? 4 : 2;
+  // (QOC_BLKP_IPW=2 on the dual launch: two workgroups per CU, the pairs' waves on different SIMDs)
+  if (const char* e = getenv("QOC_BLKP_IPW")) npw = atoi(e) == 4 ? 4 : 2;  // (tests: force either)
   const bool pair = !(getenv("QOC_BLKP_IPAIR") && atoi(getenv("QOC_BLKP_IPAIR")) == 0) &&
-                    blkp_ipair_lds(ia.D, BLKP_ISL, sym) <= 160 * 1024;
+                    blkp_ipair_lds(ia.D, BLKP_ISL, sym, npw) <= 160 * 1024;
   auto kern = pair ? (sym ? k_blkp_ichain2<BLKP_ISL, true> : k_blkp_ichain2<BLKP_ISL, false>)
                    : (sym ? k_blkp_ichain<BLKP_ISL, true> : k_blkp_ichain<BLKP_ISL, false>);
-  const size_t lds = pair ? blkp_ipair_lds(ia.D, BLKP_ISL, sym) : blkp_ichain_lds(ia.D, BLKP_ISL, 4, sym);
+  const size_t lds = pair ? blkp_ipair_lds(ia.D, BLKP_ISL, sym, npw) : blkp_ichain_lds(ia.D, BLKP_ISL, 4, sym);
   HIPCHK(c, blk_lds_attr(kern, lds));
-  const int pairs = (dual ? 2 : 1) * c->B;
+  const int per = pair ? npw : 4;  // (seed, direction) pairs per workgroup
   const int mk = mark_begin(c, dual || dir == 0 ? 1 : 2);
-  hipLaunchKernelGGL(kern, dim3((pairs + 3) / 4), dim3(pair ? 512 : 256), lds, c->stream, gf, gb, bk, ia, 0, c->B,
-                     dual ? 1 : 0, dir, stale);
+  hipLaunchKernelGGL(kern, dim3((pairs + per - 1) / per), dim3(pair ? 128 * npw : 256), lds, c->stream, gf, gb, bk, ia,
+                     0, c->B, dual ? 1 : 0, dir, stale);
   mark_end(c, mk);
   HIPCHK(c, hipGetLastError());
   if (dual || dir == 0) {

@@ -217,7 +217,8 @@ def test_blkp_tail_chunk(built_lib, monkeypatch, ch):
 def test_blkp_interpolating_chains(built_lib, monkeypatch):
     """The interpolating chains (k_blkp_ichain: each chain wave forms its slices' propagators from the interpolation
     coefficients in registers, nothing stored), on the symmetric propagators' upper triangle (the tunable bus' H is
-    real) and on every entry (QOC_BLKP_ISYM=0), two waves per chain taking alternate chunks and one (QOC_BLKP_IPAIR=0):
+    real) and on every entry (QOC_BLKP_ISYM=0), two waves per chain taking alternate chunks (2 or 4 pairs per workgroup)
+    and one (QOC_BLKP_IPAIR=0):
     the oracle's J, dJ/du, states and co-states, and bit for bit the stored
     form (k_blkp_int + k_blkp_dual / k_blkp_chain, QOC_BLKP_ICHAIN=0) in the device eval and in the split call form.
     Nt = 37 (a partial last chunk of 8 slices), B = 5 (a last workgroup with two of its four waves idle)."""
@@ -226,11 +227,12 @@ def test_blkp_interpolating_chains(built_lib, monkeypatch):
     prob = systems.tunable_bus_problem(Nt=Nt, tgate=350.0 * Nt / 2000)
     u = systems.tunable_bus_controls(B, Nt, seed=93)
     out = {}
-    for ich, isym, ipair, want in (("1", "1", "1", 2), ("1", "1", "0", 2), ("1", "0", "1", 1), ("1", "0", "0", 1),
-                                   ("0", "1", "1", 0)):
+    for ich, isym, ipair, want in (("1", "1", "1", 2), ("1", "1", "4", 2), ("1", "1", "0", 2), ("1", "0", "1", 1),
+                                   ("1", "0", "0", 1), ("0", "1", "1", 0)):
         monkeypatch.setenv("QOC_BLKP_ICHAIN", ich)
         monkeypatch.setenv("QOC_BLKP_ISYM", isym)
-        monkeypatch.setenv("QOC_BLKP_IPAIR", ipair)
+        monkeypatch.setenv("QOC_BLKP_IPAIR", "0" if ipair == "0" else "1")
+        monkeypatch.setenv("QOC_BLKP_IPW", "4" if ipair == "4" else "2")  # pairs per workgroup
         e = _engine(prob, B, monkeypatch)
         J, g = _eval(e, u, True)
         info = e.info()
@@ -245,7 +247,7 @@ def test_blkp_interpolating_chains(built_lib, monkeypatch):
         e.close()
         out[(want, ipair)] = (J, g, xs, ls, Js, gs, xs2)
     ref = out[(0, "1")]
-    for form in ((2, "1"), (2, "0"), (1, "1"), (1, "0")):
+    for form in ((2, "1"), (2, "4"), (2, "0"), (1, "1"), (1, "0")):
         J, g, xs, ls, Js, gs, xs2 = out[form]
         for b in range(B):
             J0, g0, _ = O.grape_eval(prob.A0, prob.A, u[b], prob.x0, prob.x_target, prob.n, order=3)

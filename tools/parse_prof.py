@@ -10,7 +10,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("k_blkp_exp", "k_blkp_dual", "k_blkp_chain", "k_blkp_int", "k_minmax", "k_blkseg_fwd", "k_blkseg_bwd", "k_blkp_grad", "k_blkseg_eval", "k_zero_rows", "k_bgemm_glds", "k_form_norm2", "k_blku_rec", "k_blku_fwd", "k_blku_bwdg", "k_blku_bwd", "k_blku_grad", "k_blku_dual", "k_blkrot_dual", "k_blkrot_fwd", "k_blkrot_bwd", "k_blk_dual", "k_blk_grad", "k_blk_fwd", "k_blk_bwd", "k_tchain_mf_dual", "k_grad_rr_c", "k_spec_bound", "k_tchain_mf_fwd", "k_tchain_mf_bwd", "k_tchain_prep", "k_tchain_fwd", "k_tchain_bwd", "k_pade_units",
+KERNELS = ("k_blkp_ichain", "k_blkp_phase", "k_terminal_cost", "k_blkp_exp", "k_blkp_dual", "k_blkp_chain", "k_blkp_int", "k_minmax", "k_blkseg_fwd", "k_blkseg_bwd", "k_blkp_grad", "k_blkseg_eval", "k_zero_rows", "k_bgemm_glds", "k_form_norm2", "k_blku_rec", "k_blku_fwd", "k_blku_bwdg", "k_blku_bwd", "k_blku_grad", "k_blku_dual", "k_blkrot_dual", "k_blkrot_fwd", "k_blkrot_bwd", "k_blk_dual", "k_blk_grad", "k_blk_fwd", "k_blk_bwd", "k_tchain_mf_dual", "k_grad_rr_c", "k_spec_bound", "k_tchain_mf_fwd", "k_tchain_mf_bwd", "k_tchain_prep", "k_tchain_fwd", "k_tchain_bwd", "k_pade_units",
            "k_argmin_seed", "k_expm_rr_ps", "k_expm_rr_mix", "k_expm_rr", "k_expm", "k_chain_fwd", "k_chain_bwd", "k_grad_rr_q", "k_grad_rr_p", "k_grad_rr_s", "k_grad", "k_bgemm", "k_form_norm", "k_lincomb", "k_gen_contract")
 
 
