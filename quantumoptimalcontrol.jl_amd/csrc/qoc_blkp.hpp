@@ -933,9 +933,11 @@ __global__ __launch_bounds__(512) void k_blkp_chain(const TChainArgs g, const Bl
 // of such generators for every form (the stored one too), so both give the same bits.
 // LDS: the coefficients [D + 1][256] (at blkp_upos positions) or [D + 1][128] (SYM) double2 | per wave: exchange row
 // 32 | new states SL x 16 | SYM: the entry slab SL x 128 (double2)
-__host__ __device__ constexpr int blkp_ichain_wave_lds(int SL, bool sym) { return 32 + SL * 16 + (sym ? SL * 128 : 0); }
+__host__ __device__ constexpr int blkp_ichain_wave_lds(int SL, bool sym, int D) {
+  return 32 + SL * 16 + (sym ? SL * 128 : 0) + (D + 1) * SL / 2;
+}
 __host__ __device__ inline size_t blkp_ichain_lds(int D, int SL, int waves, bool sym) {
-  return ((size_t)(D + 1) * (sym ? 128 : 256) + (size_t)waves * blkp_ichain_wave_lds(SL, sym)) * sizeof(double2);
+  return ((size_t)(D + 1) * (sym ? 128 : 256) + (size_t)waves * blkp_ichain_wave_lds(SL, sym, D)) * sizeof(double2);
 }
 // slot of the upper-triangle entry (a, b), a <= b < nl, in the packed layout (row-major triangle)
 __host__ __device__ constexpr int blkp_sym_slot(int a, int b, int nl) { return a * nl - a * (a - 1) / 2 + (b - a); }
@@ -943,38 +945,50 @@ __host__ __device__ constexpr int blkp_sym_slot(int a, int b, int nl) { return a
 // the interpolation of SL slices' propagator entries, NE per lane (k_blkp_int's arithmetic, term by term)
 template <bool FWD, int SL, int NE>
 struct BlkpIAcc {
-  double ur[SL][NE], ui[SL][NE], uu[SL], xv[SL], tm[SL], tc[SL];
-  // the slices j0 .. j0 + SL - 1 of this direction (clamped at the ends)
-  __device__ __forceinline__ void start(const BlkpIntArgs& ia, const double* ub, int Nt, int j0) {
+  double ur[SL][NE], ui[SL][NE];
+  // the Chebyshev values of slices j0 .. j0 + SL - 1 of this direction (clamped at the ends) into Ts[i SL + s]: lane
+  // s < SL runs slice s's recurrence (k_blkp_int's, the same values), so the other lanes need not
+  __device__ __forceinline__ void tvalues(const BlkpIntArgs& ia, const double* ub, int Nt, int j0, int D, double* Ts) {
+    const int l = threadIdx.x & 63;
+    if (l < SL) {
+      const int j = j0 + l;
+      const double x = fma(ia.xa, ub[FWD ? min(j, Nt - 1) : max(Nt - 1 - j, 0)], ia.xb);
+      double tm = 1.0, tc = 1.0;
+      for (int ti = 0; ti <= D; ++ti) {
+        Ts[ti * SL + l] = tc;
+        const double tn = ti == 0 ? x : fma(2.0 * x, tc, -tm);
+        tm = tc;
+        tc = tn;
+      }
+    }
 #pragma unroll
-    for (int s = 0; s < SL; ++s) {
-      const int j = j0 + s;
-      uu[s] = ub[FWD ? min(j, Nt - 1) : max(Nt - 1 - j, 0)];
-      xv[s] = fma(ia.xa, uu[s], ia.xb);
-      tm[s] = 1.0;
-      tc[s] = 1.0;
+    for (int s = 0; s < SL; ++s)
 #pragma unroll
       for (int t = 0; t < NE; ++t) ur[s][t] = ui[s][t] = 0.0;
-    }
   }
-  // terms [t0, t1) of Σ T_i(ξ) M_i: this lane's entries at off[] in each coefficient matrix of `stride` entries
-  __device__ __forceinline__ void terms(const double2* Ms, const int (&off)[NE], int stride, int t0, int t1) {
+  // terms [t0, t1) of Σ T_i(ξ) M_i: this lane's entries at off[] in each coefficient matrix of `stride` entries, the
+  // T_i(ξ_s) read from Ts (one broadcast per two slices)
+  __device__ __forceinline__ void terms(const double2* Ms, const int (&off)[NE], int stride, const double* Ts, int t0,
+                                        int t1) {
 #pragma unroll 2
     for (int ti = t0; ti < t1; ++ti) {
       double2 mv[NE];
 #pragma unroll
       for (int t = 0; t < NE; ++t) mv[t] = Ms[ti * stride + off[t]];
+      double tv[SL];
 #pragma unroll
-      for (int s = 0; s < SL; ++s) {
+      for (int s = 0; s < SL; s += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(Ts + ti * SL + s);
+        tv[s] = v.x;
+        tv[s + 1] = v.y;
+      }
+#pragma unroll
+      for (int s = 0; s < SL; ++s)
 #pragma unroll
         for (int t = 0; t < NE; ++t) {
-          ur[s][t] = fma(tc[s], mv[t].x, ur[s][t]);
-          ui[s][t] = fma(tc[s], mv[t].y, ui[s][t]);
+          ur[s][t] = fma(tv[s], mv[t].x, ur[s][t]);
+          ui[s][t] = fma(tv[s], mv[t].y, ui[s][t]);
         }
-        const double tn = ti == 0 ? xv[s] : fma(2.0 * xv[s], tc[s], -tm[s]);
-        tm[s] = tc[s];
-        tc[s] = tn;
-      }
     }
   }
   // times e^{μ(u)} (phs[s]: k_blkp_phase's); conj: the conjugates (the μ recurrence's U^H entries)
@@ -1042,14 +1056,16 @@ struct BlkpIChain {
   }
   // the propagator entries this lane applies in slices j0 .. j0 + SL - 1 (k_blkp_int's arithmetic term by term; SYM:
   // the packed entries through the slab Es)
-  __device__ __forceinline__ void form(const BlkpIntArgs& ia, const double2* Ms, double2* Es, int j0, double (&ur)[SL][4],
-                                       double (&ui)[SL][4]) {
+  __device__ __forceinline__ void form(const BlkpIntArgs& ia, const double2* Ms, double2* Es, double* Ts, int j0,
+                                       double (&ur)[SL][4], double (&ui)[SL][4]) {
     BlkpIAcc<FWD, SL, NE> a;
     double2 phs[SL];  // the slices' e^{μ(u)}, loaded with the controls, used after the terms
 #pragma unroll
     for (int s = 0; s < SL; ++s) phs[s] = phb[FWD ? min(j0 + s, Nt - 1) : max(Nt - 1 - j0 - s, 0)];
-    a.start(ia, ub, Nt, j0);
-    a.terms(Ms, off, SYM ? 128 : 256, 0, ia.Db[0] + 1);
+    a.tvalues(ia, ub, Nt, j0, ia.Db[0], Ts);
+    blkp_wave_sync();
+    a.terms(Ms, off, SYM ? 128 : 256, Ts, 0, ia.Db[0] + 1);
+    blkp_wave_sync();  // Ts is rewritten by the next chunk
     a.finish(phs, !SYM && !FWD);
     if constexpr (SYM) {
 #pragma unroll
@@ -1132,11 +1148,12 @@ __device__ __forceinline__ void blkp_ichain_body(const TChainArgs& g, const BlkA
   cw.setup(g, bk, ia, b);
   double2* const Os = xs + 32;       // [s][i]: x_{k+1} / μ_k of row i
   double2* const Es = Os + SL * 16;  // SYM: [s][slot] the slices' packed entries
+  double* const Ts = reinterpret_cast<double*>(Es + (SYM ? SL * 128 : 0));  // [i][s] the chunk's T_i(ξ_s)
   cw.init(g, xs, b);
   blkp_wave_sync();
   for (int j0 = 0; j0 < g.Nt; j0 += SL) {
     double ur[SL][4], ui[SL][4];
-    cw.form(ia, Ms, Es, j0, ur, ui);
+    cw.form(ia, Ms, Es, Ts, j0, ur, ui);
     cw.steps(ur, ui, xs, Os, j0);
     cw.flush(Os, j0);
     blkp_wave_sync();  // Os and Es are rewritten by the next chunk
@@ -1156,11 +1173,12 @@ __device__ __forceinline__ void blkp_ichain_pair_body(const TChainArgs& g, const
   cw.setup(g, bk, ia, b);
   double2* const Os = wl;            // this wave's [s][i]
   double2* const Es = Os + SL * 16;  // SYM: this wave's slab
+  double* const Ts = reinterpret_cast<double*>(Es + (SYM ? BLKP_ISLB * 128 : 0));  // [i][s] the chunk's T_i(ξ_s)
   const int Nt = g.Nt, C = (Nt + SL - 1) / SL;
   for (int c = role; c < C; c += 2) {
     const int j0 = c * SL;
     double ur[SL][4], ui[SL][4];
-    cw.form(ia, Ms, Es, j0, ur, ui);
+    cw.form(ia, Ms, Es, Ts, j0, ur, ui);
     if (c == 0) {
       cw.init(g, xs, b);
     } else {
@@ -1202,7 +1220,7 @@ __global__ __launch_bounds__(256) void k_blkp_ichain(const TChainArgs gf, const 
   const double2* const src = SYM ? ia.Msym : ia.M;
   for (int e = tid; e < msz; e += blockDim.x) Ms[e] = src[e];
   __syncthreads();
-  double2* const xs = Ms + msz + (size_t)w * blkp_ichain_wave_lds(SL, SYM);
+  double2* const xs = Ms + msz + (size_t)w * blkp_ichain_wave_lds(SL, SYM, D);
   const int p = (int)blockIdx.x * (int)(blockDim.x >> 6) + w;
   if (p >= (dual ? 2 : 1) * nseeds) return;
   const int s = dual ? p >> 1 : p, d = dual ? p & 1 : dir;
@@ -1214,9 +1232,11 @@ __global__ __launch_bounds__(256) void k_blkp_ichain(const TChainArgs gf, const 
 // direction) npw blockIdx.x + w % npw (npw = 4: the two waves of a pair on one SIMD; npw = 2 when the pairs would
 // fill only half the CUs, the single-direction launches at B = 512); LDS: the coefficients | per pair: exchange row
 // 32 + counter | per wave: new states SL x 16 | SYM: slab BLKP_ISLB x 128 (double2)
-__host__ __device__ constexpr int blkp_ipair_wave_lds(int SL, bool sym) { return SL * 16 + (sym ? BLKP_ISLB * 128 : 0); }
+__host__ __device__ constexpr int blkp_ipair_wave_lds(int SL, bool sym, int D) {
+  return SL * 16 + (sym ? BLKP_ISLB * 128 : 0) + (D + 1) * SL / 2;
+}
 __host__ __device__ inline size_t blkp_ipair_lds(int D, int SL, bool sym, int npw) {
-  return ((size_t)(D + 1) * (sym ? 128 : 256) + (size_t)npw * 34 + 2 * (size_t)npw * blkp_ipair_wave_lds(SL, sym)) *
+  return ((size_t)(D + 1) * (sym ? 128 : 256) + (size_t)npw * 34 + 2 * (size_t)npw * blkp_ipair_wave_lds(SL, sym, D)) *
          sizeof(double2);
 }
 template <int SL, bool SYM>
@@ -1234,7 +1254,7 @@ __global__ __launch_bounds__(512) void k_blkp_ichain2(const TChainArgs gf, const
   int* const flag = reinterpret_cast<int*>(pr + 32);
   if (w < npw && (tid & 63) == 0) *flag = 0;
   __syncthreads();
-  double2* const wl = Ms + msz + npw * 34 + (size_t)w * blkp_ipair_wave_lds(SL, SYM);
+  double2* const wl = Ms + msz + npw * 34 + (size_t)w * blkp_ipair_wave_lds(SL, SYM, D);
   const int p = (int)blockIdx.x * npw + pw;
   if (p >= (dual ? 2 : 1) * nseeds) return;  // both waves of the pair
   const int s = dual ? p >> 1 : p, d = dual ? p & 1 : dir;
