@@ -20,6 +20,11 @@
 //     call form: the forward chain in propagate, the μ recurrence in grape_sensitivity).
 //   * k_blkp_grad: the order-3 gradient from x_k and μ_{k+1}, 16 slices per wave as the columns of 16 x 16 x 16
 //     generator GEMMs on MFMA.
+// With one control (nu = 1) the propagators are a Chebyshev series in u over the batch's control range instead:
+//   * k_blkp_int forms the stored propagators from its coefficients (D + 1 scaled sums of LDS-resident matrices);
+//   * k_blkp_ichain / k_blkp_ichain2 (one live wave block, one state column: the tunable bus, the default) let the chain
+//     waves form their own propagators in registers and apply them at once, nothing stored (k_blkp_phase precomputes
+//     the slices' e^{μ(u_k)}; the forward's cost is k_terminal_cost's).
 #pragma once
 #include "qoc_blk.hpp"
 
@@ -1282,6 +1287,8 @@ struct BlkpGradArgs {
   long long tiles;           // B ceil(Nt / 16)
   const int* stale;          // a stale-u flag queued before the launch (nonzero: nothing is written), or nullptr
   cx<double>* coef_out;      // a copy of coef (qoc_get_costates' λ = coef ⊙ μ), written by workgroup 0, or nullptr
+  unsigned diag;             // bit j: A_j (j >= 1) diagonal on the live wave blocks' rows (the tunable bus' flux term):
+                             // its products are row scalings on the VALU instead of 12 MFMAs
 };
 __host__ __device__ inline size_t blkp_grad_lds(int nwb, int nu) { return (size_t)nwb * (nu + 1) * 2 * 256 * sizeof(double2); }
 
@@ -1354,6 +1361,31 @@ __global__ __launch_bounds__(256, 2) void k_blkp_grad(const BlkpGradArgs a) {
         }
         return M;
       };
+      // diagonal A_{q+1}: this lane's rows' entries (A_j^H: the conjugates)
+      double dr[NU][4], di[NU][4];
+#pragma unroll
+      for (int q = 0; q < NU; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const cx<double> z = rows[e] >= 0 && ((a.diag >> (q + 1)) & 1u)
+                                   ? a.A[(size_t)(q + 1) * NN + rows[e] + (size_t)N * rows[e]] : cx<double>{0.0, 0.0};
+          dr[q][e] = z.r;
+          di[q][e] = z.i;
+        }
+      // A_{q+1} M (form 0) or A_{q+1}^H M (form 1)
+      auto mulA = [&](int q, int form, const CMat& M) __attribute__((always_inline)) {
+        if ((a.diag >> (q + 1)) & 1u) {  // uniform
+          CMat Y;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const double zi = form ? -di[q][e] : di[q][e];
+            Y.r[e] = fma(dr[q][e], M.r[e], -(zi * M.i[e]));
+            Y.i[e] = fma(dr[q][e], M.i[e], zi * M.r[e]);
+          }
+          return Y;
+        }
+        return cm_mul<false>(op(q + 1, form), M, M);
+      };
       for (int c = 0; c < m; ++c) {
         const cx<double> cf = a.coef[(size_t)b * 2 * m + c];
         const cx<double>* xb = a.X + ((size_t)b * (Nt + 1) + kc) * Nm + (size_t)c * N;  // x_k
@@ -1372,10 +1404,10 @@ __global__ __launch_bounds__(256, 2) void k_blkp_grad(const BlkpGradArgs a) {
         // the co-state side: Q_1 = A_k^H λ, Q_2 = A_k^H Q_1
         CMat Q1 = cm_mul<false>(op(0, 1), Lm, Lm);
 #pragma unroll
-        for (int q = 0; q < NU; ++q) blkp_axpy(Q1, uj[q], cm_mul<false>(op(q + 1, 1), Lm, Lm));
+        for (int q = 0; q < NU; ++q) blkp_axpy(Q1, uj[q], mulA(q, 1, Lm));
         CMat Q2 = cm_mul<false>(op(0, 1), Q1, Q1);
 #pragma unroll
-        for (int q = 0; q < NU; ++q) blkp_axpy(Q2, uj[q], cm_mul<false>(op(q + 1, 1), Q1, Q1));
+        for (int q = 0; q < NU; ++q) blkp_axpy(Q2, uj[q], mulA(q, 1, Q1));
         CMat W0, W1;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1390,19 +1422,19 @@ __global__ __launch_bounds__(256, 2) void k_blkp_grad(const BlkpGradArgs a) {
         CMat P1 = cm_mul<false>(op(0, 0), X, X);
 #pragma unroll
         for (int q = 0; q < NU; ++q) {
-          const CMat Y = cm_mul<false>(op(q + 1, 0), X, X);
+          const CMat Y = mulA(q, 0, X);
           acc[q] += blkp_redot(W0, Y);
           blkp_axpy(P1, uj[q], Y);
         }
         CMat P2 = cm_mul<false>(op(0, 0), P1, P1);
 #pragma unroll
         for (int q = 0; q < NU; ++q) {
-          const CMat Y = cm_mul<false>(op(q + 1, 0), P1, P1);
+          const CMat Y = mulA(q, 0, P1);
           acc[q] += blkp_redot(W1, Y);
           blkp_axpy(P2, uj[q], Y);
         }
 #pragma unroll
-        for (int q = 0; q < NU; ++q) acc[q] += blkp_redot(Lm, cm_mul<false>(op(q + 1, 0), P2, P2));
+        for (int q = 0; q < NU; ++q) acc[q] += blkp_redot(Lm, mulA(q, 0, P2));
       }
     }
 #pragma unroll

@@ -1050,6 +1050,24 @@ static int blkp_launch_grad(qoc_ctx* c, const BlkArgs& bk, double* d_dJdu, const
   ga.tiles = (long long)c->B * ((c->Nt + 15) / 16);
   ga.stale = stale;
   ga.coef_out = coef_out;
+  // generators diagonal on the live wave blocks' rows (QOC_BLKP_GDIAG=0: every product on MFMA)
+  ga.diag = 0;
+  if (!(getenv("QOC_BLKP_GDIAG") && atoi(getenv("QOC_BLKP_GDIAG")) == 0)) {
+    const std::vector<int>& wrow = bk.wrow == c->d_wrow_live ? c->h_wrow_live : c->h_wrow;
+    const size_t NN = (size_t)c->N * c->N;
+    for (int j = 1; j <= c->nu && wrow.size() == 16 * (size_t)bk.nwb; ++j) {
+      bool dg = true;
+      for (int w = 0; w < bk.nwb && dg; ++w)
+        for (int r = 0; r < 16 && dg; ++r)
+          for (int q = 0; q < 16 && dg; ++q) {
+            const int row = wrow[16 * w + r], col = wrow[16 * w + q];
+            if (row < 0 || col < 0 || row == col) continue;
+            const double* z = c->h_gen.data() + 2 * (j * NN + row + (size_t)c->N * col);
+            dg = z[0] == 0.0 && z[1] == 0.0;
+          }
+      if (dg) ga.diag |= 1u << j;
+    }
+  }
   const size_t glds = blkp_grad_lds(bk.nwb, c->nu);
   auto gk = c->nu == 1 ? k_blkp_grad<1> : k_blkp_grad<2>;
   HIPCHK(c, blk_lds_attr(gk, glds));
