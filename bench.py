@@ -130,7 +130,7 @@ def blkseg_series_k(prob, u_all):
     return np.where(rho <= 0.24, 5, np.where(rho <= 0.66, 7, 9))
 
 
-def blkseg_unit_flops(nb, order, P=None, K=9):
+def blkseg_unit_flops(nb, order, P=None, K=9, zd=False):
     """Executed fp64 flops of the segmented block eval (csrc/qoc_blkseg.hpp) per (slice, block) unit, counted from
     the kernel's code (FMA = 2, add / mul = 1), phase 1 and phase 3 (the block exponential is formed in both: it is
     recomputed, not stored).  Blocks of 2 rows (the skew-Hermitian fast path): closed-form exponential (Â 16, the
@@ -138,11 +138,17 @@ def blkseg_unit_flops(nb, order, P=None, K=9):
     64 each, the
     contraction in the Pauli basis (sk2_contract_pauli) 20 / 53 / 75 at orders 1 / 2 / 3, 16 + 104 (order - 1) on
     skew X at order 4 (sk2_contract); blocks of 3 rows: the Taylor polynomial of degree P in the
-    Cayley-Hamilton basis (478 + 26 (P + 1)), 3x3 products 216 each, the contraction 86 + 518 (order - 1)."""
+    Cayley-Hamilton basis (478 + 26 (P + 1)), 3x3 products 216 each, the contraction 86 + 518 (order - 1).
+    zd (blocks of 2 rows; control generators with zero diagonals and zero shifts, qoc_blkseg.hpp ZD): the block's
+    diagonal, its half-difference and the phase series cos t, sin t are the same in every slice and computed once per
+    lane, so the exponential takes 43 + 4 (K + 1) flops, phase 3's μ_k 0 and the Pauli contraction's x0, x3, x0² none."""
     if nb == 2:
-        form, prod = 57.0 + 8.0 * (K + 1), 64.0
+        form = (43.0 + 4.0 * (K + 1)) if zd else (57.0 + 8.0 * (K + 1))
+        prod = 64.0
         contr = {1: 20.0, 2: 53.0, 3: 75.0}.get(order, 16.0 + 104.0 * (order - 1))
-        return form + prod, form + 2 * prod + 6.0 + contr + 2.0
+        if zd and order in (2, 3):
+            contr -= 4.0 if order == 2 else 5.0
+        return form + prod, form + 2 * prod + (2.0 if zd else 6.0) + contr + 2.0
     form = 478.0 + 26.0 * ((P or 8) + 1)
     prod, contr = 216.0, 86.0 + 518.0 * (order - 1)
     return form + prod, form + 2 * prod + 76.0 + contr + 2.0
@@ -602,7 +608,9 @@ def main():
         units = B * Nt * nblk
         if nbk == 2:  # the series degree per seed
             ks = blkseg_series_k(prob, u_all)
-            fl = [blkseg_unit_flops(2, args.order, None, int(k)) for k in ks]
+            # the controls' blocks without diagonal (and so without shifts): the kernel's ZD path
+            zd = all(not np.any(np.diag(np.asarray(a))) for a in prob.A)
+            fl = [blkseg_unit_flops(2, args.order, None, int(k), zd) for k in ks]
             f1, f3 = float(np.mean([a for a, _ in fl])), float(np.mean([c for _, c in fl]))
         else:
             ks = None

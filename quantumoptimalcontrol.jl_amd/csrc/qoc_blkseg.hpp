@@ -347,26 +347,45 @@ struct Sk2 {
 };
 __device__ __forceinline__ Sk2 sk2_of(const double2 (&e)[4]) { return Sk2{e[0].y, e[3].y, e[1].x, e[1].y}; }
 
-// Â = Ã_0 + u_1 Ã_1 + u_2 Ã_2 (no halvings) and U = e^{μ_k} exp(Â) in the closed form of seg_form (ph = e^{μ_k})
+// cos t and sin t of the block's mean diagonal t = (d0 + d1) / 2 (sk2_form's series)
 template <int K = BLKSEG_KMAX>
-__device__ __forceinline__ void sk2_form(const Sk2 (&g)[3], double2 ph, double2 u, Sk2& ah, double (&ur)[4],
-                                         double (&ui)[4]) {
+__device__ __forceinline__ void sk2_phase(double d0, double d1, double& ct, double& st) {
   constexpr BlksegTrig T = blkseg_trig();
-  ah.d0 = fma(u.y, g[2].d0, fma(u.x, g[1].d0, g[0].d0));
-  ah.d1 = fma(u.y, g[2].d1, fma(u.x, g[1].d1, g[0].d1));
-  ah.r = fma(u.y, g[2].r, fma(u.x, g[1].r, g[0].r));
-  ah.q = fma(u.y, g[2].q, fma(u.x, g[1].q, g[0].q));
-  const double t = 0.5 * (ah.d0 + ah.d1), a = 0.5 * (ah.d0 - ah.d1);
-  const double w = fma(a, a, fma(ah.r, ah.r, ah.q * ah.q)), t2 = t * t;
-  double cw = 0.0, sw = 0.0, ct = 0.0, st = 0.0;
+  const double t = 0.5 * (d0 + d1), t2 = t * t;
+  ct = 0.0;
+  st = 0.0;
 #pragma unroll
   for (int k = K; k >= 0; --k) {
-    cw = fma(cw, w, T.c[k]);
-    sw = fma(sw, w, T.s[k]);
     ct = fma(ct, t2, T.c[k]);
     st = fma(st, t2, T.s[k]);
   }
   st *= t;
+}
+// Â = Ã_0 + u_1 Ã_1 + u_2 Ã_2 (no halvings) and U = e^{μ_k} exp(Â) in the closed form of seg_form (ph = e^{μ_k}).
+// ZD: the control generators' blocks have zero diagonals, so Â's diagonal is Ã_0's for every slice and cos t, sin t
+// come precomputed (ct0, st0: sk2_phase of Ã_0's diagonal, the same values)
+template <int K = BLKSEG_KMAX, bool ZD = false>
+__device__ __forceinline__ void sk2_form(const Sk2 (&g)[3], double2 ph, double2 u, Sk2& ah, double (&ur)[4],
+                                         double (&ui)[4], double ct0 = 1.0, double st0 = 0.0, double a0 = 0.0) {
+  constexpr BlksegTrig T = blkseg_trig();
+  if constexpr (ZD) {  // the same values (u_j times a zero diagonal adds nothing)
+    ah.d0 = g[0].d0;
+    ah.d1 = g[0].d1;
+  } else {
+    ah.d0 = fma(u.y, g[2].d0, fma(u.x, g[1].d0, g[0].d0));
+    ah.d1 = fma(u.y, g[2].d1, fma(u.x, g[1].d1, g[0].d1));
+  }
+  ah.r = fma(u.y, g[2].r, fma(u.x, g[1].r, g[0].r));
+  ah.q = fma(u.y, g[2].q, fma(u.x, g[1].q, g[0].q));
+  const double a = ZD ? a0 : 0.5 * (ah.d0 - ah.d1);  // (ZD: a0 the same value, once per lane)
+  const double w = fma(a, a, fma(ah.r, ah.r, ah.q * ah.q));
+  double cw = 0.0, sw = 0.0, ct = ct0, st = st0;
+#pragma unroll
+  for (int k = K; k >= 0; --k) {
+    cw = fma(cw, w, T.c[k]);
+    sw = fma(sw, w, T.s[k]);
+  }
+  if constexpr (!ZD) sk2_phase<K>(ah.d0, ah.d1, ct, st);
   const double zr = ph.x * ct - ph.y * st, zi = fma(ph.x, st, ph.y * ct);
   const double cr = zr * cw, ci = zi * cw, sr = zr * sw, si = zi * sw;
   ur[0] = fma(-si, a, cr);
@@ -439,10 +458,13 @@ __device__ __forceinline__ void sk2_contract(const Sk2& x, const Sk2& e1, const 
 // (the Pauli products (x.σ)(k.σ)(x.σ) = 2 (x.k) x.σ - ω² k.σ etc.; checked against the matrix recurrence in numpy).
 // ~73 flops instead of sk2_contract's 224 at order 3.  aj: the generators' Pauli vectors times 2 (pre-scaled so that
 // the K components below can stay doubled: 2 k0 = K00 + K11, ...).
-template <int ORD>
+// CX: X's diagonal is the same in every slice (zero-diagonal controls, zero control shifts): x0, x3 and x0² come
+// precomputed (x0c, x3c, x02c: the same values)
+template <int ORD, bool CX = false>
 __device__ __forceinline__ void sk2_contract_pauli(const Sk2& x, const double (&a1)[4], const double (&a2)[4],
                                                    const double (&Kr)[4], const double (&Ki)[4], double& acc1,
-                                                   double& acc2) {
+                                                   double& acc2, double x0c = 0.0, double x3c = 0.0,
+                                                   double x02c = 0.0) {
   static_assert(ORD >= 1 && ORD <= 3, "Pauli form for orders 1..3");
   // doubled Pauli components of K: 2k0 = K00 + K11, 2k1 = K01 + K10, 2k2 = i (K01 - K10), 2k3 = K00 - K11
   const double k0i = Ki[0] + Ki[3], k1i = Ki[1] + Ki[2], k2i = Kr[1] - Kr[2], k3i = Ki[0] - Ki[3];
@@ -454,7 +476,7 @@ __device__ __forceinline__ void sk2_contract_pauli(const Sk2& x, const double (&
     m3 = k3i;
   } else {
     const double k0r = Kr[0] + Kr[3], k1r = Kr[1] + Kr[2], k2r = Ki[2] - Ki[1], k3r = Kr[0] - Kr[3];
-    const double x0 = 0.5 * (x.d0 + x.d1), x1 = x.q, x2 = x.r, x3 = 0.5 * (x.d0 - x.d1);
+    const double x0 = CX ? x0c : 0.5 * (x.d0 + x.d1), x1 = x.q, x2 = x.r, x3 = CX ? x3c : 0.5 * (x.d0 - x.d1);
     const double dr = fma(x3, k3r, fma(x2, k2r, x1 * k1r)), di = fma(x3, k3i, fma(x2, k2i, x1 * k1i));
     if constexpr (ORD == 2) {
       m0 = fma(x0, k0r, k0i + dr);
@@ -462,7 +484,7 @@ __device__ __forceinline__ void sk2_contract_pauli(const Sk2& x, const double (&
       m2 = fma(x0, k2r, fma(k0r, x2, k2i));
       m3 = fma(x0, k3r, fma(k0r, x3, k3i));
     } else {
-      const double w = fma(x3, x3, fma(x2, x2, x1 * x1)), x02 = x0 * x0;
+      const double w = fma(x3, x3, fma(x2, x2, x1 * x1)), x02 = CX ? x02c : x0 * x0;
       const double al0 = fma(-0.5, x02 + w, 1.0), al1 = fma(-0.5, x02, fma(-1.0 / 6.0, w, 1.0));
       m0 = fma(al0, k0i, fma(x0, k0r - di, dr));
       const double c = fma(-x0, k0i, fma(-1.0 / 3.0, di, k0r));
@@ -695,9 +717,15 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       gk[j] = sk2_of(e4);
     }
   }
-  auto p1_fast = [&](int jj, auto SEL_, auto K_) {
+  // the control generators' blocks without diagonal (cavity, zz: drives between levels): Â's diagonal is Ã_0's in
+  // every slice, so e^{it} of the block's mean diagonal is computed once per lane (uniform over the workgroup)
+  const bool zdl = NB != 2 || (gk[1].d0 == 0.0 && gk[1].d1 == 0.0 && gk[2].d0 == 0.0 && gk[2].d1 == 0.0);
+  const bool zd = __syncthreads_and(zdl ? 1 : 0) != 0 && sp.mui[1] == 0.0 && sp.mui[2] == 0.0;
+  const double za0 = NB == 2 ? 0.5 * (gk[0].d0 - gk[0].d1) : 0.0;  // ZD: the blocks' constant half-difference
+  auto p1_fast = [&](int jj, auto SEL_, auto K_, auto ZD_, double ct0, double st0) {
     constexpr bool SEL = decltype(SEL_)::value;
     constexpr int KS = decltype(K_)::value;
+    constexpr bool ZD = decltype(ZD_)::value;
     if constexpr (NB == 2) {
       double ur[2][4], ui[2][4];
       bool act[2];
@@ -707,8 +735,8 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
         act[v] = !SEL || (sact && jj + v < L && k < ke);
         const double* r = rec + 4 * (size_t)(act[v] ? k : 0);
         Sk2 ah;
-        sk2_form<KS>(gk, *reinterpret_cast<const double2*>(r), *reinterpret_cast<const double2*>(r + 2), ah, ur[v],
-                     ui[v]);
+        sk2_form<KS, ZD>(gk, *reinterpret_cast<const double2*>(r), *reinterpret_cast<const double2*>(r + 2), ah, ur[v],
+                         ui[v], ct0, st0, za0);
       }
 #pragma unroll
       for (int v = 0; v < 2; ++v) {
@@ -724,13 +752,20 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   };
   // the fast path's series degree (uniform per seed: one loop instance per degree class)
   const int ksel = __builtin_amdgcn_readfirstlane(blkseg_series_k(rmax * s0));
-  auto loop1 = [&](auto K_) {
+  auto loop1z = [&](auto K_, auto ZD_) {
+    constexpr int KS = decltype(K_)::value;
+    double ct0 = 1.0, st0 = 0.0;
+    if constexpr (NB == 2 && decltype(ZD_)::value) sk2_phase<KS>(gk[0].d0, gk[0].d1, ct0, st0);
     for (int jj = 0; jj < L; jj += 2) {
       if (turns) seg_turn(grp, ngrp, jj >> 1);
       sprog.step(jj >> 1);
-      if (jj + 1 < Lf) p1_fast(jj, std::false_type(), K_);
-      else p1_fast(jj, std::true_type(), K_);
+      if (jj + 1 < Lf) p1_fast(jj, std::false_type(), K_, ZD_, ct0, st0);
+      else p1_fast(jj, std::true_type(), K_, ZD_, ct0, st0);
     }
+  };
+  auto loop1 = [&](auto K_) {
+    if (zd) loop1z(K_, std::true_type());
+    else loop1z(K_, std::false_type());
   };
   // G at the end of the lane's segment (phase 3's start): formed here, or read back (BLKSEG_BWD)
   double Gr[E], Gi[E];
@@ -1018,13 +1053,17 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
     }
   };
   double pa1[4] = {0, 0, 0, 0}, pa2[4] = {0, 0, 0, 0};  // the generators' (A_j = Ã_j + i m_j I) doubled Pauli vectors
+  // ZD: X's diagonal in every slice (Ã_0's plus i Im μ_0) and its Pauli components
+  const double zxd0 = NB == 2 ? gk[0].d0 + sp.mui[0] : 0.0, zxd1 = NB == 2 ? gk[0].d1 + sp.mui[0] : 0.0;
+  const double zx0 = 0.5 * (zxd0 + zxd1), zx3 = 0.5 * (zxd0 - zxd1), zx02 = zx0 * zx0;
   if constexpr (NB == 2) {
     sk2_pauli2(Sk2{gk[1].d0 + mu1i, gk[1].d1 + mu1i, gk[1].r, gk[1].q}, pa1);
     sk2_pauli2(Sk2{gk[2].d0 + mu2i, gk[2].d1 + mu2i, gk[2].r, gk[2].q}, pa2);
   }
-  auto p3_fast = [&](int jj, auto SEL_, auto K_) {
+  auto p3_fast = [&](int jj, auto SEL_, auto K_, auto ZD_, double ct0, double st0) {
     constexpr bool SEL = decltype(SEL_)::value;
     constexpr int KS = decltype(K_)::value;
+    constexpr bool ZD = decltype(ZD_)::value;
     if constexpr (NB == 2) {
       const int k = kb + jj;
       const bool act = !SEL || (sact && k < ke);
@@ -1032,7 +1071,7 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       const double2 u = *reinterpret_cast<const double2*>(r + 2);
       Sk2 ah;
       double ur[4], ui[4];
-      sk2_form<KS>(gk, *reinterpret_cast<const double2*>(r), u, ah, ur, ui);
+      sk2_form<KS, ZD>(gk, *reinterpret_cast<const double2*>(r), u, ah, ur, ui, ct0, st0, za0);
       // K_k = U_k^H G_{k+1}, G_k = K_k U_k
       double Kr[4], Ki[4], tr[4], ti[4];
       seg_mm<2, true, false>(ur, ui, Gr, Gi, Kr, Ki);
@@ -1043,11 +1082,12 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
         Gi[e] = !SEL || act ? ti[e] : Gi[e];
       }
       // X = A_k = Â + μ_k I (skew: μ_k = i (Im μ_0 + u_1 Im μ_1 + u_2 Im μ_2))
-      const double mki = fma(u.y, mu2i, fma(u.x, mu1i, sp.mui[0]));
+      // (ZD: μ_k = i Im μ_0, the same value)
+      const double mki = ZD ? sp.mui[0] : fma(u.y, mu2i, fma(u.x, mu1i, sp.mui[0]));
       const Sk2 x{ah.d0 + mki, ah.d1 + mki, ah.r, ah.q};
       double acc1, acc2;
       if constexpr (ORD <= 3) {
-        sk2_contract_pauli<ORD>(x, pa1, pa2, Kr, Ki, acc1, acc2);
+        sk2_contract_pauli<ORD, ZD>(x, pa1, pa2, Kr, Ki, acc1, acc2, zx0, zx3, zx02);
       } else {
         const Sk2 e1{gk[1].d0 + mu1i, gk[1].d1 + mu1i, gk[1].r, gk[1].q};
         const Sk2 e2{gk[2].d0 + mu2i, gk[2].d1 + mu2i, gk[2].r, gk[2].q};
@@ -1056,13 +1096,20 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       reduce(jj, !SEL || act ? acc1 : 0.0, !SEL || act ? acc2 : 0.0);
     }
   };
-  auto loop3 = [&](auto K_) {
+  auto loop3z = [&](auto K_, auto ZD_) {
+    constexpr int KS = decltype(K_)::value;
+    double ct0 = 1.0, st0 = 0.0;
+    if constexpr (NB == 2 && decltype(ZD_)::value) sk2_phase<KS>(gk[0].d0, gk[0].d1, ct0, st0);
     for (int jj = L - 1; jj >= 0; --jj) {
       if (turns) seg_turn(grp, ngrp, jj);
       sprog.step(L + (L - 1 - jj));
-      if (jj < Lf) p3_fast(jj, std::false_type(), K_);
-      else p3_fast(jj, std::true_type(), K_);
+      if (jj < Lf) p3_fast(jj, std::false_type(), K_, ZD_, ct0, st0);
+      else p3_fast(jj, std::true_type(), K_, ZD_, ct0, st0);
     }
+  };
+  auto loop3 = [&](auto K_) {
+    if (zd) loop3z(K_, std::true_type());
+    else loop3z(K_, std::false_type());
   };
   if (fast) {
     if (ksel == 5) loop3(std::integral_constant<int, 5>());
