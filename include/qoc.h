@@ -244,6 +244,11 @@ int qoc_comm_init(qoc_ctx* ctx, int world, int rank, const void* id, long long s
 int qoc_comm_ranks(qoc_ctx* ctx);
 int qoc_allgather_best(qoc_ctx* ctx, double* J_best, int* seed_best);
 int qoc_allgather_best_dev(qoc_ctx* ctx, double* d_out);
+/* Registers a device buffer of two doubles (NULL: none).  With nothing to exchange (no communicator, or one rank) the
+ * evals that reduce their own J (the segmented block eval) then also write the best (J, seed) there, and
+ * qoc_allgather_best_dev(ctx, that buffer) queues nothing more: the result is the same pair, without the pick kernel
+ * after every eval.  The caller keeps the buffer valid while it is registered. */
+int qoc_set_best_output(qoc_ctx* ctx, double* d_out);
 
 /* Standalone ops on the same kernels. */
 /* exponential!(A, ExpMethodHigham2005()) for `count` independent N x N matrices

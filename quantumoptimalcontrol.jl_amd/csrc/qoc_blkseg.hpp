@@ -53,6 +53,10 @@ struct BlksegParams {
   unsigned int* done;
   double* best;
   long long seed_offset;
+  // nothing to exchange (one rank): the final pair also into the context's result slot and the registered output
+  // (qoc_set_best_output), or nullptr
+  double* best_res;
+  double* best_out;
   // the split launches: G at every segment's end, B x [NB^2][S][nblk] complex (written by BLKSEG_FWD, read by
   // BLKSEG_BWD); stale: the stale-u flag of the check queued before BLKSEG_BWD (nonzero: the launch writes nothing)
   double2* gseg;
@@ -968,8 +972,17 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
         }
       }
       if (l == 0) {
+        const double bs = bi >= 0 ? (double)(bi + sp.seed_offset) : -1.0;
         sp.best[0] = bv;
-        sp.best[1] = bi >= 0 ? (double)(bi + sp.seed_offset) : -1.0;
+        sp.best[1] = bs;
+        if (sp.best_res) {
+          sp.best_res[0] = bv;
+          sp.best_res[1] = bs;
+        }
+        if (sp.best_out) {
+          sp.best_out[0] = bv;
+          sp.best_out[1] = bs;
+        }
         *sp.done = 0;  // ready for the next launch (the kernel boundary orders it)
       }
     }

@@ -1468,6 +1468,8 @@ int qoc_allgather_best_dev(qoc_ctx* c, double* d_out) {
   }
   double* res = c->d_best + 2 + 2 * c->world;
   double* slot = c->d_best + 2 + 2 * c->rank;  // this rank's pair in the gathered array (in-place all-gather)
+  // one rank, and the eval already wrote the final pair into res and the registered output: nothing to queue
+  if (c->best_ready && c->best_direct && c->world == 1 && (d_out == nullptr || d_out == c->best_out)) return QOC_OK;
   // the segmented eval already reduced its J in its last workgroup (best_ready); otherwise k_argmin_seed
   if (!c->best_ready) {
     hipLaunchKernelGGL(k_argmin_seed, dim3(1), dim3(256), 0, c->stream, (const double*)c->d_J, c->B, c->seed_offset,
@@ -1482,6 +1484,13 @@ int qoc_allgather_best_dev(qoc_ctx* c, double* d_out) {
   hipLaunchKernelGGL(k_pick_best, dim3(1), dim3(64), 0, c->stream, (const double*)(c->d_best + 2),
                      c->comm && rccl().ok ? c->world : 1, res, d_out);
   HIPCHK(c, hipGetLastError());
+  return QOC_OK;
+}
+
+int qoc_set_best_output(qoc_ctx* c, double* d_out) {
+  if (!c) return fail(nullptr, QOC_ERR_ARG, "null context");
+  c->best_out = d_out;
+  c->best_direct = false;  // the next eval decides
   return QOC_OK;
 }
 

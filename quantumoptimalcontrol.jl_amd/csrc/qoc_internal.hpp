@@ -235,6 +235,8 @@ struct qoc_ctx {
   long long seed_offset = 0;   // global id of this context's seed 0
   double* d_best = nullptr;    // [2 local | 2 x world gathered | 2 result]
   unsigned int* d_done = nullptr;  // the segmented eval's workgroup counter (its last workgroup finds the best pair)
+  double* best_out = nullptr;  // qoc_set_best_output's buffer
+  bool best_direct = false;     // the last eval also wrote the final pair into the result slot and best_out
   bool best_ready = false;     // the last eval already wrote this rank's best (J, seed) into the gathered slot
   // exact (Fréchet) gradient mode workspace, allocated on first use
   void* d_fws = nullptr;

@@ -1734,6 +1734,11 @@ static int blkseg_params(qoc_ctx* c, const BlksegShape& s, BlksegParams& sp) {
   sp.done = c->d_done;
   sp.best = c->d_best + 2 + 2 * c->rank;
   sp.seed_offset = c->seed_offset;
+  // one rank: the pick after the (identity) exchange is done here, when a buffer is registered
+  const bool direct = c->world == 1 && c->best_out;
+  sp.best_res = direct ? c->d_best + 2 + 2 * c->world : nullptr;
+  sp.best_out = direct ? c->best_out : nullptr;
+  c->best_direct = direct;
   return QOC_OK;
 }
 

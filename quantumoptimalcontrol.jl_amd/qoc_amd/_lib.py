@@ -69,6 +69,7 @@ SIGNATURES = {
     "qoc_comm_ranks": (C.c_int, [_vp]),
     "qoc_allgather_best": (C.c_int, [_vp, _dp, _ip]),
     "qoc_allgather_best_dev": (C.c_int, [_vp, _vp]),
+    "qoc_set_best_output": (C.c_int, [_vp, _vp]),
     "qoc_chain_terms": (C.c_int, [_vp, C.POINTER(C.c_longlong), C.c_int]),
     "qoc_set_spline_basis": (C.c_int, [_vp, _dp, C.c_int]),
     "qoc_eval_spline_dev": (C.c_int, [_vp, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),

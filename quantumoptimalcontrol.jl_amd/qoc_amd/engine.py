@@ -357,6 +357,11 @@ class GrapeEngine:
         """Same, written as two doubles to device memory on the engine stream (no host synchronisation)."""
         self._chk(self._lib.qoc_allgather_best_dev(self._h, C.c_void_p(d_out)))
 
+    def set_best_output(self, d_out: int):
+        """Register a device buffer of two doubles (0: none): with one rank, the segmented eval writes the best
+        (J, seed) there itself and allgather_best_device(d_out) queues nothing more (qoc_set_best_output)."""
+        self._chk(self._lib.qoc_set_best_output(self._h, C.c_void_p(d_out or None)))
+
     def chain_terms(self, reset: bool = False) -> int:
         """Taylor terms executed per direction since the last reset (Taylor-action chains)."""
         v = C.c_longlong()

@@ -140,3 +140,41 @@ def test_two_ranks_share_the_gpu_and_gather_the_global_best(built_lib):
     for _, (Jb, sb) in out:
         assert sb == int(np.argmin(J))
         assert abs(Jb - J.min()) <= 1e-13
+
+
+def test_best_output_registered_world1(built_lib):
+    """qoc_set_best_output: with one rank the segmented eval writes the best (J, seed) into the registered buffer itself
+    and allgather_best_device(that buffer) queues nothing; the pair equals the argmin (and what the pick kernel writes
+    into another buffer); after unregistering the pick kernel runs again."""
+    import torch
+    from qoc_amd import GrapeEngine
+    prob, u = _problem()
+    e = GrapeEngine(prob.A0, prob.A, prob.x0, NT, B=B_TOTAL)
+    e.set_cost_trace(prob.x_target, prob.n)
+    e.comm_init(1, 0, None, 500)
+    ud = torch.from_numpy(np.ascontiguousarray(np.transpose(u, (0, 2, 1)))).cuda()
+    Jd = torch.empty(B_TOTAL, dtype=torch.float64, device="cuda")
+    gd = torch.empty(B_TOTAL, NT, prob.nu, dtype=torch.float64, device="cuda")
+    reg = torch.full((2,), -7.0, dtype=torch.float64, device="cuda")
+    other = torch.full((2,), -7.0, dtype=torch.float64, device="cuda")
+    e.set_best_output(reg.data_ptr())
+    for u_scale in (1.0, 0.5):
+        ud2 = ud * u_scale
+        e.eval_device(ud2.data_ptr(), 3, Jd.data_ptr(), gd.data_ptr())
+        assert e.info()["backward"] == "segmented", e.info()
+        e.allgather_best_device(reg.data_ptr())
+        e.synchronize()
+        J = Jd.cpu().numpy()
+        assert reg.cpu().tolist() == [J.min(), float(500 + int(np.argmin(J)))]
+        assert e.allgather_best() == (J.min(), 500 + int(np.argmin(J)))
+        e.allgather_best_device(other.data_ptr())  # another buffer: the pick kernel
+        e.synchronize()
+        assert other.cpu().tolist() == reg.cpu().tolist()
+    e.set_best_output(0)
+    reg.fill_(-7.0)
+    e.eval_device(ud.data_ptr(), 3, Jd.data_ptr(), gd.data_ptr())
+    e.allgather_best_device(reg.data_ptr())
+    e.synchronize()
+    J = Jd.cpu().numpy()
+    assert reg.cpu().tolist() == [J.min(), float(500 + int(np.argmin(J)))]
+    e.close()
