@@ -365,9 +365,18 @@ __device__ __forceinline__ void sk2_phase(double d0, double d1, double& ct, doub
   }
   st *= t;
 }
+// ZD with constant shifts: z = e^{μ_0} e^{it} of the lane's block, the same in every slice (rec[0..1]: e^{μ_0})
+template <int K = BLKSEG_KMAX>
+__device__ __forceinline__ void sk2_z(const Sk2& g0, const double* rec, double& zr, double& zi) {
+  double ct, st;
+  sk2_phase<K>(g0.d0, g0.d1, ct, st);
+  const double2 ph = *reinterpret_cast<const double2*>(rec);
+  zr = ph.x * ct - ph.y * st;
+  zi = fma(ph.x, st, ph.y * ct);
+}
 // Â = Ã_0 + u_1 Ã_1 + u_2 Ã_2 (no halvings) and U = e^{μ_k} exp(Â) in the closed form of seg_form (ph = e^{μ_k}).
-// ZD: the control generators' blocks have zero diagonals, so Â's diagonal is Ã_0's for every slice and cos t, sin t
-// come precomputed (ct0, st0: sk2_phase of Ã_0's diagonal, the same values)
+// ZD: the control generators' blocks have zero diagonals and no shifts, so Â's diagonal is Ã_0's and e^{μ_k} = e^{μ_0}
+// in every slice: z = e^{μ_k} e^{it} comes precomputed (ct0, st0: sk2_z, the same value)
 template <int K = BLKSEG_KMAX, bool ZD = false>
 __device__ __forceinline__ void sk2_form(const Sk2 (&g)[3], double2 ph, double2 u, Sk2& ah, double (&ur)[4],
                                          double (&ui)[4], double ct0 = 1.0, double st0 = 0.0, double a0 = 0.0) {
@@ -390,7 +399,8 @@ __device__ __forceinline__ void sk2_form(const Sk2 (&g)[3], double2 ph, double2 
     sw = fma(sw, w, T.s[k]);
   }
   if constexpr (!ZD) sk2_phase<K>(ah.d0, ah.d1, ct, st);
-  const double zr = ph.x * ct - ph.y * st, zi = fma(ph.x, st, ph.y * ct);
+  // z = e^{μ_k} e^{it}; ZD (constant shifts too): the same in every slice, (ct0, st0) hold it
+  const double zr = ZD ? ct0 : ph.x * ct - ph.y * st, zi = ZD ? st0 : fma(ph.x, st, ph.y * ct);
   const double cr = zr * cw, ci = zi * cw, sr = zr * sw, si = zi * sw;
   ur[0] = fma(-si, a, cr);
   ui[0] = fma(sr, a, ci);
@@ -608,6 +618,15 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   // [Re e^{μ_k}, Im e^{μ_k}, u_1k, u_2k] (e^{μ_k} does not depend on J; u is scaled by 2^-J below when J > 0)
   const double* ub = sp.u + (size_t)b * Nt * nu;
   double rmax = 0.0;
+  // controls without shifts: e^{μ_k} = e^{μ_0} in every slice (the same value), one exp and sincos per thread
+  const bool cmu = sp.mur[1] == 0.0 && sp.mur[2] == 0.0 && sp.mui[1] == 0.0 && sp.mui[2] == 0.0;
+  double2 emu0 = make_double2(1.0, 0.0);
+  if (cmu) {
+    const double er = exp(sp.mur[0]);
+    double sn, cs;
+    sincos(sp.mui[0], &sn, &cs);
+    emu0 = make_double2(er * cs, er * sn);
+  }
   for (int k = tid; k < Nt; k += nthr) {
     const double u1 = nu > 0 ? ub[(size_t)k * nu] : 0.0, u2 = nu > 1 ? ub[(size_t)k * nu + 1] : 0.0;
     for (int j = 0; j < nu; ++j) {
@@ -616,13 +635,17 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
       if (sp.u_copy2) sp.u_copy2[((size_t)b * Nt + k) * nu + j] = v;
     }
     rmax = fmax(rmax, fma(fabs(u2), sp.rad[2], fma(fabs(u1), sp.rad[1], sp.rad[0])));
-    const double mr = fma(u2, sp.mur[2], fma(u1, sp.mur[1], sp.mur[0]));
-    const double mi = fma(u2, sp.mui[2], fma(u1, sp.mui[1], sp.mui[0]));
-    const double er = exp(mr);
-    double sn, cs;
-    sincos(mi, &sn, &cs);
     double2* r = reinterpret_cast<double2*>(rec + 4 * (size_t)k);
-    r[0] = make_double2(er * cs, er * sn);
+    if (cmu) {  // uniform
+      r[0] = emu0;
+    } else {
+      const double mr = fma(u2, sp.mur[2], fma(u1, sp.mur[1], sp.mur[0]));
+      const double mi = fma(u2, sp.mui[2], fma(u1, sp.mui[1], sp.mui[0]));
+      const double er = exp(mr);
+      double sn, cs;
+      sincos(mi, &sn, &cs);
+      r[0] = make_double2(er * cs, er * sn);
+    }
     r[1] = make_double2(u1, u2);
   }
   rmax = block_max(rmax, red);  // (its barriers also publish the records)
@@ -724,7 +747,7 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   // the control generators' blocks without diagonal (cavity, zz: drives between levels): Â's diagonal is Ã_0's in
   // every slice, so e^{it} of the block's mean diagonal is computed once per lane (uniform over the workgroup)
   const bool zdl = NB != 2 || (gk[1].d0 == 0.0 && gk[1].d1 == 0.0 && gk[2].d0 == 0.0 && gk[2].d1 == 0.0);
-  const bool zd = __syncthreads_and(zdl ? 1 : 0) != 0 && sp.mui[1] == 0.0 && sp.mui[2] == 0.0;
+  const bool zd = __syncthreads_and(zdl ? 1 : 0) != 0 && cmu;
   const double za0 = NB == 2 ? 0.5 * (gk[0].d0 - gk[0].d1) : 0.0;  // ZD: the blocks' constant half-difference
   auto p1_fast = [&](int jj, auto SEL_, auto K_, auto ZD_, double ct0, double st0) {
     constexpr bool SEL = decltype(SEL_)::value;
@@ -759,7 +782,7 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   auto loop1z = [&](auto K_, auto ZD_) {
     constexpr int KS = decltype(K_)::value;
     double ct0 = 1.0, st0 = 0.0;
-    if constexpr (NB == 2 && decltype(ZD_)::value) sk2_phase<KS>(gk[0].d0, gk[0].d1, ct0, st0);
+    if constexpr (NB == 2 && decltype(ZD_)::value) sk2_z<KS>(gk[0], rec, ct0, st0);
     for (int jj = 0; jj < L; jj += 2) {
       if (turns) seg_turn(grp, ngrp, jj >> 1);
       sprog.step(jj >> 1);
@@ -1112,7 +1135,7 @@ __global__ __launch_bounds__(64 * WMAX) void k_blkseg_eval(const TChainArgs g, c
   auto loop3z = [&](auto K_, auto ZD_) {
     constexpr int KS = decltype(K_)::value;
     double ct0 = 1.0, st0 = 0.0;
-    if constexpr (NB == 2 && decltype(ZD_)::value) sk2_phase<KS>(gk[0].d0, gk[0].d1, ct0, st0);
+    if constexpr (NB == 2 && decltype(ZD_)::value) sk2_z<KS>(gk[0], rec, ct0, st0);
     for (int jj = L - 1; jj >= 0; --jj) {
       if (turns) seg_turn(grp, ngrp, jj);
       sprog.step(L + (L - 1 - jj));
