@@ -1670,8 +1670,14 @@ static BlksegShape blkseg_shape(const qoc_ctx* c) {
   s.S = (c->Nt + s.L - 1) / s.L;
   s.W = (s.S + s.UPW - 1) / s.UPW;
   s.RB = blkseg_rb(s.UPW, c->nu);
-  // QOC_BLKSEG_RB: slice-steps per block-sum reduction up to 64 / (UPW nu) (A/B; the LDS must still fit)
-  if (const char* e = getenv("QOC_BLKSEG_RB")) s.RB = std::max(1, std::min(atoi(e), std::max(1, 64 / (s.UPW * std::max(1, c->nu)))));
+  // blocks of 2 rows: up to 8 slice-steps per reduction when the LDS holds them (cavity: 0.0727 -> 0.0715 ms per launch,
+  // the same sums in the same order, profiles/bench_r06zl_*); QOC_BLKSEG_RB overrides (up to 64 / (UPW nu))
+  const int rbmax = std::max(1, 64 / (s.UPW * std::max(1, c->nu)));
+  if (c->blk_nb == 2) {
+    const int rb8 = std::min(8, rbmax);
+    if (blkseg_lds(c->N, c->m, c->nu, c->blk_nb, c->nblk, c->Nt, s.S, s.W, rb8) <= (size_t)160 * 1024) s.RB = rb8;
+  }
+  if (const char* e = getenv("QOC_BLKSEG_RB")) s.RB = std::max(1, std::min(atoi(e), rbmax));
   s.lds = blkseg_lds(c->N, c->m, c->nu, c->blk_nb, c->nblk, c->Nt, s.S, s.W, s.RB);
   return s;
 }
